@@ -1,0 +1,265 @@
+"""Benchmark: loop-closure constraint search throughput on MI355X.
+
+Metric (BASELINE.json): loop-closure constraint candidates/sec (node x submap
+pairs) + ms/scan-match, 2D 5 cm grid.
+
+Workload per rank (BASELINE config C2): 500 synthetic 1080-beam scans x 50
+submaps (400x400 @ 5 cm), FastCorrelativeScanMatcher2D::MatchFullSubmap,
+branch_and_bound_depth 7, min_score 0.55 = 25,000 pairs per step. With N
+GPUs the world has 50*N submaps and rank r owns submaps [50r, 50r+50): the
+constraint queue is sharded by submap with no data-path collective (weak
+scaling); accepted constraints are gathered to rank 0 over RCCL each step
+(the hand-off to the CPU pose-graph solve), ordered by submission index.
+
+A step = one pass of the search over the rank's 25,000 pairs, inputs resident
+in HBM (pyramids and clouds uploaded before timing). The secondary number is
+RealTimeCorrelativeScanMatcher2D::Match ms/scan-match at config C1.
+
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+
+
+def load_pkg():
+    sys.path.insert(0, ROOT)
+    import __graft_entry__ as ge
+    return ge._load_package()
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=2)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--nodes", type=int, default=500)
+    p.add_argument("--submaps-per-rank", type=int, default=50)
+    p.add_argument("--min-score", type=float, default=0.55)
+    p.add_argument("--search-depth", type=int, default=0, help="0 = automatic (exact)")
+    p.add_argument("--cpu-seconds", type=float, default=20.0)
+    p.add_argument("--cpu-threads", type=int, default=0)
+    p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--no-rt", action="store_true")
+    p.add_argument("--seed", type=int, default=20250127)
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world_size = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world_size > 1:
+        import torch
+        import torch.distributed as tdist
+        torch.cuda.set_device(local_rank)
+        tdist.init_process_group("nccl")
+        dist = tdist
+
+    csm = load_pkg()
+    ctx = csm.Context(local_rank)
+
+    # ---- synthetic world (identical on every rank) -------------------------
+    t0 = time.time()
+    world = csm.SyntheticWorld2D(num_nodes=args.nodes,
+                                 num_submaps=args.submaps_per_rank * world_size,
+                                 submap_cells=400, beams=1080, seed=args.seed)
+    gen_s = time.time() - t0
+    my_submaps = list(range(rank * args.submaps_per_rank, (rank + 1) * args.submaps_per_rank))
+    opts = csm.FastCorrelativeScanMatcherOptions2D(7.0, math.radians(30.0), 7, args.search_depth)
+    t0 = time.time()
+    matchers = [csm.FastCorrelativeScanMatcher2D(world.grid(s), opts, ctx) for s in my_submaps]
+    scans = csm.ScanSet(None, ctx, packed=(world.points, world.offsets))
+    build_s = time.time() - t0
+    sub_local = np.repeat(np.arange(len(my_submaps), dtype=np.int32), args.nodes)
+    node_idx = np.tile(np.arange(args.nodes, dtype=np.int32), len(my_submaps))
+    pairs = csm.make_pairs(sub_local, node_idx, args.min_score, full_submap=True)
+    # Submission index = global queue position (submap-major), used to restore
+    # ConstraintBuilder2D::WhenDone ordering on rank 0 (constraint_builder_2d.cc:285-288).
+    submission = (np.int64(rank) * len(pairs) + np.arange(len(pairs), dtype=np.int64))
+    n_pairs = len(pairs)
+
+    def gather_constraints(res):
+        ok = res["status"] == 0
+        rec = np.zeros((int(ok.sum()), 6), np.float64)
+        rec[:, 0] = submission[ok]
+        rec[:, 1] = np.asarray(my_submaps)[sub_local[ok]]
+        rec[:, 2] = node_idx[ok]
+        rec[:, 3] = res["x"][ok]
+        rec[:, 4] = res["y"][ok]
+        rec[:, 5] = res["theta"][ok]
+        if dist is None:
+            return rec
+        import torch
+        dev = torch.device("cuda", local_rank)
+        cnt = torch.tensor([rec.shape[0]], dtype=torch.int64, device=dev)
+        cnts = [torch.zeros_like(cnt) for _ in range(world_size)]
+        dist.all_gather(cnts, cnt)
+        mx = int(max(c.item() for c in cnts))
+        buf = torch.zeros((max(mx, 1), 6), dtype=torch.float64, device=dev)
+        if rec.shape[0]:
+            buf[:rec.shape[0]] = torch.from_numpy(rec).to(dev)
+        bufs = [torch.zeros_like(buf) for _ in range(world_size)] if rank == 0 else None
+        dist.gather(buf, bufs, dst=0)
+        if rank != 0:
+            return None
+        allrec = np.concatenate([b[:int(c.item())].cpu().numpy() for b, c in zip(bufs, cnts)])
+        return allrec[np.argsort(allrec[:, 0], kind="stable")]
+
+    def barrier_sync():
+        if dist is not None:
+            dist.barrier()
+            import torch
+            torch.cuda.synchronize()
+
+    # ---- warmup + timed steps ------------------------------------------------
+    for _ in range(args.warmup):
+        res = csm.match_batch(matchers, scans, pairs, ctx)
+        gather_constraints(res)
+    ctx.reset_timing()
+    ctx.enable_timing(True)
+    barrier_sync()
+    t_start = time.perf_counter()
+    accepted = 0
+    for _ in range(args.steps):
+        res = csm.match_batch(matchers, scans, pairs, ctx)
+        rec = gather_constraints(res)
+        if rank == 0:
+            accepted = len(rec)
+    barrier_sync()
+    elapsed = time.perf_counter() - t_start
+    ctx.enable_timing(False)
+    tm = ctx.timing()
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64, device=torch.device("cuda", local_rank))
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    total_pairs = n_pairs * world_size * args.steps
+    value = total_pairs / elapsed
+
+    # Roofline of the dominant kernel (fast2d_search): algorithmic bytes per
+    # launch = candidates scored x points x 1 B (uint8 pyramid lookups).
+    kernel_ms_avg = tm.search_kernel_ms / max(tm.search_launches, 1)
+    bytes_per_launch = tm.search_lookups / max(tm.search_launches, 1)
+    achieved = bytes_per_launch / (kernel_ms_avg * 1e-3) / 1e9 if kernel_ms_avg > 0 else 0.0
+    peak = 8000.0
+
+    out = {
+        "metric": "loop-closure constraint candidates/sec (node x submap pairs) + ms/scan-match, 2D 5cm grid",
+        "value": value,
+        "unit": "pairs/s",
+        "n_gpus": world_size,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (seeded building world, 1080-beam scans, ray-cast submaps)",
+        "config": {"workload": "C2: FastCorrelativeScanMatcher2D::MatchFullSubmap, "
+                               f"{args.nodes} scans x {args.submaps_per_rank} submaps per GPU "
+                               "(400x400 @5cm), branch_and_bound_depth=7, min_score=%.2f" % args.min_score,
+                   "pairs_per_step_per_gpu": n_pairs, "search_depth": matchers[0].options.search_depth,
+                   "parallelism": f"submap-sharded x{world_size}"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
+                     "frac": achieved / peak, "traffic": None,
+                     "kernel": "fast2d_search", "kernel_ms_avg": kernel_ms_avg,
+                     "algorithmic_bytes_per_launch": bytes_per_launch},
+        "accepted_constraints_per_step": accepted,
+        "setup_s": {"world": gen_s, "pyramids_and_upload": build_s},
+    }
+
+    if rank == 0 and world_size == 1 and not args.no_rt:
+        out["rt2d"] = rt2d_bench(csm, ctx, args)
+    if rank == 0 and world_size == 1 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline(world, my_submaps, args)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def rt2d_bench(csm, ctx, args):
+    """Config C1: 1080-beam scan vs 200x200 @5cm, +-0.2 m / +-10 deg window."""
+    w = csm.SyntheticWorld2D(num_nodes=4, num_submaps=4, submap_cells=200, seed=args.seed + 1)
+    opts = csm.RealTimeCorrelativeScanMatcherOptions(0.2, math.radians(10.0), 0.1, 0.1)
+    m = csm.RealTimeCorrelativeScanMatcher2D(opts, ctx)
+    g = w.grid(0)
+    n = int(w.submap_nodes[0])
+    t = w.node_poses[n]
+    init = (t[0] + 0.1, t[1] - 0.07, t[2] + math.radians(5.0))
+    cloud = w.cloud(n)
+    for _ in range(10):
+        m.Match(init, cloud, g)
+    times = []
+    for _ in range(100):
+        a = time.perf_counter()
+        m.Match(init, cloud, g)
+        times.append(time.perf_counter() - a)
+    res = {"gpu_ms_per_scan_match_median": 1e3 * float(np.median(times)), "points": len(cloud)}
+    try:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_lib
+        o = oracle_lib.Oracle()
+        cpu_s = o.rt2d_time((g.resolution, g.max_x, g.max_y), g.cells,
+                            (0.2, math.radians(10.0), 0.1, 0.1), init, cloud, 20)
+        res["cpu_ms_per_scan_match"] = cpu_s * 1e3
+        res["cpu_threads"] = 1
+    except OSError:
+        pass
+    return res
+
+
+def cpu_baseline(world, my_submaps, args):
+    """The oracle restatement (the reference's algorithm and data structures)
+    on host threads, one pair per task as ConstraintBuilder2D schedules them,
+    on a bounded random sample of the same pairs."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import ctypes as C
+
+    import oracle_lib
+    o = oracle_lib.Oracle()
+    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    rng = np.random.RandomState(12345)
+    subs = [o.fast2d((world.resolution, world.submap_max[s, 0], world.submap_max[s, 1]),
+                     world.submap_cells[s], 7.0, math.radians(30.0), 7) for s in my_submaps]
+    handles = (C.c_void_p * len(subs))(*[s.h for s in subs])
+    pts = np.ascontiguousarray(world.points, np.float32)
+    offs = np.ascontiguousarray(world.offsets, np.int64)
+
+    def run(k):
+        ps = rng.randint(0, len(subs), k).astype(np.int32)
+        pn = rng.randint(0, world.num_nodes, k).astype(np.int32)
+        scores, poses, matched = np.zeros(k, np.float32), np.zeros(3 * k), np.zeros(k, np.int32)
+        P = C.POINTER
+        wall = o.lib.oracle_fast2d_match_pairs(
+            handles, pts.ctypes.data_as(P(C.c_float)), offs.ctypes.data_as(P(C.c_int64)),
+            ps.ctypes.data_as(P(C.c_int32)), pn.ctypes.data_as(P(C.c_int32)), k, threads,
+            args.min_score, scores.ctypes.data_as(P(C.c_float)), poses.ctypes.data_as(P(C.c_double)),
+            matched.ctypes.data_as(P(C.c_int32)))
+        return wall
+
+    probe_k = threads
+    wall = run(probe_k)
+    k = max(threads, int(probe_k * args.cpu_seconds / max(wall, 1e-3)))
+    k = min(k, 20000)
+    wall = run(k)
+    return {"value": k / wall, "unit": "pairs/s", "cores": threads, "kind": "port",
+            "sample": f"{k} uniformly sampled (submap, scan) pairs of the same C2 queue, "
+                      f"{wall:.1f} s wall on {threads} threads (oracle, -O3 -DNDEBUG)"}
+
+
+if __name__ == "__main__":
+    main()

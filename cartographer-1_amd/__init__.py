@@ -1,0 +1,481 @@
+"""MI355X-native correlative scan matching — Python host mirror.
+
+Thin ctypes layer over ``libcsm_amd.so`` (C-ABI: ``include/csm_amd.h``) that
+mirrors the reference's operator interface so tests and benchmarks read like
+the reference's own code:
+
+* :class:`FastCorrelativeScanMatcher2D` — ``Match`` / ``MatchFullSubmap``
+  (reference ``mapping/internal/2d/scan_matching/fast_correlative_scan_matcher_2d.h:112-164``)
+* :class:`RealTimeCorrelativeScanMatcher2D` — ``Match``
+  (``real_time_correlative_scan_matcher_2d.h:53-85``)
+* :func:`match_batch` — the batched constraint search that replaces one
+  ``ConstraintBuilder2D`` task per (node, submap) pair
+  (``constraints/constraint_builder_2d.cc:77-137``)
+
+There is no CPU fallback: every compute call runs the HIP kernels, and loading
+fails loudly when the extension is missing. PyTorch is not used here.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import math
+import os
+from dataclasses import dataclass
+from typing import Optional, Sequence, Tuple
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libcsm_amd.so")
+SYNTH_PATH = os.path.join(_HERE, "libcsm_synth.so")
+
+CSM_OK = 0
+CSM_NO_MATCH = 1
+CSM_EINVAL = -1
+CSM_EHIP = -2
+CSM_ENOMEM = -3
+CSM_ERANGE = -4
+
+
+class CsmError(RuntimeError):
+    """A negative return code from the C-ABI (the reference would CHECK-fail)."""
+
+
+class MapLimits(C.Structure):
+    _fields_ = [("resolution", C.c_double), ("max_x", C.c_double), ("max_y", C.c_double),
+                ("num_x_cells", C.c_int32), ("num_y_cells", C.c_int32)]
+
+
+class Pose2D(C.Structure):
+    _fields_ = [("x", C.c_double), ("y", C.c_double), ("theta", C.c_double)]
+
+    def as_tuple(self) -> Tuple[float, float, float]:
+        return (self.x, self.y, self.theta)
+
+
+class Fast2DOptions(C.Structure):
+    _fields_ = [("linear_search_window", C.c_double), ("angular_search_window", C.c_double),
+                ("branch_and_bound_depth", C.c_int32), ("search_depth", C.c_int32)]
+
+
+class RtOptions(C.Structure):
+    _fields_ = [("linear_search_window", C.c_double), ("angular_search_window", C.c_double),
+                ("translation_delta_cost_weight", C.c_double),
+                ("rotation_delta_cost_weight", C.c_double)]
+
+
+class Pair2D(C.Structure):
+    _fields_ = [("submap", C.c_int32), ("scan", C.c_int32), ("full_submap", C.c_int32),
+                ("min_score", C.c_float), ("initial", Pose2D)]
+
+
+class Result2D(C.Structure):
+    _fields_ = [("status", C.c_int32), ("score", C.c_float), ("pose", Pose2D)]
+
+
+class Timing(C.Structure):
+    _fields_ = [("search_kernel_ms", C.c_double), ("search_launches", C.c_int64),
+                ("search_lookups", C.c_double), ("search_candidates", C.c_double),
+                ("other_kernel_ms", C.c_double)]
+
+
+# Exported symbols and their signatures (include/csm_amd.h).
+_SIGNATURES = {
+    "csm_context_create": (C.c_int, [C.c_int32, C.POINTER(C.c_void_p)]),
+    "csm_context_destroy": (None, [C.c_void_p]),
+    "csm_context_stream": (C.c_void_p, [C.c_void_p]),
+    "csm_context_enable_timing": (None, [C.c_void_p, C.c_int32]),
+    "csm_context_get_timing": (None, [C.c_void_p, C.POINTER(Timing)]),
+    "csm_context_reset_timing": (None, [C.c_void_p]),
+    "csm_fast2d_create": (C.c_int, [C.c_void_p, C.POINTER(MapLimits), C.POINTER(C.c_uint16),
+                                    C.c_float, C.c_float, C.POINTER(Fast2DOptions),
+                                    C.POINTER(C.c_void_p)]),
+    "csm_fast2d_destroy": (None, [C.c_void_p]),
+    "csm_fast2d_match": (C.c_int, [C.c_void_p, C.POINTER(Pose2D), C.POINTER(C.c_float),
+                                   C.c_int32, C.c_float, C.POINTER(C.c_float),
+                                   C.POINTER(Pose2D)]),
+    "csm_fast2d_match_full_submap": (C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.c_int32,
+                                               C.c_float, C.POINTER(C.c_float),
+                                               C.POINTER(Pose2D)]),
+    "csm_fast2d_read_level": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_uint8), C.c_int64,
+                                        C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+    "csm_scan_set_create": (C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_int64),
+                                      C.c_int32, C.POINTER(C.c_void_p)]),
+    "csm_scan_set_destroy": (None, [C.c_void_p]),
+    "csm_fast2d_match_batch": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.c_int32,
+                                         C.c_void_p, C.POINTER(Pair2D), C.c_int64,
+                                         C.POINTER(Result2D)]),
+    "csm_rt2d_match": (C.c_int, [C.c_void_p, C.POINTER(RtOptions), C.POINTER(MapLimits),
+                                 C.POINTER(C.c_uint16), C.c_float, C.c_float, C.POINTER(Pose2D),
+                                 C.POINTER(C.c_float), C.c_int32, C.POINTER(C.c_double),
+                                 C.POINTER(Pose2D)]),
+    "csm_strerror": (C.c_char_p, [C.c_int]),
+}
+
+_lib_handle = None
+
+
+def load_library(path: str = LIB_PATH) -> C.CDLL:
+    """Loads libcsm_amd.so; raises if it is missing (no CPU fallback exists)."""
+    global _lib_handle
+    if _lib_handle is not None:
+        return _lib_handle
+    if not os.path.exists(path):
+        raise ImportError(
+            f"{path} not found: build it with `make -C cartographer-1_amd/csrc` "
+            "(or __graft_entry__.build()); there is no CPU fallback")
+    lib = C.CDLL(path)
+    for name, (res, args) in _SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib_handle = lib
+    return lib
+
+
+def _check(code: int, what: str) -> int:
+    if code < 0:
+        msg = load_library().csm_strerror(code).decode()
+        raise CsmError(f"{what}: {msg} ({code})")
+    return code
+
+
+def _f32_points(points) -> np.ndarray:
+    pts = np.ascontiguousarray(np.asarray(points, dtype=np.float32))
+    if pts.ndim == 1:
+        pts = pts.reshape(-1, 3)
+    if pts.shape[1] == 2:
+        pts = np.ascontiguousarray(np.concatenate([pts, np.zeros((len(pts), 1), np.float32)], 1))
+    if pts.shape[1] != 3:
+        raise ValueError("point cloud must be (n, 3) or (n, 2)")
+    return pts
+
+
+def _ptr(a: np.ndarray, t):
+    return a.ctypes.data_as(C.POINTER(t))
+
+
+# kMinCorrespondenceCost / kMaxCorrespondenceCost (probability_values.h:64-67),
+# evaluated in float like the reference's constexprs.
+K_MIN_PROBABILITY = float(np.float32(0.1))
+K_MAX_PROBABILITY = float(np.float32(1.0) - np.float32(0.1))
+K_MIN_CORRESPONDENCE_COST = float(np.float32(1.0) - np.float32(K_MAX_PROBABILITY))
+K_MAX_CORRESPONDENCE_COST = float(np.float32(1.0) - np.float32(0.1))
+
+
+@dataclass
+class ProbabilityGrid:
+    """Grid2D data for the boundary: MapLimits + uint16 correspondence-cost cells
+    (x fastest: ``cells[y, x]`` for a (num_y_cells, num_x_cells) array)."""
+    resolution: float
+    max_x: float
+    max_y: float
+    cells: np.ndarray  # shape (num_y_cells, num_x_cells), uint16
+    min_correspondence_cost: float = K_MIN_CORRESPONDENCE_COST
+    max_correspondence_cost: float = K_MAX_CORRESPONDENCE_COST
+
+    @property
+    def num_x_cells(self) -> int:
+        return int(self.cells.shape[1])
+
+    @property
+    def num_y_cells(self) -> int:
+        return int(self.cells.shape[0])
+
+    def limits(self) -> MapLimits:
+        return MapLimits(self.resolution, self.max_x, self.max_y, self.num_x_cells,
+                         self.num_y_cells)
+
+
+class Context:
+    """A device, a HIP stream and per-call scratch (one per calling thread)."""
+
+    def __init__(self, device: int = 0):
+        self._lib = load_library()
+        h = C.c_void_p()
+        _check(self._lib.csm_context_create(device, C.byref(h)), "csm_context_create")
+        self.handle = h
+        self.device = device
+
+    def close(self):
+        if self.handle:
+            self._lib.csm_context_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def stream(self) -> int:
+        return self._lib.csm_context_stream(self.handle) or 0
+
+    def enable_timing(self, on: bool = True):
+        self._lib.csm_context_enable_timing(self.handle, 1 if on else 0)
+
+    def reset_timing(self):
+        self._lib.csm_context_reset_timing(self.handle)
+
+    def timing(self) -> Timing:
+        t = Timing()
+        self._lib.csm_context_get_timing(self.handle, C.byref(t))
+        return t
+
+
+_default_contexts = {}
+
+
+def default_context(device: int = 0) -> Context:
+    if device not in _default_contexts:
+        _default_contexts[device] = Context(device)
+    return _default_contexts[device]
+
+
+@dataclass
+class FastCorrelativeScanMatcherOptions2D:
+    """proto::FastCorrelativeScanMatcherOptions2D; defaults from
+    configuration_files/pose_graph.lua:25-29."""
+    linear_search_window: float = 7.0
+    angular_search_window: float = math.radians(30.0)
+    branch_and_bound_depth: int = 7
+    search_depth: int = 0  # device pyramid depth (0 = automatic; exact either way)
+
+
+@dataclass
+class RealTimeCorrelativeScanMatcherOptions:
+    """proto::RealTimeCorrelativeScanMatcherOptions; defaults from
+    configuration_files/trajectory_builder_2d.lua:38-43."""
+    linear_search_window: float = 0.1
+    angular_search_window: float = math.radians(20.0)
+    translation_delta_cost_weight: float = 1e-1
+    rotation_delta_cost_weight: float = 1e-1
+
+
+class FastCorrelativeScanMatcher2D:
+    """Device pyramid of one submap grid; Match / MatchFullSubmap run on the GPU."""
+
+    def __init__(self, grid: ProbabilityGrid, options: FastCorrelativeScanMatcherOptions2D,
+                 context: Optional[Context] = None):
+        self.context = context or default_context()
+        self._lib = self.context._lib
+        self.grid_limits = grid.limits()
+        self.options = options
+        cells = np.ascontiguousarray(grid.cells, dtype=np.uint16)
+        opts = Fast2DOptions(options.linear_search_window, options.angular_search_window,
+                             options.branch_and_bound_depth, options.search_depth)
+        h = C.c_void_p()
+        _check(self._lib.csm_fast2d_create(self.context.handle, C.byref(self.grid_limits),
+                                           _ptr(cells, C.c_uint16),
+                                           grid.min_correspondence_cost,
+                                           grid.max_correspondence_cost, C.byref(opts),
+                                           C.byref(h)), "csm_fast2d_create")
+        self.handle = h
+
+    def close(self):
+        if getattr(self, "handle", None):
+            self._lib.csm_fast2d_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def Match(self, initial_pose_estimate, point_cloud, min_score: float):
+        """fast_correlative_scan_matcher_2d.h:127-129 -> (matched, score, pose)."""
+        pts = _f32_points(point_cloud)
+        init = Pose2D(*initial_pose_estimate)
+        score = C.c_float(0.0)
+        pose = Pose2D()
+        rc = _check(self._lib.csm_fast2d_match(self.handle, C.byref(init), _ptr(pts, C.c_float),
+                                               len(pts), min_score, C.byref(score),
+                                               C.byref(pose)), "csm_fast2d_match")
+        return rc == CSM_OK, float(score.value), pose.as_tuple()
+
+    def MatchFullSubmap(self, point_cloud, min_score: float):
+        """fast_correlative_scan_matcher_2d.h:135-136 -> (matched, score, pose)."""
+        pts = _f32_points(point_cloud)
+        score = C.c_float(0.0)
+        pose = Pose2D()
+        rc = _check(self._lib.csm_fast2d_match_full_submap(
+            self.handle, _ptr(pts, C.c_float), len(pts), min_score, C.byref(score),
+            C.byref(pose)), "csm_fast2d_match_full_submap")
+        return rc == CSM_OK, float(score.value), pose.as_tuple()
+
+    def read_level(self, level: int) -> np.ndarray:
+        """PrecomputationGrid2D level as (wide_ny, wide_nx) uint8."""
+        wnx, wny = C.c_int32(), C.c_int32()
+        _check(self._lib.csm_fast2d_read_level(self.handle, level, None, 0, C.byref(wnx),
+                                               C.byref(wny)), "csm_fast2d_read_level")
+        out = np.zeros((wny.value, wnx.value), np.uint8)
+        _check(self._lib.csm_fast2d_read_level(self.handle, level, _ptr(out, C.c_uint8),
+                                               out.size, C.byref(wnx), C.byref(wny)),
+               "csm_fast2d_read_level")
+        return out
+
+
+class RealTimeCorrelativeScanMatcher2D:
+    def __init__(self, options: RealTimeCorrelativeScanMatcherOptions,
+                 context: Optional[Context] = None):
+        self.context = context or default_context()
+        self._lib = self.context._lib
+        self.options = options
+
+    def Match(self, initial_pose_estimate, point_cloud, grid: ProbabilityGrid):
+        """real_time_correlative_scan_matcher_2d.h:66-68 -> (score, pose)."""
+        pts = _f32_points(point_cloud)
+        o = self.options
+        opts = RtOptions(o.linear_search_window, o.angular_search_window,
+                         o.translation_delta_cost_weight, o.rotation_delta_cost_weight)
+        cells = np.ascontiguousarray(grid.cells, dtype=np.uint16)
+        lim = grid.limits()
+        init = Pose2D(*initial_pose_estimate)
+        score = C.c_double(0.0)
+        pose = Pose2D()
+        _check(self._lib.csm_rt2d_match(self.context.handle, C.byref(opts), C.byref(lim),
+                                        _ptr(cells, C.c_uint16), grid.min_correspondence_cost,
+                                        grid.max_correspondence_cost, C.byref(init),
+                                        _ptr(pts, C.c_float), len(pts), C.byref(score),
+                                        C.byref(pose)), "csm_rt2d_match")
+        return float(score.value), pose.as_tuple()
+
+
+class ScanSet:
+    """Node point clouds resident on the device (TrajectoryNode::Data clouds)."""
+
+    def __init__(self, clouds: Sequence, context: Optional[Context] = None,
+                 packed: Optional[Tuple[np.ndarray, np.ndarray]] = None):
+        self.context = context or default_context()
+        self._lib = self.context._lib
+        if packed is not None:
+            pts, offsets = packed
+            pts = np.ascontiguousarray(pts, np.float32).reshape(-1, 3)
+            offsets = np.ascontiguousarray(offsets, np.int64)
+        else:
+            arrs = [_f32_points(c) for c in clouds]
+            offsets = np.zeros(len(arrs) + 1, np.int64)
+            offsets[1:] = np.cumsum([len(a) for a in arrs])
+            pts = np.ascontiguousarray(np.concatenate(arrs) if arrs else np.zeros((0, 3), np.float32))
+        self.points, self.offsets = pts, offsets
+        h = C.c_void_p()
+        _check(self._lib.csm_scan_set_create(self.context.handle, _ptr(pts, C.c_float),
+                                             _ptr(offsets, C.c_int64), len(offsets) - 1,
+                                             C.byref(h)), "csm_scan_set_create")
+        self.handle = h
+
+    def __len__(self):
+        return len(self.offsets) - 1
+
+    def close(self):
+        if getattr(self, "handle", None):
+            self._lib.csm_scan_set_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+PAIR_DTYPE = np.dtype([("submap", np.int32), ("scan", np.int32), ("full_submap", np.int32),
+                       ("min_score", np.float32), ("x", np.float64), ("y", np.float64),
+                       ("theta", np.float64)])
+RESULT_DTYPE = np.dtype([("status", np.int32), ("score", np.float32), ("x", np.float64),
+                         ("y", np.float64), ("theta", np.float64)])
+assert PAIR_DTYPE.itemsize == C.sizeof(Pair2D)
+assert RESULT_DTYPE.itemsize == C.sizeof(Result2D)
+
+
+def make_pairs(submap, scan, min_score, full_submap=True, initial=None) -> np.ndarray:
+    submap = np.asarray(submap, np.int32)
+    pairs = np.zeros(len(submap), PAIR_DTYPE)
+    pairs["submap"] = submap
+    pairs["scan"] = np.asarray(scan, np.int32)
+    pairs["full_submap"] = 1 if full_submap else 0
+    pairs["min_score"] = min_score
+    if initial is not None:
+        initial = np.asarray(initial, np.float64).reshape(-1, 3)
+        pairs["x"], pairs["y"], pairs["theta"] = initial[:, 0], initial[:, 1], initial[:, 2]
+    return pairs
+
+
+def match_batch(matchers: Sequence[FastCorrelativeScanMatcher2D], scans: ScanSet,
+                pairs: np.ndarray, context: Optional[Context] = None) -> np.ndarray:
+    """Batched Match / MatchFullSubmap over (submap, node) pairs; returns a
+    RESULT_DTYPE array in pair order (status CSM_OK = constraint found)."""
+    ctx = context or scans.context
+    lib = ctx._lib
+    pairs = np.ascontiguousarray(pairs, PAIR_DTYPE)
+    results = np.zeros(len(pairs), RESULT_DTYPE)
+    handles = (C.c_void_p * len(matchers))(*[m.handle for m in matchers])
+    _check(lib.csm_fast2d_match_batch(ctx.handle, handles, len(matchers), scans.handle,
+                                      pairs.ctypes.data_as(C.POINTER(Pair2D)), len(pairs),
+                                      results.ctypes.data_as(C.POINTER(Result2D))),
+           "csm_fast2d_match_batch")
+    return results
+
+
+# --------------------------------------------------------------------------
+# Synthetic world (bench / test inputs; not the matching path).
+
+class SynthConfig(C.Structure):
+    _fields_ = [("seed", C.c_uint64), ("world_x", C.c_double), ("world_y", C.c_double),
+                ("resolution", C.c_double), ("num_nodes", C.c_int32),
+                ("num_submaps", C.c_int32), ("submap_cells", C.c_int32), ("beams", C.c_int32),
+                ("fov", C.c_double), ("max_range", C.c_double), ("range_noise", C.c_double),
+                ("decimate_to", C.c_int32), ("room_size", C.c_double),
+                ("boxes_per_room", C.c_int32), ("threads", C.c_int32)]
+
+
+class SyntheticWorld2D:
+    """Seeded building world: node clouds + fixed-size submap grids."""
+
+    def __init__(self, num_nodes=500, num_submaps=50, submap_cells=400, beams=1080,
+                 seed=20250127, decimate_to=0, max_range=30.0, threads=0, **kw):
+        lib = C.CDLL(SYNTH_PATH)
+        lib.csm_synth2d_create.argtypes = [C.POINTER(SynthConfig), C.POINTER(C.c_void_p)]
+        for name, t in [("csm_synth2d_point_offsets", C.c_int64), ("csm_synth2d_points", C.c_float),
+                        ("csm_synth2d_node_poses", C.c_double),
+                        ("csm_synth2d_submap_max", C.c_double),
+                        ("csm_synth2d_submap_nodes", C.c_int32),
+                        ("csm_synth2d_submap_cells", C.c_uint16)]:
+            getattr(lib, name).restype = C.POINTER(t)
+            getattr(lib, name).argtypes = [C.c_void_p]
+        lib.csm_synth2d_destroy.argtypes = [C.c_void_p]
+        cfg = SynthConfig()
+        lib.csm_synth2d_default_config(C.byref(cfg))
+        cfg.num_nodes, cfg.num_submaps, cfg.submap_cells = num_nodes, num_submaps, submap_cells
+        cfg.beams, cfg.seed, cfg.decimate_to, cfg.max_range = beams, seed, decimate_to, max_range
+        cfg.threads = threads
+        for k, v in kw.items():
+            setattr(cfg, k, v)
+        h = C.c_void_p()
+        if lib.csm_synth2d_create(C.byref(cfg), C.byref(h)) != 0:
+            raise ValueError("invalid synthetic world config")
+        try:
+            n, s, c = num_nodes, num_submaps, submap_cells
+            self.offsets = np.ctypeslib.as_array(lib.csm_synth2d_point_offsets(h), (n + 1,)).copy()
+            total = int(self.offsets[-1])
+            self.points = np.ctypeslib.as_array(lib.csm_synth2d_points(h), (total * 3,)).reshape(-1, 3).copy() \
+                if total else np.zeros((0, 3), np.float32)
+            self.node_poses = np.ctypeslib.as_array(lib.csm_synth2d_node_poses(h), (n * 3,)).reshape(-1, 3).copy()
+            self.submap_max = np.ctypeslib.as_array(lib.csm_synth2d_submap_max(h), (max(s, 1) * 2,)).reshape(-1, 2)[:s].copy()
+            self.submap_nodes = np.ctypeslib.as_array(lib.csm_synth2d_submap_nodes(h), (max(s, 1),))[:s].copy()
+            self.submap_cells = np.ctypeslib.as_array(lib.csm_synth2d_submap_cells(h), (max(s, 1) * c * c,)).reshape(-1, c, c)[:s].copy()
+        finally:
+            lib.csm_synth2d_destroy(h)
+        self.resolution = cfg.resolution
+        self.num_nodes, self.num_submaps, self.submap_size = num_nodes, num_submaps, submap_cells
+
+    def cloud(self, node: int) -> np.ndarray:
+        return self.points[self.offsets[node]:self.offsets[node + 1]]
+
+    def grid(self, submap: int) -> ProbabilityGrid:
+        # cells[j, i] holds cell (x=i, y=j): flat index i + j * num_x_cells.
+        return ProbabilityGrid(self.resolution, float(self.submap_max[submap, 0]),
+                               float(self.submap_max[submap, 1]), self.submap_cells[submap])

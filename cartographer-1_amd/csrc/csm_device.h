@@ -1,0 +1,88 @@
+// Structures shared between the host runtime and the gfx950 kernels.
+#ifndef CSM_DEVICE_H_
+#define CSM_DEVICE_H_
+
+#include <cstdint>
+
+#if defined(__HIPCC__)
+#define CSM_HD __host__ __device__
+#else
+#define CSM_HD
+#endif
+
+namespace csm {
+
+constexpr int kMaxLevels = 12;
+constexpr int kNumXcd = 8;           // MI355X: 8 XCDs, 32 CUs each
+constexpr int kSearchThreads = 256;  // 4 waves per workgroup
+constexpr int kWaves = kSearchThreads / 64;
+constexpr int kStackCap = 160;       // per-wave DFS stack entries
+constexpr int kTopChunk = 64;        // top-level candidates per DFS chunk
+constexpr int kMaxPoints = 16448;    // 22-bit sum field: 16448 * 255 < 2^22
+constexpr int kIndexLimit = 16383;   // |discretized cell index| bound
+constexpr int kOffsetLimit = 8191;   // |candidate offset| bound (14-bit field)
+constexpr int kMaxRotations = 16383; // 14-bit field
+constexpr int16_t kSentinel = -32768;
+
+// Device pyramid of one submap (PrecomputationGridStack2D): level d is a
+// (nx + 2^d - 1) x (ny + 2^d - 1) uint8 wide grid, x fastest, followed by one
+// zero byte used as the target of out-of-grid lookups.
+struct SubmapDesc {
+  double max_x, max_y, resolution;
+  int32_t nx, ny;
+  int32_t levels;       // search pyramid depth
+  int32_t pad0;
+  const uint8_t* level[kMaxLevels];
+  int32_t wide_nx[kMaxLevels];
+  int32_t wide_ny[kMaxLevels];
+  int32_t zero_index[kMaxLevels];  // index of the trailing zero byte
+};
+
+// One (node, submap) search.
+struct PairDesc {
+  int32_t submap;
+  int32_t num_points;
+  int64_t point_offset;     // into the scan set's packed xyz floats (points)
+  int32_t rot_offset;       // into the rotation table (w, s pairs)
+  int32_t num_scans;
+  int32_t num_linear;       // linear window in cells before ShrinkToFit
+  int32_t max_rejected_sum; // prune / reject sums <= this value
+  float tx, ty;             // initial translation, narrowed to float
+  float pre_w, pre_s;       // initial rotation quaternion (z axis)
+};
+
+// Per-XCD work queues over rotation chunks of pairs.
+struct WorkQueues {
+  const int32_t* pair_order;      // pairs, grouped by queue
+  const int64_t* chunk_prefix;    // per entry of pair_order: first chunk id
+  int32_t queue_begin[kNumXcd + 1];
+  int64_t queue_chunks[kNumXcd];  // chunks per queue
+  int32_t rot_chunk;              // rotations per chunk
+};
+
+// Best leaf per pair, packed for a 64-bit atomicMax:
+//   [63:42] level-0 integer sum (22 bits)
+//   [41:0]  ~(rotation << 28 | (x_off + 8192) << 14 | (y_off + 8192))
+// so the max key is the max sum, ties to the smallest (rotation, x, y).
+constexpr int kSumShift = 42;
+constexpr uint64_t kTieMask = (uint64_t(1) << kSumShift) - 1;
+
+CSM_HD inline uint64_t PackLeafKey(uint32_t sum, int rot, int xo, int yo) {
+  const uint64_t idx = (uint64_t(rot) << 28) | (uint64_t(xo + 8192) << 14) |
+                       uint64_t(yo + 8192);
+  return (uint64_t(sum) << kSumShift) | (~idx & kTieMask);
+}
+CSM_HD inline void UnpackLeafKey(uint64_t key, uint32_t* sum, int* rot, int* xo, int* yo) {
+  *sum = static_cast<uint32_t>(key >> kSumShift);
+  const uint64_t idx = ~key & kTieMask;
+  *rot = static_cast<int>(idx >> 28);
+  *xo = static_cast<int>((idx >> 14) & 0x3fff) - 8192;
+  *yo = static_cast<int>(idx & 0x3fff) - 8192;
+}
+
+// Per-pair status written by the search kernel (0 = ok).
+constexpr int32_t kStatusRange = 1;
+
+}  // namespace csm
+
+#endif  // CSM_DEVICE_H_

@@ -1,0 +1,648 @@
+// Host runtime of the MI355X correlative scan matcher: implements the C-ABI
+// of include/csm_amd.h on top of the kernels in csm_kernels.hip.
+//
+// Ownership follows the reference (fast_correlative_scan_matcher_2d.cc:188-194
+// copies what it needs from the grid): csm_fast2d_create copies the cells to
+// the device and builds the pyramid there; handles own device memory until
+// destroyed. Results are decoded on the host with the reference's double
+// arithmetic (Candidate2D, correlative_scan_matcher_2d.h:75-85, and the pose
+// composition of fast_correlative_scan_matcher_2d.cc:253-259).
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <tuple>
+#include <vector>
+
+#include "../../include/csm_amd.h"
+#include "csm_device.h"
+#include "csm_launch.h"
+#include "search_window.h"
+
+namespace csm {
+
+
+
+namespace {
+
+#define CSM_HIP(call)                               \
+  do {                                              \
+    if ((call) != hipSuccess) return CSM_EHIP;      \
+  } while (0)
+
+// Grow-only device buffer.
+struct DevBuf {
+  void* ptr = nullptr;
+  size_t bytes = 0;
+  ~DevBuf() {
+    if (ptr) (void)hipFree(ptr);
+  }
+  int Reserve(size_t n) {
+    if (n <= bytes) return CSM_OK;
+    if (ptr) (void)hipFree(ptr);
+    ptr = nullptr;
+    bytes = 0;
+    const size_t want = std::max<size_t>(n, 256);
+    if (hipMalloc(&ptr, want) != hipSuccess) return CSM_ENOMEM;
+    bytes = want;
+    return CSM_OK;
+  }
+  template <typename T>
+  T* as() const { return static_cast<T*>(ptr); }
+};
+
+int AutoSearchDepth(int configured, int nx, int ny) {
+  // Extra coarse levels until the top lattice step reaches ~1/2 of the grid:
+  // measured on the synthetic world this cuts lookups 2-4x.
+  int d = configured;
+  const int span = std::max(nx, ny);
+  while (d < kMaxLevels && (1 << (d - 1)) < span / 2) ++d;
+  return std::max(d, configured);
+}
+
+}  // namespace
+}  // namespace csm
+
+using namespace csm;
+
+struct csm_context {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+  DevBuf submap_desc, pair_desc, rot_table, best, status, counters, pair_order,
+      chunk_prefix, stats, rt_prob, rt_cells, rt_points, rt_best, rt_rot, rt_ptab,
+      single_points;
+  bool timing = false;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  csm_timing t{};
+  std::vector<float> ptab_host;
+  bool ptab_uploaded = false;
+  int num_cus = 256;
+};
+
+struct csm_fast2d {
+  csm_context* ctx = nullptr;
+  csm_map_limits limits{};
+  csm_fast2d_options options{};
+  float min_cc = 0.f, max_cc = 0.f, min_s = 0.f, max_s = 0.f;
+  SubmapDesc desc{};
+  DevBuf pyramid;
+};
+
+struct csm_scan_set {
+  csm_context* ctx = nullptr;
+  std::vector<float> host_points;
+  std::vector<int64_t> offsets;
+  DevBuf points;
+  // Rotation tables per (scan, angular window, linear window, resolution).
+  std::map<std::tuple<int, double, double, double>,
+           std::pair<SearchWindow2D, std::vector<ZRot>>>
+      windows;
+};
+
+namespace {
+
+int EnsureDevice(csm_context* ctx) {
+  return hipSetDevice(ctx->device) == hipSuccess ? CSM_OK : CSM_EHIP;
+}
+
+const std::pair<SearchWindow2D, std::vector<ZRot>>& WindowFor(
+    csm_scan_set* s, int scan, double lin, double ang, double res) {
+  const auto key = std::make_tuple(scan, ang, lin, res);
+  auto it = s->windows.find(key);
+  if (it != s->windows.end()) return it->second;
+  const int64_t b = s->offsets[scan], e = s->offsets[scan + 1];
+  // FastCSM builds SearchParameters from the input cloud (:202-204, :215-218).
+  SearchWindow2D w = MakeSearchWindow2D(lin, ang, s->host_points.data() + 3 * b,
+                                        static_cast<int32_t>(e - b), res, nullptr);
+  std::vector<ZRot> table;
+  RotationTable(w, &table);
+  return s->windows.emplace(key, std::make_pair(w, std::move(table))).first->second;
+}
+
+int RunBatch(csm_context* ctx, csm_fast2d* const* submaps, int32_t num_submaps,
+             csm_scan_set* scans, const csm_pair2d* pairs, int64_t num_pairs,
+             csm_result2d* results) {
+  // ---- host preparation ---------------------------------------------------
+  std::vector<SubmapDesc> sdesc(num_submaps);
+  for (int i = 0; i < num_submaps; ++i) {
+    if (!submaps[i] || submaps[i]->ctx != ctx) return CSM_EINVAL;
+    sdesc[i] = submaps[i]->desc;
+  }
+  std::vector<PairDesc> pdesc;
+  std::vector<int64_t> pair_src;  // pdesc index -> pair index
+  std::vector<float2> rot_host;
+  std::map<const void*, int32_t> rot_offsets;  // table ptr -> offset
+  int max_npad = 64;
+  for (int64_t i = 0; i < num_pairs; ++i) {
+    const csm_pair2d& p = pairs[i];
+    results[i].status = CSM_NO_MATCH;
+    results[i].score = 0.f;
+    results[i].pose = csm_pose2d{0., 0., 0.};
+    if (p.submap < 0 || p.submap >= num_submaps || p.scan < 0 ||
+        p.scan >= static_cast<int32_t>(scans->offsets.size()) - 1) {
+      results[i].status = CSM_EINVAL;
+      continue;
+    }
+    const csm_fast2d* m = submaps[p.submap];
+    const int32_t n = static_cast<int32_t>(scans->offsets[p.scan + 1] - scans->offsets[p.scan]);
+    if (n <= 0) continue;  // empty cloud: the reference cannot exceed min_score
+    if (n > kMaxPoints) { results[i].status = CSM_ERANGE; continue; }
+    const double res = m->limits.resolution;
+    double lin, ang;
+    csm_pose2d init;
+    if (p.full_submap) {
+      // fast_correlative_scan_matcher_2d.cc:215-222
+      lin = 1e6 * res;
+      ang = M_PI;
+      const double half = 0.5 * res;
+      init.x = m->limits.max_x - half * m->limits.num_y_cells;
+      init.y = m->limits.max_y - half * m->limits.num_x_cells;
+      init.theta = 0.;
+    } else {
+      lin = m->options.linear_search_window;
+      ang = m->options.angular_search_window;
+      init = p.initial;
+    }
+    const auto& win = WindowFor(scans, p.scan, lin, ang, res);
+    if (win.first.num_scans > kMaxRotations) { results[i].status = CSM_ERANGE; continue; }
+    auto ro = rot_offsets.find(&win);
+    int32_t off;
+    if (ro == rot_offsets.end()) {
+      off = static_cast<int32_t>(rot_host.size());
+      for (const ZRot& z : win.second) rot_host.push_back(make_float2(z.w, z.s));
+      rot_offsets.emplace(&win, off);
+    } else {
+      off = ro->second;
+    }
+    PairDesc d{};
+    d.submap = p.submap;
+    d.num_points = n;
+    d.point_offset = scans->offsets[p.scan];
+    d.rot_offset = off;
+    d.num_scans = win.first.num_scans;
+    d.num_linear = std::min(win.first.num_linear_perturbations, 1 << 20);
+    d.max_rejected_sum = static_cast<int32_t>(MaxRejectedSum(p.min_score, n, m->min_s, m->max_s));
+    d.tx = static_cast<float>(init.x);
+    d.ty = static_cast<float>(init.y);
+    const ZRot pre = MakeZRot(static_cast<float>(init.theta));
+    d.pre_w = pre.w;
+    d.pre_s = pre.s;
+    pdesc.push_back(d);
+    pair_src.push_back(i);
+    max_npad = std::max(max_npad, (n + 63) & ~63);
+  }
+  const int np = static_cast<int>(pdesc.size());
+  if (np == 0) return CSM_OK;
+
+  // Rotation chunk size from the LDS budget for discretized points.
+  const int lds_budget = 40 * 1024;
+  const int rc = std::max(1, std::min(16, lds_budget / (max_npad * 4)));
+
+  // Per-XCD queues: submap s -> queue s % 8 so a submap's pyramid stays in
+  // one XCD's L2; pairs within a queue in submap order.
+  std::vector<std::vector<int32_t>> q(kNumXcd);
+  for (int i = 0; i < np; ++i) q[pdesc[i].submap % kNumXcd].push_back(i);
+  // Rebalance: if a queue is much larger than the mean, spill whole submaps.
+  std::vector<int32_t> order;
+  std::vector<int64_t> prefix;
+  WorkQueues wq{};
+  wq.rot_chunk = rc;
+  int64_t running = 0;
+  for (int x = 0; x < kNumXcd; ++x) {
+    std::stable_sort(q[x].begin(), q[x].end(),
+                     [&](int a, int b) { return pdesc[a].submap < pdesc[b].submap; });
+    wq.queue_begin[x] = static_cast<int32_t>(order.size());
+    const int64_t qstart = running;
+    for (int pi : q[x]) {
+      order.push_back(pi);
+      prefix.push_back(running);
+      running += (pdesc[pi].num_scans + rc - 1) / rc;
+    }
+    wq.queue_chunks[x] = running - qstart;
+  }
+  wq.queue_begin[kNumXcd] = static_cast<int32_t>(order.size());
+  prefix.push_back(running);
+
+  // ---- uploads ---------------------------------------------------------------
+  int rcode;
+  if ((rcode = ctx->submap_desc.Reserve(sizeof(SubmapDesc) * num_submaps))) return rcode;
+  if ((rcode = ctx->pair_desc.Reserve(sizeof(PairDesc) * np))) return rcode;
+  if ((rcode = ctx->rot_table.Reserve(sizeof(float2) * rot_host.size()))) return rcode;
+  if ((rcode = ctx->best.Reserve(sizeof(uint64_t) * np))) return rcode;
+  if ((rcode = ctx->status.Reserve(sizeof(int32_t) * np))) return rcode;
+  if ((rcode = ctx->counters.Reserve(sizeof(unsigned long long) * kNumXcd))) return rcode;
+  if ((rcode = ctx->pair_order.Reserve(sizeof(int32_t) * order.size()))) return rcode;
+  if ((rcode = ctx->chunk_prefix.Reserve(sizeof(int64_t) * prefix.size()))) return rcode;
+  if ((rcode = ctx->stats.Reserve(sizeof(unsigned long long) * 2))) return rcode;
+  hipStream_t st = ctx->stream;
+  CSM_HIP(hipMemcpyAsync(ctx->submap_desc.ptr, sdesc.data(), sizeof(SubmapDesc) * num_submaps,
+                         hipMemcpyHostToDevice, st));
+  CSM_HIP(hipMemcpyAsync(ctx->pair_desc.ptr, pdesc.data(), sizeof(PairDesc) * np,
+                         hipMemcpyHostToDevice, st));
+  CSM_HIP(hipMemcpyAsync(ctx->rot_table.ptr, rot_host.data(), sizeof(float2) * rot_host.size(),
+                         hipMemcpyHostToDevice, st));
+  CSM_HIP(hipMemcpyAsync(ctx->pair_order.ptr, order.data(), sizeof(int32_t) * order.size(),
+                         hipMemcpyHostToDevice, st));
+  CSM_HIP(hipMemcpyAsync(ctx->chunk_prefix.ptr, prefix.data(), sizeof(int64_t) * prefix.size(),
+                         hipMemcpyHostToDevice, st));
+  CSM_HIP(hipMemsetAsync(ctx->best.ptr, 0, sizeof(uint64_t) * np, st));
+  CSM_HIP(hipMemsetAsync(ctx->status.ptr, 0, sizeof(int32_t) * np, st));
+  CSM_HIP(hipMemsetAsync(ctx->counters.ptr, 0, sizeof(unsigned long long) * kNumXcd, st));
+  CSM_HIP(hipMemsetAsync(ctx->stats.ptr, 0, sizeof(unsigned long long) * 2, st));
+  wq.pair_order = ctx->pair_order.as<int32_t>();
+  wq.chunk_prefix = ctx->chunk_prefix.as<int64_t>();
+
+  // ---- launch: persistent workgroups, 4 per CU ------------------------------
+  const size_t dyn_lds = static_cast<size_t>(rc) * max_npad * sizeof(uint32_t);
+  const int64_t total_chunks = running;
+  const int grid = static_cast<int>(std::min<int64_t>(static_cast<int64_t>(ctx->num_cus) * 4,
+                                                      std::max<int64_t>(total_chunks, 1)));
+  if (ctx->timing) CSM_HIP(hipEventRecord(ctx->ev0, st));
+  CSM_HIP(LaunchFast2dSearch(grid, dyn_lds, st, ctx->submap_desc.as<SubmapDesc>(),
+                             ctx->pair_desc.as<PairDesc>(), scans->points.as<float>(),
+                             ctx->rot_table.as<float2>(), wq,
+                             ctx->counters.as<unsigned long long>(), ctx->best.as<uint64_t>(),
+                             ctx->status.as<int32_t>(), ctx->stats.as<unsigned long long>()));
+  if (ctx->timing) CSM_HIP(hipEventRecord(ctx->ev1, st));
+
+  std::vector<uint64_t> keys(np);
+  std::vector<int32_t> stat(np);
+  unsigned long long stats_host[2] = {0, 0};
+  CSM_HIP(hipMemcpyAsync(keys.data(), ctx->best.ptr, sizeof(uint64_t) * np,
+                         hipMemcpyDeviceToHost, st));
+  CSM_HIP(hipMemcpyAsync(stat.data(), ctx->status.ptr, sizeof(int32_t) * np,
+                         hipMemcpyDeviceToHost, st));
+  CSM_HIP(hipMemcpyAsync(stats_host, ctx->stats.ptr, sizeof(stats_host),
+                         hipMemcpyDeviceToHost, st));
+  CSM_HIP(hipStreamSynchronize(st));
+  if (ctx->timing) {
+    float ms = 0.f;
+    CSM_HIP(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+    ctx->t.search_kernel_ms += ms;
+    ctx->t.search_launches += 1;
+    ctx->t.search_candidates += static_cast<double>(stats_host[0]);
+    ctx->t.search_lookups += static_cast<double>(stats_host[1]);
+  }
+
+  // ---- decode -----------------------------------------------------------------
+  for (int k = 0; k < np; ++k) {
+    const int64_t i = pair_src[k];
+    const PairDesc& d = pdesc[k];
+    const csm_pair2d& p = pairs[i];
+    const csm_fast2d* m = submaps[p.submap];
+    if (stat[k] & kStatusRange) {
+      results[i].status = CSM_ERANGE;
+      continue;
+    }
+    uint32_t sum;
+    int rot, xo, yo;
+    UnpackLeafKey(keys[k], &sum, &rot, &xo, &yo);
+    if (keys[k] == 0 || static_cast<int64_t>(sum) <= d.max_rejected_sum) {
+      results[i].status = CSM_NO_MATCH;
+      continue;
+    }
+    const double res = m->limits.resolution;
+    csm_pose2d init;
+    if (p.full_submap) {
+      const double half = 0.5 * res;
+      init.x = m->limits.max_x - half * m->limits.num_y_cells;
+      init.y = m->limits.max_y - half * m->limits.num_x_cells;
+      init.theta = 0.;
+    } else {
+      init = p.initial;
+    }
+    const double lin = p.full_submap ? 1e6 * res : m->options.linear_search_window;
+    const double ang = p.full_submap ? M_PI : m->options.angular_search_window;
+    const SearchWindow2D& w = WindowFor(scans, p.scan, lin, ang, res).first;
+    // Candidate2D: x = -y_off * res, y = -x_off * res,
+    // orientation = (scan_index - num_angular) * step.
+    const double cx = -yo * res, cy = -xo * res;
+    const double co = (rot - w.num_angular_perturbations) * w.angular_perturbation_step_size;
+    results[i].status = CSM_OK;
+    results[i].score = SumToScore(sum, d.num_points, m->min_s, m->max_s);
+    results[i].pose.x = init.x + cx;
+    results[i].pose.y = init.y + cy;
+    results[i].pose.theta = init.theta + co;
+  }
+  return CSM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* csm_strerror(int code) {
+  switch (code) {
+    case CSM_OK: return "ok";
+    case CSM_NO_MATCH: return "no match above min_score";
+    case CSM_EINVAL: return "invalid argument";
+    case CSM_EHIP: return "HIP runtime error";
+    case CSM_ENOMEM: return "device out of memory";
+    case CSM_ERANGE: return "input exceeds the device path's index limits";
+    default: return "unknown error";
+  }
+}
+
+int csm_context_create(int32_t device, csm_context** out) {
+  if (!out) return CSM_EINVAL;
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || device < 0 || device >= count) return CSM_EHIP;
+  auto ctx = std::make_unique<csm_context>();
+  ctx->device = device;
+  CSM_HIP(hipSetDevice(device));
+  CSM_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+  CSM_HIP(hipEventCreate(&ctx->ev0));
+  CSM_HIP(hipEventCreate(&ctx->ev1));
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+    ctx->num_cus = prop.multiProcessorCount;
+  *out = ctx.release();
+  return CSM_OK;
+}
+
+void csm_context_destroy(csm_context* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
+  if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+void* csm_context_stream(csm_context* ctx) { return ctx ? ctx->stream : nullptr; }
+
+void csm_context_enable_timing(csm_context* ctx, int32_t enable) {
+  if (ctx) ctx->timing = enable != 0;
+}
+void csm_context_get_timing(csm_context* ctx, csm_timing* out) {
+  if (ctx && out) *out = ctx->t;
+}
+void csm_context_reset_timing(csm_context* ctx) {
+  if (ctx) ctx->t = csm_timing{};
+}
+
+int csm_fast2d_create(csm_context* ctx, const csm_map_limits* limits,
+                      const uint16_t* cells, float min_cc, float max_cc,
+                      const csm_fast2d_options* options, csm_fast2d** out) {
+  if (!ctx || !limits || !cells || !options || !out) return CSM_EINVAL;
+  if (options->branch_and_bound_depth < 1 || limits->num_x_cells < 1 ||
+      limits->num_y_cells < 1 || !(limits->resolution > 0.) || !(min_cc < max_cc))
+    return CSM_EINVAL;
+  if (limits->num_x_cells > 8192 || limits->num_y_cells > 8192 ||
+      options->branch_and_bound_depth > kMaxLevels)
+    return CSM_ERANGE;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  if (EnsureDevice(ctx)) return CSM_EHIP;
+  auto m = std::make_unique<csm_fast2d>();
+  m->ctx = ctx;
+  m->limits = *limits;
+  m->options = *options;
+  m->min_cc = min_cc;
+  m->max_cc = max_cc;
+  m->min_s = 1.f - max_cc;  // fast_correlative_scan_matcher_2d.cc:97-98
+  m->max_s = 1.f - min_cc;
+  const int nx = limits->num_x_cells, ny = limits->num_y_cells;
+  int depth = options->search_depth > 0 ? options->search_depth
+                                        : AutoSearchDepth(options->branch_and_bound_depth, nx, ny);
+  depth = std::max(depth, options->branch_and_bound_depth);
+  depth = std::min(depth, kMaxLevels);
+  m->options.search_depth = depth;
+  std::vector<uint8_t> qtab(32768);
+  if (!QuantizationTable(min_cc, max_cc, qtab.data())) return CSM_EINVAL;
+
+  SubmapDesc& d = m->desc;
+  d.max_x = limits->max_x;
+  d.max_y = limits->max_y;
+  d.resolution = limits->resolution;
+  d.nx = nx;
+  d.ny = ny;
+  d.levels = depth;
+  size_t total = 0;
+  std::vector<size_t> offs(depth);
+  for (int l = 0; l < depth; ++l) {
+    const int w = 1 << l;
+    d.wide_nx[l] = nx + w - 1;
+    d.wide_ny[l] = ny + w - 1;
+    d.zero_index[l] = d.wide_nx[l] * d.wide_ny[l];
+    offs[l] = total;
+    total += (static_cast<size_t>(d.zero_index[l]) + 1 + 255) & ~size_t(255);
+  }
+  int rc;
+  if ((rc = m->pyramid.Reserve(total))) return rc;
+  for (int l = 0; l < depth; ++l) d.level[l] = m->pyramid.as<uint8_t>() + offs[l];
+
+  DevBuf dcells, dq;
+  if ((rc = dcells.Reserve(sizeof(uint16_t) * nx * ny))) return rc;
+  if ((rc = dq.Reserve(32768))) return rc;
+  hipStream_t st = ctx->stream;
+  CSM_HIP(hipMemcpyAsync(dcells.ptr, cells, sizeof(uint16_t) * nx * ny, hipMemcpyHostToDevice, st));
+  CSM_HIP(hipMemcpyAsync(dq.ptr, qtab.data(), 32768, hipMemcpyHostToDevice, st));
+  const int n0 = nx * ny;
+  CSM_HIP(LaunchPyramidLevel0(dcells.as<uint16_t>(), dq.as<uint8_t>(),
+                              const_cast<uint8_t*>(d.level[0]), n0, st));
+  for (int l = 1; l < depth; ++l) {
+    CSM_HIP(LaunchPyramidDouble(d.level[l - 1], d.wide_nx[l - 1], d.wide_ny[l - 1],
+                                const_cast<uint8_t*>(d.level[l]), d.wide_nx[l], d.wide_ny[l],
+                                1 << (l - 1), st));
+  }
+  CSM_HIP(hipStreamSynchronize(st));  // dcells/dq are freed on return
+  *out = m.release();
+  return CSM_OK;
+}
+
+void csm_fast2d_destroy(csm_fast2d* m) {
+  if (!m) return;
+  (void)hipSetDevice(m->ctx->device);
+  delete m;
+}
+
+int csm_fast2d_read_level(const csm_fast2d* m, int32_t level, uint8_t* out,
+                          int64_t capacity, int32_t* wide_nx, int32_t* wide_ny) {
+  if (!m || level < 0 || level >= m->desc.levels || !wide_nx || !wide_ny) return CSM_EINVAL;
+  *wide_nx = m->desc.wide_nx[level];
+  *wide_ny = m->desc.wide_ny[level];
+  const int64_t n = static_cast<int64_t>(*wide_nx) * *wide_ny;
+  if (!out) return CSM_OK;
+  if (capacity < n) return CSM_EINVAL;
+  std::lock_guard<std::mutex> lock(m->ctx->mu);
+  if (EnsureDevice(m->ctx)) return CSM_EHIP;
+  CSM_HIP(hipMemcpyAsync(out, m->desc.level[level], n, hipMemcpyDeviceToHost, m->ctx->stream));
+  CSM_HIP(hipStreamSynchronize(m->ctx->stream));
+  return CSM_OK;
+}
+
+int csm_scan_set_create(csm_context* ctx, const float* points_xyz, const int64_t* offsets,
+                        int32_t num_scans, csm_scan_set** out) {
+  if (!ctx || !offsets || !out || num_scans < 0) return CSM_EINVAL;
+  const int64_t total = offsets[num_scans];
+  if (total < 0 || (total > 0 && !points_xyz)) return CSM_EINVAL;
+  for (int32_t i = 0; i < num_scans; ++i)
+    if (offsets[i + 1] < offsets[i]) return CSM_EINVAL;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  if (EnsureDevice(ctx)) return CSM_EHIP;
+  auto s = std::make_unique<csm_scan_set>();
+  s->ctx = ctx;
+  s->offsets.assign(offsets, offsets + num_scans + 1);
+  s->host_points.assign(points_xyz, points_xyz + 3 * total);
+  int rc;
+  if ((rc = s->points.Reserve(sizeof(float) * 3 * std::max<int64_t>(total, 1)))) return rc;
+  if (total > 0)
+    CSM_HIP(hipMemcpyAsync(s->points.ptr, points_xyz, sizeof(float) * 3 * total,
+                           hipMemcpyHostToDevice, ctx->stream));
+  CSM_HIP(hipStreamSynchronize(ctx->stream));
+  *out = s.release();
+  return CSM_OK;
+}
+
+void csm_scan_set_destroy(csm_scan_set* s) {
+  if (!s) return;
+  (void)hipSetDevice(s->ctx->device);
+  delete s;
+}
+
+int csm_fast2d_match_batch(csm_context* ctx, csm_fast2d* const* submaps, int32_t num_submaps,
+                           const csm_scan_set* scans, const csm_pair2d* pairs,
+                           int64_t num_pairs, csm_result2d* results) {
+  if (!ctx || !submaps || !scans || (num_pairs > 0 && (!pairs || !results)) || num_pairs < 0 ||
+      scans->ctx != ctx)
+    return CSM_EINVAL;
+  if (num_pairs == 0) return CSM_OK;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  if (EnsureDevice(ctx)) return CSM_EHIP;
+  return RunBatch(ctx, submaps, num_submaps, const_cast<csm_scan_set*>(scans), pairs, num_pairs,
+                  results);
+}
+
+static int SingleMatch(const csm_fast2d* m, const csm_pose2d* initial, int full,
+                       const float* xyz, int32_t n, float min_score, float* score,
+                       csm_pose2d* pose) {
+  if (!m || !score || !pose || (n > 0 && !xyz) || n < 0 || (!full && !initial)) return CSM_EINVAL;
+  csm_context* ctx = m->ctx;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  if (EnsureDevice(ctx)) return CSM_EHIP;
+  csm_scan_set s;
+  s.ctx = ctx;
+  s.offsets = {0, n};
+  s.host_points.assign(xyz, xyz + 3 * static_cast<size_t>(n));
+  int rc;
+  if ((rc = s.points.Reserve(sizeof(float) * 3 * std::max(n, 1)))) return rc;
+  if (n > 0)
+    CSM_HIP(hipMemcpyAsync(s.points.ptr, xyz, sizeof(float) * 3 * n, hipMemcpyHostToDevice,
+                           ctx->stream));
+  csm_pair2d p{};
+  p.submap = 0;
+  p.scan = 0;
+  p.full_submap = full;
+  p.min_score = min_score;
+  if (!full) p.initial = *initial;
+  csm_fast2d* const handles[1] = {const_cast<csm_fast2d*>(m)};
+  csm_result2d r{};
+  rc = RunBatch(ctx, handles, 1, &s, &p, 1, &r);
+  if (rc < 0) return rc;
+  if (r.status == CSM_OK) {
+    *score = r.score;
+    *pose = r.pose;
+  }
+  return r.status;
+}
+
+int csm_fast2d_match(const csm_fast2d* m, const csm_pose2d* initial, const float* points_xyz,
+                     int32_t n, float min_score, float* score, csm_pose2d* pose) {
+  return SingleMatch(m, initial, 0, points_xyz, n, min_score, score, pose);
+}
+
+int csm_fast2d_match_full_submap(const csm_fast2d* m, const float* points_xyz, int32_t n,
+                                 float min_score, float* score, csm_pose2d* pose) {
+  return SingleMatch(m, nullptr, 1, points_xyz, n, min_score, score, pose);
+}
+
+int csm_rt2d_match(csm_context* ctx, const csm_rt_options* o, const csm_map_limits* l,
+                   const uint16_t* cells, float min_cc, float max_cc, const csm_pose2d* initial,
+                   const float* xyz, int32_t n, double* score, csm_pose2d* pose) {
+  (void)min_cc;
+  (void)max_cc;
+  if (!ctx || !o || !l || !cells || !initial || !score || !pose || n <= 0 || !xyz)
+    return CSM_EINVAL;
+  if (l->num_x_cells < 1 || l->num_y_cells < 1 || !(l->resolution > 0.)) return CSM_EINVAL;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  if (EnsureDevice(ctx)) return CSM_EHIP;
+  hipStream_t st = ctx->stream;
+  int rc;
+  // real_time_correlative_scan_matcher_2d.cc:123-130: window on the
+  // pre-rotated cloud.
+  const ZRot pre = MakeZRot(static_cast<float>(initial->theta));
+  const SearchWindow2D w = MakeSearchWindow2D(o->linear_search_window, o->angular_search_window,
+                                              xyz, n, l->resolution, &pre);
+  std::vector<ZRot> table;
+  RotationTable(w, &table);
+  std::vector<float2> rot(table.size());
+  for (size_t i = 0; i < table.size(); ++i) rot[i] = make_float2(table[i].w, table[i].s);
+  const int nx = l->num_x_cells, ny = l->num_y_cells, ncell = nx * ny;
+  if (!ctx->ptab_uploaded) {
+    ctx->ptab_host.resize(32768);
+    ProbabilityTable(ctx->ptab_host.data());
+    if ((rc = ctx->rt_ptab.Reserve(sizeof(float) * 32768))) return rc;
+    CSM_HIP(hipMemcpyAsync(ctx->rt_ptab.ptr, ctx->ptab_host.data(), sizeof(float) * 32768,
+                           hipMemcpyHostToDevice, st));
+    ctx->ptab_uploaded = true;
+  }
+  if ((rc = ctx->rt_cells.Reserve(sizeof(uint16_t) * ncell))) return rc;
+  if ((rc = ctx->rt_prob.Reserve(sizeof(float) * ncell))) return rc;
+  if ((rc = ctx->rt_points.Reserve(sizeof(float) * 3 * n))) return rc;
+  if ((rc = ctx->rt_rot.Reserve(sizeof(float2) * rot.size()))) return rc;
+  if ((rc = ctx->rt_best.Reserve(sizeof(unsigned long long)))) return rc;
+  CSM_HIP(hipMemcpyAsync(ctx->rt_cells.ptr, cells, sizeof(uint16_t) * ncell, hipMemcpyHostToDevice, st));
+  CSM_HIP(hipMemcpyAsync(ctx->rt_points.ptr, xyz, sizeof(float) * 3 * n, hipMemcpyHostToDevice, st));
+  CSM_HIP(hipMemcpyAsync(ctx->rt_rot.ptr, rot.data(), sizeof(float2) * rot.size(),
+                         hipMemcpyHostToDevice, st));
+  CSM_HIP(hipMemsetAsync(ctx->rt_best.ptr, 0, sizeof(unsigned long long), st));
+  CSM_HIP(LaunchCellsToProbability(ctx->rt_cells.as<uint16_t>(), ctx->rt_ptab.as<float>(),
+                                   ctx->rt_prob.as<float>(), ncell, st));
+  const int L = w.num_linear_perturbations;
+  const int side = 2 * L + 1;
+  const int64_t per_rot = static_cast<int64_t>(side) * side;
+  if (per_rot * w.num_scans > 0xffffffffll || static_cast<size_t>(n) * 8 > 60 * 1024)
+    return CSM_ERANGE;
+  const int block = 256;
+  if (ctx->timing) CSM_HIP(hipEventRecord(ctx->ev0, st));
+  CSM_HIP(LaunchRt2dScore(dim3(static_cast<unsigned>((per_rot + block - 1) / block), w.num_scans),
+                          block, sizeof(int2) * n, st, ctx->rt_prob.as<float>(), nx, ny, l->max_x,
+                          l->max_y, l->resolution, ctx->rt_points.as<float>(), n,
+                          ctx->rt_rot.as<float2>(), pre.w, pre.s, static_cast<float>(initial->x),
+                          static_cast<float>(initial->y), L, w.num_angular_perturbations,
+                          w.angular_perturbation_step_size, o->translation_delta_cost_weight,
+                          o->rotation_delta_cost_weight, ctx->rt_best.as<unsigned long long>()));
+  if (ctx->timing) CSM_HIP(hipEventRecord(ctx->ev1, st));
+  unsigned long long key = 0;
+  CSM_HIP(hipMemcpyAsync(&key, ctx->rt_best.ptr, sizeof(key), hipMemcpyDeviceToHost, st));
+  CSM_HIP(hipStreamSynchronize(st));
+  if (ctx->timing) {
+    float ms = 0.f;
+    CSM_HIP(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+    ctx->t.other_kernel_ms += ms;
+  }
+  if (key == 0) return CSM_EINVAL;
+  const uint32_t bits = static_cast<uint32_t>(key >> 32);
+  float s;
+  std::memcpy(&s, &bits, sizeof(s));
+  const uint32_t idx = 0xffffffffu - static_cast<uint32_t>(key & 0xffffffffu);
+  const int r = static_cast<int>(idx / per_rot);
+  const int t = static_cast<int>(idx % per_rot);
+  const int xo = -L + t / side, yo = -L + t % side;
+  const double cx = -yo * l->resolution, cy = -xo * l->resolution;
+  const double co = (r - w.num_angular_perturbations) * w.angular_perturbation_step_size;
+  pose->x = initial->x + cx;
+  pose->y = initial->y + cy;
+  pose->theta = initial->theta + co;
+  *score = s;
+  return CSM_OK;
+}
+
+}  // extern "C"

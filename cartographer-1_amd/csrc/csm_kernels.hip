@@ -1,0 +1,586 @@
+// gfx950 kernels of the correlative scan matcher.
+//
+//   K1  pyramid_level0 / pyramid_double — PrecomputationGridStack2D
+//       (fast_correlative_scan_matcher_2d.cc:91-186) built on the device.
+//   K2-K4 fast2d_search — per (pair, rotation chunk): discretize the rotated
+//       scan slice into LDS (correlative_scan_matcher_2d.cc:93-127 +
+//       map_limits.h:69-75), ShrinkToFit (:73-91), score the top-level lattice
+//       (fast_correlative_scan_matcher_2d.cc:264-333) and run an exact
+//       depth-first branch and bound per wave (:335-378) against a per-pair
+//       incumbent shared through a 64-bit atomicMax.
+//   K5  rt2d_score — RealTimeCorrelativeScanMatcher2D::ScoreCandidates
+//       (real_time_correlative_scan_matcher_2d.cc:61-75, 151-176) and the
+//       first-max selection (:142-143).
+//
+// Built with -ffp-contract=off; the discretization additionally uses the
+// explicit round-to-nearest intrinsics so no multiply-add is ever fused:
+// the x86-64 reference build has no FMA (DESIGN.md "Bitwise discretization").
+
+#include <hip/hip_runtime.h>
+
+#include "csm_device.h"
+
+namespace csm {
+
+// ---------------------------------------------------------------- helpers ---
+
+__device__ __forceinline__ void RotateZDev(float w, float s, float x, float y,
+                                           float* ox, float* oy) {
+  // Eigen QuaternionBase::_transformVector with q.vec = (0, 0, s).
+  const float uvx = __fsub_rn(0.f, __fmul_rn(s, y));
+  const float uvy = __fsub_rn(__fmul_rn(s, x), 0.f);
+  const float ux = __fadd_rn(uvx, uvx);
+  const float uy = __fadd_rn(uvy, uvy);
+  const float cx = __fsub_rn(0.f, __fmul_rn(s, uy));
+  const float cy = __fsub_rn(__fmul_rn(s, ux), 0.f);
+  *ox = __fadd_rn(__fadd_rn(x, __fmul_rn(w, ux)), cx);
+  *oy = __fadd_rn(__fadd_rn(y, __fmul_rn(w, uy)), cy);
+}
+
+// MapLimits::GetCellIndex: lround((max - p) / resolution - 0.5) in double.
+__device__ __forceinline__ double CellCoord(double max_v, float p, double res) {
+  return __builtin_round(__dsub_rn(__ddiv_rn(__dsub_rn(max_v, static_cast<double>(p)), res), 0.5));
+}
+
+__device__ __forceinline__ int WaveSum(int v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+  return v;
+}
+__device__ __forceinline__ int WaveMin(int v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v = min(v, __shfl_xor(v, m, 64));
+  return v;
+}
+__device__ __forceinline__ int WaveMax(int v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v = max(v, __shfl_xor(v, m, 64));
+  return v;
+}
+__device__ __forceinline__ int Uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+__device__ __forceinline__ uint64_t LoadBest(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ---------------------------------------------------------------- K1 -------
+
+// Level 0: quantized probability of every cell (ComputeCellValue of
+// 1 - |cc|); the table is computed on the host with the reference's float
+// arithmetic. The trailing byte of every level is a zero sentinel.
+__global__ void pyramid_level0(const uint16_t* __restrict__ cells,
+                               const uint8_t* __restrict__ qtab,
+                               uint8_t* __restrict__ out, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = qtab[cells[i] & 0x7fff];
+  if (i == n) out[n] = 0;
+}
+
+// Level d from level d-1 (h = 2^(d-1)): wide cell l covers source cells
+// [l - 2h + 1, l] = cover(l - h) u cover(l) of level d-1, per axis; an empty
+// cover contributes 0, which never changes a max of uint8 values.
+__global__ void pyramid_double(const uint8_t* __restrict__ prev, int pnx, int pny,
+                               uint8_t* __restrict__ next, int nnx, int nny, int h) {
+  const int lx = blockIdx.x * blockDim.x + threadIdx.x;
+  const int ly = blockIdx.y;
+  if (ly == 0 && lx == 0) next[static_cast<size_t>(nnx) * nny] = 0;
+  if (lx >= nnx || ly >= nny) return;
+  int v = 0;
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+    const int my = ly - a * h;
+    if (my < 0 || my >= pny) continue;
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int mx = lx - b * h;
+      if (mx < 0 || mx >= pnx) continue;
+      v = max(v, static_cast<int>(prev[static_cast<size_t>(my) * pnx + mx]));
+    }
+  }
+  next[static_cast<size_t>(ly) * nnx + lx] = static_cast<uint8_t>(v);
+}
+
+// ---------------------------------------------------------------- K2-K4 ----
+
+struct LevelView {
+  const uint8_t* data;
+  int wnx, wny, zero, bias;  // local index = cell + bias, bias = 2^d - 1
+};
+
+__device__ __forceinline__ LevelView MakeView(const SubmapDesc& s, int d) {
+  LevelView v;
+  v.data = s.level[d];
+  v.wnx = s.wide_nx[d];
+  v.wny = s.wide_ny[d];
+  v.zero = s.zero_index[d];
+  v.bias = (1 << d) - 1;
+  return v;
+}
+
+// Scores the (up to) four children (xo + {0,h}) x (yo + {0,h}) of one node
+// at level view L. Lanes walk the rotation's discretized points (packed
+// int16 pairs in LDS, padded with sentinels to a multiple of 64).
+__device__ __forceinline__ void ScoreChildren(const uint32_t* __restrict__ pts,
+                                              int npad, const LevelView& L,
+                                              int xo, int yo, int h, int out[4]) {
+  const int lane = threadIdx.x & 63;
+  int a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+  const int hw = h * L.wnx;
+  for (int i = lane; i < npad; i += 64) {
+    const uint32_t p = pts[i];
+    const int lx = static_cast<int>(static_cast<int16_t>(p & 0xffff)) + xo + L.bias;
+    const int ly = static_cast<int>(p) >> 16;
+    const int lyy = ly + yo + L.bias;
+    const bool vx0 = static_cast<unsigned>(lx) < static_cast<unsigned>(L.wnx);
+    const bool vx1 = static_cast<unsigned>(lx + h) < static_cast<unsigned>(L.wnx);
+    const bool vy0 = static_cast<unsigned>(lyy) < static_cast<unsigned>(L.wny);
+    const bool vy1 = static_cast<unsigned>(lyy + h) < static_cast<unsigned>(L.wny);
+    const int base = lyy * L.wnx + lx;
+    a0 += L.data[(vx0 && vy0) ? base : L.zero];
+    a1 += L.data[(vx0 && vy1) ? base + hw : L.zero];
+    a2 += L.data[(vx1 && vy0) ? base + h : L.zero];
+    a3 += L.data[(vx1 && vy1) ? base + hw + h : L.zero];
+  }
+  out[0] = WaveSum(a0);  // (xo,     yo)
+  out[1] = WaveSum(a1);  // (xo,     yo + h)
+  out[2] = WaveSum(a2);  // (xo + h, yo)
+  out[3] = WaveSum(a3);  // (xo + h, yo + h)
+}
+
+// Scores one candidate at level view L.
+__device__ __forceinline__ int ScoreOne(const uint32_t* __restrict__ pts, int npad,
+                                        const LevelView& L, int xo, int yo) {
+  const int lane = threadIdx.x & 63;
+  int acc = 0;
+  for (int i = lane; i < npad; i += 64) {
+    const uint32_t p = pts[i];
+    const int lx = static_cast<int>(static_cast<int16_t>(p & 0xffff)) + xo + L.bias;
+    const int ly = (static_cast<int>(p) >> 16) + yo + L.bias;
+    const bool v = static_cast<unsigned>(lx) < static_cast<unsigned>(L.wnx) &&
+                   static_cast<unsigned>(ly) < static_cast<unsigned>(L.wny);
+    acc += L.data[v ? ly * L.wnx + lx : L.zero];
+  }
+  return WaveSum(acc);
+}
+
+struct RotInfo {
+  int min_x, max_x, min_y, max_y;  // ShrinkToFit bounds
+  int top_begin;                   // prefix of top-level candidates
+  int top_nx, top_ny;
+  int pad;
+};
+
+// Stack entry: w0 = (uint16 xo) | (yo << 16); w1 = sum | rot << 22 | level << 27.
+__device__ __forceinline__ uint2 MakeEntry(int xo, int yo, int sum, int rot, int level) {
+  return make_uint2((static_cast<uint32_t>(xo) & 0xffff) | (static_cast<uint32_t>(yo) << 16),
+                    static_cast<uint32_t>(sum) | (static_cast<uint32_t>(rot) << 22) |
+                        (static_cast<uint32_t>(level) << 27));
+}
+
+__global__ void __launch_bounds__(kSearchThreads)
+fast2d_search(const SubmapDesc* __restrict__ submaps,
+              const PairDesc* __restrict__ pairs,
+              const float* __restrict__ points,        // xyz
+              const float2* __restrict__ rot_table,    // (w, s)
+              WorkQueues queues,
+              unsigned long long* __restrict__ counters,  // kNumXcd claim counters
+              uint64_t* __restrict__ best,            // per pair leaf key
+              int32_t* __restrict__ status,            // per pair
+              unsigned long long* __restrict__ stats)  // [0] candidates scored, [1] lookups
+{
+  extern __shared__ __align__(16) uint32_t lds_pts[];  // rot_chunk * npad_max
+  __shared__ RotInfo rinfo[32];
+  __shared__ uint2 stack[kWaves][kStackCap];
+  __shared__ uint32_t top_xy[kWaves][kTopChunk];
+  __shared__ int top_meta[kWaves][kTopChunk];  // sum | rot << 22
+  __shared__ int s_item_pair, s_item_chunk, s_total_top, s_next_chunk, s_queue;
+  __shared__ int s_mm[32][4];
+
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6;
+  const int lane = tid & 63;
+  const int rc = queues.rot_chunk;
+  unsigned long long local_cands = 0, local_lookups = 0;
+
+  if (tid == 0) s_queue = blockIdx.x % kNumXcd;
+  __syncthreads();
+  int tries = 0;
+  for (;;) {
+    // ---- claim a work item (pair, rotation chunk) from an XCD queue ------
+    if (tid == 0) {
+      int q = s_queue;
+      int pair = -1, chunk = 0;
+      while (tries < kNumXcd) {
+        const int64_t item = static_cast<int64_t>(atomicAdd(&counters[q], 1ull));
+        if (item < queues.queue_chunks[q]) {
+          // Binary search the pair whose chunk range holds `item`.
+          int lo = queues.queue_begin[q], hi = queues.queue_begin[q + 1] - 1;
+          const int64_t base = queues.chunk_prefix[queues.queue_begin[q]];
+          while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (queues.chunk_prefix[mid] - base <= item) lo = mid; else hi = mid - 1;
+          }
+          pair = queues.pair_order[lo];
+          chunk = static_cast<int>(item - (queues.chunk_prefix[lo] - base));
+          break;
+        }
+        q = (q + 1) % kNumXcd;  // own queue drained: help the next XCD's queue
+        ++tries;
+      }
+      s_queue = q;
+      s_item_pair = pair;
+      s_item_chunk = chunk;
+    }
+    __syncthreads();
+    const int pair_index = Uniform(s_item_pair);
+    if (pair_index < 0) break;
+    const PairDesc pd = pairs[pair_index];
+    const SubmapDesc& sm = submaps[pd.submap];
+    const int rot0 = Uniform(s_item_chunk) * rc;
+    const int nrot = min(rc, pd.num_scans - rot0);
+    const int n = pd.num_points;
+    const int npad = (n + 63) & ~63;
+
+    // ---- K2: discretize the chunk's rotated scans into LDS --------------
+    bool range_error = false;
+    for (int r = 0; r < nrot; ++r) {
+      const float2 q = rot_table[pd.rot_offset + rot0 + r];
+      int mnx = 0x7fffffff, mxx = -0x7fffffff, mny = 0x7fffffff, mxy = -0x7fffffff;
+      for (int i = tid; i < npad; i += kSearchThreads) {
+        uint32_t packed = (static_cast<uint32_t>(static_cast<uint16_t>(kSentinel))) |
+                          (static_cast<uint32_t>(static_cast<uint16_t>(kSentinel)) << 16);
+        if (i < n) {
+          const float* p = points + 3 * (pd.point_offset + i);
+          float x, y;
+          RotateZDev(pd.pre_w, pd.pre_s, p[0], p[1], &x, &y);
+          RotateZDev(q.x, q.y, x, y, &x, &y);
+          // Eigen::Affine2f(translation) * p == t + (1*x + 0*y) in float.
+          const float px = __fadd_rn(pd.tx, x);
+          const float py = __fadd_rn(pd.ty, y);
+          const double cx = CellCoord(sm.max_y, py, sm.resolution);
+          const double cy = CellCoord(sm.max_x, px, sm.resolution);
+          int ix = 0, iy = 0;
+          if (fabs(cx) > kIndexLimit || fabs(cy) > kIndexLimit) {
+            range_error = true;
+          } else {
+            ix = static_cast<int>(cx);
+            iy = static_cast<int>(cy);
+          }
+          mnx = min(mnx, ix); mxx = max(mxx, ix);
+          mny = min(mny, iy); mxy = max(mxy, iy);
+          packed = (static_cast<uint32_t>(ix) & 0xffff) | (static_cast<uint32_t>(iy) << 16);
+        }
+        lds_pts[r * npad + i] = packed;
+      }
+      mnx = WaveMin(mnx); mxx = WaveMax(mxx);
+      mny = WaveMin(mny); mxy = WaveMax(mxy);
+      if (lane == 0) {
+        if (wave == 0) { s_mm[r][0] = mnx; s_mm[r][1] = mxx; s_mm[r][2] = mny; s_mm[r][3] = mxy; }
+      }
+      __syncthreads();
+      if (lane == 0 && wave != 0) {
+        atomicMin(&s_mm[r][0], mnx); atomicMax(&s_mm[r][1], mxx);
+        atomicMin(&s_mm[r][2], mny); atomicMax(&s_mm[r][3], mxy);
+      }
+    }
+    if (range_error) atomicOr(&status[pair_index], kStatusRange);
+    __syncthreads();
+
+    // ---- ShrinkToFit + top-level lattice sizes -------------------------
+    const int top_level = sm.levels - 1;
+    const int step = 1 << top_level;
+    if (tid == 0) {
+      int total = 0;
+      for (int r = 0; r < nrot; ++r) {
+        RotInfo ri;
+        const int lo_x = min(0, -s_mm[r][1]), hi_x = max(0, sm.nx - 1 - s_mm[r][0]);
+        const int lo_y = min(0, -s_mm[r][3]), hi_y = max(0, sm.ny - 1 - s_mm[r][2]);
+        ri.min_x = max(-pd.num_linear, lo_x);
+        ri.max_x = min(pd.num_linear, hi_x);
+        ri.min_y = max(-pd.num_linear, lo_y);
+        ri.max_y = min(pd.num_linear, hi_y);
+        if (n == 0) { ri.min_x = ri.max_x = ri.min_y = ri.max_y = 0; }
+        ri.top_nx = (ri.max_x - ri.min_x + step) / step;
+        ri.top_ny = (ri.max_y - ri.min_y + step) / step;
+        ri.top_begin = total;
+        total += ri.top_nx * ri.top_ny;
+        rinfo[r] = ri;
+      }
+      s_total_top = total;
+      s_next_chunk = 0;
+    }
+    __syncthreads();
+
+    // ---- K3 + K4: top-level chunks, then depth-first branch and bound ---
+    const int total_top = s_total_top;
+    const int s_min = pd.max_rejected_sum;
+    uint64_t* pair_best = best + pair_index;
+    uint64_t cached = LoadBest(pair_best);
+    for (;;) {
+      int chunk = 0;
+      if (lane == 0) chunk = atomicAdd(&s_next_chunk, 1);
+      chunk = Uniform(chunk);
+      const int begin = chunk * kTopChunk;
+      if (begin >= total_top) break;
+      const int count = min(kTopChunk, total_top - begin);
+      const LevelView top = MakeView(sm, top_level);
+      // Score the chunk's candidates one after another (lanes = points).
+      for (int j = 0; j < count; ++j) {
+        const int t = begin + j;
+        int r = 0;
+        while (r + 1 < nrot && rinfo[r + 1].top_begin <= t) ++r;
+        const RotInfo& ri = rinfo[r];
+        const int k = t - ri.top_begin;
+        const int xo = ri.min_x + (k / ri.top_ny) * step;
+        const int yo = ri.min_y + (k % ri.top_ny) * step;
+        const int sum = ScoreOne(lds_pts + r * npad, npad, top, xo, yo);
+        if (lane == 0) {
+          top_xy[wave][j] = (static_cast<uint32_t>(xo) & 0xffff) | (static_cast<uint32_t>(yo) << 16);
+          top_meta[wave][j] = sum | (r << 22);
+        }
+      }
+      local_cands += count;
+      local_lookups += static_cast<unsigned long long>(count) * n;
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      const uint32_t best_sum = static_cast<uint32_t>(cached >> kSumShift);
+      // Keep candidates above min_score and not below the incumbent; sort
+      // them by bound, best on top of the stack.
+      int meta = lane < count ? top_meta[wave][lane] : 0;
+      int sum = meta & 0x3fffff;
+      const bool keep = lane < count && sum > s_min && static_cast<uint32_t>(sum) >= best_sum;
+      if (top_level == 0) {
+        // Depth-1 search: the top level is the leaf level.
+        uint64_t key = 0;
+        if (keep) {
+          const uint32_t xy = top_xy[wave][lane];
+          const int xo = static_cast<int16_t>(xy & 0xffff), yo = static_cast<int>(xy) >> 16;
+          key = PackLeafKey(sum, rot0 + (meta >> 22), xo, yo);
+        }
+        for (int m = 32; m >= 1; m >>= 1) {
+          const uint64_t o = __shfl_xor(key, m, 64);
+          key = o > key ? o : key;
+        }
+        if (key > cached) {
+          uint64_t old = 0;
+          if (lane == 0) old = atomicMax(reinterpret_cast<unsigned long long*>(pair_best), key);
+          old = __shfl(old, 0, 64);
+          cached = key > old ? key : old;
+        }
+        continue;
+      }
+      // Bitonic sort (descending) of (sum << 8 | lane) over the wave.
+      uint32_t skey = keep ? ((static_cast<uint32_t>(sum) << 8) | static_cast<uint32_t>(lane)) : 0u;
+      for (int k = 2; k <= 64; k <<= 1) {
+        for (int jj = k >> 1; jj >= 1; jj >>= 1) {
+          const uint32_t other = __shfl_xor(skey, jj, 64);
+          const bool up = ((lane & k) == 0);
+          const bool lower = ((lane & jj) == 0);
+          const uint32_t hi_v = skey > other ? skey : other;
+          const uint32_t lo_v = skey > other ? other : skey;
+          skey = (lower == up) ? hi_v : lo_v;
+        }
+      }
+      const int kept = __popcll(__ballot(keep));
+      int sp = 0;
+      if (lane < kept) {
+        const int j = skey & 0xff;
+        const uint32_t xy = top_xy[wave][j];
+        const int m2 = top_meta[wave][j];
+        // Largest sum at the highest stack slot.
+        stack[wave][kept - 1 - lane] =
+            make_uint2(xy, static_cast<uint32_t>(m2 & 0x3fffff) |
+                               (static_cast<uint32_t>(m2 >> 22) << 22) |
+                               (static_cast<uint32_t>(top_level) << 27));
+      }
+      sp = kept;
+      __builtin_amdgcn_wave_barrier();
+
+      // Depth-first branch and bound over this wave's stack.
+      int iter = 0;
+      while (sp > 0) {
+        --sp;
+        const uint2 e = stack[wave][sp];
+        const uint32_t e0 = Uniform(e.x), e1 = Uniform(e.y);
+        const int xo = static_cast<int16_t>(e0 & 0xffff);
+        const int yo = static_cast<int>(e0) >> 16;
+        const uint32_t bound = e1 & 0x3fffff;
+        const int r = (e1 >> 22) & 0x1f;
+        const int d = e1 >> 27;
+        if ((++iter & 7) == 0) {
+          uint64_t fresh = 0;
+          if (lane == 0) fresh = LoadBest(pair_best);
+          fresh = __shfl(fresh, 0, 64);
+          cached = fresh > cached ? fresh : cached;
+        }
+        if (bound < static_cast<uint32_t>(cached >> kSumShift)) continue;
+        const int h = 1 << (d - 1);
+        const RotInfo& ri = rinfo[r];
+        const bool hx = xo + h <= ri.max_x;
+        const bool hy = yo + h <= ri.max_y;
+        int sums[4];
+        const LevelView L = MakeView(sm, d - 1);
+        ScoreChildren(lds_pts + r * npad, npad, L, xo, yo, h, sums);
+        const int nchild = 1 + (hx ? 1 : 0) + (hy ? 1 : 0) + ((hx && hy) ? 1 : 0);
+        local_cands += nchild;
+        local_lookups += static_cast<unsigned long long>(nchild) * n;
+        const int cxo[4] = {xo, xo, xo + h, xo + h};
+        const int cyo[4] = {yo, yo + h, yo, yo + h};
+        const bool exists[4] = {true, hy, hx, hx && hy};
+        const uint32_t cur = static_cast<uint32_t>(cached >> kSumShift);
+        if (d - 1 == 0) {
+          uint64_t key = 0;
+          bool range_bad = false;
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            if (!exists[c] || sums[c] <= s_min || static_cast<uint32_t>(sums[c]) < cur) continue;
+            if (cxo[c] < -kOffsetLimit || cxo[c] > kOffsetLimit || cyo[c] < -kOffsetLimit ||
+                cyo[c] > kOffsetLimit) { range_bad = true; continue; }
+            const uint64_t k2 = PackLeafKey(sums[c], rot0 + r, cxo[c], cyo[c]);
+            key = k2 > key ? k2 : key;
+          }
+          if (range_bad && lane == 0) atomicOr(&status[pair_index], kStatusRange);
+          if (key > cached) {
+            uint64_t old = 0;
+            if (lane == 0) old = atomicMax(reinterpret_cast<unsigned long long*>(pair_best), key);
+            old = __shfl(old, 0, 64);
+            cached = key > old ? key : old;
+          }
+        } else {
+          // Push surviving children, ascending by bound (best popped first).
+          int order[4];
+          int m = 0;
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+            if (exists[c] && sums[c] > s_min && static_cast<uint32_t>(sums[c]) >= cur) order[m++] = c;
+          for (int a = 1; a < m; ++a) {  // insertion sort, ascending
+            const int v = order[a];
+            int b = a - 1;
+            while (b >= 0 && sums[order[b]] > sums[v]) { order[b + 1] = order[b]; --b; }
+            order[b + 1] = v;
+          }
+          if (lane < m) {
+            const int c = order[lane];
+            stack[wave][sp + lane] = MakeEntry(cxo[c], cyo[c], sums[c], r, d - 1);
+          }
+          sp += m;
+          __builtin_amdgcn_wave_barrier();
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (stats && lane == 0) {
+    atomicAdd(&stats[0], local_cands);
+    atomicAdd(&stats[1], local_lookups);
+  }
+}
+
+// ---------------------------------------------------------------- K5 -------
+
+// One workgroup per rotated scan; one lane per (x, y) offset of the full
+// (2L+1)^2 window (no ShrinkToFit on this path). Float sums run point by
+// point in the reference order so every candidate score is bit-identical.
+__global__ void rt2d_score(const float* __restrict__ prob,  // grid as probabilities
+                           int nx, int ny, double max_x, double max_y, double res,
+                           const float* __restrict__ points, int n,
+                           const float2* __restrict__ rot_table, float pre_w, float pre_s,
+                           float tx, float ty, int num_linear, int num_angular,
+                           double step, double wt, double wr,
+                           unsigned long long* __restrict__ best) {
+  extern __shared__ __align__(16) int2 lds_xy[];
+  const int r = blockIdx.y;
+  const float2 q = rot_table[r];
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    float x, y;
+    RotateZDev(pre_w, pre_s, points[3 * i], points[3 * i + 1], &x, &y);
+    RotateZDev(q.x, q.y, x, y, &x, &y);
+    const float px = __fadd_rn(tx, x), py = __fadd_rn(ty, y);
+    double cx = CellCoord(max_y, py, res), cy = CellCoord(max_x, px, res);
+    cx = fmin(fmax(cx, -1e9), 1e9);
+    cy = fmin(fmax(cy, -1e9), 1e9);
+    lds_xy[i] = make_int2(static_cast<int>(cx), static_cast<int>(cy));
+  }
+  __syncthreads();
+  const int side = 2 * num_linear + 1;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned long long key = 0;
+  if (t < side * side) {
+    const int xo = -num_linear + t / side;
+    const int yo = -num_linear + t % side;
+    float s = 0.f;
+    for (int i = 0; i < n; ++i) {
+      const int2 c = lds_xy[i];
+      const int gx = c.x + xo, gy = c.y + yo;
+      const bool in = gx >= 0 && gy >= 0 && gx < nx && gy < ny;
+      s = __fadd_rn(s, in ? prob[static_cast<size_t>(gy) * nx + gx] : 0.1f);
+    }
+    s = __fdiv_rn(s, static_cast<float>(n));
+    const double cand_x = -yo * res, cand_y = -xo * res;
+    const double theta = (r - num_angular) * step;
+    const double pen = __dadd_rn(__dmul_rn(hypot(cand_x, cand_y), wt), __dmul_rn(fabs(theta), wr));
+    const float score = static_cast<float>(__dmul_rn(static_cast<double>(s), exp(-__dmul_rn(pen, pen))));
+    const unsigned int idx = static_cast<unsigned int>(r * side * side + t);
+    key = (static_cast<unsigned long long>(__float_as_uint(score)) << 32) |
+          static_cast<unsigned long long>(0xffffffffu - idx);
+  }
+  for (int m = 32; m >= 1; m >>= 1) {
+    const unsigned long long o = __shfl_xor(key, m, 64);
+    key = o > key ? o : key;
+  }
+  if ((threadIdx.x & 63) == 0 && key != 0) atomicMax(best, key);
+}
+
+// Grid cells -> probability (ProbabilityGrid::GetProbability table).
+__global__ void cells_to_probability(const uint16_t* __restrict__ cells,
+                                     const float* __restrict__ ptab,
+                                     float* __restrict__ out, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = ptab[cells[i] & 0x7fff];
+}
+
+}  // namespace csm
+
+// ---------------------------------------------------------------- launchers -
+namespace csm {
+
+hipError_t LaunchPyramidLevel0(const uint16_t* cells, const uint8_t* qtab, uint8_t* out, int n,
+                               hipStream_t st) {
+  hipLaunchKernelGGL(pyramid_level0, dim3((n + 1 + 255) / 256), dim3(256), 0, st, cells, qtab, out, n);
+  return hipGetLastError();
+}
+
+hipError_t LaunchPyramidDouble(const uint8_t* prev, int pnx, int pny, uint8_t* next, int nnx,
+                               int nny, int h, hipStream_t st) {
+  hipLaunchKernelGGL(pyramid_double, dim3((nnx + 255) / 256, nny), dim3(256), 0, st, prev, pnx, pny,
+                     next, nnx, nny, h);
+  return hipGetLastError();
+}
+
+hipError_t LaunchFast2dSearch(int grid, size_t dyn_lds, hipStream_t st, const SubmapDesc* submaps,
+                              const PairDesc* pairs, const float* points, const float2* rot_table,
+                              const WorkQueues& queues, unsigned long long* counters,
+                              uint64_t* best, int32_t* status, unsigned long long* stats) {
+  hipLaunchKernelGGL(fast2d_search, dim3(grid), dim3(kSearchThreads), dyn_lds, st, submaps, pairs,
+                     points, rot_table, queues, counters, best, status, stats);
+  return hipGetLastError();
+}
+
+hipError_t LaunchRt2dScore(dim3 grid, int block, size_t dyn_lds, hipStream_t st, const float* prob,
+                           int nx, int ny, double max_x, double max_y, double res,
+                           const float* points, int n, const float2* rot_table, float pre_w,
+                           float pre_s, float tx, float ty, int num_linear, int num_angular,
+                           double step, double wt, double wr, unsigned long long* best) {
+  hipLaunchKernelGGL(rt2d_score, grid, dim3(block), dyn_lds, st, prob, nx, ny, max_x, max_y, res,
+                     points, n, rot_table, pre_w, pre_s, tx, ty, num_linear, num_angular, step, wt,
+                     wr, best);
+  return hipGetLastError();
+}
+
+hipError_t LaunchCellsToProbability(const uint16_t* cells, const float* ptab, float* out, int n,
+                                    hipStream_t st) {
+  hipLaunchKernelGGL(cells_to_probability, dim3((n + 255) / 256), dim3(256), 0, st, cells, ptab, out, n);
+  return hipGetLastError();
+}
+
+}  // namespace csm

@@ -1,0 +1,29 @@
+// Host-callable launchers of the kernels in csm_kernels.hip.
+#ifndef CSM_LAUNCH_H_
+#define CSM_LAUNCH_H_
+
+#include <hip/hip_runtime.h>
+
+#include "csm_device.h"
+
+namespace csm {
+
+hipError_t LaunchPyramidLevel0(const uint16_t* cells, const uint8_t* qtab, uint8_t* out, int n,
+                               hipStream_t st);
+hipError_t LaunchPyramidDouble(const uint8_t* prev, int pnx, int pny, uint8_t* next, int nnx,
+                               int nny, int h, hipStream_t st);
+hipError_t LaunchFast2dSearch(int grid, size_t dyn_lds, hipStream_t st, const SubmapDesc* submaps,
+                              const PairDesc* pairs, const float* points, const float2* rot_table,
+                              const WorkQueues& queues, unsigned long long* counters,
+                              uint64_t* best, int32_t* status, unsigned long long* stats);
+hipError_t LaunchRt2dScore(dim3 grid, int block, size_t dyn_lds, hipStream_t st, const float* prob,
+                           int nx, int ny, double max_x, double max_y, double res,
+                           const float* points, int n, const float2* rot_table, float pre_w,
+                           float pre_s, float tx, float ty, int num_linear, int num_angular,
+                           double step, double wt, double wr, unsigned long long* best);
+hipError_t LaunchCellsToProbability(const uint16_t* cells, const float* ptab, float* out, int n,
+                                    hipStream_t st);
+
+}  // namespace csm
+
+#endif  // CSM_LAUNCH_H_

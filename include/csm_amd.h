@@ -1,0 +1,179 @@
+/*
+ * csm_amd.h — C-ABI of the MI355X-native correlative scan matcher.
+ *
+ * Drop-in boundary for Cartographer's scan-matching hot path
+ * (reference: juwangvsu/cartographer-1). Every entry point below replaces a
+ * reference interface, cited as file:line relative to the reference root.
+ * Plain pointers and sizes only; no C++ or torch types cross this boundary.
+ *
+ * Return codes: CSM_OK (0) = matched / success, CSM_NO_MATCH (1) = the search
+ * completed without a score above min_score (the reference's `false` /
+ * nullptr), negative = error. The reference aborts via glog CHECK on invariant
+ * violations; the C++ shim (include/cartographer_amd/scan_matching.h) turns
+ * negative codes into aborts to keep those semantics.
+ *
+ * Threading: handles are re-entrant for concurrent match calls (the reference
+ * calls const Match methods concurrently from ThreadPool workers,
+ * constraint_builder_2d.cc:100-111); each call serialises on its context's
+ * stream. Use one context per calling thread for concurrency.
+ */
+#ifndef CSM_AMD_H_
+#define CSM_AMD_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CSM_OK 0
+#define CSM_NO_MATCH 1
+#define CSM_EINVAL (-1)
+#define CSM_EHIP (-2)
+#define CSM_ENOMEM (-3)
+#define CSM_ERANGE (-4) /* input exceeds the device path's index limits */
+
+/* mapping/2d/map_limits.h:40-96 (resolution, max corner, CellLimits
+ * xy_index.h:34-45). Cell (x, y) lives at flat index x + y * num_x_cells
+ * (grid_2d.h:113-116); x counts down from max_y, y down from max_x
+ * (map_limits.h:69-75). */
+typedef struct csm_map_limits {
+  double resolution;
+  double max_x, max_y;
+  int32_t num_x_cells, num_y_cells;
+} csm_map_limits;
+
+/* transform::Rigid2d (transform/rigid_transform.h:33-86): translation and an
+ * unnormalized rotation angle. */
+typedef struct csm_pose2d {
+  double x, y, theta;
+} csm_pose2d;
+
+/* proto::FastCorrelativeScanMatcherOptions2D
+ * (proto/scan_matching/fast_correlative_scan_matcher_options_2d.proto:19-30). */
+typedef struct csm_fast2d_options {
+  double linear_search_window;
+  double angular_search_window;
+  int32_t branch_and_bound_depth;
+  /* Device-side search pyramid depth (>= branch_and_bound_depth, <= 12). The
+   * branch and bound is exact, so extra coarse levels change only the work
+   * done, never the result (DESIGN.md "Search"). 0 = automatic. */
+  int32_t search_depth;
+} csm_fast2d_options;
+
+/* proto::RealTimeCorrelativeScanMatcherOptions
+ * (proto/scan_matching/real_time_correlative_scan_matcher_options.proto:19-31). */
+typedef struct csm_rt_options {
+  double linear_search_window;
+  double angular_search_window;
+  double translation_delta_cost_weight;
+  double rotation_delta_cost_weight;
+} csm_rt_options;
+
+typedef struct csm_context csm_context;   /* device, stream, scratch */
+typedef struct csm_fast2d csm_fast2d;     /* one submap's device pyramid */
+typedef struct csm_scan_set csm_scan_set; /* device-resident node clouds */
+
+/* ---- context -------------------------------------------------------------- */
+int csm_context_create(int32_t device, csm_context** out);
+void csm_context_destroy(csm_context* ctx);
+/* hipStream_t the context launches on (as void*), for event timing. */
+void* csm_context_stream(csm_context* ctx);
+
+/* Kernel timing, accumulated with HIP events on the context stream while
+ * enabled: the candidate-scoring (search) kernel's total device milliseconds,
+ * launches and algorithmic bytes (candidates scored x points x 1 B). */
+typedef struct csm_timing {
+  double search_kernel_ms;
+  int64_t search_launches;
+  double search_lookups;   /* candidates scored x points */
+  double search_candidates;
+  double other_kernel_ms;
+} csm_timing;
+void csm_context_enable_timing(csm_context* ctx, int32_t enable);
+void csm_context_get_timing(csm_context* ctx, csm_timing* out);
+void csm_context_reset_timing(csm_context* ctx);
+
+/* ---- FastCorrelativeScanMatcher2D ------------------------------------------
+ * csm_fast2d_create replaces the constructor
+ *   FastCorrelativeScanMatcher2D(const Grid2D&, const Options2D&)
+ *   (fast_correlative_scan_matcher_2d.h:114-116, .cc:188-194)
+ * and builds the PrecomputationGridStack2D (.cc:171-186) on the device.
+ * `cells` are the grid's uint16 correspondence-cost values
+ * (Grid2D::correspondence_cost_cells, grid_2d.h:97-99); min/max cc are
+ * Grid2D::GetMin/MaxCorrespondenceCost (grid_2d.h:61-67). The cells are copied:
+ * the caller may free them on return. */
+int csm_fast2d_create(csm_context* ctx, const csm_map_limits* limits,
+                      const uint16_t* cells, float min_correspondence_cost,
+                      float max_correspondence_cost,
+                      const csm_fast2d_options* options, csm_fast2d** out);
+void csm_fast2d_destroy(csm_fast2d* m);
+
+/* bool Match(const Rigid2d& initial_pose_estimate, const PointCloud&,
+ *            float min_score, float* score, Rigid2d* pose_estimate) const
+ *   (fast_correlative_scan_matcher_2d.h:127-129, .cc:198-208).
+ * points: n x (x, y, z) floats (sensor::RangefinderPoint, point_cloud.h). */
+int csm_fast2d_match(const csm_fast2d* m, const csm_pose2d* initial,
+                     const float* points_xyz, int32_t n, float min_score,
+                     float* score, csm_pose2d* pose);
+
+/* bool MatchFullSubmap(const PointCloud&, float min_score, float* score,
+ *                      Rigid2d* pose_estimate) const
+ *   (fast_correlative_scan_matcher_2d.h:135-136, .cc:210-225). */
+int csm_fast2d_match_full_submap(const csm_fast2d* m, const float* points_xyz,
+                                 int32_t n, float min_score, float* score,
+                                 csm_pose2d* pose);
+
+/* Test-visible: copies PrecomputationGrid2D level `level` (uint8 wide grid,
+ * fast_correlative_scan_matcher_2d.h:49-93) to host. */
+int csm_fast2d_read_level(const csm_fast2d* m, int32_t level, uint8_t* out,
+                          int64_t capacity, int32_t* wide_nx, int32_t* wide_ny);
+
+/* ---- Batched constraint search (the throughput path) ----------------------
+ * Replaces the per-pair Tasks ConstraintBuilder2D schedules
+ * (constraint_builder_2d.cc:77-137, ComputeConstraint :188-277): a set of
+ * node clouds lives on the device once; each pair names a submap handle and a
+ * node; results come back in pair order. */
+int csm_scan_set_create(csm_context* ctx, const float* points_xyz,
+                        const int64_t* offsets, int32_t num_scans,
+                        csm_scan_set** out);
+void csm_scan_set_destroy(csm_scan_set* s);
+
+typedef struct csm_pair2d {
+  int32_t submap;      /* index into the submaps[] array */
+  int32_t scan;        /* index into the scan set */
+  int32_t full_submap; /* 1 = MatchFullSubmap, 0 = Match(initial) */
+  float min_score;
+  csm_pose2d initial;  /* used when full_submap == 0 */
+} csm_pair2d;
+
+typedef struct csm_result2d {
+  int32_t status;      /* CSM_OK, CSM_NO_MATCH or a negative error */
+  float score;
+  csm_pose2d pose;
+} csm_result2d;
+
+int csm_fast2d_match_batch(csm_context* ctx, csm_fast2d* const* submaps,
+                           int32_t num_submaps, const csm_scan_set* scans,
+                           const csm_pair2d* pairs, int64_t num_pairs,
+                           csm_result2d* results);
+
+/* ---- RealTimeCorrelativeScanMatcher2D --------------------------------------
+ * double Match(const Rigid2d& initial_pose_estimate, const PointCloud&,
+ *              const Grid2D&, Rigid2d* pose_estimate) const
+ *   (real_time_correlative_scan_matcher_2d.h:66-68, .cc:117-149), for a
+ * ProbabilityGrid. Returns CSM_OK and writes the best candidate's score. */
+int csm_rt2d_match(csm_context* ctx, const csm_rt_options* options,
+                   const csm_map_limits* limits, const uint16_t* cells,
+                   float min_correspondence_cost, float max_correspondence_cost,
+                   const csm_pose2d* initial, const float* points_xyz,
+                   int32_t n, double* score, csm_pose2d* pose);
+
+/* Human-readable text for a return code. */
+const char* csm_strerror(int code);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CSM_AMD_H_ */
