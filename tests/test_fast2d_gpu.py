@@ -47,11 +47,13 @@ def assert_fast_parity(oracle, om, limits, cells, gpu, ref, full, init, cloud):
         return "exact"
     # Exact tie: recover the GPU leaf (scan index, offsets) and score it.
     res = limits[0]
-    ns, step = _window_of(oracle, limits, cells, init, om.lin, om.ang, cloud)
+    lin, ang = (1e6 * res, math.pi) if full else (om.lin, om.ang)
+    ns, step = _window_of(oracle, limits, cells, init, lin, ang, cloud)
     n_ang = (ns - 1) // 2
     k = int(round((g_pose[2] - init[2]) / step)) + n_ang
     x_off = int(round(-(g_pose[1] - init[1]) / res))
     y_off = int(round(-(g_pose[0] - init[0]) / res))
+    assert 0 <= k < ns, (k, ns, g_pose, o_pose)
     _, s = om.score_candidate(full, None if full else init, cloud, k, x_off, y_off, 0)
     assert np.float32(s) == np.float32(o_score), ("GPU leaf is not a tied maximum", g_pose, o_pose)
     return "tie"
