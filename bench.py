@@ -139,6 +139,7 @@ def main():
     elapsed = time.perf_counter() - t_start
     ctx.enable_timing(False)
     tm = ctx.timing()
+    lv_cands, lv_batches = ctx.level_stats()
     if dist is not None:
         import torch
         t = torch.tensor([elapsed], dtype=torch.float64, device=torch.device("cuda", local_rank))
@@ -177,6 +178,8 @@ def main():
                      "kernel": "fast2d_search", "kernel_ms_avg": kernel_ms_avg,
                      "algorithmic_bytes_per_launch": bytes_per_launch},
         "accepted_constraints_per_step": accepted,
+        "search_levels": {"candidates_per_pair": [c / max(n_pairs * args.steps, 1) for c in lv_cands],
+                          "mean_lanes_per_batch": [c / b if b else 0 for c, b in zip(lv_cands, lv_batches)]},
         "setup_s": {"world": gen_s, "pyramids_and_upload": build_s},
     }
 

@@ -88,6 +88,8 @@ _SIGNATURES = {
     "csm_context_enable_timing": (None, [C.c_void_p, C.c_int32]),
     "csm_context_get_timing": (None, [C.c_void_p, C.POINTER(Timing)]),
     "csm_context_reset_timing": (None, [C.c_void_p]),
+    "csm_context_level_stats": (C.c_int32, [C.c_void_p, C.POINTER(C.c_double),
+                                            C.POINTER(C.c_double), C.c_int32]),
     "csm_fast2d_create": (C.c_int, [C.c_void_p, C.POINTER(MapLimits), C.POINTER(C.c_uint16),
                                     C.c_float, C.c_float, C.POINTER(Fast2DOptions),
                                     C.POINTER(C.c_void_p)]),
@@ -218,6 +220,13 @@ class Context:
 
     def reset_timing(self):
         self._lib.csm_context_reset_timing(self.handle)
+
+    def level_stats(self):
+        """(candidates, batches) scored per pyramid level while timing was on."""
+        c = (C.c_double * 12)()
+        b = (C.c_double * 12)()
+        n = self._lib.csm_context_level_stats(self.handle, c, b, 12)
+        return list(c)[:n], list(b)[:n]
 
     def timing(self) -> Timing:
         t = Timing()

@@ -36,6 +36,15 @@ struct SubmapDesc {
   int32_t wide_nx[kMaxLevels];
   int32_t wide_ny[kMaxLevels];
   int32_t zero_index[kMaxLevels];  // index of the trailing zero byte
+  // Polyphase copy of level d (period h = 2^d): plane (px, py) holds the
+  // wide cells (kx*h + px, ky*h + py), kx < plane_w, ky < plane_h, stored at
+  // ((py*h + px) * plane_w*plane_h) + kx + ky*plane_w; cells past the wide
+  // grid are 0. Level-d candidates all lie on one 2^d lattice, so the lookups
+  // of one point by neighbouring candidates are neighbouring bytes.
+  const uint8_t* poly[kMaxLevels];
+  int32_t plane_w[kMaxLevels];
+  int32_t plane_h[kMaxLevels];
+  int32_t poly_bytes[kMaxLevels];  // h*h*plane_w*plane_h
 };
 
 // One (node, submap) search.
@@ -59,6 +68,21 @@ struct WorkQueues {
   int64_t queue_chunks[kNumXcd];  // chunks per queue
   int32_t rot_chunk;              // rotations per chunk
 };
+
+// v2 work queues: chunks of `rot_chunk` rotations of a pair; a chunk id
+// decodes to its pair in O(1) through a per-64-chunk block table.
+struct WorkQueues2 {
+  const int32_t* pair_order;    // pairs, grouped by queue
+  const int64_t* chunk_prefix;  // size |pair_order|+1, cumulative chunks
+  const int32_t* block_first;   // per queue block of 64 chunks: pair_order index
+  int32_t block_offset[kNumXcd];
+  int32_t queue_begin[kNumXcd + 1];
+  int64_t queue_chunks[kNumXcd];
+  int32_t rot_chunk;
+};
+
+constexpr int kStack2 = 1024;   // v2 per-workgroup DFS stack entries
+constexpr int kBatchNodes = 16; // nodes expanded per batch (64 children)
 
 // Best leaf per pair, packed for a 64-bit atomicMax:
 //   [63:42] level-0 integer sum (22 bits)

@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -29,6 +30,8 @@ namespace csm {
 
 
 namespace {
+
+constexpr int kStatsWords = 2 + 2 * kMaxLevels;
 
 #define CSM_HIP(call)                               \
   do {                                              \
@@ -75,13 +78,15 @@ struct csm_context {
   hipStream_t stream = nullptr;
   std::mutex mu;
   DevBuf submap_desc, pair_desc, rot_table, best, status, counters, pair_order,
-      chunk_prefix, stats, rt_prob, rt_cells, rt_points, rt_best, rt_rot, rt_ptab,
+      chunk_prefix, blocks, stats, rt_prob, rt_cells, rt_points, rt_best, rt_rot, rt_ptab,
       single_points;
   bool timing = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   csm_timing t{};
   std::vector<float> ptab_host;
   bool ptab_uploaded = false;
+  double level_cands[kMaxLevels] = {0};
+  double level_batches[kMaxLevels] = {0};
   int num_cus = 256;
 };
 
@@ -200,9 +205,15 @@ int RunBatch(csm_context* ctx, csm_fast2d* const* submaps, int32_t num_submaps,
   const int np = static_cast<int>(pdesc.size());
   if (np == 0) return CSM_OK;
 
-  // Rotation chunk size from the LDS budget for discretized points.
+  // v2 (lanes = candidates over the polyphase pyramid) keeps three N-long
+  // arrays in LDS; above ~10k points the v1 kernel (lanes = points) is used.
+  const char* forced_env = std::getenv("CSM_SEARCH_KERNEL");
+  const int forced = forced_env ? std::atoi(forced_env) : 0;
+  const bool use_v2 = forced == 2 || (forced != 1 && max_npad * 12 + 8192 <= 120 * 1024);
+  // Rotation chunk size: v1 from the LDS budget for discretized points;
+  // v2 processes rotations one at a time, claimed in small chunks.
   const int lds_budget = 40 * 1024;
-  const int rc = std::max(1, std::min(16, lds_budget / (max_npad * 4)));
+  const int rc = use_v2 ? 2 : std::max(1, std::min(16, lds_budget / (max_npad * 4)));
 
   // Per-XCD queues: submap s -> queue s % 8 so a submap's pyramid stays in
   // one XCD's L2; pairs within a queue in submap order.
@@ -239,7 +250,7 @@ int RunBatch(csm_context* ctx, csm_fast2d* const* submaps, int32_t num_submaps,
   if ((rcode = ctx->counters.Reserve(sizeof(unsigned long long) * kNumXcd))) return rcode;
   if ((rcode = ctx->pair_order.Reserve(sizeof(int32_t) * order.size()))) return rcode;
   if ((rcode = ctx->chunk_prefix.Reserve(sizeof(int64_t) * prefix.size()))) return rcode;
-  if ((rcode = ctx->stats.Reserve(sizeof(unsigned long long) * 2))) return rcode;
+  if ((rcode = ctx->stats.Reserve(sizeof(unsigned long long) * kStatsWords))) return rcode;
   hipStream_t st = ctx->stream;
   CSM_HIP(hipMemcpyAsync(ctx->submap_desc.ptr, sdesc.data(), sizeof(SubmapDesc) * num_submaps,
                          hipMemcpyHostToDevice, st));
@@ -254,26 +265,65 @@ int RunBatch(csm_context* ctx, csm_fast2d* const* submaps, int32_t num_submaps,
   CSM_HIP(hipMemsetAsync(ctx->best.ptr, 0, sizeof(uint64_t) * np, st));
   CSM_HIP(hipMemsetAsync(ctx->status.ptr, 0, sizeof(int32_t) * np, st));
   CSM_HIP(hipMemsetAsync(ctx->counters.ptr, 0, sizeof(unsigned long long) * kNumXcd, st));
-  CSM_HIP(hipMemsetAsync(ctx->stats.ptr, 0, sizeof(unsigned long long) * 2, st));
+  CSM_HIP(hipMemsetAsync(ctx->stats.ptr, 0, sizeof(unsigned long long) * kStatsWords, st));
   wq.pair_order = ctx->pair_order.as<int32_t>();
   wq.chunk_prefix = ctx->chunk_prefix.as<int64_t>();
 
-  // ---- launch: persistent workgroups, 4 per CU ------------------------------
-  const size_t dyn_lds = static_cast<size_t>(rc) * max_npad * sizeof(uint32_t);
+  // ---- launch: persistent workgroups ----------------------------------------
   const int64_t total_chunks = running;
-  const int grid = static_cast<int>(std::min<int64_t>(static_cast<int64_t>(ctx->num_cus) * 4,
-                                                      std::max<int64_t>(total_chunks, 1)));
   if (ctx->timing) CSM_HIP(hipEventRecord(ctx->ev0, st));
-  CSM_HIP(LaunchFast2dSearch(grid, dyn_lds, st, ctx->submap_desc.as<SubmapDesc>(),
-                             ctx->pair_desc.as<PairDesc>(), scans->points.as<float>(),
-                             ctx->rot_table.as<float2>(), wq,
-                             ctx->counters.as<unsigned long long>(), ctx->best.as<uint64_t>(),
-                             ctx->status.as<int32_t>(), ctx->stats.as<unsigned long long>()));
+  if (use_v2) {
+    // Block table: for every 64 chunks of a queue, the first pair_order entry.
+    std::vector<int32_t> blocks;
+    WorkQueues2 wq2{};
+    wq2.rot_chunk = rc;
+    for (int x = 0; x < kNumXcd; ++x) {
+      wq2.queue_begin[x] = wq.queue_begin[x];
+      wq2.queue_chunks[x] = wq.queue_chunks[x];
+      wq2.block_offset[x] = static_cast<int32_t>(blocks.size());
+      const int64_t qstart = prefix[wq.queue_begin[x]];
+      int e = wq.queue_begin[x];
+      for (int64_t c = 0; c < wq.queue_chunks[x]; c += 64) {
+        while (prefix[e + 1] - qstart <= c) ++e;
+        blocks.push_back(e);
+      }
+    }
+    wq2.queue_begin[kNumXcd] = wq.queue_begin[kNumXcd];
+    if ((rcode = ctx->blocks.Reserve(sizeof(int32_t) * std::max<size_t>(blocks.size(), 1))))
+      return rcode;
+    if (!blocks.empty())
+      CSM_HIP(hipMemcpyAsync(ctx->blocks.ptr, blocks.data(), sizeof(int32_t) * blocks.size(),
+                             hipMemcpyHostToDevice, st));
+    wq2.pair_order = wq.pair_order;
+    wq2.chunk_prefix = wq.chunk_prefix;
+    wq2.block_first = ctx->blocks.as<int32_t>();
+    const int maxp = max_npad;
+    // pts (4 B/pt) + per-level precompute (8 B/pt, +1024 slack entries).
+    const size_t dyn_lds = static_cast<size_t>(maxp) * 4 + (static_cast<size_t>(maxp) + 1024) * 8;
+    const int per_cu = std::max(1, std::min(8, static_cast<int>((160 * 1024) / (dyn_lds + 12 * 1024))));
+    const int grid = static_cast<int>(std::min<int64_t>(static_cast<int64_t>(ctx->num_cus) * per_cu,
+                                                        std::max<int64_t>(total_chunks, 1)));
+    CSM_HIP(LaunchFast2dSearchV2(grid, dyn_lds, st, ctx->submap_desc.as<SubmapDesc>(),
+                                 ctx->pair_desc.as<PairDesc>(), scans->points.as<float>(),
+                                 ctx->rot_table.as<float2>(), wq2,
+                                 ctx->counters.as<unsigned long long>(), ctx->best.as<uint64_t>(),
+                                 ctx->status.as<int32_t>(), ctx->stats.as<unsigned long long>(),
+                                 maxp));
+  } else {
+    const size_t dyn_lds = static_cast<size_t>(rc) * max_npad * sizeof(uint32_t);
+    const int grid = static_cast<int>(std::min<int64_t>(static_cast<int64_t>(ctx->num_cus) * 4,
+                                                        std::max<int64_t>(total_chunks, 1)));
+    CSM_HIP(LaunchFast2dSearch(grid, dyn_lds, st, ctx->submap_desc.as<SubmapDesc>(),
+                               ctx->pair_desc.as<PairDesc>(), scans->points.as<float>(),
+                               ctx->rot_table.as<float2>(), wq,
+                               ctx->counters.as<unsigned long long>(), ctx->best.as<uint64_t>(),
+                               ctx->status.as<int32_t>(), ctx->stats.as<unsigned long long>()));
+  }
   if (ctx->timing) CSM_HIP(hipEventRecord(ctx->ev1, st));
 
   std::vector<uint64_t> keys(np);
   std::vector<int32_t> stat(np);
-  unsigned long long stats_host[2] = {0, 0};
+  unsigned long long stats_host[kStatsWords] = {0};
   CSM_HIP(hipMemcpyAsync(keys.data(), ctx->best.ptr, sizeof(uint64_t) * np,
                          hipMemcpyDeviceToHost, st));
   CSM_HIP(hipMemcpyAsync(stat.data(), ctx->status.ptr, sizeof(int32_t) * np,
@@ -288,6 +338,10 @@ int RunBatch(csm_context* ctx, csm_fast2d* const* submaps, int32_t num_submaps,
     ctx->t.search_launches += 1;
     ctx->t.search_candidates += static_cast<double>(stats_host[0]);
     ctx->t.search_lookups += static_cast<double>(stats_host[1]);
+    for (int l = 0; l < kMaxLevels; ++l) {
+      ctx->level_cands[l] += static_cast<double>(stats_host[2 + l]);
+      ctx->level_batches[l] += static_cast<double>(stats_host[2 + kMaxLevels + l]);
+    }
   }
 
   // ---- decode -----------------------------------------------------------------
@@ -385,7 +439,20 @@ void csm_context_get_timing(csm_context* ctx, csm_timing* out) {
   if (ctx && out) *out = ctx->t;
 }
 void csm_context_reset_timing(csm_context* ctx) {
-  if (ctx) ctx->t = csm_timing{};
+  if (!ctx) return;
+  ctx->t = csm_timing{};
+  for (int l = 0; l < kMaxLevels; ++l) ctx->level_cands[l] = ctx->level_batches[l] = 0.;
+}
+
+int32_t csm_context_level_stats(csm_context* ctx, double* candidates, double* batches,
+                                int32_t max_levels) {
+  if (!ctx) return 0;
+  const int n = std::min<int>(max_levels, kMaxLevels);
+  for (int l = 0; l < n; ++l) {
+    if (candidates) candidates[l] = ctx->level_cands[l];
+    if (batches) batches[l] = ctx->level_batches[l];
+  }
+  return n;
 }
 
 int csm_fast2d_create(csm_context* ctx, const csm_map_limits* limits,
@@ -434,9 +501,27 @@ int csm_fast2d_create(csm_context* ctx, const csm_map_limits* limits,
     offs[l] = total;
     total += (static_cast<size_t>(d.zero_index[l]) + 1 + 255) & ~size_t(255);
   }
+  std::vector<size_t> poffs(depth), poly_entries(depth);
+  for (int l = 0; l < depth; ++l) {
+    // Polyphase planes: row stride a multiple of 4 (the search kernel reads
+    // 8-byte aligned pairs around a byte), 4-byte front pad, 16-byte zero tail.
+    const int h = 1 << l;
+    d.plane_w[l] = (((d.wide_nx[l] + h - 1) / h) + 3) & ~3;
+    d.plane_h[l] = (d.wide_ny[l] + h - 1) / h;
+    const size_t entries = static_cast<size_t>(h) * h * d.plane_w[l] * d.plane_h[l];
+    const size_t pb = 4 + entries + 16;
+    if (pb > 0x7fffff00u) return CSM_ERANGE;
+    d.poly_bytes[l] = static_cast<int32_t>(pb);
+    poly_entries[l] = entries;
+    poffs[l] = total;
+    total += (pb + 255) & ~size_t(255);
+  }
   int rc;
   if ((rc = m->pyramid.Reserve(total))) return rc;
-  for (int l = 0; l < depth; ++l) d.level[l] = m->pyramid.as<uint8_t>() + offs[l];
+  for (int l = 0; l < depth; ++l) {
+    d.level[l] = m->pyramid.as<uint8_t>() + offs[l];
+    d.poly[l] = m->pyramid.as<uint8_t>() + poffs[l];
+  }
 
   DevBuf dcells, dq;
   if ((rc = dcells.Reserve(sizeof(uint16_t) * nx * ny))) return rc;
@@ -452,6 +537,10 @@ int csm_fast2d_create(csm_context* ctx, const csm_map_limits* limits,
                                 const_cast<uint8_t*>(d.level[l]), d.wide_nx[l], d.wide_ny[l],
                                 1 << (l - 1), st));
   }
+  for (int l = 0; l < depth; ++l)
+    CSM_HIP(LaunchPyramidPolyphase(d.level[l], d.wide_nx[l], d.wide_ny[l], l, d.plane_w[l],
+                                   d.plane_h[l], const_cast<uint8_t*>(d.poly[l]),
+                                   static_cast<int>(poly_entries[l]), st));
   CSM_HIP(hipStreamSynchronize(st));  // dcells/dq are freed on return
   *out = m.release();
   return CSM_OK;

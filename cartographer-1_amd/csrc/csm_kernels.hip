@@ -18,6 +18,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "csm_device.h"
 
 namespace csm {
@@ -126,7 +128,35 @@ __device__ __forceinline__ void ScoreChildren(const uint32_t* __restrict__ pts,
   const int lane = threadIdx.x & 63;
   int a0 = 0, a1 = 0, a2 = 0, a3 = 0;
   const int hw = h * L.wnx;
-  for (int i = lane; i < npad; i += 64) {
+  // npad is a multiple of 64; take 4 points per lane per iteration so 16
+  // byte loads are in flight before any is consumed.
+  int i = lane;
+  for (; i + 192 < npad; i += 256) {
+    int ad[16];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t p = pts[i + 64 * u];
+      const int lx = static_cast<int>(static_cast<int16_t>(p & 0xffff)) + xo + L.bias;
+      const int lyy = (static_cast<int>(p) >> 16) + yo + L.bias;
+      const bool vx0 = static_cast<unsigned>(lx) < static_cast<unsigned>(L.wnx);
+      const bool vx1 = static_cast<unsigned>(lx + h) < static_cast<unsigned>(L.wnx);
+      const bool vy0 = static_cast<unsigned>(lyy) < static_cast<unsigned>(L.wny);
+      const bool vy1 = static_cast<unsigned>(lyy + h) < static_cast<unsigned>(L.wny);
+      const int base = lyy * L.wnx + lx;
+      ad[4 * u + 0] = (vx0 && vy0) ? base : L.zero;
+      ad[4 * u + 1] = (vx0 && vy1) ? base + hw : L.zero;
+      ad[4 * u + 2] = (vx1 && vy0) ? base + h : L.zero;
+      ad[4 * u + 3] = (vx1 && vy1) ? base + hw + h : L.zero;
+    }
+    int v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) v[u] = L.data[ad[u]];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      a0 += v[4 * u]; a1 += v[4 * u + 1]; a2 += v[4 * u + 2]; a3 += v[4 * u + 3];
+    }
+  }
+  for (; i < npad; i += 64) {
     const uint32_t p = pts[i];
     const int lx = static_cast<int>(static_cast<int16_t>(p & 0xffff)) + xo + L.bias;
     const int ly = static_cast<int>(p) >> 16;
@@ -152,7 +182,25 @@ __device__ __forceinline__ int ScoreOne(const uint32_t* __restrict__ pts, int np
                                         const LevelView& L, int xo, int yo) {
   const int lane = threadIdx.x & 63;
   int acc = 0;
-  for (int i = lane; i < npad; i += 64) {
+  int i = lane;
+  for (; i + 448 < npad; i += 512) {
+    int ad[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const uint32_t p = pts[i + 64 * u];
+      const int lx = static_cast<int>(static_cast<int16_t>(p & 0xffff)) + xo + L.bias;
+      const int ly = (static_cast<int>(p) >> 16) + yo + L.bias;
+      const bool v = static_cast<unsigned>(lx) < static_cast<unsigned>(L.wnx) &&
+                     static_cast<unsigned>(ly) < static_cast<unsigned>(L.wny);
+      ad[u] = v ? ly * L.wnx + lx : L.zero;
+    }
+    int val[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) val[u] = L.data[ad[u]];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc += val[u];
+  }
+  for (; i < npad; i += 64) {
     const uint32_t p = pts[i];
     const int lx = static_cast<int>(static_cast<int16_t>(p & 0xffff)) + xo + L.bias;
     const int ly = (static_cast<int>(p) >> 16) + yo + L.bias;
@@ -476,6 +524,437 @@ fast2d_search(const SubmapDesc* __restrict__ submaps,
   }
 }
 
+// ---------------------------------------------------------------- K1b ------
+
+// Polyphase copy of a row-major wide level (see SubmapDesc::poly).
+__global__ void pyramid_polyphase(const uint8_t* __restrict__ level, int wnx, int wny,
+                                  int log_h, int stride, int ph, uint8_t* __restrict__ out,
+                                  int total) {
+  // out[0..3] front pad, out[4 + o] entry o, then a 16-byte zero tail.
+  const int o = blockIdx.x * blockDim.x + threadIdx.x;
+  if (o < 4) out[o] = 0;
+  if (o < 16) out[4 + total + o] = 0;
+  if (o >= total) return;
+  const int ps = stride * ph;
+  const int pi = o / ps, k = o - pi * ps;
+  const int h = 1 << log_h;
+  const int px = pi & (h - 1), py = pi >> log_h;
+  const int ky = k / stride, kx = k - ky * stride;
+  const int X = (kx << log_h) + px, Y = (ky << log_h) + py;
+  out[4 + o] = (X < wnx && Y < wny) ? level[static_cast<size_t>(Y) * wnx + X] : 0;
+}
+
+typedef unsigned int v2u_t __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t LevelRsrc(const uint8_t* base, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base), 0, bytes, 0x00020000);
+}
+
+// DFS stack entry word 1: bound sum (22 bits) | level << 27.
+__device__ __forceinline__ uint32_t V2Entry1(int sum, int level) {
+  return static_cast<uint32_t>(sum) | (static_cast<uint32_t>(level) << 27);
+}
+
+// ---------------------------------------------------------------- K2-K4 v3 -
+//
+// One workgroup (4 waves) owns one rotation of one pair at a time; the search
+// is a best-first DFS over nodes. Expanding a node scores its 2x2 children
+// block at the next level. A lane takes one node and a strided subset of the
+// scan's points ("point group"): in the polyphase level (row stride a multiple
+// of 4) the children of one node are two pairs of adjacent bytes, so a lane
+// issues two 8-byte row loads per point and extracts 4 lookups with
+// v_alignbyte. A batch of 2^k nodes fills all 64 lanes with 64/2^k point
+// groups; the 4 waves also split the points, and partial sums meet in LDS.
+// The top lattice is expanded from virtual nodes one level above it.
+
+constexpr int kPolyFrontPad = 4;  // bytes before plane 0 (row loads at a-1)
+// Polyphase buffers end with a 16-byte zero tail (pyramid_polyphase).
+constexpr int kRootChunk = 192;   // virtual roots pushed at a time
+
+struct V3Shared {
+  uint2 stack[kStack2];
+  int part[kWaves][kBatchNodes][4];
+  int node_xo[kBatchNodes], node_yo[kBatchNodes];
+  int nodes;        // nodes in the batch (a power of two, <= 16)
+  int level;        // child level being scored
+  int item_pair, item_chunk, queue;
+  int sp;
+  uint64_t best;
+  int mm[4];
+  int bounds[4];
+  int range_error;
+  int batch_no;
+  int vny, vtotal, vnext;
+  unsigned long long lv_cands[kMaxLevels];
+  unsigned long long lv_batches[kMaxLevels];
+};
+
+// Per-point polyphase plane offset + plane coordinates at `level`, for the
+// rotation's lattice origin (min_x, min_y). Entries past n are sentinels that
+// every range check rejects.
+__device__ __forceinline__ void V3Precompute(const uint32_t* pts, uint2* pre, int n, int npre,
+                                             const SubmapDesc& sm, int level, int min_x,
+                                             int min_y) {
+  const int h = 1 << level;
+  const int bias = h - 1;
+  const int stride = sm.plane_w[level];  // row stride, multiple of 4
+  const int ps = stride * sm.plane_h[level];
+  for (int i = threadIdx.x; i < npre; i += kSearchThreads) {
+    uint2 e = make_uint2(0u, (static_cast<uint32_t>(static_cast<uint16_t>(-16000))) |
+                                 (static_cast<uint32_t>(static_cast<uint16_t>(-16000)) << 16));
+    if (i < n) {
+      const uint32_t p = pts[i];
+      const int bx = static_cast<int16_t>(p & 0xffff) + min_x + bias;
+      const int by = (static_cast<int>(p) >> 16) + min_y + bias;
+      const int kx = bx >> level, ky = by >> level;
+      const int fx = bx & (h - 1), fy = by & (h - 1);
+      e.x = static_cast<uint32_t>(kPolyFrontPad + ((fy << level) + fx) * ps + kx + ky * stride);
+      e.y = (static_cast<uint32_t>(kx) & 0xffff) | (static_cast<uint32_t>(ky) << 16);
+    }
+    pre[i] = e;
+  }
+}
+
+__device__ __forceinline__ int V3CountOf(int nodes) {  // point groups per wave
+  return 64 / nodes;
+}
+
+// Scores the children of the batch's nodes. Leaves per-wave node sums in
+// sh.part[wave][node][child].
+__device__ __forceinline__ void V3Score(V3Shared& sh, const uint2* pre, int n,
+                                        const SubmapDesc& sm, int level, int min_x,
+                                        int min_y) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nodes = Uniform(sh.nodes);
+  const int groups = 64 / nodes;
+  const int node = lane & (nodes - 1);
+  const int g = lane / nodes;
+  const int pw = sm.plane_w[level];     // row stride (multiple of 4)
+  const int tw = sm.wide_nx[level];     // valid columns: kx < ceil(wnx / h)
+  const int h = 1 << level;
+  const int cols = (tw + h - 1) >> level;
+  const int rows = sm.plane_h[level];
+  const int bytes = Uniform(sm.poly_bytes[level]);
+  const __amdgpu_buffer_rsrc_t rsrc = LevelRsrc(sm.poly[level], bytes);
+  const int li = (sh.node_xo[node] - min_x) >> level;
+  const int lj = (sh.node_yo[node] - min_y) >> level;
+  const int loff = li + lj * pw;
+  // Points of this wave: [p0, p0 + per), per a multiple of groups * 4.
+  const int quarter = (n + kWaves - 1) / kWaves;
+  const int per = Uniform(((quarter + groups * 4 - 1) / (groups * 4)) * (groups * 4));
+  const int p0 = Uniform(wave * per);
+  int a00 = 0, a01 = 0, a10 = 0, a11 = 0;
+  constexpr int kOOB = 0x7ffffff0;
+  for (int base_i = p0; base_i < p0 + per && base_i < n; base_i += 4 * groups) {
+    uint2 r0[4], r1[4];
+    uint32_t msk[4], shf[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint2 e = pre[base_i + u * groups + g];
+      const int tx = static_cast<int16_t>(e.y & 0xffff) + li;
+      const int ty = (static_cast<int>(e.y) >> 16) + lj;
+      const int a = static_cast<int>(e.x) + loff;
+      const bool vx0 = static_cast<unsigned>(tx) < static_cast<unsigned>(cols);
+      const bool vx1 = static_cast<unsigned>(tx + 1) < static_cast<unsigned>(cols);
+      const bool vy0 = static_cast<unsigned>(ty) < static_cast<unsigned>(rows);
+      const bool vy1 = static_cast<unsigned>(ty + 1) < static_cast<unsigned>(rows);
+      msk[u] = (vx0 ? 0x00ffu : 0u) | (vx1 ? 0xff00u : 0u);
+      shf[u] = static_cast<uint32_t>(a) & 3u;
+      const int al = a & ~3;
+      const int o0 = (vy0 && (vx0 || vx1)) ? al : kOOB;
+      const int o1 = (vy1 && (vx0 || vx1)) ? al + pw : kOOB;
+      const v2u_t t0 = __builtin_amdgcn_raw_buffer_load_b64(rsrc, o0, 0, 0);
+      const v2u_t t1 = __builtin_amdgcn_raw_buffer_load_b64(rsrc, o1, 0, 0);
+      r0[u] = make_uint2(t0[0], t0[1]);
+      r1[u] = make_uint2(t1[0], t1[1]);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t x0 = __builtin_amdgcn_alignbyte(r0[u].y, r0[u].x, shf[u]) & msk[u];
+      const uint32_t x1 = __builtin_amdgcn_alignbyte(r1[u].y, r1[u].x, shf[u]) & msk[u];
+      a00 += x0 & 0xff;        // (xo,     yo)
+      a10 += x0 >> 8;          // (xo + h, yo)
+      a01 += x1 & 0xff;        // (xo,     yo + h)
+      a11 += x1 >> 8;          // (xo + h, yo + h)
+    }
+  }
+  // Reduce over point groups (lanes node + k*nodes).
+  for (int m = nodes; m < 64; m <<= 1) {
+    a00 += __shfl_xor(a00, m, 64);
+    a01 += __shfl_xor(a01, m, 64);
+    a10 += __shfl_xor(a10, m, 64);
+    a11 += __shfl_xor(a11, m, 64);
+  }
+  if (lane < nodes) {
+    sh.part[wave][lane][0] = a00;
+    sh.part[wave][lane][1] = a01;
+    sh.part[wave][lane][2] = a10;
+    sh.part[wave][lane][3] = a11;
+  }
+}
+
+__global__ void __launch_bounds__(kSearchThreads)
+fast2d_search_v3(const SubmapDesc* __restrict__ submaps,
+                 const PairDesc* __restrict__ pairs,
+                 const float* __restrict__ points,
+                 const float2* __restrict__ rot_table,
+                 WorkQueues2 queues,
+                 unsigned long long* __restrict__ counters,
+                 uint64_t* __restrict__ best,
+                 int32_t* __restrict__ status,
+                 unsigned long long* __restrict__ stats,
+                 int max_points) {
+  extern __shared__ __align__(16) uint32_t dyn[];
+  // pts: max_points; pre: npre uint2 (npre = max_points rounded + slack).
+  uint32_t* pts = dyn;
+  const int npre_cap = max_points + 1024;
+  uint2* pre = reinterpret_cast<uint2*>(dyn + ((max_points + 3) & ~3));
+  __shared__ V3Shared sh;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  unsigned long long local_cands = 0, local_lookups = 0;
+  if (tid == 0) sh.queue = blockIdx.x % kNumXcd;
+  if (tid < kMaxLevels) { sh.lv_cands[tid] = 0; sh.lv_batches[tid] = 0; }
+  int tries = 0;
+  __syncthreads();
+  for (;;) {
+    if (tid == 0) {
+      int q = sh.queue, pair = -1, chunk = 0;
+      while (tries < kNumXcd) {
+        const int64_t item = static_cast<int64_t>(atomicAdd(&counters[q], 1ull));
+        if (item < queues.queue_chunks[q]) {
+          const int64_t gch = queues.chunk_prefix[queues.queue_begin[q]] + item;
+          int e = queues.block_first[queues.block_offset[q] + static_cast<int>(item >> 6)];
+          while (queues.chunk_prefix[e + 1] <= gch) ++e;
+          pair = queues.pair_order[e];
+          chunk = static_cast<int>(gch - queues.chunk_prefix[e]);
+          break;
+        }
+        q = (q + 1) % kNumXcd;
+        ++tries;
+      }
+      sh.queue = q;
+      sh.item_pair = pair;
+      sh.item_chunk = chunk;
+    }
+    __syncthreads();
+    const int pair_index = Uniform(sh.item_pair);
+    if (pair_index < 0) break;
+    const PairDesc pd = pairs[pair_index];
+    const SubmapDesc& sm = submaps[pd.submap];
+    const int n = pd.num_points;
+    const int npre = min(npre_cap, ((n + 255) & ~255) + 256);
+    const int s_min = pd.max_rejected_sum;
+    uint64_t* pair_best = best + pair_index;
+    const int rot_begin = Uniform(sh.item_chunk) * queues.rot_chunk;
+    const int rot_end = min(pd.num_scans, rot_begin + queues.rot_chunk);
+    const int top_level = sm.levels - 1;
+    for (int rot = rot_begin; rot < rot_end; ++rot) {
+      // ---- K2: discretize this rotation into LDS, reduce min/max -----------
+      const float2 q = rot_table[pd.rot_offset + rot];
+      int mnx = 0x7fffffff, mxx = -0x7fffffff, mny = 0x7fffffff, mxy = -0x7fffffff;
+      bool range_error = false;
+      for (int i = tid; i < n; i += kSearchThreads) {
+        const float* p = points + 3 * (pd.point_offset + i);
+        float x, y;
+        RotateZDev(pd.pre_w, pd.pre_s, p[0], p[1], &x, &y);
+        RotateZDev(q.x, q.y, x, y, &x, &y);
+        const float px = __fadd_rn(pd.tx, x);
+        const float py = __fadd_rn(pd.ty, y);
+        const double cx = CellCoord(sm.max_y, py, sm.resolution);
+        const double cy = CellCoord(sm.max_x, px, sm.resolution);
+        int ix = 0, iy = 0;
+        if (fabs(cx) > kIndexLimit || fabs(cy) > kIndexLimit) {
+          range_error = true;
+        } else {
+          ix = static_cast<int>(cx);
+          iy = static_cast<int>(cy);
+        }
+        mnx = min(mnx, ix); mxx = max(mxx, ix);
+        mny = min(mny, iy); mxy = max(mxy, iy);
+        pts[i] = (static_cast<uint32_t>(ix) & 0xffff) | (static_cast<uint32_t>(iy) << 16);
+      }
+      mnx = WaveMin(mnx); mxx = WaveMax(mxx); mny = WaveMin(mny); mxy = WaveMax(mxy);
+      if (tid == 0) {
+        sh.mm[0] = mnx; sh.mm[1] = mxx; sh.mm[2] = mny; sh.mm[3] = mxy;
+        sh.range_error = 0;
+      }
+      __syncthreads();
+      if (lane == 0 && wave != 0) {
+        atomicMin(&sh.mm[0], mnx); atomicMax(&sh.mm[1], mxx);
+        atomicMin(&sh.mm[2], mny); atomicMax(&sh.mm[3], mxy);
+      }
+      if (range_error) sh.range_error = 1;
+      __syncthreads();
+      // ---- ShrinkToFit; virtual root nodes over the top lattice -------------
+      const int step = 1 << top_level;
+      if (wave == 0) {
+        int b0 = 0, b1 = 0, b2 = 0, b3 = 0;
+        if (lane == 0 && sh.range_error) atomicOr(&status[pair_index], kStatusRange);
+        const int lo_x = min(0, -sh.mm[1]), hi_x = max(0, sm.nx - 1 - sh.mm[0]);
+        const int lo_y = min(0, -sh.mm[3]), hi_y = max(0, sm.ny - 1 - sh.mm[2]);
+        b0 = max(-pd.num_linear, lo_x);
+        b1 = min(pd.num_linear, hi_x);
+        b2 = max(-pd.num_linear, lo_y);
+        b3 = min(pd.num_linear, hi_y);
+        const int tnx = (b1 - b0 + step) / step, tny = (b3 - b2 + step) / step;
+        if (lane == 0) {
+          sh.bounds[0] = b0; sh.bounds[1] = b1; sh.bounds[2] = b2; sh.bounds[3] = b3;
+          sh.vny = (tny + 1) >> 1;
+          sh.vtotal = ((tnx + 1) >> 1) * sh.vny;
+          sh.vnext = 0;
+          sh.sp = 0;
+          sh.best = LoadBest(pair_best);
+          sh.batch_no = 0;
+        }
+      }
+      __syncthreads();
+      const int min_x = Uniform(sh.bounds[0]), max_x = Uniform(sh.bounds[1]);
+      const int min_y = Uniform(sh.bounds[2]), max_y = Uniform(sh.bounds[3]);
+      // ---- K3/K4: batched best-first DFS -------------------------------------
+      // Virtual root nodes (level top+1, bound "infinite") enter the stack in
+      // chunks of kRootChunk whenever it runs empty.
+      for (;;) {
+        if (wave == 0) {
+          int sp = sh.sp;
+          if (sp == 0 && sh.vnext < sh.vtotal) {
+            const int v0 = sh.vnext, vc = min(kRootChunk, sh.vtotal - v0);
+            for (int k = lane; k < vc; k += 64) {
+              const int v = v0 + vc - 1 - k;  // lowest index on top
+              const int xo = min_x + (v / sh.vny) * 2 * step, yo = min_y + (v % sh.vny) * 2 * step;
+              sh.stack[k] = make_uint2((static_cast<uint32_t>(xo) & 0xffff) |
+                                           (static_cast<uint32_t>(yo) << 16),
+                                       0x3fffffu | (static_cast<uint32_t>(top_level + 1) << 27));
+            }
+            sp = vc;
+            if (lane == 0) sh.vnext = v0 + vc;
+          }
+          if (lane == 0 && (sh.batch_no++ & 7) == 0) {
+            const uint64_t fresh = LoadBest(pair_best);
+            if (fresh > sh.best) sh.best = fresh;
+          }
+          const uint32_t cur_sum = static_cast<uint32_t>(sh.best >> kSumShift);
+          int nodes = 0, lvl = 0;
+          if (sp > 0) {
+            const uint2 top = sh.stack[sp - 1];
+            lvl = static_cast<int>(top.y >> 27);
+            uint2 e = make_uint2(0, 0);
+            bool same = false;
+            if (lane < kBatchNodes && lane < sp) {
+              e = sh.stack[sp - 1 - lane];
+              same = static_cast<int>(e.y >> 27) == lvl;
+            }
+            const unsigned long long diff = __ballot(!same);
+            const int run = static_cast<int>(__ffsll(static_cast<long long>(diff))) - 1;
+            const bool expandable = lane < run && (e.y & 0x3fffff) >= cur_sum;
+            const unsigned long long em = __ballot(expandable);
+            const int ne = __popcll(em);
+            int take = run;  // default: the whole run is pruned
+            if (ne > 0) {
+              nodes = 1 << (31 - __clz(ne));  // largest power of two <= ne
+              // Lane index of the nodes-th expandable entry.
+              unsigned long long m = em;
+              for (int k = 1; k < nodes; ++k) m &= m - 1;
+              take = static_cast<int>(__ffsll(static_cast<long long>(m)));
+              const int rank = __popcll(em & ((1ull << lane) - 1));
+              if (expandable && lane < take) {
+                sh.node_xo[rank] = static_cast<int16_t>(e.x & 0xffff);
+                sh.node_yo[rank] = static_cast<int>(e.x) >> 16;
+              }
+            }
+            sp -= take;
+          }
+          if (lane == 0) {
+            sh.sp = sp;
+            sh.nodes = nodes;
+            sh.level = lvl - 1;
+          }
+        }
+        __syncthreads();
+        const int nodes = Uniform(sh.nodes);
+        const int sp_now = Uniform(sh.sp);
+        const int lvl = Uniform(sh.level);
+        if (nodes == 0) {
+          __syncthreads();
+          if (sp_now == 0) break;
+          continue;
+        }
+        V3Precompute(pts, pre, n, npre, sm, lvl, min_x, min_y);
+        __syncthreads();
+        V3Score(sh, pre, n, sm, lvl, min_x, min_y);
+        __syncthreads();
+        local_cands += 4 * nodes;
+        local_lookups += static_cast<unsigned long long>(4 * nodes) * n;
+        if (tid == 0) { sh.lv_cands[lvl] += 4 * nodes; sh.lv_batches[lvl] += 1; }
+        if (wave == 0) {
+          // Lane = child c of node c/4: (xo,yo), (xo,yo+h), (xo+h,yo), (xo+h,yo+h).
+          const int nd = lane >> 2, c = lane & 3;
+          const int h = 1 << lvl;
+          int sum = 0, xo = 0, yo = 0;
+          bool exists = false;
+          if (nd < nodes) {
+            sum = sh.part[0][nd][c] + sh.part[1][nd][c] + sh.part[2][nd][c] + sh.part[3][nd][c];
+            xo = sh.node_xo[nd] + ((c & 2) ? h : 0);
+            yo = sh.node_yo[nd] + ((c & 1) ? h : 0);
+            exists = xo <= max_x && yo <= max_y;
+          }
+          const uint64_t cur = sh.best;
+          const uint32_t cur_sum = static_cast<uint32_t>(cur >> kSumShift);
+          const bool keep = exists && sum > s_min && static_cast<uint32_t>(sum) >= cur_sum;
+          if (lvl == 0) {
+            uint64_t key = 0;
+            if (keep) {
+              if (xo < -kOffsetLimit || xo > kOffsetLimit || yo < -kOffsetLimit || yo > kOffsetLimit)
+                atomicOr(&status[pair_index], kStatusRange);
+              else
+                key = PackLeafKey(sum, rot, xo, yo);
+            }
+            for (int m = 32; m >= 1; m >>= 1) {
+              const uint64_t o = __shfl_xor(key, m, 64);
+              key = o > key ? o : key;
+            }
+            if (lane == 0 && key > cur) {
+              atomicMax(reinterpret_cast<unsigned long long*>(pair_best), key);
+              sh.best = key;
+            }
+          } else {
+            uint32_t skey = keep ? ((static_cast<uint32_t>(sum) << 8) | static_cast<uint32_t>(lane)) : 0u;
+            for (int k = 2; k <= 64; k <<= 1)
+              for (int jj = k >> 1; jj >= 1; jj >>= 1) {
+                const uint32_t other = __shfl_xor(skey, jj, 64);
+                const bool up = ((lane & k) == 0), lower = ((lane & jj) == 0);
+                const uint32_t hi_v = skey > other ? skey : other, lo_v = skey > other ? other : skey;
+                skey = (lower == up) ? hi_v : lo_v;
+              }
+            const int kept = __popcll(__ballot(keep));
+            const int sp = sh.sp;
+            // Children of sorted position k come from lane j = skey & 0xff.
+            const int j = skey & 0xff;
+            const int cx = __shfl(xo, j, 64), cy = __shfl(yo, j, 64);
+            if (lane < kept && sp + kept <= kStack2) {
+              sh.stack[sp + kept - 1 - lane] = make_uint2(
+                  (static_cast<uint32_t>(cx) & 0xffff) | (static_cast<uint32_t>(cy) << 16),
+                  V2Entry1(static_cast<int>(skey >> 8), lvl));
+            }
+            if (lane == 0) {
+              if (sp + kept > kStack2) atomicOr(&status[pair_index], kStatusRange);
+              else sh.sp = sp + kept;
+            }
+          }
+        }
+        __syncthreads();
+      }
+    }
+  }
+  if (stats && tid == 0) {
+    atomicAdd(&stats[0], local_cands);
+    atomicAdd(&stats[1], local_lookups);
+  }
+  if (stats && tid < kMaxLevels) {
+    atomicAdd(&stats[2 + tid], sh.lv_cands[tid]);
+    atomicAdd(&stats[2 + kMaxLevels + tid], sh.lv_batches[tid]);
+  }
+}
+
 // ---------------------------------------------------------------- K5 -------
 
 // One workgroup per rotated scan; one lane per (x, y) offset of the full
@@ -563,6 +1042,23 @@ hipError_t LaunchFast2dSearch(int grid, size_t dyn_lds, hipStream_t st, const Su
                               uint64_t* best, int32_t* status, unsigned long long* stats) {
   hipLaunchKernelGGL(fast2d_search, dim3(grid), dim3(kSearchThreads), dyn_lds, st, submaps, pairs,
                      points, rot_table, queues, counters, best, status, stats);
+  return hipGetLastError();
+}
+
+hipError_t LaunchPyramidPolyphase(const uint8_t* level, int wnx, int wny, int log_h, int pw, int ph,
+                                 uint8_t* out, int total, hipStream_t st) {
+  hipLaunchKernelGGL(pyramid_polyphase, dim3((std::max(total, 16) + 255) / 256), dim3(256), 0, st,
+                     level, wnx, wny, log_h, pw, ph, out, total);
+  return hipGetLastError();
+}
+
+hipError_t LaunchFast2dSearchV2(int grid, size_t dyn_lds, hipStream_t st, const SubmapDesc* submaps,
+                                const PairDesc* pairs, const float* points, const float2* rot_table,
+                                const WorkQueues2& queues, unsigned long long* counters,
+                                uint64_t* best, int32_t* status, unsigned long long* stats,
+                                int max_points) {
+  hipLaunchKernelGGL(fast2d_search_v3, dim3(grid), dim3(kSearchThreads), dyn_lds, st, submaps, pairs,
+                     points, rot_table, queues, counters, best, status, stats, max_points);
   return hipGetLastError();
 }
 

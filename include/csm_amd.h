@@ -93,6 +93,10 @@ typedef struct csm_timing {
 void csm_context_enable_timing(csm_context* ctx, int32_t enable);
 void csm_context_get_timing(csm_context* ctx, csm_timing* out);
 void csm_context_reset_timing(csm_context* ctx);
+/* Per pyramid level: candidates scored and scoring batches (v2 kernel),
+ * accumulated while timing is enabled. Returns the number of levels written. */
+int32_t csm_context_level_stats(csm_context* ctx, double* candidates, double* batches,
+                                int32_t max_levels);
 
 /* ---- FastCorrelativeScanMatcher2D ------------------------------------------
  * csm_fast2d_create replaces the constructor

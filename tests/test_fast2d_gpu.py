@@ -89,7 +89,7 @@ def _rigid2f(x, y, a):
     return np.array([x, y, a], np.float32)
 
 
-def test_correct_pose_match(csm, oracle):
+def test_correct_pose_match(csm, oracle, search_kernel):
     """FastCorrelativeScanMatcherTest.CorrectPose (:144-192): Match() with
     depth 3 recovers random poses; GPU == oracle on every case."""
     rng = np.random.RandomState(42)
@@ -115,7 +115,7 @@ def test_correct_pose_match(csm, oracle):
     assert kinds.count("exact") + kinds.count("tie") == 50
 
 
-def test_full_submap_matching(csm, oracle):
+def test_full_submap_matching(csm, oracle, search_kernel):
     """FastCorrelativeScanMatcherTest.FullSubmapMatching (:194-246), depth 6."""
     rng = np.random.RandomState(42)
     base = np.array([[-2.5, 0.5, 0], [-2.25, 0.5, 0], [0.0, 0.5, 0], [0.25, 1.6, 0],
@@ -145,8 +145,16 @@ def world(csm):
     return csm.SyntheticWorld2D(num_nodes=64, num_submaps=8, decimate_to=200, seed=20250127)
 
 
+@pytest.fixture(params=["v2", "v1"])
+def search_kernel(request, monkeypatch):
+    """Both search kernels: v2 (lanes = candidates, polyphase pyramid) and
+    v1 (lanes = points, row-major pyramid; used above ~10k points)."""
+    monkeypatch.setenv("CSM_SEARCH_KERNEL", request.param[1])
+    return request.param
+
+
 @pytest.mark.parametrize("depth_mode", ["auto", "configured"])
-def test_synthetic_full_submap_pairs(csm, oracle, world, depth_mode):
+def test_synthetic_full_submap_pairs(csm, oracle, world, depth_mode, search_kernel):
     """BASELINE-shaped 400x400 submaps, N~200 clouds, depth 7, min_score 0.55:
     GPU batch == oracle MatchFullSubmap on every pair."""
     search_depth = 0 if depth_mode == "auto" else 7
@@ -187,7 +195,7 @@ def test_batch_equals_single_calls(csm, world):
             assert pose == (res[k]["x"], res[k]["y"], res[k]["theta"])
 
 
-def test_match_window_mode_parity(csm, oracle, world):
+def test_match_window_mode_parity(csm, oracle, world, search_kernel):
     """Match() with an initial pose near the truth (the local constraint
     search of ConstraintBuilder2D::ComputeConstraint, :221-235)."""
     opts = csm.FastCorrelativeScanMatcherOptions2D(7.0, math.radians(30), 7)
@@ -207,7 +215,7 @@ def test_match_window_mode_parity(csm, oracle, world):
         assert_fast_parity(oracle, om, limits, g.cells, gpu, ref, False, init, cloud)
 
 
-def test_edge_cases(csm, oracle):
+def test_edge_cases(csm, oracle, search_kernel):
     cells = np.zeros((20, 30), np.uint16)
     cells[5:8, 10:20] = 30000
     limits = (0.05, 1.0, 1.5)
