@@ -36,15 +36,14 @@ struct SubmapDesc {
   int32_t wide_nx[kMaxLevels];
   int32_t wide_ny[kMaxLevels];
   int32_t zero_index[kMaxLevels];  // index of the trailing zero byte
-  // Polyphase copy of level d (period h = 2^d): plane (px, py) holds the
-  // wide cells (kx*h + px, ky*h + py), kx < plane_w, ky < plane_h, stored at
-  // ((py*h + px) * plane_w*plane_h) + kx + ky*plane_w; cells past the wide
-  // grid are 0. Level-d candidates all lie on one 2^d lattice, so the lookups
-  // of one point by neighbouring candidates are neighbouring bytes.
-  const uint8_t* poly[kMaxLevels];
-  int32_t plane_w[kMaxLevels];
-  int32_t plane_h[kMaxLevels];
-  int32_t poly_bytes[kMaxLevels];  // h*h*plane_w*plane_h
+  // Quad layout of level d (h = 2^d, search kernel v4): dword (X', Y'),
+  // X' < quad_w = wide_nx + h, Y' < quad_h = wide_ny + h, packs the values
+  // of the 2x2 children whose child (0,0) is at wide cell (X' - h, Y' - h):
+  // byte0 (0,0), byte1 (0,h), byte2 (h,0), byte3 (h,h); 0 outside the grid.
+  const uint32_t* quad[kMaxLevels];
+  int32_t quad_w[kMaxLevels];
+  int32_t quad_h[kMaxLevels];
+  int32_t quad_bytes[kMaxLevels];
 };
 
 // One (node, submap) search.

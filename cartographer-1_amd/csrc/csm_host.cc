@@ -205,15 +205,17 @@ int RunBatch(csm_context* ctx, csm_fast2d* const* submaps, int32_t num_submaps,
   const int np = static_cast<int>(pdesc.size());
   if (np == 0) return CSM_OK;
 
-  // v2 (lanes = candidates over the polyphase pyramid) keeps three N-long
-  // arrays in LDS; above ~10k points the v1 kernel (lanes = points) is used.
   const char* forced_env = std::getenv("CSM_SEARCH_KERNEL");
   const int forced = forced_env ? std::atoi(forced_env) : 0;
-  const bool use_v2 = forced == 2 || (forced != 1 && max_npad * 12 + 8192 <= 120 * 1024);
-  // Rotation chunk size: v1 from the LDS budget for discretized points;
-  // v2 processes rotations one at a time, claimed in small chunks.
+  // The v4 kernel keeps rot_chunk discretized scans (4 B/point) in LDS;
+  // above ~8k points per scan the v1 kernel (lanes = points) is used.
+  const bool use_v2 = forced == 2 || (forced != 1 && max_npad <= 8192);
+  const char* rc_env = std::getenv("CSM_ROT_CHUNK");
+  const int v4_budget = 18 * 1024;
+  const int v4_rc = rc_env ? std::max(1, std::min(16, std::atoi(rc_env)))
+                           : std::max(1, std::min(8, v4_budget / (max_npad * 4)));
   const int lds_budget = 40 * 1024;
-  const int rc = use_v2 ? 2 : std::max(1, std::min(16, lds_budget / (max_npad * 4)));
+  const int rc = use_v2 ? v4_rc : std::max(1, std::min(16, lds_budget / (max_npad * 4)));
 
   // Per-XCD queues: submap s -> queue s % 8 so a submap's pyramid stays in
   // one XCD's L2; pairs within a queue in submap order.
@@ -297,10 +299,8 @@ int RunBatch(csm_context* ctx, csm_fast2d* const* submaps, int32_t num_submaps,
     wq2.pair_order = wq.pair_order;
     wq2.chunk_prefix = wq.chunk_prefix;
     wq2.block_first = ctx->blocks.as<int32_t>();
-    const int maxp = max_npad;
-    // pts (4 B/pt) + per-level precompute (8 B/pt, +1024 slack entries).
-    const size_t dyn_lds = static_cast<size_t>(maxp) * 4 + (static_cast<size_t>(maxp) + 1024) * 8;
-    const int per_cu = std::max(1, std::min(8, static_cast<int>((160 * 1024) / (dyn_lds + 12 * 1024))));
+    const size_t dyn_lds = static_cast<size_t>(rc) * max_npad * 4;
+    const int per_cu = std::max(1, std::min(8, static_cast<int>((160 * 1024) / (dyn_lds + 10 * 1024))));
     const int grid = static_cast<int>(std::min<int64_t>(static_cast<int64_t>(ctx->num_cus) * per_cu,
                                                         std::max<int64_t>(total_chunks, 1)));
     CSM_HIP(LaunchFast2dSearchV2(grid, dyn_lds, st, ctx->submap_desc.as<SubmapDesc>(),
@@ -308,7 +308,7 @@ int RunBatch(csm_context* ctx, csm_fast2d* const* submaps, int32_t num_submaps,
                                  ctx->rot_table.as<float2>(), wq2,
                                  ctx->counters.as<unsigned long long>(), ctx->best.as<uint64_t>(),
                                  ctx->status.as<int32_t>(), ctx->stats.as<unsigned long long>(),
-                                 maxp));
+                                 max_npad));
   } else {
     const size_t dyn_lds = static_cast<size_t>(rc) * max_npad * sizeof(uint32_t);
     const int grid = static_cast<int>(std::min<int64_t>(static_cast<int64_t>(ctx->num_cus) * 4,
@@ -501,26 +501,22 @@ int csm_fast2d_create(csm_context* ctx, const csm_map_limits* limits,
     offs[l] = total;
     total += (static_cast<size_t>(d.zero_index[l]) + 1 + 255) & ~size_t(255);
   }
-  std::vector<size_t> poffs(depth), poly_entries(depth);
+  std::vector<size_t> qoffs(depth);
   for (int l = 0; l < depth; ++l) {
-    // Polyphase planes: row stride a multiple of 4 (the search kernel reads
-    // 8-byte aligned pairs around a byte), 4-byte front pad, 16-byte zero tail.
     const int h = 1 << l;
-    d.plane_w[l] = (((d.wide_nx[l] + h - 1) / h) + 3) & ~3;
-    d.plane_h[l] = (d.wide_ny[l] + h - 1) / h;
-    const size_t entries = static_cast<size_t>(h) * h * d.plane_w[l] * d.plane_h[l];
-    const size_t pb = 4 + entries + 16;
-    if (pb > 0x7fffff00u) return CSM_ERANGE;
-    d.poly_bytes[l] = static_cast<int32_t>(pb);
-    poly_entries[l] = entries;
-    poffs[l] = total;
-    total += (pb + 255) & ~size_t(255);
+    d.quad_w[l] = d.wide_nx[l] + h;
+    d.quad_h[l] = d.wide_ny[l] + h;
+    const size_t qb = static_cast<size_t>(d.quad_w[l]) * d.quad_h[l] * 4;
+    if (qb > 0x7fffff00u) return CSM_ERANGE;
+    d.quad_bytes[l] = static_cast<int32_t>(qb);
+    qoffs[l] = total;
+    total += (qb + 255) & ~size_t(255);
   }
   int rc;
   if ((rc = m->pyramid.Reserve(total))) return rc;
   for (int l = 0; l < depth; ++l) {
     d.level[l] = m->pyramid.as<uint8_t>() + offs[l];
-    d.poly[l] = m->pyramid.as<uint8_t>() + poffs[l];
+    d.quad[l] = reinterpret_cast<const uint32_t*>(m->pyramid.as<uint8_t>() + qoffs[l]);
   }
 
   DevBuf dcells, dq;
@@ -538,9 +534,8 @@ int csm_fast2d_create(csm_context* ctx, const csm_map_limits* limits,
                                 1 << (l - 1), st));
   }
   for (int l = 0; l < depth; ++l)
-    CSM_HIP(LaunchPyramidPolyphase(d.level[l], d.wide_nx[l], d.wide_ny[l], l, d.plane_w[l],
-                                   d.plane_h[l], const_cast<uint8_t*>(d.poly[l]),
-                                   static_cast<int>(poly_entries[l]), st));
+    CSM_HIP(LaunchPyramidQuad(d.level[l], d.wide_nx[l], d.wide_ny[l], 1 << l,
+                              const_cast<uint32_t*>(d.quad[l]), d.quad_w[l], d.quad_h[l], st));
   CSM_HIP(hipStreamSynchronize(st));  // dcells/dq are freed on return
   *out = m.release();
   return CSM_OK;

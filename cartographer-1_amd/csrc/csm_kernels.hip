@@ -524,28 +524,6 @@ fast2d_search(const SubmapDesc* __restrict__ submaps,
   }
 }
 
-// ---------------------------------------------------------------- K1b ------
-
-// Polyphase copy of a row-major wide level (see SubmapDesc::poly).
-__global__ void pyramid_polyphase(const uint8_t* __restrict__ level, int wnx, int wny,
-                                  int log_h, int stride, int ph, uint8_t* __restrict__ out,
-                                  int total) {
-  // out[0..3] front pad, out[4 + o] entry o, then a 16-byte zero tail.
-  const int o = blockIdx.x * blockDim.x + threadIdx.x;
-  if (o < 4) out[o] = 0;
-  if (o < 16) out[4 + total + o] = 0;
-  if (o >= total) return;
-  const int ps = stride * ph;
-  const int pi = o / ps, k = o - pi * ps;
-  const int h = 1 << log_h;
-  const int px = pi & (h - 1), py = pi >> log_h;
-  const int ky = k / stride, kx = k - ky * stride;
-  const int X = (kx << log_h) + px, Y = (ky << log_h) + py;
-  out[4 + o] = (X < wnx && Y < wny) ? level[static_cast<size_t>(Y) * wnx + X] : 0;
-}
-
-typedef unsigned int v2u_t __attribute__((ext_vector_type(2)));
-
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t LevelRsrc(const uint8_t* base, int bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base), 0, bytes, 0x00020000);
 }
@@ -555,146 +533,131 @@ __device__ __forceinline__ uint32_t V2Entry1(int sum, int level) {
   return static_cast<uint32_t>(sum) | (static_cast<uint32_t>(level) << 27);
 }
 
-// ---------------------------------------------------------------- K2-K4 v3 -
+constexpr int kRootChunk = 192;  // virtual roots pushed at a time
+
+// ---------------------------------------------------------------- K1c ------
+
+// Quad layout of level d (h = 2^d): dword (X', Y') over (wnx + h) x (wny + h)
+// packs the four children of a node whose child (0,0) sits at wide cell
+// (X, Y) = (X' - h, Y' - h): byte0 G(X, Y), byte1 G(X, Y+h), byte2 G(X+h, Y),
+// byte3 G(X+h, Y+h); G = 0 outside the wide grid.
+__global__ void pyramid_quad(const uint8_t* __restrict__ level, int wnx, int wny, int h,
+                             uint32_t* __restrict__ out, int qw, int qh) {
+  const int xq = blockIdx.x * blockDim.x + threadIdx.x;
+  const int yq = blockIdx.y;
+  if (xq >= qw) return;
+  const int X = xq - h, Y = yq - h;
+  auto g = [&](int a, int b) -> uint32_t {
+    return (a >= 0 && b >= 0 && a < wnx && b < wny) ? level[static_cast<size_t>(b) * wnx + a] : 0u;
+  };
+  out[static_cast<size_t>(yq) * qw + xq] =
+      g(X, Y) | (g(X, Y + h) << 8) | (g(X + h, Y) << 16) | (g(X + h, Y + h) << 24);
+}
+
+// ---------------------------------------------------------------- K2-K4 v4 -
 //
-// One workgroup (4 waves) owns one rotation of one pair at a time; the search
-// is a best-first DFS over nodes. Expanding a node scores its 2x2 children
-// block at the next level. A lane takes one node and a strided subset of the
-// scan's points ("point group"): in the polyphase level (row stride a multiple
-// of 4) the children of one node are two pairs of adjacent bytes, so a lane
-// issues two 8-byte row loads per point and extracts 4 lookups with
-// v_alignbyte. A batch of 2^k nodes fills all 64 lanes with 64/2^k point
-// groups; the 4 waves also split the points, and partial sums meet in LDS.
-// The top lattice is expanded from virtual nodes one level above it.
+// A workgroup (4 waves) searches a chunk of R rotations of one pair at once.
+// The DFS stack mixes the chunk's rotations; a batch pops up to 16 nodes of
+// one level (best first) and scores their 2x2 children: a lane takes one node
+// and a strided subset of that node's rotated scan, and per point issues ONE
+// dword load from the quad layout that returns all four children's values.
+// The 4 waves split the points and meet in LDS; wave 0 combines, prunes,
+// pushes survivors sorted (best on top) and pops the next batch. Roots are
+// virtual nodes one level above the top lattice.
 
-constexpr int kPolyFrontPad = 4;  // bytes before plane 0 (row loads at a-1)
-// Polyphase buffers end with a 16-byte zero tail (pyramid_polyphase).
-constexpr int kRootChunk = 192;   // virtual roots pushed at a time
+constexpr int kMaxRotChunk = 16;
 
-struct V3Shared {
-  uint2 stack[kStack2];
+struct V4Shared {
+  uint2 stack[kStack2];  // w0: xo | yo << 16; w1: sum | rot << 22 | level << 27
   int part[kWaves][kBatchNodes][4];
-  int node_xo[kBatchNodes], node_yo[kBatchNodes];
-  int nodes;        // nodes in the batch (a power of two, <= 16)
-  int level;        // child level being scored
+  int node_xo[kBatchNodes], node_yo[kBatchNodes], node_rot[kBatchNodes];
+  int nodes, level, done;
   int item_pair, item_chunk, queue;
   int sp;
   uint64_t best;
-  int mm[4];
-  int bounds[4];
-  int range_error;
-  int batch_no;
-  int vny, vtotal, vnext;
+  int mm[kMaxRotChunk][4];
+  int bounds[kMaxRotChunk][4];
+  int vny[kMaxRotChunk];
+  int root_prefix[kMaxRotChunk + 1];
+  int vnext;
+  int range_error, batch_no;
   unsigned long long lv_cands[kMaxLevels];
   unsigned long long lv_batches[kMaxLevels];
 };
 
-// Per-point polyphase plane offset + plane coordinates at `level`, for the
-// rotation's lattice origin (min_x, min_y). Entries past n are sentinels that
-// every range check rejects.
-__device__ __forceinline__ void V3Precompute(const uint32_t* pts, uint2* pre, int n, int npre,
-                                             const SubmapDesc& sm, int level, int min_x,
-                                             int min_y) {
-  const int h = 1 << level;
-  const int bias = h - 1;
-  const int stride = sm.plane_w[level];  // row stride, multiple of 4
-  const int ps = stride * sm.plane_h[level];
-  for (int i = threadIdx.x; i < npre; i += kSearchThreads) {
-    uint2 e = make_uint2(0u, (static_cast<uint32_t>(static_cast<uint16_t>(-16000))) |
-                                 (static_cast<uint32_t>(static_cast<uint16_t>(-16000)) << 16));
-    if (i < n) {
-      const uint32_t p = pts[i];
-      const int bx = static_cast<int16_t>(p & 0xffff) + min_x + bias;
-      const int by = (static_cast<int>(p) >> 16) + min_y + bias;
-      const int kx = bx >> level, ky = by >> level;
-      const int fx = bx & (h - 1), fy = by & (h - 1);
-      e.x = static_cast<uint32_t>(kPolyFrontPad + ((fy << level) + fx) * ps + kx + ky * stride);
-      e.y = (static_cast<uint32_t>(kx) & 0xffff) | (static_cast<uint32_t>(ky) << 16);
-    }
-    pre[i] = e;
-  }
-}
-
-__device__ __forceinline__ int V3CountOf(int nodes) {  // point groups per wave
-  return 64 / nodes;
-}
-
-// Scores the children of the batch's nodes. Leaves per-wave node sums in
-// sh.part[wave][node][child].
-__device__ __forceinline__ void V3Score(V3Shared& sh, const uint2* pre, int n,
-                                        const SubmapDesc& sm, int level, int min_x,
-                                        int min_y) {
+__device__ __forceinline__ void V4Score(V4Shared& sh, const uint32_t* pts, int npad, int n,
+                                        const SubmapDesc& sm, int level) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nodes = Uniform(sh.nodes);
   const int groups = 64 / nodes;
   const int node = lane & (nodes - 1);
   const int g = lane / nodes;
-  const int pw = sm.plane_w[level];     // row stride (multiple of 4)
-  const int tw = sm.wide_nx[level];     // valid columns: kx < ceil(wnx / h)
   const int h = 1 << level;
-  const int cols = (tw + h - 1) >> level;
-  const int rows = sm.plane_h[level];
-  const int bytes = Uniform(sm.poly_bytes[level]);
-  const __amdgpu_buffer_rsrc_t rsrc = LevelRsrc(sm.poly[level], bytes);
-  const int li = (sh.node_xo[node] - min_x) >> level;
-  const int lj = (sh.node_yo[node] - min_y) >> level;
-  const int loff = li + lj * pw;
-  // Points of this wave: [p0, p0 + per), per a multiple of groups * 4.
+  const int qw = sm.quad_w[level], qh = sm.quad_h[level];
+  const __amdgpu_buffer_rsrc_t rsrc =
+      LevelRsrc(reinterpret_cast<const uint8_t*>(sm.quad[level]), Uniform(sm.quad_bytes[level]));
+  const uint32_t* P = pts + sh.node_rot[node] * npad;
+  const int cx = sh.node_xo[node] + (h - 1) + h;
+  const int cy = sh.node_yo[node] + (h - 1) + h;
   const int quarter = (n + kWaves - 1) / kWaves;
-  const int per = Uniform(((quarter + groups * 4 - 1) / (groups * 4)) * (groups * 4));
-  const int p0 = Uniform(wave * per);
-  int a00 = 0, a01 = 0, a10 = 0, a11 = 0;
+  const int s = Uniform(min(n, wave * quarter)), e = Uniform(min(n, wave * quarter + quarter));
   constexpr int kOOB = 0x7ffffff0;
-  for (int base_i = p0; base_i < p0 + per && base_i < n; base_i += 4 * groups) {
-    uint2 r0[4], r1[4];
-    uint32_t msk[4], shf[4];
+  constexpr int U = 8;
+  uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+  int i = s;
+  for (; i + U * groups <= e; i += U * groups) {
+    int ad[U];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const uint2 e = pre[base_i + u * groups + g];
-      const int tx = static_cast<int16_t>(e.y & 0xffff) + li;
-      const int ty = (static_cast<int>(e.y) >> 16) + lj;
-      const int a = static_cast<int>(e.x) + loff;
-      const bool vx0 = static_cast<unsigned>(tx) < static_cast<unsigned>(cols);
-      const bool vx1 = static_cast<unsigned>(tx + 1) < static_cast<unsigned>(cols);
-      const bool vy0 = static_cast<unsigned>(ty) < static_cast<unsigned>(rows);
-      const bool vy1 = static_cast<unsigned>(ty + 1) < static_cast<unsigned>(rows);
-      msk[u] = (vx0 ? 0x00ffu : 0u) | (vx1 ? 0xff00u : 0u);
-      shf[u] = static_cast<uint32_t>(a) & 3u;
-      const int al = a & ~3;
-      const int o0 = (vy0 && (vx0 || vx1)) ? al : kOOB;
-      const int o1 = (vy1 && (vx0 || vx1)) ? al + pw : kOOB;
-      const v2u_t t0 = __builtin_amdgcn_raw_buffer_load_b64(rsrc, o0, 0, 0);
-      const v2u_t t1 = __builtin_amdgcn_raw_buffer_load_b64(rsrc, o1, 0, 0);
-      r0[u] = make_uint2(t0[0], t0[1]);
-      r1[u] = make_uint2(t1[0], t1[1]);
+    for (int u = 0; u < U; ++u) {
+      const uint32_t p = P[i + u * groups + g];
+      const int X = static_cast<int16_t>(p & 0xffff) + cx;
+      const int Y = (static_cast<int>(p) >> 16) + cy;
+      const bool valid = static_cast<unsigned>(X) < static_cast<unsigned>(qw) &&
+                         static_cast<unsigned>(Y) < static_cast<unsigned>(qh);
+      ad[u] = valid ? static_cast<int>((__umul24(Y, qw) + X) << 2) : kOOB;
     }
+    uint32_t v[U];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const uint32_t x0 = __builtin_amdgcn_alignbyte(r0[u].y, r0[u].x, shf[u]) & msk[u];
-      const uint32_t x1 = __builtin_amdgcn_alignbyte(r1[u].y, r1[u].x, shf[u]) & msk[u];
-      a00 += x0 & 0xff;        // (xo,     yo)
-      a10 += x0 >> 8;          // (xo + h, yo)
-      a01 += x1 & 0xff;        // (xo,     yo + h)
-      a11 += x1 >> 8;          // (xo + h, yo + h)
+    for (int u = 0; u < U; ++u) v[u] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, ad[u], 0, 0);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      // v_dot4_u32_u8 with a one-hot weight picks one byte and accumulates.
+      a0 = __builtin_amdgcn_udot4(v[u], 0x00000001u, a0, false);
+      a1 = __builtin_amdgcn_udot4(v[u], 0x00000100u, a1, false);
+      a2 = __builtin_amdgcn_udot4(v[u], 0x00010000u, a2, false);
+      a3 = __builtin_amdgcn_udot4(v[u], 0x01000000u, a3, false);
     }
   }
-  // Reduce over point groups (lanes node + k*nodes).
+  for (; i < e; i += groups) {
+    const int idx = i + g;
+    const uint32_t p = idx < e ? P[idx] : 0x80008000u;
+    const int X = static_cast<int16_t>(p & 0xffff) + cx;
+    const int Y = (static_cast<int>(p) >> 16) + cy;
+    const bool valid = idx < e && static_cast<unsigned>(X) < static_cast<unsigned>(qw) &&
+                       static_cast<unsigned>(Y) < static_cast<unsigned>(qh);
+    const uint32_t vv = __builtin_amdgcn_raw_buffer_load_b32(
+        rsrc, valid ? static_cast<int>((__umul24(Y, qw) + X) << 2) : kOOB, 0, 0);
+    a0 = __builtin_amdgcn_udot4(vv, 0x00000001u, a0, false);
+    a1 = __builtin_amdgcn_udot4(vv, 0x00000100u, a1, false);
+    a2 = __builtin_amdgcn_udot4(vv, 0x00010000u, a2, false);
+    a3 = __builtin_amdgcn_udot4(vv, 0x01000000u, a3, false);
+  }
   for (int m = nodes; m < 64; m <<= 1) {
-    a00 += __shfl_xor(a00, m, 64);
-    a01 += __shfl_xor(a01, m, 64);
-    a10 += __shfl_xor(a10, m, 64);
-    a11 += __shfl_xor(a11, m, 64);
+    a0 += __shfl_xor(a0, m, 64);
+    a1 += __shfl_xor(a1, m, 64);
+    a2 += __shfl_xor(a2, m, 64);
+    a3 += __shfl_xor(a3, m, 64);
   }
   if (lane < nodes) {
-    sh.part[wave][lane][0] = a00;
-    sh.part[wave][lane][1] = a01;
-    sh.part[wave][lane][2] = a10;
-    sh.part[wave][lane][3] = a11;
+    sh.part[wave][lane][0] = a0;  // (xo,     yo)
+    sh.part[wave][lane][1] = a1;  // (xo,     yo + h)
+    sh.part[wave][lane][2] = a2;  // (xo + h, yo)
+    sh.part[wave][lane][3] = a3;  // (xo + h, yo + h)
   }
 }
 
 __global__ void __launch_bounds__(kSearchThreads)
-fast2d_search_v3(const SubmapDesc* __restrict__ submaps,
+fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
                  const PairDesc* __restrict__ pairs,
                  const float* __restrict__ points,
                  const float2* __restrict__ rot_table,
@@ -703,20 +666,18 @@ fast2d_search_v3(const SubmapDesc* __restrict__ submaps,
                  uint64_t* __restrict__ best,
                  int32_t* __restrict__ status,
                  unsigned long long* __restrict__ stats,
-                 int max_points) {
-  extern __shared__ __align__(16) uint32_t dyn[];
-  // pts: max_points; pre: npre uint2 (npre = max_points rounded + slack).
-  uint32_t* pts = dyn;
-  const int npre_cap = max_points + 1024;
-  uint2* pre = reinterpret_cast<uint2*>(dyn + ((max_points + 3) & ~3));
-  __shared__ V3Shared sh;
+                 int npad) {
+  extern __shared__ __align__(16) uint32_t pts[];  // rot_chunk * npad
+  __shared__ V4Shared sh;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int rc = queues.rot_chunk;
   unsigned long long local_cands = 0, local_lookups = 0;
   if (tid == 0) sh.queue = blockIdx.x % kNumXcd;
   if (tid < kMaxLevels) { sh.lv_cands[tid] = 0; sh.lv_batches[tid] = 0; }
   int tries = 0;
   __syncthreads();
   for (;;) {
+    // ---- claim (pair, rotation chunk) from an XCD-affine queue ------------
     if (tid == 0) {
       int q = sh.queue, pair = -1, chunk = 0;
       while (tries < kNumXcd) {
@@ -742,17 +703,21 @@ fast2d_search_v3(const SubmapDesc* __restrict__ submaps,
     const PairDesc pd = pairs[pair_index];
     const SubmapDesc& sm = submaps[pd.submap];
     const int n = pd.num_points;
-    const int npre = min(npre_cap, ((n + 255) & ~255) + 256);
     const int s_min = pd.max_rejected_sum;
     uint64_t* pair_best = best + pair_index;
-    const int rot_begin = Uniform(sh.item_chunk) * queues.rot_chunk;
-    const int rot_end = min(pd.num_scans, rot_begin + queues.rot_chunk);
+    const int rot0 = Uniform(sh.item_chunk) * rc;
+    const int nrot = min(rc, pd.num_scans - rot0);
     const int top_level = sm.levels - 1;
-    for (int rot = rot_begin; rot < rot_end; ++rot) {
-      // ---- K2: discretize this rotation into LDS, reduce min/max -----------
-      const float2 q = rot_table[pd.rot_offset + rot];
+    const int step = 1 << top_level;
+
+    // ---- K2: discretize the chunk's rotated scans into LDS ----------------
+    if (tid < kMaxRotChunk * 4) sh.mm[tid >> 2][tid & 3] = (tid & 1) ? -0x7fffffff : 0x7fffffff;
+    if (tid == 0) sh.range_error = 0;
+    __syncthreads();
+    bool range_error = false;
+    for (int r = 0; r < nrot; ++r) {
+      const float2 q = rot_table[pd.rot_offset + rot0 + r];
       int mnx = 0x7fffffff, mxx = -0x7fffffff, mny = 0x7fffffff, mxy = -0x7fffffff;
-      bool range_error = false;
       for (int i = tid; i < n; i += kSearchThreads) {
         const float* p = points + 3 * (pd.point_offset + i);
         float x, y;
@@ -771,131 +736,60 @@ fast2d_search_v3(const SubmapDesc* __restrict__ submaps,
         }
         mnx = min(mnx, ix); mxx = max(mxx, ix);
         mny = min(mny, iy); mxy = max(mxy, iy);
-        pts[i] = (static_cast<uint32_t>(ix) & 0xffff) | (static_cast<uint32_t>(iy) << 16);
+        pts[r * npad + i] = (static_cast<uint32_t>(ix) & 0xffff) | (static_cast<uint32_t>(iy) << 16);
       }
       mnx = WaveMin(mnx); mxx = WaveMax(mxx); mny = WaveMin(mny); mxy = WaveMax(mxy);
-      if (tid == 0) {
-        sh.mm[0] = mnx; sh.mm[1] = mxx; sh.mm[2] = mny; sh.mm[3] = mxy;
-        sh.range_error = 0;
+      if (lane == 0) {
+        atomicMin(&sh.mm[r][0], mnx); atomicMax(&sh.mm[r][1], mxx);
+        atomicMin(&sh.mm[r][2], mny); atomicMax(&sh.mm[r][3], mxy);
       }
-      __syncthreads();
-      if (lane == 0 && wave != 0) {
-        atomicMin(&sh.mm[0], mnx); atomicMax(&sh.mm[1], mxx);
-        atomicMin(&sh.mm[2], mny); atomicMax(&sh.mm[3], mxy);
-      }
-      if (range_error) sh.range_error = 1;
-      __syncthreads();
-      // ---- ShrinkToFit; virtual root nodes over the top lattice -------------
-      const int step = 1 << top_level;
+    }
+    if (range_error) sh.range_error = 1;
+    __syncthreads();
+    // ---- ShrinkToFit per rotation; root counts ------------------------------
+    if (tid < nrot) {
+      const int r = tid;
+      const int lo_x = min(0, -sh.mm[r][1]), hi_x = max(0, sm.nx - 1 - sh.mm[r][0]);
+      const int lo_y = min(0, -sh.mm[r][3]), hi_y = max(0, sm.ny - 1 - sh.mm[r][2]);
+      const int b0 = max(-pd.num_linear, lo_x), b1 = min(pd.num_linear, hi_x);
+      const int b2 = max(-pd.num_linear, lo_y), b3 = min(pd.num_linear, hi_y);
+      sh.bounds[r][0] = b0; sh.bounds[r][1] = b1; sh.bounds[r][2] = b2; sh.bounds[r][3] = b3;
+      const int tnx = (b1 - b0 + step) / step, tny = (b3 - b2 + step) / step;
+      sh.vny[r] = (tny + 1) >> 1;
+      sh.root_prefix[r + 1] = ((tnx + 1) >> 1) * sh.vny[r];
+    }
+    __syncthreads();
+    if (tid == 0) {
+      if (sh.range_error) atomicOr(&status[pair_index], kStatusRange);
+      sh.root_prefix[0] = 0;
+      for (int r = 0; r < nrot; ++r) sh.root_prefix[r + 1] += sh.root_prefix[r];
+      sh.vnext = 0;
+      sh.sp = 0;
+      sh.best = LoadBest(pair_best);
+      sh.batch_no = 0;
+      sh.nodes = 0;
+      sh.done = 0;
+    }
+    __syncthreads();
+    const int vtotal = Uniform(sh.root_prefix[nrot]);
+
+    // ---- K3/K4: batched best-first DFS over the chunk -----------------------
+    for (;;) {
       if (wave == 0) {
-        int b0 = 0, b1 = 0, b2 = 0, b3 = 0;
-        if (lane == 0 && sh.range_error) atomicOr(&status[pair_index], kStatusRange);
-        const int lo_x = min(0, -sh.mm[1]), hi_x = max(0, sm.nx - 1 - sh.mm[0]);
-        const int lo_y = min(0, -sh.mm[3]), hi_y = max(0, sm.ny - 1 - sh.mm[2]);
-        b0 = max(-pd.num_linear, lo_x);
-        b1 = min(pd.num_linear, hi_x);
-        b2 = max(-pd.num_linear, lo_y);
-        b3 = min(pd.num_linear, hi_y);
-        const int tnx = (b1 - b0 + step) / step, tny = (b3 - b2 + step) / step;
-        if (lane == 0) {
-          sh.bounds[0] = b0; sh.bounds[1] = b1; sh.bounds[2] = b2; sh.bounds[3] = b3;
-          sh.vny = (tny + 1) >> 1;
-          sh.vtotal = ((tnx + 1) >> 1) * sh.vny;
-          sh.vnext = 0;
-          sh.sp = 0;
-          sh.best = LoadBest(pair_best);
-          sh.batch_no = 0;
-        }
-      }
-      __syncthreads();
-      const int min_x = Uniform(sh.bounds[0]), max_x = Uniform(sh.bounds[1]);
-      const int min_y = Uniform(sh.bounds[2]), max_y = Uniform(sh.bounds[3]);
-      // ---- K3/K4: batched best-first DFS -------------------------------------
-      // Virtual root nodes (level top+1, bound "infinite") enter the stack in
-      // chunks of kRootChunk whenever it runs empty.
-      for (;;) {
-        if (wave == 0) {
-          int sp = sh.sp;
-          if (sp == 0 && sh.vnext < sh.vtotal) {
-            const int v0 = sh.vnext, vc = min(kRootChunk, sh.vtotal - v0);
-            for (int k = lane; k < vc; k += 64) {
-              const int v = v0 + vc - 1 - k;  // lowest index on top
-              const int xo = min_x + (v / sh.vny) * 2 * step, yo = min_y + (v % sh.vny) * 2 * step;
-              sh.stack[k] = make_uint2((static_cast<uint32_t>(xo) & 0xffff) |
-                                           (static_cast<uint32_t>(yo) << 16),
-                                       0x3fffffu | (static_cast<uint32_t>(top_level + 1) << 27));
-            }
-            sp = vc;
-            if (lane == 0) sh.vnext = v0 + vc;
-          }
-          if (lane == 0 && (sh.batch_no++ & 7) == 0) {
-            const uint64_t fresh = LoadBest(pair_best);
-            if (fresh > sh.best) sh.best = fresh;
-          }
-          const uint32_t cur_sum = static_cast<uint32_t>(sh.best >> kSumShift);
-          int nodes = 0, lvl = 0;
-          if (sp > 0) {
-            const uint2 top = sh.stack[sp - 1];
-            lvl = static_cast<int>(top.y >> 27);
-            uint2 e = make_uint2(0, 0);
-            bool same = false;
-            if (lane < kBatchNodes && lane < sp) {
-              e = sh.stack[sp - 1 - lane];
-              same = static_cast<int>(e.y >> 27) == lvl;
-            }
-            const unsigned long long diff = __ballot(!same);
-            const int run = static_cast<int>(__ffsll(static_cast<long long>(diff))) - 1;
-            const bool expandable = lane < run && (e.y & 0x3fffff) >= cur_sum;
-            const unsigned long long em = __ballot(expandable);
-            const int ne = __popcll(em);
-            int take = run;  // default: the whole run is pruned
-            if (ne > 0) {
-              nodes = 1 << (31 - __clz(ne));  // largest power of two <= ne
-              // Lane index of the nodes-th expandable entry.
-              unsigned long long m = em;
-              for (int k = 1; k < nodes; ++k) m &= m - 1;
-              take = static_cast<int>(__ffsll(static_cast<long long>(m)));
-              const int rank = __popcll(em & ((1ull << lane) - 1));
-              if (expandable && lane < take) {
-                sh.node_xo[rank] = static_cast<int16_t>(e.x & 0xffff);
-                sh.node_yo[rank] = static_cast<int>(e.x) >> 16;
-              }
-            }
-            sp -= take;
-          }
-          if (lane == 0) {
-            sh.sp = sp;
-            sh.nodes = nodes;
-            sh.level = lvl - 1;
-          }
-        }
-        __syncthreads();
-        const int nodes = Uniform(sh.nodes);
-        const int sp_now = Uniform(sh.sp);
-        const int lvl = Uniform(sh.level);
-        if (nodes == 0) {
-          __syncthreads();
-          if (sp_now == 0) break;
-          continue;
-        }
-        V3Precompute(pts, pre, n, npre, sm, lvl, min_x, min_y);
-        __syncthreads();
-        V3Score(sh, pre, n, sm, lvl, min_x, min_y);
-        __syncthreads();
-        local_cands += 4 * nodes;
-        local_lookups += static_cast<unsigned long long>(4 * nodes) * n;
-        if (tid == 0) { sh.lv_cands[lvl] += 4 * nodes; sh.lv_batches[lvl] += 1; }
-        if (wave == 0) {
-          // Lane = child c of node c/4: (xo,yo), (xo,yo+h), (xo+h,yo), (xo+h,yo+h).
-          const int nd = lane >> 2, c = lane & 3;
+        // (a) Combine the previous batch: prune, record leaves, push survivors.
+        const int pn = sh.nodes;
+        if (pn > 0) {
+          const int lvl = sh.level;
           const int h = 1 << lvl;
-          int sum = 0, xo = 0, yo = 0;
+          const int nd = lane >> 2, c = lane & 3;
+          int sum = 0, xo = 0, yo = 0, r = 0;
           bool exists = false;
-          if (nd < nodes) {
+          if (nd < pn) {
             sum = sh.part[0][nd][c] + sh.part[1][nd][c] + sh.part[2][nd][c] + sh.part[3][nd][c];
+            r = sh.node_rot[nd];
             xo = sh.node_xo[nd] + ((c & 2) ? h : 0);
             yo = sh.node_yo[nd] + ((c & 1) ? h : 0);
-            exists = xo <= max_x && yo <= max_y;
+            exists = xo <= sh.bounds[r][1] && yo <= sh.bounds[r][3];
           }
           const uint64_t cur = sh.best;
           const uint32_t cur_sum = static_cast<uint32_t>(cur >> kSumShift);
@@ -906,7 +800,7 @@ fast2d_search_v3(const SubmapDesc* __restrict__ submaps,
               if (xo < -kOffsetLimit || xo > kOffsetLimit || yo < -kOffsetLimit || yo > kOffsetLimit)
                 atomicOr(&status[pair_index], kStatusRange);
               else
-                key = PackLeafKey(sum, rot, xo, yo);
+                key = PackLeafKey(sum, rot0 + r, xo, yo);
             }
             for (int m = 32; m >= 1; m >>= 1) {
               const uint64_t o = __shfl_xor(key, m, 64);
@@ -927,22 +821,90 @@ fast2d_search_v3(const SubmapDesc* __restrict__ submaps,
               }
             const int kept = __popcll(__ballot(keep));
             const int sp = sh.sp;
-            // Children of sorted position k come from lane j = skey & 0xff.
             const int j = skey & 0xff;
-            const int cx = __shfl(xo, j, 64), cy = __shfl(yo, j, 64);
-            if (lane < kept && sp + kept <= kStack2) {
+            const int sx = __shfl(xo, j, 64), sy = __shfl(yo, j, 64), sr = __shfl(r, j, 64);
+            if (lane < kept && sp + kept <= kStack2)
               sh.stack[sp + kept - 1 - lane] = make_uint2(
-                  (static_cast<uint32_t>(cx) & 0xffff) | (static_cast<uint32_t>(cy) << 16),
-                  V2Entry1(static_cast<int>(skey >> 8), lvl));
-            }
+                  (static_cast<uint32_t>(sx) & 0xffff) | (static_cast<uint32_t>(sy) << 16),
+                  (skey >> 8) | (static_cast<uint32_t>(sr) << 22) | (static_cast<uint32_t>(lvl) << 27));
             if (lane == 0) {
               if (sp + kept > kStack2) atomicOr(&status[pair_index], kStatusRange);
               else sh.sp = sp + kept;
             }
           }
         }
-        __syncthreads();
+        // (b) Refill roots when the stack is empty.
+        int sp = sh.sp;
+        if (sp == 0 && sh.vnext < vtotal) {
+          const int v0 = sh.vnext, vc = min(kRootChunk, vtotal - v0);
+          for (int k = lane; k < vc; k += 64) {
+            const int v = v0 + vc - 1 - k;  // lowest root index on top
+            int r = 0;
+            while (sh.root_prefix[r + 1] <= v) ++r;
+            const int lv = v - sh.root_prefix[r];
+            const int xo = sh.bounds[r][0] + (lv / sh.vny[r]) * 2 * step;
+            const int yo = sh.bounds[r][2] + (lv % sh.vny[r]) * 2 * step;
+            sh.stack[k] = make_uint2((static_cast<uint32_t>(xo) & 0xffff) | (static_cast<uint32_t>(yo) << 16),
+                                     0x3fffffu | (static_cast<uint32_t>(r) << 22) |
+                                         (static_cast<uint32_t>(top_level + 1) << 27));
+          }
+          sp = vc;
+          if (lane == 0) sh.vnext = v0 + vc;
+        }
+        // (c) Pop the next batch: up to 16 same-level nodes, best first.
+        if (lane == 0 && (sh.batch_no++ & 7) == 0) {
+          const uint64_t fresh = LoadBest(pair_best);
+          if (fresh > sh.best) sh.best = fresh;
+        }
+        const uint32_t cur_sum = static_cast<uint32_t>(sh.best >> kSumShift);
+        int nodes = 0, lvl = 0;
+        if (sp > 0) {
+          lvl = static_cast<int>(sh.stack[sp - 1].y >> 27);
+          uint2 ent = make_uint2(0, 0);
+          bool same = false;
+          if (lane < kBatchNodes && lane < sp) {
+            ent = sh.stack[sp - 1 - lane];
+            same = static_cast<int>(ent.y >> 27) == lvl;
+          }
+          const unsigned long long diff = __ballot(!same);
+          const int run = static_cast<int>(__ffsll(static_cast<long long>(diff))) - 1;
+          const bool expandable = lane < run && (ent.y & 0x3fffff) >= cur_sum;
+          const unsigned long long em = __ballot(expandable);
+          const int ne = __popcll(em);
+          int take = run;
+          if (ne > 0) {
+            nodes = 1 << (31 - __clz(ne));
+            unsigned long long m = em;
+            for (int k = 1; k < nodes; ++k) m &= m - 1;
+            take = static_cast<int>(__ffsll(static_cast<long long>(m)));
+            const int rank = __popcll(em & ((1ull << lane) - 1));
+            if (expandable && lane < take) {
+              sh.node_xo[rank] = static_cast<int16_t>(ent.x & 0xffff);
+              sh.node_yo[rank] = static_cast<int>(ent.x) >> 16;
+              sh.node_rot[rank] = (ent.y >> 22) & 0x1f;
+            }
+          }
+          sp -= take;
+        }
+        if (lane == 0) {
+          sh.sp = sp;
+          sh.nodes = nodes;
+          sh.level = lvl - 1;
+          sh.done = (nodes == 0 && sp == 0 && sh.vnext >= vtotal) ? 1 : 0;
+        }
       }
+      __syncthreads();
+      const int nodes = Uniform(sh.nodes);
+      const int done = Uniform(sh.done);
+      if (done) break;
+      if (nodes > 0) {
+        const int lvl = Uniform(sh.level);
+        V4Score(sh, pts, npad, n, sm, lvl);
+        local_cands += 4 * nodes;
+        local_lookups += static_cast<unsigned long long>(4 * nodes) * n;
+        if (tid == 0) { sh.lv_cands[lvl] += 4 * nodes; sh.lv_batches[lvl] += 1; }
+      }
+      __syncthreads();
     }
   }
   if (stats && tid == 0) {
@@ -1045,10 +1007,10 @@ hipError_t LaunchFast2dSearch(int grid, size_t dyn_lds, hipStream_t st, const Su
   return hipGetLastError();
 }
 
-hipError_t LaunchPyramidPolyphase(const uint8_t* level, int wnx, int wny, int log_h, int pw, int ph,
-                                 uint8_t* out, int total, hipStream_t st) {
-  hipLaunchKernelGGL(pyramid_polyphase, dim3((std::max(total, 16) + 255) / 256), dim3(256), 0, st,
-                     level, wnx, wny, log_h, pw, ph, out, total);
+hipError_t LaunchPyramidQuad(const uint8_t* level, int wnx, int wny, int h, uint32_t* out, int qw,
+                             int qh, hipStream_t st) {
+  hipLaunchKernelGGL(pyramid_quad, dim3((qw + 255) / 256, qh), dim3(256), 0, st, level, wnx, wny, h,
+                     out, qw, qh);
   return hipGetLastError();
 }
 
@@ -1056,9 +1018,9 @@ hipError_t LaunchFast2dSearchV2(int grid, size_t dyn_lds, hipStream_t st, const 
                                 const PairDesc* pairs, const float* points, const float2* rot_table,
                                 const WorkQueues2& queues, unsigned long long* counters,
                                 uint64_t* best, int32_t* status, unsigned long long* stats,
-                                int max_points) {
-  hipLaunchKernelGGL(fast2d_search_v3, dim3(grid), dim3(kSearchThreads), dyn_lds, st, submaps, pairs,
-                     points, rot_table, queues, counters, best, status, stats, max_points);
+                                int npad) {
+  hipLaunchKernelGGL(fast2d_search_v4, dim3(grid), dim3(kSearchThreads), dyn_lds, st, submaps, pairs,
+                     points, rot_table, queues, counters, best, status, stats, npad);
   return hipGetLastError();
 }
 
