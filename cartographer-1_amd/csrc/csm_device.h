@@ -41,6 +41,11 @@ struct SubmapDesc {
   // of the 2x2 children whose child (0,0) is at wide cell (X' - h, Y' - h):
   // byte0 (0,0), byte1 (0,h), byte2 (h,0), byte3 (h,h); 0 outside the grid.
   const uint32_t* quad[kMaxLevels];
+  const uint8_t* pyramid_base;      // one allocation: row-major + quad levels
+  int32_t pyramid_bytes;
+  int32_t quad_off[kMaxLevels];     // byte offset of quad level d from the base
+  int32_t quad_pws[kMaxLevels];     // polyphase plane row stride (dwords)
+  int32_t quad_pph[kMaxLevels];     // polyphase plane rows
   int32_t quad_w[kMaxLevels];
   int32_t quad_h[kMaxLevels];
   int32_t quad_bytes[kMaxLevels];

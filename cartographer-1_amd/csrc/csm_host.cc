@@ -300,6 +300,8 @@ int RunBatch(csm_context* ctx, csm_fast2d* const* submaps, int32_t num_submaps,
     wq2.chunk_prefix = wq.chunk_prefix;
     wq2.block_first = ctx->blocks.as<int32_t>();
     const size_t dyn_lds = static_cast<size_t>(rc) * max_npad * 4;
+    const char* mixed_env = std::getenv("CSM_MIXED_LEVELS");
+    const int mixed = mixed_env ? std::atoi(mixed_env) : 1;
     const int per_cu = std::max(1, std::min(8, static_cast<int>((160 * 1024) / (dyn_lds + 10 * 1024))));
     const int grid = static_cast<int>(std::min<int64_t>(static_cast<int64_t>(ctx->num_cus) * per_cu,
                                                         std::max<int64_t>(total_chunks, 1)));
@@ -308,7 +310,7 @@ int RunBatch(csm_context* ctx, csm_fast2d* const* submaps, int32_t num_submaps,
                                  ctx->rot_table.as<float2>(), wq2,
                                  ctx->counters.as<unsigned long long>(), ctx->best.as<uint64_t>(),
                                  ctx->status.as<int32_t>(), ctx->stats.as<unsigned long long>(),
-                                 max_npad));
+                                 max_npad, mixed));
   } else {
     const size_t dyn_lds = static_cast<size_t>(rc) * max_npad * sizeof(uint32_t);
     const int grid = static_cast<int>(std::min<int64_t>(static_cast<int64_t>(ctx->num_cus) * 4,
@@ -506,17 +508,23 @@ int csm_fast2d_create(csm_context* ctx, const csm_map_limits* limits,
     const int h = 1 << l;
     d.quad_w[l] = d.wide_nx[l] + h;
     d.quad_h[l] = d.wide_ny[l] + h;
-    const size_t qb = static_cast<size_t>(d.quad_w[l]) * d.quad_h[l] * 4;
+    d.quad_pws[l] = (d.quad_w[l] + 2 * h - 1) / (2 * h);
+    d.quad_pph[l] = (d.quad_h[l] + 2 * h - 1) / (2 * h);
+    const size_t qb = static_cast<size_t>(2 * h) * (2 * h) * d.quad_pws[l] * d.quad_pph[l] * 4;
     if (qb > 0x7fffff00u) return CSM_ERANGE;
     d.quad_bytes[l] = static_cast<int32_t>(qb);
     qoffs[l] = total;
     total += (qb + 255) & ~size_t(255);
   }
+  if (total > 0x7fffff00u) return CSM_ERANGE;
   int rc;
   if ((rc = m->pyramid.Reserve(total))) return rc;
+  d.pyramid_base = m->pyramid.as<uint8_t>();
+  d.pyramid_bytes = static_cast<int32_t>(total);
   for (int l = 0; l < depth; ++l) {
     d.level[l] = m->pyramid.as<uint8_t>() + offs[l];
     d.quad[l] = reinterpret_cast<const uint32_t*>(m->pyramid.as<uint8_t>() + qoffs[l]);
+    d.quad_off[l] = static_cast<int32_t>(qoffs[l]);
   }
 
   DevBuf dcells, dq;
@@ -534,8 +542,9 @@ int csm_fast2d_create(csm_context* ctx, const csm_map_limits* limits,
                                 1 << (l - 1), st));
   }
   for (int l = 0; l < depth; ++l)
-    CSM_HIP(LaunchPyramidQuad(d.level[l], d.wide_nx[l], d.wide_ny[l], 1 << l,
-                              const_cast<uint32_t*>(d.quad[l]), d.quad_w[l], d.quad_h[l], st));
+    CSM_HIP(LaunchPyramidQuad(d.level[l], d.wide_nx[l], d.wide_ny[l], l,
+                              const_cast<uint32_t*>(d.quad[l]), d.quad_w[l], d.quad_h[l],
+                              d.quad_pws[l], d.quad_pph[l], d.quad_bytes[l] / 4, st));
   CSM_HIP(hipStreamSynchronize(st));  // dcells/dq are freed on return
   *out = m.release();
   return CSM_OK;

@@ -537,21 +537,35 @@ constexpr int kRootChunk = 192;  // virtual roots pushed at a time
 
 // ---------------------------------------------------------------- K1c ------
 
-// Quad layout of level d (h = 2^d): dword (X', Y') over (wnx + h) x (wny + h)
-// packs the four children of a node whose child (0,0) sits at wide cell
-// (X, Y) = (X' - h, Y' - h): byte0 G(X, Y), byte1 G(X, Y+h), byte2 G(X+h, Y),
-// byte3 G(X+h, Y+h); G = 0 outside the wide grid.
-__global__ void pyramid_quad(const uint8_t* __restrict__ level, int wnx, int wny, int h,
-                             uint32_t* __restrict__ out, int qw, int qh) {
-  const int xq = blockIdx.x * blockDim.x + threadIdx.x;
-  const int yq = blockIdx.y;
-  if (xq >= qw) return;
-  const int X = xq - h, Y = yq - h;
-  auto g = [&](int a, int b) -> uint32_t {
-    return (a >= 0 && b >= 0 && a < wnx && b < wny) ? level[static_cast<size_t>(b) * wnx + a] : 0u;
-  };
-  out[static_cast<size_t>(yq) * qw + xq] =
-      g(X, Y) | (g(X, Y + h) << 8) | (g(X + h, Y) << 16) | (g(X + h, Y + h) << 24);
+// Quad layout of level d (h = 2^d): the dword for quad cell (X', Y'),
+// X' < qw = wnx + h, Y' < qh = wny + h, packs the children values of a node
+// whose child (0,0) sits at wide cell (X, Y) = (X' - h, Y' - h):
+// byte0 G(X, Y), byte1 G(X, Y+h), byte2 G(X+h, Y), byte3 G(X+h, Y+h);
+// G = 0 outside the wide grid. Cells are stored polyphase with period
+// P = 2h: plane (X' mod P, Y' mod P), entry (X' / P, Y' / P), row stride pws,
+// plane size pws * pph dwords. Same-level nodes of one rotation sit on one
+// P-lattice, so one point's lookups by sibling nodes are adjacent dwords.
+__global__ void pyramid_quad(const uint8_t* __restrict__ level, int wnx, int wny, int log_h,
+                             uint32_t* __restrict__ out, int qw, int qh, int pws, int pph,
+                             int total) {
+  const int o = blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= total) return;
+  const int h = 1 << log_h;
+  const int s = log_h + 1, p = 2 * h;
+  const int ps = pws * pph;
+  const int pi = o / ps, k = o - pi * ps;
+  const int fx = pi & (p - 1), fy = pi >> s;
+  const int ky = k / pws, kx = k - ky * pws;
+  const int xq = (kx << s) + fx, yq = (ky << s) + fy;
+  uint32_t v = 0;
+  if (xq < qw && yq < qh) {
+    const int X = xq - h, Y = yq - h;
+    auto g = [&](int a, int b) -> uint32_t {
+      return (a >= 0 && b >= 0 && a < wnx && b < wny) ? level[static_cast<size_t>(b) * wnx + a] : 0u;
+    };
+    v = g(X, Y) | (g(X, Y + h) << 8) | (g(X + h, Y) << 16) | (g(X + h, Y + h) << 24);
+  }
+  out[o] = v;
 }
 
 // ---------------------------------------------------------------- K2-K4 v4 -
@@ -570,8 +584,8 @@ constexpr int kMaxRotChunk = 16;
 struct V4Shared {
   uint2 stack[kStack2];  // w0: xo | yo << 16; w1: sum | rot << 22 | level << 27
   int part[kWaves][kBatchNodes][4];
-  int node_xo[kBatchNodes], node_yo[kBatchNodes], node_rot[kBatchNodes];
-  int nodes, level, done;
+  int node_xo[kBatchNodes], node_yo[kBatchNodes], node_rot[kBatchNodes], node_level[kBatchNodes];
+  int nodes, done;
   int item_pair, item_chunk, queue;
   int sp;
   uint64_t best;
@@ -586,16 +600,21 @@ struct V4Shared {
 };
 
 __device__ __forceinline__ void V4Score(V4Shared& sh, const uint32_t* pts, int npad, int n,
-                                        const SubmapDesc& sm, int level) {
+                                        const SubmapDesc& sm) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nodes = Uniform(sh.nodes);
   const int groups = 64 / nodes;
   const int node = lane & (nodes - 1);
   const int g = lane / nodes;
+  // Each node scores its children at its own child level: one descriptor
+  // spans the whole pyramid, the level is a per-lane byte offset.
+  const int level = sh.node_level[node] - 1;
   const int h = 1 << level;
   const int qw = sm.quad_w[level], qh = sm.quad_h[level];
-  const __amdgpu_buffer_rsrc_t rsrc =
-      LevelRsrc(reinterpret_cast<const uint8_t*>(sm.quad[level]), Uniform(sm.quad_bytes[level]));
+  const int qoff = sm.quad_off[level];
+  const int sft = level + 1, pmask = (2 << level) - 1;
+  const int pws4 = sm.quad_pws[level] * 4, ps4 = sm.quad_pws[level] * sm.quad_pph[level] * 4;
+  const __amdgpu_buffer_rsrc_t rsrc = LevelRsrc(sm.pyramid_base, Uniform(sm.pyramid_bytes));
   const uint32_t* P = pts + sh.node_rot[node] * npad;
   const int cx = sh.node_xo[node] + (h - 1) + h;
   const int cy = sh.node_yo[node] + (h - 1) + h;
@@ -614,7 +633,9 @@ __device__ __forceinline__ void V4Score(V4Shared& sh, const uint32_t* pts, int n
       const int Y = (static_cast<int>(p) >> 16) + cy;
       const bool valid = static_cast<unsigned>(X) < static_cast<unsigned>(qw) &&
                          static_cast<unsigned>(Y) < static_cast<unsigned>(qh);
-      ad[u] = valid ? static_cast<int>((__umul24(Y, qw) + X) << 2) : kOOB;
+      const int a = __umul24((((Y & pmask) << sft) | (X & pmask)), ps4) + qoff;
+      const int b = __umul24(Y >> sft, pws4) + a;
+      ad[u] = valid ? ((X >> sft) << 2) + b : kOOB;
     }
     uint32_t v[U];
 #pragma unroll
@@ -635,8 +656,10 @@ __device__ __forceinline__ void V4Score(V4Shared& sh, const uint32_t* pts, int n
     const int Y = (static_cast<int>(p) >> 16) + cy;
     const bool valid = idx < e && static_cast<unsigned>(X) < static_cast<unsigned>(qw) &&
                        static_cast<unsigned>(Y) < static_cast<unsigned>(qh);
-    const uint32_t vv = __builtin_amdgcn_raw_buffer_load_b32(
-        rsrc, valid ? static_cast<int>((__umul24(Y, qw) + X) << 2) : kOOB, 0, 0);
+    const int a = __umul24((((Y & pmask) << sft) | (X & pmask)), ps4) + qoff;
+    const int b = __umul24(Y >> sft, pws4) + a;
+    const uint32_t vv = __builtin_amdgcn_raw_buffer_load_b32(rsrc, valid ? ((X >> sft) << 2) + b : kOOB,
+                                                             0, 0);
     a0 = __builtin_amdgcn_udot4(vv, 0x00000001u, a0, false);
     a1 = __builtin_amdgcn_udot4(vv, 0x00000100u, a1, false);
     a2 = __builtin_amdgcn_udot4(vv, 0x00010000u, a2, false);
@@ -666,7 +689,7 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
                  uint64_t* __restrict__ best,
                  int32_t* __restrict__ status,
                  unsigned long long* __restrict__ stats,
-                 int npad) {
+                 int npad, int mixed_levels) {
   extern __shared__ __align__(16) uint32_t pts[];  // rot_chunk * npad
   __shared__ V4Shared sh;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -779,12 +802,12 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
         // (a) Combine the previous batch: prune, record leaves, push survivors.
         const int pn = sh.nodes;
         if (pn > 0) {
-          const int lvl = sh.level;
-          const int h = 1 << lvl;
           const int nd = lane >> 2, c = lane & 3;
-          int sum = 0, xo = 0, yo = 0, r = 0;
+          int sum = 0, xo = 0, yo = 0, r = 0, clvl = 0;
           bool exists = false;
           if (nd < pn) {
+            clvl = sh.node_level[nd] - 1;
+            const int h = 1 << clvl;
             sum = sh.part[0][nd][c] + sh.part[1][nd][c] + sh.part[2][nd][c] + sh.part[3][nd][c];
             r = sh.node_rot[nd];
             xo = sh.node_xo[nd] + ((c & 2) ? h : 0);
@@ -794,43 +817,47 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
           const uint64_t cur = sh.best;
           const uint32_t cur_sum = static_cast<uint32_t>(cur >> kSumShift);
           const bool keep = exists && sum > s_min && static_cast<uint32_t>(sum) >= cur_sum;
-          if (lvl == 0) {
-            uint64_t key = 0;
-            if (keep) {
-              if (xo < -kOffsetLimit || xo > kOffsetLimit || yo < -kOffsetLimit || yo > kOffsetLimit)
-                atomicOr(&status[pair_index], kStatusRange);
-              else
-                key = PackLeafKey(sum, rot0 + r, xo, yo);
+          // Leaves (child level 0) update the incumbent.
+          uint64_t key = 0;
+          if (keep && clvl == 0) {
+            if (xo < -kOffsetLimit || xo > kOffsetLimit || yo < -kOffsetLimit || yo > kOffsetLimit)
+              atomicOr(&status[pair_index], kStatusRange);
+            else
+              key = PackLeafKey(sum, rot0 + r, xo, yo);
+          }
+          for (int m = 32; m >= 1; m >>= 1) {
+            const uint64_t o = __shfl_xor(key, m, 64);
+            key = o > key ? o : key;
+          }
+          if (lane == 0 && key > cur) {
+            atomicMax(reinterpret_cast<unsigned long long*>(pair_best), key);
+            sh.best = key;
+          }
+          // Inner survivors: deepest level first, then best bound, on top.
+          const bool push = keep && clvl > 0;
+          uint32_t skey = push ? ((static_cast<uint32_t>(15 - clvl) << 28) |
+                                  (static_cast<uint32_t>(sum) << 6) | static_cast<uint32_t>(lane))
+                               : 0u;
+          for (int k = 2; k <= 64; k <<= 1)
+            for (int jj = k >> 1; jj >= 1; jj >>= 1) {
+              const uint32_t other = __shfl_xor(skey, jj, 64);
+              const bool up = ((lane & k) == 0), lower = ((lane & jj) == 0);
+              const uint32_t hi_v = skey > other ? skey : other, lo_v = skey > other ? other : skey;
+              skey = (lower == up) ? hi_v : lo_v;
             }
-            for (int m = 32; m >= 1; m >>= 1) {
-              const uint64_t o = __shfl_xor(key, m, 64);
-              key = o > key ? o : key;
-            }
-            if (lane == 0 && key > cur) {
-              atomicMax(reinterpret_cast<unsigned long long*>(pair_best), key);
-              sh.best = key;
-            }
-          } else {
-            uint32_t skey = keep ? ((static_cast<uint32_t>(sum) << 8) | static_cast<uint32_t>(lane)) : 0u;
-            for (int k = 2; k <= 64; k <<= 1)
-              for (int jj = k >> 1; jj >= 1; jj >>= 1) {
-                const uint32_t other = __shfl_xor(skey, jj, 64);
-                const bool up = ((lane & k) == 0), lower = ((lane & jj) == 0);
-                const uint32_t hi_v = skey > other ? skey : other, lo_v = skey > other ? other : skey;
-                skey = (lower == up) ? hi_v : lo_v;
-              }
-            const int kept = __popcll(__ballot(keep));
-            const int sp = sh.sp;
-            const int j = skey & 0xff;
-            const int sx = __shfl(xo, j, 64), sy = __shfl(yo, j, 64), sr = __shfl(r, j, 64);
-            if (lane < kept && sp + kept <= kStack2)
-              sh.stack[sp + kept - 1 - lane] = make_uint2(
-                  (static_cast<uint32_t>(sx) & 0xffff) | (static_cast<uint32_t>(sy) << 16),
-                  (skey >> 8) | (static_cast<uint32_t>(sr) << 22) | (static_cast<uint32_t>(lvl) << 27));
-            if (lane == 0) {
-              if (sp + kept > kStack2) atomicOr(&status[pair_index], kStatusRange);
-              else sh.sp = sp + kept;
-            }
+          const int kept = __popcll(__ballot(push));
+          const int sp = sh.sp;
+          const int j = skey & 63;
+          const int sx = __shfl(xo, j, 64), sy = __shfl(yo, j, 64), sr = __shfl(r, j, 64);
+          const int ssum = __shfl(sum, j, 64), sl = __shfl(clvl, j, 64);
+          if (lane < kept && sp + kept <= kStack2)
+            sh.stack[sp + kept - 1 - lane] = make_uint2(
+                (static_cast<uint32_t>(sx) & 0xffff) | (static_cast<uint32_t>(sy) << 16),
+                static_cast<uint32_t>(ssum) | (static_cast<uint32_t>(sr) << 22) |
+                    (static_cast<uint32_t>(sl) << 27));
+          if (lane == 0) {
+            if (sp + kept > kStack2) atomicOr(&status[pair_index], kStatusRange);
+            else sh.sp = sp + kept;
           }
         }
         // (b) Refill roots when the stack is empty.
@@ -857,21 +884,25 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
           if (fresh > sh.best) sh.best = fresh;
         }
         const uint32_t cur_sum = static_cast<uint32_t>(sh.best >> kSumShift);
-        int nodes = 0, lvl = 0;
+        int nodes = 0;
         if (sp > 0) {
-          lvl = static_cast<int>(sh.stack[sp - 1].y >> 27);
+          // Up to 16 entries from the top (any level); expand a power of two
+          // of the unpruned ones, discard pruned ones passed over.
           uint2 ent = make_uint2(0, 0);
-          bool same = false;
-          if (lane < kBatchNodes && lane < sp) {
-            ent = sh.stack[sp - 1 - lane];
-            same = static_cast<int>(ent.y >> 27) == lvl;
+          bool in = lane < kBatchNodes && lane < sp;
+          if (in) ent = sh.stack[sp - 1 - lane];
+          if (!mixed_levels) {
+            // Same-level batches: stop at the first entry of another level.
+            const int top_lvl = static_cast<int>(sh.stack[sp - 1].y >> 27);
+            const unsigned long long diff = __ballot(!(in && static_cast<int>(ent.y >> 27) == top_lvl));
+            const int run = static_cast<int>(__ffsll(static_cast<long long>(diff))) - 1;
+            in = lane < run;
           }
-          const unsigned long long diff = __ballot(!same);
-          const int run = static_cast<int>(__ffsll(static_cast<long long>(diff))) - 1;
-          const bool expandable = lane < run && (ent.y & 0x3fffff) >= cur_sum;
+          const unsigned long long inm = __ballot(in);
+          const bool expandable = in && (ent.y & 0x3fffff) >= cur_sum;
           const unsigned long long em = __ballot(expandable);
           const int ne = __popcll(em);
-          int take = run;
+          int take = __popcll(inm);
           if (ne > 0) {
             nodes = 1 << (31 - __clz(ne));
             unsigned long long m = em;
@@ -882,6 +913,7 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
               sh.node_xo[rank] = static_cast<int16_t>(ent.x & 0xffff);
               sh.node_yo[rank] = static_cast<int>(ent.x) >> 16;
               sh.node_rot[rank] = (ent.y >> 22) & 0x1f;
+              sh.node_level[rank] = static_cast<int>(ent.y >> 27);
             }
           }
           sp -= take;
@@ -889,7 +921,6 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
         if (lane == 0) {
           sh.sp = sp;
           sh.nodes = nodes;
-          sh.level = lvl - 1;
           sh.done = (nodes == 0 && sp == 0 && sh.vnext >= vtotal) ? 1 : 0;
         }
       }
@@ -898,11 +929,14 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
       const int done = Uniform(sh.done);
       if (done) break;
       if (nodes > 0) {
-        const int lvl = Uniform(sh.level);
-        V4Score(sh, pts, npad, n, sm, lvl);
+        V4Score(sh, pts, npad, n, sm);
         local_cands += 4 * nodes;
         local_lookups += static_cast<unsigned long long>(4 * nodes) * n;
-        if (tid == 0) { sh.lv_cands[lvl] += 4 * nodes; sh.lv_batches[lvl] += 1; }
+        if (tid < nodes) {
+          const int cl = sh.node_level[tid] - 1;
+          atomicAdd(&sh.lv_cands[cl], 4ull);
+          if (tid == 0) atomicAdd(&sh.lv_batches[cl], 1ull);
+        }
       }
       __syncthreads();
     }
@@ -1007,10 +1041,10 @@ hipError_t LaunchFast2dSearch(int grid, size_t dyn_lds, hipStream_t st, const Su
   return hipGetLastError();
 }
 
-hipError_t LaunchPyramidQuad(const uint8_t* level, int wnx, int wny, int h, uint32_t* out, int qw,
-                             int qh, hipStream_t st) {
-  hipLaunchKernelGGL(pyramid_quad, dim3((qw + 255) / 256, qh), dim3(256), 0, st, level, wnx, wny, h,
-                     out, qw, qh);
+hipError_t LaunchPyramidQuad(const uint8_t* level, int wnx, int wny, int log_h, uint32_t* out,
+                             int qw, int qh, int pws, int pph, int total, hipStream_t st) {
+  hipLaunchKernelGGL(pyramid_quad, dim3((total + 255) / 256), dim3(256), 0, st, level, wnx, wny,
+                     log_h, out, qw, qh, pws, pph, total);
   return hipGetLastError();
 }
 
@@ -1018,9 +1052,9 @@ hipError_t LaunchFast2dSearchV2(int grid, size_t dyn_lds, hipStream_t st, const 
                                 const PairDesc* pairs, const float* points, const float2* rot_table,
                                 const WorkQueues2& queues, unsigned long long* counters,
                                 uint64_t* best, int32_t* status, unsigned long long* stats,
-                                int npad) {
+                                int npad, int mixed_levels) {
   hipLaunchKernelGGL(fast2d_search_v4, dim3(grid), dim3(kSearchThreads), dyn_lds, st, submaps, pairs,
-                     points, rot_table, queues, counters, best, status, stats, npad);
+                     points, rot_table, queues, counters, best, status, stats, npad, mixed_levels);
   return hipGetLastError();
 }
 

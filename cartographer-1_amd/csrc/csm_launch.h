@@ -16,13 +16,13 @@ hipError_t LaunchFast2dSearch(int grid, size_t dyn_lds, hipStream_t st, const Su
                               const PairDesc* pairs, const float* points, const float2* rot_table,
                               const WorkQueues& queues, unsigned long long* counters,
                               uint64_t* best, int32_t* status, unsigned long long* stats);
-hipError_t LaunchPyramidQuad(const uint8_t* level, int wnx, int wny, int h, uint32_t* out, int qw,
-                             int qh, hipStream_t st);
+hipError_t LaunchPyramidQuad(const uint8_t* level, int wnx, int wny, int log_h, uint32_t* out,
+                             int qw, int qh, int pws, int pph, int total, hipStream_t st);
 hipError_t LaunchFast2dSearchV2(int grid, size_t dyn_lds, hipStream_t st, const SubmapDesc* submaps,
                                 const PairDesc* pairs, const float* points, const float2* rot_table,
                                 const WorkQueues2& queues, unsigned long long* counters,
                                 uint64_t* best, int32_t* status, unsigned long long* stats,
-                                int npad);
+                                int npad, int mixed_levels);
 hipError_t LaunchRt2dScore(dim3 grid, int block, size_t dyn_lds, hipStream_t st, const float* prob,
                            int nx, int ny, double max_x, double max_y, double res,
                            const float* points, int n, const float2* rot_table, float pre_w,
