@@ -1,0 +1,229 @@
+"""ConstraintBuilder2D — the caller of the scan-matching hot path, over the
+batched C-ABI (Python mirror of ``include/cartographer_amd/constraint_builder_2d.h``).
+
+Follows reference ``mapping/internal/constraints/constraint_builder_2d.cc``:
+
+* ``MaybeAddConstraint`` (:77-112): drop pairs farther than
+  ``max_constraint_distance``, then one ``FixedRatioSampler`` per submap
+  (``common/fixed_ratio_sampler.cc:32-39``) decides; the search starts at
+  ``ComputeSubmapPose(submap) * initial_relative_pose`` (:195-197).
+* ``MaybeAddGlobalConstraint`` (:114-137): ``MatchFullSubmap`` with
+  ``global_localization_min_score`` (:208-222).
+* ``NotifyEndOfNode`` (:139-151) / ``GetNumFinishedNodes`` (:302-305): a node
+  is finished once its pairs have been searched.
+* ``WhenDone`` (:153-163, ``RunWhenDoneCallback`` :279-300): constraints in
+  submission order, failed searches dropped.
+* ``DeleteScanMatcher`` (:307-316) and the per-submap matcher cache
+  (``DispatchScanMatcherConstruction`` :165-186).
+* Constraint pose ``ComputeSubmapPose(submap).inverse() * pose_estimate``
+  (:251-252), tagged INTER_SUBMAP with the loop-closure weights (:253-257).
+
+Instead of one ``common::Task`` per pair, the pending pairs are searched as one
+GPU batch (``match_batch``) when a node ends, or once ``flush_pairs`` pairs are
+pending. The Ceres refinement (:245-249) is outside the hot path.
+"""
+
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional, Tuple
+
+import numpy as np
+
+from . import (CSM_OK, Context, FastCorrelativeScanMatcher2D,
+               FastCorrelativeScanMatcherOptions2D, ProbabilityGrid, ScanSet, _f32_points,
+               default_context, make_pairs, match_batch)
+
+
+def rigid2d_compose(a, b):
+    """transform::Rigid2d operator* (rigid_transform.h:90-96)."""
+    c, s = math.cos(a[2]), math.sin(a[2])
+    return (c * b[0] - s * b[1] + a[0], s * b[0] + c * b[1] + a[1], a[2] + b[2])
+
+
+def rigid2d_inverse(a):
+    """transform::Rigid2d::inverse (rigid_transform.h:74-78)."""
+    c, s = math.cos(-a[2]), math.sin(-a[2])
+    return (-(c * a[0] - s * a[1]), -(s * a[0] + c * a[1]), -a[2])
+
+
+class FixedRatioSampler:
+    """common/fixed_ratio_sampler.cc:32-39."""
+
+    def __init__(self, ratio: float):
+        if not (0.0 <= ratio <= 1.0):  # fixed_ratio_sampler.cc:25-28
+            raise ValueError("ratio must be within [0, 1]")
+        self.ratio = ratio
+        self.num_pulses = 0
+        self.num_samples = 0
+
+    def Pulse(self) -> bool:
+        self.num_pulses += 1
+        if self.num_samples / self.num_pulses < self.ratio:
+            self.num_samples += 1
+            return True
+        return False
+
+
+@dataclass
+class Submap2D:
+    """What the builder reads of a Submap2D: its grid and local pose
+    (ComputeSubmapPose = Project2D(local_pose), constraint_builder_2d.cc:55-57)."""
+    grid: ProbabilityGrid
+    local_pose: Tuple[float, float, float] = (0.0, 0.0, 0.0)
+
+
+@dataclass
+class ConstraintBuilderOptions:
+    """proto::ConstraintBuilderOptions (constraint_builder_options.proto:24-59);
+    defaults from configuration_files/pose_graph.lua:17-29."""
+    sampling_ratio: float = 0.3
+    max_constraint_distance: float = 15.0
+    min_score: float = 0.55
+    global_localization_min_score: float = 0.6
+    loop_closure_translation_weight: float = 1.1e4
+    loop_closure_rotation_weight: float = 1e5
+    fast_correlative_scan_matcher_options: FastCorrelativeScanMatcherOptions2D = field(
+        default_factory=FastCorrelativeScanMatcherOptions2D)
+    flush_pairs: int = 0  # 0: search each node's pairs when the node ends
+
+
+@dataclass
+class Constraint:
+    """PoseGraphInterface::Constraint (pose_graph_interface.h:36-53), 2D pose."""
+    submap_id: Tuple[int, int]
+    node_id: Tuple[int, int]
+    relative_pose: Tuple[float, float, float]
+    translation_weight: float
+    rotation_weight: float
+    tag: str = "INTER_SUBMAP"
+    score: float = 0.0
+
+
+@dataclass
+class _Pending:
+    submap_id: Tuple[int, int]
+    submap: Submap2D
+    node_id: Tuple[int, int]
+    cloud: np.ndarray
+    full: bool
+    initial: Tuple[float, float, float]
+    slot: int
+
+
+class ConstraintBuilder2D:
+    def __init__(self, options: ConstraintBuilderOptions, context: Optional[Context] = None):
+        self.options = options
+        self.context = context or default_context()
+        self._matchers: Dict[Tuple[int, int], FastCorrelativeScanMatcher2D] = {}
+        self._samplers: Dict[Tuple[int, int], FixedRatioSampler] = {}
+        self._constraints: List[Optional[Constraint]] = []
+        self._pending: List[_Pending] = []
+        self._started_nodes = 0
+        self._finished_nodes = 0
+        # Metrics (constraint_builder_2d.cc:46-53).
+        self.constraints_searched = 0
+        self.constraints_found = 0
+        self.global_constraints_searched = 0
+        self.global_constraints_found = 0
+        self.constraint_scores: List[float] = []
+        self.global_constraint_scores: List[float] = []
+
+    # -- public interface (constraint_builder_2d.h:63-110) ------------------
+    def MaybeAddConstraint(self, submap_id, submap: Submap2D, node_id, cloud,
+                           initial_relative_pose):
+        if math.hypot(initial_relative_pose[0], initial_relative_pose[1]) > \
+                self.options.max_constraint_distance:
+            return
+        sampler = self._samplers.setdefault(tuple(submap_id),
+                                            FixedRatioSampler(self.options.sampling_ratio))
+        if not sampler.Pulse():
+            return
+        self._enqueue(submap_id, submap, node_id, cloud, False,
+                      rigid2d_compose(submap.local_pose, initial_relative_pose))
+
+    def MaybeAddGlobalConstraint(self, submap_id, submap: Submap2D, node_id, cloud):
+        self._enqueue(submap_id, submap, node_id, cloud, True, (0.0, 0.0, 0.0))
+
+    def NotifyEndOfNode(self):
+        self._started_nodes += 1
+        if len(self._pending) >= self.options.flush_pairs:
+            self._flush()
+
+    def WhenDone(self, callback: Callable[[List[Constraint]], None]):
+        self._flush()
+        result = [c for c in self._constraints if c is not None]
+        self._constraints = []
+        callback(result)
+
+    def GetNumFinishedNodes(self) -> int:
+        return self._finished_nodes
+
+    def DeleteScanMatcher(self, submap_id):
+        m = self._matchers.pop(tuple(submap_id), None)
+        if m is not None:
+            m.close()
+        self._samplers.pop(tuple(submap_id), None)
+
+    @property
+    def num_submap_scan_matchers(self) -> int:  # kNumSubmapScanMatchersMetric
+        return len(self._matchers)
+
+    # -- internals ----------------------------------------------------------
+    def _enqueue(self, submap_id, submap, node_id, cloud, full, initial):
+        key = tuple(submap_id)
+        if key not in self._matchers:
+            self._matchers[key] = FastCorrelativeScanMatcher2D(
+                submap.grid, self.options.fast_correlative_scan_matcher_options, self.context)
+        self._constraints.append(None)
+        self._pending.append(_Pending(key, submap, tuple(node_id), cloud, full,
+                                      tuple(initial), len(self._constraints) - 1))
+
+    def _flush(self):
+        pending, self._pending = self._pending, []
+        if pending:
+            matchers, slot_of, clouds, scan_of = [], {}, [], {}
+            submap_idx, scan_idx = [], []
+            for p in pending:
+                if p.submap_id not in slot_of:
+                    slot_of[p.submap_id] = len(matchers)
+                    matchers.append(self._matchers[p.submap_id])
+                if id(p.cloud) not in scan_of:  # a node's cloud uploads once
+                    scan_of[id(p.cloud)] = len(clouds)
+                    clouds.append(_f32_points(p.cloud))
+                submap_idx.append(slot_of[p.submap_id])
+                scan_idx.append(scan_of[id(p.cloud)])
+            pairs = make_pairs(submap_idx, scan_idx, 0.0, full_submap=True)
+            for i, p in enumerate(pending):
+                pairs[i]["full_submap"] = 1 if p.full else 0
+                pairs[i]["min_score"] = (self.options.global_localization_min_score if p.full
+                                         else self.options.min_score)
+                pairs[i]["x"], pairs[i]["y"], pairs[i]["theta"] = p.initial
+            scans = ScanSet(clouds, self.context)
+            try:
+                results = match_batch(matchers, scans, pairs, self.context)
+            finally:
+                scans.close()
+            for p, r in zip(pending, results):
+                if p.full:
+                    self.global_constraints_searched += 1
+                else:
+                    self.constraints_searched += 1
+                if int(r["status"]) != CSM_OK:
+                    continue
+                score = float(r["score"])
+                if p.full:
+                    self.global_constraints_found += 1
+                    self.global_constraint_scores.append(score)
+                else:
+                    self.constraints_found += 1
+                    self.constraint_scores.append(score)
+                pose = (float(r["x"]), float(r["y"]), float(r["theta"]))
+                self._constraints[p.slot] = Constraint(
+                    submap_id=p.submap_id, node_id=p.node_id,
+                    relative_pose=rigid2d_compose(rigid2d_inverse(p.submap.local_pose), pose),
+                    translation_weight=self.options.loop_closure_translation_weight,
+                    rotation_weight=self.options.loop_closure_rotation_weight,
+                    score=score)
+        self._finished_nodes = self._started_nodes

@@ -1,0 +1,81 @@
+// C++ restatement of ConstraintBuilder2DTest (reference
+// mapping/internal/constraints/constraint_builder_2d_test.cc:58-128) against
+// the drop-in headers. Exits 0 when every check holds; prints the failing
+// check otherwise. Compiled by tests/test_constraint_builder.py (CPU) and run
+// there on the GPU.
+#include <cstdio>
+#include <vector>
+
+#include "cartographer_amd/constraint_builder_2d.h"
+
+using namespace cartographer_amd;
+
+static int failures = 0;
+#define EXPECT(cond)                                                  \
+  do {                                                                \
+    if (!(cond)) {                                                    \
+      std::fprintf(stderr, "%s:%d: EXPECT(%s)\n", __FILE__, __LINE__, #cond); \
+      ++failures;                                                     \
+    }                                                                 \
+  } while (0)
+
+static ConstraintBuilderOptions TestOptions() {
+  ConstraintBuilderOptions o;  // pose_graph.lua defaults, then the test's overrides
+  o.sampling_ratio = 1;
+  o.min_score = 0;
+  o.global_localization_min_score = 0;
+  return o;
+}
+
+static void CallsBack() {
+  ConstraintBuilder2D builder(TestOptions());
+  EXPECT(builder.GetNumFinishedNodes() == 0);
+  builder.NotifyEndOfNode();
+  size_t n = 99;
+  builder.WhenDone([&](const ConstraintBuilder2D::Result& r) { n = r.size(); });
+  EXPECT(n == 0);
+  EXPECT(builder.GetNumFinishedNodes() == 1);
+}
+
+static void FindsConstraints() {
+  ConstraintBuilder2D builder(TestOptions());
+  PointCloud cloud;
+  cloud.push_back(0.1f, 0.2f, 0.3f);
+  // MapLimits(1., (2., 3.), CellLimits(100, 110)), all cells unknown.
+  std::vector<uint16_t> cells(100 * 110, 0);
+  Submap2DView submap;
+  submap.grid.resolution = 1.;
+  submap.grid.max_x = 2.;
+  submap.grid.max_y = 3.;
+  submap.grid.num_x_cells = 100;
+  submap.grid.num_y_cells = 110;
+  submap.grid.cells = cells.data();
+  submap.local_pose = Rigid2d{4., 5., 0.};  // Submap2D origin (4, 5)
+  const SubmapId submap_id{0, 1};
+  int expected_nodes = 0;
+  for (int i = 0; i < 2; ++i) {
+    EXPECT(builder.GetNumFinishedNodes() == expected_nodes);
+    for (int j = 0; j < 2; ++j)
+      builder.MaybeAddConstraint(submap_id, &submap, NodeId{0, 0}, &cloud, Rigid2d::Identity());
+    builder.MaybeAddGlobalConstraint(submap_id, &submap, NodeId{0, 0}, &cloud);
+    builder.NotifyEndOfNode();
+    EXPECT(builder.GetNumFinishedNodes() == ++expected_nodes);
+    builder.NotifyEndOfNode();
+    EXPECT(builder.GetNumFinishedNodes() == ++expected_nodes);
+    ConstraintBuilder2D::Result result;
+    builder.WhenDone([&](const ConstraintBuilder2D::Result& r) { result = r; });
+    EXPECT(result.size() == 3);
+    for (const Constraint& c : result) EXPECT(c.tag == Constraint::INTER_SUBMAP);
+    builder.DeleteScanMatcher(submap_id);
+  }
+  EXPECT(builder.constraints_searched == 4 && builder.constraints_found == 4);
+  EXPECT(builder.global_constraints_searched == 2 && builder.global_constraints_found == 2);
+}
+
+int main() {
+  CallsBack();
+  FindsConstraints();
+  if (failures) return 1;
+  std::printf("constraint_builder_2d_test: OK\n");
+  return 0;
+}

@@ -1,0 +1,207 @@
+"""ConstraintBuilder2D drop-in: restates ConstraintBuilder2DTest
+(reference mapping/internal/constraints/constraint_builder_2d_test.cc:58-128)
+for the Python mirror and the C++ header, plus parity of the builder's
+constraints with the oracle on synthetic submaps.
+
+CPU tests: sampler / pose algebra / option defaults, and that the C++ headers
+compile and link against libcsm_amd.so. GPU tests: the builder runs the HIP
+batch path.
+"""
+import math
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+CPP_TEST = os.path.join(ROOT, "tests", "cpp", "constraint_builder_2d_test.cc")
+CPP_BIN = os.path.join(ROOT, "tests", "cpp", "_build", "constraint_builder_2d_test")
+
+
+@pytest.fixture(scope="session")
+def cb(csm):
+    import importlib
+    return importlib.import_module("cartographer_amd.constraint_builder")
+
+
+def test_fixed_ratio_sampler(cb):
+    # common/fixed_ratio_sampler_test.cc: ratio 0.5 alternates, ratio 1 keeps all,
+    # ratio 0 drops all, and the sample count tracks ratio * pulses.
+    s = cb.FixedRatioSampler(0.5)
+    assert [s.Pulse() for _ in range(6)] == [True, False, True, False, True, False]
+    assert all(cb.FixedRatioSampler(1.0).Pulse() for _ in range(10))
+    assert not any(cb.FixedRatioSampler(0.0).Pulse() for _ in range(10))
+    s = cb.FixedRatioSampler(0.3)
+    kept = sum(s.Pulse() for _ in range(1000))
+    assert kept == 300
+    with pytest.raises(ValueError):
+        cb.FixedRatioSampler(1.5)
+
+
+def test_rigid2d_algebra(cb):
+    a, b = (1.0, -2.0, 0.7), (0.3, 0.4, -1.9)
+    ab = cb.rigid2d_compose(a, b)
+    back = cb.rigid2d_compose(cb.rigid2d_inverse(a), ab)
+    assert np.allclose(back, b, atol=1e-12)
+    ident = cb.rigid2d_compose(a, cb.rigid2d_inverse(a))
+    assert np.allclose(ident[:2], (0, 0), atol=1e-12) and abs(ident[2]) < 1e-12
+
+
+def test_option_defaults(cb):
+    o = cb.ConstraintBuilderOptions()  # configuration_files/pose_graph.lua:17-29
+    assert (o.sampling_ratio, o.max_constraint_distance, o.min_score,
+            o.global_localization_min_score) == (0.3, 15.0, 0.55, 0.6)
+    f = o.fast_correlative_scan_matcher_options
+    assert (f.linear_search_window, f.branch_and_bound_depth) == (7.0, 7)
+    assert math.isclose(f.angular_search_window, math.radians(30.0))
+
+
+def _build_cpp():
+    os.makedirs(os.path.dirname(CPP_BIN), exist_ok=True)
+    libdir = os.path.join(ROOT, "cartographer-1_amd")
+    subprocess.check_call(["g++", "-std=c++17", "-O1", "-Wall", "-Werror",
+                           "-I", os.path.join(ROOT, "include"), CPP_TEST, "-o", CPP_BIN,
+                           "-L", libdir, "-lcsm_amd", "-Wl,-rpath," + libdir])
+
+
+def test_cpp_headers_compile_and_link(csm):
+    _build_cpp()
+    assert os.access(CPP_BIN, os.X_OK)
+
+
+@pytest.mark.gpu
+def test_cpp_constraint_builder(csm):
+    _build_cpp()
+    out = subprocess.run([CPP_BIN], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    assert "OK" in out.stdout
+
+
+def _unknown_submap(csm, cb):
+    # MapLimits(1., (2., 3.), CellLimits(100, 110)); Submap2D origin (4, 5).
+    grid = csm.ProbabilityGrid(1.0, 2.0, 3.0, np.zeros((110, 100), np.uint16))
+    return cb.Submap2D(grid, (4.0, 5.0, 0.0))
+
+
+def _test_options(cb):
+    return cb.ConstraintBuilderOptions(sampling_ratio=1.0, min_score=0.0,
+                                       global_localization_min_score=0.0)
+
+
+@pytest.mark.gpu
+def test_calls_back(csm, cb):
+    builder = cb.ConstraintBuilder2D(_test_options(cb))
+    assert builder.GetNumFinishedNodes() == 0
+    builder.NotifyEndOfNode()
+    got = []
+    builder.WhenDone(got.append)
+    assert got == [[]]
+    assert builder.GetNumFinishedNodes() == 1
+
+
+@pytest.mark.gpu
+def test_finds_constraints(csm, cb):
+    builder = cb.ConstraintBuilder2D(_test_options(cb))
+    cloud = np.array([[0.1, 0.2, 0.3]], np.float32)
+    submap = _unknown_submap(csm, cb)
+    submap_id = (0, 1)
+    expected_nodes = 0
+    for _ in range(2):
+        assert builder.GetNumFinishedNodes() == expected_nodes
+        for _ in range(2):
+            builder.MaybeAddConstraint(submap_id, submap, (0, 0), cloud, (0.0, 0.0, 0.0))
+        builder.MaybeAddGlobalConstraint(submap_id, submap, (0, 0), cloud)
+        builder.NotifyEndOfNode()
+        expected_nodes += 1
+        assert builder.GetNumFinishedNodes() == expected_nodes
+        builder.NotifyEndOfNode()
+        expected_nodes += 1
+        assert builder.GetNumFinishedNodes() == expected_nodes
+        got = []
+        builder.WhenDone(got.append)
+        assert len(got) == 1 and len(got[0]) == 3
+        assert all(c.tag == "INTER_SUBMAP" for c in got[0])
+        builder.DeleteScanMatcher(submap_id)
+        assert builder.num_submap_scan_matchers == 0
+
+
+@pytest.mark.gpu
+def test_distance_filter_and_sampling(csm, cb):
+    opts = _test_options(cb)
+    opts.sampling_ratio = 0.5
+    builder = cb.ConstraintBuilder2D(opts)
+    submap = _unknown_submap(csm, cb)
+    cloud = np.array([[0.1, 0.2, 0.3]], np.float32)
+    builder.MaybeAddConstraint((0, 0), submap, (0, 0), cloud, (15.1, 0.0, 0.0))  # too far
+    for _ in range(4):
+        builder.MaybeAddConstraint((0, 0), submap, (0, 0), cloud, (1.0, 1.0, 0.0))
+    builder.NotifyEndOfNode()
+    got = []
+    builder.WhenDone(got.append)
+    assert len(got[0]) == 2  # 4 pulses at ratio 0.5
+    assert builder.constraints_searched == 2
+
+
+@pytest.mark.gpu
+def test_builder_constraints_match_oracle(csm, cb, oracle):
+    """Constraints from the builder equal the oracle's Match / MatchFullSubmap
+    on the same pairs (score bit-identical, pose identical or an exact tie),
+    expressed in the submap frame as ComputeConstraint does (:251-252)."""
+    from test_fast2d_gpu import assert_fast_parity
+    world = csm.SyntheticWorld2D(num_nodes=48, num_submaps=4, decimate_to=160, seed=7)
+    fopts = csm.FastCorrelativeScanMatcherOptions2D()
+    opts = cb.ConstraintBuilderOptions(sampling_ratio=1.0, min_score=0.4,
+                                       global_localization_min_score=0.45,
+                                       max_constraint_distance=1e9,
+                                       fast_correlative_scan_matcher_options=fopts)
+    builder = cb.ConstraintBuilder2D(opts)
+    rng = np.random.default_rng(3)
+    # Non-trivial submap poses: the builder composes the search start with it
+    # (:195-197) and expresses the result in the submap frame (:251-252).
+    local = {s: (0.2 * s, -0.1 * s, 0.0) for s in range(world.num_submaps)}
+    submaps = {s: cb.Submap2D(world.grid(s), local[s]) for s in range(world.num_submaps)}
+    expected = []
+    for node in range(0, world.num_nodes, 3):
+        cloud = world.cloud(node)
+        for s in range(world.num_submaps):
+            if (node + s) % 4 == 0:
+                builder.MaybeAddGlobalConstraint((0, s), submaps[s], (0, node), cloud)
+                expected.append((s, node, None))
+            else:
+                pose = world.node_poses[node] + rng.normal(0, [0.3, 0.3, 0.05])
+                rel = cb.rigid2d_compose(cb.rigid2d_inverse(local[s]), tuple(pose))
+                builder.MaybeAddConstraint((0, s), submaps[s], (0, node), cloud, rel)
+                expected.append((s, node, cb.rigid2d_compose(local[s], rel)))
+        builder.NotifyEndOfNode()
+    got = []
+    builder.WhenDone(got.append)
+    got = got[0]
+
+    from test_fast2d_gpu import full_submap_center
+    oms, want = {}, []
+    for s, node, init in expected:
+        g = world.grid(s)
+        limits = (g.resolution, g.max_x, g.max_y)
+        if s not in oms:
+            oms[s] = oracle.fast2d(limits, g.cells, fopts.linear_search_window,
+                                   fopts.angular_search_window, fopts.branch_and_bound_depth)
+        cloud = world.cloud(node)
+        if init is None:
+            ref = oms[s].match_full_submap(cloud, opts.global_localization_min_score)
+            ctr = full_submap_center(limits, g.cells)
+        else:
+            ref = oms[s].match(init, cloud, opts.min_score)
+            ctr = init
+        if ref[0]:  # failed searches are dropped (RunWhenDoneCallback :285-288)
+            want.append((s, node, init is None, ctr, ref, limits, g.cells, cloud))
+    assert len(got) == len(want) and len(want) > 5
+    for c, (s, node, full, ctr, ref, limits, cells, cloud) in zip(got, want):
+        assert c.submap_id == (0, s) and c.node_id == (0, node)
+        assert c.tag == "INTER_SUBMAP"
+        assert c.translation_weight == opts.loop_closure_translation_weight
+        assert c.rotation_weight == opts.loop_closure_rotation_weight
+        pose = cb.rigid2d_compose(local[s], c.relative_pose)
+        assert_fast_parity(oracle, oms[s], limits, cells, (True, c.score, pose), ref, full,
+                           ctr, cloud)
