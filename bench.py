@@ -18,6 +18,7 @@ RealTimeCorrelativeScanMatcher2D::Match ms/scan-match at config C1.
 Prints ONE JSON line on rank 0.
 """
 import argparse
+import importlib
 import json
 import math
 import os
@@ -49,6 +50,7 @@ def parse():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-rt", action="store_true")
     p.add_argument("--seed", type=int, default=20250127)
+    p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
     return p.parse_args()
 
 
@@ -58,15 +60,19 @@ def main():
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    device = local_rank
     if world_size > 1:
         import torch
         import torch.distributed as tdist
-        torch.cuda.set_device(local_rank)
-        tdist.init_process_group("nccl")
+        # --dist-backend gloo (CPU tensors) lets ranks share one GPU for rehearsal;
+        # the production path is RCCL ("nccl"), one rank per GPU.
+        device = local_rank % max(torch.cuda.device_count(), 1)
+        torch.cuda.set_device(device)
+        tdist.init_process_group(args.dist_backend)
         dist = tdist
 
     csm = load_pkg()
-    ctx = csm.Context(local_rank)
+    ctx = csm.Context(device)
 
     # ---- synthetic world (identical on every rank) -------------------------
     t0 = time.time()
@@ -74,7 +80,8 @@ def main():
                                  num_submaps=args.submaps_per_rank * world_size,
                                  submap_cells=400, beams=1080, seed=args.seed)
     gen_s = time.time() - t0
-    my_submaps = list(range(rank * args.submaps_per_rank, (rank + 1) * args.submaps_per_rank))
+    cdist = importlib.import_module("cartographer_amd.distributed")
+    my_submaps = cdist.shard_submaps(world.num_submaps, rank, world_size, args.submaps_per_rank)
     opts = csm.FastCorrelativeScanMatcherOptions2D(7.0, math.radians(30.0), 7, args.search_depth)
     t0 = time.time()
     matchers = [csm.FastCorrelativeScanMatcher2D(world.grid(s), opts, ctx) for s in my_submaps]
@@ -88,32 +95,15 @@ def main():
     submission = (np.int64(rank) * len(pairs) + np.arange(len(pairs), dtype=np.int64))
     n_pairs = len(pairs)
 
-    def gather_constraints(res):
-        ok = res["status"] == 0
-        rec = np.zeros((int(ok.sum()), 6), np.float64)
-        rec[:, 0] = submission[ok]
-        rec[:, 1] = np.asarray(my_submaps)[sub_local[ok]]
-        rec[:, 2] = node_idx[ok]
-        rec[:, 3] = res["x"][ok]
-        rec[:, 4] = res["y"][ok]
-        rec[:, 5] = res["theta"][ok]
-        if dist is None:
-            return rec
+    coll_dev = None
+    if dist is not None:
         import torch
-        dev = torch.device("cuda", local_rank)
-        cnt = torch.tensor([rec.shape[0]], dtype=torch.int64, device=dev)
-        cnts = [torch.zeros_like(cnt) for _ in range(world_size)]
-        dist.all_gather(cnts, cnt)
-        mx = int(max(c.item() for c in cnts))
-        buf = torch.zeros((max(mx, 1), 6), dtype=torch.float64, device=dev)
-        if rec.shape[0]:
-            buf[:rec.shape[0]] = torch.from_numpy(rec).to(dev)
-        bufs = [torch.zeros_like(buf) for _ in range(world_size)] if rank == 0 else None
-        dist.gather(buf, bufs, dst=0)
-        if rank != 0:
-            return None
-        allrec = np.concatenate([b[:int(c.item())].cpu().numpy() for b, c in zip(bufs, cnts)])
-        return allrec[np.argsort(allrec[:, 0], kind="stable")]
+        coll_dev = torch.device("cuda", device) if args.dist_backend == "nccl" else None
+    sub_global = np.asarray(my_submaps, np.int64)[sub_local]
+
+    def gather_constraints(res):
+        rec = cdist.make_records(res, submission, sub_global, node_idx)
+        return cdist.gather_records(rec, dist, rank, world_size, coll_dev)
 
     def barrier_sync():
         if dist is not None:
@@ -140,11 +130,7 @@ def main():
     ctx.enable_timing(False)
     tm = ctx.timing()
     lv_cands, lv_batches = ctx.level_stats()
-    if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64, device=torch.device("cuda", local_rank))
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = cdist.max_over_ranks(elapsed, dist, coll_dev)
     total_pairs = n_pairs * world_size * args.steps
     value = total_pairs / elapsed
 

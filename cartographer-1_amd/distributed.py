@@ -1,0 +1,94 @@
+"""Multi-GPU constraint search: submap sharding and the rank-0 gather.
+
+The reference runs one ``common::Task`` per (node, submap) pair on a thread
+pool (``constraint_builder_2d.cc:102-111``) and hands every accepted
+constraint to the pose-graph solve through ``WhenDone`` in submission order
+(``:285-288``). Here the pair queue is sharded by submap across ranks (one
+process per GPU): every rank builds the pyramids of its own submaps only and
+searches its pairs with no data-path collective. The single exchange is the
+gather of accepted constraints to rank 0, which restores submission order
+(SURVEY.md 8(e)).
+
+Record layout (float64 x 9, one row per accepted constraint):
+``submission_index, submap_trajectory, submap_index, node_trajectory,
+node_index, x, y, theta, score``.
+"""
+
+from __future__ import annotations
+
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+RECORD_FIELDS = ("submission", "submap_traj", "submap_index", "node_traj", "node_index",
+                 "x", "y", "theta", "score")
+RECORD_WIDTH = len(RECORD_FIELDS)
+
+
+def shard_submaps(num_submaps: int, rank: int, world_size: int,
+                  per_rank: Optional[int] = None) -> List[int]:
+    """Submaps owned by ``rank``: contiguous blocks of ``per_rank`` when given
+    (weak scaling, each rank a fixed share), else striped ``s % world_size``."""
+    if not 0 <= rank < world_size:
+        raise ValueError("rank out of range")
+    if per_rank is not None:
+        if per_rank * world_size > num_submaps:
+            raise ValueError("not enough submaps for per_rank x world_size")
+        return list(range(rank * per_rank, (rank + 1) * per_rank))
+    return list(range(rank, num_submaps, world_size))
+
+
+def make_records(results: np.ndarray, submission: np.ndarray, submap_ids: np.ndarray,
+                 node_ids: np.ndarray, submap_traj: int = 0, node_traj: int = 0) -> np.ndarray:
+    """Accepted rows of a ``match_batch`` result as gather records."""
+    ok = results["status"] == 0
+    rec = np.zeros((int(ok.sum()), RECORD_WIDTH), np.float64)
+    rec[:, 0] = submission[ok]
+    rec[:, 1] = submap_traj
+    rec[:, 2] = submap_ids[ok]
+    rec[:, 3] = node_traj
+    rec[:, 4] = node_ids[ok]
+    rec[:, 5] = results["x"][ok]
+    rec[:, 6] = results["y"][ok]
+    rec[:, 7] = results["theta"][ok]
+    rec[:, 8] = results["score"][ok]
+    return rec
+
+
+def gather_records(rec: np.ndarray, dist=None, rank: int = 0, world_size: int = 1,
+                   device=None) -> Optional[np.ndarray]:
+    """Gathers every rank's records to rank 0, sorted by submission index.
+
+    Two collectives: an all-gather of the per-rank counts, then a gather of
+    count-padded fixed-width record blocks. ``device`` is the tensor device of
+    the process group's backend (``cuda:<local_rank>`` for RCCL, cpu for gloo).
+    Returns the sorted records on rank 0 and None elsewhere."""
+    if dist is None or world_size == 1:
+        return rec[np.argsort(rec[:, 0], kind="stable")]
+    import torch
+    dev = torch.device("cpu") if device is None else device
+    cnt = torch.tensor([rec.shape[0]], dtype=torch.int64, device=dev)
+    cnts = [torch.zeros_like(cnt) for _ in range(world_size)]
+    dist.all_gather(cnts, cnt)
+    counts = [int(c.item()) for c in cnts]
+    mx = max(max(counts), 1)
+    buf = torch.zeros((mx, RECORD_WIDTH), dtype=torch.float64, device=dev)
+    if rec.shape[0]:
+        buf[:rec.shape[0]] = torch.from_numpy(np.ascontiguousarray(rec)).to(dev)
+    bufs = [torch.zeros_like(buf) for _ in range(world_size)] if rank == 0 else None
+    dist.gather(buf, bufs, dst=0)
+    if rank != 0:
+        return None
+    allrec = np.concatenate([b[:c].cpu().numpy() for b, c in zip(bufs, counts)])
+    return allrec[np.argsort(allrec[:, 0], kind="stable")]
+
+
+def max_over_ranks(value: float, dist=None, device=None) -> float:
+    """The slowest rank's wall time (bench timing contract)."""
+    if dist is None:
+        return value
+    import torch
+    t = torch.tensor([value], dtype=torch.float64,
+                     device=torch.device("cpu") if device is None else device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())

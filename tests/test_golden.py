@@ -1,0 +1,129 @@
+"""Golden vectors (tests/golden/*.npz, written by tests/golden/make_golden.py
+from the pinned oracle).
+
+CPU: the oracle still reproduces them (guards against oracle drift; the
+cheapest C2 pairs plus every local and RTCSM case).
+GPU: the HIP path reproduces them through the C-ABI, both batched
+(csm_fast2d_match_batch) and single-call (Match / MatchFullSubmap).
+"""
+import math
+import os
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def _load(name):
+    return dict(np.load(os.path.join(GOLDEN, name)))
+
+
+def _cloud(d, c):
+    return d["points"][d["offsets"][c]:d["offsets"][c + 1]]
+
+
+def _limits(d, s):
+    res, mx, my = d["limits"][s]
+    return float(res), float(mx), float(my)
+
+
+def _full_center(d, s):
+    res, mx, my = _limits(d, s)
+    cells = d["cells"][s]
+    return (mx - 0.5 * res * cells.shape[0], my - 0.5 * res * cells.shape[1], 0.0)
+
+
+@pytest.mark.parametrize("name", ["fast2d_c2.npz", "fast2d_local.npz"])
+def test_oracle_reproduces_fast2d_golden(oracle, name):
+    d = _load(name)
+    lin, ang, depth = d["options"]
+    oms = {}
+    cheap = np.argsort(d["reference_lookups"])
+    budget = 2.5e9  # lookups, ~ a few seconds of oracle time
+    checked = 0
+    for i in cheap:
+        if d["reference_lookups"][i] > budget and checked >= 3:
+            break
+        budget -= d["reference_lookups"][i]
+        s, c, full = int(d["pairs"][i, 0]), int(d["pairs"][i, 1]), int(d["pairs"][i, 2])
+        if s not in oms:
+            oms[s] = oracle.fast2d(_limits(d, s), d["cells"][s], float(lin), float(ang), int(depth))
+        ms = float(d["pairs"][i, 6])
+        r = (oms[s].match_full_submap(_cloud(d, c), ms) if full
+             else oms[s].match(tuple(d["pairs"][i, 3:6]), _cloud(d, c), ms))
+        assert int(r[0]) == d["matched"][i]
+        if r[0]:
+            assert np.float32(r[1]) == d["score"][i]
+            assert tuple(r[2]) == tuple(d["pose"][i])
+        checked += 1
+    assert checked >= 3
+
+
+def test_oracle_reproduces_rt2d_golden(oracle):
+    d = _load("rt2d_c1.npz")
+    for i in range(len(d["score"])):
+        s = int(d["grid"][i])
+        sc, pose, _ = oracle.rt2d_match(_limits(d, s), d["cells"][s], tuple(d["options"]),
+                                        tuple(d["initial"][i]), _cloud(d, i))
+        assert sc == d["score"][i]
+        assert tuple(pose) == tuple(d["pose"][i])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["fast2d_c2.npz", "fast2d_local.npz"])
+def test_gpu_matches_fast2d_golden(csm, oracle, name):
+    from test_fast2d_gpu import assert_fast_parity
+    d = _load(name)
+    lin, ang, depth = float(d["options"][0]), float(d["options"][1]), int(d["options"][2])
+    opts = csm.FastCorrelativeScanMatcherOptions2D(lin, ang, depth)
+    grids = [csm.ProbabilityGrid(*_limits(d, s), d["cells"][s]) for s in range(len(d["cells"]))]
+    mats = [csm.FastCorrelativeScanMatcher2D(g, opts) for g in grids]
+    scans = csm.ScanSet(None, packed=(d["points"], d["offsets"]))
+    p = d["pairs"]
+    pairs = csm.make_pairs(p[:, 0].astype(np.int32), p[:, 1].astype(np.int32), 0.0)
+    pairs["full_submap"] = p[:, 2].astype(np.int32)
+    pairs["min_score"] = p[:, 6]
+    pairs["x"], pairs["y"], pairs["theta"] = p[:, 3], p[:, 4], p[:, 5]
+    res = csm.match_batch(mats, scans, pairs)
+    oms = {}
+    for i in range(len(p)):
+        s, c, full = int(p[i, 0]), int(p[i, 1]), bool(p[i, 2])
+        ok = res["status"][i] == csm.CSM_OK
+        assert int(ok) == d["matched"][i], (name, i)
+        if full:
+            single = mats[s].MatchFullSubmap(_cloud(d, c), float(p[i, 6]))
+        else:
+            single = mats[s].Match(tuple(p[i, 3:6]), _cloud(d, c), float(p[i, 6]))
+        assert single[0] == ok
+        if not ok:
+            continue
+        assert np.float32(res["score"][i]) == d["score"][i]
+        assert np.float32(single[1]) == d["score"][i]
+        gp = (float(res["x"][i]), float(res["y"][i]), float(res["theta"][i]))
+        assert tuple(single[2]) == gp  # batch == single call
+        if gp != tuple(d["pose"][i]):  # an exact tie: check in the oracle
+            if s not in oms:
+                oms[s] = oracle.fast2d(_limits(d, s), d["cells"][s], lin, ang, depth)
+            ref = (True, float(d["score"][i]), tuple(d["pose"][i]))
+            init = _full_center(d, s) if full else tuple(p[i, 3:6])
+            assert_fast_parity(oracle, oms[s], _limits(d, s), d["cells"][s], (True, res["score"][i], gp),
+                               ref, full, init, _cloud(d, c))
+
+
+@pytest.mark.gpu
+def test_gpu_matches_rt2d_golden(csm):
+    d = _load("rt2d_c1.npz")
+    o = d["options"]
+    m = csm.RealTimeCorrelativeScanMatcher2D(
+        csm.RealTimeCorrelativeScanMatcherOptions(*[float(v) for v in o]))
+    for i in range(len(d["score"])):
+        s = int(d["grid"][i])
+        g = csm.ProbabilityGrid(*_limits(d, s), d["cells"][s])
+        sc, pose = m.Match(tuple(d["initial"][i]), _cloud(d, i), g)
+        # float sum in reference order; the double exp() penalty may differ from
+        # glibc in the last ulps: 1e-6 relative (north star: 1e-4).
+        assert math.isclose(sc, d["score"][i], rel_tol=1e-6, abs_tol=0), (i, sc, d["score"][i])
+        assert tuple(pose) == tuple(d["pose"][i])
