@@ -141,6 +141,8 @@ def main():
     achieved = bytes_per_launch / (kernel_ms_avg * 1e-3) / 1e9 if kernel_ms_avg > 0 else 0.0
     peak = 8000.0
 
+    traffic = committed_traffic(args, world_size)
+
     out = {
         "metric": "loop-closure constraint candidates/sec (node x submap pairs) + ms/scan-match, 2D 5cm grid",
         "value": value,
@@ -160,7 +162,9 @@ def main():
                    "pairs_per_step_per_gpu": n_pairs, "search_depth": matchers[0].options.search_depth,
                    "parallelism": f"submap-sharded x{world_size}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
-                     "frac": achieved / peak, "traffic": None,
+                     "frac": achieved / peak,
+                     "traffic": traffic["traffic_bytes_per_launch"] if traffic else None,
+                     "traffic_source": traffic["source"] if traffic else None,
                      "kernel": "fast2d_search", "kernel_ms_avg": kernel_ms_avg,
                      "algorithmic_bytes_per_launch": bytes_per_launch},
         "accepted_constraints_per_step": accepted,
@@ -178,6 +182,22 @@ def main():
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def committed_traffic(args, world_size):
+    """HBM-side bytes per search launch from the committed PMC pass
+    (profiles/r1/traffic_c2.json: rocprofv3 --pmc FETCH_SIZE, x2 gfx950
+    correction). PMC counters cannot be read from inside this process, so the
+    figure is reported only when this run's workload is the profiled one."""
+    path = os.path.join(ROOT, "profiles", "r1", "traffic_c2.json")
+    try:
+        t = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    same = (world_size == 1 and args.nodes == t["nodes"] and
+            args.submaps_per_rank == t["submaps_per_rank"] and
+            abs(args.min_score - t["min_score"]) < 1e-9 and args.search_depth == t["search_depth"])
+    return t if same else None
 
 
 def rt2d_bench(csm, ctx, args):
