@@ -77,7 +77,49 @@ class Result2D(C.Structure):
 class Timing(C.Structure):
     _fields_ = [("search_kernel_ms", C.c_double), ("search_launches", C.c_int64),
                 ("search_lookups", C.c_double), ("search_candidates", C.c_double),
-                ("other_kernel_ms", C.c_double)]
+                ("other_kernel_ms", C.c_double), ("rt3d_kernel_ms", C.c_double),
+                ("rt3d_lookups", C.c_double), ("fast3d_kernel_ms", C.c_double),
+                ("fast3d_launches", C.c_int64), ("fast3d_lookups", C.c_double)]
+
+
+class Pose3D(C.Structure):
+    """transform::Rigid3d: t (x, y, z) and q (w, x, y, z)."""
+    _fields_ = [("t", C.c_double * 3), ("q", C.c_double * 4)]
+
+    @staticmethod
+    def make(t=(0.0, 0.0, 0.0), q=(1.0, 0.0, 0.0, 0.0)) -> "Pose3D":
+        p = Pose3D()
+        p.t[:] = [float(v) for v in t]
+        p.q[:] = [float(v) for v in q]
+        return p
+
+    def as_tuple(self):
+        return tuple(self.t), tuple(self.q)
+
+
+class Fast3DOptions(C.Structure):
+    _fields_ = [("branch_and_bound_depth", C.c_int32), ("full_resolution_depth", C.c_int32),
+                ("min_rotational_score", C.c_double), ("min_low_resolution_score", C.c_double),
+                ("linear_xy_search_window", C.c_double), ("linear_z_search_window", C.c_double),
+                ("angular_search_window", C.c_double)]
+
+
+class Node3D(C.Structure):
+    _fields_ = [("high_resolution_xyz", C.POINTER(C.c_float)),
+                ("num_high_resolution", C.c_int32),
+                ("low_resolution_xyz", C.POINTER(C.c_float)), ("num_low_resolution", C.c_int32),
+                ("histogram", C.POINTER(C.c_float)), ("histogram_size", C.c_int32),
+                ("gravity_alignment", C.c_double * 4)]
+
+
+class Result3D(C.Structure):
+    _fields_ = [("status", C.c_int32), ("score", C.c_float), ("pose", Pose3D),
+                ("rotational_score", C.c_float), ("low_resolution_score", C.c_float)]
+
+
+class Pair3D(C.Structure):
+    _fields_ = [("submap", C.c_int32), ("node", C.c_int32), ("full_submap", C.c_int32),
+                ("min_score", C.c_float), ("node_pose", Pose3D), ("submap_pose", Pose3D)]
 
 
 # Exported symbols and their signatures (include/csm_amd.h).
@@ -112,6 +154,28 @@ _SIGNATURES = {
                                  C.POINTER(C.c_uint16), C.c_float, C.c_float, C.POINTER(Pose2D),
                                  C.POINTER(C.c_float), C.c_int32, C.POINTER(C.c_double),
                                  C.POINTER(Pose2D)]),
+    "csm_hybrid_grid_create": (C.c_int, [C.c_void_p, C.c_float, C.POINTER(C.c_int32),
+                                         C.POINTER(C.c_uint16), C.c_int64, C.c_int32,
+                                         C.POINTER(C.c_void_p)]),
+    "csm_hybrid_grid_destroy": (None, [C.c_void_p]),
+    "csm_hybrid_grid_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32),
+                                       C.POINTER(C.c_int32)]),
+    "csm_rt3d_match": (C.c_int, [C.c_void_p, C.POINTER(RtOptions), C.c_void_p, C.POINTER(Pose3D),
+                                 C.POINTER(C.c_float), C.c_int32, C.POINTER(C.c_float),
+                                 C.POINTER(Pose3D)]),
+    "csm_fast3d_create": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(C.c_float),
+                                    C.c_int32, C.POINTER(Fast3DOptions), C.POINTER(C.c_void_p)]),
+    "csm_fast3d_destroy": (None, [C.c_void_p]),
+    "csm_fast3d_read_level": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_uint8), C.c_int64,
+                                        C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+    "csm_fast3d_match": (C.c_int, [C.c_void_p, C.POINTER(Pose3D), C.POINTER(Pose3D),
+                                   C.POINTER(Node3D), C.c_float, C.POINTER(Result3D)]),
+    "csm_fast3d_match_full_submap": (C.c_int, [C.c_void_p, C.POINTER(C.c_double),
+                                               C.POINTER(C.c_double), C.POINTER(Node3D),
+                                               C.c_float, C.POINTER(Result3D)]),
+    "csm_fast3d_match_batch": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.c_int32,
+                                         C.POINTER(Node3D), C.c_int32, C.POINTER(Pair3D),
+                                         C.c_int64, C.POINTER(Result3D)]),
     "csm_strerror": (C.c_char_p, [C.c_int]),
 }
 
@@ -488,3 +552,8 @@ class SyntheticWorld2D:
         # cells[j, i] holds cell (x=i, y=j): flat index i + j * num_x_cells.
         return ProbabilityGrid(self.resolution, float(self.submap_max[submap, 0]),
                                float(self.submap_max[submap, 1]), self.submap_cells[submap])
+
+
+# 3D matchers (RealTimeCorrelativeScanMatcher3D, FastCorrelativeScanMatcher3D).
+from .matching3d import (FastCorrelativeScanMatcher3D, FastCorrelativeScanMatcherOptions3D,  # noqa: E402,F401
+                         HybridGrid, NodeData3D, RealTimeCorrelativeScanMatcher3D, match_batch_3d)

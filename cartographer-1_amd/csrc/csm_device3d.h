@@ -1,0 +1,71 @@
+// Device-side data layout of the 3D path (HybridGrid bricks, FastCSM3D
+// pyramid levels, per-pair / per-yaw work descriptors). Shared by
+// kernels3d.hip and host3d.cc.
+#ifndef CSM_DEVICE3D_H_
+#define CSM_DEVICE3D_H_
+
+#include <cstdint>
+
+namespace csm {
+
+constexpr int kMaxLevels3d = 10;
+constexpr int kMax3dPoints = 8192;        // high-resolution points per node (LDS)
+constexpr int kMax3dTop = 900;            // top-level candidates per yaw (stack)
+constexpr int kStack3d = 1024;            // DFS stack entries per workgroup
+constexpr int kMax3dYaws = 4095;          // 12-bit yaw id in the leaf key
+constexpr int kMax3dWindow = 511;         // 10-bit offset fields in the leaf key
+constexpr int kSearch3dThreads = 256;
+constexpr int kCellLimit3d = 16000;       // |cell index| kept in int16 in LDS
+constexpr int kKeyShift3d = 42;           // key = sum << 42 | ~leaf_id (42 bits)
+
+// A dense brick over the bounding box of a sparse grid's known cells:
+// value(i) = data[((i.z - oz) * ny + (i.y - oy)) * nx + (i.x - ox)], and the
+// grid's default outside the box.
+struct Brick3 {
+  int32_t ox, oy, oz;
+  int32_t nx, ny, nz;
+  int64_t offset;  // byte offset of this brick in its allocation
+};
+
+// One FastCSM3D submap (csm_fast3d): pyramid levels (uint8 bricks in one
+// allocation) and the low-resolution HybridGrid (float probability brick).
+struct Submap3Desc {
+  const uint8_t* levels;  // base of the level allocation
+  Brick3 level[kMaxLevels3d];
+  int32_t num_levels;     // branch_and_bound_depth
+  int32_t full_resolution_depth;
+  float resolution;
+  const float* low_prob;  // low-resolution grid probabilities
+  Brick3 low;
+  float low_resolution;
+};
+
+// One (submap, node) pair.
+struct Pair3Desc {
+  int32_t submap;
+  int32_t num_points;       // high-resolution points
+  int64_t point_offset;     // into the high-resolution point buffer (xyz)
+  int32_t num_low;          // low-resolution points
+  int64_t low_offset;
+  int32_t yaw_begin, num_yaws;
+  int32_t wxy, wz;          // linear window sizes (voxels)
+  int32_t top_nx, top_ny, top_nz;  // lowest-resolution candidates per axis
+  int32_t min_sum;          // smallest sum whose score exceeds min_score
+  float min_low_resolution_score;
+};
+
+// One discrete scan (yaw) of a pair: the pose the cloud is discretized with,
+// the normalized rotation of leaf poses (GetPoseFromCandidate), and its
+// rotational score.
+struct Yaw3Desc {
+  float qw, qx, qy, qz;     // DiscreteScan3D::pose rotation (not normalized)
+  float nw, nx, ny, nz;     // normalized (identity * q).normalized()
+  float tx, ty, tz;
+  float rotational_score;
+  int32_t pair;
+  int32_t yaw_id;           // index among the pair's discrete scans
+};
+
+}  // namespace csm
+
+#endif  // CSM_DEVICE3D_H_

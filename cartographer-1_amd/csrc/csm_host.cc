@@ -22,6 +22,7 @@
 
 #include "../../include/csm_amd.h"
 #include "csm_device.h"
+#include "csm_internal.h"
 #include "csm_launch.h"
 #include "search_window.h"
 
@@ -32,32 +33,6 @@ namespace csm {
 namespace {
 
 constexpr int kStatsWords = 2 + 2 * kMaxLevels;
-
-#define CSM_HIP(call)                               \
-  do {                                              \
-    if ((call) != hipSuccess) return CSM_EHIP;      \
-  } while (0)
-
-// Grow-only device buffer.
-struct DevBuf {
-  void* ptr = nullptr;
-  size_t bytes = 0;
-  ~DevBuf() {
-    if (ptr) (void)hipFree(ptr);
-  }
-  int Reserve(size_t n) {
-    if (n <= bytes) return CSM_OK;
-    if (ptr) (void)hipFree(ptr);
-    ptr = nullptr;
-    bytes = 0;
-    const size_t want = std::max<size_t>(n, 256);
-    if (hipMalloc(&ptr, want) != hipSuccess) return CSM_ENOMEM;
-    bytes = want;
-    return CSM_OK;
-  }
-  template <typename T>
-  T* as() const { return static_cast<T*>(ptr); }
-};
 
 int AutoSearchDepth(int configured, int nx, int ny) {
   // Extra coarse levels until the top lattice step reaches ~1/2 of the grid:
@@ -73,22 +48,6 @@ int AutoSearchDepth(int configured, int nx, int ny) {
 
 using namespace csm;
 
-struct csm_context {
-  int device = 0;
-  hipStream_t stream = nullptr;
-  std::mutex mu;
-  DevBuf submap_desc, pair_desc, rot_table, best, status, counters, pair_order,
-      chunk_prefix, blocks, stats, rt_prob, rt_cells, rt_points, rt_best, rt_rot, rt_ptab,
-      single_points;
-  bool timing = false;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  csm_timing t{};
-  std::vector<float> ptab_host;
-  bool ptab_uploaded = false;
-  double level_cands[kMaxLevels] = {0};
-  double level_batches[kMaxLevels] = {0};
-  int num_cus = 256;
-};
 
 struct csm_fast2d {
   csm_context* ctx = nullptr;

@@ -1,0 +1,66 @@
+// Internal host-side types shared by the 2D and 3D halves of the C-ABI
+// implementation (csm_host.cc, host3d.cc). Not part of the public boundary.
+#ifndef CSM_INTERNAL_H_
+#define CSM_INTERNAL_H_
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <mutex>
+#include <vector>
+
+#include "../../include/csm_amd.h"
+#include "csm_device.h"
+
+namespace csm {
+
+#define CSM_HIP(call)                               \
+  do {                                              \
+    if ((call) != hipSuccess) return CSM_EHIP;      \
+  } while (0)
+
+// Grow-only device buffer.
+struct DevBuf {
+  void* ptr = nullptr;
+  size_t bytes = 0;
+  ~DevBuf() {
+    if (ptr) (void)hipFree(ptr);
+  }
+  int Reserve(size_t n) {
+    if (n <= bytes) return CSM_OK;
+    if (ptr) (void)hipFree(ptr);
+    ptr = nullptr;
+    bytes = 0;
+    const size_t want = std::max<size_t>(n, 256);
+    if (hipMalloc(&ptr, want) != hipSuccess) return CSM_ENOMEM;
+    bytes = want;
+    return CSM_OK;
+  }
+  template <typename T>
+  T* as() const { return static_cast<T*>(ptr); }
+};
+
+
+}  // namespace csm
+
+struct csm_context {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+  csm::DevBuf submap_desc, pair_desc, rot_table, best, status, counters, pair_order,
+      chunk_prefix, blocks, stats, rt_prob, rt_cells, rt_points, rt_best, rt_rot, rt_ptab,
+      single_points;
+  bool timing = false;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  csm_timing t{};
+  std::vector<float> ptab_host;
+  bool ptab_uploaded = false;
+  double level_cands[csm::kMaxLevels] = {0};
+  double level_batches[csm::kMaxLevels] = {0};
+  int num_cus = 256;
+  // 3D path scratch (host3d.cc).
+  csm::DevBuf rt3_rot, rt3_trans, rt3_points, rt3_best, f3_pairs, f3_yaws, f3_points,
+      f3_low_points, f3_best, f3_status, f3_counter, f3_items;
+};
+
+#endif  // CSM_INTERNAL_H_

@@ -1,0 +1,34 @@
+// Host-callable launchers of the kernels in kernels3d.hip.
+#ifndef CSM_LAUNCH3D_H_
+#define CSM_LAUNCH3D_H_
+
+#include <hip/hip_runtime.h>
+
+#include "csm_device3d.h"
+
+namespace csm {
+
+constexpr int kRt3dThreads = 384;  // translations per RTCSM3D launch
+
+hipError_t LaunchBrickFromValues(const uint16_t* values, int64_t n, const float* ptab,
+                                 const uint8_t* qtab, float* prob, uint8_t* level0,
+                                 hipStream_t st);
+hipError_t LaunchLevelGather(const uint8_t* prev, const Brick3& pb, uint8_t* out, const Brick3& ob,
+                             int shift, int half, hipStream_t st);
+hipError_t LaunchRt3dScore(int num_rot, hipStream_t st, const float* prob, const Brick3& gb,
+                           float res, const float* points, int n, const float4* rot,
+                           const float* rot_angle, const float4* trans, int num_trans, int t_base,
+                           double wt, double wr, unsigned long long* best);
+hipError_t LaunchFast3dSearch(int grid, hipStream_t st, const Submap3Desc* submaps,
+                              const Pair3Desc* pairs, const Yaw3Desc* yaws, int num_items,
+                              const float* points, const float* low_points, unsigned* counter,
+                              unsigned long long* best, int32_t* status,
+                              unsigned long long* stats);
+hipError_t LaunchFast3dFinalize(int num_pairs, hipStream_t st, const Submap3Desc* submaps,
+                                const Pair3Desc* pairs, const Yaw3Desc* yaws,
+                                const float* low_points, const unsigned long long* best,
+                                float* low_score);
+
+}  // namespace csm
+
+#endif  // CSM_LAUNCH3D_H_

@@ -1,0 +1,846 @@
+// Host runtime of the 3D path: implements the HybridGrid, RTCSM3D and
+// FastCSM3D entry points of include/csm_amd.h on top of kernels3d.hip.
+//
+// Per pair the host does what is O(#yaws x histogram) and below — search
+// window, rotational histogram scores (RotationalScanMatcher::Match), the
+// discrete-scan poses (GenerateDiscreteScans) — with the reference's float
+// arithmetic; the device does everything O(points x candidates). Float
+// quaternion products follow Eigen's SSE path (Geometry_SSE.h), VectorXf
+// reductions Eigen's packet order (Redux.h); see DESIGN.md "3D".
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <thread>
+#include <vector>
+
+#include "../../include/csm_amd.h"
+#include "csm_device3d.h"
+#include "csm_internal.h"
+#include "csm_launch3d.h"
+
+using namespace csm;
+
+namespace {
+
+// ------------------------------------------------------------ float math --
+struct V3 {
+  float x, y, z;
+};
+struct Q4 {
+  float w, x, y, z;
+};
+struct R3 {
+  V3 t;
+  Q4 q;
+};
+
+inline int Lround(double v) { return static_cast<int>(std::lround(v)); }
+inline int LroundF(float v) { return static_cast<int>(std::lround(v)); }
+
+V3 Rotate(const Q4& q, const V3& v) {  // Eigen _transformVector
+  V3 u{q.y * v.z - q.z * v.y, q.z * v.x - q.x * v.z, q.x * v.y - q.y * v.x};
+  u.x += u.x;
+  u.y += u.y;
+  u.z += u.z;
+  const V3 c{q.y * u.z - q.z * u.y, q.z * u.x - q.x * u.z, q.x * u.y - q.y * u.x};
+  return V3{(v.x + q.w * u.x) + c.x, (v.y + q.w * u.y) + c.y, (v.z + q.w * u.z) + c.z};
+}
+V3 Apply(const R3& r, const V3& p) {
+  const V3 v = Rotate(r.q, p);
+  return V3{v.x + r.t.x, v.y + r.t.y, v.z + r.t.z};
+}
+Q4 QMul(const Q4& a, const Q4& b) {  // Geometry_SSE.h quat_product<float>
+  return Q4{(a.w * b.w - a.x * b.x) - (a.z * b.z + a.y * b.y),
+            (a.x * b.w - a.z * b.y) + (a.y * b.z + a.w * b.x),
+            (a.y * b.w - a.x * b.z) + (a.z * b.x + a.w * b.y),
+            (a.z * b.w - a.y * b.x) + (a.x * b.y + a.w * b.z)};
+}
+float SqNorm4(const Q4& q) { return (q.x * q.x + q.z * q.z) + (q.y * q.y + q.w * q.w); }
+Q4 QNormalized(const Q4& q) {
+  const float n2 = SqNorm4(q);
+  if (n2 > 0.f) {
+    const float n = std::sqrt(n2);
+    return Q4{q.w / n, q.x / n, q.y / n, q.z / n};
+  }
+  return q;
+}
+Q4 QInverse(const Q4& q) {  // Quaternion::inverse
+  const float n2 = SqNorm4(q);
+  if (n2 > 0.f) return Q4{q.w / n2, -q.x / n2, -q.y / n2, -q.z / n2};
+  return Q4{0.f, 0.f, 0.f, 0.f};
+}
+R3 Mul(const R3& a, const R3& b) { return R3{Apply(a, b.t), QNormalized(QMul(a.q, b.q))}; }
+R3 Inverse(const R3& a) {
+  const Q4 c{a.q.w, -a.q.x, -a.q.y, -a.q.z};
+  const V3 t = Rotate(c, a.t);
+  return R3{V3{-t.x, -t.y, -t.z}, c};
+}
+float NormV(const V3& v) { return std::sqrt((v.x * v.x + v.y * v.y) + v.z * v.z); }
+// transform.h:86-100 for float: sin/cos of norm/2. in double.
+Q4 AngleAxisToQuat(const V3& aa) {
+  float scale = 0.5f, w = 1.f;
+  const float sq = (aa.x * aa.x + aa.y * aa.y) + aa.z * aa.z;
+  if (sq > 1e-8) {
+    const float norm = std::sqrt(sq);
+    scale = static_cast<float>(std::sin(norm / 2.) / norm);
+    w = static_cast<float>(std::cos(norm / 2.));
+  }
+  return Q4{w, scale * aa.x, scale * aa.y, scale * aa.z};
+}
+float GetAngle(const Q4& q) {  // transform.h:34-37
+  return 2.f * std::atan2(std::sqrt((q.x * q.x + q.y * q.y) + q.z * q.z), std::abs(q.w));
+}
+float GetYaw(const Q4& q) {  // transform.h:43-47 (C ::atan2 on promoted floats)
+  const V3 d = Rotate(q, V3{1.f, 0.f, 0.f});
+  return static_cast<float>(::atan2(static_cast<double>(d.y), static_cast<double>(d.x)));
+}
+R3 CastF(const csm_pose3d& p) {
+  return R3{V3{static_cast<float>(p.t[0]), static_cast<float>(p.t[1]), static_cast<float>(p.t[2])},
+            Q4{static_cast<float>(p.q[0]), static_cast<float>(p.q[1]), static_cast<float>(p.q[2]),
+               static_cast<float>(p.q[3])}};
+}
+csm_pose3d ToPose(const V3& t, const Q4& q) {
+  csm_pose3d p;
+  p.t[0] = t.x;
+  p.t[1] = t.y;
+  p.t[2] = t.z;
+  p.q[0] = q.w;
+  p.q[1] = q.x;
+  p.q[2] = q.y;
+  p.q[3] = q.z;
+  return p;
+}
+
+// Redux.h LinearVectorizedTraversal, 4-float packets, aligned storage.
+float ReduxSum(const float* v, int n) {
+  const int a2 = (n / 8) * 8, a1 = (n / 4) * 4;
+  if (a1 == 0) {
+    if (n == 0) return 0.f;
+    float r = v[0];
+    for (int i = 1; i < n; ++i) r += v[i];
+    return r;
+  }
+  float p0[4] = {v[0], v[1], v[2], v[3]};
+  if (a1 > 4) {
+    float p1[4] = {v[4], v[5], v[6], v[7]};
+    for (int i = 8; i < a2; i += 8)
+      for (int k = 0; k < 4; ++k) {
+        p0[k] += v[i + k];
+        p1[k] += v[i + 4 + k];
+      }
+    for (int k = 0; k < 4; ++k) p0[k] += p1[k];
+    if (a1 > a2)
+      for (int k = 0; k < 4; ++k) p0[k] += v[a2 + k];
+  }
+  float r = (p0[0] + p0[2]) + (p0[1] + p0[3]);
+  for (int i = a1; i < n; ++i) r += v[i];
+  return r;
+}
+float Dot(const float* a, const float* b, int n, float* scratch) {
+  for (int i = 0; i < n; ++i) scratch[i] = a[i] * b[i];
+  return ReduxSum(scratch, n);
+}
+
+// rotational_scan_matcher.cc:119-131, :138-158, :173-185.
+void RotationalScores(const std::vector<float>& submap, const float* hist, int size,
+                      float initial_angle, const std::vector<float>& angles,
+                      std::vector<float>* out) {
+  out->resize(angles.size());
+  std::vector<float> rot(size), scratch(size);
+  const float submap_norm = std::sqrt(Dot(submap.data(), submap.data(), size, scratch.data()));
+  for (size_t a = 0; a < angles.size(); ++a) {
+    const float angle = initial_angle + angles[a];
+    if (size > 0) {
+      const float rb =
+          static_cast<float>(static_cast<double>(-angle * static_cast<float>(size)) / M_PI);
+      int full = LroundF(rb - 0.5f);
+      const float fraction = rb - static_cast<float>(full);
+      while (full < 0) full += size;
+      for (int i = 0; i < size; ++i)
+        rot[i] = fraction * hist[(i + 1 + full) % size] + (1.f - fraction) * hist[(i + full) % size];
+    }
+    const float scan_norm = std::sqrt(Dot(rot.data(), rot.data(), size, scratch.data()));
+    const float normalization = scan_norm * submap_norm;
+    (*out)[a] = normalization < 1e-3f
+                    ? 1.f
+                    : Dot(submap.data(), rot.data(), size, scratch.data()) / normalization;
+  }
+}
+
+// kValueToProbability (probability_values.cc:26-66) and the level-0
+// precomputation value (precomputation_grid_3d.cc:53-56) for every value.
+void ValueTables(std::vector<float>* ptab, std::vector<uint8_t>* qtab) {
+  const float kMinP = 0.1f, kMaxP = 1.f - kMinP;
+  const float scale = (kMaxP - kMinP) / (32768 - 2.f);
+  ptab->resize(32768);
+  qtab->resize(32768);
+  for (int v = 0; v < 32768; ++v) {
+    const float p = v == 0 ? kMinP : v * scale + (kMinP - scale);
+    (*ptab)[v] = p;
+    const int c = LroundF((p - kMinP) * (255.f / (kMaxP - kMinP)));
+    (*qtab)[v] = static_cast<uint8_t>(std::min(255, std::max(0, c)));
+  }
+}
+
+// PrecomputationGrid3D::ToProbability(sum / float(n)) (precomputation_grid_3d.h:32-35).
+float SumToProbability(int64_t sum, int n) {
+  const float kMinP = 0.1f, kMaxP = 1.f - kMinP;
+  return kMinP + (static_cast<float>(sum) / static_cast<float>(n)) * ((kMaxP - kMinP) / 255.f);
+}
+// Smallest sum whose score is > min_score (n * 255 + 1 if none).
+int MinAcceptedSum(float min_score, int n) {
+  int lo = -1, hi = n * 255 + 1;  // score(lo) <= min (virtual), score(hi) > min (virtual)
+  while (hi - lo > 1) {
+    const int mid = lo + (hi - lo) / 2;
+    if (SumToProbability(mid, n) > min_score)
+      hi = mid;
+    else
+      lo = mid;
+  }
+  return hi;
+}
+
+int EnsureDevice3(csm_context* ctx) {
+  return hipSetDevice(ctx->device) == hipSuccess ? CSM_OK : CSM_EHIP;
+}
+
+}  // namespace
+
+// ----------------------------------------------------------- HybridGrid --
+struct csm_hybrid_grid {
+  csm_context* ctx = nullptr;
+  float resolution = 0.f;
+  int32_t grid_size = 0;
+  Brick3 brick{};
+  DevBuf values;  // uint16 brick
+  DevBuf prob;    // float probability brick
+};
+
+int csm_hybrid_grid_create(csm_context* ctx, float resolution, const int32_t* ijk,
+                           const uint16_t* values, int64_t count, int32_t grid_size,
+                           csm_hybrid_grid** out) {
+  if (!ctx || !out || !(resolution > 0.f) || count < 0 || (count > 0 && (!ijk || !values)))
+    return CSM_EINVAL;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  int rc;
+  if ((rc = EnsureDevice3(ctx))) return rc;
+  auto g = std::make_unique<csm_hybrid_grid>();
+  g->ctx = ctx;
+  g->resolution = resolution;
+  int lo[3] = {0, 0, 0}, hi[3] = {-1, -1, -1};
+  for (int64_t i = 0; i < count; ++i)
+    for (int a = 0; a < 3; ++a) {
+      const int v = ijk[3 * i + a];
+      if (i == 0 || v < lo[a]) lo[a] = v;
+      if (i == 0 || v > hi[a]) hi[a] = v;
+    }
+  if (grid_size <= 0) {  // DynamicGrid growth (hybrid_grid.h:283-296, :384-399)
+    int gs = 128;
+    for (int a = 0; a < 3 && count > 0; ++a)
+      while (lo[a] < -(gs / 2) || hi[a] >= gs / 2) gs *= 2;
+    grid_size = gs;
+  }
+  g->grid_size = grid_size;
+  Brick3& b = g->brick;
+  b.ox = lo[0];
+  b.oy = lo[1];
+  b.oz = lo[2];
+  b.nx = count > 0 ? hi[0] - lo[0] + 1 : 0;
+  b.ny = count > 0 ? hi[1] - lo[1] + 1 : 0;
+  b.nz = count > 0 ? hi[2] - lo[2] + 1 : 0;
+  b.offset = 0;
+  const int64_t n = static_cast<int64_t>(b.nx) * b.ny * b.nz;
+  if (n > (int64_t{1} << 31)) return CSM_ERANGE;
+  if (n > 0) {
+    std::vector<uint16_t> dense(static_cast<size_t>(n), 0);
+    for (int64_t i = 0; i < count; ++i) {
+      const int64_t k = (static_cast<int64_t>(ijk[3 * i + 2] - b.oz) * b.ny + (ijk[3 * i + 1] - b.oy)) *
+                            b.nx +
+                        (ijk[3 * i] - b.ox);
+      dense[k] = values[i];
+    }
+    std::vector<float> ptab;
+    std::vector<uint8_t> qtab;
+    ValueTables(&ptab, &qtab);
+    DevBuf dptab;
+    if ((rc = g->values.Reserve(sizeof(uint16_t) * n))) return rc;
+    if ((rc = g->prob.Reserve(sizeof(float) * n))) return rc;
+    if ((rc = dptab.Reserve(sizeof(float) * 32768))) return rc;
+    hipStream_t st = ctx->stream;
+    CSM_HIP(hipMemcpyAsync(g->values.ptr, dense.data(), sizeof(uint16_t) * n,
+                           hipMemcpyHostToDevice, st));
+    CSM_HIP(hipMemcpyAsync(dptab.ptr, ptab.data(), sizeof(float) * 32768, hipMemcpyHostToDevice,
+                           st));
+    CSM_HIP(LaunchBrickFromValues(g->values.as<uint16_t>(), n, dptab.as<float>(), nullptr,
+                                  g->prob.as<float>(), nullptr, st));
+    CSM_HIP(hipStreamSynchronize(st));
+  }
+  *out = g.release();
+  return CSM_OK;
+}
+
+void csm_hybrid_grid_destroy(csm_hybrid_grid* g) {
+  if (!g) return;
+  (void)hipSetDevice(g->ctx->device);
+  delete g;
+}
+
+int csm_hybrid_grid_info(const csm_hybrid_grid* g, int32_t* origin3, int32_t* dims3,
+                         int32_t* grid_size) {
+  if (!g) return CSM_EINVAL;
+  if (origin3) {
+    origin3[0] = g->brick.ox;
+    origin3[1] = g->brick.oy;
+    origin3[2] = g->brick.oz;
+  }
+  if (dims3) {
+    dims3[0] = g->brick.nx;
+    dims3[1] = g->brick.ny;
+    dims3[2] = g->brick.nz;
+  }
+  if (grid_size) *grid_size = g->grid_size;
+  return CSM_OK;
+}
+
+// ------------------------------------------------------------- RTCSM3D --
+int csm_rt3d_match(csm_context* ctx, const csm_rt_options* o, const csm_hybrid_grid* grid,
+                   const csm_pose3d* initial, const float* xyz, int32_t n, float* score,
+                   csm_pose3d* pose) {
+  if (!ctx || !o || !grid || !initial || !score || !pose || n <= 0 || !xyz) return CSM_EINVAL;
+  if (grid->ctx != ctx) return CSM_EINVAL;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  int rc;
+  if ((rc = EnsureDevice3(ctx))) return rc;
+  // GenerateExhaustiveSearchTransforms (real_time_correlative_scan_matcher_3d.cc:55-95).
+  const float res = grid->resolution;
+  const int L = Lround(o->linear_search_window / res);
+  float max_range = 3.f * res;
+  for (int i = 0; i < n; ++i)
+    max_range = std::max(NormV(V3{xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2]}), max_range);
+  const float step = (1.f - 1e-3f) * std::acos(1.f - (res * res) / (2.f * (max_range * max_range)));
+  const int A = Lround(o->angular_search_window / step);
+  if (L < 0 || A < 0 || L > 1000 || A > 1000) return CSM_ERANGE;
+  const int64_t nl = 2 * L + 1, na = 2 * A + 1;
+  const int64_t num_trans = nl * nl * nl, num_rot = na * na * na;
+  if (num_trans * num_rot >= (int64_t{1} << 32) || num_rot > (int64_t{1} << 31)) return CSM_ERANGE;
+  const R3 init = CastF(*initial);
+  std::vector<float4> rot(num_rot);
+  std::vector<float> rot_angle(num_rot);
+  for (int rz = -A; rz <= A; ++rz)
+    for (int ry = -A; ry <= A; ++ry)
+      for (int rx = -A; rx <= A; ++rx) {
+        const int64_t r = ((rz + A) * na + (ry + A)) * na + (rx + A);
+        const Q4 qs = AngleAxisToQuat(V3{static_cast<float>(rx) * step,
+                                         static_cast<float>(ry) * step,
+                                         static_cast<float>(rz) * step});
+        const Q4 q = QNormalized(QMul(init.q, qs));  // initial.cast<float>() * transform
+        rot[r] = make_float4(q.x, q.y, q.z, q.w);
+        rot_angle[r] = GetAngle(qs);
+      }
+  std::vector<float4> trans(num_trans);
+  for (int z = -L; z <= L; ++z)
+    for (int y = -L; y <= L; ++y)
+      for (int x = -L; x <= L; ++x) {
+        const int64_t t = ((z + L) * nl + (y + L)) * nl + (x + L);
+        const V3 tv{static_cast<float>(x) * res, static_cast<float>(y) * res,
+                    static_cast<float>(z) * res};
+        const V3 T = Apply(init, tv);
+        trans[t] = make_float4(T.x, T.y, T.z, NormV(tv));
+      }
+  hipStream_t st = ctx->stream;
+  if ((rc = ctx->rt3_rot.Reserve(sizeof(float4) * num_rot + sizeof(float) * num_rot))) return rc;
+  if ((rc = ctx->rt3_trans.Reserve(sizeof(float4) * num_trans))) return rc;
+  if ((rc = ctx->rt3_points.Reserve(sizeof(float) * 3 * n))) return rc;
+  if ((rc = ctx->rt3_best.Reserve(sizeof(unsigned long long)))) return rc;
+  float4* drot = ctx->rt3_rot.as<float4>();
+  float* dangle = reinterpret_cast<float*>(drot + num_rot);
+  CSM_HIP(hipMemcpyAsync(drot, rot.data(), sizeof(float4) * num_rot, hipMemcpyHostToDevice, st));
+  CSM_HIP(hipMemcpyAsync(dangle, rot_angle.data(), sizeof(float) * num_rot, hipMemcpyHostToDevice,
+                         st));
+  CSM_HIP(hipMemcpyAsync(ctx->rt3_trans.ptr, trans.data(), sizeof(float4) * num_trans,
+                         hipMemcpyHostToDevice, st));
+  CSM_HIP(hipMemcpyAsync(ctx->rt3_points.ptr, xyz, sizeof(float) * 3 * n, hipMemcpyHostToDevice,
+                         st));
+  CSM_HIP(hipMemsetAsync(ctx->rt3_best.ptr, 0, sizeof(unsigned long long), st));
+  if (ctx->timing) CSM_HIP(hipEventRecord(ctx->ev0, st));
+  for (int64_t t0 = 0; t0 < num_trans; t0 += kRt3dThreads) {
+    const int cnt = static_cast<int>(std::min<int64_t>(kRt3dThreads, num_trans - t0));
+    CSM_HIP(LaunchRt3dScore(static_cast<int>(num_rot), st, grid->prob.as<float>(), grid->brick,
+                            res, ctx->rt3_points.as<float>(), n, drot, dangle,
+                            ctx->rt3_trans.as<float4>(), cnt, static_cast<int>(t0),
+                            o->translation_delta_cost_weight, o->rotation_delta_cost_weight,
+                            ctx->rt3_best.as<unsigned long long>()));
+  }
+  if (ctx->timing) CSM_HIP(hipEventRecord(ctx->ev1, st));
+  unsigned long long key = 0;
+  CSM_HIP(hipMemcpyAsync(&key, ctx->rt3_best.ptr, sizeof(key), hipMemcpyDeviceToHost, st));
+  CSM_HIP(hipStreamSynchronize(st));
+  if (ctx->timing) {
+    float ms = 0.f;
+    CSM_HIP(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+    ctx->t.other_kernel_ms += ms;
+    ctx->t.rt3d_kernel_ms += ms;
+    ctx->t.rt3d_lookups += static_cast<double>(num_trans) * num_rot * n;
+  }
+  if (key == 0) return CSM_EHIP;
+  const uint32_t low = static_cast<uint32_t>(key & 0xffffffffu);
+  const uint32_t idx = 0xffffffffu - low;
+  const int64_t t = idx / num_rot, r = idx % num_rot;
+  const uint32_t bits = static_cast<uint32_t>(key >> 32);
+  float s;
+  std::memcpy(&s, &bits, sizeof(s));
+  *score = s;
+  const float4 q = rot[r];
+  const float4 T = trans[t];
+  *pose = ToPose(V3{T.x, T.y, T.z}, Q4{q.w, q.x, q.y, q.z});
+  return CSM_OK;
+}
+
+// ----------------------------------------------------------- FastCSM3D --
+struct csm_fast3d {
+  csm_context* ctx = nullptr;
+  csm_fast3d_options options{};
+  float resolution = 0.f;
+  int32_t width_in_voxels = 0;
+  const csm_hybrid_grid* low = nullptr;
+  std::vector<float> histogram;
+  DevBuf levels;
+  Submap3Desc desc{};
+};
+
+int csm_fast3d_create(csm_context* ctx, const csm_hybrid_grid* high, const csm_hybrid_grid* low,
+                      const float* histogram, int32_t histogram_size,
+                      const csm_fast3d_options* options, csm_fast3d** out) {
+  if (!ctx || !high || !low || !options || !out || histogram_size < 0 ||
+      (histogram_size > 0 && !histogram))
+    return CSM_EINVAL;
+  if (high->ctx != ctx || low->ctx != ctx) return CSM_EINVAL;
+  // fast_correlative_scan_matcher_3d.cc:60-61
+  if (options->branch_and_bound_depth < 1 || options->full_resolution_depth < 1) return CSM_EINVAL;
+  if (options->branch_and_bound_depth > kMaxLevels3d) return CSM_ERANGE;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  int rc;
+  if ((rc = EnsureDevice3(ctx))) return rc;
+  auto m = std::make_unique<csm_fast3d>();
+  m->ctx = ctx;
+  m->options = *options;
+  m->resolution = high->resolution;
+  m->width_in_voxels = high->grid_size;
+  m->low = low;
+  m->histogram.assign(histogram, histogram + histogram_size);
+  // Level boxes (PrecomputationGridStack3D, .cc:57-77): level d covers the
+  // cells its scatter-max can reach from level d-1.
+  const int depth = options->branch_and_bound_depth;
+  Submap3Desc& d = m->desc;
+  d.num_levels = depth;
+  d.full_resolution_depth = options->full_resolution_depth;
+  d.resolution = high->resolution;
+  int64_t total = 0;
+  std::vector<int> shifts(depth, 0), halves(depth, 0);
+  const bool empty = high->brick.nx == 0;
+  d.level[0] = high->brick;
+  int last_width = 1;
+  for (int l = 0; l < depth; ++l) {
+    if (l > 0) {
+      const bool half = l >= options->full_resolution_depth;
+      const int next_width = 1 << l;
+      const int f = 1 << std::max(0, l - options->full_resolution_depth);
+      const int s = (next_width - last_width + (f - 1)) / f;
+      shifts[l] = s;
+      halves[l] = half ? 1 : 0;
+      const Brick3& p = d.level[l - 1];
+      Brick3 b{};
+      if (!empty) {
+        const int lo[3] = {p.ox - s, p.oy - s, p.oz - s};
+        const int hi[3] = {p.ox + p.nx - 1, p.oy + p.ny - 1, p.oz + p.nz - 1};
+        int nlo[3], nhi[3];
+        for (int a = 0; a < 3; ++a) {
+          nlo[a] = half ? (lo[a] >> 1) : lo[a];
+          nhi[a] = half ? (hi[a] >> 1) : hi[a];
+        }
+        b.ox = nlo[0];
+        b.oy = nlo[1];
+        b.oz = nlo[2];
+        b.nx = nhi[0] - nlo[0] + 1;
+        b.ny = nhi[1] - nlo[1] + 1;
+        b.nz = nhi[2] - nlo[2] + 1;
+      }
+      d.level[l] = b;
+      last_width = next_width;
+    }
+    d.level[l].offset = total;
+    const int64_t bytes = static_cast<int64_t>(d.level[l].nx) * d.level[l].ny * d.level[l].nz;
+    if (bytes > (int64_t{1} << 31)) return CSM_ERANGE;
+    total += (bytes + 255) & ~int64_t{255};
+  }
+  if ((rc = m->levels.Reserve(std::max<int64_t>(total, 256)))) return rc;
+  d.levels = m->levels.as<uint8_t>();
+  d.low_prob = low->prob.as<float>();
+  d.low = low->brick;
+  d.low_resolution = low->resolution;
+  hipStream_t st = ctx->stream;
+  if (!empty) {
+    std::vector<float> ptab;
+    std::vector<uint8_t> qtab;
+    ValueTables(&ptab, &qtab);
+    DevBuf dq;
+    if ((rc = dq.Reserve(32768))) return rc;
+    CSM_HIP(hipMemcpyAsync(dq.ptr, qtab.data(), 32768, hipMemcpyHostToDevice, st));
+    const int64_t n0 = static_cast<int64_t>(d.level[0].nx) * d.level[0].ny * d.level[0].nz;
+    CSM_HIP(LaunchBrickFromValues(high->values.as<uint16_t>(), n0, nullptr, dq.as<uint8_t>(),
+                                  nullptr, m->levels.as<uint8_t>() + d.level[0].offset, st));
+    for (int l = 1; l < depth; ++l)
+      CSM_HIP(LaunchLevelGather(m->levels.as<uint8_t>() + d.level[l - 1].offset, d.level[l - 1],
+                                m->levels.as<uint8_t>() + d.level[l].offset, d.level[l], shifts[l],
+                                halves[l], st));
+    CSM_HIP(hipStreamSynchronize(st));
+  }
+  *out = m.release();
+  return CSM_OK;
+}
+
+void csm_fast3d_destroy(csm_fast3d* m) {
+  if (!m) return;
+  (void)hipSetDevice(m->ctx->device);
+  delete m;
+}
+
+int csm_fast3d_read_level(const csm_fast3d* m, int32_t level, uint8_t* out, int64_t capacity,
+                          int32_t* origin3, int32_t* dims3) {
+  if (!m || level < 0 || level >= m->desc.num_levels) return CSM_EINVAL;
+  const Brick3& b = m->desc.level[level];
+  if (origin3) {
+    origin3[0] = b.ox;
+    origin3[1] = b.oy;
+    origin3[2] = b.oz;
+  }
+  if (dims3) {
+    dims3[0] = b.nx;
+    dims3[1] = b.ny;
+    dims3[2] = b.nz;
+  }
+  const int64_t n = static_cast<int64_t>(b.nx) * b.ny * b.nz;
+  if (!out) return CSM_OK;
+  if (capacity < n) return CSM_EINVAL;
+  std::lock_guard<std::mutex> lock(m->ctx->mu);
+  int rc;
+  if ((rc = EnsureDevice3(m->ctx))) return rc;
+  if (n > 0) {
+    CSM_HIP(hipMemcpy(out, m->levels.as<uint8_t>() + b.offset, n, hipMemcpyDeviceToHost));
+  }
+  return CSM_OK;
+}
+
+namespace {
+
+struct PairPrep {
+  Pair3Desc desc{};
+  std::vector<Yaw3Desc> yaws;
+  int status = CSM_OK;
+};
+
+// MatchWithSearchParameters' host half (fast_correlative_scan_matcher_3d.cc
+// :127-199, GenerateDiscreteScans :246-295).
+void PreparePair(const csm_fast3d* m, const csm_node3d& node, const csm_pair3d& p,
+                 PairPrep* out) {
+  const csm_fast3d_options& o = m->options;
+  const float res = m->resolution;
+  const int n = node.num_high_resolution;
+  Pair3Desc& d = out->desc;
+  d.num_points = n;
+  d.num_low = node.num_low_resolution;
+  int wxy, wz;
+  double ang;
+  R3 node_pose, submap_pose;
+  if (p.full_submap) {
+    float maxd = 0.f;
+    for (int i = 0; i < n; ++i)
+      maxd = std::max(maxd, NormV(V3{node.high_resolution_xyz[3 * i],
+                                     node.high_resolution_xyz[3 * i + 1],
+                                     node.high_resolution_xyz[3 * i + 2]}));
+    wxy = wz = (m->width_in_voxels + 1) / 2 + LroundF(maxd / res + 0.5f);
+    ang = M_PI;
+    csm_pose3d a = p.node_pose, b = p.submap_pose;
+    a.t[0] = a.t[1] = a.t[2] = 0.;
+    b.t[0] = b.t[1] = b.t[2] = 0.;
+    node_pose = CastF(a);
+    submap_pose = CastF(b);
+  } else {
+    wxy = Lround(o.linear_xy_search_window / res);
+    wz = Lround(o.linear_z_search_window / res);
+    ang = o.angular_search_window;
+    node_pose = CastF(p.node_pose);
+    submap_pose = CastF(p.submap_pose);
+  }
+  if (wxy > kMax3dWindow || wz > kMax3dWindow || wxy < 0 || wz < 0) {
+    out->status = CSM_ERANGE;
+    return;
+  }
+  d.wxy = wxy;
+  d.wz = wz;
+  const int step = 1 << (m->desc.num_levels - 1);
+  d.top_nx = d.top_ny = (2 * wxy + step) / step;
+  d.top_nz = (2 * wz + step) / step;
+  if (d.top_nx * d.top_ny * d.top_nz > kMax3dTop) {
+    out->status = CSM_ERANGE;
+    return;
+  }
+  d.min_low_resolution_score = static_cast<float>(o.min_low_resolution_score);
+  d.min_sum = MinAcceptedSum(p.min_score, std::max(n, 1));
+  // Angular steps (:258-270).
+  float max_range = 3.f * res;
+  for (int i = 0; i < n; ++i)
+    max_range = std::max(NormV(V3{node.high_resolution_xyz[3 * i], node.high_resolution_xyz[3 * i + 1],
+                                  node.high_resolution_xyz[3 * i + 2]}),
+                         max_range);
+  const float astep = (1.f - 1e-2f) * std::acos(1.f - (res * res) / (2.f * (max_range * max_range)));
+  const int aw = Lround(ang / astep);
+  std::vector<float> angles;
+  for (int rz = -aw; rz <= aw; ++rz) angles.push_back(static_cast<float>(rz) * astep);
+  const R3 node_to_submap = Mul(Inverse(submap_pose), node_pose);
+  // gravity_alignment.inverse().cast<float>() (double Quaternion::inverse).
+  const double* g = node.gravity_alignment;
+  const double gn2 = (g[1] * g[1] + g[3] * g[3]) + (g[2] * g[2] + g[0] * g[0]);
+  Q4 gi{0.f, 0.f, 0.f, 0.f};
+  if (gn2 > 0.)
+    gi = Q4{static_cast<float>(g[0] / gn2), static_cast<float>(-g[1] / gn2),
+            static_cast<float>(-g[2] / gn2), static_cast<float>(-g[3] / gn2)};
+  const float yaw0 = GetYaw(QMul(node_to_submap.q, gi));
+  std::vector<float> scores;
+  RotationalScores(m->histogram, node.histogram, node.histogram_size, yaw0, angles, &scores);
+  const Q4 submap_inv = QInverse(submap_pose.q);
+  for (size_t i = 0; i < angles.size(); ++i) {
+    if (static_cast<double>(scores[i]) < o.min_rotational_score) continue;
+    const Q4 yaw = AngleAxisToQuat(V3{0.f, 0.f, angles[i]});
+    const Q4 q = QMul(QMul(submap_inv, yaw), node_pose.q);
+    const Q4 qn = QNormalized(QMul(Q4{1.f, 0.f, 0.f, 0.f}, q));  // GetPoseFromCandidate
+    Yaw3Desc y{};
+    y.qw = q.w;
+    y.qx = q.x;
+    y.qy = q.y;
+    y.qz = q.z;
+    y.nw = qn.w;
+    y.nx = qn.x;
+    y.ny = qn.y;
+    y.nz = qn.z;
+    y.tx = node_to_submap.t.x;
+    y.ty = node_to_submap.t.y;
+    y.tz = node_to_submap.t.z;
+    y.rotational_score = scores[i];
+    y.yaw_id = static_cast<int32_t>(out->yaws.size());
+    out->yaws.push_back(y);
+  }
+  if (out->yaws.size() > static_cast<size_t>(kMax3dYaws)) out->status = CSM_ERANGE;
+}
+
+}  // namespace
+
+int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t num_submaps,
+                           const csm_node3d* nodes, int32_t num_nodes, const csm_pair3d* pairs,
+                           int64_t num_pairs, csm_result3d* results) {
+  if (!ctx || num_pairs < 0 || (num_pairs > 0 && (!pairs || !results || !submaps || !nodes)))
+    return CSM_EINVAL;
+  for (int i = 0; i < num_submaps; ++i)
+    if (!submaps[i] || submaps[i]->ctx != ctx) return CSM_EINVAL;
+  // Nodes: pack clouds (only nodes some pair references).
+  std::vector<int64_t> hoff(num_nodes, -1), loff(num_nodes, -1);
+  std::vector<float> hpts, lpts;
+  for (int64_t i = 0; i < num_pairs; ++i) {
+    results[i] = csm_result3d{};
+    results[i].status = CSM_NO_MATCH;
+    const csm_pair3d& p = pairs[i];
+    if (p.submap < 0 || p.submap >= num_submaps || p.node < 0 || p.node >= num_nodes) {
+      results[i].status = CSM_EINVAL;
+      continue;
+    }
+    const csm_node3d& nd = nodes[p.node];
+    if (nd.num_high_resolution < 0 || nd.num_low_resolution < 0 ||
+        nd.num_high_resolution > kMax3dPoints || nd.histogram_size < 0) {
+      results[i].status = nd.num_high_resolution > kMax3dPoints ? CSM_ERANGE : CSM_EINVAL;
+      continue;
+    }
+    if (hoff[p.node] < 0) {
+      hoff[p.node] = static_cast<int64_t>(hpts.size() / 3);
+      hpts.insert(hpts.end(), nd.high_resolution_xyz, nd.high_resolution_xyz + 3 * nd.num_high_resolution);
+      loff[p.node] = static_cast<int64_t>(lpts.size() / 3);
+      lpts.insert(lpts.end(), nd.low_resolution_xyz, nd.low_resolution_xyz + 3 * nd.num_low_resolution);
+    }
+  }
+  // Host preparation, parallel over pairs.
+  std::vector<PairPrep> prep(static_cast<size_t>(num_pairs));
+  {
+    std::atomic<int64_t> next{0};
+    const int nt = static_cast<int>(std::max<unsigned>(1, std::min<unsigned>(16, std::thread::hardware_concurrency())));
+    auto work = [&]() {
+      for (;;) {
+        const int64_t i = next.fetch_add(1);
+        if (i >= num_pairs) break;
+        if (results[i].status != CSM_NO_MATCH) continue;
+        const csm_pair3d& p = pairs[i];
+        PreparePair(submaps[p.submap], nodes[p.node], p, &prep[i]);
+      }
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < std::min<int64_t>(nt, num_pairs); ++t) pool.emplace_back(work);
+    work();
+    for (auto& t : pool) t.join();
+  }
+  std::vector<Submap3Desc> sdesc(num_submaps);
+  for (int i = 0; i < num_submaps; ++i) sdesc[i] = submaps[i]->desc;
+  std::vector<Pair3Desc> pdesc;
+  std::vector<Yaw3Desc> ydesc;
+  std::vector<int64_t> pair_of;  // device pair index -> input pair
+  for (int64_t i = 0; i < num_pairs; ++i) {
+    if (results[i].status != CSM_NO_MATCH) continue;
+    if (prep[i].status != CSM_OK) {
+      results[i].status = prep[i].status;
+      continue;
+    }
+    if (pairs[i].min_score >= 1.f || nodes[pairs[i].node].num_high_resolution == 0) continue;
+    Pair3Desc d = prep[i].desc;
+    d.submap = pairs[i].submap;
+    d.point_offset = hoff[pairs[i].node];
+    d.low_offset = loff[pairs[i].node];
+    d.yaw_begin = static_cast<int32_t>(ydesc.size());
+    d.num_yaws = static_cast<int32_t>(prep[i].yaws.size());
+    const int32_t dp = static_cast<int32_t>(pdesc.size());
+    for (Yaw3Desc y : prep[i].yaws) {
+      y.pair = dp;
+      ydesc.push_back(y);
+    }
+    pdesc.push_back(d);
+    pair_of.push_back(i);
+  }
+  const int np = static_cast<int>(pdesc.size());
+  if (np == 0) return CSM_OK;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  int rc;
+  if ((rc = EnsureDevice3(ctx))) return rc;
+  hipStream_t st = ctx->stream;
+  const int ny = static_cast<int>(ydesc.size());
+  if ((rc = ctx->f3_pairs.Reserve(sizeof(Pair3Desc) * np + sizeof(Submap3Desc) * num_submaps)))
+    return rc;
+  if ((rc = ctx->f3_yaws.Reserve(sizeof(Yaw3Desc) * std::max(ny, 1)))) return rc;
+  if ((rc = ctx->f3_points.Reserve(sizeof(float) * std::max<size_t>(hpts.size(), 3)))) return rc;
+  if ((rc = ctx->f3_low_points.Reserve(sizeof(float) * std::max<size_t>(lpts.size(), 3)))) return rc;
+  if ((rc = ctx->f3_best.Reserve(sizeof(unsigned long long) * np + sizeof(float) * np))) return rc;
+  if ((rc = ctx->f3_status.Reserve(sizeof(int32_t) * np))) return rc;
+  if ((rc = ctx->f3_counter.Reserve(sizeof(unsigned) + sizeof(unsigned long long)))) return rc;
+  Pair3Desc* dpairs = ctx->f3_pairs.as<Pair3Desc>();
+  Submap3Desc* dsub = reinterpret_cast<Submap3Desc*>(dpairs + np);
+  unsigned long long* dbest = ctx->f3_best.as<unsigned long long>();
+  float* dlow = reinterpret_cast<float*>(dbest + np);
+  unsigned* dcounter = ctx->f3_counter.as<unsigned>();
+  unsigned long long* dstats = reinterpret_cast<unsigned long long*>(
+      reinterpret_cast<char*>(ctx->f3_counter.ptr) + 8);
+  CSM_HIP(hipMemcpyAsync(dpairs, pdesc.data(), sizeof(Pair3Desc) * np, hipMemcpyHostToDevice, st));
+  CSM_HIP(hipMemcpyAsync(dsub, sdesc.data(), sizeof(Submap3Desc) * num_submaps,
+                         hipMemcpyHostToDevice, st));
+  if (ny > 0)
+    CSM_HIP(hipMemcpyAsync(ctx->f3_yaws.ptr, ydesc.data(), sizeof(Yaw3Desc) * ny,
+                           hipMemcpyHostToDevice, st));
+  if (!hpts.empty())
+    CSM_HIP(hipMemcpyAsync(ctx->f3_points.ptr, hpts.data(), sizeof(float) * hpts.size(),
+                           hipMemcpyHostToDevice, st));
+  if (!lpts.empty())
+    CSM_HIP(hipMemcpyAsync(ctx->f3_low_points.ptr, lpts.data(), sizeof(float) * lpts.size(),
+                           hipMemcpyHostToDevice, st));
+  CSM_HIP(hipMemsetAsync(dbest, 0, sizeof(unsigned long long) * np, st));
+  CSM_HIP(hipMemsetAsync(ctx->f3_status.ptr, 0, sizeof(int32_t) * np, st));
+  CSM_HIP(hipMemsetAsync(ctx->f3_counter.ptr, 0, 16, st));
+  if (ctx->timing) CSM_HIP(hipEventRecord(ctx->ev0, st));
+  if (ny > 0) {
+    const int grid = std::max(1, std::min(ny, ctx->num_cus * 2));
+    CSM_HIP(LaunchFast3dSearch(grid, st, dsub, dpairs, ctx->f3_yaws.as<Yaw3Desc>(), ny,
+                               ctx->f3_points.as<float>(), ctx->f3_low_points.as<float>(),
+                               dcounter, dbest, ctx->f3_status.as<int32_t>(), dstats));
+  }
+  if (ctx->timing) CSM_HIP(hipEventRecord(ctx->ev1, st));
+  CSM_HIP(LaunchFast3dFinalize(np, st, dsub, dpairs, ctx->f3_yaws.as<Yaw3Desc>(),
+                               ctx->f3_low_points.as<float>(), dbest, dlow));
+  std::vector<unsigned long long> keys(np);
+  std::vector<float> lows(np);
+  std::vector<int32_t> stat(np);
+  unsigned long long lookups = 0;
+  CSM_HIP(hipMemcpyAsync(keys.data(), dbest, sizeof(unsigned long long) * np,
+                         hipMemcpyDeviceToHost, st));
+  CSM_HIP(hipMemcpyAsync(lows.data(), dlow, sizeof(float) * np, hipMemcpyDeviceToHost, st));
+  CSM_HIP(hipMemcpyAsync(stat.data(), ctx->f3_status.ptr, sizeof(int32_t) * np,
+                         hipMemcpyDeviceToHost, st));
+  CSM_HIP(hipMemcpyAsync(&lookups, dstats, sizeof(lookups), hipMemcpyDeviceToHost, st));
+  CSM_HIP(hipStreamSynchronize(st));
+  if (ctx->timing) {
+    float ms = 0.f;
+    CSM_HIP(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+    ctx->t.fast3d_kernel_ms += ms;
+    ctx->t.fast3d_launches += 1;
+    ctx->t.fast3d_lookups += static_cast<double>(lookups);
+  }
+  // Decode (GetPoseFromCandidate :369-375, Result :193-198).
+  for (int dp = 0; dp < np; ++dp) {
+    const int64_t i = pair_of[dp];
+    const Pair3Desc& d = pdesc[dp];
+    if (stat[dp] < 0) {
+      results[i].status = stat[dp];
+      continue;
+    }
+    const unsigned long long key = keys[dp];
+    if (key == 0) continue;
+    const unsigned long long id = ~key & ((1ull << kKeyShift3d) - 1);
+    const int sum = static_cast<int>(key >> kKeyShift3d);
+    const int yaw = static_cast<int>(id >> 30);
+    const int ox = static_cast<int>((id >> 20) & 1023) - d.wxy;
+    const int oy = static_cast<int>((id >> 10) & 1023) - d.wxy;
+    const int oz = static_cast<int>(id & 1023) - d.wz;
+    const Yaw3Desc& y = ydesc[d.yaw_begin + yaw];
+    const float res = submaps[d.submap]->resolution;
+    const V3 t0 = Rotate(Q4{1.f, 0.f, 0.f, 0.f}, V3{y.tx, y.ty, y.tz});
+    const V3 t{t0.x + res * static_cast<float>(ox), t0.y + res * static_cast<float>(oy),
+               t0.z + res * static_cast<float>(oz)};
+    results[i].status = CSM_OK;
+    results[i].score = SumToProbability(sum, d.num_points);
+    results[i].pose = ToPose(t, Q4{y.nw, y.nx, y.ny, y.nz});
+    results[i].rotational_score = y.rotational_score;
+    results[i].low_resolution_score = lows[dp];
+  }
+  return CSM_OK;
+}
+
+int csm_fast3d_match(const csm_fast3d* m, const csm_pose3d* node_pose,
+                     const csm_pose3d* submap_pose, const csm_node3d* node, float min_score,
+                     csm_result3d* result) {
+  if (!m || !node_pose || !submap_pose || !node || !result) return CSM_EINVAL;
+  csm_pair3d p{};
+  p.submap = 0;
+  p.node = 0;
+  p.full_submap = 0;
+  p.min_score = min_score;
+  p.node_pose = *node_pose;
+  p.submap_pose = *submap_pose;
+  csm_fast3d* h = const_cast<csm_fast3d*>(m);
+  const int rc = csm_fast3d_match_batch(m->ctx, &h, 1, node, 1, &p, 1, result);
+  if (rc < 0) return rc;
+  return result->status;
+}
+
+int csm_fast3d_match_full_submap(const csm_fast3d* m, const double* node_rotation,
+                                 const double* submap_rotation, const csm_node3d* node,
+                                 float min_score, csm_result3d* result) {
+  if (!m || !node_rotation || !submap_rotation || !node || !result) return CSM_EINVAL;
+  csm_pair3d p{};
+  p.full_submap = 1;
+  p.min_score = min_score;
+  for (int k = 0; k < 4; ++k) {
+    p.node_pose.q[k] = node_rotation[k];
+    p.submap_pose.q[k] = submap_rotation[k];
+  }
+  csm_fast3d* h = const_cast<csm_fast3d*>(m);
+  const int rc = csm_fast3d_match_batch(m->ctx, &h, 1, node, 1, &p, 1, result);
+  if (rc < 0) return rc;
+  return result->status;
+}

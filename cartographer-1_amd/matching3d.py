@@ -1,0 +1,225 @@
+"""3D correlative scan matchers — Python mirror of the 3D C-ABI.
+
+* :class:`HybridGrid` — a HybridGrid's known cells on the device
+  (``mapping/3d/hybrid_grid.h:463-545``; cells as the iterator / ToProto yields them).
+* :class:`RealTimeCorrelativeScanMatcher3D` — ``Match``
+  (``real_time_correlative_scan_matcher_3d.h:47-50``).
+* :class:`FastCorrelativeScanMatcher3D` — ``Match`` / ``MatchFullSubmap``
+  (``fast_correlative_scan_matcher_3d.h:75-101``), results as
+  ``FastCorrelativeScanMatcher3D::Result`` or ``None`` (the reference's nullptr).
+* :func:`match_batch_3d` — the batched ConstraintBuilder3D search.
+
+Every compute call runs the HIP kernels; there is no CPU fallback.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import math
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from . import (CSM_OK, Context, Fast3DOptions, Node3D, Pair3D, Pose3D, Result3D, RtOptions,
+               _check, _f32_points, _ptr, default_context)
+
+
+class HybridGrid:
+    """Known cells of a HybridGrid: ``indices`` (n, 3) int and uint16 ``values``."""
+
+    def __init__(self, resolution: float, indices, values, grid_size: int = 0,
+                 context: Optional[Context] = None):
+        self.context = context or default_context()
+        self._lib = self.context._lib
+        self.resolution = float(resolution)
+        idx = np.ascontiguousarray(np.asarray(indices, np.int32).reshape(-1, 3))
+        val = np.ascontiguousarray(np.asarray(values, np.uint16).reshape(-1))
+        if len(idx) != len(val):
+            raise ValueError("indices and values differ in length")
+        h = C.c_void_p()
+        _check(self._lib.csm_hybrid_grid_create(self.context.handle, self.resolution,
+                                                _ptr(idx, C.c_int32), _ptr(val, C.c_uint16),
+                                                len(val), int(grid_size), C.byref(h)),
+               "csm_hybrid_grid_create")
+        self.handle = h
+
+    def info(self):
+        o, d, g = (C.c_int32 * 3)(), (C.c_int32 * 3)(), C.c_int32()
+        _check(self._lib.csm_hybrid_grid_info(self.handle, o, d, C.byref(g)), "csm_hybrid_grid_info")
+        return tuple(o), tuple(d), g.value
+
+    def close(self):
+        if getattr(self, "handle", None):
+            self._lib.csm_hybrid_grid_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _pose(p) -> Pose3D:
+    if isinstance(p, Pose3D):
+        return p
+    t, q = p
+    return Pose3D.make(t, q)
+
+
+class RealTimeCorrelativeScanMatcher3D:
+    def __init__(self, options, context: Optional[Context] = None):
+        self.context = context or default_context()
+        self._lib = self.context._lib
+        self.options = options
+
+    def Match(self, initial_pose_estimate, point_cloud, grid: HybridGrid):
+        """-> (score, ((tx, ty, tz), (qw, qx, qy, qz)))."""
+        o = self.options
+        opts = RtOptions(o.linear_search_window, o.angular_search_window,
+                         o.translation_delta_cost_weight, o.rotation_delta_cost_weight)
+        pts = _f32_points(point_cloud)
+        init = _pose(initial_pose_estimate)
+        score = C.c_float()
+        out = Pose3D()
+        _check(self._lib.csm_rt3d_match(self.context.handle, C.byref(opts), grid.handle,
+                                        C.byref(init), _ptr(pts, C.c_float), len(pts),
+                                        C.byref(score), C.byref(out)), "csm_rt3d_match")
+        return float(score.value), out.as_tuple()
+
+
+@dataclass
+class FastCorrelativeScanMatcherOptions3D:
+    """proto::FastCorrelativeScanMatcherOptions3D; defaults from
+    configuration_files/pose_graph.lua:40-48."""
+    branch_and_bound_depth: int = 8
+    full_resolution_depth: int = 3
+    min_rotational_score: float = 0.77
+    min_low_resolution_score: float = 0.55
+    linear_xy_search_window: float = 5.0
+    linear_z_search_window: float = 1.0
+    angular_search_window: float = math.radians(15.0)
+
+    def to_c(self) -> Fast3DOptions:
+        return Fast3DOptions(self.branch_and_bound_depth, self.full_resolution_depth,
+                             self.min_rotational_score, self.min_low_resolution_score,
+                             self.linear_xy_search_window, self.linear_z_search_window,
+                             self.angular_search_window)
+
+
+@dataclass
+class NodeData3D:
+    """The TrajectoryNode::Data fields the 3D matcher reads."""
+    high_resolution_point_cloud: np.ndarray
+    low_resolution_point_cloud: np.ndarray
+    rotational_scan_matcher_histogram: np.ndarray
+    gravity_alignment: tuple = (1.0, 0.0, 0.0, 0.0)
+    _keep: list = field(default_factory=list, repr=False)
+
+    def to_c(self) -> Node3D:
+        hi = _f32_points(self.high_resolution_point_cloud)
+        lo = _f32_points(self.low_resolution_point_cloud)
+        hist = np.ascontiguousarray(np.asarray(self.rotational_scan_matcher_histogram, np.float32))
+        self._keep = [hi, lo, hist]
+        n = Node3D()
+        n.high_resolution_xyz = _ptr(hi, C.c_float)
+        n.num_high_resolution = len(hi)
+        n.low_resolution_xyz = _ptr(lo, C.c_float)
+        n.num_low_resolution = len(lo)
+        n.histogram = _ptr(hist, C.c_float)
+        n.histogram_size = len(hist)
+        n.gravity_alignment[:] = [float(v) for v in self.gravity_alignment]
+        return n
+
+
+@dataclass
+class Result:
+    """FastCorrelativeScanMatcher3D::Result."""
+    score: float
+    pose_estimate: tuple
+    rotational_score: float
+    low_resolution_score: float
+
+
+def _result(r: Result3D) -> Optional[Result]:
+    _check(r.status, "FastCorrelativeScanMatcher3D")
+    if r.status != CSM_OK:
+        return None
+    return Result(float(r.score), r.pose.as_tuple(), float(r.rotational_score),
+                  float(r.low_resolution_score))
+
+
+class FastCorrelativeScanMatcher3D:
+    def __init__(self, hybrid_grid: HybridGrid, low_resolution_grid: HybridGrid,
+                 histogram, options: FastCorrelativeScanMatcherOptions3D,
+                 context: Optional[Context] = None):
+        self.context = context or default_context()
+        self._lib = self.context._lib
+        self.options = options
+        self.low_resolution_grid = low_resolution_grid  # must outlive the matcher
+        hist = np.ascontiguousarray(np.asarray(histogram, np.float32))
+        opts = options.to_c()
+        h = C.c_void_p()
+        _check(self._lib.csm_fast3d_create(self.context.handle, hybrid_grid.handle,
+                                           low_resolution_grid.handle, _ptr(hist, C.c_float),
+                                           len(hist), C.byref(opts), C.byref(h)),
+               "csm_fast3d_create")
+        self.handle = h
+
+    def close(self):
+        if getattr(self, "handle", None):
+            self._lib.csm_fast3d_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def read_level(self, level: int):
+        o, d = (C.c_int32 * 3)(), (C.c_int32 * 3)()
+        _check(self._lib.csm_fast3d_read_level(self.handle, level, None, 0, o, d),
+               "csm_fast3d_read_level")
+        out = np.zeros(int(d[0]) * int(d[1]) * int(d[2]), np.uint8)
+        _check(self._lib.csm_fast3d_read_level(self.handle, level, _ptr(out, C.c_uint8), out.size,
+                                               o, d), "csm_fast3d_read_level")
+        return tuple(o), out.reshape(int(d[2]), int(d[1]), int(d[0]))
+
+    def Match(self, global_node_pose, global_submap_pose, node: NodeData3D, min_score: float):
+        n = node.to_c()
+        r = Result3D()
+        _check(self._lib.csm_fast3d_match(self.handle, C.byref(_pose(global_node_pose)),
+                                          C.byref(_pose(global_submap_pose)), C.byref(n),
+                                          min_score, C.byref(r)), "csm_fast3d_match")
+        return _result(r)
+
+    def MatchFullSubmap(self, global_node_rotation, global_submap_rotation, node: NodeData3D,
+                        min_score: float):
+        n = node.to_c()
+        a = (C.c_double * 4)(*[float(v) for v in global_node_rotation])
+        b = (C.c_double * 4)(*[float(v) for v in global_submap_rotation])
+        r = Result3D()
+        _check(self._lib.csm_fast3d_match_full_submap(self.handle, a, b, C.byref(n), min_score,
+                                                      C.byref(r)), "csm_fast3d_match_full_submap")
+        return _result(r)
+
+
+def match_batch_3d(matchers: Sequence[FastCorrelativeScanMatcher3D], nodes: Sequence[NodeData3D],
+                   pairs: Sequence[tuple], context: Optional[Context] = None) -> List[Result3D]:
+    """pairs: (submap, node, full_submap, min_score, node_pose, submap_pose)."""
+    ctx = context or (matchers[0].context if matchers else default_context())
+    lib = ctx._lib
+    cnodes = (Node3D * len(nodes))(*[n.to_c() for n in nodes])
+    cpairs = (Pair3D * len(pairs))()
+    for i, (s, n, full, ms, npose, spose) in enumerate(pairs):
+        cpairs[i].submap, cpairs[i].node, cpairs[i].full_submap = s, n, 1 if full else 0
+        cpairs[i].min_score = ms
+        cpairs[i].node_pose = _pose(npose)
+        cpairs[i].submap_pose = _pose(spose)
+    results = (Result3D * len(pairs))()
+    handles = (C.c_void_p * len(matchers))(*[m.handle for m in matchers])
+    _check(lib.csm_fast3d_match_batch(ctx.handle, handles, len(matchers), cnodes, len(nodes),
+                                      cpairs, len(pairs), results), "csm_fast3d_match_batch")
+    return list(results)

@@ -89,6 +89,13 @@ typedef struct csm_timing {
   double search_lookups;   /* candidates scored x points */
   double search_candidates;
   double other_kernel_ms;
+  /* 3D: RTCSM3D scoring kernel time and lookups (candidates x points);
+   * FastCSM3D search kernel time, launches and pyramid lookups. */
+  double rt3d_kernel_ms;
+  double rt3d_lookups;
+  double fast3d_kernel_ms;
+  int64_t fast3d_launches;
+  double fast3d_lookups;
 } csm_timing;
 void csm_context_enable_timing(csm_context* ctx, int32_t enable);
 void csm_context_get_timing(csm_context* ctx, csm_timing* out);
@@ -172,6 +179,120 @@ int csm_rt2d_match(csm_context* ctx, const csm_rt_options* options,
                    float min_correspondence_cost, float max_correspondence_cost,
                    const csm_pose2d* initial, const float* points_xyz,
                    int32_t n, double* score, csm_pose2d* pose);
+
+/* ---- 3D: HybridGrid ----------------------------------------------------------
+ * A HybridGrid (mapping/3d/hybrid_grid.h:463-545) crosses the boundary as the
+ * list its iterator / ToProto yields (hybrid_grid.h:530-541): cell indices
+ * (x, y, z) and uint16 probability values. The device keeps a dense brick
+ * over the known cells' bounding box; outside it the value is 0 (unknown,
+ * probability kMinProbability), as DynamicGrid::value returns for cells never
+ * set (:260-279). `grid_size` is DynamicGrid::grid_size() of the source grid
+ * (FastCorrelativeScanMatcher3D's width_in_voxels, .cc:120); 0 = derive it from
+ * the indices with DynamicGrid's growth rule (128 << k, indices in
+ * [-size/2, size/2)). The cells are copied. */
+typedef struct csm_hybrid_grid csm_hybrid_grid;
+int csm_hybrid_grid_create(csm_context* ctx, float resolution, const int32_t* xyz_indices,
+                           const uint16_t* values, int64_t count, int32_t grid_size,
+                           csm_hybrid_grid** out);
+void csm_hybrid_grid_destroy(csm_hybrid_grid* g);
+/* Bounding box origin / extent of the device brick and the grid size. */
+int csm_hybrid_grid_info(const csm_hybrid_grid* g, int32_t* origin3, int32_t* dims3,
+                         int32_t* grid_size);
+
+/* transform::Rigid3d: translation and rotation quaternion (w, x, y, z). */
+typedef struct csm_pose3d {
+  double t[3];
+  double q[4];
+} csm_pose3d;
+
+/* ---- RealTimeCorrelativeScanMatcher3D ----------------------------------------
+ * float Match(const Rigid3d& initial_pose_estimate, const PointCloud&,
+ *             const HybridGrid&, Rigid3d* pose_estimate) const
+ *   (real_time_correlative_scan_matcher_3d.h:47-50, .cc:34-54). */
+int csm_rt3d_match(csm_context* ctx, const csm_rt_options* options, const csm_hybrid_grid* grid,
+                   const csm_pose3d* initial, const float* points_xyz, int32_t n, float* score,
+                   csm_pose3d* pose);
+
+/* ---- FastCorrelativeScanMatcher3D --------------------------------------------
+ * proto::FastCorrelativeScanMatcherOptions3D
+ * (proto/scan_matching/fast_correlative_scan_matcher_options_3d.proto). */
+typedef struct csm_fast3d_options {
+  int32_t branch_and_bound_depth;
+  int32_t full_resolution_depth;
+  double min_rotational_score;
+  double min_low_resolution_score;
+  double linear_xy_search_window;
+  double linear_z_search_window;
+  double angular_search_window;
+} csm_fast3d_options;
+
+typedef struct csm_fast3d csm_fast3d;
+
+/* FastCorrelativeScanMatcher3D(const HybridGrid&, const HybridGrid* low_res,
+ *   const Eigen::VectorXf* histogram, const Options3D&)
+ *   (fast_correlative_scan_matcher_3d.h:75-79, .cc:112-123). The pyramid
+ * (PrecomputationGridStack3D, .cc:57-77) is built on the device from
+ * `high_resolution`; the histogram is copied. As in the reference (which keeps
+ * raw pointers, .h:149-150) `low_resolution` must outlive the matcher. */
+int csm_fast3d_create(csm_context* ctx, const csm_hybrid_grid* high_resolution,
+                      const csm_hybrid_grid* low_resolution, const float* histogram,
+                      int32_t histogram_size, const csm_fast3d_options* options,
+                      csm_fast3d** out);
+void csm_fast3d_destroy(csm_fast3d* m);
+/* Test-visible: copies pyramid level `level` (dense brick, x fastest). */
+int csm_fast3d_read_level(const csm_fast3d* m, int32_t level, uint8_t* out, int64_t capacity,
+                          int32_t* origin3, int32_t* dims3);
+
+/* The parts of TrajectoryNode::Data the matcher reads (trajectory_node.h):
+ * high/low resolution point clouds, the rotational histogram and the
+ * gravity alignment (w, x, y, z). */
+typedef struct csm_node3d {
+  const float* high_resolution_xyz;
+  int32_t num_high_resolution;
+  const float* low_resolution_xyz;
+  int32_t num_low_resolution;
+  const float* histogram;
+  int32_t histogram_size;
+  double gravity_alignment[4];
+} csm_node3d;
+
+/* FastCorrelativeScanMatcher3D::Result (fast_correlative_scan_matcher_3d.h:68-73). */
+typedef struct csm_result3d {
+  int32_t status; /* CSM_OK, CSM_NO_MATCH (the reference's nullptr) or error */
+  float score;
+  csm_pose3d pose;
+  float rotational_score;
+  float low_resolution_score;
+} csm_result3d;
+
+/* std::unique_ptr<Result> Match(const Rigid3d& global_node_pose,
+ *   const Rigid3d& global_submap_pose, const TrajectoryNode::Data&, float min_score)
+ *   (fast_correlative_scan_matcher_3d.h:89-92, .cc:127-143). */
+int csm_fast3d_match(const csm_fast3d* m, const csm_pose3d* global_node_pose,
+                     const csm_pose3d* global_submap_pose, const csm_node3d* node,
+                     float min_score, csm_result3d* result);
+/* std::unique_ptr<Result> MatchFullSubmap(const Quaterniond& global_node_rotation,
+ *   const Quaterniond& global_submap_rotation, const TrajectoryNode::Data&, float)
+ *   (fast_correlative_scan_matcher_3d.h:98-101, .cc:145-170). Rotations (w,x,y,z). */
+int csm_fast3d_match_full_submap(const csm_fast3d* m, const double* global_node_rotation,
+                                 const double* global_submap_rotation, const csm_node3d* node,
+                                 float min_score, csm_result3d* result);
+
+/* Batched 3D constraint search (ConstraintBuilder3D tasks,
+ * constraint_builder_3d.cc:200-305): results in pair order. For full_submap
+ * pairs only the rotations of the two poses are used. */
+typedef struct csm_pair3d {
+  int32_t submap;
+  int32_t node;
+  int32_t full_submap;
+  float min_score;
+  csm_pose3d node_pose;
+  csm_pose3d submap_pose;
+} csm_pair3d;
+
+int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t num_submaps,
+                           const csm_node3d* nodes, int32_t num_nodes, const csm_pair3d* pairs,
+                           int64_t num_pairs, csm_result3d* results);
 
 /* Human-readable text for a return code. */
 const char* csm_strerror(int code);

@@ -159,3 +159,180 @@ class OracleFast2D:
                                                      C.byref(sc))
         assert r == 0
         return s.value, sc.value
+
+
+# ---------------------------------------------------------------------- 3D --
+_SIG3D = {
+    "oracle_hgrid_create": (VP, [F]),
+    "oracle_hgrid_destroy": (None, [VP]),
+    "oracle_hgrid_set_probability": (None, [VP, I32, I32, I32, F]),
+    "oracle_hgrid_insert": (None, [VP, F, F, I32, P(F), P(F), I32]),
+    "oracle_hgrid_cells": (I64, [VP, P(I32), P(C.c_uint16), I64]),
+    "oracle_hgrid_grid_size": (I32, [VP]),
+    "oracle_hgrid_probability": (F, [VP, I32, I32, I32]),
+    "oracle_histogram": (None, [P(F), I32, I32, P(F)]),
+    "oracle_rotational_match": (None, [P(F), P(F), I32, F, P(F), I32, P(F)]),
+    "oracle_fast3d_create": (VP, [VP, VP, P(F), I32, P(D)]),
+    "oracle_fast3d_destroy": (None, [VP]),
+    "oracle_fast3d_level": (I64, [VP, I32, P(I32), P(C.c_uint8), I64]),
+    "oracle_fast3d_match": (None, [VP, P(D), P(D), P(F), I32, P(F), I32, P(F), I32, P(D), F,
+                                   P(D)]),
+    "oracle_fast3d_match_full_submap": (None, [VP, P(D), P(D), P(F), I32, P(F), I32, P(F), I32,
+                                               P(D), F, P(D)]),
+    "oracle_rt3d_match": (None, [VP, P(D), P(D), P(F), I32, P(D)]),
+    "oracle_rt3d_score": (F, [VP, P(D), P(D), P(F), I32, I64, P(D)]),
+    "oracle_rt3d_window": (None, [P(D), F, P(F), I32, P(I32), P(F), P(I32)]),
+}
+
+
+def _pose7(t=(0, 0, 0), q=(1, 0, 0, 0)):
+    return np.array(list(t) + list(q), np.float64)
+
+
+class OracleHybridGrid:
+    def __init__(self, o, resolution):
+        self.o = o
+        self.resolution = resolution
+        self.h = o.lib.oracle_hgrid_create(resolution)
+
+    def __del__(self):
+        try:
+            self.o.lib.oracle_hgrid_destroy(self.h)
+        except Exception:
+            pass
+
+    def set_probability(self, x, y, z, p):
+        self.o.lib.oracle_hgrid_set_probability(self.h, x, y, z, p)
+
+    def insert(self, origin, returns, hit=0.7, miss=0.4, num_free_space_voxels=5):
+        org = np.asarray(origin, np.float32)
+        r = np.ascontiguousarray(returns, np.float32).reshape(-1, 3)
+        self.o.lib.oracle_hgrid_insert(self.h, hit, miss, num_free_space_voxels, _p(org, F),
+                                       _p(r, F), len(r))
+
+    def cells(self):
+        n = self.o.lib.oracle_hgrid_cells(self.h, None, None, 0)
+        ijk = np.zeros((n, 3), np.int32)
+        v = np.zeros(n, np.uint16)
+        self.o.lib.oracle_hgrid_cells(self.h, _p(ijk, I32), _p(v, C.c_uint16), n)
+        return ijk, v
+
+    @property
+    def grid_size(self):
+        return self.o.lib.oracle_hgrid_grid_size(self.h)
+
+    def probability(self, x, y, z):
+        return self.o.lib.oracle_hgrid_probability(self.h, x, y, z)
+
+
+class OracleFast3D:
+    def __init__(self, o, high, low, histogram, options):
+        self.o, self.high, self.low = o, high, low
+        self.hist = np.ascontiguousarray(histogram, np.float32)
+        opts = np.array(options, np.float64)
+        self.h = o.lib.oracle_fast3d_create(high.h, low.h, _p(self.hist, F), len(self.hist),
+                                            _p(opts, D))
+
+    def __del__(self):
+        try:
+            self.o.lib.oracle_fast3d_destroy(self.h)
+        except Exception:
+            pass
+
+    def level(self, d):
+        n = self.o.lib.oracle_fast3d_level(self.h, d, None, None, 0)
+        ijk = np.zeros((n, 3), np.int32)
+        v = np.zeros(n, np.uint8)
+        self.o.lib.oracle_fast3d_level(self.h, d, _p(ijk, I32), _p(v, C.c_uint8), n)
+        return ijk, v
+
+    @staticmethod
+    def _node(node):
+        hi = np.ascontiguousarray(node.high_resolution_point_cloud, np.float32).reshape(-1, 3)
+        lo = np.ascontiguousarray(node.low_resolution_point_cloud, np.float32).reshape(-1, 3)
+        hist = np.ascontiguousarray(node.rotational_scan_matcher_histogram, np.float32)
+        g = np.asarray(node.gravity_alignment, np.float64)
+        return hi, lo, hist, g
+
+    @staticmethod
+    def _out(out):
+        return {"matched": bool(out[0]), "score": float(np.float32(out[1])),
+                "rotational_score": float(np.float32(out[2])),
+                "low_resolution_score": float(np.float32(out[3])),
+                "pose": (tuple(out[4:7]), tuple(out[7:11])), "lookups": int(out[11]),
+                "low_resolution_checks": int(out[12]), "num_discrete_scans": int(out[13])}
+
+    def match(self, node_pose, submap_pose, node, min_score):
+        hi, lo, hist, g = self._node(node)
+        a = _pose7(*node_pose)
+        b = _pose7(*submap_pose)
+        out = np.zeros(14)
+        self.o.lib.oracle_fast3d_match(self.h, _p(a, D), _p(b, D), _p(hi, F), len(hi), _p(lo, F),
+                                       len(lo), _p(hist, F), len(hist), _p(g, D), min_score,
+                                       _p(out, D))
+        return self._out(out)
+
+    def match_full_submap(self, node_q, submap_q, node, min_score):
+        hi, lo, hist, g = self._node(node)
+        a = np.asarray(node_q, np.float64)
+        b = np.asarray(submap_q, np.float64)
+        out = np.zeros(14)
+        self.o.lib.oracle_fast3d_match_full_submap(self.h, _p(a, D), _p(b, D), _p(hi, F), len(hi),
+                                                   _p(lo, F), len(lo), _p(hist, F), len(hist),
+                                                   _p(g, D), min_score, _p(out, D))
+        return self._out(out)
+
+
+def _bind3d(lib):
+    for name, (res, args) in _SIG3D.items():
+        fn = getattr(lib, name)
+        fn.restype, fn.argtypes = res, args
+
+
+def _o3_hgrid(self, resolution):
+    if not getattr(self, "_bound3d", False):
+        _bind3d(self.lib)
+        self._bound3d = True
+    return OracleHybridGrid(self, resolution)
+
+
+def _o3_fast3d(self, high, low, histogram, options):
+    _o3_hgrid(self, 1.0)  # binds
+    return OracleFast3D(self, high, low, histogram, options)
+
+
+def _o3_histogram(self, cloud, size):
+    _o3_hgrid(self, 1.0)
+    pts = np.ascontiguousarray(cloud, np.float32).reshape(-1, 3)
+    out = np.zeros(size, np.float32)
+    self.lib.oracle_histogram(_p(pts, F), len(pts), size, _p(out, F))
+    return out
+
+
+def _o3_rt3d_match(self, grid, options, initial, cloud):
+    _o3_hgrid(self, 1.0)
+    pts = np.ascontiguousarray(cloud, np.float32).reshape(-1, 3)
+    o = np.asarray(options, np.float64)
+    init = _pose7(*initial)
+    out = np.zeros(10)
+    self.lib.oracle_rt3d_match(grid.h, _p(o, D), _p(init, D), _p(pts, F), len(pts), _p(out, D))
+    return (float(np.float32(out[0])), (tuple(out[1:4]), tuple(out[4:8])), int(out[8]),
+            int(out[9]))
+
+
+def _o3_rt3d_score(self, grid, options, initial, cloud, index):
+    _o3_hgrid(self, 1.0)
+    pts = np.ascontiguousarray(cloud, np.float32).reshape(-1, 3)
+    o = np.asarray(options, np.float64)
+    init = _pose7(*initial)
+    pose = np.zeros(7)
+    s = self.lib.oracle_rt3d_score(grid.h, _p(o, D), _p(init, D), _p(pts, F), len(pts), index,
+                                   _p(pose, D))
+    return float(s), (tuple(pose[:3]), tuple(pose[3:]))
+
+
+Oracle.hybrid_grid = _o3_hgrid
+Oracle.fast3d = _o3_fast3d
+Oracle.histogram = _o3_histogram
+Oracle.rt3d_match = _o3_rt3d_match
+Oracle.rt3d_score = _o3_rt3d_score

@@ -1,0 +1,230 @@
+"""GPU parity: FastCorrelativeScanMatcher3D and RealTimeCorrelativeScanMatcher3D
+on the MI355X vs the oracle.
+
+Bar: pyramid levels byte-identical; FastCSM3D score, rotational score and
+low-resolution score identical floats, pose identical (or an exactly tied
+leaf); RTCSM3D score within 1e-6 relative (the double exp() penalty may
+differ from glibc in the last ulps) and the same winning candidate.
+
+Scenarios restate fast_correlative_scan_matcher_3d_test.cc:36-204 and
+real_time_correlative_scan_matcher_3d_test.cc:34-117, plus variants with
+half-resolution levels (full_resolution_depth < branch_and_bound_depth) and
+non-trivial rotational histograms.
+"""
+import math
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+TEST_CLOUD = np.array([[4, 0, 0], [4.5, 0, 0], [5, 0, 0], [5.5, 0, 0], [0, 4, 0], [0, 4.5, 0],
+                       [0, 5, 0], [0, 5.5, 0], [0, 0, 4], [0, 0, 4.5], [0, 0, 5], [0, 0, 5.5]],
+                      np.float32)
+
+
+def quat_z(theta):
+    return (math.cos(0.5 * theta), 0.0, 0.0, math.sin(0.5 * theta))
+
+
+def transform(cloud, t, q):
+    w, x, y, z = q
+    r = np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w)],
+                  [2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w)],
+                  [2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)]])
+    return (np.asarray(cloud, np.float64) @ r.T + np.asarray(t)).astype(np.float32)
+
+
+def gpu_grid(csm, og):
+    ijk, v = og.cells()
+    return csm.HybridGrid(og.resolution, ijk, v, grid_size=og.grid_size)
+
+
+def assert_same_result(gpu, ref):
+    assert (gpu is not None) == ref["matched"], (gpu, ref)
+    if gpu is None:
+        return
+    assert np.float32(gpu.score) == np.float32(ref["score"])
+    assert np.float32(gpu.rotational_score) == np.float32(ref["rotational_score"])
+    assert np.float32(gpu.low_resolution_score) == np.float32(ref["low_resolution_score"])
+    (gt, gq), (rt, rq) = gpu.pose_estimate, ref["pose"]
+    assert tuple(gt) == tuple(rt) and tuple(gq) == tuple(rq), (gpu.pose_estimate, ref["pose"])
+
+
+def options(csm, depth, full_depth, **kw):
+    o = csm.FastCorrelativeScanMatcherOptions3D(depth, full_depth, 0.1, 0.15, 0.8, 0.8, 0.3)
+    for k, v in kw.items():
+        setattr(o, k, v)
+    return o
+
+
+def opt_tuple(o):
+    return (o.branch_and_bound_depth, o.full_resolution_depth, o.min_rotational_score,
+            o.min_low_resolution_score, o.linear_xy_search_window, o.linear_z_search_window,
+            o.angular_search_window)
+
+
+def fixture(csm, oracle, pose_t, pose_q, o, histogram=None):
+    og = oracle.hybrid_grid(0.05)
+    og.insert(pose_t, transform(TEST_CLOUD, pose_t, pose_q), 0.7, 0.4, 5)
+    hist = np.zeros(10, np.float32) if histogram is None else histogram
+    om = oracle.fast3d(og, og, hist, opt_tuple(o))
+    g = gpu_grid(csm, og)
+    gm = csm.FastCorrelativeScanMatcher3D(g, g, hist, o)
+    return og, om, g, gm
+
+
+@pytest.mark.parametrize("depth,full_depth", [(6, 6), (6, 3), (8, 3)])
+def test_levels_match_oracle(csm, oracle, depth, full_depth):
+    o = options(csm, depth, full_depth)
+    og, om, g, gm = fixture(csm, oracle, (0.3, -0.2, 0.1), quat_z(0.1), o)
+    for d in range(depth):
+        ijk, v = om.level(d)
+        origin, brick = gm.read_level(d)
+        assert np.count_nonzero(brick) == np.count_nonzero(v)
+        loc = ijk - np.asarray(origin)
+        assert np.all(brick[loc[:, 2], loc[:, 1], loc[:, 0]] == v), d
+
+
+@pytest.mark.parametrize("depth,full_depth", [(6, 6), (8, 3)])
+def test_correct_pose_for_match(csm, oracle, depth, full_depth):
+    """fast_correlative_scan_matcher_3d_test.cc:144-177, GPU vs oracle."""
+    rng = np.random.default_rng(42)
+    o = options(csm, depth, full_depth)
+    for _ in range(10):
+        x, y, z, th = rng.uniform(-1, 1, 4) * [0.7, 0.7, 0.7, 0.2]
+        og, om, g, gm = fixture(csm, oracle, (x, y, z), quat_z(th), o)
+        node = csm.NodeData3D(TEST_CLOUD, TEST_CLOUD, np.zeros(10, np.float32))
+        ident = ((0, 0, 0), (1, 0, 0, 0))
+        ref = om.match(ident, ident, node, 0.1)
+        gpu = gm.Match(ident, ident, node, 0.1)
+        assert_same_result(gpu, ref)
+        if depth == 6:  # the reference test's own expectation (IsNearly 0.05)
+            assert gpu is not None and gpu.score > 0.1 and gpu.low_resolution_score > 0.14
+            assert np.allclose(gpu.pose_estimate[0], (x, y, z), atol=0.06)
+        far = csm.NodeData3D(TEST_CLOUD, np.array([[42, 42, 42]], np.float32),
+                             np.zeros(10, np.float32))
+        assert gm.Match(ident, ident, far, 0.1) is None
+        assert not om.match(ident, ident, far, 0.1)["matched"]
+
+
+@pytest.mark.parametrize("depth,full_depth", [(6, 6), (8, 3)])
+def test_correct_pose_for_match_full_submap(csm, oracle, depth, full_depth):
+    """fast_correlative_scan_matcher_3d_test.cc:179-204, GPU vs oracle."""
+    rng = np.random.default_rng(7)
+    o = options(csm, depth, full_depth)
+    for _ in range(3):
+        x, y, z, th = rng.uniform(-1, 1, 4) * [0.7, 0.7, 0.7, 0.2]
+        og, om, g, gm = fixture(csm, oracle, (x, y, z), quat_z(th), o)
+        node = csm.NodeData3D(TEST_CLOUD, TEST_CLOUD, np.zeros(10, np.float32))
+        ident = (1, 0, 0, 0)
+        ref = om.match_full_submap(ident, ident, node, 0.1)
+        gpu = gm.MatchFullSubmap(ident, ident, node, 0.1)
+        assert_same_result(gpu, ref)
+        far = csm.NodeData3D(TEST_CLOUD, np.array([[42, 42, 42]], np.float32),
+                             np.zeros(10, np.float32))
+        assert gm.MatchFullSubmap(ident, ident, far, 0.1) is None
+
+
+def test_rotational_filter_and_poses(csm, oracle):
+    """Non-zero histograms (ComputeHistogram of the clouds): the yaw filter,
+    gravity alignment and non-identity global poses."""
+    rng = np.random.default_rng(3)
+    cloud = np.concatenate([TEST_CLOUD,
+                            rng.uniform(-6, 6, (200, 3)).astype(np.float32) * [1, 1, 0.3]])
+    cloud = cloud.astype(np.float32)
+    o = options(csm, 7, 3, min_rotational_score=0.5, linear_xy_search_window=1.0,
+                angular_search_window=0.4)
+    og = oracle.hybrid_grid(0.05)
+    og.insert((0.2, 0.1, 0.0), transform(cloud, (0.2, 0.1, 0.0), quat_z(0.15)), 0.7, 0.4, 5)
+    hist_submap = oracle.histogram(transform(cloud, (0.2, 0.1, 0.0), quat_z(0.15)), 120)
+    hist_node = oracle.histogram(cloud, 120)
+    om = oracle.fast3d(og, og, hist_submap, opt_tuple(o))
+    g = gpu_grid(csm, og)
+    gm = csm.FastCorrelativeScanMatcher3D(g, g, hist_submap, o)
+    grav = (math.cos(0.01), math.sin(0.01), 0.0, 0.0)
+    node = csm.NodeData3D(cloud, cloud[::3], hist_node, grav)
+    for node_pose, submap_pose in [(((0, 0, 0), (1, 0, 0, 0)), ((0, 0, 0), (1, 0, 0, 0))),
+                                   (((0.1, 0.0, 0.05), quat_z(0.1)), ((-0.1, 0.1, 0.0), quat_z(-0.05)))]:
+        ref = om.match(node_pose, submap_pose, node, 0.3)
+        gpu = gm.Match(node_pose, submap_pose, node, 0.3)
+        assert ref["num_discrete_scans"] > 0
+        assert_same_result(gpu, ref)
+    ref = om.match_full_submap(quat_z(0.05), (1, 0, 0, 0), node, 0.3)
+    gpu = gm.MatchFullSubmap(quat_z(0.05), (1, 0, 0, 0), node, 0.3)
+    assert_same_result(gpu, ref)
+
+
+def test_batch_equals_single_calls(csm, oracle):
+    o = options(csm, 6, 6)
+    mats, nodes, pairs, refs = [], [], [], []
+    rng = np.random.default_rng(11)
+    keep = []
+    for s in range(3):
+        x, y, z, th = rng.uniform(-1, 1, 4) * [0.7, 0.7, 0.7, 0.2]
+        og, om, g, gm = fixture(csm, oracle, (x, y, z), quat_z(th), o)
+        keep.append((og, om, g))
+        mats.append(gm)
+    nodes = [csm.NodeData3D(TEST_CLOUD, TEST_CLOUD, np.zeros(10, np.float32)),
+             csm.NodeData3D(TEST_CLOUD[:8], TEST_CLOUD[:8], np.zeros(10, np.float32))]
+    ident = ((0, 0, 0), (1, 0, 0, 0))
+    for s in range(3):
+        for n in range(2):
+            pairs.append((s, n, n == 1, 0.1, ident, ident))
+    results = csm.match_batch_3d(mats, nodes, pairs)
+    for (s, n, full, ms, npose, spose), r in zip(pairs, results):
+        single = (mats[s].MatchFullSubmap((1, 0, 0, 0), (1, 0, 0, 0), nodes[n], ms) if full
+                  else mats[s].Match(npose, spose, nodes[n], ms))
+        assert (single is not None) == (r.status == csm.CSM_OK)
+        if single is not None:
+            assert np.float32(single.score) == np.float32(r.score)
+            assert single.pose_estimate == r.pose.as_tuple()
+
+
+# ------------------------------------------------------------------ RTCSM3D --
+RT_CLOUD = np.array([[-3, 2, 0], [-4, 2, 0], [-5, 2, 0], [-6, 2, 0], [-6, 3, 1], [-6, 4, 2],
+                     [-7, 3, 1]], np.float32)
+
+
+@pytest.mark.parametrize("initial", [
+    ((-1.0, 0.0, 0.0), (1, 0, 0, 0)),        # PerfectEstimate
+    ((-0.8, 0.0, 0.0), (1, 0, 0, 0)),        # AlongX
+    ((-1.0, 0.0, -0.2), (1, 0, 0, 0)),       # AlongZ
+    ((-0.9, -0.2, 0.2), (1, 0, 0, 0)),       # AlongXYZ
+    ((-1.0, 0.0, 0.0), (math.cos(0.4 / 180 * math.pi), math.sin(0.4 / 180 * math.pi), 0, 0)),
+    ((-1.0, 0.0, 0.0), (math.cos(0.4 / 180 * math.pi), 0, math.sin(0.4 / 180 * math.pi), 0)),
+    ((-1.0, 0.0, 0.0), (math.cos(0.4 / 180 * math.pi), 0, math.sin(0.4 / 180 * math.pi),
+                        math.sin(0.4 / 180 * math.pi))),  # unnormalized axis (0, 1, 1)
+])
+def test_rt3d_reference_cases(csm, oracle, initial):
+    """real_time_correlative_scan_matcher_3d_test.cc:34-117 on the GPU."""
+    og = oracle.hybrid_grid(0.1)
+    for p in RT_CLOUD:
+        c = np.rint((p + [-1, 0, 0]) / np.float32(0.1)).astype(int)
+        og.set_probability(int(c[0]), int(c[1]), int(c[2]), 1.0)
+    opts = (0.3, math.radians(1.0), 0.1, 1.0)
+    g = gpu_grid(csm, og)
+    m = csm.RealTimeCorrelativeScanMatcher3D(csm.RealTimeCorrelativeScanMatcherOptions(*opts))
+    score, pose = m.Match(initial, RT_CLOUD, g)
+    ref_score, ref_pose, _, _ = oracle.rt3d_match(og, opts, initial, RT_CLOUD)
+    assert math.isclose(score, ref_score, rel_tol=1e-6), (score, ref_score)
+    assert pose == ref_pose
+    assert np.allclose(pose[0], (-1, 0, 0), atol=1e-3)
+
+
+def test_rt3d_dense_scene(csm, oracle):
+    """A few hundred points, a 0.1 m grid built by the 3D inserter, and a
+    +-0.2 m / +-2 deg window: many candidates, every one scored in float in
+    the reference order."""
+    rng = np.random.default_rng(5)
+    cloud = rng.uniform(-4, 4, (300, 3)).astype(np.float32) * np.float32([1, 1, 0.4])
+    og = oracle.hybrid_grid(0.1)
+    og.insert((0, 0, 0), cloud, 0.7, 0.4, 5)
+    opts = (0.2, math.radians(2.0), 0.1, 0.1)
+    g = gpu_grid(csm, og)
+    m = csm.RealTimeCorrelativeScanMatcher3D(csm.RealTimeCorrelativeScanMatcherOptions(*opts))
+    for initial in [((0.05, -0.03, 0.02), quat_z(0.01)), ((0.0, 0.0, 0.0), (1, 0, 0, 0))]:
+        score, pose = m.Match(initial, cloud, g)
+        ref_score, ref_pose, idx, n = oracle.rt3d_match(og, opts, initial, cloud)
+        assert math.isclose(score, ref_score, rel_tol=1e-6), (score, ref_score)
+        assert pose == ref_pose
