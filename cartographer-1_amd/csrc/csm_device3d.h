@@ -10,7 +10,8 @@ namespace csm {
 
 constexpr int kMaxLevels3d = 10;
 constexpr int kMax3dPoints = 8192;        // high-resolution points per node (LDS)
-constexpr int kMax3dTop = 900;            // top-level candidates per yaw (stack)
+constexpr int kRootChunk3d = 512;         // roots searched per chunk (stack)
+constexpr int kMax3dTop = 1 << 20;        // top-level candidates per yaw
 constexpr int kStack3d = 1024;            // DFS stack entries per workgroup
 constexpr int kMax3dYaws = 4095;          // 12-bit yaw id in the leaf key
 constexpr int kMax3dWindow = 511;         // 10-bit offset fields in the leaf key

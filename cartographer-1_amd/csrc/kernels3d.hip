@@ -332,9 +332,13 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
       sh.best = best[yw.pair];
     }
     __syncthreads();
-    // Lowest-resolution candidates (GenerateLowestResolutionCandidates :297-330).
-    for (int c0 = 0; c0 < T; c0 += 8) {
-      const int cnt = min(8, T - c0);
+    // Lowest-resolution candidates (GenerateLowestResolutionCandidates
+    // :297-330), in chunks of kRootChunk3d: each chunk is scored, ordered best
+    // last and searched to exhaustion before the next one.
+    for (int r0 = 0; r0 < T; r0 += kRootChunk3d) {
+    const int r1 = min(T, r0 + kRootChunk3d);
+    for (int c0 = r0; c0 < r1; c0 += 8) {
+      const int cnt = min(8, r1 - c0);
       if (tid < 8) {
         const int j = c0 + min(tid, cnt - 1);
         const int ixx = j % pd.top_nx, iyy = (j / pd.top_nx) % pd.top_ny,
@@ -369,7 +373,7 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
       __syncthreads();
     }
     // Order the roots so that the best bound is popped first (insertion sort
-    // by thread 0; at most kMax3dTop entries).
+    // by thread 0; at most kRootChunk3d entries).
     if (tid == 0) {
       for (int a = 1; a < sh.sp; ++a) {
         const int16_t x = sh.sx[a], y = sh.sy[a], z = sh.sz[a];
@@ -509,6 +513,7 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
       }
       __syncthreads();
     }
+    }  // root chunks
   }
   if (tid == 0 && stats) atomicAdd(stats, lookups);
 }

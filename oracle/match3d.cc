@@ -276,6 +276,66 @@ FastCorrelativeScanMatcher3D::FastCorrelativeScanMatcher3D(const HybridGrid& hyb
   }
 }
 
+// Search parameters and poses of Match (:127-143) / MatchFullSubmap (:145-170).
+void FastCorrelativeScanMatcher3D::Setup(bool full_submap, const Rigid3d& node_pose,
+                                         const Rigid3d& submap_pose, const NodeData3D& node,
+                                         SearchParameters* sp, Rigid3f* np, Rigid3f* spf) const {
+  if (!full_submap) {
+    *sp = SearchParameters{RoundToInt(options_.linear_xy_search_window / resolution_),
+                           RoundToInt(options_.linear_z_search_window / resolution_),
+                           options_.angular_search_window};
+    *np = CastRigidF(node_pose);
+    *spf = CastRigidF(submap_pose);
+    return;
+  }
+  float max_point_distance = 0.f;
+  for (const Vec3f& p : node.high_resolution_point_cloud)
+    max_point_distance = std::max(max_point_distance, NormF(p));
+  const int lws = (width_in_voxels_ + 1) / 2 + RoundToIntF(max_point_distance / resolution_ + 0.5f);
+  *sp = SearchParameters{lws, lws, M_PI};
+  *np = CastRigidF(Rigid3d{Vec3d{0., 0., 0.}, node_pose.q});
+  *spf = CastRigidF(Rigid3d{Vec3d{0., 0., 0.}, submap_pose.q});
+}
+
+bool FastCorrelativeScanMatcher3D::EvaluateLeaf(bool full_submap, const Rigid3d& node_pose,
+                                                const Rigid3d& submap_pose, const NodeData3D& node,
+                                                const Rigid3d& pose, Fast3dResult* out) const {
+  SearchParameters sp;
+  Rigid3f np, spf;
+  Setup(full_submap, node_pose, submap_pose, node, &sp, &np, &spf);
+  const std::vector<DiscreteScan3D> scans =
+      GenerateDiscreteScans(sp, node.high_resolution_point_cloud,
+                            node.rotational_scan_matcher_histogram, node.gravity_alignment, np, spf);
+  const Rigid3f want = CastRigidF(pose);
+  for (int k = 0; k < static_cast<int>(scans.size()); ++k) {
+    Candidate3D c;
+    c.scan_index = k;
+    const Rigid3f base = GetPoseFromCandidate(scans, c);
+    if (base.q.w != want.q.w || base.q.x != want.q.x || base.q.y != want.q.y ||
+        base.q.z != want.q.z)
+      continue;
+    c.offset = Idx3{RoundToIntF((want.t.x - base.t.x) / resolution_),
+                    RoundToIntF((want.t.y - base.t.y) / resolution_),
+                    RoundToIntF((want.t.z - base.t.z) / resolution_)};
+    const Rigid3f got = GetPoseFromCandidate(scans, c);
+    if (got.t.x != want.t.x || got.t.y != want.t.y || got.t.z != want.t.z) continue;
+    if (std::abs(c.offset.x) > sp.linear_xy_window_size ||
+        std::abs(c.offset.y) > sp.linear_xy_window_size ||
+        std::abs(c.offset.z) > sp.linear_z_window_size)
+      continue;
+    std::vector<Candidate3D> one{c};
+    ScoreCandidates(0, scans, &one, &out->lookups);
+    out->matched = true;
+    out->score = one[0].score;
+    out->pose = CastRigidD(got);
+    out->rotational_score = scans[k].rotational_score;
+    out->low_resolution_score =
+        LowResolutionScore(*low_resolution_grid_, node.low_resolution_point_cloud, got);
+    return true;
+  }
+  return false;
+}
+
 // :127-143
 Fast3dResult FastCorrelativeScanMatcher3D::Match(const Rigid3d& global_node_pose,
                                                  const Rigid3d& global_submap_pose,

@@ -256,6 +256,11 @@ class FastCorrelativeScanMatcher3D {
   Fast3dResult MatchFullSubmap(const Quatd& global_node_rotation,
                                const Quatd& global_submap_rotation, const NodeData3D& node,
                                float min_score) const;
+  // Test hook (tie checks): the leaf whose GetPoseFromCandidate equals `pose`
+  // exactly, if any, with its score, rotational and low-resolution scores.
+  bool EvaluateLeaf(bool full_submap, const Rigid3d& global_node_pose,
+                    const Rigid3d& global_submap_pose, const NodeData3D& node,
+                    const Rigid3d& pose, Fast3dResult* out) const;
   const PrecomputationGrid3D& level(int d) const { return *levels_.at(d); }
   int num_levels() const { return static_cast<int>(levels_.size()); }
   int width_in_voxels() const { return width_in_voxels_; }
@@ -283,6 +288,8 @@ class FastCorrelativeScanMatcher3D {
                                                     const Rigid3f& global_submap_pose) const;
 
  private:
+  void Setup(bool full_submap, const Rigid3d& node_pose, const Rigid3d& submap_pose,
+             const NodeData3D& node, SearchParameters* sp, Rigid3f* np, Rigid3f* spf) const;
   Fast3dResult MatchWithSearchParameters(const SearchParameters& sp,
                                          const Rigid3f& global_node_pose,
                                          const Rigid3f& global_submap_pose,

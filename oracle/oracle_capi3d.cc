@@ -150,6 +150,19 @@ void oracle_fast3d_match_full_submap(void* h, const double* node_q, const double
   PutResult(r, out);
 }
 
+// Tie checks: evaluates the leaf behind `pose` (t[3], q[4]); returns 1 if found.
+int oracle_fast3d_evaluate_leaf(void* h, int full_submap, const double* node_pose,
+                                const double* submap_pose, const float* high, int nh,
+                                const float* low, int nl, const float* hist, int hsize,
+                                const double* gravity_q, const double* pose, double* out) {
+  Fast3dResult r;
+  const bool ok = static_cast<Fast3dHandle*>(h)->m->EvaluateLeaf(
+      full_submap != 0, Pose(node_pose), Pose(submap_pose),
+      Node(high, nh, low, nl, hist, hsize, gravity_q), Pose(pose), &r);
+  PutResult(r, out);
+  return ok ? 1 : 0;
+}
+
 // options: lin, ang, wt, wr. out: score, pose t[3] q[4], best_index, candidates.
 void oracle_rt3d_match(void* g, const double* options, const double* initial, const float* xyz,
                        int n, double* out) {

@@ -179,6 +179,8 @@ _SIG3D = {
                                    P(D)]),
     "oracle_fast3d_match_full_submap": (None, [VP, P(D), P(D), P(F), I32, P(F), I32, P(F), I32,
                                                P(D), F, P(D)]),
+    "oracle_fast3d_evaluate_leaf": (I32, [VP, I32, P(D), P(D), P(F), I32, P(F), I32, P(F), I32,
+                                          P(D), P(D), P(D)]),
     "oracle_rt3d_match": (None, [VP, P(D), P(D), P(F), I32, P(D)]),
     "oracle_rt3d_score": (F, [VP, P(D), P(D), P(F), I32, I64, P(D)]),
     "oracle_rt3d_window": (None, [P(D), F, P(F), I32, P(I32), P(F), P(I32)]),
@@ -271,6 +273,19 @@ class OracleFast3D:
                                        len(lo), _p(hist, F), len(hist), _p(g, D), min_score,
                                        _p(out, D))
         return self._out(out)
+
+    def evaluate_leaf(self, full_submap, node_pose, submap_pose, node, pose):
+        """The leaf behind `pose` ((t), (q)): dict like match(), or None."""
+        hi, lo, hist, g = self._node(node)
+        a = _pose7(*node_pose)
+        b = _pose7(*submap_pose)
+        p = _pose7(*pose)
+        out = np.zeros(14)
+        ok = self.o.lib.oracle_fast3d_evaluate_leaf(self.h, 1 if full_submap else 0, _p(a, D),
+                                                    _p(b, D), _p(hi, F), len(hi), _p(lo, F),
+                                                    len(lo), _p(hist, F), len(hist), _p(g, D),
+                                                    _p(p, D), _p(out, D))
+        return self._out(out) if ok else None
 
     def match_full_submap(self, node_q, submap_q, node, min_score):
         hi, lo, hist, g = self._node(node)
