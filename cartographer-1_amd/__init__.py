@@ -556,4 +556,5 @@ class SyntheticWorld2D:
 
 # 3D matchers (RealTimeCorrelativeScanMatcher3D, FastCorrelativeScanMatcher3D).
 from .matching3d import (FastCorrelativeScanMatcher3D, FastCorrelativeScanMatcherOptions3D,  # noqa: E402,F401
-                         HybridGrid, NodeData3D, RealTimeCorrelativeScanMatcher3D, match_batch_3d)
+                         HybridGrid, NodeData3D, RealTimeCorrelativeScanMatcher3D, SyntheticWorld3D,
+                         match_batch_3d)

@@ -13,11 +13,13 @@ constexpr int kMax3dPoints = 8192;        // high-resolution points per node (LD
 constexpr int kRootChunk3d = 512;         // roots searched per chunk (stack)
 constexpr int kMax3dTop = 1 << 20;        // top-level candidates per yaw
 constexpr int kStack3d = 1024;            // DFS stack entries per workgroup
-constexpr int kMax3dYaws = 4095;          // 12-bit yaw id in the leaf key
-constexpr int kMax3dWindow = 511;         // 10-bit offset fields in the leaf key
+constexpr int kMax3dYaws = 1 << 16;
+constexpr int kMax3dWindow = 1 << 14;
 constexpr int kSearch3dThreads = 256;
 constexpr int kCellLimit3d = 16000;       // |cell index| kept in int16 in LDS
-constexpr int kKeyShift3d = 42;           // key = sum << 42 | ~leaf_id (42 bits)
+// Per pair: key = sum << key_shift | ~leaf_id, leaf_id = ((yaw << bxy | x) << bxy
+// | y) << bz | z with x = ox + wxy etc.; the host sizes the fields so that
+// sum and id fit 64 bits (else CSM_ERANGE).
 
 // A dense brick over the bounding box of a sparse grid's known cells:
 // value(i) = data[((i.z - oz) * ny + (i.y - oy)) * nx + (i.x - ox)], and the
@@ -53,6 +55,7 @@ struct Pair3Desc {
   int32_t top_nx, top_ny, top_nz;  // lowest-resolution candidates per axis
   int32_t min_sum;          // smallest sum whose score exceeds min_score
   float min_low_resolution_score;
+  int32_t key_shift, bits_xy, bits_z;  // leaf key layout
 };
 
 // One discrete scan (yaw) of a pair: the pose the cloud is discretized with,

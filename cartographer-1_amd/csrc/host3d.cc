@@ -635,7 +635,19 @@ void PreparePair(const csm_fast3d* m, const csm_node3d& node, const csm_pair3d& 
     y.yaw_id = static_cast<int32_t>(out->yaws.size());
     out->yaws.push_back(y);
   }
-  if (out->yaws.size() > static_cast<size_t>(kMax3dYaws)) out->status = CSM_ERANGE;
+  // Leaf key layout (kernels3d.hip LeafId): sum bits + yaw + 2 x xy + z bits.
+  auto bits = [](int64_t v) {
+    int b = 0;
+    while ((int64_t{1} << b) <= v) ++b;
+    return std::max(b, 1);
+  };
+  d.bits_xy = bits(2 * wxy);
+  d.bits_z = bits(2 * wz);
+  const int yaw_bits = bits(static_cast<int64_t>(out->yaws.size()));
+  d.key_shift = yaw_bits + 2 * d.bits_xy + d.bits_z;
+  const int sum_bits = bits(static_cast<int64_t>(n) * 255);
+  if (d.key_shift + sum_bits > 63 || out->yaws.size() > static_cast<size_t>(kMax3dYaws))
+    out->status = CSM_ERANGE;
 }
 
 }  // namespace
@@ -791,12 +803,13 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
     }
     const unsigned long long key = keys[dp];
     if (key == 0) continue;
-    const unsigned long long id = ~key & ((1ull << kKeyShift3d) - 1);
-    const int sum = static_cast<int>(key >> kKeyShift3d);
-    const int yaw = static_cast<int>(id >> 30);
-    const int ox = static_cast<int>((id >> 20) & 1023) - d.wxy;
-    const int oy = static_cast<int>((id >> 10) & 1023) - d.wxy;
-    const int oz = static_cast<int>(id & 1023) - d.wz;
+    const unsigned long long id = ~key & ((1ull << d.key_shift) - 1);
+    const int sum = static_cast<int>(key >> d.key_shift);
+    const int oz = static_cast<int>(id & ((1ull << d.bits_z) - 1)) - d.wz;
+    const int oy = static_cast<int>((id >> d.bits_z) & ((1ull << d.bits_xy) - 1)) - d.wxy;
+    const int ox =
+        static_cast<int>((id >> (d.bits_z + d.bits_xy)) & ((1ull << d.bits_xy) - 1)) - d.wxy;
+    const int yaw = static_cast<int>(id >> (d.bits_z + 2 * d.bits_xy));
     const Yaw3Desc& y = ydesc[d.yaw_begin + yaw];
     const float res = submaps[d.submap]->resolution;
     const V3 t0 = Rotate(Q4{1.f, 0.f, 0.f, 0.f}, V3{y.tx, y.ty, y.tz});

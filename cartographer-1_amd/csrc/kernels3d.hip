@@ -192,11 +192,13 @@ struct F3Shared {
   unsigned long long best;
 };
 
-__device__ __forceinline__ unsigned long long LeafId(int yaw, int ox, int oy, int oz, int wxy,
-                                                     int wz) {
-  return (static_cast<unsigned long long>(yaw) << 30) |
-         (static_cast<unsigned long long>(ox + wxy) << 20) |
-         (static_cast<unsigned long long>(oy + wxy) << 10) | static_cast<unsigned long long>(oz + wz);
+__device__ __forceinline__ unsigned long long LeafId(const Pair3Desc& pd, int yaw, int ox, int oy,
+                                                     int oz) {
+  unsigned long long id = static_cast<unsigned long long>(yaw);
+  id = (id << pd.bits_xy) | static_cast<unsigned long long>(ox + pd.wxy);
+  id = (id << pd.bits_xy) | static_cast<unsigned long long>(oy + pd.wxy);
+  id = (id << pd.bits_z) | static_cast<unsigned long long>(oz + pd.wz);
+  return id;
 }
 
 // Sums of `count` (<= 8) candidates at `depth` (ScoreCandidates :332-355):
@@ -357,7 +359,7 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
       ScoreOffsets(sh, sm, pd, top, cnt, ox, oy, oz, n);
       lookups += static_cast<unsigned long long>(cnt) * n;
       if (tid == 0) {
-        const int best_sum = static_cast<int>(sh.best >> kKeyShift3d);
+        const int best_sum = static_cast<int>(sh.best >> pd.key_shift);
         for (int k = 0; k < cnt; ++k) {
           const int s = sh.sums[k];
           if (s >= pd.min_sum && s >= best_sum) {
@@ -401,7 +403,7 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
       if (tid == 0) {
         sh.nchild = 0;
         sh.best = max(sh.best, *reinterpret_cast<volatile unsigned long long*>(best + yw.pair));
-        const int best_sum = static_cast<int>(sh.best >> kKeyShift3d);
+        const int best_sum = static_cast<int>(sh.best >> pd.key_shift);
         while (sh.sp > 0 && sh.nchild == 0) {
           const int at = --sh.sp;
           const int s = sh.ssum[at];
@@ -442,7 +444,7 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
       lookups += static_cast<unsigned long long>(nc) * n;
       if (cd > 0) {
         if (tid == 0) {
-          const int best_sum = static_cast<int>(sh.best >> kKeyShift3d);
+          const int best_sum = static_cast<int>(sh.best >> pd.key_shift);
           // Push ascending so that the best child is on top.
           int idx[8];
           int m = 0;
@@ -474,9 +476,9 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
       // low-resolution check is this group's answer (:384-401).
       if (tid == 0) {
         for (int k = 0; k < nc; ++k) {
-          const unsigned long long id = LeafId(yw.yaw_id, ox[k], oy[k], oz[k], pd.wxy, pd.wz);
-          sh.leaf_key[k] = (static_cast<unsigned long long>(sh.sums[k]) << kKeyShift3d) |
-                           (~id & ((1ull << kKeyShift3d) - 1));
+          const unsigned long long id = LeafId(pd, yw.yaw_id, ox[k], oy[k], oz[k]);
+          sh.leaf_key[k] = (static_cast<unsigned long long>(sh.sums[k]) << pd.key_shift) |
+                           (~id & ((1ull << pd.key_shift) - 1));
           sh.order[k] = k;
         }
         for (int a = 1; a < nc; ++a) {
@@ -532,11 +534,11 @@ fast3d_finalize(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __rest
     if (threadIdx.x == 0) low_score[p] = 0.f;
     return;
   }
-  const unsigned long long id = ~key & ((1ull << kKeyShift3d) - 1);
-  const int yaw = static_cast<int>(id >> 30);
-  const int ox = static_cast<int>((id >> 20) & 1023) - pd.wxy;
-  const int oy = static_cast<int>((id >> 10) & 1023) - pd.wxy;
-  const int oz = static_cast<int>(id & 1023) - pd.wz;
+  const unsigned long long id = ~key & ((1ull << pd.key_shift) - 1);
+  const int oz = static_cast<int>(id & ((1ull << pd.bits_z) - 1)) - pd.wz;
+  const int oy = static_cast<int>((id >> pd.bits_z) & ((1ull << pd.bits_xy) - 1)) - pd.wxy;
+  const int ox = static_cast<int>((id >> (pd.bits_z + pd.bits_xy)) & ((1ull << pd.bits_xy) - 1)) - pd.wxy;
+  const int yaw = static_cast<int>(id >> (pd.bits_z + 2 * pd.bits_xy));
   const Yaw3Desc yw = yaws[pd.yaw_begin + yaw];
   const Submap3Desc& sm = submaps[pd.submap];
   const float rf = sm.resolution;

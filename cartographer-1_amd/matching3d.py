@@ -223,3 +223,101 @@ def match_batch_3d(matchers: Sequence[FastCorrelativeScanMatcher3D], nodes: Sequ
     _check(lib.csm_fast3d_match_batch(ctx.handle, handles, len(matchers), cnodes, len(nodes),
                                       cpairs, len(pairs), results), "csm_fast3d_match_batch")
     return list(results)
+
+
+# --------------------------------------------------------------------------
+# Synthetic 3D world (bench / test inputs; not the matching path).
+
+class SynthConfig3D(C.Structure):
+    _fields_ = [("seed", C.c_uint64), ("world_x", C.c_double), ("world_y", C.c_double),
+                ("world_z", C.c_double), ("num_boxes", C.c_int32), ("num_nodes", C.c_int32),
+                ("num_submaps", C.c_int32), ("scans_per_submap", C.c_int32),
+                ("rings", C.c_int32), ("azimuths", C.c_int32), ("min_elevation", C.c_double),
+                ("max_elevation", C.c_double), ("max_range", C.c_double),
+                ("range_noise", C.c_double), ("high_resolution", C.c_double),
+                ("low_resolution", C.c_double), ("high_resolution_max_range", C.c_double),
+                ("high_voxel", C.c_double), ("low_voxel", C.c_double),
+                ("high_max_range", C.c_double), ("high_min_points", C.c_int32),
+                ("low_min_points", C.c_int32), ("low_max_range", C.c_double),
+                ("histogram_size", C.c_int32),
+                ("insert_voxel", C.c_double), ("threads", C.c_int32)]
+
+
+class SyntheticWorld3D:
+    """Seeded warehouse, 64-ring lidar scans, submaps with high/low-resolution
+    grids and rotational histograms."""
+
+    def __init__(self, num_nodes=16, num_submaps=4, **kw):
+        from . import SYNTH_PATH
+        lib = C.CDLL(SYNTH_PATH)
+        lib.csm_synth3d_create.argtypes = [C.POINTER(SynthConfig3D), C.POINTER(C.c_void_p)]
+        lib.csm_synth3d_destroy.argtypes = [C.c_void_p]
+        lib.csm_synth3d_node_poses.restype = C.POINTER(C.c_double)
+        lib.csm_synth3d_node_poses.argtypes = [C.c_void_p]
+        lib.csm_synth3d_submap_nodes.restype = C.POINTER(C.c_int32)
+        lib.csm_synth3d_submap_nodes.argtypes = [C.c_void_p]
+        lib.csm_synth3d_cloud.restype = C.c_int64
+        lib.csm_synth3d_cloud.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.POINTER(C.c_float),
+                                          C.c_int64]
+        lib.csm_synth3d_node_histogram.argtypes = [C.c_void_p, C.c_int32, C.POINTER(C.c_float)]
+        lib.csm_synth3d_submap_histogram.argtypes = [C.c_void_p, C.c_int32, C.POINTER(C.c_float)]
+        lib.csm_synth3d_grid.restype = C.c_int64
+        lib.csm_synth3d_grid.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.POINTER(C.c_int32),
+                                         C.POINTER(C.c_uint16), C.c_int64]
+        cfg = SynthConfig3D()
+        lib.csm_synth3d_default_config(C.byref(cfg))
+        cfg.num_nodes, cfg.num_submaps = num_nodes, num_submaps
+        for k, v in kw.items():
+            setattr(cfg, k, v)
+        h = C.c_void_p()
+        if lib.csm_synth3d_create(C.byref(cfg), C.byref(h)) != 0:
+            raise ValueError("invalid synthetic 3D world config")
+        try:
+            n, s, hs = num_nodes, num_submaps, cfg.histogram_size
+            self.node_poses = np.ctypeslib.as_array(lib.csm_synth3d_node_poses(h), (n * 4,)).reshape(-1, 4).copy()
+            self.submap_nodes = np.ctypeslib.as_array(lib.csm_synth3d_submap_nodes(h), (max(s, 1),))[:s].copy()
+
+            def cloud(i, kind):
+                m = lib.csm_synth3d_cloud(h, i, kind, None, 0)
+                out = np.zeros((m, 3), np.float32)
+                lib.csm_synth3d_cloud(h, i, kind, _ptr(out, C.c_float), m)
+                return out
+
+            self.raw = [cloud(i, 0) for i in range(n)]
+            self.high = [cloud(i, 1) for i in range(n)]
+            self.low = [cloud(i, 2) for i in range(n)]
+            self.node_hist = []
+            for i in range(n):
+                out = np.zeros(hs, np.float32)
+                lib.csm_synth3d_node_histogram(h, i, _ptr(out, C.c_float))
+                self.node_hist.append(out)
+            self.submap_hist, self.high_cells, self.low_cells = [], [], []
+            for j in range(s):
+                out = np.zeros(hs, np.float32)
+                lib.csm_synth3d_submap_histogram(h, j, _ptr(out, C.c_float))
+                self.submap_hist.append(out)
+                for grid, dst in ((0, self.high_cells), (1, self.low_cells)):
+                    m = lib.csm_synth3d_grid(h, j, grid, None, None, 0)
+                    ijk = np.zeros((m, 3), np.int32)
+                    val = np.zeros(m, np.uint16)
+                    lib.csm_synth3d_grid(h, j, grid, _ptr(ijk, C.c_int32), _ptr(val, C.c_uint16), m)
+                    dst.append((ijk, val))
+        finally:
+            lib.csm_synth3d_destroy(h)
+        self.high_resolution = cfg.high_resolution
+        self.low_resolution = cfg.low_resolution
+        self.num_nodes, self.num_submaps = num_nodes, num_submaps
+
+    def node(self, i) -> NodeData3D:
+        return NodeData3D(self.high[i], self.low[i], self.node_hist[i])
+
+    def node_rotation(self, i):
+        yaw = float(self.node_poses[i, 3])
+        return (math.cos(0.5 * yaw), 0.0, 0.0, math.sin(0.5 * yaw))
+
+    def node_in_submap(self, i, s):
+        """Ground-truth node pose in submap s's frame: ((t), (q))."""
+        c = int(self.submap_nodes[s])
+        t = (float(self.node_poses[i, 0] - self.node_poses[c, 0]),
+             float(self.node_poses[i, 1] - self.node_poses[c, 1]), 0.0)
+        return t, self.node_rotation(i)

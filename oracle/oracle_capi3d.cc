@@ -37,6 +37,11 @@ void oracle_hgrid_destroy(void* g) { delete static_cast<HybridGrid*>(g); }
 void oracle_hgrid_set_probability(void* g, int x, int y, int z, float p) {
   static_cast<HybridGrid*>(g)->SetProbability(Idx3{x, y, z}, p);
 }
+void oracle_hgrid_set_values(void* g, const int32_t* ijk, const uint16_t* values, int64_t n) {
+  auto* h = static_cast<HybridGrid*>(g);
+  for (int64_t i = 0; i < n; ++i)
+    *h->mutable_value(Idx3{ijk[3 * i], ijk[3 * i + 1], ijk[3 * i + 2]}) = values[i];
+}
 void oracle_hgrid_insert(void* g, float hit, float miss, int num_free_space_voxels,
                          const float* origin, const float* xyz, int n) {
   RangeDataInserter3D ins(hit, miss, num_free_space_voxels);

@@ -167,6 +167,7 @@ _SIG3D = {
     "oracle_hgrid_destroy": (None, [VP]),
     "oracle_hgrid_set_probability": (None, [VP, I32, I32, I32, F]),
     "oracle_hgrid_insert": (None, [VP, F, F, I32, P(F), P(F), I32]),
+    "oracle_hgrid_set_values": (None, [VP, P(I32), P(C.c_uint16), I64]),
     "oracle_hgrid_cells": (I64, [VP, P(I32), P(C.c_uint16), I64]),
     "oracle_hgrid_grid_size": (I32, [VP]),
     "oracle_hgrid_probability": (F, [VP, I32, I32, I32]),
@@ -211,6 +212,11 @@ class OracleHybridGrid:
         r = np.ascontiguousarray(returns, np.float32).reshape(-1, 3)
         self.o.lib.oracle_hgrid_insert(self.h, hit, miss, num_free_space_voxels, _p(org, F),
                                        _p(r, F), len(r))
+
+    def set_values(self, ijk, values):
+        ijk = np.ascontiguousarray(ijk, np.int32).reshape(-1, 3)
+        v = np.ascontiguousarray(values, np.uint16)
+        self.o.lib.oracle_hgrid_set_values(self.h, _p(ijk, I32), _p(v, C.c_uint16), len(v))
 
     def cells(self):
         n = self.o.lib.oracle_hgrid_cells(self.h, None, None, 0)

@@ -243,3 +243,41 @@ def test_rt3d_dense_scene(csm, oracle):
         ref_score, ref_pose, idx, n = oracle.rt3d_match(og, opts, initial, cloud)
         assert math.isclose(score, ref_score, rel_tol=1e-6), (score, ref_score)
         assert pose == ref_pose
+
+
+# ------------------------------------------------- synthetic world (C5 shape) --
+@pytest.fixture(scope="module")
+def world3d(csm):
+    return csm.SyntheticWorld3D(num_nodes=24, num_submaps=3, seed=99)
+
+
+def test_synthetic_pairs_match_oracle(csm, oracle, world3d):
+    """C5-shaped inputs: 0.10 m high / 0.45 m low resolution grids built from
+    64-ring scans, ~200-point node clouds, 120-bucket histograms, the
+    pose_graph.lua 3D options; MatchFullSubmap and Match on the same pairs."""
+    w = world3d
+    o = csm.FastCorrelativeScanMatcherOptions3D()  # pose_graph.lua:40-48
+    stats = {"exact": 0, "tie": 0, "nomatch": 0}
+    for s in range(w.num_submaps):
+        oh, ol = oracle.hybrid_grid(w.high_resolution), oracle.hybrid_grid(w.low_resolution)
+        oh.set_values(*w.high_cells[s])
+        ol.set_values(*w.low_cells[s])
+        om = oracle.fast3d(oh, ol, w.submap_hist[s], opt_tuple(o))
+        gh = csm.HybridGrid(w.high_resolution, *w.high_cells[s])
+        gl = csm.HybridGrid(w.low_resolution, *w.low_cells[s])
+        assert gh.info()[2] == oh.grid_size
+        gm = csm.FastCorrelativeScanMatcher3D(gh, gl, w.submap_hist[s], o)
+        c = int(w.submap_nodes[s])
+        for n in [c, (c + 1) % w.num_nodes, (c + 7) % w.num_nodes]:
+            node = w.node(n)
+            ref = om.match_full_submap(w.node_rotation(n), (1, 0, 0, 0), node, 0.6)
+            gpu = gm.MatchFullSubmap(w.node_rotation(n), (1, 0, 0, 0), node, 0.6)
+            stats[assert_same_result(gpu, ref, om, True, w.node_rotation(n), (1, 0, 0, 0), node,
+                                     o.min_low_resolution_score)] += 1
+            truth = w.node_in_submap(n, s)
+            init = ((truth[0][0] + 0.3, truth[0][1] - 0.2, 0.1), truth[1])
+            ref = om.match(init, ((0, 0, 0), (1, 0, 0, 0)), node, 0.55)
+            gpu = gm.Match(init, ((0, 0, 0), (1, 0, 0, 0)), node, 0.55)
+            stats[assert_same_result(gpu, ref, om, False, init, ((0, 0, 0), (1, 0, 0, 0)), node,
+                                     o.min_low_resolution_score)] += 1
+    assert stats["exact"] + stats["tie"] >= 3, stats
