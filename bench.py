@@ -51,6 +51,9 @@ def parse():
     p.add_argument("--no-rt", action="store_true")
     p.add_argument("--seed", type=int, default=20250127)
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
+    p.add_argument("--no-3d", action="store_true")
+    p.add_argument("--nodes3d", type=int, default=500)
+    p.add_argument("--submaps3d", type=int, default=25)
     return p.parse_args()
 
 
@@ -177,6 +180,9 @@ def main():
         out["rt2d"] = rt2d_bench(csm, ctx, args)
     if rank == 0 and world_size == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(world, my_submaps, args)
+    if rank == 0 and world_size == 1 and not args.no_3d:
+        out["rt3d"] = rt3d_bench(csm, ctx, args)
+        out["fast3d"] = fast3d_bench(csm, ctx, args)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:
@@ -229,6 +235,165 @@ def rt2d_bench(csm, ctx, args):
     except OSError:
         pass
     return res
+
+
+def rt3d_bench(csm, ctx, args):
+    """Config C4: RealTimeCorrelativeScanMatcher3D, one 64-ring scan (~55k
+    points, R <= 14 m) vs the 0.10 m HybridGrid of a 20x20x5 m box world,
+    +-0.3 m / +-15 deg, weights 0.1. Every candidate is scored (exhaustive, as
+    the reference); the CPU figure extrapolates the oracle's per-candidate
+    time (one thread, like Match) measured on a spread sample of candidates."""
+    w = csm.SyntheticWorld3D(num_nodes=2, num_submaps=1, world_x=20.0, world_y=20.0,
+                             world_z=5.0, num_boxes=8, max_range=14.0, seed=args.seed + 3)
+    c = int(w.submap_nodes[0])
+    cloud = w.raw[c]
+    grid = csm.HybridGrid(w.high_resolution, *w.high_cells[0], context=ctx)
+    (tx, ty, tz), q = w.node_in_submap(c, 0)
+    dyaw = math.radians(4.0)
+    q0 = (q[0] * math.cos(dyaw / 2) - q[3] * math.sin(dyaw / 2), 0.0, 0.0,
+          q[3] * math.cos(dyaw / 2) + q[0] * math.sin(dyaw / 2))
+    init = ((tx + 0.12, ty - 0.08, tz + 0.05), q0)
+    opts = (0.3, math.radians(15.0), 0.1, 0.1)
+    m = csm.RealTimeCorrelativeScanMatcher3D(csm.RealTimeCorrelativeScanMatcherOptions(*opts), ctx)
+    m.Match(init, cloud[:64], grid)  # warm-up (module load), tiny
+    ctx.reset_timing()
+    ctx.enable_timing(True)
+    t0 = time.perf_counter()
+    score, pose = m.Match(init, cloud, grid)
+    wall = time.perf_counter() - t0
+    tm = ctx.timing()
+    ctx.enable_timing(False)
+    lookups = tm.rt3d_lookups
+    n = len(cloud)
+    res = {"config": "C4: 64-ring scan vs 0.10 m HybridGrid, +-0.3 m / +-15 deg, wt=wr=0.1",
+           "points": n, "candidates": lookups / n, "gpu_ms_per_scan_match": wall * 1e3,
+           "kernel_ms": tm.rt3d_kernel_ms, "lookups": lookups,
+           "lookups_per_s": lookups / (tm.rt3d_kernel_ms * 1e-3) if tm.rt3d_kernel_ms else 0.0,
+           "algorithmic_GBps": 2.0 * lookups / (tm.rt3d_kernel_ms * 1e-3) / 1e9
+           if tm.rt3d_kernel_ms else 0.0, "score": score,
+           "pose_error_m": math.dist(pose[0], (tx, ty, tz))}
+    if not args.no_cpu:
+        try:
+            sys.path.insert(0, os.path.join(ROOT, "tests"))
+            import ctypes as C
+
+            import oracle_lib
+            o = oracle_lib.Oracle()
+            og = o.hybrid_grid(w.high_resolution)
+            og.set_values(*w.high_cells[0])
+            total = int(round(lookups / n))
+            P = C.POINTER
+            oo = np.asarray(opts, np.float64)
+            ii = oracle_lib._pose7(*init)
+            pts = np.ascontiguousarray(cloud, np.float32)
+
+            def timed(k):
+                return o.lib.oracle_rt3d_time(og.h, oo.ctypes.data_as(P(C.c_double)),
+                                              ii.ctypes.data_as(P(C.c_double)),
+                                              pts.ctypes.data_as(P(C.c_float)), n, k,
+                                              max(1, total // k))
+
+            probe = timed(16)
+            sample = int(min(50000, max(16, 10.0 / max(probe / 16, 1e-6))))
+            sec = timed(sample)
+            res["cpu_baseline"] = {
+                "value": sec / sample * total * 1e3, "unit": "ms/scan-match", "cores": 1,
+                "kind": "port",
+                "sample": f"{sample} candidates spread over the {total} of one match, "
+                          f"{sec:.2f} s, extrapolated to all candidates (oracle, -O3)"}
+        except OSError:
+            pass
+    return res
+
+
+def fast3d_bench(csm, ctx, args):
+    """C5 per-GPU share: FastCorrelativeScanMatcher3D::MatchFullSubmap over
+    nodes3d x submaps3d pairs (500 x 25 = the 8-GPU C5 sweep's share of one
+    GPU), pose_graph.lua 3D options, global_localization_min_score 0.6."""
+    t0 = time.time()
+    w = csm.SyntheticWorld3D(num_nodes=args.nodes3d, num_submaps=args.submaps3d,
+                             seed=args.seed + 5)
+    gen = time.time() - t0
+    o = csm.FastCorrelativeScanMatcherOptions3D()
+    grids = [(csm.HybridGrid(w.high_resolution, *w.high_cells[s], context=ctx),
+              csm.HybridGrid(w.low_resolution, *w.low_cells[s], context=ctx))
+             for s in range(w.num_submaps)]
+    mats = [csm.FastCorrelativeScanMatcher3D(g[0], g[1], w.submap_hist[s], o, ctx)
+            for s, g in enumerate(grids)]
+    nodes = [w.node(i) for i in range(w.num_nodes)]
+    ident = ((0, 0, 0), (1, 0, 0, 0))
+    pairs = [(s, n, True, 0.6, ((0, 0, 0), w.node_rotation(n)), ident)
+             for s in range(w.num_submaps) for n in range(w.num_nodes)]
+    csm.match_batch_3d(mats, nodes, pairs[:64], ctx)  # warm-up
+    ctx.reset_timing()
+    ctx.enable_timing(True)
+    t0 = time.perf_counter()
+    res3 = csm.match_batch_3d(mats, nodes, pairs, ctx)
+    wall = time.perf_counter() - t0
+    tm = ctx.timing()
+    ctx.enable_timing(False)
+    out = {"config": f"C5 share: MatchFullSubmap, {w.num_nodes} nodes x {w.num_submaps} submaps "
+                     "(0.10/0.45 m grids, ~200-point clouds, 120-bucket histograms), "
+                     "branch_and_bound_depth 8, full_resolution_depth 3",
+           "pairs": len(pairs), "value": len(pairs) / wall, "unit": "pairs/s",
+           "accepted": sum(1 for r in res3 if r.status == 0), "wall_s": wall,
+           "kernel_ms": tm.fast3d_kernel_ms, "lookups": tm.fast3d_lookups,
+           "algorithmic_GBps": tm.fast3d_lookups / (tm.fast3d_kernel_ms * 1e-3) / 1e9
+           if tm.fast3d_kernel_ms else 0.0, "setup_s": gen}
+    if not args.no_cpu:
+        try:
+            sys.path.insert(0, os.path.join(ROOT, "tests"))
+            import ctypes as C
+
+            import oracle_lib
+            orc = oracle_lib.Oracle()
+            opt = (o.branch_and_bound_depth, o.full_resolution_depth, o.min_rotational_score,
+                   o.min_low_resolution_score, o.linear_xy_search_window,
+                   o.linear_z_search_window, o.angular_search_window)
+            keep = []
+            handles = []
+            for s in range(w.num_submaps):
+                oh, ol = orc.hybrid_grid(w.high_resolution), orc.hybrid_grid(w.low_resolution)
+                oh.set_values(*w.high_cells[s])
+                ol.set_values(*w.low_cells[s])
+                om = orc.fast3d(oh, ol, w.submap_hist[s], opt)
+                keep.append((oh, ol, om))
+                handles.append(om.h)
+            hoff = np.zeros(w.num_nodes + 1, np.int64)
+            hoff[1:] = np.cumsum([len(x) for x in w.high])
+            loff = np.zeros(w.num_nodes + 1, np.int64)
+            loff[1:] = np.cumsum([len(x) for x in w.low])
+            high = np.ascontiguousarray(np.concatenate(w.high), np.float32)
+            low = np.ascontiguousarray(np.concatenate(w.low), np.float32)
+            hists = np.ascontiguousarray(np.stack(w.node_hist), np.float32)
+            nq = np.ascontiguousarray([w.node_rotation(i) for i in range(w.num_nodes)], np.float64)
+            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+            rng = np.random.RandomState(777)
+            P = C.POINTER
+            hv = (C.c_void_p * len(handles))(*handles)
+
+            def run(k):
+                ps = rng.randint(0, w.num_submaps, k).astype(np.int32)
+                pn = rng.randint(0, w.num_nodes, k).astype(np.int32)
+                matched = np.zeros(k, np.int32)
+                return orc.lib.oracle_fast3d_match_pairs(
+                    hv, high.ctypes.data_as(P(C.c_float)), hoff.ctypes.data_as(P(C.c_int64)),
+                    low.ctypes.data_as(P(C.c_float)), loff.ctypes.data_as(P(C.c_int64)),
+                    hists.ctypes.data_as(P(C.c_float)), hists.shape[1],
+                    nq.ctypes.data_as(P(C.c_double)), ps.ctypes.data_as(P(C.c_int32)),
+                    pn.ctypes.data_as(P(C.c_int32)), k, threads, 0.6,
+                    matched.ctypes.data_as(P(C.c_int32)))
+
+            probe = run(threads)
+            k = min(20000, max(threads, int(threads * 10.0 / max(probe, 1e-3))))
+            sec = run(k)
+            out["cpu_baseline"] = {"value": k / sec, "unit": "pairs/s", "cores": threads,
+                                   "kind": "port",
+                                   "sample": f"{k} uniformly sampled pairs of the same queue, "
+                                             f"{sec:.1f} s on {threads} threads (oracle, -O3)"}
+        except OSError:
+            pass
+    return out
 
 
 def cpu_baseline(world, my_submaps, args):

@@ -2,6 +2,7 @@
 // RotationalScanMatcher, low-resolution matcher, FastCorrelativeScanMatcher3D
 // and RealTimeCorrelativeScanMatcher3D, restated from the reference.
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <map>
 
@@ -594,6 +595,27 @@ float RealTimeScore3D(const RtOptions3D& o, const Rigid3d& initial, const PointC
   const Rigid3f candidate = Mul3(CastRigidF(initial), t);
   if (candidate_out) *candidate_out = candidate;
   return RtScore(o, grid, cloud, candidate, t);
+}
+
+double RealTimeTime3D(const RtOptions3D& o, const Rigid3d& initial, const PointCloud& cloud,
+                      const HybridGrid& grid, int64_t count, int64_t stride, float* sink) {
+  Rt3dGeometry g;
+  g.res = grid.resolution();
+  RealTime3DWindow(o, g.res, cloud, &g.L, &g.step, &g.A);
+  const Rigid3f init = CastRigidF(initial);
+  const auto t0 = std::chrono::steady_clock::now();
+  float acc = 0.f;
+  for (int64_t i = 0; i < count; ++i) {
+    const Rigid3f t = RtTransform(g, i * stride);
+    const Rigid3f candidate = Mul3(init, t);
+    // ScoreCandidate on TransformPointCloud(point_cloud, candidate) (:41-44).
+    const PointCloud transformed = TransformPointCloud(cloud, candidate);
+    float score = 0.f;
+    for (const Vec3f& p : transformed) score += grid.GetProbability(grid.GetCellIndex(p));
+    acc += score;
+  }
+  *sink = acc;
+  return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 }
 
 // :34-54 — loops z, y, x, rz, ry, rx; first strict maximum wins.

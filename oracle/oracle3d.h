@@ -331,6 +331,10 @@ struct Rt3dResult {
 // `max_candidates` bounds the work (0 = no bound; larger searches abort).
 Rt3dResult RealTimeMatch3D(const RtOptions3D& options, const Rigid3d& initial,
                            const PointCloud& cloud, const HybridGrid& grid);
+// CPU baseline timing: seconds for `count` candidates (indices i * stride),
+// each transformed and scored the way Match does it.
+double RealTimeTime3D(const RtOptions3D& options, const Rigid3d& initial, const PointCloud& cloud,
+                      const HybridGrid& grid, int64_t count, int64_t stride, float* sink);
 // Search-space geometry (for tests/bench): linear window size, angular step
 // and window size.
 void RealTime3DWindow(const RtOptions3D& options, float resolution, const PointCloud& cloud,

@@ -1,6 +1,9 @@
 // ORACLE — TEST INFRASTRUCTURE ONLY (see csm_oracle.h).
 // C API of the 3D restatement, for tests/oracle_lib.py.
+#include <atomic>
+#include <chrono>
 #include <cstring>
+#include <thread>
 
 #include "oracle3d.h"
 
@@ -125,6 +128,8 @@ static void PutResult(const Fast3dResult& r, double* out) {
   out[13] = r.num_discrete_scans;
 }
 
+static const double kIdentityQ[4] = {1., 0., 0., 0.};
+
 static NodeData3D Node(const float* high, int nh, const float* low, int nl, const float* hist,
                        int hsize, const double* gravity_q) {
   NodeData3D n;
@@ -204,6 +209,52 @@ void oracle_rt3d_window(const double* options, float resolution, const float* xy
   o.linear_search_window = options[0];
   o.angular_search_window = options[1];
   RealTime3DWindow(o, resolution, Cloud(xyz, n), linear_window, angular_step, angular_window);
+}
+
+
+// CPU baseline (bench.py): MatchFullSubmap over (submap, node) pairs on
+// `threads` host threads, one pair per task like ConstraintBuilder3D's pool.
+// nodes: packed clouds with offsets; rotations (w,x,y,z) per node. Returns
+// wall seconds; matched[i] = 1 when a Result was returned.
+double oracle_fast3d_match_pairs(void** submaps, const float* high, const int64_t* high_off,
+                                 const float* low, const int64_t* low_off, const float* hists,
+                                 int hsize, const double* node_q, const int32_t* pair_submap,
+                                 const int32_t* pair_node, int64_t num_pairs, int threads,
+                                 float min_score, int32_t* matched) {
+  std::atomic<int64_t> next{0};
+  const auto t0 = std::chrono::steady_clock::now();
+  auto work = [&]() {
+    for (int64_t i = next++; i < num_pairs; i = next++) {
+      const int n = pair_node[i];
+      const NodeData3D node =
+          Node(high + 3 * high_off[n], static_cast<int>(high_off[n + 1] - high_off[n]),
+               low + 3 * low_off[n], static_cast<int>(low_off[n + 1] - low_off[n]),
+               hists + static_cast<int64_t>(hsize) * n, hsize, kIdentityQ);
+      const double* q = node_q + 4 * n;
+      const Fast3dResult r = static_cast<Fast3dHandle*>(submaps[pair_submap[i]])->m->MatchFullSubmap(
+          Quatd{q[0], q[1], q[2], q[3]}, Quatd{1., 0., 0., 0.}, node, min_score);
+      matched[i] = r.matched ? 1 : 0;
+    }
+  };
+  std::vector<std::thread> pool;
+  for (int t = 1; t < threads; ++t) pool.emplace_back(work);
+  work();
+  for (auto& t : pool) t.join();
+  return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
+// CPU baseline for RTCSM3D: seconds to score `count` candidates spread over
+// the search (indices i * stride), single-threaded like Match.
+double oracle_rt3d_time(void* g, const double* options, const double* initial, const float* xyz,
+                        int n, int64_t count, int64_t stride) {
+  RtOptions3D o;
+  o.linear_search_window = options[0];
+  o.angular_search_window = options[1];
+  o.translation_delta_cost_weight = options[2];
+  o.rotation_delta_cost_weight = options[3];
+  float sink = 0.f;
+  return RealTimeTime3D(o, Pose(initial), Cloud(xyz, n), *static_cast<HybridGrid*>(g), count,
+                        stride, &sink);
 }
 
 }  // extern "C"
