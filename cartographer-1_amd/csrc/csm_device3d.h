@@ -9,8 +9,11 @@
 namespace csm {
 
 constexpr int kMaxLevels3d = 10;
-constexpr int kMax3dPoints = 8192;        // high-resolution points per node (LDS)
-constexpr int kRootChunk3d = 512;         // roots searched per chunk (stack)
+constexpr int kMax3dPoints = 4096;        // high-resolution points per node (LDS)
+constexpr int kTopLds3d = 24 * 1024;      // top pyramid level cached in LDS when it fits
+constexpr int kRootChunk3d = 128;         // roots fed to the DFS stack at a time
+constexpr int kRootScore3d = 512;         // roots scored at a time (one per lane)
+constexpr int kBatch3d = 16;              // DFS nodes scored per step (16 lanes each)
 constexpr int kMax3dTop = 1 << 20;        // top-level candidates per yaw
 constexpr int kStack3d = 1024;            // DFS stack entries per workgroup
 constexpr int kMax3dYaws = 1 << 16;
@@ -34,6 +37,7 @@ struct Brick3 {
 // allocation) and the low-resolution HybridGrid (float probability brick).
 struct Submap3Desc {
   const uint8_t* levels;  // base of the level allocation
+  int32_t levels_bytes;   // its size (< 2^31: one buffer resource spans it)
   Brick3 level[kMaxLevels3d];
   int32_t num_levels;     // branch_and_bound_depth
   int32_t full_resolution_depth;

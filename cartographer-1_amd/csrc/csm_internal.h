@@ -60,7 +60,7 @@ struct csm_context {
   int num_cus = 256;
   // 3D path scratch (host3d.cc).
   csm::DevBuf rt3_rot, rt3_trans, rt3_points, rt3_best, f3_pairs, f3_yaws, f3_points,
-      f3_low_points, f3_best, f3_status, f3_counter, f3_items;
+      f3_low_points, f3_best, f3_status, f3_counter, f3_items, f3_scores;
 };
 
 #endif  // CSM_INTERNAL_H_

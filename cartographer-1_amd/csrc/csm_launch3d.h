@@ -29,6 +29,17 @@ hipError_t LaunchFast3dFinalize(int num_pairs, hipStream_t st, const Submap3Desc
                                 const float* low_points, const unsigned long long* best,
                                 float* low_score);
 
+// Rotational scores of every (pair, yaw); `pairs` points to RotPair3 records
+// (kernels3d.hip): {node_hist, submap_hist, size, window, step, yaw0, out}.
+struct RotPair3Host {
+  int32_t node_hist, submap_hist, size, window;
+  float step, yaw0;
+  int64_t out;
+};
+constexpr int kMaxHistogram = 512;
+hipError_t LaunchRotScores(const void* pairs, int num_pairs, int max_yaws, const float* hists,
+                           float* out, hipStream_t st);
+
 }  // namespace csm
 
 #endif  // CSM_LAUNCH3D_H_

@@ -13,6 +13,8 @@
 #include <algorithm>
 #include <atomic>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <thread>
@@ -114,62 +116,6 @@ csm_pose3d ToPose(const V3& t, const Q4& q) {
   p.q[2] = q.y;
   p.q[3] = q.z;
   return p;
-}
-
-// Redux.h LinearVectorizedTraversal, 4-float packets, aligned storage.
-float ReduxSum(const float* v, int n) {
-  const int a2 = (n / 8) * 8, a1 = (n / 4) * 4;
-  if (a1 == 0) {
-    if (n == 0) return 0.f;
-    float r = v[0];
-    for (int i = 1; i < n; ++i) r += v[i];
-    return r;
-  }
-  float p0[4] = {v[0], v[1], v[2], v[3]};
-  if (a1 > 4) {
-    float p1[4] = {v[4], v[5], v[6], v[7]};
-    for (int i = 8; i < a2; i += 8)
-      for (int k = 0; k < 4; ++k) {
-        p0[k] += v[i + k];
-        p1[k] += v[i + 4 + k];
-      }
-    for (int k = 0; k < 4; ++k) p0[k] += p1[k];
-    if (a1 > a2)
-      for (int k = 0; k < 4; ++k) p0[k] += v[a2 + k];
-  }
-  float r = (p0[0] + p0[2]) + (p0[1] + p0[3]);
-  for (int i = a1; i < n; ++i) r += v[i];
-  return r;
-}
-float Dot(const float* a, const float* b, int n, float* scratch) {
-  for (int i = 0; i < n; ++i) scratch[i] = a[i] * b[i];
-  return ReduxSum(scratch, n);
-}
-
-// rotational_scan_matcher.cc:119-131, :138-158, :173-185.
-void RotationalScores(const std::vector<float>& submap, const float* hist, int size,
-                      float initial_angle, const std::vector<float>& angles,
-                      std::vector<float>* out) {
-  out->resize(angles.size());
-  std::vector<float> rot(size), scratch(size);
-  const float submap_norm = std::sqrt(Dot(submap.data(), submap.data(), size, scratch.data()));
-  for (size_t a = 0; a < angles.size(); ++a) {
-    const float angle = initial_angle + angles[a];
-    if (size > 0) {
-      const float rb =
-          static_cast<float>(static_cast<double>(-angle * static_cast<float>(size)) / M_PI);
-      int full = LroundF(rb - 0.5f);
-      const float fraction = rb - static_cast<float>(full);
-      while (full < 0) full += size;
-      for (int i = 0; i < size; ++i)
-        rot[i] = fraction * hist[(i + 1 + full) % size] + (1.f - fraction) * hist[(i + full) % size];
-    }
-    const float scan_norm = std::sqrt(Dot(rot.data(), rot.data(), size, scratch.data()));
-    const float normalization = scan_norm * submap_norm;
-    (*out)[a] = normalization < 1e-3f
-                    ? 1.f
-                    : Dot(submap.data(), rot.data(), size, scratch.data()) / normalization;
-  }
 }
 
 // kValueToProbability (probability_values.cc:26-66) and the level-0
@@ -478,8 +424,10 @@ int csm_fast3d_create(csm_context* ctx, const csm_hybrid_grid* high, const csm_h
     if (bytes > (int64_t{1} << 31)) return CSM_ERANGE;
     total += (bytes + 255) & ~int64_t{255};
   }
+  if (total > 0x7fffff00) return CSM_ERANGE;
   if ((rc = m->levels.Reserve(std::max<int64_t>(total, 256)))) return rc;
   d.levels = m->levels.as<uint8_t>();
+  d.levels_bytes = static_cast<int32_t>(std::max<int64_t>(total, 256));
   d.low_prob = low->prob.as<float>();
   d.low = low->brick;
   d.low_resolution = low->resolution;
@@ -542,10 +490,16 @@ struct PairPrep {
   Pair3Desc desc{};
   std::vector<Yaw3Desc> yaws;
   int status = CSM_OK;
+  // Phase 1 results: the discrete-scan yaws and their rotational inputs.
+  int angular_window = 0;
+  float astep = 0.f, yaw0 = 0.f;
+  R3 node_to_submap{};
+  Q4 submap_inv{}, node_q{};
+  int64_t score_offset = 0;
 };
 
-// MatchWithSearchParameters' host half (fast_correlative_scan_matcher_3d.cc
-// :127-199, GenerateDiscreteScans :246-295).
+// MatchWithSearchParameters' host half up to the rotational scores
+// (fast_correlative_scan_matcher_3d.cc:127-199, GenerateDiscreteScans :246-276).
 void PreparePair(const csm_fast3d* m, const csm_node3d& node, const csm_pair3d& p,
                  PairPrep* out) {
   const csm_fast3d_options& o = m->options;
@@ -586,7 +540,7 @@ void PreparePair(const csm_fast3d* m, const csm_node3d& node, const csm_pair3d& 
   const int step = 1 << (m->desc.num_levels - 1);
   d.top_nx = d.top_ny = (2 * wxy + step) / step;
   d.top_nz = (2 * wz + step) / step;
-  if (d.top_nx * d.top_ny * d.top_nz > kMax3dTop) {
+  if (static_cast<int64_t>(d.top_nx) * d.top_ny * d.top_nz > kMax3dTop) {
     out->status = CSM_ERANGE;
     return;
   }
@@ -598,11 +552,13 @@ void PreparePair(const csm_fast3d* m, const csm_node3d& node, const csm_pair3d& 
     max_range = std::max(NormV(V3{node.high_resolution_xyz[3 * i], node.high_resolution_xyz[3 * i + 1],
                                   node.high_resolution_xyz[3 * i + 2]}),
                          max_range);
-  const float astep = (1.f - 1e-2f) * std::acos(1.f - (res * res) / (2.f * (max_range * max_range)));
-  const int aw = Lround(ang / astep);
-  std::vector<float> angles;
-  for (int rz = -aw; rz <= aw; ++rz) angles.push_back(static_cast<float>(rz) * astep);
-  const R3 node_to_submap = Mul(Inverse(submap_pose), node_pose);
+  out->astep = (1.f - 1e-2f) * std::acos(1.f - (res * res) / (2.f * (max_range * max_range)));
+  out->angular_window = Lround(ang / out->astep);
+  if (out->angular_window > kMax3dYaws / 2) {
+    out->status = CSM_ERANGE;
+    return;
+  }
+  out->node_to_submap = Mul(Inverse(submap_pose), node_pose);
   // gravity_alignment.inverse().cast<float>() (double Quaternion::inverse).
   const double* g = node.gravity_alignment;
   const double gn2 = (g[1] * g[1] + g[3] * g[3]) + (g[2] * g[2] + g[0] * g[0]);
@@ -610,14 +566,20 @@ void PreparePair(const csm_fast3d* m, const csm_node3d& node, const csm_pair3d& 
   if (gn2 > 0.)
     gi = Q4{static_cast<float>(g[0] / gn2), static_cast<float>(-g[1] / gn2),
             static_cast<float>(-g[2] / gn2), static_cast<float>(-g[3] / gn2)};
-  const float yaw0 = GetYaw(QMul(node_to_submap.q, gi));
-  std::vector<float> scores;
-  RotationalScores(m->histogram, node.histogram, node.histogram_size, yaw0, angles, &scores);
-  const Q4 submap_inv = QInverse(submap_pose.q);
-  for (size_t i = 0; i < angles.size(); ++i) {
-    if (static_cast<double>(scores[i]) < o.min_rotational_score) continue;
-    const Q4 yaw = AngleAxisToQuat(V3{0.f, 0.f, angles[i]});
-    const Q4 q = QMul(QMul(submap_inv, yaw), node_pose.q);
+  out->yaw0 = GetYaw(QMul(out->node_to_submap.q, gi));
+  out->submap_inv = QInverse(submap_pose.q);
+  out->node_q = node_pose.q;
+}
+
+// GenerateDiscreteScans :277-294 given the rotational scores of the pair.
+void BuildYaws(const csm_fast3d* m, const float* scores, PairPrep* out) {
+  const int A = out->angular_window;
+  Pair3Desc& d = out->desc;
+  for (int k = 0; k <= 2 * A; ++k) {
+    if (static_cast<double>(scores[k]) < m->options.min_rotational_score) continue;
+    const float angle = static_cast<float>(k - A) * out->astep;
+    const Q4 yaw = AngleAxisToQuat(V3{0.f, 0.f, angle});
+    const Q4 q = QMul(QMul(out->submap_inv, yaw), out->node_q);
     const Q4 qn = QNormalized(QMul(Q4{1.f, 0.f, 0.f, 0.f}, q));  // GetPoseFromCandidate
     Yaw3Desc y{};
     y.qw = q.w;
@@ -628,11 +590,11 @@ void PreparePair(const csm_fast3d* m, const csm_node3d& node, const csm_pair3d& 
     y.nx = qn.x;
     y.ny = qn.y;
     y.nz = qn.z;
-    y.tx = node_to_submap.t.x;
-    y.ty = node_to_submap.t.y;
-    y.tz = node_to_submap.t.z;
-    y.rotational_score = scores[i];
-    y.yaw_id = static_cast<int32_t>(out->yaws.size());
+    y.tx = out->node_to_submap.t.x;
+    y.ty = out->node_to_submap.t.y;
+    y.tz = out->node_to_submap.t.z;
+    y.rotational_score = scores[k];
+    y.yaw_id = static_cast<int32_t>(out->yaws.size());  // increasing angle order
     out->yaws.push_back(y);
   }
   // Leaf key layout (kernels3d.hip LeafId): sum bits + yaw + 2 x xy + z bits.
@@ -641,13 +603,26 @@ void PreparePair(const csm_fast3d* m, const csm_node3d& node, const csm_pair3d& 
     while ((int64_t{1} << b) <= v) ++b;
     return std::max(b, 1);
   };
-  d.bits_xy = bits(2 * wxy);
-  d.bits_z = bits(2 * wz);
+  d.bits_xy = bits(2 * d.wxy);
+  d.bits_z = bits(2 * d.wz);
   const int yaw_bits = bits(static_cast<int64_t>(out->yaws.size()));
   d.key_shift = yaw_bits + 2 * d.bits_xy + d.bits_z;
-  const int sum_bits = bits(static_cast<int64_t>(n) * 255);
-  if (d.key_shift + sum_bits > 63 || out->yaws.size() > static_cast<size_t>(kMax3dYaws))
-    out->status = CSM_ERANGE;
+  const int sum_bits = bits(static_cast<int64_t>(d.num_points) * 255);
+  if (d.key_shift + sum_bits > 63) out->status = CSM_ERANGE;
+}
+
+template <typename F>
+void ParallelPairs(int64_t num, F&& f) {
+  std::atomic<int64_t> next{0};
+  const int nt = static_cast<int>(
+      std::max<unsigned>(1, std::min<unsigned>(16, std::thread::hardware_concurrency())));
+  auto work = [&]() {
+    for (int64_t i = next.fetch_add(1); i < num; i = next.fetch_add(1)) f(i);
+  };
+  std::vector<std::thread> pool;
+  for (int t = 1; t < std::min<int64_t>(nt, num); ++t) pool.emplace_back(work);
+  work();
+  for (auto& t : pool) t.join();
 }
 
 }  // namespace
@@ -683,24 +658,82 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
       lpts.insert(lpts.end(), nd.low_resolution_xyz, nd.low_resolution_xyz + 3 * nd.num_low_resolution);
     }
   }
-  // Host preparation, parallel over pairs.
+  // Phase 1 (host, parallel): search windows, angular steps, initial yaws.
   std::vector<PairPrep> prep(static_cast<size_t>(num_pairs));
+  ParallelPairs(num_pairs, [&](int64_t i) {
+    if (results[i].status != CSM_NO_MATCH) return;
+    const csm_pair3d& p = pairs[i];
+    const csm_node3d& nd = nodes[p.node];
+    if (nd.histogram_size != static_cast<int32_t>(submaps[p.submap]->histogram.size()) ||
+        nd.histogram_size > kMaxHistogram || (nd.histogram_size > 0 && !nd.histogram)) {
+      prep[i].status = CSM_EINVAL;
+      return;
+    }
+    PreparePair(submaps[p.submap], nd, p, &prep[i]);
+  });
+  // Phase 2 (device): rotational scores of every (pair, yaw).
   {
-    std::atomic<int64_t> next{0};
-    const int nt = static_cast<int>(std::max<unsigned>(1, std::min<unsigned>(16, std::thread::hardware_concurrency())));
-    auto work = [&]() {
-      for (;;) {
-        const int64_t i = next.fetch_add(1);
-        if (i >= num_pairs) break;
-        if (results[i].status != CSM_NO_MATCH) continue;
-        const csm_pair3d& p = pairs[i];
-        PreparePair(submaps[p.submap], nodes[p.node], p, &prep[i]);
+    std::vector<float> hists;
+    std::vector<int64_t> node_hist(num_nodes, -1), sub_hist(num_submaps, -1);
+    std::vector<RotPair3Host> rp;
+    std::vector<int64_t> rp_pair;
+    int64_t total = 0;
+    int max_yaws = 0;
+    for (int64_t i = 0; i < num_pairs; ++i) {
+      if (results[i].status != CSM_NO_MATCH || prep[i].status != CSM_OK) continue;
+      const csm_pair3d& p = pairs[i];
+      if (node_hist[p.node] < 0) {
+        node_hist[p.node] = static_cast<int64_t>(hists.size());
+        const csm_node3d& nd = nodes[p.node];
+        hists.insert(hists.end(), nd.histogram, nd.histogram + nd.histogram_size);
       }
-    };
-    std::vector<std::thread> pool;
-    for (int t = 1; t < std::min<int64_t>(nt, num_pairs); ++t) pool.emplace_back(work);
-    work();
-    for (auto& t : pool) t.join();
+      if (sub_hist[p.submap] < 0) {
+        sub_hist[p.submap] = static_cast<int64_t>(hists.size());
+        const auto& h = submaps[p.submap]->histogram;
+        hists.insert(hists.end(), h.begin(), h.end());
+      }
+      RotPair3Host r{};
+      r.node_hist = static_cast<int32_t>(node_hist[p.node]);
+      r.submap_hist = static_cast<int32_t>(sub_hist[p.submap]);
+      r.size = nodes[p.node].histogram_size;
+      r.window = prep[i].angular_window;
+      r.step = prep[i].astep;
+      r.yaw0 = prep[i].yaw0;
+      r.out = total;
+      prep[i].score_offset = total;
+      total += 2 * r.window + 1;
+      max_yaws = std::max(max_yaws, 2 * r.window + 1);
+      rp.push_back(r);
+      rp_pair.push_back(i);
+    }
+    std::vector<float> scores(static_cast<size_t>(std::max<int64_t>(total, 1)));
+    if (!rp.empty()) {
+      std::lock_guard<std::mutex> lock(ctx->mu);
+      int rc;
+      if ((rc = EnsureDevice3(ctx))) return rc;
+      hipStream_t st = ctx->stream;
+      if ((rc = ctx->f3_items.Reserve(sizeof(RotPair3Host) * rp.size() +
+                                      sizeof(float) * std::max<size_t>(hists.size(), 1))))
+        return rc;
+      if ((rc = ctx->f3_scores.Reserve(sizeof(float) * scores.size()))) return rc;
+      RotPair3Host* drp = ctx->f3_items.as<RotPair3Host>();
+      float* dh = reinterpret_cast<float*>(drp + rp.size());
+      CSM_HIP(hipMemcpyAsync(drp, rp.data(), sizeof(RotPair3Host) * rp.size(),
+                             hipMemcpyHostToDevice, st));
+      if (!hists.empty())
+        CSM_HIP(hipMemcpyAsync(dh, hists.data(), sizeof(float) * hists.size(),
+                               hipMemcpyHostToDevice, st));
+      CSM_HIP(LaunchRotScores(drp, static_cast<int>(rp.size()), max_yaws, dh,
+                              ctx->f3_scores.as<float>(), st));
+      CSM_HIP(hipMemcpyAsync(scores.data(), ctx->f3_scores.ptr, sizeof(float) * total,
+                             hipMemcpyDeviceToHost, st));
+      CSM_HIP(hipStreamSynchronize(st));
+    }
+    // Phase 3 (host, parallel): discrete-scan poses of the yaws that pass.
+    ParallelPairs(static_cast<int64_t>(rp_pair.size()), [&](int64_t j) {
+      const int64_t i = rp_pair[j];
+      BuildYaws(submaps[pairs[i].submap], scores.data() + prep[i].score_offset, &prep[i]);
+    });
   }
   std::vector<Submap3Desc> sdesc(num_submaps);
   for (int i = 0; i < num_submaps; ++i) sdesc[i] = submaps[i]->desc;
@@ -742,7 +775,7 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
   if ((rc = ctx->f3_low_points.Reserve(sizeof(float) * std::max<size_t>(lpts.size(), 3)))) return rc;
   if ((rc = ctx->f3_best.Reserve(sizeof(unsigned long long) * np + sizeof(float) * np))) return rc;
   if ((rc = ctx->f3_status.Reserve(sizeof(int32_t) * np))) return rc;
-  if ((rc = ctx->f3_counter.Reserve(sizeof(unsigned) + sizeof(unsigned long long)))) return rc;
+  if ((rc = ctx->f3_counter.Reserve(8 + 8 * sizeof(unsigned long long)))) return rc;
   Pair3Desc* dpairs = ctx->f3_pairs.as<Pair3Desc>();
   Submap3Desc* dsub = reinterpret_cast<Submap3Desc*>(dpairs + np);
   unsigned long long* dbest = ctx->f3_best.as<unsigned long long>();
@@ -764,7 +797,7 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
                            hipMemcpyHostToDevice, st));
   CSM_HIP(hipMemsetAsync(dbest, 0, sizeof(unsigned long long) * np, st));
   CSM_HIP(hipMemsetAsync(ctx->f3_status.ptr, 0, sizeof(int32_t) * np, st));
-  CSM_HIP(hipMemsetAsync(ctx->f3_counter.ptr, 0, 16, st));
+  CSM_HIP(hipMemsetAsync(ctx->f3_counter.ptr, 0, 8 + 8 * sizeof(unsigned long long), st));
   if (ctx->timing) CSM_HIP(hipEventRecord(ctx->ev0, st));
   if (ny > 0) {
     const int grid = std::max(1, std::min(ny, ctx->num_cus * 2));
@@ -778,20 +811,27 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
   std::vector<unsigned long long> keys(np);
   std::vector<float> lows(np);
   std::vector<int32_t> stat(np);
-  unsigned long long lookups = 0;
+  unsigned long long lookups = 0, prof[8] = {0};
   CSM_HIP(hipMemcpyAsync(keys.data(), dbest, sizeof(unsigned long long) * np,
                          hipMemcpyDeviceToHost, st));
   CSM_HIP(hipMemcpyAsync(lows.data(), dlow, sizeof(float) * np, hipMemcpyDeviceToHost, st));
   CSM_HIP(hipMemcpyAsync(stat.data(), ctx->f3_status.ptr, sizeof(int32_t) * np,
                          hipMemcpyDeviceToHost, st));
-  CSM_HIP(hipMemcpyAsync(&lookups, dstats, sizeof(lookups), hipMemcpyDeviceToHost, st));
+  CSM_HIP(hipMemcpyAsync(prof, dstats, sizeof(prof), hipMemcpyDeviceToHost, st));
   CSM_HIP(hipStreamSynchronize(st));
   if (ctx->timing) {
     float ms = 0.f;
     CSM_HIP(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
     ctx->t.fast3d_kernel_ms += ms;
     ctx->t.fast3d_launches += 1;
+    lookups = prof[0];
     ctx->t.fast3d_lookups += static_cast<double>(lookups);
+    if (std::getenv("CSM_PROFILE3D"))
+      std::fprintf(stderr,
+                   "fast3d phases (Mcycles, thread 0 sums): item+discretize %.1f roots %.1f "
+                   "sort %.1f dfs %.1f leaf %.1f | batches %llu leaves %llu items %d\n",
+                   prof[1] / 1e6, prof[2] / 1e6, prof[3] / 1e6, prof[4] / 1e6, prof[5] / 1e6,
+                   prof[6], prof[7], ny);
   }
   // Decode (GetPoseFromCandidate :369-375, Result :193-198).
   for (int dp = 0; dp < np; ++dp) {

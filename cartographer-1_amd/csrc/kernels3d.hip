@@ -188,7 +188,15 @@ struct F3Shared {
   unsigned long long leaf_key[8];
   int order[8];
   float lr[kSearch3dThreads];
-  int nchild, child_depth, sp, item, error, accepted;
+  uint8_t top[kTopLds3d];
+  int bn_x[kBatch3d], bn_y[kBatch3d], bn_z[kBatch3d], bn_d[kBatch3d];
+  unsigned long long leaf_keys[8 * kBatch3d];
+  int leaf_x[8 * kBatch3d], leaf_y[8 * kBatch3d], leaf_z[8 * kBatch3d];
+  int rmin[3], rmax[3];  // bounds of the cloud's cells at the top level
+  int16_t rbx[kRootScore3d], rby[kRootScore3d], rbz[kRootScore3d];
+  int rbs[kRootScore3d];
+  int nroot;
+  int nbatch, nleaf, nchild, child_depth, sp, item, error, accepted, cached_submap;
   unsigned long long best;
 };
 
@@ -294,12 +302,15 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
               unsigned long long* __restrict__ stats) {
   __shared__ F3Shared sh;
   const int tid = threadIdx.x;
-  unsigned long long lookups = 0;
+  unsigned long long lookups = 0, root_lookups = 0;
+  long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // thread 0: phase cycles / counts
+  if (tid == 0) sh.cached_submap = -1;
   for (;;) {
     if (tid == 0) sh.item = static_cast<int>(atomicAdd(counter, 1u));
     __syncthreads();
     const int item = sh.item;
     if (item >= num_items) break;
+    long long t_item = clock64();
     const Yaw3Desc yw = yaws[item];
     const Pair3Desc pd = pairs[yw.pair];
     const Submap3Desc& sm = submaps[pd.submap];
@@ -326,6 +337,8 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
       __syncthreads();
       continue;
     }
+    long long t_mark = clock64();
+    if (tid == 0) prof[0] += t_mark - t_item;
     const int top = sm.num_levels - 1;
     const int step = 1 << top;
     const int T = pd.top_nx * pd.top_ny * pd.top_nz;
@@ -335,178 +348,327 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
     }
     __syncthreads();
     // Lowest-resolution candidates (GenerateLowestResolutionCandidates
-    // :297-330), in chunks of kRootChunk3d: each chunk is scored, ordered best
-    // last and searched to exhaustion before the next one.
-    for (int r0 = 0; r0 < T; r0 += kRootChunk3d) {
-    const int r1 = min(T, r0 + kRootChunk3d);
-    for (int c0 = r0; c0 < r1; c0 += 8) {
-      const int cnt = min(8, r1 - c0);
-      if (tid < 8) {
-        const int j = c0 + min(tid, cnt - 1);
-        const int ixx = j % pd.top_nx, iyy = (j / pd.top_nx) % pd.top_ny,
-                  izz = j / (pd.top_nx * pd.top_ny);
-        sh.co_x[tid] = -pd.wxy + ixx * step;
-        sh.co_y[tid] = -pd.wxy + iyy * step;
-        sh.co_z[tid] = -pd.wz + izz * step;
-      }
+    // :297-330), in chunks of kRootChunk3d: each chunk is scored (one root
+    // per lane, the top level from LDS when it fits), ordered best last and
+    // searched to exhaustion before the next one.
+    const Brick3 tb = sm.level[top];
+    const int64_t tbytes = static_cast<int64_t>(tb.nx) * tb.ny * tb.nz;
+    const bool lds_top = tbytes <= kTopLds3d;
+    if (lds_top && sh.cached_submap != pd.submap) {
+      const uint8_t* src = sm.levels + tb.offset;
+      for (int64_t k = tid; k < tbytes; k += kSearch3dThreads) sh.top[k] = src[k];
       __syncthreads();
-      int ox[8], oy[8], oz[8];
-      for (int k = 0; k < 8; ++k) {
-        ox[k] = sh.co_x[k];
-        oy[k] = sh.co_y[k];
-        oz[k] = sh.co_z[k];
-      }
-      ScoreOffsets(sh, sm, pd, top, cnt, ox, oy, oz, n);
-      lookups += static_cast<unsigned long long>(cnt) * n;
-      if (tid == 0) {
-        const int best_sum = static_cast<int>(sh.best >> pd.key_shift);
-        for (int k = 0; k < cnt; ++k) {
-          const int s = sh.sums[k];
-          if (s >= pd.min_sum && s >= best_sum) {
-            const int at = sh.sp++;
-            sh.sx[at] = static_cast<int16_t>(ox[k]);
-            sh.sy[at] = static_cast<int16_t>(oy[k]);
-            sh.sz[at] = static_cast<int16_t>(oz[k]);
-            sh.sd[at] = static_cast<int8_t>(top);
-            sh.ssum[at] = s;
-          }
-        }
-      }
-      __syncthreads();
+      if (tid == 0) sh.cached_submap = pd.submap;
     }
-    // Order the roots so that the best bound is popped first (insertion sort
-    // by thread 0; at most kRootChunk3d entries).
-    if (tid == 0) {
-      for (int a = 1; a < sh.sp; ++a) {
-        const int16_t x = sh.sx[a], y = sh.sy[a], z = sh.sz[a];
-        const int8_t d = sh.sd[a];
-        const int s = sh.ssum[a];
-        int b = a - 1;
-        while (b >= 0 && sh.ssum[b] > s) {
-          sh.sx[b + 1] = sh.sx[b];
-          sh.sy[b + 1] = sh.sy[b];
-          sh.sz[b + 1] = sh.sz[b];
-          sh.sd[b + 1] = sh.sd[b];
-          sh.ssum[b + 1] = sh.ssum[b];
-          --b;
+    __syncthreads();
+    const int te = max(0, top - sm.full_resolution_depth + 1);
+    const bool treduced = top >= sm.full_resolution_depth;
+    const int lwx = (-pd.wxy) >> te, lwy = (-pd.wxy) >> te, lwz = (-pd.wz) >> te;
+    const uint8_t* tglobal = sm.levels + tb.offset;
+    // A root whose shifted cloud box misses the top-level brick sums to 0: it
+    // cannot exceed min_score when min_sum > 0 and is not scored.
+    if (tid < 3) {
+      sh.rmin[tid] = 1 << 30;
+      sh.rmax[tid] = -(1 << 30);
+    }
+    __syncthreads();
+    {
+      int mn[3] = {1 << 30, 1 << 30, 1 << 30}, mx[3] = {-(1 << 30), -(1 << 30), -(1 << 30)};
+      for (int i = tid; i < n; i += kSearch3dThreads) {
+        int c[3] = {sh.cx[i], sh.cy[i], sh.cz[i]};
+        if (treduced) {
+          c[0] = ((c[0] - pd.wxy) >> te) - lwx;
+          c[1] = ((c[1] - pd.wxy) >> te) - lwy;
+          c[2] = ((c[2] - pd.wz) >> te) - lwz;
         }
-        sh.sx[b + 1] = x;
-        sh.sy[b + 1] = y;
-        sh.sz[b + 1] = z;
-        sh.sd[b + 1] = d;
-        sh.ssum[b + 1] = s;
+        for (int a = 0; a < 3; ++a) {
+          mn[a] = min(mn[a], c[a]);
+          mx[a] = max(mx[a], c[a]);
+        }
+      }
+      for (int a = 0; a < 3; ++a) {
+        atomicMin(&sh.rmin[a], mn[a]);
+        atomicMax(&sh.rmax[a], mx[a]);
       }
     }
     __syncthreads();
-    // Best-first DFS.
+    const bool skip_empty = pd.min_sum > 0;
+    for (int r0 = 0; r0 < T; r0 += kRootScore3d) {
+    const int r1 = min(T, r0 + kRootScore3d);
+    if (tid == 0) sh.nroot = 0;
+    __syncthreads();
+    {
+      const int best_sum = static_cast<int>(sh.best >> pd.key_shift);
+      for (int j = r0 + tid; j < r1; j += kSearch3dThreads) {
+        const int ixx = j % pd.top_nx, iyy = (j / pd.top_nx) % pd.top_ny,
+                  izz = j / (pd.top_nx * pd.top_ny);
+        const int ox = -pd.wxy + ixx * step, oy = -pd.wxy + iyy * step, oz = -pd.wz + izz * step;
+        const int sx = ox >> te, sy = oy >> te, sz = oz >> te;
+        if (skip_empty &&
+            (sh.rmax[0] + sx < tb.ox || sh.rmin[0] + sx >= tb.ox + tb.nx ||
+             sh.rmax[1] + sy < tb.oy || sh.rmin[1] + sy >= tb.oy + tb.ny ||
+             sh.rmax[2] + sz < tb.oz || sh.rmin[2] + sz >= tb.oz + tb.nz))
+          continue;
+        int sum = 0;
+        root_lookups += n;
+        for (int i = 0; i < n; ++i) {
+          int x = sh.cx[i], y = sh.cy[i], z = sh.cz[i];
+          if (treduced) {
+            x = ((x - pd.wxy) >> te) - lwx;
+            y = ((y - pd.wxy) >> te) - lwy;
+            z = ((z - pd.wz) >> te) - lwz;
+          }
+          int64_t idx;
+          if (InBrick(tb, x + sx, y + sy, z + sz, &idx)) sum += lds_top ? sh.top[idx] : tglobal[idx];
+        }
+        if (sum >= pd.min_sum && sum >= best_sum) {
+          const int at = atomicAdd(&sh.nroot, 1);
+          sh.rbx[at] = static_cast<int16_t>(ox);
+          sh.rby[at] = static_cast<int16_t>(oy);
+          sh.rbz[at] = static_cast<int16_t>(oz);
+          sh.rbs[at] = sum;
+        }
+      }
+
+    }
+    __syncthreads();
+    if (tid == 0) {
+      const long long now = clock64();
+      prof[1] += now - t_mark;
+      t_mark = now;
+    }
+    // Order the roots ascending by bound (the best is fed last, popped
+    // first): parallel rank sort into the (empty) stack arrays.
+    {
+      const int m = sh.nroot;
+      for (int a = tid; a < m; a += kSearch3dThreads) {
+        const int s0 = sh.rbs[a];
+        int rank = 0;
+        for (int b2 = 0; b2 < m; ++b2) {
+          const int s1 = sh.rbs[b2];
+          rank += (s1 < s0) || (s1 == s0 && b2 < a);
+        }
+        sh.sx[rank] = sh.rbx[a];
+        sh.sy[rank] = sh.rby[a];
+        sh.sz[rank] = sh.rbz[a];
+        sh.ssum[rank] = s0;
+      }
+      __syncthreads();
+      for (int a = tid; a < m; a += kSearch3dThreads) {
+        sh.rbx[a] = sh.sx[a];
+        sh.rby[a] = sh.sy[a];
+        sh.rbz[a] = sh.sz[a];
+        sh.rbs[a] = sh.ssum[a];
+      }
+    }
+    __syncthreads();
+    if (tid == 0) {
+      const long long now = clock64();
+      prof[2] += now - t_mark;
+      t_mark = now;
+    }
+    for (int rb_end = sh.nroot; rb_end > 0;) {
+      const int k0 = max(0, rb_end - kRootChunk3d);
+      for (int a = tid; a < rb_end - k0; a += kSearch3dThreads) {
+        sh.sx[a] = sh.rbx[k0 + a];
+        sh.sy[a] = sh.rby[k0 + a];
+        sh.sz[a] = sh.rbz[k0 + a];
+        sh.sd[a] = static_cast<int8_t>(top);
+        sh.ssum[a] = sh.rbs[k0 + a];
+      }
+      if (tid == 0) sh.sp = rb_end - k0;
+      __syncthreads();
+    // Best-first DFS in batches of up to kBatch3d nodes, kLanes lanes each:
+    // the lanes of a node split the points and score its (up to) 8 children,
+    // reduced with shuffles only.
     for (;;) {
       if (tid == 0) {
-        sh.nchild = 0;
         sh.best = max(sh.best, *reinterpret_cast<volatile unsigned long long*>(best + yw.pair));
         const int best_sum = static_cast<int>(sh.best >> pd.key_shift);
-        while (sh.sp > 0 && sh.nchild == 0) {
+        int m = 0;
+        while (sh.sp > 0 && m < kBatch3d) {
           const int at = --sh.sp;
           const int s = sh.ssum[at];
           if (s < best_sum || s < pd.min_sum) continue;
-          const int d = sh.sd[at];
-          const int ox = sh.sx[at], oy = sh.sy[at], oz = sh.sz[at];
-          const int hw = 1 << (d - 1);
-          int c = 0;
-          for (int z = 0; z <= hw; z += hw) {
-            if (oz + z > pd.wz) break;
-            for (int y = 0; y <= hw; y += hw) {
-              if (oy + y > pd.wxy) break;
-              for (int x = 0; x <= hw; x += hw) {
-                if (ox + x > pd.wxy) break;
-                sh.co_x[c] = ox + x;
-                sh.co_y[c] = oy + y;
-                sh.co_z[c] = oz + z;
-                ++c;
-              }
-            }
-          }
-          sh.nchild = c;
-          sh.child_depth = d - 1;
+          sh.bn_x[m] = sh.sx[at];
+          sh.bn_y[m] = sh.sy[at];
+          sh.bn_z[m] = sh.sz[at];
+          sh.bn_d[m] = sh.sd[at];
+          ++m;
         }
-        if (sh.nchild == 0) sh.nchild = -1;  // stack exhausted
+        sh.nbatch = m;
+        sh.nleaf = 0;
       }
       __syncthreads();
-      const int nc = sh.nchild;
-      if (nc < 0) break;
-      const int cd = sh.child_depth;
-      int ox[8], oy[8], oz[8];
-      for (int k = 0; k < 8; ++k) {
-        ox[k] = sh.co_x[k];
-        oy[k] = sh.co_y[k];
-        oz[k] = sh.co_z[k];
+      const int nb = sh.nbatch;
+      if (nb == 0) break;
+      constexpr int kLanes = kSearch3dThreads / kBatch3d;  // lanes per node
+      const int half = tid / kLanes, hl = tid % kLanes;
+      int cx8[8], cy8[8], cz8[8];
+      int nc = 0, cd = 0;
+      int acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (half < nb) {
+        const int d = sh.bn_d[half];
+        const int ox = sh.bn_x[half], oy = sh.bn_y[half], oz = sh.bn_z[half];
+        const int hw = 1 << (d - 1);
+        for (int z = 0; z <= hw; z += hw) {
+          if (oz + z > pd.wz) break;
+          for (int y = 0; y <= hw; y += hw) {
+            if (oy + y > pd.wxy) break;
+            for (int x = 0; x <= hw; x += hw) {
+              if (ox + x > pd.wxy) break;
+              cx8[nc] = ox + x;
+              cy8[nc] = oy + y;
+              cz8[nc] = oz + z;
+              ++nc;
+            }
+          }
+        }
+        cd = d - 1;
+        const int e = max(0, cd - sm.full_resolution_depth + 1);
+        const bool reduced = cd >= sm.full_resolution_depth;
+        const Brick3 b = sm.level[cd];
+        const int lx = (-pd.wxy) >> e, ly = (-pd.wxy) >> e, lz = (-pd.wz) >> e;
+        // Children offsets relative to the brick origin; absent children get
+        // an impossible x so that their loads fall out of range (value 0).
+        int sx[8], sy[8], sz[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          sx[k] = k < nc ? (cx8[k] >> e) - b.ox : -(1 << 28);
+          sy[k] = k < nc ? (cy8[k] >> e) - b.oy : 0;
+          sz[k] = k < nc ? (cz8[k] >> e) - b.oz : 0;
+        }
+        // One buffer resource spans all levels; out-of-brick lookups use an
+        // offset beyond it, which the buffer unit returns as 0 (no branches,
+        // so the loads of consecutive points can be in flight together).
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint8_t*>(sm.levels), 0, sm.levels_bytes, 0x00020000);
+        const int bnx = b.nx, bny = b.ny, bnz = b.nz, boff = static_cast<int>(b.offset);
+        constexpr int kOOB3 = 0x7ffffff0;
+        auto off_of = [&](int x, int y, int z) {
+          const bool in = static_cast<unsigned>(x) < static_cast<unsigned>(bnx) &&
+                          static_cast<unsigned>(y) < static_cast<unsigned>(bny) &&
+                          static_cast<unsigned>(z) < static_cast<unsigned>(bnz);
+          return in ? boff + (z * bny + y) * bnx + x : kOOB3;
+        };
+        auto cell = [&](int i, int* x, int* y, int* z) {
+          int a = sh.cx[i], bb = sh.cy[i], c = sh.cz[i];
+          if (reduced) {
+            a = ((a - pd.wxy) >> e) - lx;
+            bb = ((bb - pd.wxy) >> e) - ly;
+            c = ((c - pd.wz) >> e) - lz;
+          }
+          *x = a;
+          *y = bb;
+          *z = c;
+        };
+        int i = hl;
+        for (; i + kLanes < n; i += 2 * kLanes) {
+          int xa, ya, za, xb, yb, zb;
+          cell(i, &xa, &ya, &za);
+          cell(i + kLanes, &xb, &yb, &zb);
+          uint32_t va[8], vb[8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            va[k] = __builtin_amdgcn_raw_buffer_load_b8(rs, off_of(xa + sx[k], ya + sy[k], za + sz[k]), 0, 0);
+            vb[k] = __builtin_amdgcn_raw_buffer_load_b8(rs, off_of(xb + sx[k], yb + sy[k], zb + sz[k]), 0, 0);
+          }
+#pragma unroll
+          for (int k = 0; k < 8; ++k) acc[k] += static_cast<int>(va[k] + vb[k]);
+        }
+        if (i < n) {
+          int xa, ya, za;
+          cell(i, &xa, &ya, &za);
+#pragma unroll
+          for (int k = 0; k < 8; ++k)
+            acc[k] += static_cast<int>(__builtin_amdgcn_raw_buffer_load_b8(
+                rs, off_of(xa + sx[k], ya + sy[k], za + sz[k]), 0, 0));
+        }
       }
-      ScoreOffsets(sh, sm, pd, cd, nc, ox, oy, oz, n);
-      lookups += static_cast<unsigned long long>(nc) * n;
-      if (cd > 0) {
-        if (tid == 0) {
-          const int best_sum = static_cast<int>(sh.best >> pd.key_shift);
-          // Push ascending so that the best child is on top.
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        for (int m = kLanes / 2; m > 0; m >>= 1) acc[k] += __shfl_xor(acc[k], m, 64);
+      if (half < nb && hl == 0) {
+        lookups += static_cast<unsigned long long>(nc) * n;
+        const int best_sum = static_cast<int>(sh.best >> pd.key_shift);
+        if (cd > 0) {
           int idx[8];
           int m = 0;
           for (int k = 0; k < nc; ++k)
-            if (sh.sums[k] >= pd.min_sum && sh.sums[k] >= best_sum) idx[m++] = k;
-          for (int a = 1; a < m; ++a) {
+            if (acc[k] >= pd.min_sum && acc[k] >= best_sum) idx[m++] = k;
+          for (int a = 1; a < m; ++a) {  // ascending: the best child is popped first
             const int v = idx[a];
-            int b = a - 1;
-            while (b >= 0 && sh.sums[idx[b]] > sh.sums[v]) {
-              idx[b + 1] = idx[b];
-              --b;
+            int b2 = a - 1;
+            while (b2 >= 0 && acc[idx[b2]] > acc[v]) {
+              idx[b2 + 1] = idx[b2];
+              --b2;
             }
-            idx[b + 1] = v;
+            idx[b2 + 1] = v;
           }
+          const int base = atomicAdd(&sh.sp, m);
           for (int a = 0; a < m; ++a) {
             const int k = idx[a];
-            const int at = sh.sp++;
-            sh.sx[at] = static_cast<int16_t>(ox[k]);
-            sh.sy[at] = static_cast<int16_t>(oy[k]);
-            sh.sz[at] = static_cast<int16_t>(oz[k]);
-            sh.sd[at] = static_cast<int8_t>(cd);
-            sh.ssum[at] = sh.sums[k];
+            sh.sx[base + a] = static_cast<int16_t>(cx8[k]);
+            sh.sy[base + a] = static_cast<int16_t>(cy8[k]);
+            sh.sz[base + a] = static_cast<int16_t>(cz8[k]);
+            sh.sd[base + a] = static_cast<int8_t>(cd);
+            sh.ssum[base + a] = acc[k];
+          }
+        } else {
+          for (int k = 0; k < nc; ++k) {
+            if (acc[k] < pd.min_sum) continue;
+            const unsigned long long id = LeafId(pd, yw.yaw_id, cx8[k], cy8[k], cz8[k]);
+            const unsigned long long key = (static_cast<unsigned long long>(acc[k]) << pd.key_shift) |
+                                           (~id & ((1ull << pd.key_shift) - 1));
+            if (key <= sh.best) continue;
+            const int at = atomicAdd(&sh.nleaf, 1);
+            sh.leaf_keys[at] = key;
+            sh.leaf_x[at] = cx8[k];
+            sh.leaf_y[at] = cy8[k];
+            sh.leaf_z[at] = cz8[k];
           }
         }
-        __syncthreads();
-        continue;
-      }
-      // Leaves: descending key order; the first one that passes the
-      // low-resolution check is this group's answer (:384-401).
-      if (tid == 0) {
-        for (int k = 0; k < nc; ++k) {
-          const unsigned long long id = LeafId(pd, yw.yaw_id, ox[k], oy[k], oz[k]);
-          sh.leaf_key[k] = (static_cast<unsigned long long>(sh.sums[k]) << pd.key_shift) |
-                           (~id & ((1ull << pd.key_shift) - 1));
-          sh.order[k] = k;
-        }
-        for (int a = 1; a < nc; ++a) {
-          const int v = sh.order[a];
-          int b = a - 1;
-          while (b >= 0 && sh.leaf_key[sh.order[b]] < sh.leaf_key[v]) {
-            sh.order[b + 1] = sh.order[b];
-            --b;
-          }
-          sh.order[b + 1] = v;
-        }
-        sh.accepted = 0;
       }
       __syncthreads();
-      for (int a = 0; a < nc; ++a) {
-        const int k = sh.order[a];
-        if (sh.sums[k] < pd.min_sum) break;
-        if (sh.leaf_key[k] <= sh.best) break;  // uniform: sh.best is shared
+      if (tid == 0) prof[5] += 1;
+      const int nl = sh.nleaf;
+      if (nl == 0) continue;
+      const long long t_leaf = clock64();
+      // Leaves: descending key order; the first that passes the
+      // low-resolution check (:384-401) beats every later one.
+      if (tid == 0) {
+        for (int a = 1; a < nl; ++a) {
+          const unsigned long long kk = sh.leaf_keys[a];
+          const int x = sh.leaf_x[a], y = sh.leaf_y[a], z = sh.leaf_z[a];
+          int b2 = a - 1;
+          while (b2 >= 0 && sh.leaf_keys[b2] < kk) {
+            sh.leaf_keys[b2 + 1] = sh.leaf_keys[b2];
+            sh.leaf_x[b2 + 1] = sh.leaf_x[b2];
+            sh.leaf_y[b2 + 1] = sh.leaf_y[b2];
+            sh.leaf_z[b2 + 1] = sh.leaf_z[b2];
+            --b2;
+          }
+          sh.leaf_keys[b2 + 1] = kk;
+          sh.leaf_x[b2 + 1] = x;
+          sh.leaf_y[b2 + 1] = y;
+          sh.leaf_z[b2 + 1] = z;
+        }
+        sh.accepted = 0;
+        sh.best = max(sh.best, *reinterpret_cast<volatile unsigned long long*>(best + yw.pair));
+      }
+      __syncthreads();
+      for (int a = 0; a < nl; ++a) {
+        if (sh.leaf_keys[a] <= sh.best) break;  // uniform: sh.best is shared
         const float rf = res;
-        const float tx = __fadd_rn(yw.tx, __fmul_rn(rf, static_cast<float>(ox[k])));
-        const float ty = __fadd_rn(yw.ty, __fmul_rn(rf, static_cast<float>(oy[k])));
-        const float tz = __fadd_rn(yw.tz, __fmul_rn(rf, static_cast<float>(oz[k])));
+        const float tx = __fadd_rn(yw.tx, __fmul_rn(rf, static_cast<float>(sh.leaf_x[a])));
+        const float ty = __fadd_rn(yw.ty, __fmul_rn(rf, static_cast<float>(sh.leaf_y[a])));
+        const float tz = __fadd_rn(yw.tz, __fmul_rn(rf, static_cast<float>(sh.leaf_z[a])));
         const float lrs = LowResScore(sh, sm, low_points + 3 * pd.low_offset, pd.num_low, yw.nw,
                                       yw.nx, yw.ny, yw.nz, tx, ty, tz);
         if (tid == 0) {
           if (static_cast<double>(lrs) >= static_cast<double>(pd.min_low_resolution_score)) {
-            atomicMax(best + yw.pair, sh.leaf_key[k]);
-            sh.best = max(sh.best, sh.leaf_key[k]);
+            atomicMax(best + yw.pair, sh.leaf_keys[a]);
+            sh.best = max(sh.best, sh.leaf_keys[a]);
             sh.accepted = 1;
           }
         }
@@ -514,10 +676,21 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
         if (sh.accepted) break;
       }
       __syncthreads();
+      if (tid == 0) {
+        prof[4] += clock64() - t_leaf;
+        prof[6] += nl;
+      }
     }
+      rb_end = k0;
+    }
+    if (tid == 0) prof[3] += clock64() - t_mark;
     }  // root chunks
   }
-  if (tid == 0 && stats) atomicAdd(stats, lookups);
+  lookups += root_lookups;
+  for (int m = 32; m > 0; m >>= 1) lookups += __shfl_xor(lookups, m, 64);
+  if ((tid & 63) == 0 && stats && lookups) atomicAdd(stats, lookups);
+  if (tid == 0 && stats)
+    for (int k = 0; k < 7; ++k) atomicAdd(stats + 1 + k, static_cast<unsigned long long>(prof[k]));
 }
 
 // Low-resolution score of each pair's winning leaf (the Result field), with
@@ -548,6 +721,96 @@ fast3d_finalize(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __rest
   const float s = LowResScore(sh, sm, low_points + 3 * pd.low_offset, pd.num_low, yw.nw, yw.nx,
                               yw.ny, yw.nz, tx, ty, tz);
   if (threadIdx.x == 0) low_score[p] = s;
+}
+
+// --------------------------------------------------- rotational scores ----
+//
+// RotationalScanMatcher::Match (rotational_scan_matcher.cc:173-185) for every
+// (pair, yaw): RotateHistogram (:138-158) then MatchHistograms (:119-131), one
+// thread per yaw, with the float operations of the reference's x86-64 build:
+// Eigen's 4-wide packet order for dot() / norm() (Redux.h), correctly rounded
+// sqrt and division. Note: sqrtf, not __fsqrt_rn — on this toolchain the latter
+// is not correctly rounded for gfx950 (tools/check_fp.hip: 15% of inputs differ
+// from IEEE), while sqrtf and '/' are.
+struct RotPair3 {
+  int32_t node_hist;    // float offset of the node histogram
+  int32_t submap_hist;  // float offset of the submap histogram
+  int32_t size;         // buckets
+  int32_t window;       // angular window A: yaws k = 0..2A
+  float step, yaw0;
+  int64_t out;          // score offset
+};
+
+template <typename F>
+__device__ __forceinline__ float PacketSum(F v, int n) {
+  // Redux.h LinearVectorizedTraversal, aligned, 4-wide packets.
+  const int a2 = (n / 8) * 8, a1 = (n / 4) * 4;
+  if (a1 == 0) {
+    if (n == 0) return 0.f;
+    float r = v(0);
+    for (int i = 1; i < n; ++i) r = __fadd_rn(r, v(i));
+    return r;
+  }
+  float p0 = v(0), p1 = v(1), p2 = v(2), p3 = v(3);
+  if (a1 > 4) {
+    float q0 = v(4), q1 = v(5), q2 = v(6), q3 = v(7);
+    for (int i = 8; i < a2; i += 8) {
+      p0 = __fadd_rn(p0, v(i));
+      p1 = __fadd_rn(p1, v(i + 1));
+      p2 = __fadd_rn(p2, v(i + 2));
+      p3 = __fadd_rn(p3, v(i + 3));
+      q0 = __fadd_rn(q0, v(i + 4));
+      q1 = __fadd_rn(q1, v(i + 5));
+      q2 = __fadd_rn(q2, v(i + 6));
+      q3 = __fadd_rn(q3, v(i + 7));
+    }
+    p0 = __fadd_rn(p0, q0);
+    p1 = __fadd_rn(p1, q1);
+    p2 = __fadd_rn(p2, q2);
+    p3 = __fadd_rn(p3, q3);
+    if (a1 > a2) {
+      p0 = __fadd_rn(p0, v(a2));
+      p1 = __fadd_rn(p1, v(a2 + 1));
+      p2 = __fadd_rn(p2, v(a2 + 2));
+      p3 = __fadd_rn(p3, v(a2 + 3));
+    }
+  }
+  float r = __fadd_rn(__fadd_rn(p0, p2), __fadd_rn(p1, p3));
+  for (int i = a1; i < n; ++i) r = __fadd_rn(r, v(i));
+  return r;
+}
+
+__global__ void rot_scores(const RotPair3* __restrict__ pairs, int num_pairs,
+                           const float* __restrict__ hists, float* __restrict__ out) {
+  const int p = blockIdx.y;
+  if (p >= num_pairs) return;
+  const RotPair3 rp = pairs[p];
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k > 2 * rp.window) return;
+  const int n = rp.size;
+  const float* h = hists + rp.node_hist;
+  const float* sub = hists + rp.submap_hist;
+  const float angle = __fadd_rn(rp.yaw0, __fmul_rn(static_cast<float>(k - rp.window), rp.step));
+  int full = 0;
+  float fraction = 0.f;
+  if (n > 0) {
+    const float rb = static_cast<float>(
+        static_cast<double>(__fmul_rn(-angle, static_cast<float>(n))) / 3.14159265358979323846);
+    full = static_cast<int>(roundf(__fsub_rn(rb, 0.5f)));
+    fraction = __fsub_rn(rb, static_cast<float>(full));
+    while (full < 0) full += n;
+  }
+  const float one_minus = __fsub_rn(1.f, fraction);
+  auto rot = [&](int i) {
+    return __fadd_rn(__fmul_rn(fraction, h[(i + 1 + full) % n]), __fmul_rn(one_minus, h[(i + full) % n]));
+  };
+  const float scan_norm = sqrtf(PacketSum([&](int i) { const float r = rot(i); return __fmul_rn(r, r); }, n));
+  const float submap_norm = sqrtf(PacketSum([&](int i) { return __fmul_rn(sub[i], sub[i]); }, n));
+  const float normalization = __fmul_rn(scan_norm, submap_norm);
+  float score = 1.f;
+  if (!(normalization < 1e-3f))
+    score = __fdiv_rn(PacketSum([&](int i) { return __fmul_rn(sub[i], rot(i)); }, n), normalization);
+  out[rp.out + k] = score;
 }
 
 // ------------------------------------------------------------ launchers ----
@@ -598,6 +861,15 @@ hipError_t LaunchFast3dFinalize(int num_pairs, hipStream_t st, const Submap3Desc
   if (num_pairs <= 0) return hipSuccess;
   hipLaunchKernelGGL(fast3d_finalize, dim3(num_pairs), dim3(kSearch3dThreads), 0, st, submaps,
                      pairs, yaws, low_points, best, low_score);
+  return hipGetLastError();
+}
+
+hipError_t LaunchRotScores(const void* pairs, int num_pairs, int max_yaws, const float* hists,
+                           float* out, hipStream_t st) {
+  if (num_pairs <= 0 || max_yaws <= 0) return hipSuccess;
+  const int threads = 64;
+  hipLaunchKernelGGL(rot_scores, dim3((max_yaws + threads - 1) / threads, num_pairs), dim3(threads),
+                     0, st, static_cast<const RotPair3*>(pairs), num_pairs, hists, out);
   return hipGetLastError();
 }
 
