@@ -42,6 +42,15 @@ struct Submap3Desc {
   int32_t num_levels;     // branch_and_bound_depth
   int32_t full_resolution_depth;
   float resolution;
+  // Octet layout of levels 0..num_levels-2 (the DFS child levels): one
+  // uint64 per cell c packs the 8 values at c + H*(x, y, z), x, y, z in {0,1},
+  // byte (z << 2 | y << 1 | x); H = 2^L below full_resolution_depth, else
+  // 2^(full_resolution_depth - 1). Boxes are the level's box grown by H
+  // towards -inf so that every cell with a child inside is present.
+  const uint8_t* octs;
+  int32_t octs_bytes;  // < 2^31 (0: octets disabled, byte path)
+  Brick3 oct[kMaxLevels3d];
+  int32_t oct_h[kMaxLevels3d];
   const float* low_prob;  // low-resolution grid probabilities
   Brick3 low;
   float low_resolution;

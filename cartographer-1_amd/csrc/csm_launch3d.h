@@ -15,6 +15,8 @@ hipError_t LaunchBrickFromValues(const uint16_t* values, int64_t n, const float*
                                  hipStream_t st);
 hipError_t LaunchLevelGather(const uint8_t* prev, const Brick3& pb, uint8_t* out, const Brick3& ob,
                              int shift, int half, hipStream_t st);
+hipError_t LaunchOctetBuild(const uint8_t* level, const Brick3& lb, int h, uint64_t* out,
+                            const Brick3& ob, hipStream_t st);
 hipError_t LaunchRt3dScore(int num_rot, hipStream_t st, const float* prob, const Brick3& gb,
                            float res, const float* points, int n, const float4* rot,
                            const float* rot_angle, const float4* trans, int num_trans, int t_base,

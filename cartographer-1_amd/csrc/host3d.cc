@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -355,7 +356,7 @@ struct csm_fast3d {
   int32_t width_in_voxels = 0;
   const csm_hybrid_grid* low = nullptr;
   std::vector<float> histogram;
-  DevBuf levels;
+  DevBuf levels, octs;
   Submap3Desc desc{};
 };
 
@@ -428,6 +429,29 @@ int csm_fast3d_create(csm_context* ctx, const csm_hybrid_grid* high, const csm_h
   if ((rc = m->levels.Reserve(std::max<int64_t>(total, 256)))) return rc;
   d.levels = m->levels.as<uint8_t>();
   d.levels_bytes = static_cast<int32_t>(std::max<int64_t>(total, 256));
+  // Octet bricks of the DFS child levels 0..depth-2.
+  int64_t otot = 0;
+  for (int l = 0; l + 1 < depth; ++l) {
+    const int h = l < options->full_resolution_depth ? (1 << l)
+                                                     : (1 << (options->full_resolution_depth - 1));
+    d.oct_h[l] = h;
+    Brick3 ob = d.level[l];
+    if (ob.nx > 0) {
+      ob.ox -= h;
+      ob.oy -= h;
+      ob.oz -= h;
+      ob.nx += h;
+      ob.ny += h;
+      ob.nz += h;
+    }
+    ob.offset = otot;
+    d.oct[l] = ob;
+    otot += static_cast<int64_t>(ob.nx) * ob.ny * ob.nz * 8;
+  }
+  if (otot > 0x7fffff00) return CSM_ERANGE;
+  if ((rc = m->octs.Reserve(std::max<int64_t>(otot, 256)))) return rc;
+  d.octs = m->octs.as<uint8_t>();
+  d.octs_bytes = static_cast<int32_t>(std::max<int64_t>(otot, 256));
   d.low_prob = low->prob.as<float>();
   d.low = low->brick;
   d.low_resolution = low->resolution;
@@ -446,6 +470,10 @@ int csm_fast3d_create(csm_context* ctx, const csm_hybrid_grid* high, const csm_h
       CSM_HIP(LaunchLevelGather(m->levels.as<uint8_t>() + d.level[l - 1].offset, d.level[l - 1],
                                 m->levels.as<uint8_t>() + d.level[l].offset, d.level[l], shifts[l],
                                 halves[l], st));
+    for (int l = 0; l + 1 < depth; ++l)
+      CSM_HIP(LaunchOctetBuild(m->levels.as<uint8_t>() + d.level[l].offset, d.level[l], d.oct_h[l],
+                               reinterpret_cast<uint64_t*>(m->octs.as<uint8_t>() + d.oct[l].offset),
+                               d.oct[l], st));
     CSM_HIP(hipStreamSynchronize(st));
   }
   *out = m.release();
@@ -634,6 +662,15 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
     return CSM_EINVAL;
   for (int i = 0; i < num_submaps; ++i)
     if (!submaps[i] || submaps[i]->ctx != ctx) return CSM_EINVAL;
+  using Clock = std::chrono::steady_clock;
+  const bool prof3 = std::getenv("CSM_PROFILE3D") != nullptr;
+  auto ht = Clock::now();
+  double hms[6] = {0, 0, 0, 0, 0, 0};
+  auto lap = [&](int k) {
+    const auto now = Clock::now();
+    hms[k] += std::chrono::duration<double, std::milli>(now - ht).count();
+    ht = now;
+  };
   // Nodes: pack clouds (only nodes some pair references).
   std::vector<int64_t> hoff(num_nodes, -1), loff(num_nodes, -1);
   std::vector<float> hpts, lpts;
@@ -658,6 +695,7 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
       lpts.insert(lpts.end(), nd.low_resolution_xyz, nd.low_resolution_xyz + 3 * nd.num_low_resolution);
     }
   }
+  lap(0);
   // Phase 1 (host, parallel): search windows, angular steps, initial yaws.
   std::vector<PairPrep> prep(static_cast<size_t>(num_pairs));
   ParallelPairs(num_pairs, [&](int64_t i) {
@@ -671,6 +709,7 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
     }
     PreparePair(submaps[p.submap], nd, p, &prep[i]);
   });
+  lap(1);
   // Phase 2 (device): rotational scores of every (pair, yaw).
   {
     std::vector<float> hists;
@@ -729,12 +768,14 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
                              hipMemcpyDeviceToHost, st));
       CSM_HIP(hipStreamSynchronize(st));
     }
+    lap(2);
     // Phase 3 (host, parallel): discrete-scan poses of the yaws that pass.
     ParallelPairs(static_cast<int64_t>(rp_pair.size()), [&](int64_t j) {
       const int64_t i = rp_pair[j];
       BuildYaws(submaps[pairs[i].submap], scores.data() + prep[i].score_offset, &prep[i]);
     });
   }
+  lap(3);
   std::vector<Submap3Desc> sdesc(num_submaps);
   for (int i = 0; i < num_submaps; ++i) sdesc[i] = submaps[i]->desc;
   std::vector<Pair3Desc> pdesc;
@@ -798,6 +839,7 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
   CSM_HIP(hipMemsetAsync(dbest, 0, sizeof(unsigned long long) * np, st));
   CSM_HIP(hipMemsetAsync(ctx->f3_status.ptr, 0, sizeof(int32_t) * np, st));
   CSM_HIP(hipMemsetAsync(ctx->f3_counter.ptr, 0, 8 + 8 * sizeof(unsigned long long), st));
+  lap(4);
   if (ctx->timing) CSM_HIP(hipEventRecord(ctx->ev0, st));
   if (ny > 0) {
     const int grid = std::max(1, std::min(ny, ctx->num_cus * 2));
@@ -833,6 +875,12 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
                    prof[1] / 1e6, prof[2] / 1e6, prof[3] / 1e6, prof[4] / 1e6, prof[5] / 1e6,
                    prof[6], prof[7], ny);
   }
+  lap(5);
+  if (prof3)
+    std::fprintf(stderr,
+                 "fast3d host (ms): pack %.1f phase1 %.1f rotscores %.1f yaws %.1f descs+upload %.1f "
+                 "search+download %.1f\n",
+                 hms[0], hms[1], hms[2], hms[3], hms[4], hms[5]);
   // Decode (GetPoseFromCandidate :369-375, Result :193-198).
   for (int dp = 0; dp < np; ++dp) {
     const int64_t i = pair_of[dp];

@@ -98,6 +98,24 @@ __global__ void level_gather(const uint8_t* __restrict__ prev, Brick3 pb, uint8_
   out[i] = static_cast<uint8_t>(v);
 }
 
+// Octet layout (Submap3Desc::octs): out[c] packs level[c + H*(x, y, z)].
+__global__ void octet_build(const uint8_t* __restrict__ level, Brick3 lb, int h,
+                            uint64_t* __restrict__ out, Brick3 ob) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const int64_t total = static_cast<int64_t>(ob.nx) * ob.ny * ob.nz;
+  if (i >= total) return;
+  const int x = static_cast<int>(i % ob.nx) + ob.ox;
+  const int y = static_cast<int>((i / ob.nx) % ob.ny) + ob.oy;
+  const int z = static_cast<int>(i / (static_cast<int64_t>(ob.nx) * ob.ny)) + ob.oz;
+  uint64_t v = 0;
+  for (int k = 0; k < 8; ++k) {
+    int64_t idx;
+    if (InBrick(lb, x + h * (k & 1), y + h * ((k >> 1) & 1), z + h * ((k >> 2) & 1), &idx))
+      v |= static_cast<uint64_t>(level[idx]) << (8 * k);
+  }
+  out[i] = v;
+}
+
 // ------------------------------------------------------------- RTCSM3D ----
 //
 // One workgroup per search rotation r; thread t scores translation t. The
@@ -511,91 +529,88 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
         const int d = sh.bn_d[half];
         const int ox = sh.bn_x[half], oy = sh.bn_y[half], oz = sh.bn_z[half];
         const int hw = 1 << (d - 1);
-        for (int z = 0; z <= hw; z += hw) {
-          if (oz + z > pd.wz) break;
-          for (int y = 0; y <= hw; y += hw) {
-            if (oy + y > pd.wxy) break;
-            for (int x = 0; x <= hw; x += hw) {
-              if (ox + x > pd.wxy) break;
-              cx8[nc] = ox + x;
-              cy8[nc] = oy + y;
-              cz8[nc] = oz + z;
-              ++nc;
-            }
-          }
+        // Children by octant k = z << 2 | y << 1 | x; present unless past the
+        // window (the reference's breaks, :412-430).
+        int present = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          cx8[k] = ox + ((k & 1) ? hw : 0);
+          cy8[k] = oy + ((k & 2) ? hw : 0);
+          cz8[k] = oz + ((k & 4) ? hw : 0);
+          if (cx8[k] <= pd.wxy && cy8[k] <= pd.wxy && cz8[k] <= pd.wz) present |= 1 << k;
         }
+        nc = present;
         cd = d - 1;
         const int e = max(0, cd - sm.full_resolution_depth + 1);
         const bool reduced = cd >= sm.full_resolution_depth;
-        const Brick3 b = sm.level[cd];
         const int lx = (-pd.wxy) >> e, ly = (-pd.wxy) >> e, lz = (-pd.wz) >> e;
-        // Children offsets relative to the brick origin; absent children get
-        // an impossible x so that their loads fall out of range (value 0).
-        int sx[8], sy[8], sz[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          sx[k] = k < nc ? (cx8[k] >> e) - b.ox : -(1 << 28);
-          sy[k] = k < nc ? (cy8[k] >> e) - b.oy : 0;
-          sz[k] = k < nc ? (cz8[k] >> e) - b.oz : 0;
-        }
-        // One buffer resource spans all levels; out-of-brick lookups use an
-        // offset beyond it, which the buffer unit returns as 0 (no branches,
-        // so the loads of consecutive points can be in flight together).
+        const Brick3 ob = sm.oct[cd];
+        // Base child (octant 0) offset relative to the octet box origin.
+        const int bx = (ox >> e) - ob.ox, by = (oy >> e) - ob.oy, bz = (oz >> e) - ob.oz;
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<uint8_t*>(sm.levels), 0, sm.levels_bytes, 0x00020000);
-        const int bnx = b.nx, bny = b.ny, bnz = b.nz, boff = static_cast<int>(b.offset);
+            const_cast<uint8_t*>(sm.octs), 0, sm.octs_bytes, 0x00020000);
+        const int onx = ob.nx, ony = ob.ny, onz = ob.nz, ooff = static_cast<int>(ob.offset);
         constexpr int kOOB3 = 0x7ffffff0;
-        auto off_of = [&](int x, int y, int z) {
-          const bool in = static_cast<unsigned>(x) < static_cast<unsigned>(bnx) &&
-                          static_cast<unsigned>(y) < static_cast<unsigned>(bny) &&
-                          static_cast<unsigned>(z) < static_cast<unsigned>(bnz);
-          return in ? boff + (z * bny + y) * bnx + x : kOOB3;
-        };
-        auto cell = [&](int i, int* x, int* y, int* z) {
+        auto load = [&](int i) -> uint64_t {
           int a = sh.cx[i], bb = sh.cy[i], c = sh.cz[i];
           if (reduced) {
             a = ((a - pd.wxy) >> e) - lx;
             bb = ((bb - pd.wxy) >> e) - ly;
             c = ((c - pd.wz) >> e) - lz;
           }
-          *x = a;
-          *y = bb;
-          *z = c;
+          a += bx;
+          bb += by;
+          c += bz;
+          const bool in = static_cast<unsigned>(a) < static_cast<unsigned>(onx) &&
+                          static_cast<unsigned>(bb) < static_cast<unsigned>(ony) &&
+                          static_cast<unsigned>(c) < static_cast<unsigned>(onz);
+          const int off = in ? ooff + ((c * ony + bb) * onx + a) * 8 : kOOB3;
+          const uint32_t lo = __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0);
+          const uint32_t hi = __builtin_amdgcn_raw_buffer_load_b32(rs, off + 4, 0, 0);
+          return (static_cast<uint64_t>(hi) << 32) | lo;
+        };
+        uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0, a4 = 0, a5 = 0, a6 = 0, a7 = 0;
+        auto accumulate = [&](uint64_t v) {
+          const uint32_t lo = static_cast<uint32_t>(v), hi = static_cast<uint32_t>(v >> 32);
+          a0 = __builtin_amdgcn_udot4(lo, 0x00000001u, a0, false);
+          a1 = __builtin_amdgcn_udot4(lo, 0x00000100u, a1, false);
+          a2 = __builtin_amdgcn_udot4(lo, 0x00010000u, a2, false);
+          a3 = __builtin_amdgcn_udot4(lo, 0x01000000u, a3, false);
+          a4 = __builtin_amdgcn_udot4(hi, 0x00000001u, a4, false);
+          a5 = __builtin_amdgcn_udot4(hi, 0x00000100u, a5, false);
+          a6 = __builtin_amdgcn_udot4(hi, 0x00010000u, a6, false);
+          a7 = __builtin_amdgcn_udot4(hi, 0x01000000u, a7, false);
         };
         int i = hl;
-        for (; i + kLanes < n; i += 2 * kLanes) {
-          int xa, ya, za, xb, yb, zb;
-          cell(i, &xa, &ya, &za);
-          cell(i + kLanes, &xb, &yb, &zb);
-          uint32_t va[8], vb[8];
-#pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            va[k] = __builtin_amdgcn_raw_buffer_load_b8(rs, off_of(xa + sx[k], ya + sy[k], za + sz[k]), 0, 0);
-            vb[k] = __builtin_amdgcn_raw_buffer_load_b8(rs, off_of(xb + sx[k], yb + sy[k], zb + sz[k]), 0, 0);
-          }
-#pragma unroll
-          for (int k = 0; k < 8; ++k) acc[k] += static_cast<int>(va[k] + vb[k]);
+        for (; i + 3 * kLanes < n; i += 4 * kLanes) {
+          const uint64_t v0 = load(i), v1 = load(i + kLanes), v2 = load(i + 2 * kLanes),
+                         v3 = load(i + 3 * kLanes);
+          accumulate(v0);
+          accumulate(v1);
+          accumulate(v2);
+          accumulate(v3);
         }
-        if (i < n) {
-          int xa, ya, za;
-          cell(i, &xa, &ya, &za);
-#pragma unroll
-          for (int k = 0; k < 8; ++k)
-            acc[k] += static_cast<int>(__builtin_amdgcn_raw_buffer_load_b8(
-                rs, off_of(xa + sx[k], ya + sy[k], za + sz[k]), 0, 0));
-        }
+        for (; i < n; i += kLanes) accumulate(load(i));
+        acc[0] = a0;
+        acc[1] = a1;
+        acc[2] = a2;
+        acc[3] = a3;
+        acc[4] = a4;
+        acc[5] = a5;
+        acc[6] = a6;
+        acc[7] = a7;
       }
 #pragma unroll
       for (int k = 0; k < 8; ++k)
         for (int m = kLanes / 2; m > 0; m >>= 1) acc[k] += __shfl_xor(acc[k], m, 64);
       if (half < nb && hl == 0) {
-        lookups += static_cast<unsigned long long>(nc) * n;
+        lookups += static_cast<unsigned long long>(__popc(nc)) * n;
         const int best_sum = static_cast<int>(sh.best >> pd.key_shift);
         if (cd > 0) {
           int idx[8];
           int m = 0;
-          for (int k = 0; k < nc; ++k)
-            if (acc[k] >= pd.min_sum && acc[k] >= best_sum) idx[m++] = k;
+          for (int k = 0; k < 8; ++k)
+            if (((nc >> k) & 1) && acc[k] >= pd.min_sum && acc[k] >= best_sum) idx[m++] = k;
           for (int a = 1; a < m; ++a) {  // ascending: the best child is popped first
             const int v = idx[a];
             int b2 = a - 1;
@@ -615,8 +630,8 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
             sh.ssum[base + a] = acc[k];
           }
         } else {
-          for (int k = 0; k < nc; ++k) {
-            if (acc[k] < pd.min_sum) continue;
+          for (int k = 0; k < 8; ++k) {
+            if (!((nc >> k) & 1) || acc[k] < pd.min_sum) continue;
             const unsigned long long id = LeafId(pd, yw.yaw_id, cx8[k], cy8[k], cz8[k]);
             const unsigned long long key = (static_cast<unsigned long long>(acc[k]) << pd.key_shift) |
                                            (~id & ((1ull << pd.key_shift) - 1));
@@ -831,6 +846,15 @@ hipError_t LaunchLevelGather(const uint8_t* prev, const Brick3& pb, uint8_t* out
   if (total <= 0) return hipSuccess;
   hipLaunchKernelGGL(level_gather, dim3(static_cast<unsigned>((total + 255) / 256)), dim3(256), 0,
                      st, prev, pb, out, ob, shift, half);
+  return hipGetLastError();
+}
+
+hipError_t LaunchOctetBuild(const uint8_t* level, const Brick3& lb, int h, uint64_t* out,
+                            const Brick3& ob, hipStream_t st) {
+  const int64_t total = static_cast<int64_t>(ob.nx) * ob.ny * ob.nz;
+  if (total <= 0) return hipSuccess;
+  hipLaunchKernelGGL(octet_build, dim3(static_cast<unsigned>((total + 255) / 256)), dim3(256), 0,
+                     st, level, lb, h, out, ob);
   return hipGetLastError();
 }
 

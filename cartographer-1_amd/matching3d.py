@@ -206,12 +206,53 @@ class FastCorrelativeScanMatcher3D:
         return _result(r)
 
 
+PAIR3_DTYPE = np.dtype([("submap", np.int32), ("node", np.int32), ("full_submap", np.int32),
+                        ("min_score", np.float32), ("node_t", np.float64, 3),
+                        ("node_q", np.float64, 4), ("submap_t", np.float64, 3),
+                        ("submap_q", np.float64, 4)])
+RESULT3_DTYPE = np.dtype([("status", np.int32), ("score", np.float32), ("t", np.float64, 3),
+                          ("q", np.float64, 4), ("rotational_score", np.float32),
+                          ("low_resolution_score", np.float32)])
+
+
+def make_pairs_3d(submap, node, min_score, full_submap=True, node_q=None, node_t=None,
+                  submap_q=None, submap_t=None) -> np.ndarray:
+    """Vectorised csm_pair3d array (pose rotations as (w, x, y, z))."""
+    submap = np.asarray(submap, np.int32)
+    pairs = np.zeros(len(submap), PAIR3_DTYPE)
+    pairs["submap"] = submap
+    pairs["node"] = np.asarray(node, np.int32)
+    pairs["full_submap"] = np.asarray(full_submap, np.int32)
+    pairs["min_score"] = min_score
+    pairs["node_q"] = (1.0, 0.0, 0.0, 0.0) if node_q is None else node_q
+    pairs["submap_q"] = (1.0, 0.0, 0.0, 0.0) if submap_q is None else submap_q
+    if node_t is not None:
+        pairs["node_t"] = node_t
+    if submap_t is not None:
+        pairs["submap_t"] = submap_t
+    return pairs
+
+
 def match_batch_3d(matchers: Sequence[FastCorrelativeScanMatcher3D], nodes: Sequence[NodeData3D],
-                   pairs: Sequence[tuple], context: Optional[Context] = None) -> List[Result3D]:
-    """pairs: (submap, node, full_submap, min_score, node_pose, submap_pose)."""
+                   pairs, context: Optional[Context] = None):
+    """Batched FastCSM3D search. `pairs` is a PAIR3_DTYPE array (make_pairs_3d)
+    or a sequence of (submap, node, full_submap, min_score, node_pose,
+    submap_pose) tuples. Returns a RESULT3_DTYPE array in pair order (tuple
+    input: a list of Result3D records)."""
     ctx = context or (matchers[0].context if matchers else default_context())
     lib = ctx._lib
+    assert PAIR3_DTYPE.itemsize == C.sizeof(Pair3D)
+    assert RESULT3_DTYPE.itemsize == C.sizeof(Result3D)
     cnodes = (Node3D * len(nodes))(*[n.to_c() for n in nodes])
+    handles = (C.c_void_p * len(matchers))(*[m.handle for m in matchers])
+    if isinstance(pairs, np.ndarray):
+        arr = np.ascontiguousarray(pairs, PAIR3_DTYPE)
+        out = np.zeros(len(arr), RESULT3_DTYPE)
+        _check(lib.csm_fast3d_match_batch(ctx.handle, handles, len(matchers), cnodes, len(nodes),
+                                          arr.ctypes.data_as(C.POINTER(Pair3D)), len(arr),
+                                          out.ctypes.data_as(C.POINTER(Result3D))),
+               "csm_fast3d_match_batch")
+        return out
     cpairs = (Pair3D * len(pairs))()
     for i, (s, n, full, ms, npose, spose) in enumerate(pairs):
         cpairs[i].submap, cpairs[i].node, cpairs[i].full_submap = s, n, 1 if full else 0
@@ -219,7 +260,6 @@ def match_batch_3d(matchers: Sequence[FastCorrelativeScanMatcher3D], nodes: Sequ
         cpairs[i].node_pose = _pose(npose)
         cpairs[i].submap_pose = _pose(spose)
     results = (Result3D * len(pairs))()
-    handles = (C.c_void_p * len(matchers))(*[m.handle for m in matchers])
     _check(lib.csm_fast3d_match_batch(ctx.handle, handles, len(matchers), cnodes, len(nodes),
                                       cpairs, len(pairs), results), "csm_fast3d_match_batch")
     return list(results)

@@ -33,8 +33,9 @@ mats = [csm.FastCorrelativeScanMatcher3D(g[0], g[1], w.submap_hist[s], o, ctx) f
 build = time.time() - t
 nodes = [w.node(i) for i in range(a.nodes)]
 ident = ((0, 0, 0), (1, 0, 0, 0))
-pairs = [(s, n, True, 0.6, ((0, 0, 0), w.node_rotation(n)), ident) for s in range(a.submaps)
-         for n in range(a.nodes)]
+sub = np.repeat(np.arange(a.submaps), a.nodes)
+nod = np.tile(np.arange(a.nodes), a.submaps)
+pairs = csm.make_pairs_3d(sub, nod, 0.6, True, node_q=np.array([w.node_rotation(n) for n in nod]))
 csm.match_batch_3d(mats, nodes, pairs[:50], ctx)
 ctx.reset_timing()
 ctx.enable_timing(True)
@@ -42,7 +43,7 @@ t = time.time()
 res = csm.match_batch_3d(mats, nodes, pairs, ctx)
 dt = time.time() - t
 tm = ctx.timing()
-acc = sum(1 for r in res if r.status == 0)
+acc = int((res["status"] == 0).sum())
 out = {"pairs": len(pairs), "s": dt, "pairs_per_s": len(pairs) / dt, "accepted": acc,
        "kernel_ms": tm.fast3d_kernel_ms, "lookups": tm.fast3d_lookups,
        "GBps_alg": tm.fast3d_lookups / (tm.fast3d_kernel_ms * 1e-3) / 1e9 if tm.fast3d_kernel_ms else 0,
