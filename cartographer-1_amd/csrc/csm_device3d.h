@@ -13,6 +13,7 @@ constexpr int kMax3dPoints = 4096;        // high-resolution points per node (LD
 constexpr int kTopLds3d = 24 * 1024;      // top pyramid level cached in LDS when it fits
 constexpr int kRootChunk3d = 128;         // roots fed to the DFS stack at a time
 constexpr int kRootScore3d = 512;         // roots scored at a time (one per lane)
+constexpr int kTopCells3d = 512;          // distinct top-level cells of a cloud (LDS list)
 constexpr int kBatch3d = 16;              // DFS nodes scored per step (16 lanes each)
 constexpr int kMax3dTop = 1 << 20;        // top-level candidates per yaw
 constexpr int kStack3d = 1024;            // DFS stack entries per workgroup

@@ -214,8 +214,14 @@ struct F3Shared {
   int16_t rbx[kRootScore3d], rby[kRootScore3d], rbz[kRootScore3d];
   int rbs[kRootScore3d];
   int nroot;
+  // The cloud at top-level resolution as distinct cells with counts (root
+  // sums = sum over cells of count x top[cell + offset]).
+  int tcell[kTopCells3d];
+  uint16_t tcount[kTopCells3d];
+  int ntcell;
   int nbatch, nleaf, nchild, child_depth, sp, item, error, accepted, cached_submap;
   unsigned long long best;
+  unsigned long long best_seen;  // last read of the pair's global best
 };
 
 __device__ __forceinline__ unsigned long long LeafId(const Pair3Desc& pd, int yaw, int ox, int oy,
@@ -363,6 +369,7 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
     if (tid == 0) {
       sh.sp = 0;
       sh.best = best[yw.pair];
+      sh.best_seen = 0;
     }
     __syncthreads();
     // Lowest-resolution candidates (GenerateLowestResolutionCandidates
@@ -410,6 +417,43 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
       }
     }
     __syncthreads();
+    // Histogram of the cloud's top-level cells over its box (count grid in
+    // the empty stack sums), compacted to a list when box and list fit.
+    const int gbx = sh.rmax[0] - sh.rmin[0] + 1, gby = sh.rmax[1] - sh.rmin[1] + 1,
+              gbz = sh.rmax[2] - sh.rmin[2] + 1;
+    const bool use_cells = n > 0 && static_cast<int64_t>(gbx) * gby * gbz <= kStack3d &&
+                           sh.rmin[0] >= -1024 && sh.rmax[0] < 1024 && sh.rmin[1] >= -1024 &&
+                           sh.rmax[1] < 1024 && sh.rmin[2] >= -512 && sh.rmax[2] < 512;
+    if (use_cells) {
+      for (int k = tid; k < gbx * gby * gbz; k += kSearch3dThreads) sh.ssum[k] = 0;
+      if (tid == 0) sh.ntcell = 0;
+      __syncthreads();
+      for (int i = tid; i < n; i += kSearch3dThreads) {
+        int c[3] = {sh.cx[i], sh.cy[i], sh.cz[i]};
+        if (treduced) {
+          c[0] = ((c[0] - pd.wxy) >> te) - lwx;
+          c[1] = ((c[1] - pd.wxy) >> te) - lwy;
+          c[2] = ((c[2] - pd.wz) >> te) - lwz;
+        }
+        atomicAdd(&sh.ssum[((c[2] - sh.rmin[2]) * gby + (c[1] - sh.rmin[1])) * gbx + (c[0] - sh.rmin[0])], 1);
+      }
+      __syncthreads();
+      for (int k = tid; k < gbx * gby * gbz; k += kSearch3dThreads) {
+        const int cnt = sh.ssum[k];
+        if (cnt > 0) {
+          const int at = atomicAdd(&sh.ntcell, 1);
+          if (at < kTopCells3d) {
+            const int x = k % gbx + sh.rmin[0], y = (k / gbx) % gby + sh.rmin[1],
+                      z = k / (gbx * gby) + sh.rmin[2];
+            sh.tcell[at] = (x + 1024) | ((y + 1024) << 11) | ((z + 512) << 22);
+            sh.tcount[at] = static_cast<uint16_t>(cnt);
+          }
+        }
+      }
+      __syncthreads();
+    }
+    const bool cells_ok = use_cells && sh.ntcell <= kTopCells3d;
+    const int ntc = cells_ok ? sh.ntcell : 0;
     const bool skip_empty = pd.min_sum > 0;
     for (int r0 = 0; r0 < T; r0 += kRootScore3d) {
     const int r1 = min(T, r0 + kRootScore3d);
@@ -428,16 +472,31 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
              sh.rmax[2] + sz < tb.oz || sh.rmin[2] + sz >= tb.oz + tb.nz))
           continue;
         int sum = 0;
-        root_lookups += n;
-        for (int i = 0; i < n; ++i) {
-          int x = sh.cx[i], y = sh.cy[i], z = sh.cz[i];
-          if (treduced) {
-            x = ((x - pd.wxy) >> te) - lwx;
-            y = ((y - pd.wxy) >> te) - lwy;
-            z = ((z - pd.wz) >> te) - lwz;
+        if (cells_ok) {
+          root_lookups += ntc;
+          const int qx = sx - tb.ox - 1024, qy = sy - tb.oy - 1024, qz = sz - tb.oz - 512;
+          for (int c = 0; c < ntc; ++c) {
+            const int pc = sh.tcell[c];
+            const int x = (pc & 2047) + qx, y = ((pc >> 11) & 2047) + qy, z = static_cast<int>(static_cast<unsigned>(pc) >> 22) + qz;
+            if (static_cast<unsigned>(x) < static_cast<unsigned>(tb.nx) &&
+                static_cast<unsigned>(y) < static_cast<unsigned>(tb.ny) &&
+                static_cast<unsigned>(z) < static_cast<unsigned>(tb.nz)) {
+              const int idx = (z * tb.ny + y) * tb.nx + x;
+              sum += static_cast<int>(sh.tcount[c]) * (lds_top ? sh.top[idx] : tglobal[idx]);
+            }
           }
-          int64_t idx;
-          if (InBrick(tb, x + sx, y + sy, z + sz, &idx)) sum += lds_top ? sh.top[idx] : tglobal[idx];
+        } else {
+          root_lookups += n;
+          for (int i = 0; i < n; ++i) {
+            int x = sh.cx[i], y = sh.cy[i], z = sh.cz[i];
+            if (treduced) {
+              x = ((x - pd.wxy) >> te) - lwx;
+              y = ((y - pd.wxy) >> te) - lwy;
+              z = ((z - pd.wz) >> te) - lwz;
+            }
+            int64_t idx;
+            if (InBrick(tb, x + sx, y + sy, z + sz, &idx)) sum += lds_top ? sh.top[idx] : tglobal[idx];
+          }
         }
         if (sum >= pd.min_sum && sum >= best_sum) {
           const int at = atomicAdd(&sh.nroot, 1);
@@ -500,22 +559,40 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
     // the lanes of a node split the points and score its (up to) 8 children,
     // reduced with shuffles only.
     for (;;) {
-      if (tid == 0) {
-        sh.best = max(sh.best, *reinterpret_cast<volatile unsigned long long*>(best + yw.pair));
-        const int best_sum = static_cast<int>(sh.best >> pd.key_shift);
-        int m = 0;
-        while (sh.sp > 0 && m < kBatch3d) {
-          const int at = --sh.sp;
-          const int s = sh.ssum[at];
-          if (s < best_sum || s < pd.min_sum) continue;
-          sh.bn_x[m] = sh.sx[at];
-          sh.bn_y[m] = sh.sy[at];
-          sh.bn_z[m] = sh.sz[at];
-          sh.bn_d[m] = sh.sd[at];
-          ++m;
+      // Pop up to kBatch3d nodes, skipping pruned ones, 64 entries per step
+      // across wave 0 (the same nodes, in the same order, as popping one by
+      // one from the top).
+      if (tid < 64) {
+        const unsigned long long bk = max(sh.best, sh.best_seen);
+        const int best_sum = static_cast<int>(bk >> pd.key_shift);
+        int sp = sh.sp, m = 0;
+        while (sp > 0 && m < kBatch3d) {
+          const int at = sp - 1 - tid;
+          int s = 0;
+          bool keep = false;
+          if (at >= 0) {
+            s = sh.ssum[at];
+            keep = s >= best_sum && s >= pd.min_sum;
+          }
+          const unsigned long long mask = __ballot(keep);
+          const int rank = m + __popcll(mask & ((1ull << tid) - 1ull));
+          if (keep && rank < kBatch3d) {
+            sh.bn_x[rank] = sh.sx[at];
+            sh.bn_y[rank] = sh.sy[at];
+            sh.bn_z[rank] = sh.sz[at];
+            sh.bn_d[rank] = sh.sd[at];
+          }
+          const unsigned long long last = __ballot(keep && rank == kBatch3d - 1);
+          const int consumed = last ? __ffsll(static_cast<long long>(last)) : min(64, sp);
+          m = min(kBatch3d, m + __popcll(mask));
+          sp -= consumed;
         }
-        sh.nbatch = m;
-        sh.nleaf = 0;
+        if (tid == 0) {
+          sh.best = bk;
+          sh.sp = sp;
+          sh.nbatch = m;
+          sh.nleaf = 0;
+        }
       }
       __syncthreads();
       const int nb = sh.nbatch;
@@ -525,6 +602,10 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
       int cx8[8], cy8[8], cz8[8];
       int nc = 0, cd = 0;
       int acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      // Other yaws' progress on this pair, read while the batch scores and
+      // folded in at the next pop.
+      unsigned long long gbest = 0;
+      if (tid == 0) gbest = *reinterpret_cast<volatile unsigned long long*>(best + yw.pair);
       if (half < nb) {
         const int d = sh.bn_d[half];
         const int ox = sh.bn_x[half], oy = sh.bn_y[half], oz = sh.bn_z[half];
@@ -582,6 +663,13 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
           a7 = __builtin_amdgcn_udot4(hi, 0x01000000u, a7, false);
         };
         int i = hl;
+        for (; i + 7 * kLanes < n; i += 8 * kLanes) {
+          uint64_t v[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) v[u] = load(i + u * kLanes);
+#pragma unroll
+          for (int u = 0; u < 8; ++u) accumulate(v[u]);
+        }
         for (; i + 3 * kLanes < n; i += 4 * kLanes) {
           const uint64_t v0 = load(i), v1 = load(i + kLanes), v2 = load(i + 2 * kLanes),
                          v3 = load(i + 3 * kLanes);
@@ -600,9 +688,18 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
         acc[6] = a6;
         acc[7] = a7;
       }
+      // Row (16-lane) sums with DPP: xor 1, xor 2 (quad_perm), then the
+      // half-row and row mirrors; every lane of the row ends with the sum.
+      static_assert(kLanes == 16, "DPP row reduction assumes 16 lanes per node");
 #pragma unroll
-      for (int k = 0; k < 8; ++k)
-        for (int m = kLanes / 2; m > 0; m >>= 1) acc[k] += __shfl_xor(acc[k], m, 64);
+      for (int k = 0; k < 8; ++k) {
+        int v = acc[k];
+        v += __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+        v += __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+        v += __builtin_amdgcn_update_dpp(0, v, 0x141, 0xF, 0xF, false);  // row_half_mirror
+        v += __builtin_amdgcn_update_dpp(0, v, 0x140, 0xF, 0xF, false);  // row_mirror
+        acc[k] = v;
+      }
       if (half < nb && hl == 0) {
         lookups += static_cast<unsigned long long>(__popc(nc)) * n;
         const int best_sum = static_cast<int>(sh.best >> pd.key_shift);
@@ -644,8 +741,11 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
           }
         }
       }
+      if (tid == 0) {
+        sh.best_seen = gbest;
+        prof[5] += 1;
+      }
       __syncthreads();
-      if (tid == 0) prof[5] += 1;
       const int nl = sh.nleaf;
       if (nl == 0) continue;
       const long long t_leaf = clock64();
