@@ -8,11 +8,13 @@
 
 namespace csm {
 
-constexpr int kMaxLevels3d = 10;
+constexpr int kMaxLevels3d = 12;
+constexpr int kExtraLevels3d = 2;       // coarser levels above the reference's stack (roots only)
+constexpr int kRootTarget3d = 512;       // a pair's roots start at the lowest level with <= this many
 constexpr int kMax3dPoints = 4096;        // high-resolution points per node (LDS)
-constexpr int kTopLds3d = 24 * 1024;      // top pyramid level cached in LDS when it fits
+constexpr int kTopLds3d = 6 * 1024;       // top pyramid level cached in LDS when it fits
 constexpr int kRootChunk3d = 128;         // roots fed to the DFS stack at a time
-constexpr int kRootScore3d = 512;         // roots scored at a time (one per lane)
+constexpr int kRootScore3d = 256;         // roots scored at a time (one per lane)
 constexpr int kTopCells3d = 512;          // distinct top-level cells of a cloud (LDS list)
 constexpr int kBatch3d = 16;              // DFS nodes scored per step (16 lanes each)
 constexpr int kMax3dTop = 1 << 20;        // top-level candidates per yaw
@@ -20,6 +22,7 @@ constexpr int kStack3d = 1024;            // DFS stack entries per workgroup
 constexpr int kMax3dYaws = 1 << 16;
 constexpr int kMax3dWindow = 1 << 14;
 constexpr int kSearch3dThreads = 256;
+constexpr int kSearch3dBlocksPerCu = 3;   // resident workgroups per CU (LDS < 160 KiB / 3)
 constexpr int kCellLimit3d = 16000;       // |cell index| kept in int16 in LDS
 // Per pair: key = sum << key_shift | ~leaf_id, leaf_id = ((yaw << bxy | x) << bxy
 // | y) << bz | z with x = ox + wxy etc.; the host sizes the fields so that
@@ -41,6 +44,12 @@ struct Submap3Desc {
   int32_t levels_bytes;   // its size (< 2^31: one buffer resource spans it)
   Brick3 level[kMaxLevels3d];
   int32_t num_levels;     // branch_and_bound_depth
+  // Levels built: num_levels plus up to kExtraLevels3d coarser ones with the
+  // same recurrence. A node of level L + 1 bounds its (up to) 8 children of
+  // level L exactly as within the reference's stack, so rooting a search
+  // there reaches the same top-level candidates (the children past the
+  // window are dropped) while scoring far fewer roots.
+  int32_t search_levels;
   int32_t full_resolution_depth;
   float resolution;
   // Octet layout of levels 0..num_levels-2 (the DFS child levels): one
@@ -66,7 +75,8 @@ struct Pair3Desc {
   int64_t low_offset;
   int32_t yaw_begin, num_yaws;
   int32_t wxy, wz;          // linear window sizes (voxels)
-  int32_t top_nx, top_ny, top_nz;  // lowest-resolution candidates per axis
+  int32_t root_level;       // level the pair's roots are generated and scored at
+  int32_t top_nx, top_ny, top_nz;  // roots per axis at root_level
   int32_t min_sum;          // smallest sum whose score exceeds min_score
   float min_low_resolution_score;
   int32_t key_shift, bits_xy, bits_z;  // leaf key layout

@@ -382,9 +382,10 @@ int csm_fast3d_create(csm_context* ctx, const csm_hybrid_grid* high, const csm_h
   m->histogram.assign(histogram, histogram + histogram_size);
   // Level boxes (PrecomputationGridStack3D, .cc:57-77): level d covers the
   // cells its scatter-max can reach from level d-1.
-  const int depth = options->branch_and_bound_depth;
+  const int depth = std::min(options->branch_and_bound_depth + kExtraLevels3d, kMaxLevels3d);
   Submap3Desc& d = m->desc;
-  d.num_levels = depth;
+  d.num_levels = options->branch_and_bound_depth;
+  d.search_levels = depth;
   d.full_resolution_depth = options->full_resolution_depth;
   d.resolution = high->resolution;
   int64_t total = 0;
@@ -429,7 +430,7 @@ int csm_fast3d_create(csm_context* ctx, const csm_hybrid_grid* high, const csm_h
   if ((rc = m->levels.Reserve(std::max<int64_t>(total, 256)))) return rc;
   d.levels = m->levels.as<uint8_t>();
   d.levels_bytes = static_cast<int32_t>(std::max<int64_t>(total, 256));
-  // Octet bricks of the DFS child levels 0..depth-2.
+  // Octet bricks of the DFS child levels 0..search_levels-2.
   int64_t otot = 0;
   for (int l = 0; l + 1 < depth; ++l) {
     const int h = l < options->full_resolution_depth ? (1 << l)
@@ -565,9 +566,23 @@ void PreparePair(const csm_fast3d* m, const csm_node3d& node, const csm_pair3d& 
   }
   d.wxy = wxy;
   d.wz = wz;
-  const int step = 1 << (m->desc.num_levels - 1);
-  d.top_nx = d.top_ny = (2 * wxy + step) / step;
-  d.top_nz = (2 * wz + step) / step;
+  // Roots: the reference's lowest-resolution candidates (:301-326) at level
+  // max_depth, or a coarser level of the same grid of offsets when that
+  // level has more than kRootTarget3d of them or does not fit the LDS cache.
+  int level = m->desc.num_levels - 1;
+  for (;;) {
+    const int step = 1 << level;
+    d.root_level = level;
+    d.top_nx = d.top_ny = (2 * wxy + step) / step;
+    d.top_nz = (2 * wz + step) / step;
+    const Brick3& b = m->desc.level[level];
+    const int64_t bytes = static_cast<int64_t>(b.nx) * b.ny * b.nz;
+    if (level + 1 >= m->desc.search_levels ||
+        (static_cast<int64_t>(d.top_nx) * d.top_ny * d.top_nz <= kRootTarget3d &&
+         bytes <= kTopLds3d))
+      break;
+    ++level;
+  }
   if (static_cast<int64_t>(d.top_nx) * d.top_ny * d.top_nz > kMax3dTop) {
     out->status = CSM_ERANGE;
     return;
@@ -710,6 +725,20 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
     PreparePair(submaps[p.submap], nd, p, &prep[i]);
   });
   lap(1);
+  if (prof3 && num_pairs > 0) {
+    long hist[kMaxLevels3d] = {};
+    for (int64_t i = 0; i < num_pairs; ++i)
+      if (prep[i].status == CSM_OK) ++hist[prep[i].desc.root_level];
+    const Submap3Desc& sd0 = submaps[pairs[0].submap]->desc;
+    std::fprintf(stderr, "fast3d root levels:");
+    for (int l = 0; l < kMaxLevels3d; ++l)
+      if (hist[l]) std::fprintf(stderr, " L%d:%ld", l, hist[l]);
+    std::fprintf(stderr, " | submap0 levels %d/%d bytes:", sd0.num_levels, sd0.search_levels);
+    for (int l = 0; l < sd0.search_levels; ++l)
+      std::fprintf(stderr, " %lld", static_cast<long long>(sd0.level[l].nx) * sd0.level[l].ny * sd0.level[l].nz);
+    std::fprintf(stderr, " | pair0 w %d/%d T %d\n", prep[0].desc.wxy, prep[0].desc.wz,
+                 prep[0].desc.top_nx * prep[0].desc.top_ny * prep[0].desc.top_nz);
+  }
   // Phase 2 (device): rotational scores of every (pair, yaw).
   {
     std::vector<float> hists;
@@ -816,7 +845,7 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
   if ((rc = ctx->f3_low_points.Reserve(sizeof(float) * std::max<size_t>(lpts.size(), 3)))) return rc;
   if ((rc = ctx->f3_best.Reserve(sizeof(unsigned long long) * np + sizeof(float) * np))) return rc;
   if ((rc = ctx->f3_status.Reserve(sizeof(int32_t) * np))) return rc;
-  if ((rc = ctx->f3_counter.Reserve(8 + 8 * sizeof(unsigned long long)))) return rc;
+  if ((rc = ctx->f3_counter.Reserve(8 + 16 * sizeof(unsigned long long)))) return rc;
   Pair3Desc* dpairs = ctx->f3_pairs.as<Pair3Desc>();
   Submap3Desc* dsub = reinterpret_cast<Submap3Desc*>(dpairs + np);
   unsigned long long* dbest = ctx->f3_best.as<unsigned long long>();
@@ -838,11 +867,11 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
                            hipMemcpyHostToDevice, st));
   CSM_HIP(hipMemsetAsync(dbest, 0, sizeof(unsigned long long) * np, st));
   CSM_HIP(hipMemsetAsync(ctx->f3_status.ptr, 0, sizeof(int32_t) * np, st));
-  CSM_HIP(hipMemsetAsync(ctx->f3_counter.ptr, 0, 8 + 8 * sizeof(unsigned long long), st));
+  CSM_HIP(hipMemsetAsync(ctx->f3_counter.ptr, 0, 8 + 16 * sizeof(unsigned long long), st));
   lap(4);
   if (ctx->timing) CSM_HIP(hipEventRecord(ctx->ev0, st));
   if (ny > 0) {
-    const int grid = std::max(1, std::min(ny, ctx->num_cus * 2));
+    const int grid = std::max(1, std::min(ny, ctx->num_cus * kSearch3dBlocksPerCu));
     CSM_HIP(LaunchFast3dSearch(grid, st, dsub, dpairs, ctx->f3_yaws.as<Yaw3Desc>(), ny,
                                ctx->f3_points.as<float>(), ctx->f3_low_points.as<float>(),
                                dcounter, dbest, ctx->f3_status.as<int32_t>(), dstats));
@@ -853,7 +882,7 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
   std::vector<unsigned long long> keys(np);
   std::vector<float> lows(np);
   std::vector<int32_t> stat(np);
-  unsigned long long lookups = 0, prof[8] = {0};
+  unsigned long long lookups = 0, prof[16] = {0};
   CSM_HIP(hipMemcpyAsync(keys.data(), dbest, sizeof(unsigned long long) * np,
                          hipMemcpyDeviceToHost, st));
   CSM_HIP(hipMemcpyAsync(lows.data(), dlow, sizeof(float) * np, hipMemcpyDeviceToHost, st));
@@ -870,10 +899,12 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
     ctx->t.fast3d_lookups += static_cast<double>(lookups);
     if (std::getenv("CSM_PROFILE3D"))
       std::fprintf(stderr,
-                   "fast3d phases (Mcycles, thread 0 sums): item+discretize %.1f roots %.1f "
-                   "sort %.1f dfs %.1f leaf %.1f | batches %llu leaves %llu items %d\n",
-                   prof[1] / 1e6, prof[2] / 1e6, prof[3] / 1e6, prof[4] / 1e6, prof[5] / 1e6,
-                   prof[6], prof[7], ny);
+                   "fast3d phases (Mcycles, thread 0 sums): item+discretize %.1f top-copy %.1f "
+                   "box %.1f cells %.1f roots %.1f sort %.1f dfs %.1f leaf %.1f | batches %llu "
+                   "leaves %llu items %d roots-scored %llu roots-kept %llu\n",
+                   prof[1] / 1e6, prof[8] / 1e6, prof[9] / 1e6, prof[10] / 1e6, prof[2] / 1e6,
+                   prof[3] / 1e6, prof[4] / 1e6, prof[5] / 1e6, prof[6], prof[7], ny, prof[11],
+                   prof[12]);
   }
   lap(5);
   if (prof3)

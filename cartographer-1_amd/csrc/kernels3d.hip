@@ -206,7 +206,7 @@ struct F3Shared {
   unsigned long long leaf_key[8];
   int order[8];
   float lr[kSearch3dThreads];
-  uint8_t top[kTopLds3d];
+  alignas(16) uint8_t top[kTopLds3d];
   int bn_x[kBatch3d], bn_y[kBatch3d], bn_z[kBatch3d], bn_d[kBatch3d];
   unsigned long long leaf_keys[8 * kBatch3d];
   int leaf_x[8 * kBatch3d], leaf_y[8 * kBatch3d], leaf_z[8 * kBatch3d];
@@ -327,7 +327,7 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
   __shared__ F3Shared sh;
   const int tid = threadIdx.x;
   unsigned long long lookups = 0, root_lookups = 0;
-  long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // thread 0: phase cycles / counts
+  long long prof[12] = {};  // thread 0: phase cycles / counts
   if (tid == 0) sh.cached_submap = -1;
   for (;;) {
     if (tid == 0) sh.item = static_cast<int>(atomicAdd(counter, 1u));
@@ -363,7 +363,7 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
     }
     long long t_mark = clock64();
     if (tid == 0) prof[0] += t_mark - t_item;
-    const int top = sm.num_levels - 1;
+    const int top = pd.root_level;
     const int step = 1 << top;
     const int T = pd.top_nx * pd.top_ny * pd.top_nz;
     if (tid == 0) {
@@ -378,14 +378,32 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
     // searched to exhaustion before the next one.
     const Brick3 tb = sm.level[top];
     const int64_t tbytes = static_cast<int64_t>(tb.nx) * tb.ny * tb.nz;
-    const bool lds_top = tbytes <= kTopLds3d;
-    if (lds_top && sh.cached_submap != pd.submap) {
-      const uint8_t* src = sm.levels + tb.offset;
-      for (int64_t k = tid; k < tbytes; k += kSearch3dThreads) sh.top[k] = src[k];
+    const int tvec = static_cast<int>((tbytes + 15) / 16);  // level offsets are 256-aligned
+    const bool lds_top = tvec * 16 <= kTopLds3d;
+    if (lds_top && sh.cached_submap != pd.submap * 16 + top) {
+      const uint4* src = reinterpret_cast<const uint4*>(sm.levels + tb.offset);
+      uint4* dst = reinterpret_cast<uint4*>(sh.top);
+      constexpr int kPer = (kTopLds3d / 16 + kSearch3dThreads - 1) / kSearch3dThreads;
+      uint4 v[kPer];
+#pragma unroll
+      for (int u = 0; u < kPer; ++u) {
+        const int k = tid + u * kSearch3dThreads;
+        if (k < tvec) v[u] = src[k];
+      }
+#pragma unroll
+      for (int u = 0; u < kPer; ++u) {
+        const int k = tid + u * kSearch3dThreads;
+        if (k < tvec) dst[k] = v[u];
+      }
       __syncthreads();
-      if (tid == 0) sh.cached_submap = pd.submap;
+      if (tid == 0) sh.cached_submap = pd.submap * 16 + top;
     }
     __syncthreads();
+    if (tid == 0) {
+      const long long now = clock64();
+      prof[7] += now - t_mark;
+      t_mark = now;
+    }
     const int te = max(0, top - sm.full_resolution_depth + 1);
     const bool treduced = top >= sm.full_resolution_depth;
     const int lwx = (-pd.wxy) >> te, lwy = (-pd.wxy) >> te, lwz = (-pd.wz) >> te;
@@ -412,11 +430,24 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
         }
       }
       for (int a = 0; a < 3; ++a) {
-        atomicMin(&sh.rmin[a], mn[a]);
-        atomicMax(&sh.rmax[a], mx[a]);
+        for (int m = 32; m > 0; m >>= 1) {
+          mn[a] = min(mn[a], __shfl_xor(mn[a], m, 64));
+          mx[a] = max(mx[a], __shfl_xor(mx[a], m, 64));
+        }
+      }
+      if ((tid & 63) == 0) {
+        for (int a = 0; a < 3; ++a) {
+          atomicMin(&sh.rmin[a], mn[a]);
+          atomicMax(&sh.rmax[a], mx[a]);
+        }
       }
     }
     __syncthreads();
+    if (tid == 0) {
+      const long long now = clock64();
+      prof[8] += now - t_mark;
+      t_mark = now;
+    }
     // Histogram of the cloud's top-level cells over its box (count grid in
     // the empty stack sums), compacted to a list when box and list fit.
     const int gbx = sh.rmax[0] - sh.rmin[0] + 1, gby = sh.rmax[1] - sh.rmin[1] + 1,
@@ -454,6 +485,11 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
     }
     const bool cells_ok = use_cells && sh.ntcell <= kTopCells3d;
     const int ntc = cells_ok ? sh.ntcell : 0;
+    if (tid == 0) {
+      const long long now = clock64();
+      prof[9] += now - t_mark;
+      t_mark = now;
+    }
     const bool skip_empty = pd.min_sum > 0;
     for (int r0 = 0; r0 < T; r0 += kRootScore3d) {
     const int r1 = min(T, r0 + kRootScore3d);
@@ -461,31 +497,57 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
     __syncthreads();
     {
       const int best_sum = static_cast<int>(sh.best >> pd.key_shift);
-      for (int j = r0 + tid; j < r1; j += kSearch3dThreads) {
+      const int lane = tid & 63;
+      for (int j0 = r0; j0 < r1; j0 += kSearch3dThreads) {
+        const int j = j0 + tid;
         const int ixx = j % pd.top_nx, iyy = (j / pd.top_nx) % pd.top_ny,
                   izz = j / (pd.top_nx * pd.top_ny);
         const int ox = -pd.wxy + ixx * step, oy = -pd.wxy + iyy * step, oz = -pd.wz + izz * step;
         const int sx = ox >> te, sy = oy >> te, sz = oz >> te;
-        if (skip_empty &&
-            (sh.rmax[0] + sx < tb.ox || sh.rmin[0] + sx >= tb.ox + tb.nx ||
-             sh.rmax[1] + sy < tb.oy || sh.rmin[1] + sy >= tb.oy + tb.ny ||
-             sh.rmax[2] + sz < tb.oz || sh.rmin[2] + sz >= tb.oz + tb.nz))
-          continue;
+        const bool valid =
+            j < r1 && !(skip_empty &&
+                        (sh.rmax[0] + sx < tb.ox || sh.rmin[0] + sx >= tb.ox + tb.nx ||
+                         sh.rmax[1] + sy < tb.oy || sh.rmin[1] + sy >= tb.oy + tb.ny ||
+                         sh.rmax[2] + sz < tb.oz || sh.rmin[2] + sz >= tb.oz + tb.nz));
+        if (__ballot(valid) == 0) continue;  // wave-uniform
         int sum = 0;
         if (cells_ok) {
-          root_lookups += ntc;
-          const int qx = sx - tb.ox - 1024, qy = sy - tb.oy - 1024, qz = sz - tb.oz - 512;
-          for (int c = 0; c < ntc; ++c) {
-            const int pc = sh.tcell[c];
-            const int x = (pc & 2047) + qx, y = ((pc >> 11) & 2047) + qy, z = static_cast<int>(static_cast<unsigned>(pc) >> 22) + qz;
-            if (static_cast<unsigned>(x) < static_cast<unsigned>(tb.nx) &&
-                static_cast<unsigned>(y) < static_cast<unsigned>(tb.ny) &&
-                static_cast<unsigned>(z) < static_cast<unsigned>(tb.nz)) {
-              const int idx = (z * tb.ny + y) * tb.nx + x;
-              sum += static_cast<int>(sh.tcount[c]) * (lds_top ? sh.top[idx] : tglobal[idx]);
+          // Each group of 64 cells sits in the wave's registers (one per
+          // lane) and is broadcast with readlane: only the level value is
+          // read per (root, cell).
+          if (valid) root_lookups += ntc;
+          const int qx = (valid ? sx : -(1 << 20)) - tb.ox - 1024, qy = sy - tb.oy - 1024,
+                    qz = sz - tb.oz - 512;
+          for (int cb = 0; cb < ntc; cb += 64) {
+            const int myc = cb + lane < ntc ? sh.tcell[cb + lane] : 0;
+            const int mycnt = cb + lane < ntc ? sh.tcount[cb + lane] : 0;
+            const int cn = min(64, ntc - cb);
+            if (lds_top) {
+              for (int c = 0; c < cn; ++c) {
+                const int pc = __builtin_amdgcn_readlane(myc, c);
+                const int cnt = __builtin_amdgcn_readlane(mycnt, c);
+                const int x = (pc & 2047) + qx, y = ((pc >> 11) & 2047) + qy,
+                          z = static_cast<int>(static_cast<unsigned>(pc) >> 22) + qz;
+                const bool in = static_cast<unsigned>(x) < static_cast<unsigned>(tb.nx) &&
+                                static_cast<unsigned>(y) < static_cast<unsigned>(tb.ny) &&
+                                static_cast<unsigned>(z) < static_cast<unsigned>(tb.nz);
+                const int v = sh.top[in ? (z * tb.ny + y) * tb.nx + x : 0];
+                sum += in ? cnt * v : 0;
+              }
+            } else {
+              for (int c = 0; c < cn; ++c) {
+                const int pc = __builtin_amdgcn_readlane(myc, c);
+                const int cnt = __builtin_amdgcn_readlane(mycnt, c);
+                const int x = (pc & 2047) + qx, y = ((pc >> 11) & 2047) + qy,
+                          z = static_cast<int>(static_cast<unsigned>(pc) >> 22) + qz;
+                if (static_cast<unsigned>(x) < static_cast<unsigned>(tb.nx) &&
+                    static_cast<unsigned>(y) < static_cast<unsigned>(tb.ny) &&
+                    static_cast<unsigned>(z) < static_cast<unsigned>(tb.nz))
+                  sum += cnt * tglobal[(z * tb.ny + y) * tb.nx + x];
+              }
             }
           }
-        } else {
+        } else if (valid) {
           root_lookups += n;
           for (int i = 0; i < n; ++i) {
             int x = sh.cx[i], y = sh.cy[i], z = sh.cz[i];
@@ -498,7 +560,7 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
             if (InBrick(tb, x + sx, y + sy, z + sz, &idx)) sum += lds_top ? sh.top[idx] : tglobal[idx];
           }
         }
-        if (sum >= pd.min_sum && sum >= best_sum) {
+        if (valid && sum >= pd.min_sum && sum >= best_sum) {
           const int at = atomicAdd(&sh.nroot, 1);
           sh.rbx[at] = static_cast<int16_t>(ox);
           sh.rby[at] = static_cast<int16_t>(oy);
@@ -512,6 +574,7 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
     if (tid == 0) {
       const long long now = clock64();
       prof[1] += now - t_mark;
+      prof[11] += sh.nroot;
       t_mark = now;
     }
     // Order the roots ascending by bound (the best is fed last, popped
@@ -798,14 +861,18 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
     }
       rb_end = k0;
     }
-    if (tid == 0) prof[3] += clock64() - t_mark;
+    if (tid == 0) {
+      const long long now = clock64();
+      prof[3] += now - t_mark;
+      t_mark = now;
+    }
     }  // root chunks
   }
   lookups += root_lookups;
   for (int m = 32; m > 0; m >>= 1) lookups += __shfl_xor(lookups, m, 64);
   if ((tid & 63) == 0 && stats && lookups) atomicAdd(stats, lookups);
   if (tid == 0 && stats)
-    for (int k = 0; k < 7; ++k) atomicAdd(stats + 1 + k, static_cast<unsigned long long>(prof[k]));
+    for (int k = 0; k < 12; ++k) atomicAdd(stats + 1 + k, static_cast<unsigned long long>(prof[k]));
 }
 
 // Low-resolution score of each pair's winning leaf (the Result field), with
