@@ -11,7 +11,7 @@ namespace csm {
 constexpr int kMaxLevels3d = 12;
 constexpr int kExtraLevels3d = 2;       // coarser levels above the reference's stack (roots only)
 constexpr int kRootTarget3d = 512;       // a pair's roots start at the lowest level with <= this many
-constexpr int kMax3dPoints = 4096;        // high-resolution points per node (LDS)
+constexpr int kMax3dPoints = 2048;        // high-resolution points per node (LDS)
 constexpr int kTopLds3d = 6 * 1024;       // top pyramid level cached in LDS when it fits
 constexpr int kRootChunk3d = 128;         // roots fed to the DFS stack at a time
 constexpr int kRootScore3d = 256;         // roots scored at a time (one per lane)
@@ -22,7 +22,7 @@ constexpr int kStack3d = 1024;            // DFS stack entries per workgroup
 constexpr int kMax3dYaws = 1 << 16;
 constexpr int kMax3dWindow = 1 << 14;
 constexpr int kSearch3dThreads = 256;
-constexpr int kSearch3dBlocksPerCu = 3;   // resident workgroups per CU (LDS < 160 KiB / 3)
+constexpr int kSearch3dBlocksPerCu = 4;   // resident workgroups per CU (LDS < 160 KiB / 3)
 constexpr int kCellLimit3d = 16000;       // |cell index| kept in int16 in LDS
 // Per pair: key = sum << key_shift | ~leaf_id, leaf_id = ((yaw << bxy | x) << bxy
 // | y) << bz | z with x = ox + wxy etc.; the host sizes the fields so that

@@ -318,7 +318,40 @@ __device__ float LowResScore(F3Shared& sh, const Submap3Desc& sm, const float* _
   return __fdiv_rn(sum, static_cast<float>(m));
 }
 
-__global__ void __launch_bounds__(kSearch3dThreads)
+// Phase timers of thread 0 (s_memtime), compiled in with -DCSM_KPROF only:
+// they cost ~24 VGPRs. stats[1 + slot]: 0 item+discretize, 7 top copy,
+// 8 cloud box, 9 cell list, 1 roots, 2 sort, 3 DFS + leaves (cycles);
+// 5 batches, 6 leaves, 11 roots kept (counts).
+#ifdef CSM_KPROF
+#define F3_PROF_DECL long long prof[12] = {}, t_mark = 0
+#define F3_RESET() (t_mark = clock64())
+#define F3_MARK(slot)                    \
+  do {                                   \
+    if (tid == 0) {                      \
+      const long long now_ = clock64();  \
+      prof[slot] += now_ - t_mark;       \
+      t_mark = now_;                     \
+    }                                    \
+  } while (0)
+#define F3_COUNT(slot, v) \
+  do {                    \
+    if (tid == 0) prof[slot] += (v); \
+  } while (0)
+#define F3_FLUSH(stats)                                                                   \
+  do {                                                                                    \
+    if (tid == 0 && (stats))                                                              \
+      for (int k_ = 0; k_ < 12; ++k_)                                                     \
+        atomicAdd((stats) + 1 + k_, static_cast<unsigned long long>(prof[k_]));          \
+  } while (0)
+#else
+#define F3_PROF_DECL (void)0
+#define F3_RESET() (void)0
+#define F3_MARK(slot) (void)0
+#define F3_COUNT(slot, v) (void)0
+#define F3_FLUSH(stats) (void)0
+#endif
+
+__global__ void __launch_bounds__(kSearch3dThreads) __attribute__((amdgpu_waves_per_eu(kSearch3dBlocksPerCu, kSearch3dBlocksPerCu)))
 fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restrict__ pairs,
               const Yaw3Desc* __restrict__ yaws, int num_items, const float* __restrict__ points,
               const float* __restrict__ low_points, unsigned* __restrict__ counter,
@@ -327,14 +360,14 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
   __shared__ F3Shared sh;
   const int tid = threadIdx.x;
   unsigned long long lookups = 0, root_lookups = 0;
-  long long prof[12] = {};  // thread 0: phase cycles / counts
+  F3_PROF_DECL;
   if (tid == 0) sh.cached_submap = -1;
   for (;;) {
     if (tid == 0) sh.item = static_cast<int>(atomicAdd(counter, 1u));
     __syncthreads();
     const int item = sh.item;
     if (item >= num_items) break;
-    long long t_item = clock64();
+    F3_RESET();
     const Yaw3Desc yw = yaws[item];
     const Pair3Desc pd = pairs[yw.pair];
     const Submap3Desc& sm = submaps[pd.submap];
@@ -361,8 +394,7 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
       __syncthreads();
       continue;
     }
-    long long t_mark = clock64();
-    if (tid == 0) prof[0] += t_mark - t_item;
+    F3_MARK(0);
     const int top = pd.root_level;
     const int step = 1 << top;
     const int T = pd.top_nx * pd.top_ny * pd.top_nz;
@@ -383,27 +415,18 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
     if (lds_top && sh.cached_submap != pd.submap * 16 + top) {
       const uint4* src = reinterpret_cast<const uint4*>(sm.levels + tb.offset);
       uint4* dst = reinterpret_cast<uint4*>(sh.top);
-      constexpr int kPer = (kTopLds3d / 16 + kSearch3dThreads - 1) / kSearch3dThreads;
-      uint4 v[kPer];
-#pragma unroll
-      for (int u = 0; u < kPer; ++u) {
-        const int k = tid + u * kSearch3dThreads;
-        if (k < tvec) v[u] = src[k];
-      }
-#pragma unroll
-      for (int u = 0; u < kPer; ++u) {
-        const int k = tid + u * kSearch3dThreads;
-        if (k < tvec) dst[k] = v[u];
-      }
+      static_assert(kTopLds3d <= 2 * 16 * kSearch3dThreads, "two 16-byte pieces per thread");
+      const int k0 = tid, k1 = tid + kSearch3dThreads;
+      uint4 v0 = make_uint4(0, 0, 0, 0), v1 = make_uint4(0, 0, 0, 0);
+      if (k0 < tvec) v0 = src[k0];
+      if (k1 < tvec) v1 = src[k1];
+      if (k0 < tvec) dst[k0] = v0;
+      if (k1 < tvec) dst[k1] = v1;
       __syncthreads();
       if (tid == 0) sh.cached_submap = pd.submap * 16 + top;
     }
     __syncthreads();
-    if (tid == 0) {
-      const long long now = clock64();
-      prof[7] += now - t_mark;
-      t_mark = now;
-    }
+    F3_MARK(7);
     const int te = max(0, top - sm.full_resolution_depth + 1);
     const bool treduced = top >= sm.full_resolution_depth;
     const int lwx = (-pd.wxy) >> te, lwy = (-pd.wxy) >> te, lwz = (-pd.wz) >> te;
@@ -443,11 +466,7 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
       }
     }
     __syncthreads();
-    if (tid == 0) {
-      const long long now = clock64();
-      prof[8] += now - t_mark;
-      t_mark = now;
-    }
+    F3_MARK(8);
     // Histogram of the cloud's top-level cells over its box (count grid in
     // the empty stack sums), compacted to a list when box and list fit.
     const int gbx = sh.rmax[0] - sh.rmin[0] + 1, gby = sh.rmax[1] - sh.rmin[1] + 1,
@@ -485,11 +504,7 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
     }
     const bool cells_ok = use_cells && sh.ntcell <= kTopCells3d;
     const int ntc = cells_ok ? sh.ntcell : 0;
-    if (tid == 0) {
-      const long long now = clock64();
-      prof[9] += now - t_mark;
-      t_mark = now;
-    }
+    F3_MARK(9);
     const bool skip_empty = pd.min_sum > 0;
     for (int r0 = 0; r0 < T; r0 += kRootScore3d) {
     const int r1 = min(T, r0 + kRootScore3d);
@@ -571,12 +586,8 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
 
     }
     __syncthreads();
-    if (tid == 0) {
-      const long long now = clock64();
-      prof[1] += now - t_mark;
-      prof[11] += sh.nroot;
-      t_mark = now;
-    }
+    F3_MARK(1);
+    F3_COUNT(11, sh.nroot);
     // Order the roots ascending by bound (the best is fed last, popped
     // first): parallel rank sort into the (empty) stack arrays.
     {
@@ -602,11 +613,7 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
       }
     }
     __syncthreads();
-    if (tid == 0) {
-      const long long now = clock64();
-      prof[2] += now - t_mark;
-      t_mark = now;
-    }
+    F3_MARK(2);
     for (int rb_end = sh.nroot; rb_end > 0;) {
       const int k0 = max(0, rb_end - kRootChunk3d);
       for (int a = tid; a < rb_end - k0; a += kSearch3dThreads) {
@@ -767,29 +774,31 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
         lookups += static_cast<unsigned long long>(__popc(nc)) * n;
         const int best_sum = static_cast<int>(sh.best >> pd.key_shift);
         if (cd > 0) {
-          int idx[8];
+          // Kept children in ascending bound order (stable; the best is
+          // popped first), ranked with static indices only.
+          bool keep[8];
           int m = 0;
-          for (int k = 0; k < 8; ++k)
-            if (((nc >> k) & 1) && acc[k] >= pd.min_sum && acc[k] >= best_sum) idx[m++] = k;
-          for (int a = 1; a < m; ++a) {  // ascending: the best child is popped first
-            const int v = idx[a];
-            int b2 = a - 1;
-            while (b2 >= 0 && acc[idx[b2]] > acc[v]) {
-              idx[b2 + 1] = idx[b2];
-              --b2;
-            }
-            idx[b2 + 1] = v;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            keep[k] = ((nc >> k) & 1) && acc[k] >= pd.min_sum && acc[k] >= best_sum;
+            m += keep[k];
           }
           const int base = atomicAdd(&sh.sp, m);
-          for (int a = 0; a < m; ++a) {
-            const int k = idx[a];
-            sh.sx[base + a] = static_cast<int16_t>(cx8[k]);
-            sh.sy[base + a] = static_cast<int16_t>(cy8[k]);
-            sh.sz[base + a] = static_cast<int16_t>(cz8[k]);
-            sh.sd[base + a] = static_cast<int8_t>(cd);
-            sh.ssum[base + a] = acc[k];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            if (!keep[k]) continue;
+            int rank = 0;
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+              rank += keep[j] && (acc[j] < acc[k] || (acc[j] == acc[k] && j < k));
+            sh.sx[base + rank] = static_cast<int16_t>(cx8[k]);
+            sh.sy[base + rank] = static_cast<int16_t>(cy8[k]);
+            sh.sz[base + rank] = static_cast<int16_t>(cz8[k]);
+            sh.sd[base + rank] = static_cast<int8_t>(cd);
+            sh.ssum[base + rank] = acc[k];
           }
         } else {
+#pragma unroll
           for (int k = 0; k < 8; ++k) {
             if (!((nc >> k) & 1) || acc[k] < pd.min_sum) continue;
             const unsigned long long id = LeafId(pd, yw.yaw_id, cx8[k], cy8[k], cz8[k]);
@@ -804,14 +813,11 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
           }
         }
       }
-      if (tid == 0) {
-        sh.best_seen = gbest;
-        prof[5] += 1;
-      }
+      if (tid == 0) sh.best_seen = gbest;
+      F3_COUNT(5, 1);
       __syncthreads();
       const int nl = sh.nleaf;
       if (nl == 0) continue;
-      const long long t_leaf = clock64();
       // Leaves: descending key order; the first that passes the
       // low-resolution check (:384-401) beats every later one.
       if (tid == 0) {
@@ -854,25 +860,17 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
         if (sh.accepted) break;
       }
       __syncthreads();
-      if (tid == 0) {
-        prof[4] += clock64() - t_leaf;
-        prof[6] += nl;
-      }
+      F3_COUNT(6, nl);
     }
       rb_end = k0;
     }
-    if (tid == 0) {
-      const long long now = clock64();
-      prof[3] += now - t_mark;
-      t_mark = now;
-    }
+    F3_MARK(3);
     }  // root chunks
   }
   lookups += root_lookups;
   for (int m = 32; m > 0; m >>= 1) lookups += __shfl_xor(lookups, m, 64);
   if ((tid & 63) == 0 && stats && lookups) atomicAdd(stats, lookups);
-  if (tid == 0 && stats)
-    for (int k = 0; k < 12; ++k) atomicAdd(stats + 1 + k, static_cast<unsigned long long>(prof[k]));
+  F3_FLUSH(stats);
 }
 
 // Low-resolution score of each pair's winning leaf (the Result field), with
