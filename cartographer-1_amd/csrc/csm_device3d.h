@@ -11,7 +11,8 @@ namespace csm {
 constexpr int kMaxLevels3d = 12;
 constexpr int kExtraLevels3d = 2;       // coarser levels above the reference's stack (roots only)
 constexpr int kRootTarget3d = 512;       // a pair's roots start at the lowest level with <= this many
-constexpr int kMax3dPoints = 2048;        // high-resolution points per node (LDS)
+constexpr int kSmall3dPoints = 2048;      // cloud capacity (LDS) of the 4-workgroups-per-CU build
+constexpr int kMax3dPoints = 8192;        // of the large-cloud build (2 per CU); more: CSM_ERANGE
 constexpr int kTopLds3d = 6 * 1024;       // top pyramid level cached in LDS when it fits
 constexpr int kRootChunk3d = 128;         // roots fed to the DFS stack at a time
 constexpr int kRootScore3d = 256;         // roots scored at a time (one per lane)
@@ -22,7 +23,8 @@ constexpr int kStack3d = 1024;            // DFS stack entries per workgroup
 constexpr int kMax3dYaws = 1 << 16;
 constexpr int kMax3dWindow = 1 << 14;
 constexpr int kSearch3dThreads = 256;
-constexpr int kSearch3dBlocksPerCu = 4;   // resident workgroups per CU (LDS < 160 KiB / 3)
+constexpr int kSearch3dBlocksPerCu = 4;       // resident workgroups per CU, small-cloud build
+constexpr int kSearch3dBlocksPerCuLarge = 2;  // large-cloud build
 constexpr int kCellLimit3d = 16000;       // |cell index| kept in int16 in LDS
 // Per pair: key = sum << key_shift | ~leaf_id, leaf_id = ((yaw << bxy | x) << bxy
 // | y) << bz | z with x = ox + wxy etc.; the host sizes the fields so that

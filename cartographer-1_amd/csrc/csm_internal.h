@@ -40,6 +40,26 @@ struct DevBuf {
   T* as() const { return static_cast<T*>(ptr); }
 };
 
+// Page-locked host staging (H2D copies at full PCIe rate).
+struct PinnedBuf {
+  void* ptr = nullptr;
+  size_t bytes = 0;
+  ~PinnedBuf() {
+    if (ptr) (void)hipHostFree(ptr);
+  }
+  int Reserve(size_t n) {
+    if (n <= bytes) return CSM_OK;
+    if (ptr) (void)hipHostFree(ptr);
+    ptr = nullptr;
+    bytes = 0;
+    const size_t want = std::max<size_t>(n + n / 4, 4096);
+    if (hipHostMalloc(&ptr, want, hipHostMallocDefault) != hipSuccess) return CSM_ENOMEM;
+    bytes = want;
+    return CSM_OK;
+  }
+  template <typename T>
+  T* as() const { return static_cast<T*>(ptr); }
+};
 
 }  // namespace csm
 
@@ -61,6 +81,7 @@ struct csm_context {
   // 3D path scratch (host3d.cc).
   csm::DevBuf rt3_rot, rt3_trans, rt3_points, rt3_best, f3_pairs, f3_yaws, f3_points,
       f3_low_points, f3_best, f3_status, f3_counter, f3_items, f3_scores;
+  csm::PinnedBuf f3_host_yaws;
 };
 
 #endif  // CSM_INTERNAL_H_

@@ -21,10 +21,12 @@ hipError_t LaunchRt3dScore(int num_rot, hipStream_t st, const float* prob, const
                            float res, const float* points, int n, const float4* rot,
                            const float* rot_angle, const float4* trans, int num_trans, int t_base,
                            double wt, double wr, unsigned long long* best);
-hipError_t LaunchFast3dSearch(int grid, hipStream_t st, const Submap3Desc* submaps,
-                              const Pair3Desc* pairs, const Yaw3Desc* yaws, int num_items,
-                              const float* points, const float* low_points, unsigned* counter,
-                              unsigned long long* best, int32_t* status,
+// Items [item_begin, item_begin + num_items) of the yaw list; `large`
+// selects the build for clouds of more than kSmall3dPoints points.
+hipError_t LaunchFast3dSearch(bool large, int grid, hipStream_t st, const Submap3Desc* submaps,
+                              const Pair3Desc* pairs, const Yaw3Desc* yaws, int item_begin,
+                              int num_items, const float* points, const float* low_points,
+                              unsigned* counter, unsigned long long* best, int32_t* status,
                               unsigned long long* stats);
 hipError_t LaunchFast3dFinalize(int num_pairs, hipStream_t st, const Submap3Desc* submaps,
                                 const Pair3Desc* pairs, const Yaw3Desc* yaws,
@@ -37,10 +39,16 @@ struct RotPair3Host {
   int32_t node_hist, submap_hist, size, window;
   float step, yaw0;
   int64_t out;
+  double min_score;
 };
 constexpr int kMaxHistogram = 512;
 hipError_t LaunchRotScores(const void* pairs, int num_pairs, int max_yaws, const float* hists,
                            float* out, hipStream_t st);
+// Passing yaws of each pair (k, score), compacted: range[p] = {offset, count}
+// at a global cursor (zeroed by the caller).
+hipError_t LaunchYawCompact(const void* pairs, int num_pairs, const float* scores,
+                            unsigned* cursor, int2* range, int32_t* out_k, float* out_s,
+                            hipStream_t st);
 
 }  // namespace csm
 

@@ -524,7 +524,6 @@ struct PairPrep {
   float astep = 0.f, yaw0 = 0.f;
   R3 node_to_submap{};
   Q4 submap_inv{}, node_q{};
-  int64_t score_offset = 0;
 };
 
 // MatchWithSearchParameters' host half up to the rotational scores
@@ -615,11 +614,16 @@ void PreparePair(const csm_fast3d* m, const csm_node3d& node, const csm_pair3d& 
 }
 
 // GenerateDiscreteScans :277-294 given the rotational scores of the pair.
-void BuildYaws(const csm_fast3d* m, const float* scores, PairPrep* out) {
+// The discrete scans of the yaws that passed the rotational filter (k in
+// increasing order, with their scores; yaw_compact on the device).
+void BuildYaws(const csm_fast3d* m, const int32_t* ks, const float* scores, int count,
+               PairPrep* out) {
+  (void)m;
   const int A = out->angular_window;
   Pair3Desc& d = out->desc;
-  for (int k = 0; k <= 2 * A; ++k) {
-    if (static_cast<double>(scores[k]) < m->options.min_rotational_score) continue;
+  out->yaws.reserve(count);
+  for (int j = 0; j < count; ++j) {
+    const int k = ks[j];
     const float angle = static_cast<float>(k - A) * out->astep;
     const Q4 yaw = AngleAxisToQuat(V3{0.f, 0.f, angle});
     const Q4 q = QMul(QMul(out->submap_inv, yaw), out->node_q);
@@ -636,7 +640,7 @@ void BuildYaws(const csm_fast3d* m, const float* scores, PairPrep* out) {
     y.tx = out->node_to_submap.t.x;
     y.ty = out->node_to_submap.t.y;
     y.tz = out->node_to_submap.t.z;
-    y.rotational_score = scores[k];
+    y.rotational_score = scores[j];
     y.yaw_id = static_cast<int32_t>(out->yaws.size());  // increasing angle order
     out->yaws.push_back(y);
   }
@@ -768,13 +772,15 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
       r.step = prep[i].astep;
       r.yaw0 = prep[i].yaw0;
       r.out = total;
-      prep[i].score_offset = total;
+      r.min_score = submaps[p.submap]->options.min_rotational_score;
       total += 2 * r.window + 1;
       max_yaws = std::max(max_yaws, 2 * r.window + 1);
       rp.push_back(r);
       rp_pair.push_back(i);
     }
-    std::vector<float> scores(static_cast<size_t>(std::max<int64_t>(total, 1)));
+    std::vector<int2> range(rp.size());
+    std::vector<int32_t> yk;
+    std::vector<float> ys;
     if (!rp.empty()) {
       std::lock_guard<std::mutex> lock(ctx->mu);
       int rc;
@@ -783,7 +789,13 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
       if ((rc = ctx->f3_items.Reserve(sizeof(RotPair3Host) * rp.size() +
                                       sizeof(float) * std::max<size_t>(hists.size(), 1))))
         return rc;
-      if ((rc = ctx->f3_scores.Reserve(sizeof(float) * scores.size()))) return rc;
+      // [scores | passing k | passing scores | ranges | cursor]
+      if ((rc = ctx->f3_scores.Reserve(12 * total + sizeof(int2) * rp.size() + 16))) return rc;
+      float* dscores = ctx->f3_scores.as<float>();
+      int32_t* dk = reinterpret_cast<int32_t*>(dscores + total);
+      float* ds = reinterpret_cast<float*>(dk + total);
+      int2* drange = reinterpret_cast<int2*>(ds + total + (total & 1));
+      unsigned* dcursor = reinterpret_cast<unsigned*>(drange + rp.size());
       RotPair3Host* drp = ctx->f3_items.as<RotPair3Host>();
       float* dh = reinterpret_cast<float*>(drp + rp.size());
       CSM_HIP(hipMemcpyAsync(drp, rp.data(), sizeof(RotPair3Host) * rp.size(),
@@ -791,45 +803,59 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
       if (!hists.empty())
         CSM_HIP(hipMemcpyAsync(dh, hists.data(), sizeof(float) * hists.size(),
                                hipMemcpyHostToDevice, st));
-      CSM_HIP(LaunchRotScores(drp, static_cast<int>(rp.size()), max_yaws, dh,
-                              ctx->f3_scores.as<float>(), st));
-      CSM_HIP(hipMemcpyAsync(scores.data(), ctx->f3_scores.ptr, sizeof(float) * total,
+      CSM_HIP(hipMemsetAsync(dcursor, 0, sizeof(unsigned), st));
+      CSM_HIP(LaunchRotScores(drp, static_cast<int>(rp.size()), max_yaws, dh, dscores, st));
+      CSM_HIP(LaunchYawCompact(drp, static_cast<int>(rp.size()), dscores, dcursor, drange, dk, ds,
+                               st));
+      unsigned kept = 0;
+      CSM_HIP(hipMemcpyAsync(range.data(), drange, sizeof(int2) * rp.size(),
                              hipMemcpyDeviceToHost, st));
+      CSM_HIP(hipMemcpyAsync(&kept, dcursor, sizeof(unsigned), hipMemcpyDeviceToHost, st));
       CSM_HIP(hipStreamSynchronize(st));
+      yk.resize(std::max(kept, 1u));
+      ys.resize(std::max(kept, 1u));
+      if (kept > 0) {
+        CSM_HIP(hipMemcpyAsync(yk.data(), dk, sizeof(int32_t) * kept, hipMemcpyDeviceToHost, st));
+        CSM_HIP(hipMemcpyAsync(ys.data(), ds, sizeof(float) * kept, hipMemcpyDeviceToHost, st));
+        CSM_HIP(hipStreamSynchronize(st));
+      }
     }
     lap(2);
     // Phase 3 (host, parallel): discrete-scan poses of the yaws that pass.
     ParallelPairs(static_cast<int64_t>(rp_pair.size()), [&](int64_t j) {
       const int64_t i = rp_pair[j];
-      BuildYaws(submaps[pairs[i].submap], scores.data() + prep[i].score_offset, &prep[i]);
+      BuildYaws(submaps[pairs[i].submap], yk.data() + range[j].x, ys.data() + range[j].x,
+                range[j].y, &prep[i]);
     });
   }
   lap(3);
   std::vector<Submap3Desc> sdesc(num_submaps);
   for (int i = 0; i < num_submaps; ++i) sdesc[i] = submaps[i]->desc;
   std::vector<Pair3Desc> pdesc;
-  std::vector<Yaw3Desc> ydesc;
   std::vector<int64_t> pair_of;  // device pair index -> input pair
+  int ny = 0;
+  // Pairs whose cloud fits the small-cloud build first, then the rest: two
+  // launches over the two item ranges.
+  int ny_small = 0;
+  for (int pass = 0; pass < 2; ++pass)
   for (int64_t i = 0; i < num_pairs; ++i) {
     if (results[i].status != CSM_NO_MATCH) continue;
     if (prep[i].status != CSM_OK) {
-      results[i].status = prep[i].status;
+      if (pass == 0) results[i].status = prep[i].status;
       continue;
     }
     if (pairs[i].min_score >= 1.f || nodes[pairs[i].node].num_high_resolution == 0) continue;
+    if ((nodes[pairs[i].node].num_high_resolution > kSmall3dPoints) != (pass == 1)) continue;
     Pair3Desc d = prep[i].desc;
     d.submap = pairs[i].submap;
     d.point_offset = hoff[pairs[i].node];
     d.low_offset = loff[pairs[i].node];
-    d.yaw_begin = static_cast<int32_t>(ydesc.size());
+    d.yaw_begin = ny;
     d.num_yaws = static_cast<int32_t>(prep[i].yaws.size());
-    const int32_t dp = static_cast<int32_t>(pdesc.size());
-    for (Yaw3Desc y : prep[i].yaws) {
-      y.pair = dp;
-      ydesc.push_back(y);
-    }
+    ny += d.num_yaws;
     pdesc.push_back(d);
     pair_of.push_back(i);
+    if (pass == 0) ny_small = ny;
   }
   const int np = static_cast<int>(pdesc.size());
   if (np == 0) return CSM_OK;
@@ -837,7 +863,6 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
   int rc;
   if ((rc = EnsureDevice3(ctx))) return rc;
   hipStream_t st = ctx->stream;
-  const int ny = static_cast<int>(ydesc.size());
   if ((rc = ctx->f3_pairs.Reserve(sizeof(Pair3Desc) * np + sizeof(Submap3Desc) * num_submaps)))
     return rc;
   if ((rc = ctx->f3_yaws.Reserve(sizeof(Yaw3Desc) * std::max(ny, 1)))) return rc;
@@ -856,9 +881,20 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
   CSM_HIP(hipMemcpyAsync(dpairs, pdesc.data(), sizeof(Pair3Desc) * np, hipMemcpyHostToDevice, st));
   CSM_HIP(hipMemcpyAsync(dsub, sdesc.data(), sizeof(Submap3Desc) * num_submaps,
                          hipMemcpyHostToDevice, st));
-  if (ny > 0)
-    CSM_HIP(hipMemcpyAsync(ctx->f3_yaws.ptr, ydesc.data(), sizeof(Yaw3Desc) * ny,
-                           hipMemcpyHostToDevice, st));
+  if (ny > 0) {
+    // Yaw descriptors written in parallel straight into pinned staging.
+    if ((rc = ctx->f3_host_yaws.Reserve(sizeof(Yaw3Desc) * ny))) return rc;
+    Yaw3Desc* hy = ctx->f3_host_yaws.as<Yaw3Desc>();
+    ParallelPairs(np, [&](int64_t dp) {
+      const std::vector<Yaw3Desc>& ys = prep[pair_of[dp]].yaws;
+      Yaw3Desc* o = hy + pdesc[dp].yaw_begin;
+      for (size_t k = 0; k < ys.size(); ++k) {
+        o[k] = ys[k];
+        o[k].pair = static_cast<int32_t>(dp);
+      }
+    });
+    CSM_HIP(hipMemcpyAsync(ctx->f3_yaws.ptr, hy, sizeof(Yaw3Desc) * ny, hipMemcpyHostToDevice, st));
+  }
   if (!hpts.empty())
     CSM_HIP(hipMemcpyAsync(ctx->f3_points.ptr, hpts.data(), sizeof(float) * hpts.size(),
                            hipMemcpyHostToDevice, st));
@@ -870,11 +906,19 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
   CSM_HIP(hipMemsetAsync(ctx->f3_counter.ptr, 0, 8 + 16 * sizeof(unsigned long long), st));
   lap(4);
   if (ctx->timing) CSM_HIP(hipEventRecord(ctx->ev0, st));
-  if (ny > 0) {
-    const int grid = std::max(1, std::min(ny, ctx->num_cus * kSearch3dBlocksPerCu));
-    CSM_HIP(LaunchFast3dSearch(grid, st, dsub, dpairs, ctx->f3_yaws.as<Yaw3Desc>(), ny,
-                               ctx->f3_points.as<float>(), ctx->f3_low_points.as<float>(),
-                               dcounter, dbest, ctx->f3_status.as<int32_t>(), dstats));
+  if (ny_small > 0) {
+    const int grid = std::max(1, std::min(ny_small, ctx->num_cus * kSearch3dBlocksPerCu));
+    CSM_HIP(LaunchFast3dSearch(false, grid, st, dsub, dpairs, ctx->f3_yaws.as<Yaw3Desc>(), 0,
+                               ny_small, ctx->f3_points.as<float>(),
+                               ctx->f3_low_points.as<float>(), dcounter, dbest,
+                               ctx->f3_status.as<int32_t>(), dstats));
+  }
+  if (ny > ny_small) {
+    const int grid = std::max(1, std::min(ny - ny_small, ctx->num_cus * kSearch3dBlocksPerCuLarge));
+    CSM_HIP(LaunchFast3dSearch(true, grid, st, dsub, dpairs, ctx->f3_yaws.as<Yaw3Desc>(), ny_small,
+                               ny - ny_small, ctx->f3_points.as<float>(),
+                               ctx->f3_low_points.as<float>(), dcounter + 1, dbest,
+                               ctx->f3_status.as<int32_t>(), dstats));
   }
   if (ctx->timing) CSM_HIP(hipEventRecord(ctx->ev1, st));
   CSM_HIP(LaunchFast3dFinalize(np, st, dsub, dpairs, ctx->f3_yaws.as<Yaw3Desc>(),
@@ -929,7 +973,7 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
     const int ox =
         static_cast<int>((id >> (d.bits_z + d.bits_xy)) & ((1ull << d.bits_xy) - 1)) - d.wxy;
     const int yaw = static_cast<int>(id >> (d.bits_z + 2 * d.bits_xy));
-    const Yaw3Desc& y = ydesc[d.yaw_begin + yaw];
+    const Yaw3Desc& y = prep[i].yaws[yaw];
     const float res = submaps[d.submap]->resolution;
     const V3 t0 = Rotate(Q4{1.f, 0.f, 0.f, 0.f}, V3{y.tx, y.ty, y.tz});
     const V3 t{t0.x + res * static_cast<float>(ox), t0.y + res * static_cast<float>(oy),

@@ -195,16 +195,12 @@ rt3d_score(const float* __restrict__ prob, Brick3 gb, float res, float inv,
 // passes min_low_resolution_score (:384-401). Each pair keeps one 64-bit key
 // sum << 42 | ~leaf_id, updated with atomicMax.
 
-struct F3Shared {
-  int16_t cx[kMax3dPoints], cy[kMax3dPoints], cz[kMax3dPoints];
+template <int kPts>
+struct F3SharedT {
+  int16_t cx[kPts], cy[kPts], cz[kPts];
   int16_t sx[kStack3d], sy[kStack3d], sz[kStack3d];
   int8_t sd[kStack3d];
   int ssum[kStack3d];
-  int part[kSearch3dThreads / 64][8];
-  int sums[8];
-  int co_x[8], co_y[8], co_z[8];
-  unsigned long long leaf_key[8];
-  int order[8];
   float lr[kSearch3dThreads];
   alignas(16) uint8_t top[kTopLds3d];
   int bn_x[kBatch3d], bn_y[kBatch3d], bn_z[kBatch3d], bn_d[kBatch3d];
@@ -219,7 +215,7 @@ struct F3Shared {
   int tcell[kTopCells3d];
   uint16_t tcount[kTopCells3d];
   int ntcell;
-  int nbatch, nleaf, nchild, child_depth, sp, item, error, accepted, cached_submap;
+  int nbatch, nleaf, sp, item, error, accepted, cached_submap;
   unsigned long long best;
   unsigned long long best_seen;  // last read of the pair's global best
 };
@@ -233,64 +229,11 @@ __device__ __forceinline__ unsigned long long LeafId(const Pair3Desc& pd, int ya
   return id;
 }
 
-// Sums of `count` (<= 8) candidates at `depth` (ScoreCandidates :332-355):
-// reduction exponent e = max(0, depth - full_resolution_depth + 1); the
-// discrete scan at depth >= full_resolution_depth is ((c + ws) >> e) - (ws >> e).
-__device__ void ScoreOffsets(F3Shared& sh, const Submap3Desc& sm, const Pair3Desc& pd, int depth,
-                             int count, const int* ox, const int* oy, const int* oz, int n) {
-  const int tid = threadIdx.x;
-  const int e = max(0, depth - sm.full_resolution_depth + 1);
-  const Brick3 b = sm.level[depth];
-  const uint8_t* g = sm.levels + b.offset;
-  const int wsx = -pd.wxy, wsy = -pd.wxy, wsz = -pd.wz;
-  const int lwx = wsx >> e, lwy = wsy >> e, lwz = wsz >> e;
-  int sx[8], sy[8], sz[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    sx[k] = k < count ? (ox[k] >> e) : 0;
-    sy[k] = k < count ? (oy[k] >> e) : 0;
-    sz[k] = k < count ? (oz[k] >> e) : 0;
-  }
-  int acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  const bool reduced = depth >= sm.full_resolution_depth;
-  for (int i = tid; i < n; i += kSearch3dThreads) {
-    int x = sh.cx[i], y = sh.cy[i], z = sh.cz[i];
-    if (reduced) {
-      x = ((x + wsx) >> e) - lwx;
-      y = ((y + wsy) >> e) - lwy;
-      z = ((z + wsz) >> e) - lwz;
-    }
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      if (k < count) {
-        int64_t idx;
-        if (InBrick(b, x + sx[k], y + sy[k], z + sz[k], &idx)) acc[k] += g[idx];
-      }
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    int v = acc[k];
-    for (int m = 32; m > 0; m >>= 1) v += __shfl_xor(v, m, 64);
-    acc[k] = v;
-  }
-  if ((tid & 63) == 0) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) sh.part[tid >> 6][k] = acc[k];
-  }
-  __syncthreads();
-  if (tid < 8) {
-    int s = 0;
-    for (int w = 0; w < kSearch3dThreads / 64; ++w) s += sh.part[w][tid];
-    sh.sums[tid] = s;
-  }
-  __syncthreads();
-}
-
 // Low-resolution matcher score of a leaf pose (low_resolution_matcher.cc:23-35):
 // float sum in point order. Probabilities are computed in parallel, summed
 // sequentially by thread 0. Result valid in thread 0.
-__device__ float LowResScore(F3Shared& sh, const Submap3Desc& sm, const float* __restrict__ low_pts,
+template <class Shared>
+__device__ float LowResScore(Shared& sh, const Submap3Desc& sm, const float* __restrict__ low_pts,
                              int m, float qw, float qx, float qy, float qz, float tx, float ty,
                              float tz) {
   const int tid = threadIdx.x;
@@ -351,13 +294,17 @@ __device__ float LowResScore(F3Shared& sh, const Submap3Desc& sm, const float* _
 #define F3_FLUSH(stats) (void)0
 #endif
 
-__global__ void __launch_bounds__(kSearch3dThreads) __attribute__((amdgpu_waves_per_eu(kSearch3dBlocksPerCu, kSearch3dBlocksPerCu)))
+// kPts: cloud capacity in LDS; kWaves: waves per SIMD the kernel is built
+// for (= workgroups per CU with 256 threads).
+template <int kPts, int kWaves>
+__global__ void __launch_bounds__(kSearch3dThreads) __attribute__((amdgpu_waves_per_eu(kWaves, kWaves)))
 fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restrict__ pairs,
-              const Yaw3Desc* __restrict__ yaws, int num_items, const float* __restrict__ points,
+              const Yaw3Desc* __restrict__ yaws, int item_begin, int num_items,
+              const float* __restrict__ points,
               const float* __restrict__ low_points, unsigned* __restrict__ counter,
               unsigned long long* __restrict__ best, int32_t* __restrict__ status,
               unsigned long long* __restrict__ stats) {
-  __shared__ F3Shared sh;
+  __shared__ F3SharedT<kPts> sh;
   const int tid = threadIdx.x;
   unsigned long long lookups = 0, root_lookups = 0;
   F3_PROF_DECL;
@@ -365,8 +312,8 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
   for (;;) {
     if (tid == 0) sh.item = static_cast<int>(atomicAdd(counter, 1u));
     __syncthreads();
-    const int item = sh.item;
-    if (item >= num_items) break;
+    if (sh.item >= num_items) break;
+    const int item = item_begin + sh.item;
     F3_RESET();
     const Yaw3Desc yw = yaws[item];
     const Pair3Desc pd = pairs[yw.pair];
@@ -879,7 +826,7 @@ __global__ void __launch_bounds__(kSearch3dThreads)
 fast3d_finalize(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restrict__ pairs,
                 const Yaw3Desc* __restrict__ yaws, const float* __restrict__ low_points,
                 const unsigned long long* __restrict__ best, float* __restrict__ low_score) {
-  __shared__ F3Shared sh;
+  __shared__ F3SharedT<kSmall3dPoints> sh;
   const int p = blockIdx.x;
   const unsigned long long key = best[p];
   const Pair3Desc pd = pairs[p];
@@ -919,6 +866,7 @@ struct RotPair3 {
   int32_t window;       // angular window A: yaws k = 0..2A
   float step, yaw0;
   int64_t out;          // score offset
+  double min_score;     // the submap's min_rotational_score
 };
 
 template <typename F>
@@ -993,6 +941,53 @@ __global__ void rot_scores(const RotPair3* __restrict__ pairs, int num_pairs,
   out[rp.out + k] = score;
 }
 
+// The yaws of each pair whose rotational score passes (the filter of
+// GetDiscreteScans, fast_correlative_scan_matcher_3d.cc:258-270: kept unless
+// score < min_rotational_score, compared in double), in increasing k,
+// appended at a global cursor: range[p] = {offset, count}. Only these travel
+// back to the host.
+__global__ void __launch_bounds__(256)
+yaw_compact(const RotPair3* __restrict__ pairs, const float* __restrict__ scores,
+            unsigned* __restrict__ cursor, int2* __restrict__ range, int32_t* __restrict__ out_k,
+            float* __restrict__ out_s) {
+  __shared__ int wcount[4];
+  __shared__ int base_sh;
+  const int p = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const RotPair3 rp = pairs[p];
+  const int nk = 2 * rp.window + 1;
+  const float* sc = scores + rp.out;
+  auto pass = [&](int k) { return k < nk && !(static_cast<double>(sc[k]) < rp.min_score); };
+  int cnt = 0;
+  for (int k = tid; k < nk; k += 256) cnt += pass(k);
+  for (int m = 32; m > 0; m >>= 1) cnt += __shfl_xor(cnt, m, 64);
+  if (lane == 0) wcount[w] = cnt;
+  __syncthreads();
+  if (tid == 0) {
+    const int total = wcount[0] + wcount[1] + wcount[2] + wcount[3];
+    const int base = static_cast<int>(atomicAdd(cursor, static_cast<unsigned>(total)));
+    range[p] = make_int2(base, total);
+    base_sh = base;
+  }
+  __syncthreads();
+  int at = base_sh;
+  for (int c0 = 0; c0 < nk; c0 += 256) {
+    const int k = c0 + tid;
+    const bool f = pass(k);
+    const unsigned long long b = __ballot(f);
+    __syncthreads();
+    if (lane == 0) wcount[w] = __popcll(b);
+    __syncthreads();
+    int before = 0;
+    for (int v = 0; v < w; ++v) before += wcount[v];
+    if (f) {
+      const int pos = at + before + __popcll(b & ((1ull << lane) - 1ull));
+      out_k[pos] = k;
+      out_s[pos] = sc[k];
+    }
+    at += wcount[0] + wcount[1] + wcount[2] + wcount[3];
+  }
+}
+
 // ------------------------------------------------------------ launchers ----
 
 hipError_t LaunchBrickFromValues(const uint16_t* values, int64_t n, const float* ptab,
@@ -1033,13 +1028,19 @@ hipError_t LaunchRt3dScore(int num_rot, hipStream_t st, const float* prob, const
   return hipGetLastError();
 }
 
-hipError_t LaunchFast3dSearch(int grid, hipStream_t st, const Submap3Desc* submaps,
-                              const Pair3Desc* pairs, const Yaw3Desc* yaws, int num_items,
-                              const float* points, const float* low_points, unsigned* counter,
-                              unsigned long long* best, int32_t* status,
+hipError_t LaunchFast3dSearch(bool large, int grid, hipStream_t st, const Submap3Desc* submaps,
+                              const Pair3Desc* pairs, const Yaw3Desc* yaws, int item_begin,
+                              int num_items, const float* points, const float* low_points,
+                              unsigned* counter, unsigned long long* best, int32_t* status,
                               unsigned long long* stats) {
-  hipLaunchKernelGGL(fast3d_search, dim3(grid), dim3(kSearch3dThreads), 0, st, submaps, pairs,
-                     yaws, num_items, points, low_points, counter, best, status, stats);
+  if (large)
+    hipLaunchKernelGGL((fast3d_search<kMax3dPoints, kSearch3dBlocksPerCuLarge>), dim3(grid),
+                       dim3(kSearch3dThreads), 0, st, submaps, pairs, yaws, item_begin, num_items,
+                       points, low_points, counter, best, status, stats);
+  else
+    hipLaunchKernelGGL((fast3d_search<kSmall3dPoints, kSearch3dBlocksPerCu>), dim3(grid),
+                       dim3(kSearch3dThreads), 0, st, submaps, pairs, yaws, item_begin, num_items,
+                       points, low_points, counter, best, status, stats);
   return hipGetLastError();
 }
 
@@ -1059,6 +1060,15 @@ hipError_t LaunchRotScores(const void* pairs, int num_pairs, int max_yaws, const
   const int threads = 64;
   hipLaunchKernelGGL(rot_scores, dim3((max_yaws + threads - 1) / threads, num_pairs), dim3(threads),
                      0, st, static_cast<const RotPair3*>(pairs), num_pairs, hists, out);
+  return hipGetLastError();
+}
+
+hipError_t LaunchYawCompact(const void* pairs, int num_pairs, const float* scores,
+                            unsigned* cursor, int2* range, int32_t* out_k, float* out_s,
+                            hipStream_t st) {
+  if (num_pairs <= 0) return hipSuccess;
+  hipLaunchKernelGGL(yaw_compact, dim3(num_pairs), dim3(256), 0, st,
+                     static_cast<const RotPair3*>(pairs), scores, cursor, range, out_k, out_s);
   return hipGetLastError();
 }
 

@@ -281,3 +281,56 @@ def test_synthetic_pairs_match_oracle(csm, oracle, world3d):
             stats[assert_same_result(gpu, ref, om, False, init, ((0, 0, 0), (1, 0, 0, 0)), node,
                                      o.min_low_resolution_score)] += 1
     assert stats["exact"] + stats["tie"] >= 3, stats
+
+
+def test_large_clouds_match_oracle(csm, oracle, world3d):
+    """Clouds past the small build's LDS capacity (2048 points) take the
+    large-cloud build (up to 8192); a batch mixing both is split over the
+    two launches and results come back in pair order. Past 8192: CSM_ERANGE."""
+    w = world3d
+    o = csm.FastCorrelativeScanMatcherOptions3D()
+    s = 0
+    oh, ol = oracle.hybrid_grid(w.high_resolution), oracle.hybrid_grid(w.low_resolution)
+    oh.set_values(*w.high_cells[s])
+    ol.set_values(*w.low_cells[s])
+    om = oracle.fast3d(oh, ol, w.submap_hist[s], opt_tuple(o))
+    gm = csm.FastCorrelativeScanMatcher3D(csm.HybridGrid(w.high_resolution, *w.high_cells[s]),
+                                          csm.HybridGrid(w.low_resolution, *w.low_cells[s]),
+                                          w.submap_hist[s], o)
+    c = int(w.submap_nodes[s])
+    small = w.node(c)
+    rng = np.random.default_rng(5)
+    pts = small.high_resolution_point_cloud
+    reps = 2100 // len(pts) + 1
+    big_cloud = np.concatenate([pts + rng.uniform(-0.03, 0.03, pts.shape).astype(np.float32)
+                                for _ in range(reps)]).astype(np.float32)
+    assert 2048 < len(big_cloud) <= 8192
+    big = csm.NodeData3D(big_cloud, small.low_resolution_point_cloud,
+                         small.rotational_scan_matcher_histogram, small.gravity_alignment)
+    rot = w.node_rotation(c)
+    ref = om.match_full_submap(rot, (1, 0, 0, 0), big, 0.55)
+    gpu = gm.MatchFullSubmap(rot, (1, 0, 0, 0), big, 0.55)
+    assert assert_same_result(gpu, ref, om, True, rot, (1, 0, 0, 0), big,
+                              o.min_low_resolution_score) in ("exact", "tie")
+    truth = w.node_in_submap(c, s)
+    init = ((truth[0][0] + 0.3, truth[0][1] - 0.2, 0.1), truth[1])
+    ident = ((0, 0, 0), (1, 0, 0, 0))
+    ref = om.match(init, ident, big, 0.55)
+    gpu = gm.Match(init, ident, big, 0.55)
+    assert_same_result(gpu, ref, om, False, init, ident, big, o.min_low_resolution_score)
+    # Mixed batch, large first in input order.
+    huge = csm.NodeData3D(np.tile(big_cloud, (4, 1)), small.low_resolution_point_cloud,
+                          small.rotational_scan_matcher_histogram, small.gravity_alignment)
+    pairs = [(0, 1, False, 0.55, init, ident), (0, 0, False, 0.55, init, ident),
+             (0, 1, True, 0.55, ((0, 0, 0), rot), ident),
+             (0, 2, False, 0.55, init, ident)]
+    res = csm.match_batch_3d([gm], [small, big, huge], pairs)
+    for (sub, n, full, ms, npose, spose), r in zip(pairs[:3], res[:3]):
+        node = [small, big][n]
+        single = (gm.MatchFullSubmap(npose[1], spose[1], node, ms) if full
+                  else gm.Match(npose, spose, node, ms))
+        assert (single is not None) == (r.status == csm.CSM_OK)
+        if single is not None:
+            assert np.float32(single.score) == np.float32(r.score)
+            assert single.pose_estimate == r.pose.as_tuple()
+    assert res[3].status == csm.CSM_ERANGE
