@@ -197,7 +197,19 @@ rt3d_score(const float* __restrict__ prob, Brick3 gb, float res, float inv,
 
 template <int kPts>
 struct F3SharedT {
-  int16_t cx[kPts], cy[kPts], cz[kPts];
+  // The discretized cloud: full-resolution cells (int16 x, y, z), or — once
+  // roots are scored from the cell list — packed words relative to an origin
+  // aligned to 2^E (PackedCloud below).
+  union {
+    struct {
+      int16_t x[kPts], y[kPts], z[kPts];
+    } c;
+    uint32_t pk[kPts];
+  } cloud;
+  int org[3];              // packed origin (full-resolution cells)
+  int rel_min[3], rel_max[3];
+  int fmin[3], fmax[3];    // full-resolution cloud bounds
+  int packed;
   int16_t sx[kStack3d], sy[kStack3d], sz[kStack3d];
   int8_t sd[kStack3d];
   int ssum[kStack3d];
@@ -331,9 +343,9 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
       const int iy = RoundDiv(__fadd_rn(oy, yw.ty), res, inv);
       const int iz = RoundDiv(__fadd_rn(oz, yw.tz), res, inv);
       if (abs(ix) > kCellLimit3d || abs(iy) > kCellLimit3d || abs(iz) > kCellLimit3d) sh.error = 1;
-      sh.cx[i] = static_cast<int16_t>(ix);
-      sh.cy[i] = static_cast<int16_t>(iy);
-      sh.cz[i] = static_cast<int16_t>(iz);
+      sh.cloud.c.x[i] = static_cast<int16_t>(ix);
+      sh.cloud.c.y[i] = static_cast<int16_t>(iy);
+      sh.cloud.c.z[i] = static_cast<int16_t>(iz);
     }
     __syncthreads();
     if (sh.error) {
@@ -383,12 +395,19 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
     if (tid < 3) {
       sh.rmin[tid] = 1 << 30;
       sh.rmax[tid] = -(1 << 30);
+      sh.fmin[tid] = 1 << 30;
+      sh.fmax[tid] = -(1 << 30);
     }
     __syncthreads();
     {
       int mn[3] = {1 << 30, 1 << 30, 1 << 30}, mx[3] = {-(1 << 30), -(1 << 30), -(1 << 30)};
+      int fmn[3] = {1 << 30, 1 << 30, 1 << 30}, fmx[3] = {-(1 << 30), -(1 << 30), -(1 << 30)};
       for (int i = tid; i < n; i += kSearch3dThreads) {
-        int c[3] = {sh.cx[i], sh.cy[i], sh.cz[i]};
+        int c[3] = {sh.cloud.c.x[i], sh.cloud.c.y[i], sh.cloud.c.z[i]};
+        for (int a = 0; a < 3; ++a) {
+          fmn[a] = min(fmn[a], c[a]);
+          fmx[a] = max(fmx[a], c[a]);
+        }
         if (treduced) {
           c[0] = ((c[0] - pd.wxy) >> te) - lwx;
           c[1] = ((c[1] - pd.wxy) >> te) - lwy;
@@ -403,12 +422,16 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
         for (int m = 32; m > 0; m >>= 1) {
           mn[a] = min(mn[a], __shfl_xor(mn[a], m, 64));
           mx[a] = max(mx[a], __shfl_xor(mx[a], m, 64));
+          fmn[a] = min(fmn[a], __shfl_xor(fmn[a], m, 64));
+          fmx[a] = max(fmx[a], __shfl_xor(fmx[a], m, 64));
         }
       }
       if ((tid & 63) == 0) {
         for (int a = 0; a < 3; ++a) {
           atomicMin(&sh.rmin[a], mn[a]);
           atomicMax(&sh.rmax[a], mx[a]);
+          atomicMin(&sh.fmin[a], fmn[a]);
+          atomicMax(&sh.fmax[a], fmx[a]);
         }
       }
     }
@@ -426,7 +449,7 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
       if (tid == 0) sh.ntcell = 0;
       __syncthreads();
       for (int i = tid; i < n; i += kSearch3dThreads) {
-        int c[3] = {sh.cx[i], sh.cy[i], sh.cz[i]};
+        int c[3] = {sh.cloud.c.x[i], sh.cloud.c.y[i], sh.cloud.c.z[i]};
         if (treduced) {
           c[0] = ((c[0] - pd.wxy) >> te) - lwx;
           c[1] = ((c[1] - pd.wxy) >> te) - lwy;
@@ -451,6 +474,43 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
     }
     const bool cells_ok = use_cells && sh.ntcell <= kTopCells3d;
     const int ntc = cells_ok ? sh.ntcell : 0;
+    // Packed cloud for the DFS (only when roots are scored from the cell list:
+    // nothing reads the int16 cells after this). Origin o = w + 2^E * floor((min
+    // - w) / 2^E), E the largest reduction exponent of the DFS child levels, so
+    // that ((c - w) >> e) = ((o - w) >> e) + ((c - o) >> e) for every e <= E.
+    // Fields: x bits 0-10, y 11-21, z 22-31 of c - o; the words are recomputed
+    // from the points with the discretization's arithmetic.
+    if (tid == 0) {
+      const int E = max(0, (top - 1) - sm.full_resolution_depth + 1);
+      const int w3[3] = {pd.wxy, pd.wxy, pd.wz};
+      const int lim[3] = {2048, 2048, 1024};
+      bool ok = cells_ok && n > 0 && top >= 1 && E <= 9;
+      for (int l = 0; ok && l < top; ++l)  // slab strides fit __umul24
+        ok = static_cast<int64_t>(sm.oct[l].nx) * sm.oct[l].ny * 8 < (1 << 24);
+      for (int a = 0; a < 3; ++a) {
+        const int o = w3[a] + (((sh.fmin[a] - w3[a]) >> E) << E);
+        sh.org[a] = o;
+        sh.rel_min[a] = sh.fmin[a] - o;
+        sh.rel_max[a] = sh.fmax[a] - o;
+        ok = ok && sh.rel_max[a] < lim[a];
+      }
+      sh.packed = ok;
+    }
+    __syncthreads();
+    const bool packed = sh.packed;
+    if (packed) {
+      for (int i = tid; i < n; i += kSearch3dThreads) {
+        const float* p = points + 3 * (pd.point_offset + i);
+        float ox, oy, oz;
+        Rotate3(yw.qw, yw.qx, yw.qy, yw.qz, p[0], p[1], p[2], &ox, &oy, &oz);
+        const int ix = RoundDiv(__fadd_rn(ox, yw.tx), res, inv) - sh.org[0];
+        const int iy = RoundDiv(__fadd_rn(oy, yw.ty), res, inv) - sh.org[1];
+        const int iz = RoundDiv(__fadd_rn(oz, yw.tz), res, inv) - sh.org[2];
+        sh.cloud.pk[i] = static_cast<uint32_t>(ix) | (static_cast<uint32_t>(iy) << 11) |
+                         (static_cast<uint32_t>(iz) << 22);
+      }
+    }
+    __syncthreads();
     F3_MARK(9);
     const bool skip_empty = pd.min_sum > 0;
     for (int r0 = 0; r0 < T; r0 += kRootScore3d) {
@@ -512,7 +572,7 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
         } else if (valid) {
           root_lookups += n;
           for (int i = 0; i < n; ++i) {
-            int x = sh.cx[i], y = sh.cy[i], z = sh.cz[i];
+            int x = sh.cloud.c.x[i], y = sh.cloud.c.y[i], z = sh.cloud.c.z[i];
             if (treduced) {
               x = ((x - pd.wxy) >> te) - lwx;
               y = ((y - pd.wxy) >> te) - lwy;
@@ -616,8 +676,7 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
       if (nb == 0) break;
       constexpr int kLanes = kSearch3dThreads / kBatch3d;  // lanes per node
       const int half = tid / kLanes, hl = tid % kLanes;
-      int cx8[8], cy8[8], cz8[8];
-      int nc = 0, cd = 0;
+      int nc = 0, cd = 0, ox = 0, oy = 0, oz = 0, hw = 0;
       int acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
       // Other yaws' progress on this pair, read while the batch scores and
       // folded in at the next pop.
@@ -625,19 +684,15 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
       if (tid == 0) gbest = *reinterpret_cast<volatile unsigned long long*>(best + yw.pair);
       if (half < nb) {
         const int d = sh.bn_d[half];
-        const int ox = sh.bn_x[half], oy = sh.bn_y[half], oz = sh.bn_z[half];
-        const int hw = 1 << (d - 1);
-        // Children by octant k = z << 2 | y << 1 | x; present unless past the
-        // window (the reference's breaks, :412-430).
-        int present = 0;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          cx8[k] = ox + ((k & 1) ? hw : 0);
-          cy8[k] = oy + ((k & 2) ? hw : 0);
-          cz8[k] = oz + ((k & 4) ? hw : 0);
-          if (cx8[k] <= pd.wxy && cy8[k] <= pd.wxy && cz8[k] <= pd.wz) present |= 1 << k;
-        }
-        nc = present;
+        ox = sh.bn_x[half];
+        oy = sh.bn_y[half];
+        oz = sh.bn_z[half];
+        hw = 1 << (d - 1);
+        // Children by octant k = z << 2 | y << 1 | x. Octant 0 sits at the
+        // node's own offset (inside the window); the others are present unless
+        // past it (the reference's breaks, :412-430).
+        nc = (ox + hw <= pd.wxy ? 0xFF : 0x55) & (oy + hw <= pd.wxy ? 0xFF : 0x33) &
+             (oz + hw <= pd.wz ? 0xFF : 0x0F);
         cd = d - 1;
         const int e = max(0, cd - sm.full_resolution_depth + 1);
         const bool reduced = cd >= sm.full_resolution_depth;
@@ -650,7 +705,9 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
         const int onx = ob.nx, ony = ob.ny, onz = ob.nz, ooff = static_cast<int>(ob.offset);
         constexpr int kOOB3 = 0x7ffffff0;
         auto load = [&](int i) -> uint64_t {
-          int a = sh.cx[i], bb = sh.cy[i], c = sh.cz[i];
+          const bool live = i < n;
+          i = live ? i : 0;
+          int a = sh.cloud.c.x[i], bb = sh.cloud.c.y[i], c = sh.cloud.c.z[i];
           if (reduced) {
             a = ((a - pd.wxy) >> e) - lx;
             bb = ((bb - pd.wxy) >> e) - ly;
@@ -659,7 +716,7 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
           a += bx;
           bb += by;
           c += bz;
-          const bool in = static_cast<unsigned>(a) < static_cast<unsigned>(onx) &&
+          const bool in = live && static_cast<unsigned>(a) < static_cast<unsigned>(onx) &&
                           static_cast<unsigned>(bb) < static_cast<unsigned>(ony) &&
                           static_cast<unsigned>(c) < static_cast<unsigned>(onz);
           const int off = in ? ooff + ((c * ony + bb) * onx + a) * 8 : kOOB3;
@@ -679,23 +736,79 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
           a6 = __builtin_amdgcn_udot4(hi, 0x00010000u, a6, false);
           a7 = __builtin_amdgcn_udot4(hi, 0x01000000u, a7, false);
         };
-        int i = hl;
-        for (; i + 7 * kLanes < n; i += 8 * kLanes) {
-          uint64_t v[8];
+        // All of a lane's points (up to kRound per round) in flight at once;
+        // past-the-end slots load from the out-of-range offset and add 0.
+        constexpr int kRound = 16;
+        if (packed) {
+          // c - o of a point as bitfields; at this level, with e <= E,
+          // a = ((c - o) >> e) + Kx etc. (the window and box origin folded in).
+          const int kx = (reduced ? ((sh.org[0] - pd.wxy) >> e) - lx : sh.org[0]) + bx;
+          const int ky = (reduced ? ((sh.org[1] - pd.wxy) >> e) - ly : sh.org[1]) + by;
+          const int kz = (reduced ? ((sh.org[2] - pd.wz) >> e) - lz : sh.org[2]) + bz;
+          const unsigned wxy = 11 - e, wzz = 10 - e;  // e <= E <= 9
+          // Wave-uniform: every node of the wave has the whole cloud box inside
+          // its octet brick, so no point needs a bounds check.
+          const bool inside = (sh.rel_min[0] >> e) + kx >= 0 && (sh.rel_max[0] >> e) + kx < onx &&
+                              (sh.rel_min[1] >> e) + ky >= 0 && (sh.rel_max[1] >> e) + ky < ony &&
+                              (sh.rel_min[2] >> e) + kz >= 0 && (sh.rel_max[2] >> e) + kz < onz;
+          if (__ballot(!inside) == 0) {
+            const unsigned sy = static_cast<unsigned>(onx) * 8u, sz = static_cast<unsigned>(ony) * sy;
+            const int kall = static_cast<int>(
+                static_cast<unsigned>(ooff) +
+                ((static_cast<unsigned>(kz) * ony + static_cast<unsigned>(ky)) * onx +
+                 static_cast<unsigned>(kx)) * 8u);
+            auto load_in = [&](int i) -> uint64_t {
+              const bool live = i < n;
+              const uint32_t w = sh.cloud.pk[live ? i : 0];
+              const unsigned rx = __builtin_amdgcn_ubfe(w, e, wxy);
+              const unsigned ry = __builtin_amdgcn_ubfe(w, 11 + e, wxy);
+              const unsigned rz = __builtin_amdgcn_ubfe(w, 22 + e, wzz);
+              const int off = live ? static_cast<int>(__umul24(rz, sz) + __umul24(ry, sy) + (rx << 3) +
+                                                      static_cast<unsigned>(kall))
+                                   : kOOB3;
+              const uint32_t lo = __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0);
+              const uint32_t hi = __builtin_amdgcn_raw_buffer_load_b32(rs, off + 4, 0, 0);
+              return (static_cast<uint64_t>(hi) << 32) | lo;
+            };
+            for (int i0 = hl; i0 < n; i0 += kRound * kLanes) {
+              uint64_t v[kRound];
 #pragma unroll
-          for (int u = 0; u < 8; ++u) v[u] = load(i + u * kLanes);
+              for (int u = 0; u < kRound; ++u) v[u] = load_in(i0 + u * kLanes);
 #pragma unroll
-          for (int u = 0; u < 8; ++u) accumulate(v[u]);
+              for (int u = 0; u < kRound; ++u) accumulate(v[u]);
+            }
+          } else {
+            auto load_chk = [&](int i) -> uint64_t {
+              const bool live = i < n;
+              const uint32_t w = sh.cloud.pk[live ? i : 0];
+              const int a = static_cast<int>(__builtin_amdgcn_ubfe(w, e, wxy)) + kx;
+              const int bb = static_cast<int>(__builtin_amdgcn_ubfe(w, 11 + e, wxy)) + ky;
+              const int c = static_cast<int>(__builtin_amdgcn_ubfe(w, 22 + e, wzz)) + kz;
+              const bool in = live && static_cast<unsigned>(a) < static_cast<unsigned>(onx) &&
+                              static_cast<unsigned>(bb) < static_cast<unsigned>(ony) &&
+                              static_cast<unsigned>(c) < static_cast<unsigned>(onz);
+              const int off = in ? ooff + ((c * ony + bb) * onx + a) * 8 : kOOB3;
+              const uint32_t lo = __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0);
+              const uint32_t hi = __builtin_amdgcn_raw_buffer_load_b32(rs, off + 4, 0, 0);
+              return (static_cast<uint64_t>(hi) << 32) | lo;
+            };
+            for (int i0 = hl; i0 < n; i0 += kRound * kLanes) {
+              uint64_t v[kRound];
+#pragma unroll
+              for (int u = 0; u < kRound; ++u) v[u] = load_chk(i0 + u * kLanes);
+#pragma unroll
+              for (int u = 0; u < kRound; ++u) accumulate(v[u]);
+            }
+          }
+        } else {
+          for (int i0 = hl; i0 < n; i0 += kRound * kLanes) {
+            uint64_t v[kRound];
+#pragma unroll
+            for (int u = 0; u < kRound; ++u) v[u] = load(i0 + u * kLanes);
+#pragma unroll
+            for (int u = 0; u < kRound; ++u) accumulate(v[u]);
+          }
         }
-        for (; i + 3 * kLanes < n; i += 4 * kLanes) {
-          const uint64_t v0 = load(i), v1 = load(i + kLanes), v2 = load(i + 2 * kLanes),
-                         v3 = load(i + 3 * kLanes);
-          accumulate(v0);
-          accumulate(v1);
-          accumulate(v2);
-          accumulate(v3);
-        }
-        for (; i < n; i += kLanes) accumulate(load(i));
         acc[0] = a0;
         acc[1] = a1;
         acc[2] = a2;
@@ -717,46 +830,46 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
         v += __builtin_amdgcn_update_dpp(0, v, 0x140, 0xF, 0xF, false);  // row_mirror
         acc[k] = v;
       }
-      if (half < nb && hl == 0) {
-        lookups += static_cast<unsigned long long>(__popc(nc)) * n;
+      // Lane k < 8 of a node handles child k: its sum, then its rank among
+      // the kept children (ascending bound, stable; the best is popped first).
+      if (half < nb && hl < 8) {
+        const int k = hl;
+        if (k == 0) lookups += static_cast<unsigned long long>(__popc(nc)) * n;
         const int best_sum = static_cast<int>(sh.best >> pd.key_shift);
+        int my = acc[0];
+#pragma unroll
+        for (int j = 1; j < 8; ++j) my = k == j ? acc[j] : my;
+        const int cxk = ox + ((k & 1) ? hw : 0), cyk = oy + ((k & 2) ? hw : 0),
+                  czk = oz + ((k & 4) ? hw : 0);
+        const bool pres = (nc >> k) & 1;
         if (cd > 0) {
-          // Kept children in ascending bound order (stable; the best is
-          // popped first), ranked with static indices only.
-          bool keep[8];
-          int m = 0;
+          int m = 0, rank = 0;
 #pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            keep[k] = ((nc >> k) & 1) && acc[k] >= pd.min_sum && acc[k] >= best_sum;
-            m += keep[k];
+          for (int j = 0; j < 8; ++j) {
+            const bool kj = ((nc >> j) & 1) && acc[j] >= pd.min_sum && acc[j] >= best_sum;
+            m += kj;
+            rank += kj && (acc[j] < my || (acc[j] == my && j < k));
           }
-          const int base = atomicAdd(&sh.sp, m);
-#pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            if (!keep[k]) continue;
-            int rank = 0;
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-              rank += keep[j] && (acc[j] < acc[k] || (acc[j] == acc[k] && j < k));
-            sh.sx[base + rank] = static_cast<int16_t>(cx8[k]);
-            sh.sy[base + rank] = static_cast<int16_t>(cy8[k]);
-            sh.sz[base + rank] = static_cast<int16_t>(cz8[k]);
+          int base = 0;
+          if (k == 0 && m > 0) base = atomicAdd(&sh.sp, m);
+          base = __shfl(base, (tid & 63) & ~(kLanes - 1), 64);
+          if (pres && my >= pd.min_sum && my >= best_sum) {
+            sh.sx[base + rank] = static_cast<int16_t>(cxk);
+            sh.sy[base + rank] = static_cast<int16_t>(cyk);
+            sh.sz[base + rank] = static_cast<int16_t>(czk);
             sh.sd[base + rank] = static_cast<int8_t>(cd);
-            sh.ssum[base + rank] = acc[k];
+            sh.ssum[base + rank] = my;
           }
-        } else {
-#pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            if (!((nc >> k) & 1) || acc[k] < pd.min_sum) continue;
-            const unsigned long long id = LeafId(pd, yw.yaw_id, cx8[k], cy8[k], cz8[k]);
-            const unsigned long long key = (static_cast<unsigned long long>(acc[k]) << pd.key_shift) |
-                                           (~id & ((1ull << pd.key_shift) - 1));
-            if (key <= sh.best) continue;
+        } else if (pres && my >= pd.min_sum) {
+          const unsigned long long id = LeafId(pd, yw.yaw_id, cxk, cyk, czk);
+          const unsigned long long key = (static_cast<unsigned long long>(my) << pd.key_shift) |
+                                         (~id & ((1ull << pd.key_shift) - 1));
+          if (key > sh.best) {
             const int at = atomicAdd(&sh.nleaf, 1);
             sh.leaf_keys[at] = key;
-            sh.leaf_x[at] = cx8[k];
-            sh.leaf_y[at] = cy8[k];
-            sh.leaf_z[at] = cz8[k];
+            sh.leaf_x[at] = cxk;
+            sh.leaf_y[at] = cyk;
+            sh.leaf_z[at] = czk;
           }
         }
       }
