@@ -53,7 +53,8 @@ def parse():
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
     p.add_argument("--no-3d", action="store_true")
     p.add_argument("--nodes3d", type=int, default=500)
-    p.add_argument("--submaps3d", type=int, default=25)
+    p.add_argument("--submaps3d", type=int, default=25, help="3D submaps per GPU (C5: 200 / 8)")
+    p.add_argument("--steps3d", type=int, default=3)
     return p.parse_args()
 
 
@@ -182,7 +183,10 @@ def main():
         out["cpu_baseline"] = cpu_baseline(world, my_submaps, args)
     if rank == 0 and world_size == 1 and not args.no_3d:
         out["rt3d"] = rt3d_bench(csm, ctx, args)
-        out["fast3d"] = fast3d_bench(csm, ctx, args)
+    if not args.no_3d:  # collective over ranks: the C5 sweep, submap-sharded
+        f3 = fast3d_bench(csm, ctx, args, rank, world_size, dist, coll_dev, barrier_sync, cdist)
+        if rank == 0:
+            out["fast3d"] = f3
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:
@@ -306,12 +310,17 @@ def rt3d_bench(csm, ctx, args):
     return res
 
 
-def fast3d_bench(csm, ctx, args):
-    """C5 per-GPU share: FastCorrelativeScanMatcher3D::MatchFullSubmap over
-    nodes3d x submaps3d pairs (500 x 25 = the 8-GPU C5 sweep's share of one
-    GPU), pose_graph.lua 3D options, global_localization_min_score 0.6."""
+def fast3d_bench(csm, ctx, args, rank=0, world_size=1, dist=None, coll_dev=None,
+                 barrier_sync=lambda: None, cdist=None):
+    """C5: FastCorrelativeScanMatcher3D::MatchFullSubmap over nodes3d nodes x
+    (submaps3d x world_size) submaps, submap-sharded: each rank builds and
+    searches its submaps3d submaps of the same world against every node (the
+    8-GPU sweep of 500 x 200 is 500 x 25 per GPU), pose_graph.lua 3D options,
+    global_localization_min_score 0.6. Accepted constraints are gathered to
+    rank 0 each step; value = all ranks' pairs / the slowest rank's time."""
     t0 = time.time()
-    w = csm.SyntheticWorld3D(num_nodes=args.nodes3d, num_submaps=args.submaps3d,
+    w = csm.SyntheticWorld3D(num_nodes=args.nodes3d, num_submaps=args.submaps3d * world_size,
+                             submap_range=(rank * args.submaps3d, args.submaps3d),
                              seed=args.seed + 5)
     gen = time.time() - t0
     o = csm.FastCorrelativeScanMatcherOptions3D()
@@ -321,27 +330,47 @@ def fast3d_bench(csm, ctx, args):
     mats = [csm.FastCorrelativeScanMatcher3D(g[0], g[1], w.submap_hist[s], o, ctx)
             for s, g in enumerate(grids)]
     nodes = [w.node(i) for i in range(w.num_nodes)]
-    ident = ((0, 0, 0), (1, 0, 0, 0))
     sub = np.repeat(np.arange(w.num_submaps), w.num_nodes)
     nod = np.tile(np.arange(w.num_nodes), w.num_submaps)
     rot = np.array([w.node_rotation(n) for n in range(w.num_nodes)])
     pairs = csm.make_pairs_3d(sub, nod, 0.6, True, node_q=rot[nod])
-    csm.match_batch_3d(mats, nodes, pairs[:64], ctx)  # warm-up
+    submission = np.int64(rank) * len(pairs) + np.arange(len(pairs), dtype=np.int64)
+    sub_global = w.submap_ids[sub].astype(np.int64)
+
+    def step():
+        res = csm.match_batch_3d(mats, nodes, pairs, ctx)
+        rec = cdist.make_records_3d(res, submission, sub_global, nod) if cdist else None
+        if cdist is not None:
+            rec = cdist.gather_records(rec, dist, rank, world_size, coll_dev)
+        return res, rec
+
+    step()  # warm-up at full size (staging buffers)
     ctx.reset_timing()
     ctx.enable_timing(True)
+    barrier_sync()
     t0 = time.perf_counter()
-    res3 = csm.match_batch_3d(mats, nodes, pairs, ctx)
+    reps = max(1, args.steps3d)
+    for _ in range(reps):
+        res3, rec = step()
+    barrier_sync()
     wall = time.perf_counter() - t0
     tm = ctx.timing()
     ctx.enable_timing(False)
-    out = {"config": f"C5 share: MatchFullSubmap, {w.num_nodes} nodes x {w.num_submaps} submaps "
-                     "(0.10/0.45 m grids, ~200-point clouds, 120-bucket histograms), "
-                     "branch_and_bound_depth 8, full_resolution_depth 3",
-           "pairs": len(pairs), "value": len(pairs) / wall, "unit": "pairs/s",
-           "accepted": int((res3["status"] == 0).sum()), "wall_s": wall,
-           "kernel_ms": tm.fast3d_kernel_ms, "lookups": tm.fast3d_lookups,
+    if cdist is not None:
+        wall = cdist.max_over_ranks(wall, dist, coll_dev)
+    total = len(pairs) * world_size * reps
+    out = {"config": f"C5: MatchFullSubmap, {w.num_nodes} nodes x {w.num_submaps} submaps per GPU "
+                     f"({w.num_submaps * world_size} total; 0.10/0.45 m grids, ~200-point clouds, "
+                     "120-bucket histograms), branch_and_bound_depth 8, full_resolution_depth 3",
+           "pairs_per_step": len(pairs) * world_size, "steps": reps, "value": total / wall,
+           "unit": "pairs/s", "n_gpus": world_size, "scaling": "weak",
+           "accepted_per_step": int(len(rec)) if rec is not None else int((res3["status"] == 0).sum()),
+           "ms_per_step": wall / reps * 1e3,
+           "kernel_ms_per_step": tm.fast3d_kernel_ms / reps, "lookups_per_step": tm.fast3d_lookups / reps,
            "algorithmic_GBps": tm.fast3d_lookups / (tm.fast3d_kernel_ms * 1e-3) / 1e9
            if tm.fast3d_kernel_ms else 0.0, "setup_s": gen}
+    if rank != 0 or world_size != 1:
+        return out
     if not args.no_cpu:
         try:
             sys.path.insert(0, os.path.join(ROOT, "tests"))

@@ -62,6 +62,10 @@ typedef struct csm_synth3d_config {
   int32_t histogram_size;
   double insert_voxel;                     // decimation of scans inserted into submaps
   int32_t threads;
+  // Build only submaps [submap_begin, submap_begin + submap_count) of the
+  // num_submaps-submap world (0 = all): a rank's shard, identical to those
+  // submaps of the full world. Submap queries index the built range from 0.
+  int32_t submap_begin, submap_count;
 } csm_synth3d_config;
 
 typedef struct csm_synth3d csm_synth3d;

@@ -290,11 +290,15 @@ void csm_synth3d_default_config(csm_synth3d_config* c) {
   c->histogram_size = 120;
   c->insert_voxel = 0.15;  // voxel_filter_size (trajectory_builder_3d.lua)
   c->threads = 0;
+  c->submap_begin = 0;
+  c->submap_count = 0;
 }
 
 int csm_synth3d_create(const csm_synth3d_config* cfg, csm_synth3d** out) {
   if (!cfg || !out || cfg->num_nodes <= 0 || cfg->num_submaps < 0 ||
-      cfg->num_submaps > cfg->num_nodes || cfg->rings <= 0 || cfg->azimuths <= 0)
+      cfg->num_submaps > cfg->num_nodes || cfg->rings <= 0 || cfg->azimuths <= 0 ||
+      cfg->submap_begin < 0 || cfg->submap_count < 0 ||
+      (cfg->submap_count > 0 && cfg->submap_begin + cfg->submap_count > cfg->num_submaps))
     return -1;
   auto* w = new csm_synth3d;
   w->cfg = *cfg;
@@ -384,14 +388,18 @@ int csm_synth3d_create(const csm_synth3d_config* cfg, csm_synth3d** out) {
   // trajectory around it: the scan of node c itself plus scans_per_submap - 1
   // scans from viewpoints within +-1 m and any yaw (half the azimuths), all
   // in the submap frame (origin = centre position, axes = world axes).
-  const int S = cfg->num_submaps;
+  const int S_all = cfg->num_submaps;
+  const int s0 = cfg->submap_count > 0 ? cfg->submap_begin : 0;
+  const int S = cfg->submap_count > 0 ? cfg->submap_count : S_all;
   w->submap_node.resize(S);
   w->high_grid.resize(S);
   w->low_grid.resize(S);
   w->submap_hist.resize(S);
-  for (int s = 0; s < S; ++s) w->submap_node[s] = static_cast<int32_t>((static_cast<int64_t>(s) * N) / std::max(S, 1));
-  std::vector<uint64_t> submap_seeds(S);
-  for (int s = 0; s < S; ++s) submap_seeds[s] = rng();
+  for (int s = 0; s < S; ++s)
+    w->submap_node[s] = static_cast<int32_t>((static_cast<int64_t>(s0 + s) * N) / std::max(S_all, 1));
+  std::vector<uint64_t> all_seeds(S_all), submap_seeds(S);
+  for (int s = 0; s < S_all; ++s) all_seeds[s] = rng();
+  for (int s = 0; s < S; ++s) submap_seeds[s] = all_seeds[s0 + s];
   const std::vector<uint16_t> hit = OddsTable(Odds(0.55f)), miss = OddsTable(Odds(0.49f));
   ParallelFor(S, threads, [&](int s) {
     const int c = w->submap_node[s];

@@ -9,9 +9,10 @@ searches its pairs with no data-path collective. The single exchange is the
 gather of accepted constraints to rank 0, which restores submission order
 (SURVEY.md 8(e)).
 
-Record layout (float64 x 9, one row per accepted constraint):
+Record layout (float64, one row per accepted constraint): 2D (x 9)
 ``submission_index, submap_trajectory, submap_index, node_trajectory,
-node_index, x, y, theta, score``.
+node_index, x, y, theta, score``; 3D (x 13, ConstraintBuilder3D) the same ids,
+then ``tx, ty, tz, qw, qx, qy, qz, score``.
 """
 
 from __future__ import annotations
@@ -23,6 +24,9 @@ import numpy as np
 RECORD_FIELDS = ("submission", "submap_traj", "submap_index", "node_traj", "node_index",
                  "x", "y", "theta", "score")
 RECORD_WIDTH = len(RECORD_FIELDS)
+RECORD3_FIELDS = ("submission", "submap_traj", "submap_index", "node_traj", "node_index",
+                  "tx", "ty", "tz", "qw", "qx", "qy", "qz", "score")
+RECORD3_WIDTH = len(RECORD3_FIELDS)
 
 
 def shard_submaps(num_submaps: int, rank: int, world_size: int,
@@ -55,6 +59,22 @@ def make_records(results: np.ndarray, submission: np.ndarray, submap_ids: np.nda
     return rec
 
 
+def make_records_3d(results: np.ndarray, submission: np.ndarray, submap_ids: np.ndarray,
+                    node_ids: np.ndarray, submap_traj: int = 0, node_traj: int = 0) -> np.ndarray:
+    """Accepted rows of a ``match_batch_3d`` (RESULT3_DTYPE) result as records."""
+    ok = results["status"] == 0
+    rec = np.zeros((int(ok.sum()), RECORD3_WIDTH), np.float64)
+    rec[:, 0] = submission[ok]
+    rec[:, 1] = submap_traj
+    rec[:, 2] = submap_ids[ok]
+    rec[:, 3] = node_traj
+    rec[:, 4] = node_ids[ok]
+    rec[:, 5:8] = results["t"][ok]
+    rec[:, 8:12] = results["q"][ok]
+    rec[:, 12] = results["score"][ok]
+    return rec
+
+
 def gather_records(rec: np.ndarray, dist=None, rank: int = 0, world_size: int = 1,
                    device=None) -> Optional[np.ndarray]:
     """Gathers every rank's records to rank 0, sorted by submission index.
@@ -72,7 +92,7 @@ def gather_records(rec: np.ndarray, dist=None, rank: int = 0, world_size: int = 
     dist.all_gather(cnts, cnt)
     counts = [int(c.item()) for c in cnts]
     mx = max(max(counts), 1)
-    buf = torch.zeros((mx, RECORD_WIDTH), dtype=torch.float64, device=dev)
+    buf = torch.zeros((mx, rec.shape[1]), dtype=torch.float64, device=dev)
     if rec.shape[0]:
         buf[:rec.shape[0]] = torch.from_numpy(np.ascontiguousarray(rec)).to(dev)
     bufs = [torch.zeros_like(buf) for _ in range(world_size)] if rank == 0 else None

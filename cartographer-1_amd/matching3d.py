@@ -280,14 +280,18 @@ class SynthConfig3D(C.Structure):
                 ("high_max_range", C.c_double), ("high_min_points", C.c_int32),
                 ("low_min_points", C.c_int32), ("low_max_range", C.c_double),
                 ("histogram_size", C.c_int32),
-                ("insert_voxel", C.c_double), ("threads", C.c_int32)]
+                ("insert_voxel", C.c_double), ("threads", C.c_int32),
+                ("submap_begin", C.c_int32), ("submap_count", C.c_int32)]
 
 
 class SyntheticWorld3D:
     """Seeded warehouse, 64-ring lidar scans, submaps with high/low-resolution
     grids and rotational histograms."""
 
-    def __init__(self, num_nodes=16, num_submaps=4, **kw):
+    def __init__(self, num_nodes=16, num_submaps=4, submap_range=None, **kw):
+        """submap_range=(begin, count): build only those submaps of the
+        num_submaps-submap world (a rank's shard); they are indexed 0..count-1
+        here, with submap_ids the world indices."""
         from . import SYNTH_PATH
         lib = C.CDLL(SYNTH_PATH)
         lib.csm_synth3d_create.argtypes = [C.POINTER(SynthConfig3D), C.POINTER(C.c_void_p)]
@@ -307,13 +311,17 @@ class SyntheticWorld3D:
         cfg = SynthConfig3D()
         lib.csm_synth3d_default_config(C.byref(cfg))
         cfg.num_nodes, cfg.num_submaps = num_nodes, num_submaps
+        if submap_range is not None:
+            cfg.submap_begin, cfg.submap_count = int(submap_range[0]), int(submap_range[1])
         for k, v in kw.items():
             setattr(cfg, k, v)
         h = C.c_void_p()
         if lib.csm_synth3d_create(C.byref(cfg), C.byref(h)) != 0:
             raise ValueError("invalid synthetic 3D world config")
         try:
-            n, s, hs = num_nodes, num_submaps, cfg.histogram_size
+            n, hs = num_nodes, cfg.histogram_size
+            s = cfg.submap_count if cfg.submap_count > 0 else num_submaps
+            self.submap_ids = np.arange(s) + (cfg.submap_begin if cfg.submap_count > 0 else 0)
             self.node_poses = np.ctypeslib.as_array(lib.csm_synth3d_node_poses(h), (n * 4,)).reshape(-1, 4).copy()
             self.submap_nodes = np.ctypeslib.as_array(lib.csm_synth3d_submap_nodes(h), (max(s, 1),))[:s].copy()
 
@@ -346,7 +354,7 @@ class SyntheticWorld3D:
             lib.csm_synth3d_destroy(h)
         self.high_resolution = cfg.high_resolution
         self.low_resolution = cfg.low_resolution
-        self.num_nodes, self.num_submaps = num_nodes, num_submaps
+        self.num_nodes, self.num_submaps = num_nodes, s
 
     def node(self, i) -> NodeData3D:
         return NodeData3D(self.high[i], self.low[i], self.node_hist[i])

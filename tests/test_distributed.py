@@ -84,3 +84,69 @@ def test_gather_two_ranks_gloo(csm, tmp_path):
     assert np.array_equal(got, want)
     assert np.all(np.diff(got[:, 0]) > 0)
     assert set(got[:, 2].astype(int)) <= set(range(6))
+
+
+# ---------------------------------------------------------------- 3D (C5) --
+def _fake_results_3d(csm, n, seed, accept=0.4):
+    rng = np.random.default_rng(seed)
+    res = np.zeros(n, csm.RESULT3_DTYPE)
+    res["status"] = np.where(rng.random(n) < accept, 0, 1)
+    res["score"] = rng.random(n).astype(np.float32)
+    res["t"] = rng.normal(size=(n, 3))
+    q = rng.normal(size=(n, 4))
+    res["q"] = q / np.linalg.norm(q, axis=1, keepdims=True)
+    return res
+
+
+def _worker3d(rank, world_size, port, out_dir):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world_size)
+    try:
+        csm = load_package()
+        import importlib
+        d = importlib.import_module("cartographer_amd.distributed")
+        nodes, per_rank = 5, 2
+        sub = np.repeat(np.arange(per_rank, dtype=np.int64) + rank * per_rank, nodes)
+        node = np.tile(np.arange(nodes), per_rank)
+        submission = rank * len(sub) + np.arange(len(sub))
+        # Rank 1 accepts nothing: the gather pads and still agrees on width.
+        res = _fake_results_3d(csm, len(sub), seed=rank, accept=0.5 if rank == 0 else 0.0)
+        got = d.gather_records(d.make_records_3d(res, submission, sub, node), dist, rank,
+                               world_size)
+        if rank == 0:
+            np.save(os.path.join(out_dir, "gathered3d.npy"), got)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gather_3d_two_ranks_gloo(csm, tmp_path):
+    import torch.multiprocessing as mp
+    mp.spawn(_worker3d, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    got = np.load(tmp_path / "gathered3d.npy")
+    d = __import__("cartographer_amd.distributed", fromlist=["x"])
+    res = _fake_results_3d(csm, 10, seed=0, accept=0.5)
+    sub = np.repeat(np.arange(2, dtype=np.int64), 5)
+    want = d.make_records_3d(res, np.arange(10), sub, np.tile(np.arange(5), 2))
+    assert got.shape[1] == d.RECORD3_WIDTH == 13
+    assert np.array_equal(got, want)
+    ok = res["status"] == 0
+    assert np.allclose(got[:, 5:8], res["t"][ok]) and np.allclose(got[:, 8:12], res["q"][ok])
+
+
+def test_synthetic_3d_shard_is_the_full_worlds_submaps(csm):
+    """bench.py's C5 sharding: a rank building submaps [b, b + k) of the world
+    gets exactly those submaps (grids, histograms, centre nodes) and the same
+    nodes as a rank building the whole world."""
+    kw = dict(num_nodes=8, num_submaps=4, seed=11, scans_per_submap=3, azimuths=240)
+    full = csm.SyntheticWorld3D(**kw)
+    part = csm.SyntheticWorld3D(submap_range=(2, 2), **kw)
+    assert part.num_submaps == 2 and list(part.submap_ids) == [2, 3]
+    assert np.array_equal(part.submap_nodes, full.submap_nodes[2:4])
+    for j in range(2):
+        for a, b in ((full.high_cells[2 + j], part.high_cells[j]),
+                     (full.low_cells[2 + j], part.low_cells[j])):
+            assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+        assert np.array_equal(full.submap_hist[2 + j], part.submap_hist[j])
+    for i in range(8):
+        assert np.array_equal(full.high[i], part.high[i])
