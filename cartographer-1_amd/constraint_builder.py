@@ -31,9 +31,10 @@ from typing import Callable, Dict, List, Optional, Tuple
 
 import numpy as np
 
-from . import (CSM_OK, Context, FastCorrelativeScanMatcher2D,
-               FastCorrelativeScanMatcherOptions2D, ProbabilityGrid, ScanSet, _f32_points,
-               default_context, make_pairs, match_batch)
+from . import (CSM_OK, Context, FastCorrelativeScanMatcher2D, FastCorrelativeScanMatcher3D,
+               FastCorrelativeScanMatcherOptions2D, FastCorrelativeScanMatcherOptions3D,
+               HybridGrid, NodeData3D, ProbabilityGrid, ScanSet, _f32_points, default_context,
+               make_pairs, make_pairs_3d, match_batch, match_batch_3d)
 
 
 def rigid2d_compose(a, b):
@@ -86,6 +87,8 @@ class ConstraintBuilderOptions:
     loop_closure_rotation_weight: float = 1e5
     fast_correlative_scan_matcher_options: FastCorrelativeScanMatcherOptions2D = field(
         default_factory=FastCorrelativeScanMatcherOptions2D)
+    fast_correlative_scan_matcher_options_3d: FastCorrelativeScanMatcherOptions3D = field(
+        default_factory=FastCorrelativeScanMatcherOptions3D)
     flush_pairs: int = 0  # 0: search each node's pairs when the node ends
 
 
@@ -226,4 +229,188 @@ class ConstraintBuilder2D:
                     translation_weight=self.options.loop_closure_translation_weight,
                     rotation_weight=self.options.loop_closure_rotation_weight,
                     score=score)
+        self._finished_nodes = self._started_nodes
+
+
+# ---------------------------------------------------------------------------
+# ConstraintBuilder3D (reference constraint_builder_3d.cc; C++ mirror
+# include/cartographer_amd/constraint_builder_3d.h).
+#
+# * MaybeAddConstraint (:79-114): drop pairs whose global translations are
+#   farther apart than max_constraint_distance, then the per-submap
+#   FixedRatioSampler; FastCorrelativeScanMatcher3D::Match(global_node_pose,
+#   global_submap_pose, data, min_score) (:239-241).
+# * MaybeAddGlobalConstraint (:116-142): MatchFullSubmap(node rotation,
+#   submap rotation, data, global_localization_min_score) (:221-223).
+# * NotifyEndOfNode / WhenDone / GetNumFinishedNodes / DeleteScanMatcher
+#   (:144-168, :307-349); metrics (:46-59) as counters and score lists.
+# * Constraint pose: the CSM estimate (submap <- node). The Ceres refinement
+#   (:264-275) is outside the hot path.
+# ---------------------------------------------------------------------------
+
+@dataclass
+class Submap3D:
+    """What the builder reads of a Submap3D (submap_3d.h:57-73): the high and
+    low resolution HybridGrids (as (indices, values) cell lists) and the
+    rotational scan-matcher histogram."""
+    high_resolution: float
+    high_cells: Tuple[np.ndarray, np.ndarray]
+    low_resolution: float
+    low_cells: Tuple[np.ndarray, np.ndarray]
+    rotational_scan_matcher_histogram: np.ndarray
+    high_grid_size: int = 0
+    low_grid_size: int = 0
+
+
+@dataclass
+class Constraint3D:
+    """PoseGraphInterface::Constraint (pose_graph_interface.h:36-53), 3D pose
+    ((tx, ty, tz), (qw, qx, qy, qz)), submap <- node."""
+    submap_id: Tuple[int, int]
+    node_id: Tuple[int, int]
+    relative_pose: Tuple[Tuple[float, float, float], Tuple[float, float, float, float]]
+    translation_weight: float
+    rotation_weight: float
+    tag: str = "INTER_SUBMAP"
+    score: float = 0.0
+    rotational_score: float = 0.0
+    low_resolution_score: float = 0.0
+
+
+@dataclass
+class _Pending3D:
+    submap_id: Tuple[int, int]
+    node_id: Tuple[int, int]
+    data: NodeData3D
+    full: bool
+    node_pose: tuple
+    submap_pose: tuple
+    slot: int
+
+
+class ConstraintBuilder3D:
+    def __init__(self, options: ConstraintBuilderOptions, context: Optional[Context] = None):
+        self.options = options
+        self.context = context or default_context()
+        self._matchers: Dict[Tuple[int, int], tuple] = {}
+        self._samplers: Dict[Tuple[int, int], FixedRatioSampler] = {}
+        self._constraints: List[Optional[Constraint3D]] = []
+        self._pending: List[_Pending3D] = []
+        self._started_nodes = 0
+        self._finished_nodes = 0
+        self.constraints_searched = 0
+        self.constraints_found = 0
+        self.global_constraints_searched = 0
+        self.global_constraints_found = 0
+        self.constraint_scores: List[float] = []
+        self.global_constraint_scores: List[float] = []
+        self.rotational_scores: List[float] = []
+        self.low_resolution_scores: List[float] = []
+
+    # -- public interface (constraint_builder_3d.h:55-108) ------------------
+    def MaybeAddConstraint(self, submap_id, submap: Submap3D, node_id, constant_data: NodeData3D,
+                           global_node_pose, global_submap_pose):
+        d = np.asarray(global_node_pose[0], np.float64) - np.asarray(global_submap_pose[0],
+                                                                      np.float64)
+        if float(np.linalg.norm(d)) > self.options.max_constraint_distance:
+            return
+        sampler = self._samplers.setdefault(tuple(submap_id),
+                                            FixedRatioSampler(self.options.sampling_ratio))
+        if not sampler.Pulse():
+            return
+        self._enqueue(submap_id, submap, node_id, constant_data, False,
+                      global_node_pose, global_submap_pose)
+
+    def MaybeAddGlobalConstraint(self, submap_id, submap: Submap3D, node_id,
+                                 constant_data: NodeData3D, global_node_rotation,
+                                 global_submap_rotation):
+        self._enqueue(submap_id, submap, node_id, constant_data, True,
+                      ((0.0, 0.0, 0.0), tuple(global_node_rotation)),
+                      ((0.0, 0.0, 0.0), tuple(global_submap_rotation)))
+
+    def NotifyEndOfNode(self):
+        self._started_nodes += 1
+        if len(self._pending) >= self.options.flush_pairs:
+            self._flush()
+
+    def WhenDone(self, callback: Callable[[List[Constraint3D]], None]):
+        self._flush()
+        result = [c for c in self._constraints if c is not None]
+        self._constraints = []
+        callback(result)
+
+    def GetNumFinishedNodes(self) -> int:
+        return self._finished_nodes
+
+    def DeleteScanMatcher(self, submap_id):
+        entry = self._matchers.pop(tuple(submap_id), None)
+        if entry is not None:
+            for obj in reversed(entry):  # matcher, then its grids
+                obj.close()
+        self._samplers.pop(tuple(submap_id), None)
+
+    @property
+    def num_submap_scan_matchers(self) -> int:  # kNumSubmapScanMatchersMetric
+        return len(self._matchers)
+
+    # -- internals ----------------------------------------------------------
+    def _enqueue(self, submap_id, submap, node_id, data, full, node_pose, submap_pose):
+        key = tuple(submap_id)
+        if key not in self._matchers:  # DispatchScanMatcherConstruction (:170-198)
+            high = HybridGrid(submap.high_resolution, *submap.high_cells,
+                              grid_size=submap.high_grid_size, context=self.context)
+            low = HybridGrid(submap.low_resolution, *submap.low_cells,
+                             grid_size=submap.low_grid_size, context=self.context)
+            m = FastCorrelativeScanMatcher3D(high, low, submap.rotational_scan_matcher_histogram,
+                                             self.options.fast_correlative_scan_matcher_options_3d,
+                                             self.context)
+            self._matchers[key] = (high, low, m)
+        self._constraints.append(None)
+        self._pending.append(_Pending3D(key, tuple(node_id), data, full, node_pose, submap_pose,
+                                        len(self._constraints) - 1))
+
+    def _flush(self):
+        pending, self._pending = self._pending, []
+        if pending:
+            matchers, slot_of, nodes, node_of = [], {}, [], {}
+            for p in pending:
+                if p.submap_id not in slot_of:
+                    slot_of[p.submap_id] = len(matchers)
+                    matchers.append(self._matchers[p.submap_id][2])
+                if id(p.data) not in node_of:  # a node's data uploads once
+                    node_of[id(p.data)] = len(nodes)
+                    nodes.append(p.data)
+            pairs = make_pairs_3d(
+                [slot_of[p.submap_id] for p in pending], [node_of[id(p.data)] for p in pending],
+                [self.options.global_localization_min_score if p.full else self.options.min_score
+                 for p in pending],
+                [p.full for p in pending],
+                node_q=[p.node_pose[1] for p in pending], node_t=[p.node_pose[0] for p in pending],
+                submap_q=[p.submap_pose[1] for p in pending],
+                submap_t=[p.submap_pose[0] for p in pending])
+            results = match_batch_3d(matchers, nodes, pairs, self.context)
+            for p, r in zip(pending, results):
+                if p.full:
+                    self.global_constraints_searched += 1
+                else:
+                    self.constraints_searched += 1
+                if int(r["status"]) != CSM_OK:
+                    continue
+                score = float(r["score"])
+                if p.full:
+                    self.global_constraints_found += 1
+                    self.global_constraint_scores.append(score)
+                else:
+                    self.constraints_found += 1
+                    self.constraint_scores.append(score)
+                self.rotational_scores.append(float(r["rotational_score"]))
+                self.low_resolution_scores.append(float(r["low_resolution_score"]))
+                self._constraints[p.slot] = Constraint3D(
+                    submap_id=p.submap_id, node_id=p.node_id,
+                    relative_pose=(tuple(float(v) for v in r["t"]),
+                                   tuple(float(v) for v in r["q"])),
+                    translation_weight=self.options.loop_closure_translation_weight,
+                    rotation_weight=self.options.loop_closure_rotation_weight,
+                    score=score, rotational_score=float(r["rotational_score"]),
+                    low_resolution_score=float(r["low_resolution_score"]))
         self._finished_nodes = self._started_nodes

@@ -22,39 +22,16 @@
 #include <utility>
 #include <vector>
 
+#include "constraint_builder_common.h"
 #include "scan_matching.h"
 
 namespace cartographer_amd {
-
-struct SubmapId {
-  int trajectory_id = 0, submap_index = 0;
-  bool operator<(const SubmapId& o) const {
-    return trajectory_id != o.trajectory_id ? trajectory_id < o.trajectory_id
-                                            : submap_index < o.submap_index;
-  }
-};
-struct NodeId {
-  int trajectory_id = 0, node_index = 0;
-};
 
 // What the builder reads of a Submap2D: its grid and ComputeSubmapPose(),
 // i.e. Project2D(submap.local_pose()) (constraint_builder_2d.cc:55-57).
 struct Submap2DView {
   Grid2DView grid;
   Rigid2d local_pose;
-};
-
-// proto::ConstraintBuilderOptions (constraint_builder_options.proto:24-59),
-// defaults from configuration_files/pose_graph.lua:17-29.
-struct ConstraintBuilderOptions {
-  double sampling_ratio = 0.3;
-  double max_constraint_distance = 15.;
-  float min_score = 0.55f;
-  float global_localization_min_score = 0.6f;
-  double loop_closure_translation_weight = 1.1e4;
-  double loop_closure_rotation_weight = 1e5;
-  FastCorrelativeScanMatcherOptions2D fast_correlative_scan_matcher_options;
-  int flush_pairs = 0;  // 0: search each node's pairs when the node ends
 };
 
 // PoseGraphInterface::Constraint (pose_graph_interface.h:36-53), 2D pose.
@@ -65,24 +42,6 @@ struct Constraint {
   double translation_weight = 0., rotation_weight = 0.;
   enum Tag { INTRA_SUBMAP, INTER_SUBMAP } tag = INTER_SUBMAP;
   float score = 0.f;
-};
-
-// common/fixed_ratio_sampler.cc:32-39
-class FixedRatioSampler {
- public:
-  explicit FixedRatioSampler(double ratio) : ratio_(ratio) {}
-  bool Pulse() {
-    ++num_pulses_;
-    if (static_cast<double>(num_samples_) / num_pulses_ < ratio_) {
-      ++num_samples_;
-      return true;
-    }
-    return false;
-  }
-
- private:
-  double ratio_;
-  int64_t num_pulses_ = 0, num_samples_ = 0;
 };
 
 inline Rigid2d Compose(const Rigid2d& a, const Rigid2d& b) {

@@ -1,0 +1,215 @@
+// ConstraintBuilder3D drop-in over the batched 3D C-ABI.
+//
+// Mirrors mapping/internal/constraints/constraint_builder_3d.{h,cc}: the
+// public methods; MaybeAddConstraint's distance filter on the global
+// translations and its per-submap FixedRatioSampler (:79-114);
+// MaybeAddGlobalConstraint with the poses reduced to their rotations
+// (:116-142); NotifyEndOfNode (:144-156); WhenDone (:158-168) with results in
+// submission order and failed searches dropped (RunWhenDoneCallback
+// :307-333); GetNumFinishedNodes (:335-338); DeleteScanMatcher (:340-349); the
+// per-submap matcher cache (DispatchScanMatcherConstruction :170-198, which
+// reads the submap's high/low-resolution grids and rotational histogram); and
+// the metrics (:46-59, counters and score lists). Pending pairs are searched
+// as one GPU batch when a node ends (or once `flush_pairs` are pending)
+// instead of one Task per pair. The Ceres refinement (:264-275) is outside
+// this drop-in (DESIGN.md "Out of scope"): a constraint's pose is the CSM
+// estimate (submap <- node), which the reference passes to Ceres as its
+// initial and previous pose.
+#ifndef CARTOGRAPHER_AMD_CONSTRAINT_BUILDER_3D_H_
+#define CARTOGRAPHER_AMD_CONSTRAINT_BUILDER_3D_H_
+
+#include <cmath>
+#include <functional>
+#include <map>
+#include <memory>
+#include <utility>
+#include <vector>
+
+#include "constraint_builder_common.h"
+#include "scan_matching_3d.h"
+
+namespace cartographer_amd {
+
+// What the builder reads of a Submap3D (submap_3d.h:57-73).
+struct Submap3DView {
+  HybridGridView high_resolution_hybrid_grid;
+  HybridGridView low_resolution_hybrid_grid;
+  std::vector<float> rotational_scan_matcher_histogram;
+};
+
+// PoseGraphInterface::Constraint (pose_graph_interface.h:36-53).
+struct Constraint3D {
+  SubmapId submap_id;
+  NodeId node_id;
+  Rigid3d relative_pose;  // zbar_ij: submap <- node
+  double translation_weight = 0., rotation_weight = 0.;
+  enum Tag { INTRA_SUBMAP, INTER_SUBMAP } tag = INTER_SUBMAP;
+  float score = 0.f, rotational_score = 0.f, low_resolution_score = 0.f;
+};
+
+class ConstraintBuilder3D {
+ public:
+  using Result = std::vector<Constraint3D>;
+
+  explicit ConstraintBuilder3D(const ConstraintBuilderOptions& options,
+                               csm_context* context = nullptr)
+      : options_(options), context_(context ? context : ThreadContext()) {}
+
+  void MaybeAddConstraint(const SubmapId& submap_id, const Submap3DView* submap,
+                          const NodeId& node_id, const TrajectoryNodeData3D* constant_data,
+                          const Rigid3d& global_node_pose, const Rigid3d& global_submap_pose) {
+    const double dx = global_node_pose.t[0] - global_submap_pose.t[0],
+                 dy = global_node_pose.t[1] - global_submap_pose.t[1],
+                 dz = global_node_pose.t[2] - global_submap_pose.t[2];
+    if (std::sqrt(dx * dx + dy * dy + dz * dz) > options_.max_constraint_distance) return;
+    auto it = samplers_.emplace(submap_id, FixedRatioSampler(options_.sampling_ratio)).first;
+    if (!it->second.Pulse()) return;
+    Enqueue(submap_id, submap, node_id, constant_data, false, global_node_pose,
+            global_submap_pose);
+  }
+
+  void MaybeAddGlobalConstraint(const SubmapId& submap_id, const Submap3DView* submap,
+                                const NodeId& node_id, const TrajectoryNodeData3D* constant_data,
+                                const Quaterniond& global_node_rotation,
+                                const Quaterniond& global_submap_rotation) {
+    Enqueue(submap_id, submap, node_id, constant_data, true,
+            Rigid3d::Rotation(global_node_rotation), Rigid3d::Rotation(global_submap_rotation));
+  }
+
+  void NotifyEndOfNode() {
+    ++num_started_nodes_;
+    if (static_cast<int>(pending_.size()) >= options_.flush_pairs) Flush();
+  }
+
+  void WhenDone(const std::function<void(const Result&)>& callback) {
+    Flush();
+    Result result;
+    for (auto& c : constraints_)
+      if (c) result.push_back(*c);
+    constraints_.clear();
+    callback(result);
+  }
+
+  int GetNumFinishedNodes() const { return num_finished_nodes_; }
+
+  void DeleteScanMatcher(const SubmapId& submap_id) {
+    matchers_.erase(submap_id);
+    samplers_.erase(submap_id);
+  }
+
+  // Metrics (constraint_builder_3d.cc:46-59).
+  int64_t constraints_searched = 0, constraints_found = 0;
+  int64_t global_constraints_searched = 0, global_constraints_found = 0;
+  std::vector<float> constraint_scores, global_constraint_scores;
+  std::vector<float> rotational_scores, low_resolution_scores;
+  int num_submap_scan_matchers() const { return static_cast<int>(matchers_.size()); }
+
+ private:
+  // SubmapScanMatcher (constraint_builder_3d.h:117-123): device grids and the
+  // matcher built from them.
+  struct SubmapScanMatcher {
+    std::unique_ptr<HybridGrid3D> high, low;
+    std::unique_ptr<FastCorrelativeScanMatcher3D> matcher;
+  };
+
+  struct Pending {
+    SubmapId submap_id;
+    NodeId node_id;
+    const TrajectoryNodeData3D* data;
+    bool full;
+    Rigid3d node_pose, submap_pose;
+    size_t slot;
+  };
+
+  void Enqueue(const SubmapId& submap_id, const Submap3DView* submap, const NodeId& node_id,
+               const TrajectoryNodeData3D* data, bool full, const Rigid3d& node_pose,
+               const Rigid3d& submap_pose) {
+    if (!matchers_.count(submap_id)) {  // DispatchScanMatcherConstruction
+      auto m = std::make_shared<SubmapScanMatcher>();
+      m->high.reset(new HybridGrid3D(submap->high_resolution_hybrid_grid, context_));
+      m->low.reset(new HybridGrid3D(submap->low_resolution_hybrid_grid, context_));
+      m->matcher.reset(new FastCorrelativeScanMatcher3D(
+          *m->high, m->low.get(), &submap->rotational_scan_matcher_histogram,
+          options_.fast_correlative_scan_matcher_options_3d, context_));
+      matchers_.emplace(submap_id, std::move(m));
+    }
+    constraints_.emplace_back();
+    pending_.push_back(Pending{submap_id, node_id, data, full, node_pose, submap_pose,
+                               constraints_.size() - 1});
+  }
+
+  void Flush() {
+    if (pending_.empty()) {
+      num_finished_nodes_ = num_started_nodes_;
+      return;
+    }
+    std::vector<csm_fast3d*> handles;
+    std::vector<std::shared_ptr<SubmapScanMatcher>> keep;
+    std::map<SubmapId, int> slot_of;
+    std::map<const TrajectoryNodeData3D*, int32_t> node_of;  // a node's data uploads once
+    std::vector<csm_node3d> nodes;
+    std::vector<csm_pair3d> pairs;
+    for (const Pending& p : pending_) {
+      auto s = slot_of.find(p.submap_id);
+      if (s == slot_of.end()) {
+        s = slot_of.emplace(p.submap_id, static_cast<int>(handles.size())).first;
+        auto m = matchers_.at(p.submap_id);
+        handles.push_back(m->matcher->handle());
+        keep.push_back(m);
+      }
+      auto n = node_of.find(p.data);
+      if (n == node_of.end()) {
+        n = node_of.emplace(p.data, static_cast<int32_t>(nodes.size())).first;
+        nodes.push_back(p.data->ToC());
+      }
+      csm_pair3d q{};
+      q.submap = s->second;
+      q.node = n->second;
+      q.full_submap = p.full ? 1 : 0;
+      q.min_score = p.full ? options_.global_localization_min_score : options_.min_score;
+      q.node_pose = p.node_pose.ToC();
+      q.submap_pose = p.submap_pose.ToC();
+      pairs.push_back(q);
+    }
+    std::vector<csm_result3d> results(pairs.size());
+    CheckOk(csm_fast3d_match_batch(context_, handles.data(), static_cast<int32_t>(handles.size()),
+                                   nodes.data(), static_cast<int32_t>(nodes.size()), pairs.data(),
+                                   static_cast<int64_t>(pairs.size()), results.data()),
+            "csm_fast3d_match_batch");
+    for (size_t i = 0; i < pending_.size(); ++i) {
+      const Pending& p = pending_[i];
+      (p.full ? global_constraints_searched : constraints_searched) += 1;
+      CheckOk(results[i].status, "ComputeConstraint");
+      if (results[i].status != CSM_OK) continue;
+      (p.full ? global_constraints_found : constraints_found) += 1;
+      (p.full ? global_constraint_scores : constraint_scores).push_back(results[i].score);
+      rotational_scores.push_back(results[i].rotational_score);
+      low_resolution_scores.push_back(results[i].low_resolution_score);
+      Constraint3D c;
+      c.submap_id = p.submap_id;
+      c.node_id = p.node_id;
+      c.relative_pose = Rigid3d::FromC(results[i].pose);
+      c.translation_weight = options_.loop_closure_translation_weight;
+      c.rotation_weight = options_.loop_closure_rotation_weight;
+      c.tag = Constraint3D::INTER_SUBMAP;
+      c.score = results[i].score;
+      c.rotational_score = results[i].rotational_score;
+      c.low_resolution_score = results[i].low_resolution_score;
+      constraints_[p.slot].reset(new Constraint3D(c));
+    }
+    pending_.clear();
+    num_finished_nodes_ = num_started_nodes_;
+  }
+
+  ConstraintBuilderOptions options_;
+  csm_context* context_;
+  std::map<SubmapId, std::shared_ptr<SubmapScanMatcher>> matchers_;
+  std::map<SubmapId, FixedRatioSampler> samplers_;
+  std::vector<std::unique_ptr<Constraint3D>> constraints_;
+  std::vector<Pending> pending_;
+  int num_started_nodes_ = 0, num_finished_nodes_ = 0;
+};
+
+}  // namespace cartographer_amd
+
+#endif  // CARTOGRAPHER_AMD_CONSTRAINT_BUILDER_3D_H_

@@ -1,0 +1,147 @@
+// C++ restatement of ConstraintBuilder3DTest (reference
+// mapping/internal/constraints/constraint_builder_3d_test.cc:40-120) against
+// the drop-in headers, plus a located match on a small occupied submap.
+// Exits 0 when every check holds. Compiled by tests/test_constraint_builder_3d.py
+// (CPU) and run there on the GPU.
+#include <cmath>
+#include <cstdio>
+#include <vector>
+
+#include "cartographer_amd/constraint_builder_3d.h"
+
+using namespace cartographer_amd;
+
+static int failures = 0;
+#define EXPECT(cond)                                                          \
+  do {                                                                        \
+    if (!(cond)) {                                                            \
+      std::fprintf(stderr, "%s:%d: EXPECT(%s)\n", __FILE__, __LINE__, #cond); \
+      ++failures;                                                             \
+    }                                                                         \
+  } while (0)
+
+// constraint_builder_3d_test.cc:42-52: pose_graph.lua with sampling_ratio 1
+// and every score threshold 0.
+static ConstraintBuilderOptions TestOptions() {
+  ConstraintBuilderOptions o;
+  o.sampling_ratio = 1;
+  o.min_score = 0;
+  o.global_localization_min_score = 0;
+  o.fast_correlative_scan_matcher_options_3d.min_low_resolution_score = 0;
+  o.fast_correlative_scan_matcher_options_3d.min_rotational_score = 0;
+  return o;
+}
+
+static void CallsBack() {  // :61-71
+  ConstraintBuilder3D builder(TestOptions());
+  EXPECT(builder.GetNumFinishedNodes() == 0);
+  builder.NotifyEndOfNode();
+  size_t n = 99;
+  builder.WhenDone([&](const ConstraintBuilder3D::Result& r) { n = r.size(); });
+  EXPECT(n == 0);
+  EXPECT(builder.GetNumFinishedNodes() == 1);
+}
+
+static void FindsConstraints() {  // :73-116
+  TrajectoryNodeData3D node;
+  node.high_resolution_point_cloud.push_back(0.1f, 0.2f, 0.3f);
+  node.low_resolution_point_cloud.push_back(0.1f, 0.2f, 0.3f);
+  node.rotational_scan_matcher_histogram.assign(3, 0.f);
+  Submap3DView submap;  // Submap3D(0.1, 0.1, Identity, Zero(3)): empty grids
+  submap.high_resolution_hybrid_grid.resolution = 0.1f;
+  submap.low_resolution_hybrid_grid.resolution = 0.1f;
+  submap.rotational_scan_matcher_histogram.assign(3, 0.f);
+  const SubmapId submap_id{0, 1};
+  ConstraintBuilder3D builder(TestOptions());
+  int expected_nodes = 0;
+  for (int i = 0; i < 2; ++i) {
+    EXPECT(builder.GetNumFinishedNodes() == expected_nodes);
+    for (int j = 0; j < 2; ++j)
+      builder.MaybeAddConstraint(submap_id, &submap, NodeId{0, 0}, &node, Rigid3d::Identity(),
+                                 Rigid3d::Identity());
+    builder.MaybeAddGlobalConstraint(submap_id, &submap, NodeId{0, 0}, &node,
+                                     Quaterniond::Identity(), Quaterniond::Identity());
+    builder.NotifyEndOfNode();
+    EXPECT(builder.GetNumFinishedNodes() == ++expected_nodes);
+    builder.NotifyEndOfNode();
+    EXPECT(builder.GetNumFinishedNodes() == ++expected_nodes);
+    size_t n = 0, inter = 0;
+    builder.WhenDone([&](const ConstraintBuilder3D::Result& r) {
+      n = r.size();
+      for (const Constraint3D& c : r) inter += c.tag == Constraint3D::INTER_SUBMAP;
+    });
+    EXPECT(n == 3);
+    EXPECT(inter == 3);
+    builder.DeleteScanMatcher(submap_id);
+    EXPECT(builder.num_submap_scan_matchers() == 0);
+  }
+  EXPECT(builder.constraints_searched == 4 && builder.constraints_found == 4);
+  EXPECT(builder.global_constraints_searched == 2 && builder.global_constraints_found == 2);
+}
+
+// Three walls of occupied voxels; the node sees them shifted by (-0.3, +0.2):
+// the local search recovers the shift within one voxel, and the distance
+// filter drops pairs farther than max_constraint_distance.
+static void LocatesShiftedWall() {
+  Submap3DView submap;
+  for (HybridGridView* g : {&submap.high_resolution_hybrid_grid, &submap.low_resolution_hybrid_grid}) {
+    g->resolution = 0.1f;
+    for (int y = -20; y <= 20; ++y)
+      for (int z = -5; z <= 5; ++z)
+        for (int x : {15, -15}) {
+          g->xyz.insert(g->xyz.end(), {x, y, z});
+          g->values.push_back(32767);  // probability 0.9 (kMaxProbability)
+        }
+    for (int x = -14; x <= 14; ++x)
+      for (int z = -5; z <= 5; ++z) {
+        g->xyz.insert(g->xyz.end(), {x, 20, z});
+        g->values.push_back(32767);
+      }
+  }
+  submap.rotational_scan_matcher_histogram.assign(3, 0.f);
+  TrajectoryNodeData3D node;
+  // Side walls (fix x), the back wall (fixes y), the full wall height (fixes z).
+  for (int z = -5; z <= 5; ++z) {
+    for (int y = -15; y <= 15; y += 3) {
+      node.high_resolution_point_cloud.push_back(1.5f - 0.3f, 0.1f * y + 0.2f, 0.1f * z);
+      node.high_resolution_point_cloud.push_back(-1.5f - 0.3f, 0.1f * y + 0.2f, 0.1f * z);
+    }
+    for (int x = -10; x <= 10; x += 4)
+      node.high_resolution_point_cloud.push_back(0.1f * x - 0.3f, 2.0f + 0.2f, 0.1f * z);
+  }
+  node.low_resolution_point_cloud = node.high_resolution_point_cloud;
+  node.rotational_scan_matcher_histogram.assign(3, 0.f);
+  ConstraintBuilderOptions o = TestOptions();
+  o.min_score = 0.5f;
+  o.fast_correlative_scan_matcher_options_3d.linear_xy_search_window = 0.6;
+  o.fast_correlative_scan_matcher_options_3d.linear_z_search_window = 0.2;
+  o.fast_correlative_scan_matcher_options_3d.angular_search_window = 0.05;
+  ConstraintBuilder3D builder(o);
+  builder.MaybeAddConstraint(SubmapId{0, 0}, &submap, NodeId{0, 7}, &node, Rigid3d::Identity(),
+                             Rigid3d::Identity());
+  Rigid3d far = Rigid3d::Identity();
+  far.t[0] = 100.;
+  builder.MaybeAddConstraint(SubmapId{0, 0}, &submap, NodeId{0, 8}, &node, far,
+                             Rigid3d::Identity());
+  builder.NotifyEndOfNode();
+  std::vector<Constraint3D> got;
+  builder.WhenDone([&](const ConstraintBuilder3D::Result& r) { got = r; });
+  EXPECT(got.size() == 1);
+  if (got.size() == 1) {
+    EXPECT(got[0].node_id.node_index == 7);
+    EXPECT(std::fabs(got[0].relative_pose.t[0] - 0.3) < 0.1 + 1e-6);
+    EXPECT(std::fabs(got[0].relative_pose.t[1] + 0.2) < 0.1 + 1e-6);
+    EXPECT(got[0].score > 0.5f);
+    EXPECT(got[0].translation_weight == o.loop_closure_translation_weight);
+  }
+  EXPECT(builder.constraints_searched == 1);
+}
+
+int main() {
+  CallsBack();
+  FindsConstraints();
+  LocatesShiftedWall();
+  if (failures) return 1;
+  std::printf("OK\n");
+  return 0;
+}
