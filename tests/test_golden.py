@@ -127,3 +127,125 @@ def test_gpu_matches_rt2d_golden(csm):
         # glibc in the last ulps: 1e-6 relative (north star: 1e-4).
         assert math.isclose(sc, d["score"][i], rel_tol=1e-6, abs_tol=0), (i, sc, d["score"][i])
         assert tuple(pose) == tuple(d["pose"][i])
+
+
+# ------------------------------------------------------------------ 3D (C4/C5) --
+def _cells3(d, kind, s):
+    o = d[kind + "_off"]
+    return d[kind + "_idx"][o[s]:o[s + 1]], d[kind + "_val"][o[s]:o[s + 1]]
+
+
+def _node3(csm_or_none, d, n):
+    from types import SimpleNamespace
+    hi = d["high_points"][d["high_offsets"][n]:d["high_offsets"][n + 1]]
+    lo = d["low_points"][d["low_offsets"][n]:d["low_offsets"][n + 1]]
+    if csm_or_none is None:
+        return SimpleNamespace(high_resolution_point_cloud=hi, low_resolution_point_cloud=lo,
+                               rotational_scan_matcher_histogram=d["node_hist"][n],
+                               gravity_alignment=(1.0, 0.0, 0.0, 0.0))
+    return csm_or_none.NodeData3D(hi, lo, d["node_hist"][n])
+
+
+def _pair3(row):
+    s, n, full, ms = int(row[0]), int(row[1]), bool(row[2]), float(row[3])
+    return s, n, full, ms, (tuple(row[4:7]), tuple(row[7:11])), (tuple(row[11:14]), tuple(row[14:18]))
+
+
+def _oracle3(oracle, d):
+    oms = []
+    for s in range(len(d["submap_hist"])):
+        oh, ol = oracle.hybrid_grid(float(d["high_resolution"])), oracle.hybrid_grid(float(d["low_resolution"]))
+        oh.set_values(*_cells3(d, "high", s))
+        ol.set_values(*_cells3(d, "low", s))
+        oms.append((oh, ol, oracle.fast3d(oh, ol, d["submap_hist"][s],
+                                          tuple(float(v) if i >= 2 else int(v)
+                                                for i, v in enumerate(d["options"])))))
+    return oms
+
+
+def test_oracle_reproduces_fast3d_golden(oracle):
+    d = _load("fast3d_c5.npz")
+    oms = _oracle3(oracle, d)
+    for i, row in enumerate(d["pairs"]):
+        s, n, full, ms, npose, spose = _pair3(row)
+        node = _node3(None, d, n)
+        om = oms[s][2]
+        r = om.match_full_submap(npose[1], spose[1], node, ms) if full else om.match(npose, spose, node, ms)
+        assert int(r["matched"]) == d["matched"][i], i
+        assert r["lookups"] == d["reference_lookups"][i]
+        if r["matched"]:
+            assert np.float32(r["score"]) == d["score"][i]
+            assert r["pose"] == (tuple(d["t"][i]), tuple(d["q"][i]))
+            assert np.float32(r["rotational_score"]) == d["rotational_score"][i]
+            assert np.float32(r["low_resolution_score"]) == d["low_resolution_score"][i]
+
+
+def test_oracle_reproduces_rt3d_golden(oracle):
+    d = _load("rt3d_c4.npz")
+    f = _load("fast3d_c5.npz")
+    grids = {}
+    for i in range(len(d["score"])):
+        s = int(d["grid"][i])
+        if s not in grids:
+            grids[s] = oracle.hybrid_grid(float(f["high_resolution"]))
+            grids[s].set_values(*_cells3(f, "high", s))
+        init = (tuple(d["initial"][i][:3]), tuple(d["initial"][i][3:]))
+        sc, pose, idx, ncand = oracle.rt3d_match(grids[s], tuple(d["options"]), init, _cloud(d, i))
+        assert np.float32(sc) == d["score"][i]
+        assert (tuple(pose[0]), tuple(pose[1])) == (tuple(d["pose"][i][:3]), tuple(d["pose"][i][3:]))
+        assert (idx, ncand) == (d["candidate"][i], d["candidates"][i])
+
+
+@pytest.mark.gpu
+def test_gpu_matches_fast3d_golden(csm, oracle):
+    from test_fast3d_gpu import assert_same_result
+    d = _load("fast3d_c5.npz")
+    o = csm.FastCorrelativeScanMatcherOptions3D(*[int(v) if i < 2 else float(v)
+                                                   for i, v in enumerate(d["options"])])
+    grids, mats = [], []
+    for s in range(len(d["submap_hist"])):
+        gh = csm.HybridGrid(float(d["high_resolution"]), *_cells3(d, "high", s))
+        gl = csm.HybridGrid(float(d["low_resolution"]), *_cells3(d, "low", s))
+        grids.append((gh, gl))
+        mats.append(csm.FastCorrelativeScanMatcher3D(gh, gl, d["submap_hist"][s], o))
+    nodes = [_node3(csm, d, n) for n in range(len(d["node_hist"]))]
+    rows = [_pair3(r) for r in d["pairs"]]
+    res = csm.match_batch_3d(mats, nodes, [(s, n, full, ms, npose, spose)
+                                           for s, n, full, ms, npose, spose in rows])
+    oms = None
+    for i, (s, n, full, ms, npose, spose) in enumerate(rows):
+        single = (mats[s].MatchFullSubmap(npose[1], spose[1], nodes[n], ms) if full
+                  else mats[s].Match(npose, spose, nodes[n], ms))
+        assert (single is not None) == bool(d["matched"][i]) == (res[i].status == csm.CSM_OK), i
+        if single is None:
+            continue
+        assert np.float32(single.score) == d["score"][i] == np.float32(res[i].score)
+        assert single.pose_estimate == res[i].pose.as_tuple()  # batch == single call
+        ref = {"matched": True, "score": float(d["score"][i]),
+               "pose": (tuple(d["t"][i]), tuple(d["q"][i])),
+               "rotational_score": float(d["rotational_score"][i]),
+               "low_resolution_score": float(d["low_resolution_score"][i])}
+        if single.pose_estimate != ref["pose"] and oms is None:
+            oms = _oracle3(oracle, d)
+        assert_same_result(single, ref, oms[s][2] if oms else None, full,
+                           npose[1] if full else npose, spose[1] if full else spose,
+                           _node3(None, d, n), o.min_low_resolution_score)
+
+
+@pytest.mark.gpu
+def test_gpu_matches_rt3d_golden(csm):
+    d = _load("rt3d_c4.npz")
+    f = _load("fast3d_c5.npz")
+    m = csm.RealTimeCorrelativeScanMatcher3D(
+        csm.RealTimeCorrelativeScanMatcherOptions(*[float(v) for v in d["options"]]))
+    grids = {}
+    for i in range(len(d["score"])):
+        s = int(d["grid"][i])
+        if s not in grids:
+            grids[s] = csm.HybridGrid(float(f["high_resolution"]), *_cells3(f, "high", s))
+        init = (tuple(d["initial"][i][:3]), tuple(d["initial"][i][3:]))
+        score, pose = m.Match(init, _cloud(d, i), grids[s])
+        # float sums in reference order; the double exp() penalty may differ
+        # from glibc in the last ulps: 1e-6 relative (north star: 1e-4).
+        assert math.isclose(score, float(d["score"][i]), rel_tol=1e-6), (i, score)
+        assert pose == (tuple(d["pose"][i][:3]), tuple(d["pose"][i][3:]))
