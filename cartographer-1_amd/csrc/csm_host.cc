@@ -32,7 +32,7 @@ namespace csm {
 
 namespace {
 
-constexpr int kStatsWords = 2 + 2 * kMaxLevels;
+constexpr int kStatsWords = 2 + 2 * kMaxLevels + 4;  // + CSM_KPROF phase cycles
 
 int AutoSearchDepth(int configured, int nx, int ny) {
   // Extra coarse levels until the top lattice step reaches ~1/2 of the grid:
@@ -303,6 +303,12 @@ int RunBatch(csm_context* ctx, csm_fast2d* const* submaps, int32_t num_submaps,
       ctx->level_cands[l] += static_cast<double>(stats_host[2 + l]);
       ctx->level_batches[l] += static_cast<double>(stats_host[2 + kMaxLevels + l]);
     }
+    const unsigned long long* kp = stats_host + 2 + 2 * kMaxLevels;
+    if (std::getenv("CSM_PROFILE2D") && (kp[0] | kp[1] | kp[2]))
+      std::fprintf(stderr,
+                   "fast2d phases (Mcycles, thread 0 sums): discretize+shrink %.1f control %.1f "
+                   "score %.1f | batches %llu\n",
+                   kp[0] / 1e6, kp[1] / 1e6, kp[2] / 1e6, kp[3]);
   }
 
   // ---- decode -----------------------------------------------------------------

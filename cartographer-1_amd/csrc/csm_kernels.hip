@@ -695,6 +695,9 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int rc = queues.rot_chunk;
   unsigned long long local_cands = 0, local_lookups = 0;
+#ifdef CSM_KPROF
+  long long kprof[4] = {0, 0, 0, 0};  // thread 0: discretize, control, score cycles; batches
+#endif
   if (tid == 0) sh.queue = blockIdx.x % kNumXcd;
   if (tid < kMaxLevels) { sh.lv_cands[tid] = 0; sh.lv_batches[tid] = 0; }
   int tries = 0;
@@ -734,6 +737,9 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
     const int step = 1 << top_level;
 
     // ---- K2: discretize the chunk's rotated scans into LDS ----------------
+#ifdef CSM_KPROF
+    long long t_mark = clock64();
+#endif
     if (tid < kMaxRotChunk * 4) sh.mm[tid >> 2][tid & 3] = (tid & 1) ? -0x7fffffff : 0x7fffffff;
     if (tid == 0) sh.range_error = 0;
     __syncthreads();
@@ -795,6 +801,13 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
     }
     __syncthreads();
     const int vtotal = Uniform(sh.root_prefix[nrot]);
+#ifdef CSM_KPROF
+    if (tid == 0) {
+      const long long now = clock64();
+      kprof[0] += now - t_mark;
+      t_mark = now;
+    }
+#endif
 
     // ---- K3/K4: batched best-first DFS over the chunk -----------------------
     for (;;) {
@@ -925,6 +938,14 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
         }
       }
       __syncthreads();
+#ifdef CSM_KPROF
+      if (tid == 0) {
+        const long long now = clock64();
+        kprof[1] += now - t_mark;
+        t_mark = now;
+        kprof[3] += 1;
+      }
+#endif
       const int nodes = Uniform(sh.nodes);
       const int done = Uniform(sh.done);
       if (done) break;
@@ -939,11 +960,21 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
         }
       }
       __syncthreads();
+#ifdef CSM_KPROF
+      if (tid == 0) {
+        const long long now = clock64();
+        kprof[2] += now - t_mark;
+        t_mark = now;
+      }
+#endif
     }
   }
   if (stats && tid == 0) {
     atomicAdd(&stats[0], local_cands);
     atomicAdd(&stats[1], local_lookups);
+#ifdef CSM_KPROF
+    for (int k = 0; k < 4; ++k) atomicAdd(&stats[2 + 2 * kMaxLevels + k], static_cast<unsigned long long>(kprof[k]));
+#endif
   }
   if (stats && tid < kMaxLevels) {
     atomicAdd(&stats[2 + tid], sh.lv_cands[tid]);
