@@ -85,8 +85,8 @@ struct WorkQueues2 {
   int32_t rot_chunk;
 };
 
-constexpr int kStack2 = 1024;   // v2 per-workgroup DFS stack entries
-constexpr int kBatchNodes = 16; // nodes expanded per batch (64 children)
+constexpr int kStack2 = 2048;   // v2 per-workgroup DFS stack entries
+constexpr int kBatchNodes = 64; // nodes expanded per batch (256 children)
 
 // Best leaf per pair, packed for a 64-bit atomicMax:
 //   [63:42] level-0 integer sum (22 bits)

@@ -170,7 +170,7 @@ int RunBatch(csm_context* ctx, csm_fast2d* const* submaps, int32_t num_submaps,
   // above ~8k points per scan the v1 kernel (lanes = points) is used.
   const bool use_v2 = forced == 2 || (forced != 1 && max_npad <= 8192);
   const char* rc_env = std::getenv("CSM_ROT_CHUNK");
-  const int v4_budget = 18 * 1024;
+  const int v4_budget = 9 * 1024;  // C2 (1088 padded points): 2 rotations per chunk, the measured best
   const int v4_rc = rc_env ? std::max(1, std::min(16, std::atoi(rc_env)))
                            : std::max(1, std::min(8, v4_budget / (max_npad * 4)));
   const int lds_budget = 40 * 1024;

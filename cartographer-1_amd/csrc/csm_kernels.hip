@@ -814,8 +814,9 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
       if (wave == 0) {
         // (a) Combine the previous batch: prune, record leaves, push survivors.
         const int pn = sh.nodes;
-        if (pn > 0) {
-          const int nd = lane >> 2, c = lane & 3;
+        // 16 nodes' children per pass (one per lane).
+        for (int pass = 0; pass * 16 < pn; ++pass) {
+          const int nd = pass * 16 + (lane >> 2), c = lane & 3;
           int sum = 0, xo = 0, yo = 0, r = 0, clvl = 0;
           bool exists = false;
           if (nd < pn) {
