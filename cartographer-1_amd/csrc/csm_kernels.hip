@@ -811,11 +811,12 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
 
     // ---- K3/K4: batched best-first DFS over the chunk -----------------------
     for (;;) {
-      if (wave == 0) {
+      {
         // (a) Combine the previous batch: prune, record leaves, push survivors.
+        // 16 nodes' children per pass (one per lane); the waves take the
+        // passes in parallel and claim stack space atomically.
         const int pn = sh.nodes;
-        // 16 nodes' children per pass (one per lane).
-        for (int pass = 0; pass * 16 < pn; ++pass) {
+        for (int pass = wave; pass * 16 < pn; pass += kWaves) {
           const int nd = pass * 16 + (lane >> 2), c = lane & 3;
           int sum = 0, xo = 0, yo = 0, r = 0, clvl = 0;
           bool exists = false;
@@ -839,43 +840,46 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
             else
               key = PackLeafKey(sum, rot0 + r, xo, yo);
           }
-          for (int m = 32; m >= 1; m >>= 1) {
-            const uint64_t o = __shfl_xor(key, m, 64);
-            key = o > key ? o : key;
-          }
-          if (lane == 0 && key > cur) {
-            atomicMax(reinterpret_cast<unsigned long long*>(pair_best), key);
-            sh.best = key;
+          if (__ballot(key != 0)) {  // wave-uniform: any leaf this pass
+            for (int m = 32; m >= 1; m >>= 1) {
+              const uint64_t o = __shfl_xor(key, m, 64);
+              key = o > key ? o : key;
+            }
+            if (lane == 0 && key > cur) {
+              atomicMax(reinterpret_cast<unsigned long long*>(pair_best), key);
+              atomicMax(reinterpret_cast<unsigned long long*>(&sh.best), key);
+            }
           }
           // Inner survivors: deepest level first, then best bound, on top.
+          // Rank among survivors by counting larger keys (lane ids make keys
+          // distinct); each survivor writes its own entry.
           const bool push = keep && clvl > 0;
-          uint32_t skey = push ? ((static_cast<uint32_t>(15 - clvl) << 28) |
-                                  (static_cast<uint32_t>(sum) << 6) | static_cast<uint32_t>(lane))
-                               : 0u;
-          for (int k = 2; k <= 64; k <<= 1)
-            for (int jj = k >> 1; jj >= 1; jj >>= 1) {
-              const uint32_t other = __shfl_xor(skey, jj, 64);
-              const bool up = ((lane & k) == 0), lower = ((lane & jj) == 0);
-              const uint32_t hi_v = skey > other ? skey : other, lo_v = skey > other ? other : skey;
-              skey = (lower == up) ? hi_v : lo_v;
-            }
-          const int kept = __popcll(__ballot(push));
-          const int sp = sh.sp;
-          const int j = skey & 63;
-          const int sx = __shfl(xo, j, 64), sy = __shfl(yo, j, 64), sr = __shfl(r, j, 64);
-          const int ssum = __shfl(sum, j, 64), sl = __shfl(clvl, j, 64);
-          if (lane < kept && sp + kept <= kStack2)
-            sh.stack[sp + kept - 1 - lane] = make_uint2(
-                (static_cast<uint32_t>(sx) & 0xffff) | (static_cast<uint32_t>(sy) << 16),
-                static_cast<uint32_t>(ssum) | (static_cast<uint32_t>(sr) << 22) |
-                    (static_cast<uint32_t>(sl) << 27));
-          if (lane == 0) {
-            if (sp + kept > kStack2) atomicOr(&status[pair_index], kStatusRange);
-            else sh.sp = sp + kept;
+          const uint32_t skey = push ? ((static_cast<uint32_t>(15 - clvl) << 28) |
+                                        (static_cast<uint32_t>(sum) << 6) | static_cast<uint32_t>(lane))
+                                     : 0u;
+          const unsigned long long pm = __ballot(push);
+          const int kept = __popcll(pm);
+          int rank = 0;
+          for (unsigned long long m = pm; m; m &= m - 1) {
+            const int jl = static_cast<int>(__ffsll(static_cast<long long>(m))) - 1;
+            rank += static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(skey), jl)) > skey;
           }
+          int sp = 0;
+          if (lane == 0 && kept > 0) sp = atomicAdd(&sh.sp, kept);
+          sp = __shfl(sp, 0, 64);
+          if (push && sp + kept <= kStack2)
+            sh.stack[sp + kept - 1 - rank] = make_uint2(
+                (static_cast<uint32_t>(xo) & 0xffff) | (static_cast<uint32_t>(yo) << 16),
+                static_cast<uint32_t>(sum) | (static_cast<uint32_t>(r) << 22) |
+                    (static_cast<uint32_t>(clvl) << 27));
+          if (lane == 0 && sp + kept > kStack2) atomicOr(&status[pair_index], kStatusRange);
         }
-        // (b) Refill roots when the stack is empty.
-        int sp = sh.sp;
+      }
+      __syncthreads();
+      if (wave == 0) {
+        // (b) Refill roots when the stack is empty. (An overflowed stack has
+        // flagged the pair; its result is discarded.)
+        int sp = min(sh.sp, kStack2);
         if (sp == 0 && sh.vnext < vtotal) {
           const int v0 = sh.vnext, vc = min(kRootChunk, vtotal - v0);
           for (int k = lane; k < vc; k += 64) {
