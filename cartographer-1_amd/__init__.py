@@ -154,6 +154,10 @@ _SIGNATURES = {
                                  C.POINTER(C.c_uint16), C.c_float, C.c_float, C.POINTER(Pose2D),
                                  C.POINTER(C.c_float), C.c_int32, C.POINTER(C.c_double),
                                  C.POINTER(Pose2D)]),
+    "csm_rt2d_match_tsdf": (C.c_int, [C.c_void_p, C.POINTER(RtOptions), C.POINTER(MapLimits),
+                                      C.POINTER(C.c_uint16), C.POINTER(C.c_uint16), C.c_float,
+                                      C.c_float, C.POINTER(Pose2D), C.POINTER(C.c_float),
+                                      C.c_int32, C.POINTER(C.c_double), C.POINTER(Pose2D)]),
     "csm_hybrid_grid_create": (C.c_int, [C.c_void_p, C.c_float, C.POINTER(C.c_int32),
                                          C.POINTER(C.c_uint16), C.c_int64, C.c_int32,
                                          C.POINTER(C.c_void_p)]),
@@ -248,6 +252,32 @@ class ProbabilityGrid:
     @property
     def num_y_cells(self) -> int:
         return int(self.cells.shape[0])
+
+    def limits(self) -> MapLimits:
+        return MapLimits(self.resolution, self.max_x, self.max_y, self.num_x_cells,
+                         self.num_y_cells)
+
+
+@dataclass
+class TSDF2D:
+    """TSDF2D data for the boundary (mapping/internal/2d/tsdf_2d.h): MapLimits,
+    the uint16 TSD cells (Grid2D correspondence_cost_cells) and weight cells,
+    both ``[y, x]``, and the TSDValueConverter parameters."""
+    resolution: float
+    max_x: float
+    max_y: float
+    tsd_cells: np.ndarray     # shape (num_y_cells, num_x_cells), uint16
+    weight_cells: np.ndarray  # same shape, uint16
+    truncation_distance: float
+    max_weight: float
+
+    @property
+    def num_x_cells(self) -> int:
+        return int(self.tsd_cells.shape[1])
+
+    @property
+    def num_y_cells(self) -> int:
+        return int(self.tsd_cells.shape[0])
 
     def limits(self) -> MapLimits:
         return MapLimits(self.resolution, self.max_x, self.max_y, self.num_x_cells,
@@ -398,22 +428,35 @@ class RealTimeCorrelativeScanMatcher2D:
         self._lib = self.context._lib
         self.options = options
 
-    def Match(self, initial_pose_estimate, point_cloud, grid: ProbabilityGrid):
-        """real_time_correlative_scan_matcher_2d.h:66-68 -> (score, pose)."""
+    def Match(self, initial_pose_estimate, point_cloud, grid):
+        """real_time_correlative_scan_matcher_2d.h:66-68 -> (score, pose). ``grid`` is a
+        ProbabilityGrid or a TSDF2D (ScoreCandidates switches on the grid type,
+        .cc:155-168)."""
         pts = _f32_points(point_cloud)
         o = self.options
         opts = RtOptions(o.linear_search_window, o.angular_search_window,
                          o.translation_delta_cost_weight, o.rotation_delta_cost_weight)
-        cells = np.ascontiguousarray(grid.cells, dtype=np.uint16)
         lim = grid.limits()
         init = Pose2D(*initial_pose_estimate)
         score = C.c_double(0.0)
         pose = Pose2D()
-        _check(self._lib.csm_rt2d_match(self.context.handle, C.byref(opts), C.byref(lim),
-                                        _ptr(cells, C.c_uint16), grid.min_correspondence_cost,
-                                        grid.max_correspondence_cost, C.byref(init),
-                                        _ptr(pts, C.c_float), len(pts), C.byref(score),
-                                        C.byref(pose)), "csm_rt2d_match")
+        if isinstance(grid, TSDF2D):
+            tsd = np.ascontiguousarray(grid.tsd_cells, dtype=np.uint16)
+            wgt = np.ascontiguousarray(grid.weight_cells, dtype=np.uint16)
+            if tsd.shape != wgt.shape:
+                raise ValueError("TSDF2D tsd_cells and weight_cells differ in shape")
+            _check(self._lib.csm_rt2d_match_tsdf(
+                self.context.handle, C.byref(opts), C.byref(lim), _ptr(tsd, C.c_uint16),
+                _ptr(wgt, C.c_uint16), grid.truncation_distance, grid.max_weight, C.byref(init),
+                _ptr(pts, C.c_float), len(pts), C.byref(score), C.byref(pose)),
+                "csm_rt2d_match_tsdf")
+        else:
+            cells = np.ascontiguousarray(grid.cells, dtype=np.uint16)
+            _check(self._lib.csm_rt2d_match(self.context.handle, C.byref(opts), C.byref(lim),
+                                            _ptr(cells, C.c_uint16), grid.min_correspondence_cost,
+                                            grid.max_correspondence_cost, C.byref(init),
+                                            _ptr(pts, C.c_float), len(pts), C.byref(score),
+                                            C.byref(pose)), "csm_rt2d_match")
         return float(score.value), pose.as_tuple()
 
 

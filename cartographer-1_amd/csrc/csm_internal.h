@@ -69,7 +69,10 @@ struct csm_context {
   std::mutex mu;
   csm::DevBuf submap_desc, pair_desc, rot_table, best, status, counters, pair_order,
       chunk_prefix, blocks, stats, rt_prob, rt_cells, rt_points, rt_best, rt_rot, rt_ptab,
-      single_points;
+      single_points, rt_wcells, rt_tsdw, rt_ttab;
+  // TSDValueConverter tables for the last (truncation, max_weight) uploaded.
+  float ttab_key[2] = {0.f, 0.f};
+  bool ttab_uploaded = false;
   bool timing = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   csm_timing t{};

@@ -992,8 +992,13 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
 // One workgroup per rotated scan; one lane per (x, y) offset of the full
 // (2L+1)^2 window (no ShrinkToFit on this path). Float sums run point by
 // point in the reference order so every candidate score is bit-identical.
-__global__ void rt2d_score(const float* __restrict__ prob,  // grid as probabilities
-                           int nx, int ny, double max_x, double max_y, double res,
+// kTsdf selects the grid: ProbabilityGrid (`prob`, 0.1 outside the limits,
+// real_time_correlative_scan_matcher_2d.cc:61-75) or TSDF2D (`tsdw` = (tsd,
+// weight), (-truncation, 0) outside, :38-59).
+template <bool kTsdf>
+__global__ void rt2d_score(const float* __restrict__ prob,   // ProbabilityGrid as probabilities
+                           const float2* __restrict__ tsdw,  // TSDF2D as (tsd, weight)
+                           float max_cc, int nx, int ny, double max_x, double max_y, double res,
                            const float* __restrict__ points, int n,
                            const float2* __restrict__ rot_table, float pre_w, float pre_s,
                            float tx, float ty, int num_linear, int num_angular,
@@ -1020,13 +1025,27 @@ __global__ void rt2d_score(const float* __restrict__ prob,  // grid as probabili
     const int xo = -num_linear + t / side;
     const int yo = -num_linear + t % side;
     float s = 0.f;
-    for (int i = 0; i < n; ++i) {
-      const int2 c = lds_xy[i];
-      const int gx = c.x + xo, gy = c.y + yo;
-      const bool in = gx >= 0 && gy >= 0 && gx < nx && gy < ny;
-      s = __fadd_rn(s, in ? prob[static_cast<size_t>(gy) * nx + gx] : 0.1f);
+    if constexpr (kTsdf) {
+      float sw = 0.f;
+      for (int i = 0; i < n; ++i) {
+        const int2 c = lds_xy[i];
+        const int gx = c.x + xo, gy = c.y + yo;
+        const bool in = gx >= 0 && gy >= 0 && gx < nx && gy < ny;
+        const float2 v = in ? tsdw[static_cast<size_t>(gy) * nx + gx] : make_float2(-max_cc, 0.f);
+        const float norm = __fdiv_rn(__fsub_rn(max_cc, fabsf(v.x)), max_cc);
+        s = __fadd_rn(s, __fmul_rn(norm, v.y));
+        sw = __fadd_rn(sw, v.y);
+      }
+      s = sw == 0.f ? 0.f : __fdiv_rn(s, sw);
+    } else {
+      for (int i = 0; i < n; ++i) {
+        const int2 c = lds_xy[i];
+        const int gx = c.x + xo, gy = c.y + yo;
+        const bool in = gx >= 0 && gy >= 0 && gx < nx && gy < ny;
+        s = __fadd_rn(s, in ? prob[static_cast<size_t>(gy) * nx + gx] : 0.1f);
+      }
+      s = __fdiv_rn(s, static_cast<float>(n));
     }
-    s = __fdiv_rn(s, static_cast<float>(n));
     const double cand_x = -yo * res, cand_y = -xo * res;
     const double theta = (r - num_angular) * step;
     const double pen = __dadd_rn(__dmul_rn(hypot(cand_x, cand_y), wt), __dmul_rn(fabs(theta), wr));
@@ -1040,6 +1059,16 @@ __global__ void rt2d_score(const float* __restrict__ prob,  // grid as probabili
     key = o > key ? o : key;
   }
   if ((threadIdx.x & 63) == 0 && key != 0) atomicMax(best, key);
+}
+
+// TSDF2D cells -> (tsd, weight) through TSDValueConverter's tables
+// (tsd_value_converter.h:54-62; bit 15, the update marker, is masked).
+__global__ void cells_to_tsdf(const uint16_t* __restrict__ tsd_cells,
+                              const uint16_t* __restrict__ weight_cells,
+                              const float* __restrict__ tsd_tab, const float* __restrict__ w_tab,
+                              float2* __restrict__ out, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = make_float2(tsd_tab[tsd_cells[i] & 0x7fff], w_tab[weight_cells[i] & 0x7fff]);
 }
 
 // Grid cells -> probability (ProbabilityGrid::GetProbability table).
@@ -1095,13 +1124,26 @@ hipError_t LaunchFast2dSearchV2(int grid, size_t dyn_lds, hipStream_t st, const 
 }
 
 hipError_t LaunchRt2dScore(dim3 grid, int block, size_t dyn_lds, hipStream_t st, const float* prob,
-                           int nx, int ny, double max_x, double max_y, double res,
-                           const float* points, int n, const float2* rot_table, float pre_w,
-                           float pre_s, float tx, float ty, int num_linear, int num_angular,
-                           double step, double wt, double wr, unsigned long long* best) {
-  hipLaunchKernelGGL(rt2d_score, grid, dim3(block), dyn_lds, st, prob, nx, ny, max_x, max_y, res,
-                     points, n, rot_table, pre_w, pre_s, tx, ty, num_linear, num_angular, step, wt,
-                     wr, best);
+                           const float2* tsdw, float max_cc, int nx, int ny, double max_x,
+                           double max_y, double res, const float* points, int n,
+                           const float2* rot_table, float pre_w, float pre_s, float tx, float ty,
+                           int num_linear, int num_angular, double step, double wt, double wr,
+                           unsigned long long* best) {
+  if (tsdw)
+    hipLaunchKernelGGL(rt2d_score<true>, grid, dim3(block), dyn_lds, st, prob, tsdw, max_cc, nx, ny,
+                       max_x, max_y, res, points, n, rot_table, pre_w, pre_s, tx, ty, num_linear,
+                       num_angular, step, wt, wr, best);
+  else
+    hipLaunchKernelGGL(rt2d_score<false>, grid, dim3(block), dyn_lds, st, prob, tsdw, max_cc, nx, ny,
+                       max_x, max_y, res, points, n, rot_table, pre_w, pre_s, tx, ty, num_linear,
+                       num_angular, step, wt, wr, best);
+  return hipGetLastError();
+}
+
+hipError_t LaunchCellsToTsdf(const uint16_t* tsd, const uint16_t* weight, const float* tsd_tab,
+                             const float* w_tab, float2* out, int n, hipStream_t st) {
+  hipLaunchKernelGGL(cells_to_tsdf, dim3((n + 255) / 256), dim3(256), 0, st, tsd, weight, tsd_tab,
+                     w_tab, out, n);
   return hipGetLastError();
 }
 

@@ -80,6 +80,11 @@ void ProbabilityTable(float* out) {
   }
 }
 
+void ConversionTable(float unknown_result, float lower, float upper, float* out) {
+  const float scale = (upper - lower) / 32766.f;
+  for (int v = 0; v < 32768; ++v) out[v] = v == 0 ? unknown_result : v * scale + (lower - scale);
+}
+
 float SumToScore(int64_t sum, int32_t n, float min_s, float max_s) {
   const float mean = static_cast<int>(sum) / static_cast<float>(n);
   return min_s + mean * ((max_s - min_s) / 255.f);

@@ -48,6 +48,9 @@ bool QuantizationTable(float min_cc, float max_cc, uint8_t* out32768);
 // Probability table for RTCSM: 1 - kValueToCorrespondenceCost[v]
 // (probability_grid.cc:78-82, probability_values.cc:26-66).
 void ProbabilityTable(float* out32768);
+// ValueConversionTables::GetConversionTable(unknown, lower, upper)
+// (value_conversion_tables.cc:28-52) over the 32768 unmarked values.
+void ConversionTable(float unknown_result, float lower, float upper, float* out32768);
 
 // PrecomputationGrid2D::ToScore(sum / float(n)) (fast_correlative_scan_
 // matcher_2d.h:74-76, .cc:328-329).

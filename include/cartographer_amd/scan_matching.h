@@ -50,12 +50,18 @@ struct PointCloud {
 
 // Grid2D view: MapLimits + uint16 correspondence-cost cells (x fastest).
 struct Grid2DView {
+  // Grid2D::GetGridType() (grid_2d.h:32): which cells the view carries.
+  enum class GridType { PROBABILITY_GRID, TSDF };
+  GridType grid_type = GridType::PROBABILITY_GRID;
   double resolution = 0.05;
   double max_x = 0., max_y = 0.;
   int num_x_cells = 0, num_y_cells = 0;
-  const uint16_t* cells = nullptr;
-  float min_correspondence_cost = 0.1f;  // kMinCorrespondenceCost
-  float max_correspondence_cost = 0.9f;  // kMaxCorrespondenceCost
+  const uint16_t* cells = nullptr;       // correspondence_cost_cells() (TSD values for a TSDF)
+  float min_correspondence_cost = 0.1f;  // kMinCorrespondenceCost (-truncation for a TSDF)
+  float max_correspondence_cost = 0.9f;  // kMaxCorrespondenceCost (truncation for a TSDF)
+  // TSDF2D only (tsdf_2d.h:55-60): weight_cells_ and TSDValueConverter's max weight.
+  const uint16_t* weight_cells = nullptr;
+  float max_weight = 0.f;
 };
 
 // proto::FastCorrelativeScanMatcherOptions2D (pose_graph.lua:25-29 defaults).
@@ -149,11 +155,19 @@ class RealTimeCorrelativeScanMatcher2D {
                           initial_pose_estimate.theta};
     csm_pose2d out{};
     double score = 0.;
-    CheckOk(csm_rt2d_match(ThreadContext(), &options_, &limits, grid.cells,
-                           grid.min_correspondence_cost, grid.max_correspondence_cost, &init,
-                           point_cloud.xyz.data(), static_cast<int32_t>(point_cloud.size()),
-                           &score, &out),
-            "RealTimeCorrelativeScanMatcher2D::Match");
+    // ScoreCandidates switches on grid.GetGridType() (.cc:155-168).
+    if (grid.grid_type == Grid2DView::GridType::TSDF)
+      CheckOk(csm_rt2d_match_tsdf(ThreadContext(), &options_, &limits, grid.cells,
+                                  grid.weight_cells, grid.max_correspondence_cost, grid.max_weight,
+                                  &init, point_cloud.xyz.data(),
+                                  static_cast<int32_t>(point_cloud.size()), &score, &out),
+              "RealTimeCorrelativeScanMatcher2D::Match");
+    else
+      CheckOk(csm_rt2d_match(ThreadContext(), &options_, &limits, grid.cells,
+                             grid.min_correspondence_cost, grid.max_correspondence_cost, &init,
+                             point_cloud.xyz.data(), static_cast<int32_t>(point_cloud.size()),
+                             &score, &out),
+              "RealTimeCorrelativeScanMatcher2D::Match");
     *pose_estimate = Rigid2d{out.x, out.y, out.theta};
     return score;
   }

@@ -180,6 +180,22 @@ int csm_rt2d_match(csm_context* ctx, const csm_rt_options* options,
                    const csm_pose2d* initial, const float* points_xyz,
                    int32_t n, double* score, csm_pose2d* pose);
 
+/* The same Match() for a TSDF2D grid (GridType::TSDF,
+ * real_time_correlative_scan_matcher_2d.cc:38-59 and :162-167): the grid
+ * crosses as its two uint16 arrays, correspondence_cost_cells() (TSD values,
+ * tsdf_2d.cc:73-79) and weight_cells_ (tsdf_2d.cc:81-87), both x-fastest
+ * num_x_cells * num_y_cells, plus the TSDValueConverter parameters
+ * (truncation distance = max TSD, max weight; tsd_value_converter.cc:22-33).
+ * Candidate score = sum((trunc - |tsd|) / trunc * weight) / sum(weight), 0 when
+ * no point lands on a weighted cell; outside the limits a point reads
+ * (-trunc, 0). */
+int csm_rt2d_match_tsdf(csm_context* ctx, const csm_rt_options* options,
+                        const csm_map_limits* limits, const uint16_t* tsd_cells,
+                        const uint16_t* weight_cells, float truncation_distance,
+                        float max_weight, const csm_pose2d* initial,
+                        const float* points_xyz, int32_t n, double* score,
+                        csm_pose2d* pose);
+
 /* ---- 3D: HybridGrid ----------------------------------------------------------
  * A HybridGrid (mapping/3d/hybrid_grid.h:463-545) crosses the boundary as the
  * list its iterator / ToProto yields (hybrid_grid.h:530-541): cell indices

@@ -351,7 +351,8 @@ TEST(ProbabilityValuesTables) {
 
 }  // namespace
 
-int RunRefTests3D(int* checks);  // ref_tests_3d.cc
+int RunRefTests3D(int* checks);    // ref_tests_3d.cc
+int RunRefTestsTSDF(int* checks);  // ref_tests_tsdf.cc
 
 int main() {
   for (const TestCase& t : Registry()) {
@@ -360,9 +361,11 @@ int main() {
     t.fn();
     std::printf("%-70s %s\n", t.name, g_failures == before ? "OK" : "FAILED");
   }
-  int checks3d = 0;
+  int checks3d = 0, checks_tsdf = 0;
   const int failures3d = RunRefTests3D(&checks3d);
-  std::printf("checks: %d (2D) + %d (3D), failures: %d\n", g_checks, checks3d,
-              g_failures + failures3d);
-  return (g_failures + failures3d) == 0 ? 0 : 1;
+  const int failures_tsdf = RunRefTestsTSDF(&checks_tsdf);
+  const int failures = g_failures + failures3d + failures_tsdf;
+  std::printf("checks: %d (2D) + %d (3D) + %d (TSDF), failures: %d\n", g_checks, checks3d,
+              checks_tsdf, failures);
+  return failures == 0 ? 0 : 1;
 }

@@ -42,6 +42,13 @@ class Oracle:
             "oracle_grid_info": (None, [VP, P(D), P(I32)]),
             "oracle_grid_cells": (None, [VP, P(C.c_uint16)]),
             "oracle_transform_cloud_2d": (None, [P(F), P(F), I32, P(F)]),
+            "oracle_tsdf_create": (VP, [D, D, D, I32, I32, F, F]),
+            "oracle_tsdf_destroy": (None, [VP]),
+            "oracle_tsdf_insert": (None, [VP, P(D), P(F), P(F), I32]),
+            "oracle_tsdf_info": (None, [VP, P(D), P(I32)]),
+            "oracle_tsdf_cells": (None, [VP, P(C.c_uint16), P(C.c_uint16)]),
+            "oracle_rt2d_match_tsdf": (D, [D, D, D, I32, I32, P(C.c_uint16), P(C.c_uint16), F,
+                                           F, D, D, D, D, P(D), P(F), I32, P(D), P(I64)]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(lib, name)
@@ -78,6 +85,48 @@ class Oracle:
         out = np.zeros((cells[1], cells[0]), np.uint16)
         self.lib.oracle_grid_cells(g, _p(out, C.c_uint16))
         return (float(info[0]), float(info[1]), float(info[2])), out
+
+    # ---- TSDF2D (restated TSDFRangeDataInserter2D) -----------------------
+    # Inserter options in proto order: truncation_distance, maximum_weight,
+    # update_free_space, num_normal_samples, sample_radius,
+    # project_sdf_distance_to_scan_normal, update_weight_range_exponent,
+    # angle bandwidth, distance bandwidth.
+    TSDF_TEST_OPTIONS = (0.3, 10.0, 0, 4, 0.5, 1, 0, 0.5, 0.5)  # rtcsm_2d_test.cc:67-90
+
+    def tsdf_from_inserts(self, res, max_x, max_y, nx, ny, truncation, max_weight, inserts,
+                          options=TSDF_TEST_OPTIONS):
+        """TSDF2D built by the restated inserter; inserts: list of (origin xyz,
+        returns (n,3)). Returns (limits, tsd_cells, weight_cells)."""
+        g = self.lib.oracle_tsdf_create(res, max_x, max_y, nx, ny, truncation, max_weight)
+        try:
+            opts = np.asarray(options, np.float64)
+            for origin, ret in inserts:
+                o = np.asarray(origin, np.float32)
+                r = np.ascontiguousarray(ret, np.float32)
+                self.lib.oracle_tsdf_insert(g, _p(opts, D), _p(o, F), _p(r, F), len(r))
+            info = np.zeros(3)
+            cells = np.zeros(2, np.int32)
+            self.lib.oracle_tsdf_info(g, _p(info, D), _p(cells, I32))
+            tsd = np.zeros((cells[1], cells[0]), np.uint16)
+            wgt = np.zeros_like(tsd)
+            self.lib.oracle_tsdf_cells(g, _p(tsd, C.c_uint16), _p(wgt, C.c_uint16))
+            return (float(info[0]), float(info[1]), float(info[2])), tsd, wgt
+        finally:
+            self.lib.oracle_tsdf_destroy(g)
+
+    def rt2d_match_tsdf(self, limits, tsd, wgt, truncation, max_weight, opts, initial, cloud):
+        res, mx, my = limits
+        tsd = np.ascontiguousarray(tsd, np.uint16)
+        wgt = np.ascontiguousarray(wgt, np.uint16)
+        init = np.asarray(initial, np.float64)
+        pts = np.ascontiguousarray(cloud, np.float32)
+        pose = np.zeros(3)
+        ncand = C.c_int64()
+        s = self.lib.oracle_rt2d_match_tsdf(res, mx, my, tsd.shape[1], tsd.shape[0],
+                                            _p(tsd, C.c_uint16), _p(wgt, C.c_uint16), truncation,
+                                            max_weight, *opts, _p(init, D), _p(pts, F), len(pts),
+                                            _p(pose, D), C.byref(ncand))
+        return s, tuple(pose), ncand.value
 
     def transform_cloud(self, pose_f, cloud):
         pose = np.asarray(pose_f, np.float32)

@@ -129,6 +129,37 @@ def test_gpu_matches_rt2d_golden(csm):
         assert tuple(pose) == tuple(d["pose"][i])
 
 
+def _tsdf_case(d, i):
+    s = int(d["grid"][i])
+    return (tuple(float(v) for v in d[f"limits_{s}"]), d[f"tsd_{s}"], d[f"wgt_{s}"])
+
+
+def test_oracle_reproduces_rt2d_tsdf_golden(oracle):
+    d = _load("rt2d_tsdf.npz")
+    for i in range(len(d["score"])):
+        lim, tsd, wgt = _tsdf_case(d, i)
+        sc, pose, _ = oracle.rt2d_match_tsdf(lim, tsd, wgt, float(d["truncation"]),
+                                             float(d["max_weight"]), tuple(d["options"]),
+                                             tuple(d["initial"][i]), _cloud(d, i))
+        assert sc == d["score"][i]
+        assert tuple(pose) == tuple(d["pose"][i])
+
+
+@pytest.mark.gpu
+def test_gpu_matches_rt2d_tsdf_golden(csm):
+    d = _load("rt2d_tsdf.npz")
+    m = csm.RealTimeCorrelativeScanMatcher2D(
+        csm.RealTimeCorrelativeScanMatcherOptions(*[float(v) for v in d["options"]]))
+    for i in range(len(d["score"])):
+        lim, tsd, wgt = _tsdf_case(d, i)
+        g = csm.TSDF2D(*lim, tsd, wgt, float(d["truncation"]), float(d["max_weight"]))
+        sc, pose = m.Match(tuple(d["initial"][i]), _cloud(d, i), g)
+        # TSDF sums are float, in reference order, so bit-identical; the double
+        # exp() penalty may differ from glibc in the last ulps: 1e-6 relative.
+        assert math.isclose(sc, d["score"][i], rel_tol=1e-6, abs_tol=0), (i, sc, d["score"][i])
+        assert tuple(pose) == tuple(d["pose"][i])
+
+
 # ------------------------------------------------------------------ 3D (C4/C5) --
 def _cells3(d, kind, s):
     o = d[kind + "_off"]
