@@ -27,7 +27,9 @@ from typing import Optional, Sequence, Tuple
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libcsm_amd.so")
+# CSM_AMD_LIB points experiments (e.g. a CSM_KPROF build) at another build of
+# the same library; the default is the in-tree build.
+LIB_PATH = os.environ.get("CSM_AMD_LIB") or os.path.join(_HERE, "libcsm_amd.so")
 SYNTH_PATH = os.path.join(_HERE, "libcsm_synth.so")
 
 CSM_OK = 0

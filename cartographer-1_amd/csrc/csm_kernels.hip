@@ -903,7 +903,53 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
         }
         const uint32_t cur_sum = static_cast<uint32_t>(sh.best >> kSumShift);
         int nodes = 0;
-        if (sp > 0) {
+        if (sp > 0 && mixed_levels == 2) {
+          // Homogeneous batches: the nodes of one (rotation, level) group,
+          // that of the top entry, picked from the top 128 entries, best
+          // first. One group shares the child level's planes for a given
+          // point, so a gather over the batch touches few cache lines.
+          // Pruned entries in the window are dropped; the others keep their
+          // order and the window is compacted in place.
+          const int W = min(sp, 2 * 64);
+          const bool in0 = lane < W, in1 = lane + 64 < W;
+          const uint2 e0 = in0 ? sh.stack[sp - 1 - lane] : make_uint2(0, 0);
+          const uint2 e1 = in1 ? sh.stack[sp - 1 - 64 - lane] : make_uint2(0, 0);
+          const uint32_t group = sh.stack[sp - 1].y >> 22;  // level << 5 | rotation
+          const bool live0 = in0 && (e0.y & 0x3fffff) >= cur_sum;
+          const bool live1 = in1 && (e1.y & 0x3fffff) >= cur_sum;
+          const bool m0 = live0 && (e0.y >> 22) == group, m1 = live1 && (e1.y >> 22) == group;
+          const unsigned long long b0 = __ballot(m0), b1 = __ballot(m1);
+          const int ne = __popcll(b0) + __popcll(b1);
+          const unsigned long long below = (1ull << lane) - 1;
+          bool s0 = false, s1 = false;
+          int r0 = 0, r1 = 0;
+          if (ne > 0) {
+            nodes = 1 << (31 - __clz(ne));
+            r0 = __popcll(b0 & below);
+            r1 = __popcll(b0) + __popcll(b1 & below);
+            s0 = m0 && r0 < nodes;
+            s1 = m1 && r1 < nodes;
+            if (s0) {
+              sh.node_xo[r0] = static_cast<int16_t>(e0.x & 0xffff);
+              sh.node_yo[r0] = static_cast<int>(e0.x) >> 16;
+              sh.node_rot[r0] = (e0.y >> 22) & 0x1f;
+              sh.node_level[r0] = static_cast<int>(e0.y >> 27);
+            }
+            if (s1) {
+              sh.node_xo[r1] = static_cast<int16_t>(e1.x & 0xffff);
+              sh.node_yo[r1] = static_cast<int>(e1.x) >> 16;
+              sh.node_rot[r1] = (e1.y >> 22) & 0x1f;
+              sh.node_level[r1] = static_cast<int>(e1.y >> 27);
+            }
+          }
+          const bool k0 = live0 && !s0, k1 = live1 && !s1;
+          const unsigned long long c0 = __ballot(k0), c1 = __ballot(k1);
+          const int kept = __popcll(c0) + __popcll(c1);
+          const int base = sp - W + kept;  // new stack pointer
+          if (k0) sh.stack[base - 1 - __popcll(c0 & below)] = e0;
+          if (k1) sh.stack[base - 1 - __popcll(c0) - __popcll(c1 & below)] = e1;
+          sp = base;
+        } else if (sp > 0) {
           // Up to 16 entries from the top (any level); expand a power of two
           // of the unpruned ones, discard pruned ones passed over.
           uint2 ent = make_uint2(0, 0);

@@ -18,6 +18,7 @@ groups=(
  "TCC_HIT_sum TCC_MISS_sum"
  "FETCH_SIZE"
 )
+mkdir -p $R/$OUT
 i=0
 for g in "${groups[@]}"; do
   timeout -k 10 240 rocprofv3 --pmc $g -d $R/$OUT/p$i -o run --output-format csv -- python3 $R/bench.py "$@" > $R/$OUT/p$i.log 2>&1 || echo "pass $i failed"
