@@ -83,11 +83,13 @@ R3 Inverse(const R3& a) {
   const V3 t = Rotate(c, a.t);
   return R3{V3{-t.x, -t.y, -t.z}, c};
 }
-float NormV(const V3& v) { return std::sqrt((v.x * v.x + v.y * v.y) + v.z * v.z); }
+// Vector3f::norm(): Eigen unrolls a 3-element sum as x0 + (x1 + x2)
+// (Redux.h redux_novec_unroller splits at Length / 2).
+float NormV(const V3& v) { return std::sqrt(v.x * v.x + (v.y * v.y + v.z * v.z)); }
 // transform.h:86-100 for float: sin/cos of norm/2. in double.
 Q4 AngleAxisToQuat(const V3& aa) {
   float scale = 0.5f, w = 1.f;
-  const float sq = (aa.x * aa.x + aa.y * aa.y) + aa.z * aa.z;
+  const float sq = aa.x * aa.x + (aa.y * aa.y + aa.z * aa.z);
   if (sq > 1e-8) {
     const float norm = std::sqrt(sq);
     scale = static_cast<float>(std::sin(norm / 2.) / norm);
@@ -96,7 +98,7 @@ Q4 AngleAxisToQuat(const V3& aa) {
   return Q4{w, scale * aa.x, scale * aa.y, scale * aa.z};
 }
 float GetAngle(const Q4& q) {  // transform.h:34-37
-  return 2.f * std::atan2(std::sqrt((q.x * q.x + q.y * q.y) + q.z * q.z), std::abs(q.w));
+  return 2.f * std::atan2(std::sqrt(q.x * q.x + (q.y * q.y + q.z * q.z)), std::abs(q.w));
 }
 float GetYaw(const Q4& q) {  // transform.h:43-47 (C ::atan2 on promoted floats)
   const V3 d = Rotate(q, V3{1.f, 0.f, 0.f});

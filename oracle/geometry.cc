@@ -65,13 +65,13 @@ Quatd QuatMul(const Quatd& a, const Quatd& b) { return QuatMulImpl(a, b); }
 
 // Eigen QuaternionBase::normalized -> coeffs / coeffs.norm() (x,y,z,w storage).
 Quatf QuatNormalized(const Quatf& q) {
-  const float n2 = q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w;
+  const float n2 = (q.x * q.x + q.z * q.z) + (q.y * q.y + q.w * q.w);  // SSE predux
   const float n = std::sqrt(n2);
   if (n > 0.f) return Quatf{q.w / n, q.x / n, q.y / n, q.z / n};
   return q;
 }
 Quatd QuatNormalized(const Quatd& q) {
-  const double n2 = q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w;
+  const double n2 = (q.x * q.x + q.z * q.z) + (q.y * q.y + q.w * q.w);  // SSE2 packets
   const double n = std::sqrt(n2);
   if (n > 0.) return Quatd{q.w / n, q.x / n, q.y / n, q.z / n};
   return q;

@@ -99,11 +99,13 @@ Rigid3f Inverse3(const Rigid3f& a) {
   return Rigid3f{Vec3f{-t.x, -t.y, -t.z}, c};
 }
 
-float NormF(const Vec3f& v) { return std::sqrt((v.x * v.x + v.y * v.y) + v.z * v.z); }
+// Vector3f::norm(): Eigen unrolls a 3-element sum as x0 + (x1 + x2)
+// (Redux.h redux_novec_unroller splits at Length / 2).
+float NormF(const Vec3f& v) { return std::sqrt(v.x * v.x + (v.y * v.y + v.z * v.z)); }
 
 Quatf AngleAxisVectorToRotationQuaternionF(const Vec3f& aa) {
   float scale = 0.5f, w = 1.f;
-  const float sq = (aa.x * aa.x + aa.y * aa.y) + aa.z * aa.z;
+  const float sq = aa.x * aa.x + (aa.y * aa.y + aa.z * aa.z);
   if (sq > 1e-8) {
     const float norm = std::sqrt(sq);
     scale = static_cast<float>(std::sin(norm / 2.) / norm);
@@ -113,7 +115,7 @@ Quatf AngleAxisVectorToRotationQuaternionF(const Vec3f& aa) {
 }
 
 float GetAngleF(const Quatf& q) {
-  const float vn = std::sqrt((q.x * q.x + q.y * q.y) + q.z * q.z);
+  const float vn = std::sqrt(q.x * q.x + (q.y * q.y + q.z * q.z));
   return 2.f * std::atan2(vn, std::abs(q.w));
 }
 

@@ -43,7 +43,8 @@ float NormalizeAngleDifferenceF(float d) {
 }
 
 float Norm2(float x, float y) { return std::sqrt(x * x + y * y); }
-float Norm3(float x, float y, float z) { return std::sqrt(x * x + y * y + z * z); }
+// Vector3f::norm(): Eigen's unrolled 3-element sum is x0 + (x1 + x2).
+float Norm3(float x, float y, float z) { return std::sqrt(x * x + (y * y + z * z)); }
 
 }  // namespace
 
