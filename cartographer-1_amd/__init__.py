@@ -119,6 +119,17 @@ class Result3D(C.Structure):
                 ("rotational_score", C.c_float), ("low_resolution_score", C.c_float)]
 
 
+class AdaptiveVoxelFilterOptions(C.Structure):
+    """proto::AdaptiveVoxelFilterOptions (all floats); defaults are
+    trajectory_builder_2d.lua:25-29's adaptive_voxel_filter."""
+    _fields_ = [("max_length", C.c_float), ("min_num_points", C.c_float),
+                ("max_range", C.c_float)]
+
+    @staticmethod
+    def make(max_length=0.5, min_num_points=200, max_range=50.0) -> "AdaptiveVoxelFilterOptions":
+        return AdaptiveVoxelFilterOptions(max_length, min_num_points, max_range)
+
+
 class Pair3D(C.Structure):
     _fields_ = [("submap", C.c_int32), ("node", C.c_int32), ("full_submap", C.c_int32),
                 ("min_score", C.c_float), ("node_pose", Pose3D), ("submap_pose", Pose3D)]
@@ -182,6 +193,19 @@ _SIGNATURES = {
     "csm_fast3d_match_batch": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.c_int32,
                                          C.POINTER(Node3D), C.c_int32, C.POINTER(Pair3D),
                                          C.c_int64, C.POINTER(Result3D)]),
+    "csm_voxel_filter": (C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_int64),
+                                   C.c_int32, C.c_float, C.POINTER(C.c_uint8),
+                                   C.POINTER(C.c_int32)]),
+    "csm_adaptive_voxel_filter": (C.c_int, [C.c_void_p, C.POINTER(C.c_float),
+                                            C.POINTER(C.c_int64), C.c_int32,
+                                            C.POINTER(AdaptiveVoxelFilterOptions),
+                                            C.POINTER(C.c_uint8), C.POINTER(C.c_int32)]),
+    "csm_voxel_filter_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32,
+                                          C.c_int32, C.c_float, C.c_void_p, C.c_void_p]),
+    "csm_adaptive_voxel_filter_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p,
+                                                   C.c_int32, C.c_int32,
+                                                   C.POINTER(AdaptiveVoxelFilterOptions),
+                                                   C.c_void_p, C.c_void_p]),
     "csm_strerror": (C.c_char_p, [C.c_int]),
 }
 
@@ -604,3 +628,65 @@ from .matching3d import (FastCorrelativeScanMatcher3D, FastCorrelativeScanMatche
                          HybridGrid, NodeData3D, PAIR3_DTYPE, RESULT3_DTYPE,
                          RealTimeCorrelativeScanMatcher3D, SyntheticWorld3D, make_pairs_3d,
                          match_batch_3d)
+
+
+# --------------------------------------------------------------------------
+# Node clouds: voxel filters (sensor/internal/voxel_filter.cc).
+
+def _pack_clouds(clouds):
+    arrs = [_f32_points(c) for c in clouds]
+    offsets = np.zeros(len(arrs) + 1, np.int64)
+    offsets[1:] = np.cumsum([len(a) for a in arrs])
+    pts = np.ascontiguousarray(np.concatenate(arrs) if arrs else np.zeros((0, 3), np.float32))
+    return pts, offsets
+
+
+def voxel_filter_masks(clouds, resolution: float, context: Optional[Context] = None):
+    """sensor::VoxelFilter(cloud, resolution) for each cloud (voxel_filter.cc:212-232):
+    returns (keep mask over the concatenated points, per-cloud counts, offsets).
+    The survivors of cloud c are ``points[offsets[c]:offsets[c+1]][mask[...]]``."""
+    ctx = context or default_context()
+    pts, offsets = _pack_clouds(clouds)
+    keep = np.zeros(len(pts), np.uint8)
+    counts = np.zeros(len(offsets) - 1, np.int32)
+    _check(ctx._lib.csm_voxel_filter(ctx.handle, _ptr(pts, C.c_float), _ptr(offsets, C.c_int64),
+                                     len(offsets) - 1, float(resolution), _ptr(keep, C.c_uint8),
+                                     _ptr(counts, C.c_int32)), "csm_voxel_filter")
+    return keep.astype(bool), counts, offsets
+
+
+def adaptive_voxel_filter_masks(clouds, options: AdaptiveVoxelFilterOptions,
+                                context: Optional[Context] = None):
+    """sensor::AdaptiveVoxelFilter(cloud, options) for each cloud
+    (voxel_filter.cc:263-268): (keep mask, counts, offsets) as voxel_filter_masks."""
+    ctx = context or default_context()
+    pts, offsets = _pack_clouds(clouds)
+    keep = np.zeros(len(pts), np.uint8)
+    counts = np.zeros(len(offsets) - 1, np.int32)
+    _check(ctx._lib.csm_adaptive_voxel_filter(ctx.handle, _ptr(pts, C.c_float),
+                                              _ptr(offsets, C.c_int64), len(offsets) - 1,
+                                              C.byref(options), _ptr(keep, C.c_uint8),
+                                              _ptr(counts, C.c_int32)),
+           "csm_adaptive_voxel_filter")
+    return keep.astype(bool), counts, offsets
+
+
+def VoxelFilter(point_cloud, resolution: float, intensities=None,
+                context: Optional[Context] = None):
+    """sensor::VoxelFilter(const PointCloud&, float) (voxel_filter.cc:212-232):
+    the surviving points in input order (and their intensities, if given)."""
+    pts = _f32_points(point_cloud)
+    keep, _, _ = voxel_filter_masks([pts], resolution, context)
+    if intensities is None:
+        return pts[keep]
+    return pts[keep], np.asarray(intensities, np.float32)[keep[:len(intensities)]]
+
+
+def AdaptiveVoxelFilter(point_cloud, options: AdaptiveVoxelFilterOptions, intensities=None,
+                        context: Optional[Context] = None):
+    """sensor::AdaptiveVoxelFilter(const PointCloud&, options) (voxel_filter.cc:263-268)."""
+    pts = _f32_points(point_cloud)
+    keep, _, _ = adaptive_voxel_filter_masks([pts], options, context)
+    if intensities is None:
+        return pts[keep]
+    return pts[keep], np.asarray(intensities, np.float32)[keep[:len(intensities)]]

@@ -85,6 +85,8 @@ struct csm_context {
   csm::DevBuf rt3_rot, rt3_trans, rt3_points, rt3_best, f3_pairs, f3_yaws, f3_points,
       f3_low_points, f3_best, f3_status, f3_counter, f3_items, f3_scores;
   csm::PinnedBuf f3_host_yaws;
+  // Voxel filter scratch (voxel_filter.hip).
+  csm::DevBuf vf_points, vf_offsets, vf_keep, vf_counts;
 };
 
 #endif  // CSM_INTERNAL_H_

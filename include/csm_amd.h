@@ -310,6 +310,43 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
                            const csm_node3d* nodes, int32_t num_nodes, const csm_pair3d* pairs,
                            int64_t num_pairs, csm_result3d* results);
 
+/* ---- node clouds: voxel filters -------------------------------------------
+ * sensor::VoxelFilter and sensor::AdaptiveVoxelFilter
+ * (sensor/internal/voxel_filter.h, voxel_filter.cc:212-232 and :263-268), the
+ * filters that make the clouds the matchers search with
+ * (local_trajectory_builder_2d.cc:61-62, :229-231;
+ * local_trajectory_builder_3d.cc:682-683, :735-748). A batch of clouds: cloud
+ * c is points [offsets[c], offsets[c+1]) of xyz (float x, y, z). keep[i] = 1
+ * when point i survives; the reference returns the survivors in input order
+ * and filters intensities with the same mask. counts[c] = survivors of cloud c
+ * (may be NULL). The kept set is the reference's exactly (same voxel keys, same
+ * minstd_rand0 reservoir draws). Clouds of up to 8192 points (larger:
+ * CSM_ERANGE). */
+typedef struct csm_adaptive_voxel_filter_options {
+  /* proto::AdaptiveVoxelFilterOptions
+   * (sensor/proto/adaptive_voxel_filter_options.proto): all floats. */
+  float max_length;
+  float min_num_points;
+  float max_range;
+} csm_adaptive_voxel_filter_options;
+
+int csm_voxel_filter(csm_context* ctx, const float* xyz, const int64_t* offsets,
+                     int32_t num_clouds, float resolution, uint8_t* keep, int32_t* counts);
+int csm_adaptive_voxel_filter(csm_context* ctx, const float* xyz, const int64_t* offsets,
+                              int32_t num_clouds, const csm_adaptive_voxel_filter_options* options,
+                              uint8_t* keep, int32_t* counts);
+/* The same on device-resident buffers (d_offsets relative to d_xyz), enqueued
+ * on the context's stream without synchronising; max_points bounds every
+ * cloud's size. */
+int csm_voxel_filter_device(csm_context* ctx, const float* d_xyz, const int64_t* d_offsets,
+                            int32_t num_clouds, int32_t max_points, float resolution,
+                            uint8_t* d_keep, int32_t* d_counts);
+int csm_adaptive_voxel_filter_device(csm_context* ctx, const float* d_xyz,
+                                     const int64_t* d_offsets, int32_t num_clouds,
+                                     int32_t max_points,
+                                     const csm_adaptive_voxel_filter_options* options,
+                                     uint8_t* d_keep, int32_t* d_counts);
+
 /* Human-readable text for a return code. */
 const char* csm_strerror(int code);
 

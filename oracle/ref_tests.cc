@@ -353,6 +353,7 @@ TEST(ProbabilityValuesTables) {
 
 int RunRefTests3D(int* checks);    // ref_tests_3d.cc
 int RunRefTestsTSDF(int* checks);  // ref_tests_tsdf.cc
+int RunRefTestsVoxel(int* checks);  // ref_tests_voxel.cc
 
 int main() {
   for (const TestCase& t : Registry()) {
@@ -361,11 +362,12 @@ int main() {
     t.fn();
     std::printf("%-70s %s\n", t.name, g_failures == before ? "OK" : "FAILED");
   }
-  int checks3d = 0, checks_tsdf = 0;
+  int checks3d = 0, checks_tsdf = 0, checks_voxel = 0;
   const int failures3d = RunRefTests3D(&checks3d);
   const int failures_tsdf = RunRefTestsTSDF(&checks_tsdf);
-  const int failures = g_failures + failures3d + failures_tsdf;
-  std::printf("checks: %d (2D) + %d (3D) + %d (TSDF), failures: %d\n", g_checks, checks3d,
-              checks_tsdf, failures);
+  const int failures_voxel = RunRefTestsVoxel(&checks_voxel);
+  const int failures = g_failures + failures3d + failures_tsdf + failures_voxel;
+  std::printf("checks: %d (2D) + %d (3D) + %d (TSDF) + %d (voxel filter), failures: %d\n",
+              g_checks, checks3d, checks_tsdf, checks_voxel, failures);
   return failures == 0 ? 0 : 1;
 }

@@ -47,6 +47,8 @@ class Oracle:
             "oracle_tsdf_insert": (None, [VP, P(D), P(F), P(F), I32]),
             "oracle_tsdf_info": (None, [VP, P(D), P(I32)]),
             "oracle_tsdf_cells": (None, [VP, P(C.c_uint16), P(C.c_uint16)]),
+            "oracle_voxel_filter": (I64, [P(F), P(I64), I32, F, P(C.c_uint8)]),
+            "oracle_adaptive_voxel_filter": (I64, [P(F), P(I64), I32, F, F, F, P(C.c_uint8)]),
             "oracle_rt2d_match_tsdf": (D, [D, D, D, I32, I32, P(C.c_uint16), P(C.c_uint16), F,
                                            F, D, D, D, D, P(D), P(F), I32, P(D), P(I64)]),
         }
@@ -409,3 +411,33 @@ Oracle.fast3d = _o3_fast3d
 Oracle.histogram = _o3_histogram
 Oracle.rt3d_match = _o3_rt3d_match
 Oracle.rt3d_score = _o3_rt3d_score
+
+
+# ---- voxel filters (oracle/voxel_filter.cc) ------------------------------
+def _pack_clouds(clouds):
+    arrs = [np.ascontiguousarray(np.asarray(c, np.float32).reshape(-1, 3)) for c in clouds]
+    offsets = np.zeros(len(arrs) + 1, np.int64)
+    offsets[1:] = np.cumsum([len(a) for a in arrs])
+    pts = np.ascontiguousarray(np.concatenate(arrs) if arrs else np.zeros((0, 3), np.float32))
+    return pts, offsets
+
+
+def _o_voxel_filter_masks(self, clouds, resolution):
+    pts, offsets = _pack_clouds(clouds)
+    keep = np.zeros(max(len(pts), 1), np.uint8)
+    self.lib.oracle_voxel_filter(_p(pts, F), _p(offsets, I64), len(offsets) - 1,
+                                 float(resolution), _p(keep, C.c_uint8))
+    return keep[:len(pts)].astype(bool), offsets
+
+
+def _o_adaptive_voxel_filter_masks(self, clouds, max_length, min_num_points, max_range):
+    pts, offsets = _pack_clouds(clouds)
+    keep = np.zeros(max(len(pts), 1), np.uint8)
+    self.lib.oracle_adaptive_voxel_filter(_p(pts, F), _p(offsets, I64), len(offsets) - 1,
+                                          float(max_length), float(min_num_points),
+                                          float(max_range), _p(keep, C.c_uint8))
+    return keep[:len(pts)].astype(bool), offsets
+
+
+Oracle.voxel_filter_masks = _o_voxel_filter_masks
+Oracle.adaptive_voxel_filter_masks = _o_adaptive_voxel_filter_masks
