@@ -181,6 +181,8 @@ def main():
         out["rt2d"] = rt2d_bench(csm, ctx, args)
     if rank == 0 and world_size == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(world, my_submaps, args)
+    if rank == 0 and world_size == 1 and not args.no_rt:
+        out["voxel_filter"] = voxel_filter_bench(csm, ctx, world, args)
     if rank == 0 and world_size == 1 and not args.no_3d:
         out["rt3d"] = rt3d_bench(csm, ctx, args)
     if not args.no_3d:  # collective over ranks: the C5 sweep, submap-sharded
@@ -236,6 +238,62 @@ def rt2d_bench(csm, ctx, args):
                             (0.2, math.radians(10.0), 0.1, 0.1), init, cloud, 20)
         res["cpu_ms_per_scan_match"] = cpu_s * 1e3
         res["cpu_threads"] = 1
+    except OSError:
+        pass
+    return res
+
+
+def voxel_filter_bench(csm, ctx, world, args):
+    """AdaptiveVoxelFilter (trajectory_builder_2d.lua:25-29 options) over the
+    C2 node clouds as one device-resident batch: the step that makes the
+    clouds the loop-closure search uses (local_trajectory_builder_2d.cc:229-231)."""
+    import ctypes as C
+    import torch
+    clouds = [world.cloud(n) for n in range(args.nodes)]
+    pts = np.ascontiguousarray(np.concatenate(clouds), np.float32)
+    offsets = np.zeros(len(clouds) + 1, np.int64)
+    offsets[1:] = np.cumsum([len(c) for c in clouds])
+    dev = torch.device("cuda", torch.cuda.current_device())
+    d_pts = torch.from_numpy(pts).to(dev)
+    d_off = torch.from_numpy(offsets).to(dev)
+    d_keep = torch.zeros(len(pts), dtype=torch.uint8, device=dev)
+    d_cnt = torch.zeros(len(clouds), dtype=torch.int32, device=dev)
+    opts = csm.AdaptiveVoxelFilterOptions.make(0.5, 200, 50.0)
+    lib = ctx._lib
+    max_pts = int(np.diff(offsets).max())
+    stream = torch.cuda.ExternalStream(ctx.stream)
+    torch.cuda.synchronize()
+
+    def launch():
+        csm._check(lib.csm_adaptive_voxel_filter_device(
+            ctx.handle, C.c_void_p(d_pts.data_ptr()), C.c_void_p(d_off.data_ptr()), len(clouds),
+            max_pts, C.byref(opts), C.c_void_p(d_keep.data_ptr()), C.c_void_p(d_cnt.data_ptr())),
+            "csm_adaptive_voxel_filter_device")
+
+    for _ in range(3):
+        launch()
+    stream.synchronize()
+    reps = 20
+    a = time.perf_counter()
+    for _ in range(reps):
+        launch()
+    stream.synchronize()
+    gpu_s = (time.perf_counter() - a) / reps
+    counts = d_cnt.cpu().numpy()
+    res = {"workload": f"AdaptiveVoxelFilter(max_length 0.5, min_num_points 200, max_range 50) "
+                       f"over {len(clouds)} clouds x {max_pts} points",
+           "gpu_ms_per_batch": gpu_s * 1e3, "clouds_per_s": len(clouds) / gpu_s,
+           "mean_kept_points": float(counts.mean())}
+    try:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_lib
+        o = oracle_lib.Oracle()
+        a = time.perf_counter()
+        ref, _ = o.adaptive_voxel_filter_masks(clouds, 0.5, 200, 50.0)
+        cpu_s = time.perf_counter() - a
+        res["cpu_clouds_per_s"] = len(clouds) / cpu_s
+        res["cpu_threads"] = 1
+        res["matches_oracle"] = bool((ref == d_keep.cpu().numpy().astype(bool)).all())
     except OSError:
         pass
     return res

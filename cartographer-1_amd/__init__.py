@@ -206,6 +206,10 @@ _SIGNATURES = {
                                                    C.c_int32, C.c_int32,
                                                    C.POINTER(AdaptiveVoxelFilterOptions),
                                                    C.c_void_p, C.c_void_p]),
+    "csm_grid2d_cropped_limits": (C.c_int, [C.POINTER(MapLimits), C.POINTER(C.c_uint16),
+                                            C.POINTER(C.c_int32), C.POINTER(MapLimits)]),
+    "csm_grid2d_crop": (C.c_int, [C.POINTER(MapLimits), C.POINTER(C.c_uint16),
+                                  C.POINTER(MapLimits), C.POINTER(C.c_uint16), C.c_int64]),
     "csm_strerror": (C.c_char_p, [C.c_int]),
 }
 
@@ -282,6 +286,21 @@ class ProbabilityGrid:
     def limits(self) -> MapLimits:
         return MapLimits(self.resolution, self.max_x, self.max_y, self.num_x_cells,
                          self.num_y_cells)
+
+
+def ComputeCroppedGrid(grid: "ProbabilityGrid") -> "ProbabilityGrid":
+    """Submap2D::Finish's crop (ProbabilityGrid::ComputeCroppedGrid,
+    probability_grid.cc:91-106) through csm_grid2d_crop."""
+    lib = load_library()
+    cells = np.ascontiguousarray(grid.cells, np.uint16)
+    lim = grid.limits()
+    out_lim = MapLimits()
+    out = np.zeros(max(cells.size, 1), np.uint16)
+    _check(lib.csm_grid2d_crop(C.byref(lim), _ptr(cells, C.c_uint16), C.byref(out_lim),
+                               _ptr(out, C.c_uint16), out.size), "csm_grid2d_crop")
+    nx, ny = out_lim.num_x_cells, out_lim.num_y_cells
+    return ProbabilityGrid(out_lim.resolution, out_lim.max_x, out_lim.max_y,
+                           out[:nx * ny].reshape(ny, nx).copy())
 
 
 @dataclass

@@ -310,6 +310,21 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
                            const csm_node3d* nodes, int32_t num_nodes, const csm_pair3d* pairs,
                            int64_t num_pairs, csm_result3d* results);
 
+/* ---- submap grid formats ---------------------------------------------------
+ * Submap2D::Finish (submap_2d.cc:146-150) crops a finished submap's grid to
+ * its known cells: ProbabilityGrid::ComputeCroppedGrid
+ * (probability_grid.cc:91-106) with Grid2D::ComputeCroppedLimits
+ * (grid_2d.cc:110-120). `cells` are num_x_cells * num_y_cells uint16 values
+ * (x fastest); the known box is the bounding box of the nonzero cells.
+ * csm_grid2d_cropped_limits returns the cropped MapLimits and the offset
+ * (x, y) of its first cell; csm_grid2d_crop also copies the cells into
+ * cropped_cells (capacity >= cropped nx * ny). An all-unknown grid crops to
+ * one unknown cell, as the reference does. Host-only. */
+int csm_grid2d_cropped_limits(const csm_map_limits* limits, const uint16_t* cells,
+                              int32_t* offset_xy, csm_map_limits* cropped);
+int csm_grid2d_crop(const csm_map_limits* limits, const uint16_t* cells,
+                    csm_map_limits* cropped, uint16_t* cropped_cells, int64_t capacity);
+
 /* ---- node clouds: voxel filters -------------------------------------------
  * sensor::VoxelFilter and sensor::AdaptiveVoxelFilter
  * (sensor/internal/voxel_filter.h, voxel_filter.cc:212-232 and :263-268), the

@@ -303,6 +303,13 @@ void oracle_grid_set_probability(void* g, int32_t x, int32_t y, float p) {
   static_cast<ProbabilityGrid*>(g)->SetProbability(Idx2{x, y}, p);
 }
 
+// Submap2D::Finish (submap_2d.cc:146-150): replaces the grid by
+// ComputeCroppedGrid(), cropped to the known box its updates tracked.
+void oracle_grid_crop(void* g) {
+  ProbabilityGrid* grid = static_cast<ProbabilityGrid*>(g);
+  *grid = grid->ComputeCroppedGrid();
+}
+
 // info: resolution, max_x, max_y; cells: nx, ny.
 void oracle_grid_info(void* g, double* info, int32_t* cells) {
   const MapLimits& l = static_cast<ProbabilityGrid*>(g)->limits();

@@ -39,6 +39,7 @@ class Oracle:
             "oracle_grid_destroy": (None, [VP]),
             "oracle_grid_insert": (None, [VP, F, F, I32, P(F), P(F), I32]),
             "oracle_grid_set_probability": (None, [VP, I32, I32, F]),
+            "oracle_grid_crop": (None, [VP]),
             "oracle_grid_info": (None, [VP, P(D), P(I32)]),
             "oracle_grid_cells": (None, [VP, P(C.c_uint16)]),
             "oracle_transform_cloud_2d": (None, [P(F), P(F), I32, P(F)]),
@@ -58,24 +59,30 @@ class Oracle:
         self.lib = lib
 
     # ---- grids ---------------------------------------------------------
-    def grid_from_inserts(self, res, max_x, max_y, nx, ny, inserts, hit=0.7, miss=0.4):
+    def grid_from_inserts(self, res, max_x, max_y, nx, ny, inserts, hit=0.7, miss=0.4,
+                          crop=False):
         """Grid built with the restated ProbabilityGridRangeDataInserter2D.
-        inserts: list of (origin xyz, returns (n,3)). Returns (limits, cells)."""
+        inserts: list of (origin xyz, returns (n,3)). Returns (limits, cells);
+        crop=True finishes it like Submap2D::Finish (ComputeCroppedGrid)."""
         g = self.lib.oracle_grid_create(res, max_x, max_y, nx, ny)
         try:
             for origin, ret in inserts:
                 o = np.asarray(origin, np.float32)
                 r = np.ascontiguousarray(ret, np.float32)
                 self.lib.oracle_grid_insert(g, hit, miss, 1, _p(o, F), _p(r, F), len(r))
+            if crop:
+                self.lib.oracle_grid_crop(g)
             return self._grid_out(g)
         finally:
             self.lib.oracle_grid_destroy(g)
 
-    def grid_from_probabilities(self, res, max_x, max_y, nx, ny, cells_xy_p):
+    def grid_from_probabilities(self, res, max_x, max_y, nx, ny, cells_xy_p, crop=False):
         g = self.lib.oracle_grid_create(res, max_x, max_y, nx, ny)
         try:
             for x, y, p in cells_xy_p:
                 self.lib.oracle_grid_set_probability(g, int(x), int(y), float(p))
+            if crop:
+                self.lib.oracle_grid_crop(g)
             return self._grid_out(g)
         finally:
             self.lib.oracle_grid_destroy(g)
