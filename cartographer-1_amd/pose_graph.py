@@ -1,0 +1,157 @@
+"""The constraint-search half of PoseGraph2D: which (node, submap) pairs reach
+the ConstraintBuilder2D, local or global, in the reference's order.
+
+Python mirror of include/cartographer_amd/pose_graph_2d_search.h, following
+mapping/internal/2d/pose_graph_2d.cc: ComputeConstraintsForNode (:304-402),
+ComputeConstraint (:260-302), GetLatestNodeTime (:404-416),
+UpdateTrajectoryConnectivity (:418-425, applied to found constraints at
+:478-482), and trajectory_connectivity_state.cc / connected_components.cc.
+Global poses (the optimization problem's, :293-297) are supplied by the caller.
+"""
+import math
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Set, Tuple
+
+from .constraint_builder import FixedRatioSampler, rigid2d_compose, rigid2d_inverse
+
+TIME_MIN = -math.inf  # common::Time::min()
+
+
+@dataclass
+class PoseGraphSearchOptions:
+    """proto::PoseGraphOptions fields read here (pose_graph.lua:79-80)."""
+    global_sampling_ratio: float = 0.003
+    global_constraint_search_after_n_seconds: float = 10.0
+
+
+class TrajectoryConnectivityState:
+    def __init__(self):
+        self._forest: Dict[int, int] = {}
+        self._last: Dict[Tuple[int, int], float] = {}
+
+    def Add(self, trajectory_id: int):
+        self._forest.setdefault(trajectory_id, trajectory_id)
+
+    def _find(self, i: int) -> int:
+        root = i
+        while self._forest[root] != root:
+            root = self._forest[root]
+        while self._forest[i] != root:  # path compression
+            self._forest[i], i = root, self._forest[i]
+        return root
+
+    def _component(self, i: int) -> List[int]:
+        self._forest.setdefault(i, i)
+        s = self._find(i)
+        return [t for t in sorted(self._forest) if self._find(t) == s]
+
+    def TransitivelyConnected(self, a: int, b: int) -> bool:
+        if a == b:
+            return True
+        if a not in self._forest or b not in self._forest:
+            return False
+        return self._find(a) == self._find(b)
+
+    def Connect(self, a: int, b: int, time: float):
+        if self.TransitivelyConnected(a, b):
+            key = (min(a, b), max(a, b))
+            if self._last.get(key, TIME_MIN) < time:
+                self._last[key] = time
+        else:
+            for ia in self._component(a):
+                for ib in self._component(b):
+                    self._last[(min(ia, ib), max(ia, ib))] = time
+        self._forest.setdefault(a, a)
+        self._forest.setdefault(b, b)
+        self._forest[self._find(a)] = self._find(b)
+
+    def LastConnectionTime(self, a: int, b: int) -> float:
+        return self._last.get((min(a, b), max(a, b)), TIME_MIN)
+
+
+@dataclass
+class _SubmapData:
+    submap: object
+    global_pose: Tuple[float, float, float]
+    node_ids: Set[Tuple[int, int]] = field(default_factory=set)
+    finished: bool = False
+
+
+@dataclass
+class _NodeData:
+    time: float
+    global_pose: Tuple[float, float, float]
+    cloud: object
+
+
+class PoseGraph2DConstraintSearch:
+    def __init__(self, options: PoseGraphSearchOptions, builder):
+        self.options = options
+        self.builder = builder
+        self._submaps: Dict[Tuple[int, int], _SubmapData] = {}
+        self._nodes: Dict[Tuple[int, int], _NodeData] = {}
+        self._samplers: Dict[int, FixedRatioSampler] = {}
+        self.connectivity = TrajectoryConnectivityState()
+        self.local_searches = 0
+        self.global_searches = 0
+
+    def _add_trajectory(self, trajectory_id: int):
+        if trajectory_id not in self._samplers:
+            self.connectivity.Add(trajectory_id)
+            self._samplers[trajectory_id] = FixedRatioSampler(self.options.global_sampling_ratio)
+
+    def AddSubmap(self, submap_id, submap, global_pose):
+        submap_id = tuple(submap_id)
+        self._add_trajectory(submap_id[0])
+        self._submaps[submap_id] = _SubmapData(submap, tuple(global_pose))
+
+    def AddNode(self, node_id, time: float, global_pose, cloud, insertion_submaps,
+                newly_finished_submap: bool):
+        """ComputeConstraintsForNode (pose_graph_2d.cc:304-402)."""
+        node_id = tuple(node_id)
+        insertion_submaps = [tuple(s) for s in insertion_submaps]
+        self._add_trajectory(node_id[0])
+        self._nodes[node_id] = _NodeData(time, tuple(global_pose), cloud)
+        for s in insertion_submaps:
+            self._submaps[s].node_ids.add(node_id)
+        finished = [s for s in sorted(self._submaps) if self._submaps[s].finished]
+        newly_finished_nodes: Set = set()
+        if newly_finished_submap:
+            d = self._submaps[insertion_submaps[0]]
+            d.finished = True
+            newly_finished_nodes = set(d.node_ids)
+        for s in finished:
+            self._compute_constraint(node_id, s)
+        if newly_finished_submap:
+            for n in sorted(self._nodes):
+                if n not in newly_finished_nodes:
+                    self._compute_constraint(n, insertion_submaps[0])
+        self.builder.NotifyEndOfNode()
+
+    def HandleConstraints(self, constraints):
+        """UpdateTrajectoryConnectivity for each found loop closure (:478-482)."""
+        for c in constraints:
+            nid, sid = tuple(c.node_id), tuple(c.submap_id)
+            self.connectivity.Connect(nid[0], sid[0], self._latest_node_time(nid, sid))
+
+    def _latest_node_time(self, node_id, submap_id) -> float:
+        t = self._nodes[node_id].time
+        ids = self._submaps[submap_id].node_ids
+        if ids:
+            t = max(t, self._nodes[max(ids)].time)
+        return t
+
+    def _compute_constraint(self, node_id, submap_id):
+        """ComputeConstraint (pose_graph_2d.cc:260-302)."""
+        node_time = self._latest_node_time(node_id, submap_id)
+        last = self.connectivity.LastConnectionTime(node_id[0], submap_id[0])
+        s, n = self._submaps[submap_id], self._nodes[node_id]
+        if node_id[0] == submap_id[0] or \
+                node_time < last + self.options.global_constraint_search_after_n_seconds:
+            self.local_searches += 1
+            self.builder.MaybeAddConstraint(
+                submap_id, s.submap, node_id, n.cloud,
+                rigid2d_compose(rigid2d_inverse(s.global_pose), n.global_pose))
+        elif self._samplers[node_id[0]].Pulse():
+            self.global_searches += 1
+            self.builder.MaybeAddGlobalConstraint(submap_id, s.submap, node_id, n.cloud)
