@@ -248,38 +248,33 @@ def voxel_filter_bench(csm, ctx, world, args):
     C2 node clouds as one device-resident batch: the step that makes the
     clouds the loop-closure search uses (local_trajectory_builder_2d.cc:229-231)."""
     import ctypes as C
-    import torch
     clouds = [world.cloud(n) for n in range(args.nodes)]
     pts = np.ascontiguousarray(np.concatenate(clouds), np.float32)
     offsets = np.zeros(len(clouds) + 1, np.int64)
     offsets[1:] = np.cumsum([len(c) for c in clouds])
-    dev = torch.device("cuda", torch.cuda.current_device())
-    d_pts = torch.from_numpy(pts).to(dev)
-    d_off = torch.from_numpy(offsets).to(dev)
-    d_keep = torch.zeros(len(pts), dtype=torch.uint8, device=dev)
-    d_cnt = torch.zeros(len(clouds), dtype=torch.int32, device=dev)
+    d_pts, d_off = csm.DeviceBuffer(pts), csm.DeviceBuffer(offsets)
+    d_keep = csm.DeviceBuffer(nbytes=len(pts))
+    d_cnt = csm.DeviceBuffer(nbytes=4 * len(clouds))
     opts = csm.AdaptiveVoxelFilterOptions.make(0.5, 200, 50.0)
     lib = ctx._lib
     max_pts = int(np.diff(offsets).max())
-    stream = torch.cuda.ExternalStream(ctx.stream)
-    torch.cuda.synchronize()
 
     def launch():
         csm._check(lib.csm_adaptive_voxel_filter_device(
-            ctx.handle, C.c_void_p(d_pts.data_ptr()), C.c_void_p(d_off.data_ptr()), len(clouds),
-            max_pts, C.byref(opts), C.c_void_p(d_keep.data_ptr()), C.c_void_p(d_cnt.data_ptr())),
-            "csm_adaptive_voxel_filter_device")
+            ctx.handle, d_pts.ptr, d_off.ptr, len(clouds), max_pts, C.byref(opts), d_keep.ptr,
+            d_cnt.ptr), "csm_adaptive_voxel_filter_device")
 
     for _ in range(3):
         launch()
-    stream.synchronize()
+    csm.synchronize(ctx)
     reps = 20
     a = time.perf_counter()
     for _ in range(reps):
         launch()
-    stream.synchronize()
+    csm.synchronize(ctx)
     gpu_s = (time.perf_counter() - a) / reps
-    counts = d_cnt.cpu().numpy()
+    counts = d_cnt.to_numpy(np.int32, len(clouds))
+    keep = d_keep.to_numpy(np.uint8, len(pts)).astype(bool)
     res = {"workload": f"AdaptiveVoxelFilter(max_length 0.5, min_num_points 200, max_range 50) "
                        f"over {len(clouds)} clouds x {max_pts} points",
            "gpu_ms_per_batch": gpu_s * 1e3, "clouds_per_s": len(clouds) / gpu_s,
@@ -293,7 +288,7 @@ def voxel_filter_bench(csm, ctx, world, args):
         cpu_s = time.perf_counter() - a
         res["cpu_clouds_per_s"] = len(clouds) / cpu_s
         res["cpu_threads"] = 1
-        res["matches_oracle"] = bool((ref == d_keep.cpu().numpy().astype(bool)).all())
+        res["matches_oracle"] = bool((ref == keep).all())
     except OSError:
         pass
     return res

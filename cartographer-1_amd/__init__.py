@@ -709,3 +709,59 @@ def AdaptiveVoxelFilter(point_cloud, options: AdaptiveVoxelFilterOptions, intens
     if intensities is None:
         return pts[keep]
     return pts[keep], np.asarray(intensities, np.float32)[keep[:len(intensities)]]
+
+
+# --------------------------------------------------------------------------
+# Device buffers for the *_device entry points (bench / tests), allocated with
+# the HIP runtime libcsm_amd.so itself links (same soname, same instance).
+
+_hip_handle = None
+
+
+def _hip():
+    global _hip_handle
+    if _hip_handle is None:
+        load_library()
+        h = C.CDLL("libamdhip64.so.7")
+        h.hipMalloc.argtypes = [C.POINTER(C.c_void_p), C.c_size_t]
+        h.hipFree.argtypes = [C.c_void_p]
+        h.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+        h.hipStreamSynchronize.argtypes = [C.c_void_p]
+        _hip_handle = h
+    return _hip_handle
+
+
+class DeviceBuffer:
+    """hipMalloc'd bytes holding a copy of a numpy array (or zeros)."""
+
+    def __init__(self, array: np.ndarray = None, nbytes: int = 0):
+        self.nbytes = int(array.nbytes if array is not None else nbytes)
+        self.ptr = C.c_void_p()
+        if _hip().hipMalloc(C.byref(self.ptr), max(self.nbytes, 1)) != 0:
+            raise CsmError("hipMalloc failed")
+        if array is not None and self.nbytes:
+            a = np.ascontiguousarray(array)
+            if _hip().hipMemcpy(self.ptr, a.ctypes.data, self.nbytes, 1) != 0:  # H2D
+                raise CsmError("hipMemcpy failed")
+
+    def to_numpy(self, dtype, count) -> np.ndarray:
+        out = np.empty(count, dtype)
+        if out.nbytes and _hip().hipMemcpy(out.ctypes.data, self.ptr, out.nbytes, 2) != 0:  # D2H
+            raise CsmError("hipMemcpy failed")
+        return out
+
+    def free(self):
+        if self.ptr:
+            _hip().hipFree(self.ptr)
+            self.ptr = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def synchronize(context: "Context"):
+    if _hip().hipStreamSynchronize(C.c_void_p(context.stream)) != 0:
+        raise CsmError("hipStreamSynchronize failed")
