@@ -21,6 +21,14 @@ hipError_t LaunchRt3dScore(int num_rot, hipStream_t st, const float* prob, const
                            float res, const float* points, int n, const float4* rot,
                            const float* rot_angle, const float4* trans, int num_trans, int t_base,
                            double wt, double wr, unsigned long long* best);
+// rt3d_score2 over a brick padded by one 0.1 cell per side (LaunchPadProbBrick
+// builds it); gb is the unpadded brick. num_trans <= kRt3dThreads.
+hipError_t LaunchPadProbBrick(const float* prob, const Brick3& gb, float* out, hipStream_t st);
+hipError_t LaunchRt3dScore2( int num_rot, hipStream_t st, const float* pad,
+                            const Brick3& gb, float res, const float* points, int n,
+                            const float4* rot, const float* rot_angle, const float4* trans,
+                            int num_trans, int t_base, double wt, double wr,
+                            unsigned long long* best);
 // Items [item_begin, item_begin + num_items) of the yaw list; `large`
 // selects the build for clouds of more than kSmall3dPoints points.
 hipError_t LaunchFast3dSearch(bool large, int grid, hipStream_t st, const Submap3Desc* submaps,

@@ -168,6 +168,8 @@ struct csm_hybrid_grid {
   Brick3 brick{};
   DevBuf values;  // uint16 brick
   DevBuf prob;    // float probability brick
+  DevBuf prob_pad;  // the same padded by one 0.1 cell per side (RTCSM3D), built on first use
+  bool prob_pad_ready = false;
 };
 
 int csm_hybrid_grid_create(csm_context* ctx, float resolution, const int32_t* ijk,
@@ -316,14 +318,35 @@ int csm_rt3d_match(csm_context* ctx, const csm_rt_options* o, const csm_hybrid_g
   CSM_HIP(hipMemcpyAsync(ctx->rt3_points.ptr, xyz, sizeof(float) * 3 * n, hipMemcpyHostToDevice,
                          st));
   CSM_HIP(hipMemsetAsync(ctx->rt3_best.ptr, 0, sizeof(unsigned long long), st));
+  const Brick3& gb = grid->brick;
+  // v2 addresses the padded brick with 24-bit row products and a 32-bit byte
+  // offset; larger bricks take the v1 kernel.
+  const bool v2 = !std::getenv("CSM_RT3D_V1") &&
+                  static_cast<int64_t>(gb.nx + 2) * (gb.ny + 2) * (gb.nz + 2) < (int64_t{1} << 29) &&
+                  static_cast<int64_t>(gb.ny + 2) * (gb.nz + 2) < (int64_t{1} << 24);
+  if (v2 && !grid->prob_pad_ready) {
+    csm_hybrid_grid* g = const_cast<csm_hybrid_grid*>(grid);
+    if ((rc = g->prob_pad.Reserve(sizeof(float) * (gb.nx + 2) * (gb.ny + 2) * (gb.nz + 2))))
+      return rc;
+    CSM_HIP(LaunchPadProbBrick(grid->prob.as<float>(), gb, g->prob_pad.as<float>(), st));
+    g->prob_pad_ready = true;
+  }
+
   if (ctx->timing) CSM_HIP(hipEventRecord(ctx->ev0, st));
   for (int64_t t0 = 0; t0 < num_trans; t0 += kRt3dThreads) {
     const int cnt = static_cast<int>(std::min<int64_t>(kRt3dThreads, num_trans - t0));
-    CSM_HIP(LaunchRt3dScore(static_cast<int>(num_rot), st, grid->prob.as<float>(), grid->brick,
-                            res, ctx->rt3_points.as<float>(), n, drot, dangle,
-                            ctx->rt3_trans.as<float4>(), cnt, static_cast<int>(t0),
-                            o->translation_delta_cost_weight, o->rotation_delta_cost_weight,
-                            ctx->rt3_best.as<unsigned long long>()));
+    if (v2)
+      CSM_HIP(LaunchRt3dScore2(static_cast<int>(num_rot), st, grid->prob_pad.as<float>(), gb, res,
+                               ctx->rt3_points.as<float>(), n, drot, dangle,
+                               ctx->rt3_trans.as<float4>(), cnt, static_cast<int>(t0),
+                               o->translation_delta_cost_weight, o->rotation_delta_cost_weight,
+                               ctx->rt3_best.as<unsigned long long>()));
+    else
+      CSM_HIP(LaunchRt3dScore(static_cast<int>(num_rot), st, grid->prob.as<float>(), gb, res,
+                              ctx->rt3_points.as<float>(), n, drot, dangle,
+                              ctx->rt3_trans.as<float4>(), cnt, static_cast<int>(t0),
+                              o->translation_delta_cost_weight, o->rotation_delta_cost_weight,
+                              ctx->rt3_best.as<unsigned long long>()));
   }
   if (ctx->timing) CSM_HIP(hipEventRecord(ctx->ev1, st));
   unsigned long long key = 0;

@@ -183,6 +183,145 @@ rt3d_score(const float* __restrict__ prob, Brick3 gb, float res, float inv,
   }
 }
 
+// RTCSM3D, v2. Same candidates, sums and key as rt3d_score, cheaper per lookup:
+//  * the probability brick is padded by one cell of 0.1 (the unknown / outside
+//    probability) on every side, so a lookup clamps each cell coordinate into
+//    [-1, n] (v_med3) instead of testing bounds and selecting the default;
+//  * the cell coordinate is rint(v * (1 / res)), and the exact IEEE quotient
+//    (RoundDiv) is taken only for points whose product lies within 2^-21 |y|
+//    of a half-integer, where the product's error could change the rounding
+//    decision (RoundFast);
+//  * two rotations per workgroup (2 x 343 = 686 of 704 lanes busy at C4's
+//    7^3 translations, against 343 of 384).
+constexpr int kRt3Rpb = 2;
+
+__global__ void pad_prob_brick(const float* __restrict__ prob, Brick3 gb, float* __restrict__ out) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const int px = gb.nx + 2, py = gb.ny + 2, pz = gb.nz + 2;
+  if (i >= static_cast<int64_t>(px) * py * pz) return;
+  const int x = static_cast<int>(i % px) - 1;
+  const int y = static_cast<int>((i / px) % py) - 1;
+  const int z = static_cast<int>(i / (static_cast<int64_t>(px) * py)) - 1;
+  float v = 0.1f;
+  if (x >= 0 && x < gb.nx && y >= 0 && y < gb.ny && z >= 0 && z < gb.nz)
+    v = prob[(static_cast<int64_t>(z) * gb.ny + y) * gb.nx + x];
+  out[i] = v;
+}
+
+// rint(v * inv) as a float; flags products too close to a half-integer.
+// y = fl(v * fl(1 / res)) is within 2^-23 |x| of x = v / res, and fl(x) within
+// half an ulp (<= 2^-24 |x|) of x, so when y lies more than 2^-21 |y| from a
+// half-integer h, fl(x) lies strictly on y's side of h and lround(fl(x)) =
+// rint(y).
+__device__ __forceinline__ float RoundFast(float v, float inv, bool* risky) {
+  const float y = __fmul_rn(v, inv);
+  const float r = rintf(y);
+  const float d = fabsf(__fsub_rn(y, r));
+  *risky |= fmaf(fabsf(y), 4.7683716e-7f, d) >= 0.5f;
+  return r;
+}
+
+__global__ void __launch_bounds__(768)
+rt3d_score2(const float* __restrict__ pad, int pnx, int pny, int pnz, int ox, int oy, int oz,
+            float res, float inv, const float* __restrict__ points, int n,
+            const float4* __restrict__ rot, const float* __restrict__ rot_angle,
+            const float4* __restrict__ trans, int num_trans, int t_base, int num_rot, double wt,
+            double wr, unsigned long long* __restrict__ best) {
+  __shared__ float4 rp[kRt3Rpb][kRt3Tile];
+  __shared__ unsigned long long red[768 / 64];
+  const int tid = threadIdx.x;
+  const int sub = tid / num_trans;
+  const int t = tid - sub * num_trans;
+  const int r = blockIdx.x * kRt3Rpb + sub;
+  const bool active = sub < kRt3Rpb && r < num_rot;
+  const float4 tr = active ? trans[t] : make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4* my = rp[active ? sub : 0];
+  // Cell (ix, iy, iz) lives at padded index ((iz + 1 - oz) * pny + iy + 1 - oy) * pnx + ix + 1 - ox,
+  // each coordinate clamped to the padded box (exact in float: |coordinates| < 2^24).
+  const float bx = static_cast<float>(1 - ox), by = static_cast<float>(1 - oy),
+              bz = static_cast<float>(1 - oz);
+  const float mx = static_cast<float>(pnx - 1), my_ = static_cast<float>(pny - 1),
+              mz = static_cast<float>(pnz - 1);
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(pad), 0, static_cast<int>(4u * pnx * pny * pnz), 0x00020000);
+  float sum = 0.f;
+  for (int base = 0; base < n; base += kRt3Tile) {
+    const int cnt = min(kRt3Tile, n - base);
+    __syncthreads();
+    for (int i = tid; i < kRt3Rpb * cnt; i += blockDim.x) {
+      const int s = i / cnt, j = i - s * cnt;
+      const int rr = min(blockIdx.x * kRt3Rpb + s, num_rot - 1);
+      const float4 q = rot[rr];
+      const float* p = points + 3 * static_cast<int64_t>(base + j);
+      float ox_, oy_, oz_;
+      Rotate3(q.w, q.x, q.y, q.z, p[0], p[1], p[2], &ox_, &oy_, &oz_);
+      rp[s][j] = make_float4(ox_, oy_, oz_, 0.f);
+    }
+    __syncthreads();
+    if (active) {
+      auto cell = [&](const float4& a, bool* risky, float* f) {
+        f[0] = RoundFast(__fadd_rn(a.x, tr.x), inv, risky);
+        f[1] = RoundFast(__fadd_rn(a.y, tr.y), inv, risky);
+        f[2] = RoundFast(__fadd_rn(a.z, tr.z), inv, risky);
+      };
+      auto exact = [&](const float4& a, float* f) {  // rare: the IEEE quotient decides
+        f[0] = static_cast<float>(RoundDiv(__fadd_rn(a.x, tr.x), res, inv));
+        f[1] = static_cast<float>(RoundDiv(__fadd_rn(a.y, tr.y), res, inv));
+        f[2] = static_cast<float>(RoundDiv(__fadd_rn(a.z, tr.z), res, inv));
+      };
+      auto load = [&](const float* f) {
+        const unsigned cx = static_cast<unsigned>(__builtin_amdgcn_fmed3f(__fadd_rn(f[0], bx), 0.f, mx));
+        const unsigned cy = static_cast<unsigned>(__builtin_amdgcn_fmed3f(__fadd_rn(f[1], by), 0.f, my_));
+        const unsigned cz = static_cast<unsigned>(__builtin_amdgcn_fmed3f(__fadd_rn(f[2], bz), 0.f, mz));
+        const unsigned k = __umul24(__umul24(cz, pny) + cy, pnx) + cx;
+        return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, k << 2, 0, 0));
+      };
+      // One point per step: batching 2 or 4 points' loads, software-pipelining
+      // the loads one point ahead, or a 4 x 4 x 2 tiled brick were all slower
+      // on C4 (8.9, 7.4 and 8.3 s against 6.6-6.9 s). The exact
+      // path re-reads the point from LDS inside its own loop: this shape
+      // compiled to the fastest schedule measured (6.9 s; 7.6 s reusing `a`).
+      for (int i = 0; i + 1 <= cnt; i += 1) {
+        float4 a[1];
+        a[0] = my[i];
+        bool risky = false;
+        float f[1][3];
+        cell(a[0], &risky, f[0]);
+        if (risky) {
+#pragma unroll 1
+          for (int u = 0; u < 1; ++u) {
+            float g[3];
+            exact(my[i + u], g);
+            f[0][0] = g[0];
+            f[0][1] = g[1];
+            f[0][2] = g[2];
+          }
+        }
+        sum = __fadd_rn(sum, load(f[0]));
+      }
+    }
+  }
+  unsigned long long key = 0;
+  if (active) {
+    float score = __fdiv_rn(sum, static_cast<float>(n));
+    const double e = static_cast<double>(tr.w) * wt + static_cast<double>(rot_angle[r]) * wr;
+    score = static_cast<float>(static_cast<double>(score) * exp(-(e * e)));
+    const unsigned idx = static_cast<unsigned>(t_base + t) * static_cast<unsigned>(num_rot) + r;
+    key = (static_cast<unsigned long long>(__float_as_uint(score)) << 32) | (0xffffffffu - idx);
+  }
+  for (int m = 32; m > 0; m >>= 1) {
+    const unsigned long long o = __shfl_xor(key, m, 64);
+    key = o > key ? o : key;
+  }
+  if ((tid & 63) == 0) red[tid >> 6] = key;
+  __syncthreads();
+  if (tid == 0) {
+    unsigned long long k = red[0];
+    for (int w = 1; w < static_cast<int>(blockDim.x / 64); ++w) k = red[w] > k ? red[w] : k;
+    atomicMax(best, k);
+  }
+}
+
 // ------------------------------------------------------------ FastCSM3D ----
 //
 // Persistent workgroups pull (pair, yaw) items from a global counter. Per
@@ -1138,6 +1277,26 @@ hipError_t LaunchRt3dScore(int num_rot, hipStream_t st, const float* prob, const
   hipLaunchKernelGGL(rt3d_score, dim3(num_rot), dim3(kRt3Threads), 0, st, prob, gb, res,
                      1.f / res, points, n, rot, rot_angle, trans + t_base, num_trans, t_base,
                      num_rot, wt, wr, best);
+  return hipGetLastError();
+}
+
+hipError_t LaunchPadProbBrick(const float* prob, const Brick3& gb, float* out, hipStream_t st) {
+  const int64_t total = static_cast<int64_t>(gb.nx + 2) * (gb.ny + 2) * (gb.nz + 2);
+  hipLaunchKernelGGL(pad_prob_brick, dim3(static_cast<unsigned>((total + 255) / 256)), dim3(256), 0,
+                     st, prob, gb, out);
+  return hipGetLastError();
+}
+
+hipError_t LaunchRt3dScore2(int num_rot, hipStream_t st, const float* pad,
+                            const Brick3& gb, float res, const float* points, int n,
+                            const float4* rot, const float* rot_angle, const float4* trans,
+                            int num_trans, int t_base, double wt, double wr,
+                            unsigned long long* best) {
+  const int threads = (kRt3Rpb * num_trans + 63) / 64 * 64;
+  const int blocks = (num_rot + kRt3Rpb - 1) / kRt3Rpb;
+  hipLaunchKernelGGL(rt3d_score2, dim3(blocks), dim3(threads), 0, st, pad, gb.nx + 2, gb.ny + 2,
+                     gb.nz + 2, gb.ox, gb.oy, gb.oz, res, 1.f / res, points, n, rot, rot_angle,
+                     trans + t_base, num_trans, t_base, num_rot, wt, wr, best);
   return hipGetLastError();
 }
 
