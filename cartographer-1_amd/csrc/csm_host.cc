@@ -258,7 +258,8 @@ int RunBatch(csm_context* ctx, csm_fast2d* const* submaps, int32_t num_submaps,
     wq2.pair_order = wq.pair_order;
     wq2.chunk_prefix = wq.chunk_prefix;
     wq2.block_first = ctx->blocks.as<int32_t>();
-    const size_t dyn_lds = static_cast<size_t>(rc) * max_npad * 4;
+    // rot_chunk * npad cells (4 B) and run counts (1 B), 16-B aligned.
+    const size_t dyn_lds = (static_cast<size_t>(rc) * max_npad * 5 + 15) & ~size_t{15};
     const char* mixed_env = std::getenv("CSM_MIXED_LEVELS");
     const int mixed = mixed_env ? std::atoi(mixed_env) : 1;
     const int per_cu = std::max(1, std::min(8, static_cast<int>((160 * 1024) / (dyn_lds + 10 * 1024))));

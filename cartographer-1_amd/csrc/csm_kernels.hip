@@ -583,7 +583,9 @@ constexpr int kMaxRotChunk = 16;
 
 struct V4Shared {
   uint2 stack[kStack2];  // w0: xo | yo << 16; w1: sum | rot << 22 | level << 27
-  int part[kWaves][kBatchNodes][4];
+  int part[kBatchNodes][4];  // children sums, accumulated by the 4 waves (LDS atomics)
+  int n_eff;                  // run-list length shared by the chunk's rotations
+  int run_len[kMaxRotChunk];  // each rotation's own run-list length
   int node_xo[kBatchNodes], node_yo[kBatchNodes], node_rot[kBatchNodes], node_level[kBatchNodes];
   int nodes, done;
   int item_pair, item_chunk, queue;
@@ -599,8 +601,12 @@ struct V4Shared {
   unsigned long long lv_batches[kMaxLevels];
 };
 
-__device__ __forceinline__ void V4Score(V4Shared& sh, const uint32_t* pts, int npad, int n,
-                                        const SubmapDesc& sm) {
+// Scores the children of the batch's nodes over the chunk's run lists: entry
+// k of rotation r is a cell (pts) and the number of consecutive scan points
+// that fell into it (cnt, <= 255; 0 for padding). A child's sum is
+// sum_k cnt[k] * value, the reference's per-point sum regrouped.
+__device__ __forceinline__ void V4Score(V4Shared& sh, const uint32_t* pts, const uint8_t* cnt,
+                                        int npad, int n, const SubmapDesc& sm) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nodes = Uniform(sh.nodes);
   const int groups = 64 / nodes;
@@ -616,6 +622,7 @@ __device__ __forceinline__ void V4Score(V4Shared& sh, const uint32_t* pts, int n
   const int pws4 = sm.quad_pws[level] * 4, ps4 = sm.quad_pws[level] * sm.quad_pph[level] * 4;
   const __amdgpu_buffer_rsrc_t rsrc = LevelRsrc(sm.pyramid_base, Uniform(sm.pyramid_bytes));
   const uint32_t* P = pts + sh.node_rot[node] * npad;
+  const uint8_t* Cn = cnt + sh.node_rot[node] * npad;
   const int cx = sh.node_xo[node] + (h - 1) + h;
   const int cy = sh.node_yo[node] + (h - 1) + h;
   const int quarter = (n + kWaves - 1) / kWaves;
@@ -623,47 +630,44 @@ __device__ __forceinline__ void V4Score(V4Shared& sh, const uint32_t* pts, int n
   constexpr int kOOB = 0x7ffffff0;
   constexpr int U = 8;
   uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+  auto address = [&](uint32_t p, bool in) {
+    const int X = static_cast<int16_t>(p & 0xffff) + cx;
+    const int Y = (static_cast<int>(p) >> 16) + cy;
+    const bool valid = in && static_cast<unsigned>(X) < static_cast<unsigned>(qw) &&
+                       static_cast<unsigned>(Y) < static_cast<unsigned>(qh);
+    const int a = __umul24((((Y & pmask) << sft) | (X & pmask)), ps4) + qoff;
+    const int b = __umul24(Y >> sft, pws4) + a;
+    return valid ? ((X >> sft) << 2) + b : kOOB;
+  };
+  // v_dot4_u32_u8 with the run count in one byte of the weight multiplies
+  // that child's byte by the count and accumulates.
+  auto accumulate = [&](uint32_t v, uint32_t c) {
+    a0 = __builtin_amdgcn_udot4(v, c, a0, false);
+    a1 = __builtin_amdgcn_udot4(v, c << 8, a1, false);
+    a2 = __builtin_amdgcn_udot4(v, c << 16, a2, false);
+    a3 = __builtin_amdgcn_udot4(v, c << 24, a3, false);
+  };
   int i = s;
   for (; i + U * groups <= e; i += U * groups) {
     int ad[U];
+    uint32_t c[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const uint32_t p = P[i + u * groups + g];
-      const int X = static_cast<int16_t>(p & 0xffff) + cx;
-      const int Y = (static_cast<int>(p) >> 16) + cy;
-      const bool valid = static_cast<unsigned>(X) < static_cast<unsigned>(qw) &&
-                         static_cast<unsigned>(Y) < static_cast<unsigned>(qh);
-      const int a = __umul24((((Y & pmask) << sft) | (X & pmask)), ps4) + qoff;
-      const int b = __umul24(Y >> sft, pws4) + a;
-      ad[u] = valid ? ((X >> sft) << 2) + b : kOOB;
+      ad[u] = address(P[i + u * groups + g], true);
+      c[u] = Cn[i + u * groups + g];
     }
     uint32_t v[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) v[u] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, ad[u], 0, 0);
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      // v_dot4_u32_u8 with a one-hot weight picks one byte and accumulates.
-      a0 = __builtin_amdgcn_udot4(v[u], 0x00000001u, a0, false);
-      a1 = __builtin_amdgcn_udot4(v[u], 0x00000100u, a1, false);
-      a2 = __builtin_amdgcn_udot4(v[u], 0x00010000u, a2, false);
-      a3 = __builtin_amdgcn_udot4(v[u], 0x01000000u, a3, false);
-    }
+    for (int u = 0; u < U; ++u) accumulate(v[u], c[u]);
   }
   for (; i < e; i += groups) {
     const int idx = i + g;
-    const uint32_t p = idx < e ? P[idx] : 0x80008000u;
-    const int X = static_cast<int16_t>(p & 0xffff) + cx;
-    const int Y = (static_cast<int>(p) >> 16) + cy;
-    const bool valid = idx < e && static_cast<unsigned>(X) < static_cast<unsigned>(qw) &&
-                       static_cast<unsigned>(Y) < static_cast<unsigned>(qh);
-    const int a = __umul24((((Y & pmask) << sft) | (X & pmask)), ps4) + qoff;
-    const int b = __umul24(Y >> sft, pws4) + a;
-    const uint32_t vv = __builtin_amdgcn_raw_buffer_load_b32(rsrc, valid ? ((X >> sft) << 2) + b : kOOB,
+    const bool in = idx < e;
+    const uint32_t vv = __builtin_amdgcn_raw_buffer_load_b32(rsrc, address(in ? P[idx] : 0u, in),
                                                              0, 0);
-    a0 = __builtin_amdgcn_udot4(vv, 0x00000001u, a0, false);
-    a1 = __builtin_amdgcn_udot4(vv, 0x00000100u, a1, false);
-    a2 = __builtin_amdgcn_udot4(vv, 0x00010000u, a2, false);
-    a3 = __builtin_amdgcn_udot4(vv, 0x01000000u, a3, false);
+    accumulate(vv, in ? Cn[idx] : 0u);
   }
   for (int m = nodes; m < 64; m <<= 1) {
     a0 += __shfl_xor(a0, m, 64);
@@ -672,14 +676,74 @@ __device__ __forceinline__ void V4Score(V4Shared& sh, const uint32_t* pts, int n
     a3 += __shfl_xor(a3, m, 64);
   }
   if (lane < nodes) {
-    sh.part[wave][lane][0] = a0;  // (xo,     yo)
-    sh.part[wave][lane][1] = a1;  // (xo,     yo + h)
-    sh.part[wave][lane][2] = a2;  // (xo + h, yo)
-    sh.part[wave][lane][3] = a3;  // (xo + h, yo + h)
+    atomicAdd(&sh.part[lane][0], static_cast<int>(a0));  // (xo,     yo)
+    atomicAdd(&sh.part[lane][1], static_cast<int>(a1));  // (xo,     yo + h)
+    atomicAdd(&sh.part[lane][2], static_cast<int>(a2));  // (xo + h, yo)
+    atomicAdd(&sh.part[lane][3], static_cast<int>(a3));  // (xo + h, yo + h)
   }
 }
 
-__global__ void __launch_bounds__(kSearchThreads)
+// Run lists (per rotation, in place): consecutive scan points that fall in
+// the same cell become one entry with their count. Wave w compacts rotations
+// w, w + 4, ...; a run longer than 255 points is split so counts fit a byte.
+// Writes each rotation's list length to lens[r]; returns this wave's longest
+// list (wave-uniform).
+__device__ int CompactRuns(uint32_t* pts, uint8_t* cnt, int npad, int n, int nrot, int* lens) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const unsigned long long below = (1ull << lane) - 1;
+  int longest = 0;
+  for (int r = wave; r < nrot; r += kWaves) {
+    uint32_t* P = pts + r * npad;
+    uint8_t* C = cnt + r * npad;
+    int out = 0;                // entries written so far
+    int run_start = 0;          // start of the run open at the block boundary
+    uint32_t last = 0;          // last cell of the previous block
+    int open_k = -1, open_pos = 0;  // the previous block's last entry, count pending
+    for (int base = 0; base < n; base += 64) {
+      const int i = base + lane;
+      const bool in = i < n;
+      const uint32_t v = in ? P[i] : 0u;
+      uint32_t prev = __shfl_up(v, 1, 64);
+      if (lane == 0) prev = last;
+      const bool head0 = in && (i == 0 || v != prev);
+      // Start of each lane's run: inclusive max-scan of head positions.
+      int rs = head0 ? i : -1;
+      for (int d = 1; d < 64; d <<= 1) {
+        const int o = __shfl_up(rs, d, 64);
+        if (lane >= d) rs = max(rs, o);
+      }
+      rs = max(rs, run_start);
+      const bool head = head0 || (in && (i - rs) % 255 == 0);
+      const unsigned long long hm = __ballot(head);
+      const int k = out + __popcll(hm & below);
+      // Close the entry left open by the previous block.
+      if (open_k >= 0 && hm) {
+        const int first = base + static_cast<int>(__ffsll(static_cast<long long>(hm))) - 1;
+        if (lane == 0) C[open_k] = static_cast<uint8_t>(first - open_pos);
+        open_k = -1;
+      }
+      if (head) {
+        const unsigned long long above = hm & ~(below | (1ull << lane));
+        P[k] = v;
+        if (above) C[k] = static_cast<uint8_t>(__ffsll(static_cast<long long>(above)) - 1 - lane);
+      }
+      if (hm) {
+        const int lastl = 63 - __clzll(hm);
+        open_k = out + __popcll(hm) - 1;
+        open_pos = base + lastl;
+      }
+      out += __popcll(hm);
+      run_start = __shfl(rs, 63, 64);
+      last = __shfl(v, 63, 64);
+    }
+    if (open_k >= 0 && lane == 0) C[open_k] = static_cast<uint8_t>(n - open_pos);
+    if (lane == 0) lens[r] = out;
+    longest = max(longest, out);
+  }
+  return longest;
+}
+
+__global__ void __launch_bounds__(kSearchThreads) __attribute__((amdgpu_waves_per_eu(5)))
 fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
                  const PairDesc* __restrict__ pairs,
                  const float* __restrict__ points,
@@ -690,10 +754,12 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
                  int32_t* __restrict__ status,
                  unsigned long long* __restrict__ stats,
                  int npad, int mixed_levels) {
-  extern __shared__ __align__(16) uint32_t pts[];  // rot_chunk * npad
+  extern __shared__ __align__(16) uint32_t pts[];  // rot_chunk * npad cells, then counts
   __shared__ V4Shared sh;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int rc = queues.rot_chunk;
+  uint8_t* cnt = reinterpret_cast<uint8_t*>(pts + rc * npad);
+  for (int k = tid; k < kBatchNodes * 4; k += kSearchThreads) sh.part[k >> 2][k & 3] = 0;
   unsigned long long local_cands = 0, local_lookups = 0;
 #ifdef CSM_KPROF
   long long kprof[4] = {0, 0, 0, 0};  // thread 0: discretize, control, score cycles; batches
@@ -774,6 +840,20 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
       }
     }
     if (range_error) sh.range_error = 1;
+    if (tid == 0) sh.n_eff = 0;
+    __syncthreads();
+    // ---- Run lists; pad every rotation to the longest with empty entries ----
+    {
+      const int longest = CompactRuns(pts, cnt, npad, n, nrot, sh.run_len);
+      if (lane == 0) atomicMax(&sh.n_eff, longest);
+    }
+    __syncthreads();
+    const int n_eff = Uniform(sh.n_eff);
+    for (int r = 0; r < nrot; ++r)  // past a rotation's own list: out-of-range cell, count 0
+      for (int k = sh.run_len[r] + tid; k < n_eff; k += kSearchThreads) {
+        pts[r * npad + k] = 0x80008000u;
+        cnt[r * npad + k] = 0;
+      }
     __syncthreads();
     // ---- ShrinkToFit per rotation; root counts ------------------------------
     if (tid < nrot) {
@@ -823,7 +903,8 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
           if (nd < pn) {
             clvl = sh.node_level[nd] - 1;
             const int h = 1 << clvl;
-            sum = sh.part[0][nd][c] + sh.part[1][nd][c] + sh.part[2][nd][c] + sh.part[3][nd][c];
+            sum = sh.part[nd][c];
+            sh.part[nd][c] = 0;
             r = sh.node_rot[nd];
             xo = sh.node_xo[nd] + ((c & 2) ? h : 0);
             yo = sh.node_yo[nd] + ((c & 1) ? h : 0);
@@ -1001,7 +1082,7 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
       const int done = Uniform(sh.done);
       if (done) break;
       if (nodes > 0) {
-        V4Score(sh, pts, npad, n, sm);
+        V4Score(sh, pts, cnt, npad, n_eff, sm);
         local_cands += 4 * nodes;
         local_lookups += static_cast<unsigned long long>(4 * nodes) * n;
         if (tid < nodes) {
