@@ -119,6 +119,23 @@ class Result3D(C.Structure):
                 ("rotational_score", C.c_float), ("low_resolution_score", C.c_float)]
 
 
+class CeresOptions2D(C.Structure):
+    """proto::CeresScanMatcherOptions2D; defaults pose_graph.lua:30-39."""
+    _fields_ = [("occupied_space_weight", C.c_double), ("translation_weight", C.c_double),
+                ("rotation_weight", C.c_double), ("max_num_iterations", C.c_int32)]
+
+    @staticmethod
+    def make(occupied_space_weight=20.0, translation_weight=10.0, rotation_weight=1.0,
+             max_num_iterations=10) -> "CeresOptions2D":
+        return CeresOptions2D(occupied_space_weight, translation_weight, rotation_weight,
+                              max_num_iterations)
+
+
+class Refine2D(C.Structure):
+    _fields_ = [("submap", C.c_int32), ("scan", C.c_int32), ("initial", Pose2D),
+                ("target_x", C.c_double), ("target_y", C.c_double)]
+
+
 class AdaptiveVoxelFilterOptions(C.Structure):
     """proto::AdaptiveVoxelFilterOptions (all floats); defaults are
     trajectory_builder_2d.lua:25-29's adaptive_voxel_filter."""
@@ -206,6 +223,10 @@ _SIGNATURES = {
                                                    C.c_int32, C.c_int32,
                                                    C.POINTER(AdaptiveVoxelFilterOptions),
                                                    C.c_void_p, C.c_void_p]),
+    "csm_ceres2d_refine_batch": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.c_int32,
+                                           C.c_void_p, C.POINTER(Refine2D), C.c_int64,
+                                           C.POINTER(CeresOptions2D), C.POINTER(Pose2D),
+                                           C.POINTER(C.c_int32)]),
     "csm_grid2d_cropped_limits": (C.c_int, [C.POINTER(MapLimits), C.POINTER(C.c_uint16),
                                             C.POINTER(C.c_int32), C.POINTER(MapLimits)]),
     "csm_grid2d_crop": (C.c_int, [C.POINTER(MapLimits), C.POINTER(C.c_uint16),
@@ -579,6 +600,31 @@ def match_batch(matchers: Sequence[FastCorrelativeScanMatcher2D], scans: ScanSet
                                       results.ctypes.data_as(C.POINTER(Result2D))),
            "csm_fast2d_match_batch")
     return results
+
+
+def ceres_refine_batch(matchers: Sequence[FastCorrelativeScanMatcher2D], scans: ScanSet,
+                       submap_idx, scan_idx, initial, target=None,
+                       options: Optional["CeresOptions2D"] = None,
+                       context: Optional[Context] = None):
+    """CeresScanMatcher2D::Match for each (submap, scan) item on the device
+    (ceres_scan_matcher_2d.cc:64-105): returns (poses (n, 3), iterations)."""
+    ctx = context or scans.context
+    n = len(submap_idx)
+    initial = np.asarray(initial, np.float64).reshape(n, 3)
+    target = initial[:, :2] if target is None else np.asarray(target, np.float64).reshape(n, 2)
+    items = (Refine2D * max(n, 1))()
+    for i in range(n):
+        items[i] = Refine2D(int(submap_idx[i]), int(scan_idx[i]), Pose2D(*initial[i]),
+                            float(target[i, 0]), float(target[i, 1]))
+    out = (Pose2D * max(n, 1))()
+    iters = np.zeros(max(n, 1), np.int32)
+    handles = (C.c_void_p * len(matchers))(*[m.handle for m in matchers])
+    opts = options or CeresOptions2D.make()
+    _check(ctx._lib.csm_ceres2d_refine_batch(ctx.handle, handles, len(matchers), scans.handle,
+                                             items, n, C.byref(opts), out,
+                                             _ptr(iters, C.c_int32)),
+           "csm_ceres2d_refine_batch")
+    return np.array([out[i].as_tuple() for i in range(n)]).reshape(n, 3), iters[:n]
 
 
 # --------------------------------------------------------------------------

@@ -49,26 +49,6 @@ int AutoSearchDepth(int configured, int nx, int ny) {
 using namespace csm;
 
 
-struct csm_fast2d {
-  csm_context* ctx = nullptr;
-  csm_map_limits limits{};
-  csm_fast2d_options options{};
-  float min_cc = 0.f, max_cc = 0.f, min_s = 0.f, max_s = 0.f;
-  SubmapDesc desc{};
-  DevBuf pyramid;
-};
-
-struct csm_scan_set {
-  csm_context* ctx = nullptr;
-  std::vector<float> host_points;
-  std::vector<int64_t> offsets;
-  DevBuf points;
-  // Rotation tables per (scan, angular window, linear window, resolution).
-  std::map<std::tuple<int, double, double, double>,
-           std::pair<SearchWindow2D, std::vector<ZRot>>>
-      windows;
-};
-
 namespace {
 
 int EnsureDevice(csm_context* ctx) {
@@ -511,7 +491,19 @@ int csm_fast2d_create(csm_context* ctx, const csm_map_limits* limits,
     CSM_HIP(LaunchPyramidQuad(d.level[l], d.wide_nx[l], d.wide_ny[l], l,
                               const_cast<uint32_t*>(d.quad[l]), d.quad_w[l], d.quad_h[l],
                               d.quad_pws[l], d.quad_pph[l], d.quad_bytes[l] / 4, st));
-  CSM_HIP(hipStreamSynchronize(st));  // dcells/dq are freed on return
+  // Correspondence costs (Grid2D::GetCorrespondenceCost, grid_2d.cc) for the
+  // CeresScanMatcher2D refinement: the value table with unknown -> max_cc.
+  {
+    std::vector<float> ctab(32768);
+    ConversionTable(max_cc, min_cc, max_cc, ctab.data());
+    DevBuf dtab;
+    if ((rc = dtab.Reserve(sizeof(float) * 32768))) return rc;
+    if ((rc = m->cost.Reserve(sizeof(float) * n0))) return rc;
+    CSM_HIP(hipMemcpyAsync(dtab.ptr, ctab.data(), sizeof(float) * 32768, hipMemcpyHostToDevice, st));
+    CSM_HIP(LaunchCellsToProbability(dcells.as<uint16_t>(), dtab.as<float>(), m->cost.as<float>(),
+                                     n0, st));
+    CSM_HIP(hipStreamSynchronize(st));  // dcells/dq/dtab are freed on return
+  }
   *out = m.release();
   return CSM_OK;
 }

@@ -6,11 +6,14 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <map>
 #include <mutex>
+#include <tuple>
 #include <vector>
 
 #include "../../include/csm_amd.h"
 #include "csm_device.h"
+#include "search_window.h"
 
 namespace csm {
 
@@ -87,6 +90,30 @@ struct csm_context {
   csm::PinnedBuf f3_host_yaws;
   // Voxel filter scratch (voxel_filter.hip).
   csm::DevBuf vf_points, vf_offsets, vf_keep, vf_counts;
+  // CeresScanMatcher2D refinement scratch (ceres2d.hip).
+  csm::DevBuf cr_items, cr_out;
+};
+
+// One submap's device data (csm_host.cc builds it).
+struct csm_fast2d {
+  csm_context* ctx = nullptr;
+  csm_map_limits limits{};
+  csm_fast2d_options options{};
+  float min_cc = 0.f, max_cc = 0.f, min_s = 0.f, max_s = 0.f;
+  csm::SubmapDesc desc{};
+  csm::DevBuf pyramid;
+  csm::DevBuf cost;  // float correspondence costs, x fastest (CeresScanMatcher2D refinement)
+};
+
+struct csm_scan_set {
+  csm_context* ctx = nullptr;
+  std::vector<float> host_points;
+  std::vector<int64_t> offsets;
+  csm::DevBuf points;
+  // Rotation tables per (scan, angular window, linear window, resolution).
+  std::map<std::tuple<int, double, double, double>,
+           std::pair<csm::SearchWindow2D, std::vector<csm::ZRot>>>
+      windows;
 };
 
 #endif  // CSM_INTERNAL_H_

@@ -310,6 +310,37 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
                            const csm_node3d* nodes, int32_t num_nodes, const csm_pair3d* pairs,
                            int64_t num_pairs, csm_result3d* results);
 
+/* ---- CeresScanMatcher2D refinement ------------------------------------------
+ * ConstraintBuilder2D::ComputeConstraint refines every accepted match with
+ * CeresScanMatcher2D::Match(target_translation = match translation,
+ * initial = match, filtered cloud, submap grid) (constraint_builder_2d.cc:
+ * 245-249; ceres_scan_matcher_2d.cc:64-105). csm_ceres2d_refine_batch runs
+ * that refinement for n (submap, scan) items on the device, over the submaps'
+ * csm_fast2d handles (their correspondence-cost grids) and a scan set.
+ * Ceres is not part of this library: the solver restates Ceres' trust-region
+ * Levenberg-Marquardt defaults (parity with Ceres unpinned).
+ * iterations (may be NULL) receives the iterations each item ran. */
+typedef struct csm_ceres2d_options {
+  /* proto::CeresScanMatcherOptions2D (pose_graph.lua:30-39 defaults 20, 10, 1;
+   * ceres_solver_options.max_num_iterations = 10). */
+  double occupied_space_weight;
+  double translation_weight;
+  double rotation_weight;
+  int32_t max_num_iterations;
+} csm_ceres2d_options;
+
+typedef struct csm_refine2d {
+  int32_t submap;  /* index into submaps[] */
+  int32_t scan;    /* index into the scan set */
+  csm_pose2d initial;
+  double target_x, target_y;
+} csm_refine2d;
+
+int csm_ceres2d_refine_batch(csm_context* ctx, csm_fast2d* const* submaps, int32_t num_submaps,
+                             const csm_scan_set* scans, const csm_refine2d* items, int64_t n,
+                             const csm_ceres2d_options* options, csm_pose2d* out,
+                             int32_t* iterations);
+
 /* ---- submap grid formats ---------------------------------------------------
  * Submap2D::Finish (submap_2d.cc:146-150) crops a finished submap's grid to
  * its known cells: ProbabilityGrid::ComputeCroppedGrid

@@ -40,6 +40,8 @@ class Oracle:
             "oracle_grid_insert": (None, [VP, F, F, I32, P(F), P(F), I32]),
             "oracle_grid_set_probability": (None, [VP, I32, I32, F]),
             "oracle_grid_crop": (None, [VP]),
+            "oracle_ceres2d_match": (I32, [D, D, D, I32, I32, P(C.c_uint16), F, F, P(D), P(D), P(D),
+                                           P(F), I32, P(D)]),
             "oracle_grid_info": (None, [VP, P(D), P(I32)]),
             "oracle_grid_cells": (None, [VP, P(C.c_uint16)]),
             "oracle_transform_cloud_2d": (None, [P(F), P(F), I32, P(F)]),
@@ -448,3 +450,23 @@ def _o_adaptive_voxel_filter_masks(self, clouds, max_length, min_num_points, max
 
 Oracle.voxel_filter_masks = _o_voxel_filter_masks
 Oracle.adaptive_voxel_filter_masks = _o_adaptive_voxel_filter_masks
+
+
+def _o_ceres2d_match(self, limits, cells, options, target, initial, cloud,
+                     min_cc=0.1, max_cc=0.9):
+    """CeresScanMatcher2D::Match restated (oracle/ceres2d.cc): (pose, iterations)."""
+    cells = np.ascontiguousarray(cells, np.uint16)
+    pts = np.ascontiguousarray(cloud, np.float32).reshape(-1, 3)
+    o = np.asarray(options, np.float64)
+    t = np.asarray(target, np.float64)
+    i = np.asarray(initial, np.float64)
+    out = np.zeros(3)
+    it = self.lib.oracle_ceres2d_match(limits[0], limits[1], limits[2], cells.shape[1],
+                                       cells.shape[0], _p(cells, C.c_uint16),
+                                       float(np.float32(min_cc)), float(np.float32(max_cc)),
+                                       _p(o, D), _p(t, D), _p(i, D), _p(pts, F), len(pts),
+                                       _p(out, D))
+    return tuple(out), int(it)
+
+
+Oracle.ceres2d_match = _o_ceres2d_match
