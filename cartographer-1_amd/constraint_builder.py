@@ -20,7 +20,9 @@ Follows reference ``mapping/internal/constraints/constraint_builder_2d.cc``:
 
 Instead of one ``common::Task`` per pair, the pending pairs are searched as one
 GPU batch (``match_batch``) when a node ends, or once ``flush_pairs`` pairs are
-pending. The Ceres refinement (:245-249) is outside the hot path.
+pending. Accepted matches are then refined as one batch with the
+CeresScanMatcher2D restatement (:245-249; ``ceres_refine_batch``, parity with
+Ceres unpinned) unless ``refine_with_ceres`` is off.
 """
 
 from __future__ import annotations
@@ -31,7 +33,8 @@ from typing import Callable, Dict, List, Optional, Tuple
 
 import numpy as np
 
-from . import (CSM_OK, Context, FastCorrelativeScanMatcher2D, FastCorrelativeScanMatcher3D,
+from . import (CSM_OK, CeresOptions2D, Context, FastCorrelativeScanMatcher2D,
+               FastCorrelativeScanMatcher3D, ceres_refine_batch,
                FastCorrelativeScanMatcherOptions2D, FastCorrelativeScanMatcherOptions3D,
                HybridGrid, NodeData3D, ProbabilityGrid, ScanSet, _f32_points, default_context,
                make_pairs, make_pairs_3d, match_batch, match_batch_3d)
@@ -90,6 +93,10 @@ class ConstraintBuilderOptions:
     fast_correlative_scan_matcher_options_3d: FastCorrelativeScanMatcherOptions3D = field(
         default_factory=FastCorrelativeScanMatcherOptions3D)
     flush_pairs: int = 0  # 0: search each node's pairs when the node ends
+    # ceres_scan_matcher (pose_graph.lua:30-39): every accepted 2D match is
+    # refined with CeresScanMatcher2D (constraint_builder_2d.cc:245-249).
+    ceres_scan_matcher_options: CeresOptions2D = field(default_factory=CeresOptions2D.make)
+    refine_with_ceres: bool = True
 
 
 @dataclass
@@ -206,9 +213,20 @@ class ConstraintBuilder2D:
             scans = ScanSet(clouds, self.context)
             try:
                 results = match_batch(matchers, scans, pairs, self.context)
+                refined = {}
+                ok = [i for i, r in enumerate(results) if int(r["status"]) == CSM_OK]
+                if self.options.refine_with_ceres and ok:
+                    # ceres_scan_matcher_.Match(pose.translation(), pose, cloud, grid)
+                    init = [(float(results[i]["x"]), float(results[i]["y"]),
+                             float(results[i]["theta"])) for i in ok]
+                    poses, _ = ceres_refine_batch(
+                        matchers, scans, [submap_idx[i] for i in ok], [scan_idx[i] for i in ok],
+                        init, [q[:2] for q in init], self.options.ceres_scan_matcher_options,
+                        self.context)
+                    refined = {i: tuple(float(v) for v in poses[k]) for k, i in enumerate(ok)}
             finally:
                 scans.close()
-            for p, r in zip(pending, results):
+            for i, (p, r) in enumerate(zip(pending, results)):
                 if p.full:
                     self.global_constraints_searched += 1
                 else:
@@ -222,7 +240,7 @@ class ConstraintBuilder2D:
                 else:
                     self.constraints_found += 1
                     self.constraint_scores.append(score)
-                pose = (float(r["x"]), float(r["y"]), float(r["theta"]))
+                pose = refined.get(i, (float(r["x"]), float(r["y"]), float(r["theta"])))
                 self._constraints[p.slot] = Constraint(
                     submap_id=p.submap_id, node_id=p.node_id,
                     relative_pose=rigid2d_compose(rigid2d_inverse(p.submap.local_pose), pose),

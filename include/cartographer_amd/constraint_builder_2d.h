@@ -9,9 +9,10 @@
 // (DispatchScanMatcherConstruction :165-186) and the metric counters
 // (:46-53). Instead of one Task per pair on common::ThreadPool, pending pairs
 // are searched as one GPU batch when a node ends (or when `flush_pairs` are
-// pending). The Ceres refinement of ComputeConstraint (:245-249) is not part
-// of this drop-in (DESIGN.md "Out of scope"): constraint poses are the CSM
-// estimates.
+// pending). Accepted matches are then refined as one batch by the
+// CeresScanMatcher2D restatement of ComputeConstraint (:245-249;
+// csm_ceres2d_refine_batch, parity with Ceres unpinned) unless
+// options.refine_with_ceres is off.
 #ifndef CARTOGRAPHER_AMD_CONSTRAINT_BUILDER_2D_H_
 #define CARTOGRAPHER_AMD_CONSTRAINT_BUILDER_2D_H_
 
@@ -173,6 +174,26 @@ class ConstraintBuilder2D {
                                    scans_, pairs.data(), static_cast<int64_t>(pairs.size()),
                                    results.data()),
             "csm_fast2d_match_batch");
+    // CeresScanMatcher2D::Match(pose.translation(), pose, cloud, grid) on the accepted ones.
+    if (options_.refine_with_ceres) {
+      std::vector<csm_refine2d> items;
+      std::vector<size_t> which;
+      for (size_t i = 0; i < pairs.size(); ++i)
+        if (results[i].status == CSM_OK) {
+          items.push_back(csm_refine2d{pairs[i].submap, pairs[i].scan, results[i].pose,
+                                       results[i].pose.x, results[i].pose.y});
+          which.push_back(i);
+        }
+      std::vector<csm_pose2d> out(items.size());
+      if (!items.empty())
+        CheckOk(csm_ceres2d_refine_batch(context_, handles.data(),
+                                         static_cast<int32_t>(handles.size()), scans_,
+                                         items.data(), static_cast<int64_t>(items.size()),
+                                         &options_.ceres_scan_matcher_options, out.data(),
+                                         nullptr),
+                "csm_ceres2d_refine_batch");
+      for (size_t k = 0; k < which.size(); ++k) results[which[k]].pose = out[k];
+    }
     for (size_t i = 0; i < pending_.size(); ++i) {
       const Pending& p = pending_[i];
       (p.full ? global_constraints_searched : constraints_searched) += 1;

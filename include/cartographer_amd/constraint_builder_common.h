@@ -35,6 +35,10 @@ struct ConstraintBuilderOptions {
   FastCorrelativeScanMatcherOptions2D fast_correlative_scan_matcher_options;
   FastCorrelativeScanMatcherOptions3D fast_correlative_scan_matcher_options_3d;
   int flush_pairs = 0;  // 0: search each node's pairs when the node ends
+  // ceres_scan_matcher (pose_graph.lua:30-39): accepted 2D matches are refined
+  // with CeresScanMatcher2D (constraint_builder_2d.cc:245-249).
+  csm_ceres2d_options ceres_scan_matcher_options{20., 10., 1., 10};
+  bool refine_with_ceres = true;
 };
 
 // common/fixed_ratio_sampler.cc:32-39

@@ -155,7 +155,8 @@ def test_builder_constraints_match_oracle(csm, cb, oracle):
     opts = cb.ConstraintBuilderOptions(sampling_ratio=1.0, min_score=0.4,
                                        global_localization_min_score=0.45,
                                        max_constraint_distance=1e9,
-                                       fast_correlative_scan_matcher_options=fopts)
+                                       fast_correlative_scan_matcher_options=fopts,
+                                       refine_with_ceres=False)
     builder = cb.ConstraintBuilder2D(opts)
     rng = np.random.default_rng(3)
     # Non-trivial submap poses: the builder composes the search start with it
@@ -205,3 +206,42 @@ def test_builder_constraints_match_oracle(csm, cb, oracle):
         pose = cb.rigid2d_compose(local[s], c.relative_pose)
         assert_fast_parity(oracle, oms[s], limits, cells, (True, c.score, pose), ref, full,
                            ctr, cloud)
+
+
+@pytest.mark.gpu
+def test_builder_refines_accepted_matches(csm, cb, oracle):
+    """With refine_with_ceres (the reference's ComputeConstraint, :245-249),
+    each constraint is the CeresScanMatcher2D refinement of the branch-and-bound
+    match: oracle/ceres2d.cc started from the builder's own match pose (the
+    unrefined run), to 1e-6 (parity with Ceres itself unpinned)."""
+    world = csm.SyntheticWorld2D(num_nodes=30, num_submaps=3, decimate_to=200, seed=17)
+    base = dict(sampling_ratio=1.0, min_score=0.45, global_localization_min_score=0.5,
+                max_constraint_distance=1e9)
+    runs = {}
+    for refine in (False, True):
+        builder = cb.ConstraintBuilder2D(cb.ConstraintBuilderOptions(refine_with_ceres=refine,
+                                                                     **base))
+        local = {s: (0.1 * s, -0.2 * s, 0.05 * s) for s in range(world.num_submaps)}
+        for node in range(0, world.num_nodes, 2):
+            for s in range(world.num_submaps):
+                sm = cb.Submap2D(world.grid(s), local[s])
+                builder.MaybeAddGlobalConstraint((0, s), sm, (0, node), world.cloud(node))
+            builder.NotifyEndOfNode()
+        got = []
+        builder.WhenDone(got.append)
+        runs[refine] = (got[0], local)
+    plain, local = runs[False]
+    refined, _ = runs[True]
+    assert len(plain) == len(refined) and len(plain) > 3
+    o = cb.ConstraintBuilderOptions().ceres_scan_matcher_options
+    opts = (o.occupied_space_weight, o.translation_weight, o.rotation_weight,
+            o.max_num_iterations)
+    for a, b in zip(plain, refined):
+        assert a.submap_id == b.submap_id and a.node_id == b.node_id and a.score == b.score
+        s = a.submap_id[1]
+        match = cb.rigid2d_compose(local[s], a.relative_pose)  # global CSM pose
+        g = world.grid(s)
+        ref, _ = oracle.ceres2d_match((g.resolution, g.max_x, g.max_y), g.cells, opts,
+                                      match[:2], match, world.cloud(a.node_id[1]))
+        got_pose = cb.rigid2d_compose(local[s], b.relative_pose)
+        assert np.allclose(got_pose, ref, atol=1e-6), (got_pose, ref)
