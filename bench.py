@@ -183,6 +183,8 @@ def main():
         out["cpu_baseline"] = cpu_baseline(world, my_submaps, args)
     if rank == 0 and world_size == 1 and not args.no_rt:
         out["voxel_filter"] = voxel_filter_bench(csm, ctx, world, args)
+        out["ceres2d"] = ceres_bench(csm, ctx, world, matchers, scans, pairs, res, my_submaps,
+                                     node_idx, sub_local, args)
     if rank == 0 and world_size == 1 and not args.no_3d:
         out["rt3d"] = rt3d_bench(csm, ctx, args)
     if not args.no_3d:  # collective over ranks: the C5 sweep, submap-sharded
@@ -198,10 +200,10 @@ def main():
 
 def committed_traffic(args, world_size):
     """HBM-side bytes per search launch from the committed PMC pass
-    (profiles/r1b/traffic_c2.json: rocprofv3 --pmc FETCH_SIZE, x2 gfx950
+    (profiles/r1d/traffic_c2.json: rocprofv3 --pmc FETCH_SIZE, x2 gfx950
     correction). PMC counters cannot be read from inside this process, so the
     figure is reported only when this run's workload is the profiled one."""
-    path = os.path.join(ROOT, "profiles", "r1b", "traffic_c2.json")
+    path = os.path.join(ROOT, "profiles", "r1d", "traffic_c2.json")
     try:
         t = json.load(open(path))
     except (OSError, ValueError):
@@ -292,6 +294,44 @@ def voxel_filter_bench(csm, ctx, world, args):
     except OSError:
         pass
     return res
+
+
+def ceres_bench(csm, ctx, world, matchers, scans, pairs, res, my_submaps, node_idx, sub_local,
+                args):
+    """CeresScanMatcher2D refinement of one C2 step's accepted matches (what
+    ComputeConstraint does next, constraint_builder_2d.cc:245-249), as one
+    device batch; CPU: the oracle restatement on a sample, one thread."""
+    ok = np.nonzero(res["status"] == csm.CSM_OK)[0]
+    if len(ok) == 0:
+        return {"accepted": 0}
+    init = np.stack([res["x"][ok], res["y"][ok], res["theta"][ok]], 1)
+    sub, scn = sub_local[ok], node_idx[ok]
+    opts = csm.CeresOptions2D.make()
+    csm.ceres_refine_batch(matchers, scans, sub, scn, init, None, opts, ctx)  # warm-up
+    a = time.perf_counter()
+    poses, iters = csm.ceres_refine_batch(matchers, scans, sub, scn, init, None, opts, ctx)
+    gpu_s = time.perf_counter() - a
+    out = {"workload": f"CeresScanMatcher2D::Match on the {len(ok)} accepted matches of one C2 "
+                       "step (pose_graph.lua options), 1080-point clouds",
+           "accepted": int(len(ok)), "gpu_ms": gpu_s * 1e3,
+           "refinements_per_s": len(ok) / gpu_s, "mean_iterations": float(iters.mean())}
+    try:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_lib
+        o = oracle_lib.Oracle()
+        k = min(len(ok), 64)
+        a = time.perf_counter()
+        for j in range(k):
+            g = world.grid(int(my_submaps[int(sub[j])]))
+            o.ceres2d_match((g.resolution, g.max_x, g.max_y), g.cells, (20.0, 10.0, 1.0, 10),
+                            init[j][:2], init[j], world.cloud(int(scn[j])))
+        cpu_s = (time.perf_counter() - a) / k
+        out["cpu_baseline"] = {"value": 1.0 / cpu_s, "unit": "refinements/s", "cores": 1,
+                               "kind": "port", "sample": f"{k} of the accepted matches (oracle "
+                                                         "restatement, includes grid copy-in)"}
+    except OSError:
+        pass
+    return out
 
 
 def rt3d_bench(csm, ctx, args):

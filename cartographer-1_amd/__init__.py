@@ -602,6 +602,13 @@ def match_batch(matchers: Sequence[FastCorrelativeScanMatcher2D], scans: ScanSet
     return results
 
 
+REFINE_DTYPE = np.dtype([("submap", np.int32), ("scan", np.int32), ("x", np.float64),
+                         ("y", np.float64), ("theta", np.float64), ("target_x", np.float64),
+                         ("target_y", np.float64)])
+POSE_DTYPE = np.dtype([("x", np.float64), ("y", np.float64), ("theta", np.float64)])
+assert REFINE_DTYPE.itemsize == C.sizeof(Refine2D) and POSE_DTYPE.itemsize == C.sizeof(Pose2D)
+
+
 def ceres_refine_batch(matchers: Sequence[FastCorrelativeScanMatcher2D], scans: ScanSet,
                        submap_idx, scan_idx, initial, target=None,
                        options: Optional["CeresOptions2D"] = None,
@@ -612,19 +619,22 @@ def ceres_refine_batch(matchers: Sequence[FastCorrelativeScanMatcher2D], scans: 
     n = len(submap_idx)
     initial = np.asarray(initial, np.float64).reshape(n, 3)
     target = initial[:, :2] if target is None else np.asarray(target, np.float64).reshape(n, 2)
-    items = (Refine2D * max(n, 1))()
-    for i in range(n):
-        items[i] = Refine2D(int(submap_idx[i]), int(scan_idx[i]), Pose2D(*initial[i]),
-                            float(target[i, 0]), float(target[i, 1]))
-    out = (Pose2D * max(n, 1))()
+    items = np.zeros(max(n, 1), REFINE_DTYPE)
+    items["submap"][:n] = np.asarray(submap_idx, np.int32)
+    items["scan"][:n] = np.asarray(scan_idx, np.int32)
+    items["x"][:n], items["y"][:n], items["theta"][:n] = initial[:, 0], initial[:, 1], initial[:, 2]
+    items["target_x"][:n], items["target_y"][:n] = target[:, 0], target[:, 1]
+    out = np.zeros(max(n, 1), POSE_DTYPE)
     iters = np.zeros(max(n, 1), np.int32)
     handles = (C.c_void_p * len(matchers))(*[m.handle for m in matchers])
     opts = options or CeresOptions2D.make()
     _check(ctx._lib.csm_ceres2d_refine_batch(ctx.handle, handles, len(matchers), scans.handle,
-                                             items, n, C.byref(opts), out,
+                                             items.ctypes.data_as(C.POINTER(Refine2D)), n,
+                                             C.byref(opts), out.ctypes.data_as(C.POINTER(Pose2D)),
                                              _ptr(iters, C.c_int32)),
            "csm_ceres2d_refine_batch")
-    return np.array([out[i].as_tuple() for i in range(n)]).reshape(n, 3), iters[:n]
+    poses = np.stack([out["x"][:n], out["y"][:n], out["theta"][:n]], 1)
+    return poses, iters[:n]
 
 
 # --------------------------------------------------------------------------
