@@ -239,3 +239,47 @@ def test_edge_cases(csm, oracle, search_kernel):
     ref = om1.match((0.0, 0.0, 0.0), cloud, 0.0)
     assert_fast_parity(oracle, om1, (0.05, 0.05, 0.05), np.full((1, 1), 20000, np.uint16), gpu, ref,
                        False, (0.0, 0.0, 0.0), cloud)
+
+
+def _run_list_clouds(world):
+    """Clouds whose run lists stress the compaction: long runs (split at 255),
+    runs crossing 64-point blocks, no runs, and ragged sizes around 64."""
+    rng = np.random.default_rng(23)
+    base = world.cloud(0)
+    a, b = base[10], base[len(base) // 2]
+    clouds = [
+        np.concatenate([np.repeat(a[None], 600, 0), base[:300]]),          # one run of 600
+        np.concatenate([np.repeat(a[None], 70, 0), np.repeat(b[None], 70, 0),
+                        np.repeat(a[None], 130, 0)]),                        # runs across blocks
+        np.stack([a, b] * 100),                                              # alternating, no runs
+        np.repeat(b[None], 256, 0),                                          # exactly 256 in one cell
+    ]
+    for n in (1, 2, 63, 64, 65, 129):
+        clouds.append(base[rng.choice(len(base), n, replace=False)])
+    return [np.ascontiguousarray(c, np.float32) for c in clouds]
+
+
+def test_run_lists_parity(csm, oracle, world):
+    """Run-list compaction (consecutive points in one cell scored once with
+    their count) leaves every score and pose unchanged, through the batch path
+    with ragged clouds in one batch."""
+    s = 0
+    g = world.grid(s)
+    limits = (g.resolution, g.max_x, g.max_y)
+    opts = csm.FastCorrelativeScanMatcherOptions2D()
+    m = csm.FastCorrelativeScanMatcher2D(g, opts)
+    om = oracle.fast2d(limits, g.cells, opts.linear_search_window, opts.angular_search_window,
+                       opts.branch_and_bound_depth)
+    clouds = _run_list_clouds(world)
+    scans = csm.ScanSet(clouds)
+    pairs = csm.make_pairs(np.zeros(len(clouds), np.int32), np.arange(len(clouds), dtype=np.int32),
+                           0.3, full_submap=True)
+    res = csm.match_batch([m], scans, pairs)
+    kinds = []
+    for k, c in enumerate(clouds):
+        gpu = (int(res[k]["status"]) == csm.CSM_OK, float(res[k]["score"]),
+               (float(res[k]["x"]), float(res[k]["y"]), float(res[k]["theta"])))
+        ref = om.match_full_submap(c, 0.3)
+        kinds.append(assert_fast_parity(oracle, om, limits, g.cells, gpu, ref, True,
+                                        full_submap_center(limits, g.cells), c))
+    assert kinds.count("nomatch") < len(kinds)
