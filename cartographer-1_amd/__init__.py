@@ -131,6 +131,23 @@ class CeresOptions2D(C.Structure):
                               max_num_iterations)
 
 
+class CeresOptions3D(C.Structure):
+    """proto::CeresScanMatcherOptions3D; defaults pose_graph.lua:49-60."""
+    _fields_ = [("occupied_space_weight_0", C.c_double), ("occupied_space_weight_1", C.c_double),
+                ("translation_weight", C.c_double), ("rotation_weight", C.c_double),
+                ("max_num_iterations", C.c_int32)]
+
+    @staticmethod
+    def make(w0=5.0, w1=30.0, translation_weight=10.0, rotation_weight=1.0,
+             max_num_iterations=10) -> "CeresOptions3D":
+        return CeresOptions3D(w0, w1, translation_weight, rotation_weight, max_num_iterations)
+
+
+class Refine3D(C.Structure):
+    _fields_ = [("high_grid", C.c_int32), ("low_grid", C.c_int32), ("node", C.c_int32),
+                ("initial", Pose3D), ("target", C.c_double * 3)]
+
+
 class Refine2D(C.Structure):
     _fields_ = [("submap", C.c_int32), ("scan", C.c_int32), ("initial", Pose2D),
                 ("target_x", C.c_double), ("target_y", C.c_double)]
@@ -227,6 +244,10 @@ _SIGNATURES = {
                                            C.c_void_p, C.POINTER(Refine2D), C.c_int64,
                                            C.POINTER(CeresOptions2D), C.POINTER(Pose2D),
                                            C.POINTER(C.c_int32)]),
+    "csm_ceres3d_refine_batch": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.c_int32,
+                                           C.POINTER(Node3D), C.c_int32, C.POINTER(Refine3D),
+                                           C.c_int64, C.POINTER(CeresOptions3D),
+                                           C.POINTER(Pose3D), C.POINTER(C.c_int32)]),
     "csm_grid2d_cropped_limits": (C.c_int, [C.POINTER(MapLimits), C.POINTER(C.c_uint16),
                                             C.POINTER(C.c_int32), C.POINTER(MapLimits)]),
     "csm_grid2d_crop": (C.c_int, [C.POINTER(MapLimits), C.POINTER(C.c_uint16),
@@ -701,8 +722,8 @@ class SyntheticWorld2D:
 # 3D matchers (RealTimeCorrelativeScanMatcher3D, FastCorrelativeScanMatcher3D).
 from .matching3d import (FastCorrelativeScanMatcher3D, FastCorrelativeScanMatcherOptions3D,  # noqa: E402,F401
                          HybridGrid, NodeData3D, PAIR3_DTYPE, RESULT3_DTYPE,
-                         RealTimeCorrelativeScanMatcher3D, SyntheticWorld3D, make_pairs_3d,
-                         match_batch_3d)
+                         RealTimeCorrelativeScanMatcher3D, SyntheticWorld3D, ceres_refine_batch_3d,
+                         make_pairs_3d, match_batch_3d)
 
 
 # --------------------------------------------------------------------------

@@ -13,6 +13,7 @@
 
 #include "../../include/csm_amd.h"
 #include "csm_device.h"
+#include "csm_device3d.h"
 #include "search_window.h"
 
 namespace csm {
@@ -91,7 +92,7 @@ struct csm_context {
   // Voxel filter scratch (voxel_filter.hip).
   csm::DevBuf vf_points, vf_offsets, vf_keep, vf_counts;
   // CeresScanMatcher2D refinement scratch (ceres2d.hip).
-  csm::DevBuf cr_items, cr_out;
+  csm::DevBuf cr_items, cr_out, cr3_items, cr3_points, cr3_out;
 };
 
 // One submap's device data (csm_host.cc builds it).
@@ -114,6 +115,18 @@ struct csm_scan_set {
   std::map<std::tuple<int, double, double, double>,
            std::pair<csm::SearchWindow2D, std::vector<csm::ZRot>>>
       windows;
+};
+
+// A HybridGrid on the device (host3d.cc builds it).
+struct csm_hybrid_grid {
+  csm_context* ctx = nullptr;
+  float resolution = 0.f;
+  int32_t grid_size = 0;
+  csm::Brick3 brick{};
+  csm::DevBuf values;    // uint16 brick
+  csm::DevBuf prob;      // float probability brick
+  csm::DevBuf prob_pad;  // the same padded by one 0.1 cell per side (RTCSM3D), built on first use
+  bool prob_pad_ready = false;
 };
 
 #endif  // CSM_INTERNAL_H_

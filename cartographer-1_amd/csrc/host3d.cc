@@ -161,17 +161,6 @@ int EnsureDevice3(csm_context* ctx) {
 }  // namespace
 
 // ----------------------------------------------------------- HybridGrid --
-struct csm_hybrid_grid {
-  csm_context* ctx = nullptr;
-  float resolution = 0.f;
-  int32_t grid_size = 0;
-  Brick3 brick{};
-  DevBuf values;  // uint16 brick
-  DevBuf prob;    // float probability brick
-  DevBuf prob_pad;  // the same padded by one 0.1 cell per side (RTCSM3D), built on first use
-  bool prob_pad_ready = false;
-};
-
 int csm_hybrid_grid_create(csm_context* ctx, float resolution, const int32_t* ijk,
                            const uint16_t* values, int64_t count, int32_t grid_size,
                            csm_hybrid_grid** out) {

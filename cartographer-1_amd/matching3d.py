@@ -265,6 +265,32 @@ def match_batch_3d(matchers: Sequence[FastCorrelativeScanMatcher3D], nodes: Sequ
     return list(results)
 
 
+def ceres_refine_batch_3d(grids: Sequence[HybridGrid], nodes: Sequence[NodeData3D], items,
+                          options=None, context: Optional[Context] = None):
+    """CeresScanMatcher3D::Match on the device for each item
+    (high_grid, low_grid, node, initial ((t), (w, x, y, z)), target (t))
+    (ceres_scan_matcher_3d.cc:84-160): returns ([((t), (q)), ...], iterations)."""
+    from . import CeresOptions3D, Refine3D
+    ctx = context or (grids[0].context if grids else default_context())
+    n = len(items)
+    citems = (Refine3D * max(n, 1))()
+    for i, (hg, lg, nd, init, target) in enumerate(items):
+        citems[i].high_grid, citems[i].low_grid, citems[i].node = hg, lg, nd
+        citems[i].initial = _pose(init)
+        for a in range(3):
+            citems[i].target[a] = float(target[a])
+    cnodes = (Node3D * max(len(nodes), 1))(*[nd.to_c() for nd in nodes])
+    handles = (C.c_void_p * max(len(grids), 1))(*[g.handle for g in grids])
+    out = (Pose3D * max(n, 1))()
+    iters = np.zeros(max(n, 1), np.int32)
+    opts = options or CeresOptions3D.make()
+    _check(ctx._lib.csm_ceres3d_refine_batch(ctx.handle, handles, len(grids), cnodes, len(nodes),
+                                             citems, n, C.byref(opts), out,
+                                             _ptr(iters, C.c_int32)),
+           "csm_ceres3d_refine_batch")
+    return [out[i].as_tuple() for i in range(n)], iters[:n]
+
+
 # --------------------------------------------------------------------------
 # Synthetic 3D world (bench / test inputs; not the matching path).
 

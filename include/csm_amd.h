@@ -341,6 +341,34 @@ int csm_ceres2d_refine_batch(csm_context* ctx, csm_fast2d* const* submaps, int32
                              const csm_ceres2d_options* options, csm_pose2d* out,
                              int32_t* iterations);
 
+/* CeresScanMatcher3D refinement (ConstraintBuilder3D::ComputeConstraint,
+ * constraint_builder_3d.cc:264-275; ceres_scan_matcher_3d.cc:84-160): the
+ * match pose is refined against the submap's high- and low-resolution
+ * HybridGrids with the node's high- and low-resolution clouds. Item i uses
+ * grids[high_grid], grids[low_grid] and nodes[node]; target is the match
+ * translation. Same solver notes as csm_ceres2d_refine_batch. */
+typedef struct csm_ceres3d_options {
+  /* proto::CeresScanMatcherOptions3D (pose_graph.lua:49-60: 5, 30, 10, 1,
+   * max_num_iterations 10). */
+  double occupied_space_weight_0;
+  double occupied_space_weight_1;
+  double translation_weight;
+  double rotation_weight;
+  int32_t max_num_iterations;
+} csm_ceres3d_options;
+
+typedef struct csm_refine3d {
+  int32_t high_grid, low_grid, node;
+  csm_pose3d initial;
+  double target[3];
+} csm_refine3d;
+
+int csm_ceres3d_refine_batch(csm_context* ctx, const csm_hybrid_grid* const* grids,
+                             int32_t num_grids, const csm_node3d* nodes, int32_t num_nodes,
+                             const csm_refine3d* items, int64_t n,
+                             const csm_ceres3d_options* options, csm_pose3d* out,
+                             int32_t* iterations);
+
 /* ---- submap grid formats ---------------------------------------------------
  * Submap2D::Finish (submap_2d.cc:146-150) crops a finished submap's grid to
  * its known cells: ProbabilityGrid::ComputeCroppedGrid

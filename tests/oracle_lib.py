@@ -470,3 +470,25 @@ def _o_ceres2d_match(self, limits, cells, options, target, initial, cloud,
 
 
 Oracle.ceres2d_match = _o_ceres2d_match
+
+
+def _o_ceres3d_match(self, high, low, high_cloud, low_cloud, options, target, initial_t,
+                     initial_q):
+    """CeresScanMatcher3D::Match restated (oracle/ceres3d.cc): ((t, q), iterations).
+    high / low: OracleHybridGrid objects; q as (w, x, y, z)."""
+    _o3_hgrid(self, 1.0)  # binds the 3D signatures
+    f = self.lib.oracle_ceres3d_match
+    f.restype = I32
+    f.argtypes = [VP, VP, P(F), I32, P(F), I32, P(D), P(D), P(D), P(D)]
+    hc = np.ascontiguousarray(high_cloud, np.float32).reshape(-1, 3)
+    lc = np.ascontiguousarray(low_cloud, np.float32).reshape(-1, 3)
+    o = np.asarray(options, np.float64)
+    t = np.asarray(target, np.float64)
+    init = np.concatenate([np.asarray(initial_t, np.float64), np.asarray(initial_q, np.float64)])
+    out = np.zeros(7)
+    it = f(high.h, low.h, _p(hc, F), len(hc), _p(lc, F), len(lc), _p(o, D), _p(t, D),
+           _p(init, D), _p(out, D))
+    return (tuple(out[:3]), tuple(out[3:])), int(it)
+
+
+Oracle.ceres3d_match = _o_ceres3d_match
