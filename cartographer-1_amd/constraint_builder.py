@@ -33,8 +33,8 @@ from typing import Callable, Dict, List, Optional, Tuple
 
 import numpy as np
 
-from . import (CSM_OK, CeresOptions2D, Context, FastCorrelativeScanMatcher2D,
-               FastCorrelativeScanMatcher3D, ceres_refine_batch,
+from . import (CSM_OK, CeresOptions2D, CeresOptions3D, Context, FastCorrelativeScanMatcher2D,
+               FastCorrelativeScanMatcher3D, ceres_refine_batch, ceres_refine_batch_3d,
                FastCorrelativeScanMatcherOptions2D, FastCorrelativeScanMatcherOptions3D,
                HybridGrid, NodeData3D, ProbabilityGrid, ScanSet, _f32_points, default_context,
                make_pairs, make_pairs_3d, match_batch, match_batch_3d)
@@ -96,6 +96,8 @@ class ConstraintBuilderOptions:
     # ceres_scan_matcher (pose_graph.lua:30-39): every accepted 2D match is
     # refined with CeresScanMatcher2D (constraint_builder_2d.cc:245-249).
     ceres_scan_matcher_options: CeresOptions2D = field(default_factory=CeresOptions2D.make)
+    # ceres_scan_matcher_3d (pose_graph.lua:49-60), ConstraintBuilder3D (:264-275).
+    ceres_scan_matcher_options_3d: CeresOptions3D = field(default_factory=CeresOptions3D.make)
     refine_with_ceres: bool = True
 
 
@@ -262,8 +264,9 @@ class ConstraintBuilder2D:
 #   submap rotation, data, global_localization_min_score) (:221-223).
 # * NotifyEndOfNode / WhenDone / GetNumFinishedNodes / DeleteScanMatcher
 #   (:144-168, :307-349); metrics (:46-59) as counters and score lists.
-# * Constraint pose: the CSM estimate (submap <- node). The Ceres refinement
-#   (:264-275) is outside the hot path.
+# * Constraint pose: the CSM estimate (submap <- node), refined by the
+#   CeresScanMatcher3D restatement (:264-275; ceres_refine_batch_3d, parity
+#   with Ceres unpinned) unless refine_with_ceres is off.
 # ---------------------------------------------------------------------------
 
 @dataclass
@@ -407,7 +410,25 @@ class ConstraintBuilder3D:
                 submap_q=[p.submap_pose[1] for p in pending],
                 submap_t=[p.submap_pose[0] for p in pending])
             results = match_batch_3d(matchers, nodes, pairs, self.context)
-            for p, r in zip(pending, results):
+            refined = {}
+            ok = [i for i, r in enumerate(results) if int(r["status"]) == CSM_OK]
+            if self.options.refine_with_ceres and ok:
+                # ceres_scan_matcher_.Match(pose.translation(), pose, {high, low clouds and grids})
+                grids = []
+                for key in slot_of:
+                    grids.extend(self._matchers[key][:2])
+                items = []
+                for i in ok:
+                    p, r = pending[i], results[i]
+                    t = tuple(float(v) for v in r["t"])
+                    q = tuple(float(v) for v in r["q"])
+                    slot = slot_of[p.submap_id]
+                    items.append((2 * slot, 2 * slot + 1, node_of[id(p.data)], (t, q), t))
+                poses, _ = ceres_refine_batch_3d(grids, nodes, items,
+                                                 self.options.ceres_scan_matcher_options_3d,
+                                                 self.context)
+                refined = dict(zip(ok, poses))
+            for i, (p, r) in enumerate(zip(pending, results)):
                 if p.full:
                     self.global_constraints_searched += 1
                 else:
@@ -423,10 +444,11 @@ class ConstraintBuilder3D:
                     self.constraint_scores.append(score)
                 self.rotational_scores.append(float(r["rotational_score"]))
                 self.low_resolution_scores.append(float(r["low_resolution_score"]))
+                pose = refined.get(i, (tuple(float(v) for v in r["t"]),
+                                       tuple(float(v) for v in r["q"])))
                 self._constraints[p.slot] = Constraint3D(
                     submap_id=p.submap_id, node_id=p.node_id,
-                    relative_pose=(tuple(float(v) for v in r["t"]),
-                                   tuple(float(v) for v in r["q"])),
+                    relative_pose=(tuple(pose[0]), tuple(pose[1])),
                     translation_weight=self.options.loop_closure_translation_weight,
                     rotation_weight=self.options.loop_closure_rotation_weight,
                     score=score, rotational_score=float(r["rotational_score"]),

@@ -11,10 +11,10 @@
 // reads the submap's high/low-resolution grids and rotational histogram); and
 // the metrics (:46-59, counters and score lists). Pending pairs are searched
 // as one GPU batch when a node ends (or once `flush_pairs` are pending)
-// instead of one Task per pair. The Ceres refinement (:264-275) is outside
-// this drop-in (DESIGN.md "Out of scope"): a constraint's pose is the CSM
-// estimate (submap <- node), which the reference passes to Ceres as its
-// initial and previous pose.
+// instead of one Task per pair. Accepted matches are then refined as one
+// batch by the CeresScanMatcher3D restatement (:264-275;
+// csm_ceres3d_refine_batch, parity with Ceres unpinned) unless
+// options.refine_with_ceres is off.
 #ifndef CARTOGRAPHER_AMD_CONSTRAINT_BUILDER_3D_H_
 #define CARTOGRAPHER_AMD_CONSTRAINT_BUILDER_3D_H_
 
@@ -176,6 +176,36 @@ class ConstraintBuilder3D {
                                    nodes.data(), static_cast<int32_t>(nodes.size()), pairs.data(),
                                    static_cast<int64_t>(pairs.size()), results.data()),
             "csm_fast3d_match_batch");
+    if (options_.refine_with_ceres) {
+      // ceres_scan_matcher_.Match(pose.translation(), pose, {high, low}) (:264-275).
+      std::vector<const csm_hybrid_grid*> grids;
+      for (const auto& m : keep) {
+        grids.push_back(m->high->handle());
+        grids.push_back(m->low->handle());
+      }
+      std::vector<csm_refine3d> items;
+      std::vector<size_t> which;
+      for (size_t i = 0; i < pairs.size(); ++i)
+        if (results[i].status == CSM_OK) {
+          csm_refine3d it{};
+          it.high_grid = 2 * pairs[i].submap;
+          it.low_grid = 2 * pairs[i].submap + 1;
+          it.node = pairs[i].node;
+          it.initial = results[i].pose;
+          for (int a = 0; a < 3; ++a) it.target[a] = results[i].pose.t[a];
+          items.push_back(it);
+          which.push_back(i);
+        }
+      std::vector<csm_pose3d> out(items.size());
+      if (!items.empty())
+        CheckOk(csm_ceres3d_refine_batch(context_, grids.data(), static_cast<int32_t>(grids.size()),
+                                         nodes.data(), static_cast<int32_t>(nodes.size()),
+                                         items.data(), static_cast<int64_t>(items.size()),
+                                         &options_.ceres_scan_matcher_options_3d, out.data(),
+                                         nullptr),
+                "csm_ceres3d_refine_batch");
+      for (size_t k = 0; k < which.size(); ++k) results[which[k]].pose = out[k];
+    }
     for (size_t i = 0; i < pending_.size(); ++i) {
       const Pending& p = pending_[i];
       (p.full ? global_constraints_searched : constraints_searched) += 1;

@@ -118,7 +118,7 @@ def test_builder_matches_oracle_on_synthetic_pairs(csm, cb, oracle):
     the distance filter and sampler act before any search."""
     from test_fast3d_gpu import assert_same_result, opt_tuple
     w = csm.SyntheticWorld3D(num_nodes=16, num_submaps=2, seed=41)
-    o = cb.ConstraintBuilderOptions(sampling_ratio=0.5)
+    o = cb.ConstraintBuilderOptions(sampling_ratio=0.5, refine_with_ceres=False)
     f3 = o.fast_correlative_scan_matcher_options_3d
     builder = cb.ConstraintBuilder3D(o)
     subs, oms = [], []
@@ -166,3 +166,43 @@ def test_builder_matches_oracle_on_synthetic_pairs(csm, cb, oracle):
         assert_same_result(r, ref, oms[s][2], full, a, b, w.node(n), f3.min_low_resolution_score)
         assert c.translation_weight == o.loop_closure_translation_weight
     assert builder.constraints_searched + builder.global_constraints_searched == len(submitted)
+
+
+@pytest.mark.gpu
+def test_builder_refines_accepted_matches_3d(csm, cb, oracle):
+    """With refine_with_ceres (the reference's ComputeConstraint, :264-275) each
+    3D constraint is the CeresScanMatcher3D refinement of the unrefined
+    builder's match (oracle/ceres3d.cc, to 1e-6; parity with Ceres unpinned)."""
+    w = csm.SyntheticWorld3D(num_nodes=10, num_submaps=2, seed=43)
+    runs = {}
+    for refine in (False, True):
+        o = cb.ConstraintBuilderOptions(sampling_ratio=1.0, refine_with_ceres=refine)
+        builder = cb.ConstraintBuilder3D(o)
+        for node in range(w.num_nodes):
+            for s in range(w.num_submaps):
+                sub = cb.Submap3D(w.high_resolution, w.high_cells[s], w.low_resolution,
+                                  w.low_cells[s], w.submap_hist[s])
+                builder.MaybeAddGlobalConstraint((0, s), sub, (0, node), w.node(node),
+                                                 w.node_rotation(node), (1.0, 0.0, 0.0, 0.0))
+            builder.NotifyEndOfNode()
+        got = []
+        builder.WhenDone(got.append)
+        runs[refine] = got[0]
+    plain, refined = runs[False], runs[True]
+    assert len(plain) == len(refined) and len(plain) > 0
+    ogr = {}
+    o3 = cb.ConstraintBuilderOptions().ceres_scan_matcher_options_3d
+    opts = (o3.occupied_space_weight_0, o3.occupied_space_weight_1, o3.translation_weight,
+            o3.rotation_weight, o3.max_num_iterations)
+    for a, b in zip(plain, refined):
+        assert a.submap_id == b.submap_id and a.node_id == b.node_id and a.score == b.score
+        s, n = a.submap_id[1], a.node_id[1]
+        if s not in ogr:
+            hg, lg = oracle.hybrid_grid(w.high_resolution), oracle.hybrid_grid(w.low_resolution)
+            hg.set_values(*w.high_cells[s])
+            lg.set_values(*w.low_cells[s])
+            ogr[s] = (hg, lg)
+        t, q = a.relative_pose
+        (rt, rq), _ = oracle.ceres3d_match(ogr[s][0], ogr[s][1], w.high[n], w.low[n], opts, t, t, q)
+        assert np.allclose(b.relative_pose[0], rt, atol=1e-6)
+        assert np.allclose(b.relative_pose[1], rq, atol=1e-6)
