@@ -464,6 +464,20 @@ def fast3d_bench(csm, ctx, args, rank=0, world_size=1, dist=None, coll_dev=None,
            if tm.fast3d_kernel_ms else 0.0, "setup_s": gen}
     if rank != 0 or world_size != 1:
         return out
+    # CeresScanMatcher3D refinement of the last step's accepted matches
+    # (constraint_builder_3d.cc:264-275), one device batch.
+    ok = np.nonzero(res3["status"] == csm.CSM_OK)[0]
+    if len(ok):
+        flat = [g for pair in grids for g in pair]
+        items = [(2 * int(sub[i]), 2 * int(sub[i]) + 1, int(nod[i]),
+                  (tuple(res3["t"][i]), tuple(res3["q"][i])), tuple(res3["t"][i])) for i in ok]
+        csm.ceres_refine_batch_3d(flat, nodes, items, context=ctx)  # warm-up
+        a = time.perf_counter()
+        _, it3 = csm.ceres_refine_batch_3d(flat, nodes, items, context=ctx)
+        out["ceres3d"] = {"accepted": int(len(ok)), "gpu_ms": (time.perf_counter() - a) * 1e3,
+                          "mean_iterations": float(np.mean(it3)),
+                          "workload": "CeresScanMatcher3D::Match on one C5 step's accepted "
+                                      "matches (pose_graph.lua options)"}
     if not args.no_cpu:
         try:
             sys.path.insert(0, os.path.join(ROOT, "tests"))
