@@ -252,6 +252,19 @@ _SIGNATURES = {
                                             C.POINTER(C.c_int32), C.POINTER(MapLimits)]),
     "csm_grid2d_crop": (C.c_int, [C.POINTER(MapLimits), C.POINTER(C.c_uint16),
                                   C.POINTER(MapLimits), C.POINTER(C.c_uint16), C.c_int64]),
+    "csm_pbstream_open": (C.c_int, [C.c_char_p, C.POINTER(C.c_void_p)]),
+    "csm_pbstream_close": (None, [C.c_void_p]),
+    "csm_pbstream_format_version": (C.c_uint32, [C.c_void_p]),
+    "csm_pbstream_num_submaps2d": (C.c_int32, [C.c_void_p]),
+    "csm_pbstream_num_nodes": (C.c_int32, [C.c_void_p]),
+    "csm_pbstream_submap2d": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_int32),
+                                        C.POINTER(MapLimits), C.POINTER(C.c_float),
+                                        C.POINTER(C.c_int32), C.POINTER(C.c_double),
+                                        C.POINTER(C.c_uint16), C.c_int64]),
+    "csm_pbstream_node": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_int32),
+                                    C.POINTER(C.c_int64), C.POINTER(C.c_double),
+                                    C.POINTER(C.c_double), C.POINTER(C.c_float), C.c_int64,
+                                    C.POINTER(C.c_int32)]),
     "csm_strerror": (C.c_char_p, [C.c_int]),
 }
 
@@ -343,6 +356,78 @@ def ComputeCroppedGrid(grid: "ProbabilityGrid") -> "ProbabilityGrid":
     nx, ny = out_lim.num_x_cells, out_lim.num_y_cells
     return ProbabilityGrid(out_lim.resolution, out_lim.max_x, out_lim.max_y,
                            out[:nx * ny].reshape(ny, nx).copy())
+
+
+@dataclass
+class SerializedSubmap2D:
+    """A Submap2D read from a pbstream (mapping/proto/submap.proto:24-29)."""
+    trajectory_id: int
+    submap_index: int
+    local_pose: np.ndarray  # (tx, ty, tz, qw, qx, qy, qz)
+    finished: bool
+    grid: ProbabilityGrid
+
+
+@dataclass
+class SerializedNode:
+    """A trajectory node read from a pbstream (trajectory_node_data.proto:23-32):
+    ``points`` is the decompressed filtered_gravity_aligned_point_cloud."""
+    trajectory_id: int
+    node_index: int
+    timestamp: int
+    local_pose: np.ndarray  # (tx, ty, tz, qw, qx, qy, qz)
+    gravity_alignment: np.ndarray  # (w, x, y, z)
+    points: np.ndarray  # (n, 3) float32
+
+
+@dataclass
+class PbStream:
+    format_version: int
+    submaps: list
+    nodes: list
+
+
+def read_pbstream(path) -> PbStream:
+    """Loads the Submap2D grids and node clouds of a serialized state file
+    (io/proto_stream.cc, io/internal/mapping_state_serialization.cc) through
+    csm_pbstream_*; other message kinds are skipped."""
+    lib = load_library()
+    h = C.c_void_p()
+    _check(lib.csm_pbstream_open(os.fsencode(os.fspath(path)), C.byref(h)), "csm_pbstream_open")
+    try:
+        submaps, nodes = [], []
+        for i in range(lib.csm_pbstream_num_submaps2d(h)):
+            ids = (C.c_int32 * 2)()
+            lim = MapLimits()
+            cc = (C.c_float * 2)()
+            fin = C.c_int32()
+            pose = np.zeros(7, np.float64)
+            _check(lib.csm_pbstream_submap2d(h, i, ids, C.byref(lim), cc, C.byref(fin),
+                                             _ptr(pose, C.c_double), None, 0),
+                   "csm_pbstream_submap2d")
+            cells = np.zeros((lim.num_y_cells, lim.num_x_cells), np.uint16)
+            _check(lib.csm_pbstream_submap2d(h, i, None, None, None, None, None,
+                                             _ptr(cells, C.c_uint16), cells.size),
+                   "csm_pbstream_submap2d")
+            grid = ProbabilityGrid(lim.resolution, lim.max_x, lim.max_y, cells,
+                                   float(cc[0]), float(cc[1]))
+            submaps.append(SerializedSubmap2D(ids[0], ids[1], pose, bool(fin.value), grid))
+        for i in range(lib.csm_pbstream_num_nodes(h)):
+            ids = (C.c_int32 * 2)()
+            ts = C.c_int64()
+            pose = np.zeros(7, np.float64)
+            grav = np.zeros(4, np.float64)
+            n = C.c_int32()
+            _check(lib.csm_pbstream_node(h, i, ids, C.byref(ts), _ptr(pose, C.c_double),
+                                         _ptr(grav, C.c_double), None, 0, C.byref(n)),
+                   "csm_pbstream_node")
+            pts = np.zeros((n.value, 3), np.float32)
+            _check(lib.csm_pbstream_node(h, i, None, None, None, None, _ptr(pts, C.c_float),
+                                         n.value, None), "csm_pbstream_node")
+            nodes.append(SerializedNode(ids[0], ids[1], ts.value, pose, grav, pts))
+        return PbStream(int(lib.csm_pbstream_format_version(h)), submaps, nodes)
+    finally:
+        lib.csm_pbstream_close(h)
 
 
 @dataclass

@@ -421,6 +421,35 @@ int csm_adaptive_voxel_filter_device(csm_context* ctx, const float* d_xyz,
                                      const csm_adaptive_voxel_filter_options* options,
                                      uint8_t* d_keep, int32_t* d_counts);
 
+/* ---- pbstream ingest --------------------------------------------------------
+ * Reads a serialized state file (io/proto_stream.cc:26-86: magic, then per
+ * message an 8-byte size and a gzip member; SerializationHeader then
+ * SerializedData, mapping/proto/serialization.proto:72-88) and keeps what a
+ * ConstraintBuilder2D needs: every Submap2D (id, local pose, finished flag,
+ * Grid2D as in Grid2D::Grid2D(proto), mapping/2d/grid_2d.cc:75-96) and every
+ * Node (id, timestamp, gravity alignment, local pose and the decompressed
+ * filtered_gravity_aligned_point_cloud, sensor/compressed_point_cloud.cc:79-97).
+ * Poses are (tx, ty, tz, qw, qx, qy, qz); gravity_alignment is (w, x, y, z).
+ * Other message kinds (pose graph, options, 3D submaps, sensor data) are
+ * skipped. Host-only; returns CSM_EINVAL for a malformed file. Pass NULL for
+ * any output not wanted; cells / xyz need capacity >= the item's size
+ * (CSM_ERANGE otherwise). */
+typedef struct csm_pbstream csm_pbstream;
+int csm_pbstream_open(const char* path, csm_pbstream** out);
+void csm_pbstream_close(csm_pbstream* stream);
+uint32_t csm_pbstream_format_version(const csm_pbstream* stream);
+int32_t csm_pbstream_num_submaps2d(const csm_pbstream* stream);
+int32_t csm_pbstream_num_nodes(const csm_pbstream* stream);
+/* ids = (trajectory_id, submap_index); min_max_cc = (min, max)
+ * correspondence cost; cells are num_x_cells * num_y_cells values, x fastest. */
+int csm_pbstream_submap2d(const csm_pbstream* stream, int32_t index, int32_t* ids,
+                          csm_map_limits* limits, float* min_max_cc, int32_t* finished,
+                          double* local_pose7, uint16_t* cells, int64_t capacity);
+/* ids = (trajectory_id, node_index); capacity and num_points count points. */
+int csm_pbstream_node(const csm_pbstream* stream, int32_t index, int32_t* ids,
+                      int64_t* timestamp, double* local_pose7, double* gravity_alignment,
+                      float* xyz, int64_t capacity, int32_t* num_points);
+
 /* Human-readable text for a return code. */
 const char* csm_strerror(int code);
 
