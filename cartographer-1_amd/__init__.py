@@ -265,6 +265,19 @@ _SIGNATURES = {
                                     C.POINTER(C.c_int64), C.POINTER(C.c_double),
                                     C.POINTER(C.c_double), C.POINTER(C.c_float), C.c_int64,
                                     C.POINTER(C.c_int32)]),
+    "csm_pbstream_node_cloud": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.POINTER(C.c_float),
+                                          C.c_int64, C.POINTER(C.c_int32)]),
+    "csm_pbstream_node_histogram": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_float),
+                                              C.c_int32, C.POINTER(C.c_int32)]),
+    "csm_pbstream_num_submaps3d": (C.c_int32, [C.c_void_p]),
+    "csm_pbstream_submap3d": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_int32),
+                                        C.POINTER(C.c_int32), C.POINTER(C.c_double),
+                                        C.POINTER(C.c_int64), C.POINTER(C.c_int32)]),
+    "csm_pbstream_submap3d_grid": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32,
+                                             C.POINTER(C.c_float), C.POINTER(C.c_int32),
+                                             C.POINTER(C.c_uint16), C.c_int64]),
+    "csm_pbstream_submap3d_histogram": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_float),
+                                                  C.c_int32]),
     "csm_strerror": (C.c_char_p, [C.c_int]),
 }
 
@@ -378,6 +391,24 @@ class SerializedNode:
     local_pose: np.ndarray  # (tx, ty, tz, qw, qx, qy, qz)
     gravity_alignment: np.ndarray  # (w, x, y, z)
     points: np.ndarray  # (n, 3) float32
+    # 3D node data (trajectory_node_data.proto:28-30); empty for 2D nodes.
+    high_resolution_points: np.ndarray = None
+    low_resolution_points: np.ndarray = None
+    rotational_scan_matcher_histogram: np.ndarray = None
+
+
+@dataclass
+class SerializedSubmap3D:
+    """A Submap3D read from a pbstream (mapping/proto/submap.proto:32-39): each
+    grid is (resolution, (n, 3) int32 indices, uint16 values), values as
+    HybridGrid(proto) stores them (hybrid_grid.h:473-484)."""
+    trajectory_id: int
+    submap_index: int
+    local_pose: np.ndarray
+    finished: bool
+    high_resolution_hybrid_grid: tuple
+    low_resolution_hybrid_grid: tuple
+    rotational_scan_matcher_histogram: np.ndarray
 
 
 @dataclass
@@ -385,6 +416,7 @@ class PbStream:
     format_version: int
     submaps: list
     nodes: list
+    submaps3d: list = None
 
 
 def read_pbstream(path) -> PbStream:
@@ -424,8 +456,45 @@ def read_pbstream(path) -> PbStream:
             pts = np.zeros((n.value, 3), np.float32)
             _check(lib.csm_pbstream_node(h, i, None, None, None, None, _ptr(pts, C.c_float),
                                          n.value, None), "csm_pbstream_node")
-            nodes.append(SerializedNode(ids[0], ids[1], ts.value, pose, grav, pts))
-        return PbStream(int(lib.csm_pbstream_format_version(h)), submaps, nodes)
+            clouds = []
+            for which in (1, 2):
+                _check(lib.csm_pbstream_node_cloud(h, i, which, None, 0, C.byref(n)),
+                       "csm_pbstream_node_cloud")
+                c = np.zeros((n.value, 3), np.float32)
+                _check(lib.csm_pbstream_node_cloud(h, i, which, _ptr(c, C.c_float), n.value, None),
+                       "csm_pbstream_node_cloud")
+                clouds.append(c)
+            _check(lib.csm_pbstream_node_histogram(h, i, None, 0, C.byref(n)),
+                   "csm_pbstream_node_histogram")
+            hist = np.zeros(n.value, np.float32)
+            _check(lib.csm_pbstream_node_histogram(h, i, _ptr(hist, C.c_float), n.value, None),
+                   "csm_pbstream_node_histogram")
+            nodes.append(SerializedNode(ids[0], ids[1], ts.value, pose, grav, pts, clouds[0],
+                                        clouds[1], hist))
+        submaps3d = []
+        for i in range(lib.csm_pbstream_num_submaps3d(h)):
+            ids = (C.c_int32 * 2)()
+            fin = C.c_int32()
+            pose = np.zeros(7, np.float64)
+            cells = (C.c_int64 * 2)()
+            hs = C.c_int32()
+            _check(lib.csm_pbstream_submap3d(h, i, ids, C.byref(fin), _ptr(pose, C.c_double),
+                                             cells, C.byref(hs)), "csm_pbstream_submap3d")
+            grids = []
+            for which in (0, 1):
+                res = C.c_float()
+                idx = np.zeros((cells[which], 3), np.int32)
+                val = np.zeros(cells[which], np.uint16)
+                _check(lib.csm_pbstream_submap3d_grid(h, i, which, C.byref(res),
+                                                      _ptr(idx, C.c_int32), _ptr(val, C.c_uint16),
+                                                      cells[which]), "csm_pbstream_submap3d_grid")
+                grids.append((float(res.value), idx, val))
+            hist = np.zeros(hs.value, np.float32)
+            _check(lib.csm_pbstream_submap3d_histogram(h, i, _ptr(hist, C.c_float), hs.value),
+                   "csm_pbstream_submap3d_histogram")
+            submaps3d.append(SerializedSubmap3D(ids[0], ids[1], pose, bool(fin.value), grids[0],
+                                                grids[1], hist))
+        return PbStream(int(lib.csm_pbstream_format_version(h)), submaps, nodes, submaps3d)
     finally:
         lib.csm_pbstream_close(h)
 

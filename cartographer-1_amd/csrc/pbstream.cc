@@ -19,8 +19,17 @@
 // Cost (:22-44), cells must fit uint16 (:93). Clouds decode exactly as
 // CompressedPointCloud::ConstIterator (sensor/compressed_point_cloud.cc:79-97):
 // int block origin + raster offset, times 0.001f.
+//
+// 3D: Submap3D (submap.proto:32-39) keeps both HybridGrids (hybrid_grid.proto:
+// resolution, sint32 x/y/z indices, int32 values) and the rotational
+// histogram; values load as HybridGrid(proto) (mapping/3d/hybrid_grid.h:
+// 473-484) does, through ValueToProbability then ProbabilityToValue
+// (probability_values.cc:27-49, probability_values.h:32-93), so an unknown 0
+// loads as 1 and the update marker is dropped. Nodes also keep their high /
+// low resolution clouds and histogram (trajectory_node_data.proto:28-30).
 #include <zlib.h>
 
+#include <cmath>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -140,6 +149,34 @@ void Int32s(int wire, Reader& r, std::vector<int32_t>* out) {
   }
 }
 
+// repeated sint32 (zigzag), packed or not.
+void SInt32s(int wire, Reader& r, std::vector<int32_t>* out) {
+  auto zz = [](uint64_t n) {
+    const uint32_t u = static_cast<uint32_t>(n);
+    return static_cast<int32_t>((u >> 1) ^ (~(u & 1) + 1));
+  };
+  if (wire == 2) {
+    Reader s = r.Sub();
+    while (!s.Done()) out->push_back(zz(s.Varint()));
+    if (!s.ok) r.ok = false;
+  } else if (wire == 0) {
+    out->push_back(zz(r.Varint()));
+  } else {
+    r.Skip(wire);
+  }
+}
+
+// repeated float, packed (fixed32 run) or one value per key.
+void Floats(int wire, Reader& r, std::vector<float>* out) {
+  if (wire == 2) {
+    Reader s = r.Sub();
+    while (!s.Done()) out->push_back(s.Float(5));
+    if (!s.ok) r.ok = false;
+  } else {
+    out->push_back(r.Float(wire));
+  }
+}
+
 bool Vec(Reader r, double* v, int n) {
   return Fields(r, [&](int f, int w, Reader& x) {
     if (f >= 1 && f <= n) v[f - 1] = x.Double(w);
@@ -206,8 +243,64 @@ struct NodeRec {
   int64_t timestamp = 0;
   double local_pose[7] = {0., 0., 0., 1., 0., 0., 0.};
   double gravity_alignment[4] = {1., 0., 0., 0.};
-  std::vector<float> xyz;
+  std::vector<float> clouds[3];  // filtered gravity-aligned, high, low resolution
+  std::vector<float> histogram;
 };
+
+struct HybridGridRec {
+  float resolution = 0.f;
+  std::vector<int32_t> xyz;  // 3 per cell
+  std::vector<uint16_t> values;
+};
+
+struct Submap3DRec {
+  int32_t trajectory_id = 0, submap_index = 0;
+  int32_t finished = 0;
+  double local_pose[7] = {0., 0., 0., 1., 0., 0., 0.};
+  HybridGridRec grids[2];  // high, low resolution
+  std::vector<float> histogram;
+};
+
+// ProbabilityToValue(ValueToProbability(v)): PrecomputeValueToBoundedFloat's
+// table (probability_values.cc:27-49, both update-marker halves) followed by
+// BoundedFloatToValue (probability_values.h:32-45).
+uint16_t LoadedProbabilityValue(uint16_t value) {
+  const float kMinProbability = 0.1f, kMaxProbability = 1.f - kMinProbability;
+  const uint16_t v = value & 0x7fff;
+  float p = kMinProbability;
+  if (v != 0) {
+    const float kScale = (kMaxProbability - kMinProbability) / (32768 - 2.f);
+    p = static_cast<float>(v) * kScale + (kMinProbability - kScale);
+  }
+  const float c = std::fmin(std::fmax(p, kMinProbability), kMaxProbability);
+  return static_cast<uint16_t>(
+      std::lround((c - kMinProbability) * (32766.f / (kMaxProbability - kMinProbability))) + 1);
+}
+
+int ParseHybridGrid(Reader r, HybridGridRec* g) {
+  std::vector<int32_t> x, y, z, values;
+  bool ok = Fields(r, [&](int f, int w, Reader& q) {
+    if (f == 1) g->resolution = q.Float(w);
+    else if (f == 3) SInt32s(w, q, &x);
+    else if (f == 4) SInt32s(w, q, &y);
+    else if (f == 5) SInt32s(w, q, &z);
+    else if (f == 6) Int32s(w, q, &values);
+    else q.Skip(w);
+  });
+  if (!ok || x.size() != values.size() || y.size() != values.size() ||
+      z.size() != values.size())  // hybrid_grid.h:475-477
+    return CSM_EINVAL;
+  g->xyz.resize(3 * values.size());
+  g->values.resize(values.size());
+  for (size_t i = 0; i < values.size(); ++i) {
+    if (values[i] < 0 || values[i] > 0xffff) return CSM_EINVAL;
+    g->xyz[3 * i] = x[i];
+    g->xyz[3 * i + 1] = y[i];
+    g->xyz[3 * i + 2] = z[i];
+    g->values[i] = LoadedProbabilityValue(static_cast<uint16_t>(values[i]));
+  }
+  return CSM_OK;
+}
 
 bool ParseLimits(Reader r, csm_map_limits* l) {
   bool ok = true;
@@ -262,16 +355,27 @@ int ParseGrid(Reader r, Submap2DRec* s) {
   return CSM_OK;
 }
 
-// Returns 1 when a Submap2D was read into *s, 0 for a Submap3D (skipped).
-int ParseSubmap(Reader r, Submap2DRec* s) {
-  bool ok = true, is2d = false;
+// Returns 1 when a Submap2D was read into *s, 2 for a Submap3D read into *s3.
+int ParseSubmap(Reader r, Submap2DRec* s, Submap3DRec* s3) {
+  bool ok = true, is2d = false, is3d = false;
   int rc = CSM_OK;
   ok &= Fields(r, [&](int f, int w, Reader& x) {
     if (f == 1 && w == 2) {
       ok &= Fields(x.Sub(), [&](int g, int v, Reader& y) {
-        if (g == 1) s->trajectory_id = static_cast<int32_t>(y.Int(v));
-        else if (g == 2) s->submap_index = static_cast<int32_t>(y.Int(v));
+        if (g == 1) s->trajectory_id = s3->trajectory_id = static_cast<int32_t>(y.Int(v));
+        else if (g == 2) s->submap_index = s3->submap_index = static_cast<int32_t>(y.Int(v));
         else y.Skip(v);
+      });
+    } else if (f == 3 && w == 2) {
+      is3d = true;
+      ok &= Fields(x.Sub(), [&](int g, int v, Reader& y) {
+        int grc = CSM_OK;
+        if (g == 1 && v == 2) ok &= Rigid(y.Sub(), s3->local_pose);
+        else if (g == 3) s3->finished = y.Int(v) != 0;
+        else if ((g == 4 || g == 5) && v == 2) grc = ParseHybridGrid(y.Sub(), &s3->grids[g - 4]);
+        else if (g == 6) Floats(v, y, &s3->histogram);
+        else y.Skip(v);
+        if (grc != CSM_OK) rc = grc;
       });
     } else if (f == 2 && w == 2) {
       is2d = true;
@@ -287,7 +391,7 @@ int ParseSubmap(Reader r, Submap2DRec* s) {
   });
   if (!ok) return CSM_EINVAL;
   if (rc != CSM_OK) return rc;
-  return is2d ? 1 : 0;
+  return is2d ? 1 : (is3d ? 2 : 0);
 }
 
 // CompressedPointCloud::ConstIterator::ReadNextPoint
@@ -333,7 +437,7 @@ int ParseNode(Reader r, NodeRec* n) {
           n->timestamp = y.Int(v);
         } else if (g == 2 && v == 2) {
           ok &= Quat(y.Sub(), n->gravity_alignment);
-        } else if (g == 3 && v == 2) {
+        } else if (g >= 3 && g <= 5 && v == 2) {
           int32_t num_points = 0;
           std::vector<int32_t> data;
           ok &= Fields(y.Sub(), [&](int h, int u, Reader& z) {
@@ -341,7 +445,10 @@ int ParseNode(Reader r, NodeRec* n) {
             else if (h == 3) Int32s(u, z, &data);
             else z.Skip(u);
           });
-          rc = Decompress(data, num_points, &n->xyz);
+          const int drc = Decompress(data, num_points, &n->clouds[g - 3]);
+          if (drc != CSM_OK) rc = drc;
+        } else if (g == 6) {
+          Floats(v, y, &n->histogram);
         } else if (g == 7 && v == 2) {
           ok &= Rigid(y.Sub(), n->local_pose);
         } else {
@@ -368,6 +475,7 @@ bool ReadU64(FILE* f, uint64_t* v) {
 
 struct csm_pbstream {
   std::vector<Submap2DRec> submaps;
+  std::vector<Submap3DRec> submaps3d;
   std::vector<NodeRec> nodes;
   uint32_t format_version = 0;
 };
@@ -413,9 +521,11 @@ int csm_pbstream_open(const char* path, csm_pbstream** out) {
         x.Skip(w);
       } else if (fld == 3 && w == 2) {
         Submap2DRec sub;
-        const int got = ParseSubmap(x.Sub(), &sub);
+        Submap3DRec sub3;
+        const int got = ParseSubmap(x.Sub(), &sub, &sub3);
         if (got < 0) rc = got;
         else if (got == 1) s->submaps.push_back(std::move(sub));
+        else if (got == 2) s->submaps3d.push_back(std::move(sub3));
       } else if (fld == 4 && w == 2) {
         NodeRec node;
         const int got = ParseNode(x.Sub(), &node);
@@ -477,7 +587,7 @@ int csm_pbstream_node(const csm_pbstream* s, int32_t i, int32_t* ids, int64_t* t
                       int64_t capacity, int32_t* num_points) {
   if (!s || i < 0 || i >= static_cast<int32_t>(s->nodes.size())) return CSM_EINVAL;
   const NodeRec& r = s->nodes[i];
-  const int64_t n = static_cast<int64_t>(r.xyz.size() / 3);
+  const int64_t n = static_cast<int64_t>(r.clouds[0].size() / 3);
   if (ids) {
     ids[0] = r.trajectory_id;
     ids[1] = r.node_index;
@@ -488,7 +598,80 @@ int csm_pbstream_node(const csm_pbstream* s, int32_t i, int32_t* ids, int64_t* t
   if (num_points) *num_points = static_cast<int32_t>(n);
   if (xyz) {
     if (capacity < n) return CSM_ERANGE;
-    std::memcpy(xyz, r.xyz.data(), r.xyz.size() * sizeof(float));
+    std::memcpy(xyz, r.clouds[0].data(), r.clouds[0].size() * sizeof(float));
+  }
+  return CSM_OK;
+}
+
+int csm_pbstream_node_cloud(const csm_pbstream* s, int32_t i, int32_t which, float* xyz,
+                            int64_t capacity, int32_t* num_points) {
+  if (!s || i < 0 || i >= static_cast<int32_t>(s->nodes.size()) || which < 0 || which > 2)
+    return CSM_EINVAL;
+  const std::vector<float>& c = s->nodes[i].clouds[which];
+  const int64_t n = static_cast<int64_t>(c.size() / 3);
+  if (num_points) *num_points = static_cast<int32_t>(n);
+  if (xyz) {
+    if (capacity < n) return CSM_ERANGE;
+    std::memcpy(xyz, c.data(), c.size() * sizeof(float));
+  }
+  return CSM_OK;
+}
+
+int csm_pbstream_node_histogram(const csm_pbstream* s, int32_t i, float* histogram,
+                                int32_t capacity, int32_t* size) {
+  if (!s || i < 0 || i >= static_cast<int32_t>(s->nodes.size())) return CSM_EINVAL;
+  const std::vector<float>& h = s->nodes[i].histogram;
+  if (size) *size = static_cast<int32_t>(h.size());
+  if (histogram) {
+    if (capacity < static_cast<int32_t>(h.size())) return CSM_ERANGE;
+    std::memcpy(histogram, h.data(), h.size() * sizeof(float));
+  }
+  return CSM_OK;
+}
+
+int32_t csm_pbstream_num_submaps3d(const csm_pbstream* s) {
+  return s ? static_cast<int32_t>(s->submaps3d.size()) : 0;
+}
+
+int csm_pbstream_submap3d(const csm_pbstream* s, int32_t i, int32_t* ids, int32_t* finished,
+                          double* local_pose7, int64_t* num_cells, int32_t* histogram_size) {
+  if (!s || i < 0 || i >= static_cast<int32_t>(s->submaps3d.size())) return CSM_EINVAL;
+  const Submap3DRec& r = s->submaps3d[i];
+  if (ids) {
+    ids[0] = r.trajectory_id;
+    ids[1] = r.submap_index;
+  }
+  if (finished) *finished = r.finished;
+  if (local_pose7) std::memcpy(local_pose7, r.local_pose, sizeof(r.local_pose));
+  if (num_cells) {
+    num_cells[0] = static_cast<int64_t>(r.grids[0].values.size());
+    num_cells[1] = static_cast<int64_t>(r.grids[1].values.size());
+  }
+  if (histogram_size) *histogram_size = static_cast<int32_t>(r.histogram.size());
+  return CSM_OK;
+}
+
+int csm_pbstream_submap3d_grid(const csm_pbstream* s, int32_t i, int32_t which, float* resolution,
+                               int32_t* xyz_indices, uint16_t* values, int64_t capacity) {
+  if (!s || i < 0 || i >= static_cast<int32_t>(s->submaps3d.size()) || which < 0 || which > 1)
+    return CSM_EINVAL;
+  const HybridGridRec& g = s->submaps3d[i].grids[which];
+  if (resolution) *resolution = g.resolution;
+  if (xyz_indices || values) {
+    if (capacity < static_cast<int64_t>(g.values.size())) return CSM_ERANGE;
+    if (xyz_indices) std::memcpy(xyz_indices, g.xyz.data(), g.xyz.size() * sizeof(int32_t));
+    if (values) std::memcpy(values, g.values.data(), g.values.size() * sizeof(uint16_t));
+  }
+  return CSM_OK;
+}
+
+int csm_pbstream_submap3d_histogram(const csm_pbstream* s, int32_t i, float* histogram,
+                                    int32_t capacity) {
+  if (!s || i < 0 || i >= static_cast<int32_t>(s->submaps3d.size())) return CSM_EINVAL;
+  const std::vector<float>& h = s->submaps3d[i].histogram;
+  if (histogram) {
+    if (capacity < static_cast<int32_t>(h.size())) return CSM_ERANGE;
+    std::memcpy(histogram, h.data(), h.size() * sizeof(float));
   }
   return CSM_OK;
 }

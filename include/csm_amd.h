@@ -430,8 +430,8 @@ int csm_adaptive_voxel_filter_device(csm_context* ctx, const float* d_xyz,
  * Node (id, timestamp, gravity alignment, local pose and the decompressed
  * filtered_gravity_aligned_point_cloud, sensor/compressed_point_cloud.cc:79-97).
  * Poses are (tx, ty, tz, qw, qx, qy, qz); gravity_alignment is (w, x, y, z).
- * Other message kinds (pose graph, options, 3D submaps, sensor data) are
- * skipped. Host-only; returns CSM_EINVAL for a malformed file. Pass NULL for
+ * 3D submaps and the nodes' 3D clouds are kept too (below). Other message
+ * kinds (pose graph, options, sensor data) are skipped. Host-only; returns CSM_EINVAL for a malformed file. Pass NULL for
  * any output not wanted; cells / xyz need capacity >= the item's size
  * (CSM_ERANGE otherwise). */
 typedef struct csm_pbstream csm_pbstream;
@@ -449,6 +449,28 @@ int csm_pbstream_submap2d(const csm_pbstream* stream, int32_t index, int32_t* id
 int csm_pbstream_node(const csm_pbstream* stream, int32_t index, int32_t* ids,
                       int64_t* timestamp, double* local_pose7, double* gravity_alignment,
                       float* xyz, int64_t capacity, int32_t* num_points);
+/* A node's clouds: which = 0 filtered_gravity_aligned_point_cloud (what
+ * csm_pbstream_node returns), 1 high_resolution_point_cloud, 2
+ * low_resolution_point_cloud (the 3D matcher's inputs); and its
+ * rotational_scan_matcher_histogram (size = number of buckets). */
+int csm_pbstream_node_cloud(const csm_pbstream* stream, int32_t index, int32_t which, float* xyz,
+                            int64_t capacity, int32_t* num_points);
+int csm_pbstream_node_histogram(const csm_pbstream* stream, int32_t index, float* histogram,
+                                int32_t capacity, int32_t* size);
+/* Submap3D (submap.proto:32-39): ids, finished, local pose, the cell counts of
+ * its (high, low) resolution HybridGrids and its histogram size. A grid's
+ * cells come back as csm_hybrid_grid_create takes them (xyz_indices 3 per
+ * cell, uint16 values as HybridGrid(proto) stores them, hybrid_grid.h:473-484);
+ * which = 0 high, 1 low resolution. */
+int32_t csm_pbstream_num_submaps3d(const csm_pbstream* stream);
+int csm_pbstream_submap3d(const csm_pbstream* stream, int32_t index, int32_t* ids,
+                          int32_t* finished, double* local_pose7, int64_t* num_cells,
+                          int32_t* histogram_size);
+int csm_pbstream_submap3d_grid(const csm_pbstream* stream, int32_t index, int32_t which,
+                               float* resolution, int32_t* xyz_indices, uint16_t* values,
+                               int64_t capacity);
+int csm_pbstream_submap3d_histogram(const csm_pbstream* stream, int32_t index, float* histogram,
+                                    int32_t capacity);
 
 /* Human-readable text for a return code. */
 const char* csm_strerror(int code);

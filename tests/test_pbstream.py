@@ -273,3 +273,147 @@ def test_stream_loaded_submap_matches_oracle(csm, oracle, tmp_path):
     assert_fast_parity(oracle, om, limits, lg.cells, gpu, ref, True,
                        full_submap_center(limits, lg.cells), pts)
     assert gpu[0]
+
+
+# ---- 3D: Submap3D HybridGrids, node clouds and histograms -------------------
+def f_sint_packed(f, vals):
+    return f_msg(f, b"".join(varint((int(v) << 1) ^ (int(v) >> 31)) for v in vals))
+
+
+def f_floats_packed(f, vals):
+    return f_msg(f, np.asarray(vals, "<f4").tobytes())
+
+
+def hybrid_grid(resolution, idx, values):
+    idx = np.asarray(idx, np.int64).reshape(-1, 3)
+    return (f_flt(1, resolution) + f_sint_packed(3, idx[:, 0]) + f_sint_packed(4, idx[:, 1]) +
+            f_sint_packed(5, idx[:, 2]) + f_packed(6, values))
+
+
+def submap3d_full_msg(traj, index, pose7, high, low, hist, finished=True):
+    sid = f_int(1, traj) + f_int(2, index)
+    s3d = (f_msg(1, rigid3d(pose7)) + f_int(2, 20) + f_int(3, int(finished)) +
+           f_msg(4, hybrid_grid(*high)) + f_msg(5, hybrid_grid(*low)) + f_floats_packed(6, hist))
+    return f_msg(3, f_msg(1, sid) + f_msg(3, s3d))
+
+
+def node3d_msg(traj, index, gravity, filtered, high, low, hist):
+    parts = []
+    decoded = []
+    for fld, pts in ((3, filtered), (4, high), (5, low)):
+        data, dec, _ = compress(pts)
+        parts.append(f_msg(fld, f_int(1, len(pts)) + f_packed(3, data)))
+        decoded.append(dec)
+    nd = (f_int(1, 1) + f_msg(2, quaternion(gravity)) + b"".join(parts) +
+          f_floats_packed(6, hist) + f_msg(7, rigid3d([0, 0, 0, 1, 0, 0, 0])))
+    return f_msg(4, f_msg(1, f_int(1, traj) + f_int(2, index)) + f_msg(5, nd)), decoded
+
+
+def loaded_value(v):
+    """ProbabilityToValue(ValueToProbability(v)) in float32
+    (probability_values.cc:27-49, probability_values.h:32-93)."""
+    f = np.float32
+    v = np.asarray(v, np.int64)
+    kmin = f(0.1)
+    kmax = f(f(1.0) - kmin)
+    scale = f((kmax - kmin) / f(32766.0))
+    low = (v & 0x7FFF).astype(np.float32)
+    p = np.where((v & 0x7FFF) == 0, kmin, (low * scale + f(kmin - scale)).astype(np.float32))
+    c = np.clip(p.astype(np.float32), kmin, kmax)
+    x = ((c - kmin) * f(f(32766.0) / f(kmax - kmin))).astype(np.float32)
+    return (np.floor(x.astype(np.float64) + 0.5) + 1).astype(np.uint16)
+
+
+def test_round_trip_3d(csm, tmp_path):
+    rng = np.random.default_rng(11)
+    hi_idx = rng.integers(-300, 300, size=(400, 3))
+    lo_idx = rng.integers(-60, 60, size=(90, 3))
+    hi_val = rng.integers(1, 32768, size=400)
+    hi_val[:4] = [0, 32768 + 5, 65535, 32767]  # unknown and update-marked values
+    lo_val = rng.integers(1, 32768, size=90)
+    hist = rng.uniform(0, 50, 120).astype(np.float32)
+    pose = [0.5, -1.0, 2.0, math.cos(0.3), 0.0, math.sin(0.3), 0.0]
+    sub = submap3d_full_msg(2, 7, pose, (0.1, hi_idx, hi_val), (0.45, lo_idx, lo_val), hist)
+    clouds = [rng.uniform(-20, 20, size=(k, 3)).astype(np.float32) for k in (300, 150, 60)]
+    nhist = rng.uniform(0, 5, 120).astype(np.float32)
+    nd, decoded = node3d_msg(2, 9, [1, 0, 0, 0], *clouds, nhist)
+    path = tmp_path / "state3d.pbstream"
+    write_stream(path, [sub, nd])
+    st = csm.read_pbstream(path)
+    assert st.submaps == [] and len(st.submaps3d) == 1 and len(st.nodes) == 1
+    s3 = st.submaps3d[0]
+    assert (s3.trajectory_id, s3.submap_index, s3.finished) == (2, 7, True)
+    np.testing.assert_array_equal(s3.local_pose, pose)
+    for (res, idx, val), (eres, eidx, evals) in ((s3.high_resolution_hybrid_grid, (0.1, hi_idx, hi_val)),
+                                                 (s3.low_resolution_hybrid_grid, (0.45, lo_idx, lo_val))):
+        assert res == float(np.float32(eres))
+        np.testing.assert_array_equal(idx, eidx)
+        np.testing.assert_array_equal(val, loaded_value(evals))
+    # Known values round-trip unchanged; 0 loads as 1, the marker is dropped.
+    assert list(s3.high_resolution_hybrid_grid[2][:4]) == [1, 5, 32767, 32767]
+    np.testing.assert_array_equal(loaded_value(np.arange(1, 32768)), np.arange(1, 32768))
+    np.testing.assert_array_equal(s3.rotational_scan_matcher_histogram, hist)
+    n = st.nodes[0]
+    for got, dec in zip((n.points, n.high_resolution_points, n.low_resolution_points), decoded):
+        assert got.tobytes() == dec.tobytes()
+    np.testing.assert_array_equal(n.rotational_scan_matcher_histogram, nhist)
+
+
+def test_hybrid_grid_length_mismatch_fails(csm, tmp_path):
+    """HybridGrid(proto) CHECKs equal index and value counts (hybrid_grid.h:475-477)."""
+    body = (f_flt(1, 0.1) + f_sint_packed(3, [1, 2]) + f_sint_packed(4, [1, 2]) +
+            f_sint_packed(5, [1]) + f_packed(6, [5, 6]))
+    sub = f_msg(3, f_msg(1, f_int(1, 0)) + f_msg(3, f_msg(4, body)))
+    path = tmp_path / "bad3d.pbstream"
+    write_stream(path, [sub])
+    with pytest.raises(csm.CsmError):
+        csm.read_pbstream(path)
+
+
+@pytest.mark.gpu
+def test_stream_loaded_3d_world_matches_direct(csm):
+    """C5-shaped submaps and nodes written to a pbstream and read back give the
+    same FastCorrelativeScanMatcher3D results as the in-memory grids and
+    histograms (both sides use the 1 mm-decoded clouds)."""
+    import tempfile
+    import os
+    w = csm.SyntheticWorld3D(num_nodes=12, num_submaps=2, seed=77)
+    msgs = []
+    for s in range(w.num_submaps):
+        msgs.append(submap3d_full_msg(0, s, [0, 0, 0, 1, 0, 0, 0],
+                                      (w.high_resolution, *w.high_cells[s]),
+                                      (w.low_resolution, *w.low_cells[s]), w.submap_hist[s]))
+    decoded_nodes = []
+    for i in range(w.num_nodes):
+        m, dec = node3d_msg(0, i, w.node(i).gravity_alignment, w.raw[i], w.high[i], w.low[i],
+                            w.node_hist[i])
+        msgs.append(m)
+        decoded_nodes.append(dec)
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "world3d.pbstream")
+        write_stream(path, msgs)
+        st = csm.read_pbstream(path)
+    opts = csm.FastCorrelativeScanMatcherOptions3D()
+    direct, loaded = [], []
+    for s in range(w.num_submaps):
+        direct.append(csm.FastCorrelativeScanMatcher3D(
+            csm.HybridGrid(w.high_resolution, *w.high_cells[s]),
+            csm.HybridGrid(w.low_resolution, *w.low_cells[s]), w.submap_hist[s], opts))
+        s3 = st.submaps3d[s]
+        loaded.append(csm.FastCorrelativeScanMatcher3D(
+            csm.HybridGrid(*s3.high_resolution_hybrid_grid),
+            csm.HybridGrid(*s3.low_resolution_hybrid_grid),
+            s3.rotational_scan_matcher_histogram, opts))
+    nodes_direct = [csm.NodeData3D(dec[1], dec[2], w.node_hist[i], w.node(i).gravity_alignment)
+                    for i, dec in enumerate(decoded_nodes)]
+    nodes_loaded = [csm.NodeData3D(n.high_resolution_points, n.low_resolution_points,
+                                   n.rotational_scan_matcher_histogram, tuple(n.gravity_alignment))
+                    for n in st.nodes]
+    sub_idx = [s for s in range(w.num_submaps) for _ in range(w.num_nodes)]
+    node_idx = [i for _ in range(w.num_submaps) for i in range(w.num_nodes)]
+    pairs = csm.make_pairs_3d(sub_idx, node_idx, 0.3)
+    a = csm.match_batch_3d(direct, nodes_direct, pairs)
+    b = csm.match_batch_3d(loaded, nodes_loaded, pairs)
+    for name in a.dtype.names:
+        np.testing.assert_array_equal(a[name], b[name])
+    assert (a["status"] == 0).sum() >= 2
