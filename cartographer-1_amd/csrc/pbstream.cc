@@ -496,7 +496,7 @@ int csm_pbstream_open(const char* path, csm_pbstream** out) {
   bool header = true;
   uint64_t size;
   while (rc == CSM_OK && ReadU64(f, &size)) {
-    if (size > (1ull << 34)) {
+    if (size > 0xffffffffull) {  // one zlib call takes a uInt-sized input
       rc = CSM_EINVAL;
       break;
     }
