@@ -456,6 +456,11 @@ int csm_fast2d_create(csm_context* ctx, const csm_map_limits* limits,
     d.quad_h[l] = d.wide_ny[l] + h;
     d.quad_pws[l] = (d.quad_w[l] + 2 * h - 1) / (2 * h);
     d.quad_pph[l] = (d.quad_h[l] + 2 * h - 1) / (2 * h);
+#ifdef CSM_QUAD_TILED
+    // Planes stored as 8 x 4 tiles of entries (one 128 B line each).
+    d.quad_pws[l] = (d.quad_pws[l] + 7) & ~7;
+    d.quad_pph[l] = (d.quad_pph[l] + 3) & ~3;
+#endif
     const size_t qb = static_cast<size_t>(2 * h) * (2 * h) * d.quad_pws[l] * d.quad_pph[l] * 4;
     if (qb > 0x7fffff00u) return CSM_ERANGE;
     d.quad_bytes[l] = static_cast<int32_t>(qb);

@@ -555,7 +555,15 @@ __global__ void pyramid_quad(const uint8_t* __restrict__ level, int wnx, int wny
   const int ps = pws * pph;
   const int pi = o / ps, k = o - pi * ps;
   const int fx = pi & (p - 1), fy = pi >> s;
+#ifdef CSM_QUAD_TILED
+  // 8 x 4 tiles of entries, row-major tiles (pws % 8 == 0, pph % 4 == 0).
+  const int tile = k >> 5, inner = k & 31;
+  const int tiles_x = pws >> 3;
+  const int ty = tile / tiles_x, tx = tile - ty * tiles_x;
+  const int ky = (ty << 2) + (inner >> 3), kx = (tx << 3) + (inner & 7);
+#else
   const int ky = k / pws, kx = k - ky * pws;
+#endif
   const int xq = (kx << s) + fx, yq = (ky << s) + fy;
   uint32_t v = 0;
   if (xq < qw && yq < qh) {
@@ -636,8 +644,14 @@ __device__ __forceinline__ void V4Score(V4Shared& sh, const uint32_t* pts, const
     const bool valid = in && static_cast<unsigned>(X) < static_cast<unsigned>(qw) &&
                        static_cast<unsigned>(Y) < static_cast<unsigned>(qh);
     const int a = __umul24((((Y & pmask) << sft) | (X & pmask)), ps4) + qoff;
+#ifdef CSM_QUAD_TILED
+    const int ey = Y >> sft, ex = X >> sft;
+    const int b = __umul24(ey >> 2, pws4 << 2) + a + ((ey & 3) << 5);
+    return valid ? ((ex >> 3) << 7) + ((ex & 7) << 2) + b : kOOB;
+#else
     const int b = __umul24(Y >> sft, pws4) + a;
     return valid ? ((X >> sft) << 2) + b : kOOB;
+#endif
   };
   // v_dot4_u32_u8 with the run count in one byte of the weight multiplies
   // that child's byte by the count and accumulates.
