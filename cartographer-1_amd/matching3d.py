@@ -133,6 +133,26 @@ class NodeData3D:
         return n
 
 
+class NodeSet3D:
+    """A node list converted once to the C-ABI's csm_node3d array (the clouds
+    stay referenced, not copied). match_batch_3d / ceres_refine_batch_3d take
+    it in place of a NodeData3D sequence when the same nodes are searched
+    repeatedly, as a ConstraintBuilder's pending nodes are."""
+
+    def __init__(self, nodes: Sequence[NodeData3D]):
+        self.nodes = list(nodes)
+        self.array = (Node3D * max(len(self.nodes), 1))(*[n.to_c() for n in self.nodes])
+
+    def __len__(self):
+        return len(self.nodes)
+
+
+def _c_nodes(nodes):
+    if isinstance(nodes, NodeSet3D):
+        return nodes.array
+    return (Node3D * max(len(nodes), 1))(*[n.to_c() for n in nodes])
+
+
 @dataclass
 class Result:
     """FastCorrelativeScanMatcher3D::Result."""
@@ -243,7 +263,7 @@ def match_batch_3d(matchers: Sequence[FastCorrelativeScanMatcher3D], nodes: Sequ
     lib = ctx._lib
     assert PAIR3_DTYPE.itemsize == C.sizeof(Pair3D)
     assert RESULT3_DTYPE.itemsize == C.sizeof(Result3D)
-    cnodes = (Node3D * len(nodes))(*[n.to_c() for n in nodes])
+    cnodes = _c_nodes(nodes)
     handles = (C.c_void_p * len(matchers))(*[m.handle for m in matchers])
     if isinstance(pairs, np.ndarray):
         arr = np.ascontiguousarray(pairs, PAIR3_DTYPE)
@@ -279,7 +299,7 @@ def ceres_refine_batch_3d(grids: Sequence[HybridGrid], nodes: Sequence[NodeData3
         citems[i].initial = _pose(init)
         for a in range(3):
             citems[i].target[a] = float(target[a])
-    cnodes = (Node3D * max(len(nodes), 1))(*[nd.to_c() for nd in nodes])
+    cnodes = _c_nodes(nodes)
     handles = (C.c_void_p * max(len(grids), 1))(*[g.handle for g in grids])
     out = (Pose3D * max(n, 1))()
     iters = np.zeros(max(n, 1), np.int32)
