@@ -1024,6 +1024,30 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
             r1 = __popcll(b0) + __popcll(b1 & below);
             s0 = m0 && r0 < nodes;
             s1 = m1 && r1 < nodes;
+#ifdef CSM_SORT_BATCH
+            // Slot order by (yo, xo): lanes next to each other then look up
+            // neighbouring dwords of one plane row.
+            auto key = [](uint32_t x) {
+              return (((x >> 16) ^ 0x8000u) << 16) | ((x & 0xffffu) ^ 0x8000u);
+            };
+            const uint32_t k0 = key(e0.x), k1 = key(e1.x);
+            const unsigned long long q0 = __ballot(s0), q1 = __ballot(s1);
+            int n0 = 0, n1 = 0;
+            for (unsigned long long m = q0; m; m &= m - 1) {
+              const int j = static_cast<int>(__ffsll(static_cast<long long>(m))) - 1;
+              const uint32_t kj = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(k0), j));
+              n0 += kj < k0;
+              n1 += kj < k1;
+            }
+            for (unsigned long long m = q1; m; m &= m - 1) {
+              const int j = static_cast<int>(__ffsll(static_cast<long long>(m))) - 1;
+              const uint32_t kj = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(k1), j));
+              n0 += kj < k0;
+              n1 += kj < k1;
+            }
+            if (s0) r0 = n0;
+            if (s1) r1 = n1;
+#endif
             if (s0) {
               sh.node_xo[r0] = static_cast<int16_t>(e0.x & 0xffff);
               sh.node_yo[r0] = static_cast<int>(e0.x) >> 16;
