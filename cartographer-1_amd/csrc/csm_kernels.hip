@@ -1019,7 +1019,8 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
           bool s0 = false, s1 = false;
           int r0 = 0, r1 = 0;
           if (ne > 0) {
-            nodes = 1 << (31 - __clz(ne));
+            // The 128-entry window can hold more than kBatchNodes matches.
+            nodes = 1 << (31 - __clz(min(ne, kBatchNodes)));
             r0 = __popcll(b0 & below);
             r1 = __popcll(b0) + __popcll(b1 & below);
             s0 = m0 && r0 < nodes;
@@ -1078,7 +1079,8 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
             // Same-level batches: stop at the first entry of another level.
             const int top_lvl = static_cast<int>(sh.stack[sp - 1].y >> 27);
             const unsigned long long diff = __ballot(!(in && static_cast<int>(ent.y >> 27) == top_lvl));
-            const int run = static_cast<int>(__ffsll(static_cast<long long>(diff))) - 1;
+            // diff == 0: every one of the 64 lanes holds a top-level entry.
+            const int run = diff ? static_cast<int>(__ffsll(static_cast<long long>(diff))) - 1 : 64;
             in = lane < run;
           }
           const unsigned long long inm = __ballot(in);

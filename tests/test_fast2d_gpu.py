@@ -283,3 +283,30 @@ def test_run_lists_parity(csm, oracle, world):
         kinds.append(assert_fast_parity(oracle, om, limits, g.cells, gpu, ref, True,
                                         full_submap_center(limits, g.cells), c))
     assert kinds.count("nomatch") < len(kinds)
+
+
+@pytest.mark.parametrize("mode", ["0", "2"])
+def test_batch_selection_modes_parity(csm, oracle, world, mode, monkeypatch):
+    """The v4 kernel's other batch-selection modes (CSM_MIXED_LEVELS: 0 =
+    same-level runs from the stack top, 2 = one (rotation, level) group from
+    a 128-entry window, capped at kBatchNodes) keep parity with the oracle."""
+    monkeypatch.setenv("CSM_MIXED_LEVELS", mode)
+    opts = csm.FastCorrelativeScanMatcherOptions2D(7.0, math.radians(30), 7)
+    mats = [csm.FastCorrelativeScanMatcher2D(world.grid(s), opts) for s in range(8)]
+    scans = csm.ScanSet(None, packed=(world.points, world.offsets))
+    pairs_sn = [(s, int(world.submap_nodes[s])) for s in range(8)] + [(1, 3), (2, 40), (5, 17)]
+    pairs = csm.make_pairs([p[0] for p in pairs_sn], [p[1] for p in pairs_sn], 0.55)
+    res = csm.match_batch(mats, scans, pairs)
+    matched = 0
+    for k, (s, n) in enumerate(pairs_sn):
+        g = world.grid(s)
+        limits = (g.resolution, g.max_x, g.max_y)
+        om = oracle.fast2d(limits, g.cells, 7.0, math.radians(30), 7)
+        cloud = world.cloud(n)
+        ref = om.match_full_submap(cloud, 0.55)
+        gpu = (res[k]["status"] == 0, float(res[k]["score"]),
+               (res[k]["x"], res[k]["y"], res[k]["theta"]))
+        assert_fast_parity(oracle, om, limits, g.cells, gpu, ref, True,
+                           full_submap_center(limits, g.cells), cloud)
+        matched += int(gpu[0])
+    assert matched >= 3
