@@ -487,6 +487,9 @@ int csm_pbstream_open(const char* path, csm_pbstream** out) {
   *out = nullptr;
   FILE* f = std::fopen(path, "rb");
   if (!f) return CSM_EINVAL;
+  std::fseek(f, 0, SEEK_END);
+  const long file_size = std::ftell(f);
+  std::fseek(f, 0, SEEK_SET);
   auto* s = new csm_pbstream();
   int rc = CSM_OK;
   uint64_t magic = 0;
@@ -496,7 +499,10 @@ int csm_pbstream_open(const char* path, csm_pbstream** out) {
   bool header = true;
   uint64_t size;
   while (rc == CSM_OK && ReadU64(f, &size)) {
-    if (size > 0xffffffffull) {  // one zlib call takes a uInt-sized input
+    // One zlib call takes a uInt-sized input; a size past the end of the file
+    // is a truncated or corrupt stream (checked before allocating).
+    if (size > 0xffffffffull || file_size < 0 ||
+        size > static_cast<uint64_t>(file_size - std::ftell(f))) {
       rc = CSM_EINVAL;
       break;
     }
