@@ -200,10 +200,10 @@ def main():
 
 def committed_traffic(args, world_size):
     """HBM-side bytes per search launch from the committed PMC pass
-    (profiles/r1d/traffic_c2.json: rocprofv3 --pmc FETCH_SIZE, x2 gfx950
+    (profiles/r1e/traffic_c2.json: rocprofv3 --pmc FETCH_SIZE, x2 gfx950
     correction). PMC counters cannot be read from inside this process, so the
     figure is reported only when this run's workload is the profiled one."""
-    path = os.path.join(ROOT, "profiles", "r1d", "traffic_c2.json")
+    path = os.path.join(ROOT, "profiles", "r1e", "traffic_c2.json")
     try:
         t = json.load(open(path))
     except (OSError, ValueError):
