@@ -124,8 +124,10 @@ def main():
     barrier_sync()
     t_start = time.perf_counter()
     accepted = 0
+    errors = 0  # pairs whose search returned an error status (never counted as work)
     for _ in range(args.steps):
         res = csm.match_batch(matchers, scans, pairs, ctx)
+        errors += int((res["status"] < 0).sum())
         rec = gather_constraints(res)
         if rank == 0:
             accepted = len(rec)
@@ -135,6 +137,7 @@ def main():
     tm = ctx.timing()
     lv_cands, lv_batches = ctx.level_stats()
     elapsed = cdist.max_over_ranks(elapsed, dist, coll_dev)
+    errors = int(cdist.sum_over_ranks(errors, dist, coll_dev))
     total_pairs = n_pairs * world_size * args.steps
     value = total_pairs / elapsed
 
@@ -172,6 +175,8 @@ def main():
                      "kernel": "fast2d_search", "kernel_ms_avg": kernel_ms_avg,
                      "algorithmic_bytes_per_launch": bytes_per_launch},
         "accepted_constraints_per_step": accepted,
+        "errors_per_step": errors / args.steps,
+        "stack_high_water": int(tm.stack_high_water),
         "search_levels": {"candidates_per_pair": [c / max(n_pairs * args.steps, 1) for c in lv_cands],
                           "mean_lanes_per_batch": [c / b if b else 0 for c, b in zip(lv_cands, lv_batches)]},
         "setup_s": {"world": gen_s, "pyramids_and_upload": build_s},
@@ -196,6 +201,10 @@ def main():
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+    failed = errors + (out.get("fast3d", {}).get("errors_per_step", 0) if rank == 0 else 0)
+    if failed:
+        print(f"bench: {failed} pair searches returned an error status", file=sys.stderr)
+        sys.exit(3)
 
 
 def committed_traffic(args, world_size):
@@ -444,8 +453,10 @@ def fast3d_bench(csm, ctx, args, rank=0, world_size=1, dist=None, coll_dev=None,
     barrier_sync()
     t0 = time.perf_counter()
     reps = max(1, args.steps3d)
+    errors3 = 0
     for _ in range(reps):
         res3, rec = step()
+        errors3 += int((res3["status"] < 0).sum())
     barrier_sync()
     wall = time.perf_counter() - t0
     tm = ctx.timing()
@@ -460,6 +471,7 @@ def fast3d_bench(csm, ctx, args, rank=0, world_size=1, dist=None, coll_dev=None,
            "unit": "pairs/s", "n_gpus": world_size, "scaling": "weak",
            "accepted_per_step": int(len(rec)) if rec is not None else int((res3["status"] == 0).sum()),
            "ms_per_step": wall / reps * 1e3,
+           "errors_per_step": errors3 / reps, "stack_high_water": int(tm.stack_high_water),
            "kernel_ms_per_step": tm.fast3d_kernel_ms / reps, "lookups_per_step": tm.fast3d_lookups / reps,
            "algorithmic_GBps": tm.fast3d_lookups / (tm.fast3d_kernel_ms * 1e-3) / 1e9
            if tm.fast3d_kernel_ms else 0.0, "setup_s": gen}

@@ -85,7 +85,8 @@ struct WorkQueues2 {
   int32_t rot_chunk;
 };
 
-constexpr int kStack2 = 2048;   // v2 per-workgroup DFS stack entries
+constexpr int kStack2 = 2048;   // v4 per-workgroup DFS stack entries in LDS
+constexpr int kSpill2 = 6144;   // further entries per workgroup in global memory
 constexpr int kBatchNodes = 64; // nodes expanded per batch (256 children)
 
 // Best leaf per pair, packed for a 64-bit atomicMax:
@@ -107,6 +108,13 @@ CSM_HD inline void UnpackLeafKey(uint64_t key, uint32_t* sum, int* rot, int* xo,
   *xo = static_cast<int>((idx >> 14) & 0x3fff) - 8192;
   *yo = static_cast<int>(idx & 0x3fff) - 8192;
 }
+
+// Search statistics words (csm_host.cc reads them back): [0] candidates,
+// [1] lookups, [2, 2 + L) candidates per child level, [2 + L, 2 + 2L)
+// batches per level, 4 CSM_KPROF phase counters, the DFS stack high-water
+// mark (max over workgroups, entries).
+constexpr int kStatHighWater = 2 + 2 * kMaxLevels + 4;
+constexpr int kStatsWords = kStatHighWater + 1;
 
 // Per-pair status written by the search kernel (0 = ok).
 constexpr int32_t kStatusRange = 1;

@@ -19,7 +19,9 @@ constexpr int kRootScore3d = 256;         // roots scored at a time (one per lan
 constexpr int kTopCells3d = 512;          // distinct top-level cells of a cloud (LDS list)
 constexpr int kBatch3d = 16;              // DFS nodes scored per step (16 lanes each)
 constexpr int kMax3dTop = 1 << 20;        // top-level candidates per yaw
-constexpr int kStack3d = 1024;            // DFS stack entries per workgroup
+constexpr int kStack3d = 1024;            // DFS stack entries per workgroup in LDS
+constexpr int kSpill3d = 3072;            // further entries per workgroup in global memory
+constexpr int kStat3dHighWater = 14;      // stats word: DFS stack high-water (max over workgroups)
 constexpr int kMax3dYaws = 1 << 16;
 constexpr int kMax3dWindow = 1 << 14;
 constexpr int kSearch3dThreads = 256;

@@ -32,7 +32,6 @@ namespace csm {
 
 namespace {
 
-constexpr int kStatsWords = 2 + 2 * kMaxLevels + 4;  // + CSM_KPROF phase cycles
 
 int AutoSearchDepth(int configured, int nx, int ny) {
   // Extra coarse levels until the top lattice step reaches ~1/2 of the grid:
@@ -240,17 +239,18 @@ int RunBatch(csm_context* ctx, csm_fast2d* const* submaps, int32_t num_submaps,
     wq2.block_first = ctx->blocks.as<int32_t>();
     // rot_chunk * npad cells (4 B) and run counts (1 B), 16-B aligned.
     const size_t dyn_lds = (static_cast<size_t>(rc) * max_npad * 5 + 15) & ~size_t{15};
-    const char* mixed_env = std::getenv("CSM_MIXED_LEVELS");
-    const int mixed = mixed_env ? std::atoi(mixed_env) : 1;
     const int per_cu = std::max(1, std::min(8, static_cast<int>((160 * 1024) / (dyn_lds + 10 * 1024))));
     const int grid = static_cast<int>(std::min<int64_t>(static_cast<int64_t>(ctx->num_cus) * per_cu,
                                                         std::max<int64_t>(total_chunks, 1)));
+    // DFS stack spill: kSpill2 entries per persistent workgroup.
+    if ((rcode = ctx->spill.Reserve(sizeof(uint2) * kSpill2 * static_cast<size_t>(grid))))
+      return rcode;
     CSM_HIP(LaunchFast2dSearchV2(grid, dyn_lds, st, ctx->submap_desc.as<SubmapDesc>(),
                                  ctx->pair_desc.as<PairDesc>(), scans->points.as<float>(),
                                  ctx->rot_table.as<float2>(), wq2,
                                  ctx->counters.as<unsigned long long>(), ctx->best.as<uint64_t>(),
                                  ctx->status.as<int32_t>(), ctx->stats.as<unsigned long long>(),
-                                 max_npad, mixed));
+                                 ctx->spill.as<uint2>(), max_npad));
   } else {
     const size_t dyn_lds = static_cast<size_t>(rc) * max_npad * sizeof(uint32_t);
     const int grid = static_cast<int>(std::min<int64_t>(static_cast<int64_t>(ctx->num_cus) * 4,
@@ -284,6 +284,8 @@ int RunBatch(csm_context* ctx, csm_fast2d* const* submaps, int32_t num_submaps,
       ctx->level_cands[l] += static_cast<double>(stats_host[2 + l]);
       ctx->level_batches[l] += static_cast<double>(stats_host[2 + kMaxLevels + l]);
     }
+    ctx->t.stack_high_water = std::max<int64_t>(ctx->t.stack_high_water,
+                                                static_cast<int64_t>(stats_host[kStatHighWater]));
     const unsigned long long* kp = stats_host + 2 + 2 * kMaxLevels;
     if (std::getenv("CSM_PROFILE2D") && (kp[0] | kp[1] | kp[2]))
       std::fprintf(stderr,
@@ -300,6 +302,7 @@ int RunBatch(csm_context* ctx, csm_fast2d* const* submaps, int32_t num_submaps,
     const csm_fast2d* m = submaps[p.submap];
     if (stat[k] & kStatusRange) {
       results[i].status = CSM_ERANGE;
+      ctx->t.search_errors += 1;
       continue;
     }
     uint32_t sum;
@@ -456,11 +459,6 @@ int csm_fast2d_create(csm_context* ctx, const csm_map_limits* limits,
     d.quad_h[l] = d.wide_ny[l] + h;
     d.quad_pws[l] = (d.quad_w[l] + 2 * h - 1) / (2 * h);
     d.quad_pph[l] = (d.quad_h[l] + 2 * h - 1) / (2 * h);
-#ifdef CSM_QUAD_TILED
-    // Planes stored as 8 x 4 tiles of entries (one 128 B line each).
-    d.quad_pws[l] = (d.quad_pws[l] + 7) & ~7;
-    d.quad_pph[l] = (d.quad_pph[l] + 3) & ~3;
-#endif
     const size_t qb = static_cast<size_t>(2 * h) * (2 * h) * d.quad_pws[l] * d.quad_pph[l] * 4;
     if (qb > 0x7fffff00u) return CSM_ERANGE;
     d.quad_bytes[l] = static_cast<int32_t>(qb);

@@ -72,7 +72,7 @@ struct csm_context {
   hipStream_t stream = nullptr;
   std::mutex mu;
   csm::DevBuf submap_desc, pair_desc, rot_table, best, status, counters, pair_order,
-      chunk_prefix, blocks, stats, rt_prob, rt_cells, rt_points, rt_best, rt_rot, rt_ptab,
+      chunk_prefix, blocks, stats, spill, rt_prob, rt_cells, rt_points, rt_best, rt_rot, rt_ptab,
       single_points, rt_wcells, rt_tsdw, rt_ttab;
   // TSDValueConverter tables for the last (truncation, max_weight) uploaded.
   float ttab_key[2] = {0.f, 0.f};
@@ -87,7 +87,7 @@ struct csm_context {
   int num_cus = 256;
   // 3D path scratch (host3d.cc).
   csm::DevBuf rt3_rot, rt3_trans, rt3_points, rt3_best, f3_pairs, f3_yaws, f3_points,
-      f3_low_points, f3_best, f3_status, f3_counter, f3_items, f3_scores;
+      f3_low_points, f3_best, f3_status, f3_counter, f3_items, f3_scores, f3_spill;
   csm::PinnedBuf f3_host_yaws;
   // Voxel filter scratch (voxel_filter.hip).
   csm::DevBuf vf_points, vf_offsets, vf_keep, vf_counts;

@@ -555,15 +555,7 @@ __global__ void pyramid_quad(const uint8_t* __restrict__ level, int wnx, int wny
   const int ps = pws * pph;
   const int pi = o / ps, k = o - pi * ps;
   const int fx = pi & (p - 1), fy = pi >> s;
-#ifdef CSM_QUAD_TILED
-  // 8 x 4 tiles of entries, row-major tiles (pws % 8 == 0, pph % 4 == 0).
-  const int tile = k >> 5, inner = k & 31;
-  const int tiles_x = pws >> 3;
-  const int ty = tile / tiles_x, tx = tile - ty * tiles_x;
-  const int ky = (ty << 2) + (inner >> 3), kx = (tx << 3) + (inner & 7);
-#else
   const int ky = k / pws, kx = k - ky * pws;
-#endif
   const int xq = (kx << s) + fx, yq = (ky << s) + fy;
   uint32_t v = 0;
   if (xq < qw && yq < qh) {
@@ -604,10 +596,20 @@ struct V4Shared {
   int vny[kMaxRotChunk];
   int root_prefix[kMaxRotChunk + 1];
   int vnext;
-  int range_error, batch_no;
+  int range_error, batch_no, high_water;
   unsigned long long lv_cands[kMaxLevels];
   unsigned long long lv_batches[kMaxLevels];
 };
+
+// The DFS stack: entries [0, kStack2) in LDS, [kStack2, kStack2 + kSpill2)
+// in the workgroup's spill region (global memory; the workgroup's own waves
+// write and read it, ordered by the __syncthreads between phases).
+__device__ __forceinline__ uint2 StackGet(const V4Shared& sh, const uint2* spill, int i) {
+  return i < kStack2 ? sh.stack[i] : spill[i - kStack2];
+}
+__device__ __forceinline__ void StackPut(V4Shared& sh, uint2* spill, int i, uint2 v) {
+  if (i < kStack2) sh.stack[i] = v; else spill[i - kStack2] = v;
+}
 
 // Scores the children of the batch's nodes over the chunk's run lists: entry
 // k of rotation r is a cell (pts) and the number of consecutive scan points
@@ -644,14 +646,8 @@ __device__ __forceinline__ void V4Score(V4Shared& sh, const uint32_t* pts, const
     const bool valid = in && static_cast<unsigned>(X) < static_cast<unsigned>(qw) &&
                        static_cast<unsigned>(Y) < static_cast<unsigned>(qh);
     const int a = __umul24((((Y & pmask) << sft) | (X & pmask)), ps4) + qoff;
-#ifdef CSM_QUAD_TILED
-    const int ey = Y >> sft, ex = X >> sft;
-    const int b = __umul24(ey >> 2, pws4 << 2) + a + ((ey & 3) << 5);
-    return valid ? ((ex >> 3) << 7) + ((ex & 7) << 2) + b : kOOB;
-#else
     const int b = __umul24(Y >> sft, pws4) + a;
     return valid ? ((X >> sft) << 2) + b : kOOB;
-#endif
   };
   // v_dot4_u32_u8 with the run count in one byte of the weight multiplies
   // that child's byte by the count and accumulates.
@@ -767,13 +763,15 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
                  uint64_t* __restrict__ best,
                  int32_t* __restrict__ status,
                  unsigned long long* __restrict__ stats,
-                 int npad, int mixed_levels) {
+                 uint2* __restrict__ spill_base, int npad) {
   extern __shared__ __align__(16) uint32_t pts[];  // rot_chunk * npad cells, then counts
   __shared__ V4Shared sh;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int rc = queues.rot_chunk;
   uint8_t* cnt = reinterpret_cast<uint8_t*>(pts + rc * npad);
+  uint2* spill = spill_base + static_cast<size_t>(blockIdx.x) * kSpill2;
   for (int k = tid; k < kBatchNodes * 4; k += kSearchThreads) sh.part[k >> 2][k & 3] = 0;
+  if (tid == 0) sh.high_water = 0;
   unsigned long long local_cands = 0, local_lookups = 0;
 #ifdef CSM_KPROF
   long long kprof[4] = {0, 0, 0, 0};  // thread 0: discretize, control, score cycles; batches
@@ -960,21 +958,27 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
             rank += static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(skey), jl)) > skey;
           }
           int sp = 0;
-          if (lane == 0 && kept > 0) sp = atomicAdd(&sh.sp, kept);
+          if (lane == 0 && kept > 0) {
+            sp = atomicAdd(&sh.sp, kept);
+            atomicMax(&sh.high_water, sp + kept);
+          }
           sp = __shfl(sp, 0, 64);
-          if (push && sp + kept <= kStack2)
-            sh.stack[sp + kept - 1 - rank] = make_uint2(
+          // Entries past the LDS stack go to this workgroup's spill region in
+          // global memory (StackPut); past that the pair is flagged (the
+          // bound is ~2.8k entries: <= 256 pushed per level).
+          if (push && sp + kept <= kStack2 + kSpill2)
+            StackPut(sh, spill, sp + kept - 1 - rank, make_uint2(
                 (static_cast<uint32_t>(xo) & 0xffff) | (static_cast<uint32_t>(yo) << 16),
                 static_cast<uint32_t>(sum) | (static_cast<uint32_t>(r) << 22) |
-                    (static_cast<uint32_t>(clvl) << 27));
-          if (lane == 0 && sp + kept > kStack2) atomicOr(&status[pair_index], kStatusRange);
+                    (static_cast<uint32_t>(clvl) << 27)));
+          if (lane == 0 && sp + kept > kStack2 + kSpill2) atomicOr(&status[pair_index], kStatusRange);
         }
       }
       __syncthreads();
       if (wave == 0) {
         // (b) Refill roots when the stack is empty. (An overflowed stack has
         // flagged the pair; its result is discarded.)
-        int sp = min(sh.sp, kStack2);
+        int sp = min(sh.sp, kStack2 + kSpill2);
         if (sp == 0 && sh.vnext < vtotal) {
           const int v0 = sh.vnext, vc = min(kRootChunk, vtotal - v0);
           for (int k = lane; k < vc; k += 64) {
@@ -998,91 +1002,12 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
         }
         const uint32_t cur_sum = static_cast<uint32_t>(sh.best >> kSumShift);
         int nodes = 0;
-        if (sp > 0 && mixed_levels == 2) {
-          // Homogeneous batches: the nodes of one (rotation, level) group,
-          // that of the top entry, picked from the top 128 entries, best
-          // first. One group shares the child level's planes for a given
-          // point, so a gather over the batch touches few cache lines.
-          // Pruned entries in the window are dropped; the others keep their
-          // order and the window is compacted in place.
-          const int W = min(sp, 2 * 64);
-          const bool in0 = lane < W, in1 = lane + 64 < W;
-          const uint2 e0 = in0 ? sh.stack[sp - 1 - lane] : make_uint2(0, 0);
-          const uint2 e1 = in1 ? sh.stack[sp - 1 - 64 - lane] : make_uint2(0, 0);
-          const uint32_t group = sh.stack[sp - 1].y >> 22;  // level << 5 | rotation
-          const bool live0 = in0 && (e0.y & 0x3fffff) >= cur_sum;
-          const bool live1 = in1 && (e1.y & 0x3fffff) >= cur_sum;
-          const bool m0 = live0 && (e0.y >> 22) == group, m1 = live1 && (e1.y >> 22) == group;
-          const unsigned long long b0 = __ballot(m0), b1 = __ballot(m1);
-          const int ne = __popcll(b0) + __popcll(b1);
-          const unsigned long long below = (1ull << lane) - 1;
-          bool s0 = false, s1 = false;
-          int r0 = 0, r1 = 0;
-          if (ne > 0) {
-            // The 128-entry window can hold more than kBatchNodes matches.
-            nodes = 1 << (31 - __clz(min(ne, kBatchNodes)));
-            r0 = __popcll(b0 & below);
-            r1 = __popcll(b0) + __popcll(b1 & below);
-            s0 = m0 && r0 < nodes;
-            s1 = m1 && r1 < nodes;
-#ifdef CSM_SORT_BATCH
-            // Slot order by (yo, xo): lanes next to each other then look up
-            // neighbouring dwords of one plane row.
-            auto key = [](uint32_t x) {
-              return (((x >> 16) ^ 0x8000u) << 16) | ((x & 0xffffu) ^ 0x8000u);
-            };
-            const uint32_t k0 = key(e0.x), k1 = key(e1.x);
-            const unsigned long long q0 = __ballot(s0), q1 = __ballot(s1);
-            int n0 = 0, n1 = 0;
-            for (unsigned long long m = q0; m; m &= m - 1) {
-              const int j = static_cast<int>(__ffsll(static_cast<long long>(m))) - 1;
-              const uint32_t kj = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(k0), j));
-              n0 += kj < k0;
-              n1 += kj < k1;
-            }
-            for (unsigned long long m = q1; m; m &= m - 1) {
-              const int j = static_cast<int>(__ffsll(static_cast<long long>(m))) - 1;
-              const uint32_t kj = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(k1), j));
-              n0 += kj < k0;
-              n1 += kj < k1;
-            }
-            if (s0) r0 = n0;
-            if (s1) r1 = n1;
-#endif
-            if (s0) {
-              sh.node_xo[r0] = static_cast<int16_t>(e0.x & 0xffff);
-              sh.node_yo[r0] = static_cast<int>(e0.x) >> 16;
-              sh.node_rot[r0] = (e0.y >> 22) & 0x1f;
-              sh.node_level[r0] = static_cast<int>(e0.y >> 27);
-            }
-            if (s1) {
-              sh.node_xo[r1] = static_cast<int16_t>(e1.x & 0xffff);
-              sh.node_yo[r1] = static_cast<int>(e1.x) >> 16;
-              sh.node_rot[r1] = (e1.y >> 22) & 0x1f;
-              sh.node_level[r1] = static_cast<int>(e1.y >> 27);
-            }
-          }
-          const bool k0 = live0 && !s0, k1 = live1 && !s1;
-          const unsigned long long c0 = __ballot(k0), c1 = __ballot(k1);
-          const int kept = __popcll(c0) + __popcll(c1);
-          const int base = sp - W + kept;  // new stack pointer
-          if (k0) sh.stack[base - 1 - __popcll(c0 & below)] = e0;
-          if (k1) sh.stack[base - 1 - __popcll(c0) - __popcll(c1 & below)] = e1;
-          sp = base;
-        } else if (sp > 0) {
-          // Up to 16 entries from the top (any level); expand a power of two
+        if (sp > 0) {
+          // Up to 64 entries from the top (any level); expand a power of two
           // of the unpruned ones, discard pruned ones passed over.
           uint2 ent = make_uint2(0, 0);
-          bool in = lane < kBatchNodes && lane < sp;
-          if (in) ent = sh.stack[sp - 1 - lane];
-          if (!mixed_levels) {
-            // Same-level batches: stop at the first entry of another level.
-            const int top_lvl = static_cast<int>(sh.stack[sp - 1].y >> 27);
-            const unsigned long long diff = __ballot(!(in && static_cast<int>(ent.y >> 27) == top_lvl));
-            // diff == 0: every one of the 64 lanes holds a top-level entry.
-            const int run = diff ? static_cast<int>(__ffsll(static_cast<long long>(diff))) - 1 : 64;
-            in = lane < run;
-          }
+          const bool in = lane < kBatchNodes && lane < sp;
+          if (in) ent = StackGet(sh, spill, sp - 1 - lane);
           const unsigned long long inm = __ballot(in);
           const bool expandable = in && (ent.y & 0x3fffff) >= cur_sum;
           const unsigned long long em = __ballot(expandable);
@@ -1152,6 +1077,7 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
     atomicAdd(&stats[2 + tid], sh.lv_cands[tid]);
     atomicAdd(&stats[2 + kMaxLevels + tid], sh.lv_batches[tid]);
   }
+  if (stats && tid == 0) atomicMax(&stats[kStatHighWater], static_cast<unsigned long long>(sh.high_water));
 }
 
 // ---------------------------------------------------------------- K5 -------
@@ -1284,9 +1210,9 @@ hipError_t LaunchFast2dSearchV2(int grid, size_t dyn_lds, hipStream_t st, const 
                                 const PairDesc* pairs, const float* points, const float2* rot_table,
                                 const WorkQueues2& queues, unsigned long long* counters,
                                 uint64_t* best, int32_t* status, unsigned long long* stats,
-                                int npad, int mixed_levels) {
+                                uint2* spill, int npad) {
   hipLaunchKernelGGL(fast2d_search_v4, dim3(grid), dim3(kSearchThreads), dyn_lds, st, submaps, pairs,
-                     points, rot_table, queues, counters, best, status, stats, npad, mixed_levels);
+                     points, rot_table, queues, counters, best, status, stats, spill, npad);
   return hipGetLastError();
 }
 

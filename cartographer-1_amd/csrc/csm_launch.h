@@ -22,7 +22,7 @@ hipError_t LaunchFast2dSearchV2(int grid, size_t dyn_lds, hipStream_t st, const 
                                 const PairDesc* pairs, const float* points, const float2* rot_table,
                                 const WorkQueues2& queues, unsigned long long* counters,
                                 uint64_t* best, int32_t* status, unsigned long long* stats,
-                                int npad, int mixed_levels);
+                                uint2* spill, int npad);
 hipError_t LaunchRt2dScore(dim3 grid, int block, size_t dyn_lds, hipStream_t st, const float* prob,
                            const float2* tsdw, float max_cc, int nx, int ny, double max_x,
                            double max_y, double res, const float* points, int n,

@@ -35,7 +35,7 @@ hipError_t LaunchFast3dSearch(bool large, int grid, hipStream_t st, const Submap
                               const Pair3Desc* pairs, const Yaw3Desc* yaws, int item_begin,
                               int num_items, const float* points, const float* low_points,
                               unsigned* counter, unsigned long long* best, int32_t* status,
-                              unsigned long long* stats);
+                              unsigned long long* stats, int4* spill);
 hipError_t LaunchFast3dFinalize(int num_pairs, hipStream_t st, const Submap3Desc* submaps,
                                 const Pair3Desc* pairs, const Yaw3Desc* yaws,
                                 const float* low_points, const unsigned long long* best,

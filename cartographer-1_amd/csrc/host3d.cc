@@ -919,20 +919,25 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
   CSM_HIP(hipMemsetAsync(ctx->f3_status.ptr, 0, sizeof(int32_t) * np, st));
   CSM_HIP(hipMemsetAsync(ctx->f3_counter.ptr, 0, 8 + 16 * sizeof(unsigned long long), st));
   lap(4);
+  {
+    const size_t wgs = static_cast<size_t>(ctx->num_cus) *
+                       std::max(kSearch3dBlocksPerCu, kSearch3dBlocksPerCuLarge);
+    if ((rc = ctx->f3_spill.Reserve(sizeof(int4) * kSpill3d * wgs))) return rc;
+  }
   if (ctx->timing) CSM_HIP(hipEventRecord(ctx->ev0, st));
   if (ny_small > 0) {
     const int grid = std::max(1, std::min(ny_small, ctx->num_cus * kSearch3dBlocksPerCu));
     CSM_HIP(LaunchFast3dSearch(false, grid, st, dsub, dpairs, ctx->f3_yaws.as<Yaw3Desc>(), 0,
                                ny_small, ctx->f3_points.as<float>(),
                                ctx->f3_low_points.as<float>(), dcounter, dbest,
-                               ctx->f3_status.as<int32_t>(), dstats));
+                               ctx->f3_status.as<int32_t>(), dstats, ctx->f3_spill.as<int4>()));
   }
   if (ny > ny_small) {
     const int grid = std::max(1, std::min(ny - ny_small, ctx->num_cus * kSearch3dBlocksPerCuLarge));
     CSM_HIP(LaunchFast3dSearch(true, grid, st, dsub, dpairs, ctx->f3_yaws.as<Yaw3Desc>(), ny_small,
                                ny - ny_small, ctx->f3_points.as<float>(),
                                ctx->f3_low_points.as<float>(), dcounter + 1, dbest,
-                               ctx->f3_status.as<int32_t>(), dstats));
+                               ctx->f3_status.as<int32_t>(), dstats, ctx->f3_spill.as<int4>()));
   }
   if (ctx->timing) CSM_HIP(hipEventRecord(ctx->ev1, st));
   CSM_HIP(LaunchFast3dFinalize(np, st, dsub, dpairs, ctx->f3_yaws.as<Yaw3Desc>(),
@@ -955,6 +960,9 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
     ctx->t.fast3d_launches += 1;
     lookups = prof[0];
     ctx->t.fast3d_lookups += static_cast<double>(lookups);
+    ctx->t.stack_high_water =
+        std::max<int64_t>(ctx->t.stack_high_water, static_cast<int64_t>(prof[kStat3dHighWater]));
+    for (int dp = 0; dp < np; ++dp) ctx->t.search_errors += stat[dp] < 0 ? 1 : 0;
     if (std::getenv("CSM_PROFILE3D"))
       std::fprintf(stderr,
                    "fast3d phases (Mcycles, thread 0 sums): item+discretize %.1f top-copy %.1f "

@@ -366,7 +366,7 @@ struct F3SharedT {
   int tcell[kTopCells3d];
   uint16_t tcount[kTopCells3d];
   int ntcell;
-  int nbatch, nleaf, sp, item, error, accepted, cached_submap;
+  int nbatch, nleaf, sp, item, error, accepted, cached_submap, high_water;
   unsigned long long best;
   unsigned long long best_seen;  // last read of the pair's global best
 };
@@ -454,12 +454,18 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
               const float* __restrict__ points,
               const float* __restrict__ low_points, unsigned* __restrict__ counter,
               unsigned long long* __restrict__ best, int32_t* __restrict__ status,
-              unsigned long long* __restrict__ stats) {
+              unsigned long long* __restrict__ stats, int4* __restrict__ spill_base) {
   __shared__ F3SharedT<kPts> sh;
   const int tid = threadIdx.x;
   unsigned long long lookups = 0, root_lookups = 0;
   F3_PROF_DECL;
-  if (tid == 0) sh.cached_submap = -1;
+  // DFS stack entries past kStack3d live in this workgroup's spill region
+  // (global memory, written and read only by this workgroup's waves).
+  int4* spill = spill_base + static_cast<size_t>(blockIdx.x) * kSpill3d;
+  if (tid == 0) {
+    sh.cached_submap = -1;
+    sh.high_water = 0;
+  }
   for (;;) {
     if (tid == 0) sh.item = static_cast<int>(atomicAdd(counter, 1u));
     __syncthreads();
@@ -786,17 +792,20 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
           const int at = sp - 1 - tid;
           int s = 0;
           bool keep = false;
+          int4 e = make_int4(0, 0, 0, 0);
           if (at >= 0) {
-            s = sh.ssum[at];
+            e = at < kStack3d ? make_int4(sh.sx[at], sh.sy[at], (sh.sz[at] & 0xffff) | (sh.sd[at] << 16), sh.ssum[at])
+                              : spill[at - kStack3d];
+            s = e.w;
             keep = s >= best_sum && s >= pd.min_sum;
           }
           const unsigned long long mask = __ballot(keep);
           const int rank = m + __popcll(mask & ((1ull << tid) - 1ull));
           if (keep && rank < kBatch3d) {
-            sh.bn_x[rank] = sh.sx[at];
-            sh.bn_y[rank] = sh.sy[at];
-            sh.bn_z[rank] = sh.sz[at];
-            sh.bn_d[rank] = sh.sd[at];
+            sh.bn_x[rank] = e.x;
+            sh.bn_y[rank] = e.y;
+            sh.bn_z[rank] = static_cast<int16_t>(e.z & 0xffff);
+            sh.bn_d[rank] = e.z >> 16;
           }
           const unsigned long long last = __ballot(keep && rank == kBatch3d - 1);
           const int consumed = last ? __ffsll(static_cast<long long>(last)) : min(64, sp);
@@ -990,14 +999,23 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
             rank += kj && (acc[j] < my || (acc[j] == my && j < k));
           }
           int base = 0;
-          if (k == 0 && m > 0) base = atomicAdd(&sh.sp, m);
+          if (k == 0 && m > 0) {
+            base = atomicAdd(&sh.sp, m);
+            atomicMax(&sh.high_water, base + m);
+            if (base + m > kStack3d + kSpill3d) sh.error = 1;  // flagged after the batch
+          }
           base = __shfl(base, (tid & 63) & ~(kLanes - 1), 64);
-          if (pres && my >= pd.min_sum && my >= best_sum) {
-            sh.sx[base + rank] = static_cast<int16_t>(cxk);
-            sh.sy[base + rank] = static_cast<int16_t>(cyk);
-            sh.sz[base + rank] = static_cast<int16_t>(czk);
-            sh.sd[base + rank] = static_cast<int8_t>(cd);
-            sh.ssum[base + rank] = my;
+          const int at = base + rank;
+          if (pres && my >= pd.min_sum && my >= best_sum && at < kStack3d + kSpill3d) {
+            if (at < kStack3d) {
+              sh.sx[at] = static_cast<int16_t>(cxk);
+              sh.sy[at] = static_cast<int16_t>(cyk);
+              sh.sz[at] = static_cast<int16_t>(czk);
+              sh.sd[at] = static_cast<int8_t>(cd);
+              sh.ssum[at] = my;
+            } else {
+              spill[at - kStack3d] = make_int4(cxk, cyk, (czk & 0xffff) | (cd << 16), my);
+            }
           }
         } else if (pres && my >= pd.min_sum) {
           const unsigned long long id = LeafId(pd, yw.yaw_id, cxk, cyk, czk);
@@ -1015,6 +1033,10 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
       if (tid == 0) sh.best_seen = gbest;
       F3_COUNT(5, 1);
       __syncthreads();
+      if (sh.error) {  // stack beyond LDS + spill: the pair's result is void
+        if (tid == 0) atomicExch(reinterpret_cast<int*>(status + yw.pair), -4);
+        break;
+      }
       const int nl = sh.nleaf;
       if (nl == 0) continue;
       // Leaves: descending key order; the first that passes the
@@ -1069,6 +1091,7 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
   lookups += root_lookups;
   for (int m = 32; m > 0; m >>= 1) lookups += __shfl_xor(lookups, m, 64);
   if ((tid & 63) == 0 && stats && lookups) atomicAdd(stats, lookups);
+  if (tid == 0 && stats) atomicMax(stats + kStat3dHighWater, static_cast<unsigned long long>(sh.high_water));
   F3_FLUSH(stats);
 }
 
@@ -1304,15 +1327,15 @@ hipError_t LaunchFast3dSearch(bool large, int grid, hipStream_t st, const Submap
                               const Pair3Desc* pairs, const Yaw3Desc* yaws, int item_begin,
                               int num_items, const float* points, const float* low_points,
                               unsigned* counter, unsigned long long* best, int32_t* status,
-                              unsigned long long* stats) {
+                              unsigned long long* stats, int4* spill) {
   if (large)
     hipLaunchKernelGGL((fast3d_search<kMax3dPoints, kSearch3dBlocksPerCuLarge>), dim3(grid),
                        dim3(kSearch3dThreads), 0, st, submaps, pairs, yaws, item_begin, num_items,
-                       points, low_points, counter, best, status, stats);
+                       points, low_points, counter, best, status, stats, spill);
   else
     hipLaunchKernelGGL((fast3d_search<kSmall3dPoints, kSearch3dBlocksPerCu>), dim3(grid),
                        dim3(kSearch3dThreads), 0, st, submaps, pairs, yaws, item_begin, num_items,
-                       points, low_points, counter, best, status, stats);
+                       points, low_points, counter, best, status, stats, spill);
   return hipGetLastError();
 }
 

@@ -112,3 +112,14 @@ def max_over_ranks(value: float, dist=None, device=None) -> float:
                      device=torch.device("cpu") if device is None else device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def sum_over_ranks(value: float, dist=None, device=None) -> float:
+    """Sum of a per-rank count (e.g. pairs that returned an error)."""
+    if dist is None:
+        return value
+    import torch
+    t = torch.tensor([value], dtype=torch.float64,
+                     device=torch.device("cpu") if device is None else device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())

@@ -96,6 +96,11 @@ typedef struct csm_timing {
   double fast3d_kernel_ms;
   int64_t fast3d_launches;
   double fast3d_lookups;
+  /* Search health, accumulated while timing is enabled: pairs whose batch
+   * search returned an error status (< 0), and the largest DFS stack depth
+   * (entries) any workgroup reached (2D and 3D). */
+  int64_t search_errors;
+  int64_t stack_high_water;
 } csm_timing;
 void csm_context_enable_timing(csm_context* ctx, int32_t enable);
 void csm_context_get_timing(csm_context* ctx, csm_timing* out);

@@ -52,3 +52,13 @@ def oracle():
     ensure_built()
     import oracle_lib
     return oracle_lib.Oracle()
+
+
+def assert_search_ok(csm, status):
+    """Every pair of a batch search was searched to the end: matched or no
+    match. A negative status (an error, e.g. CSM_ERANGE) is never read as
+    "no match" by a parity test."""
+    import numpy as np
+    st = np.asarray(status)
+    bad = np.nonzero((st != csm.CSM_OK) & (st != csm.CSM_NO_MATCH))[0]
+    assert len(bad) == 0, f"pairs {bad[:10].tolist()} returned error statuses {st[bad[:10]].tolist()}"

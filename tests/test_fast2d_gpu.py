@@ -13,6 +13,7 @@ import math
 
 import numpy as np
 import pytest
+from conftest import assert_search_ok
 
 pytestmark = pytest.mark.gpu
 
@@ -164,6 +165,7 @@ def test_synthetic_full_submap_pairs(csm, oracle, world, depth_mode, search_kern
     pairs_sn = [(s, int(world.submap_nodes[s])) for s in range(8)] + [(1, 3), (2, 40), (5, 17), (7, 0)]
     pairs = csm.make_pairs([p[0] for p in pairs_sn], [p[1] for p in pairs_sn], 0.55)
     res = csm.match_batch(mats, scans, pairs)
+    assert_search_ok(csm, res["status"])
     matched = 0
     for k, (s, n) in enumerate(pairs_sn):
         g = world.grid(s)
@@ -187,6 +189,7 @@ def test_batch_equals_single_calls(csm, world):
     nodes = [int(world.submap_nodes[0]), int(world.submap_nodes[1]), 5, 9,
              int(world.submap_nodes[0]) + 1, 30]
     res = csm.match_batch(mats, scans, csm.make_pairs(sub, nodes, 0.5))
+    assert_search_ok(csm, res["status"])
     for k, (s, n) in enumerate(zip(sub, nodes)):
         ok, score, pose = mats[s].MatchFullSubmap(world.cloud(n), 0.5)
         assert ok == (res[k]["status"] == 0)
@@ -275,6 +278,7 @@ def test_run_lists_parity(csm, oracle, world):
     pairs = csm.make_pairs(np.zeros(len(clouds), np.int32), np.arange(len(clouds), dtype=np.int32),
                            0.3, full_submap=True)
     res = csm.match_batch([m], scans, pairs)
+    assert_search_ok(csm, res["status"])
     kinds = []
     for k, c in enumerate(clouds):
         gpu = (int(res[k]["status"]) == csm.CSM_OK, float(res[k]["score"]),
@@ -297,6 +301,7 @@ def test_batch_selection_modes_parity(csm, oracle, world, mode, monkeypatch):
     pairs_sn = [(s, int(world.submap_nodes[s])) for s in range(8)] + [(1, 3), (2, 40), (5, 17)]
     pairs = csm.make_pairs([p[0] for p in pairs_sn], [p[1] for p in pairs_sn], 0.55)
     res = csm.match_batch(mats, scans, pairs)
+    assert_search_ok(csm, res["status"])
     matched = 0
     for k, (s, n) in enumerate(pairs_sn):
         g = world.grid(s)

@@ -15,6 +15,7 @@ import math
 
 import numpy as np
 import pytest
+from conftest import assert_search_ok
 
 pytestmark = pytest.mark.gpu
 
@@ -187,6 +188,7 @@ def test_batch_equals_single_calls(csm, oracle):
         for n in range(2):
             pairs.append((s, n, n == 1, 0.1, ident, ident))
     results = csm.match_batch_3d(mats, nodes, pairs)
+    assert_search_ok(csm, [r.status for r in results])
     for (s, n, full, ms, npose, spose), r in zip(pairs, results):
         single = (mats[s].MatchFullSubmap((1, 0, 0, 0), (1, 0, 0, 0), nodes[n], ms) if full
                   else mats[s].Match(npose, spose, nodes[n], ms))

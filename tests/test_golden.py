@@ -11,6 +11,7 @@ import os
 
 import numpy as np
 import pytest
+from conftest import assert_search_ok
 
 from conftest import ROOT
 
@@ -88,6 +89,7 @@ def test_gpu_matches_fast2d_golden(csm, oracle, name):
     pairs["min_score"] = p[:, 6]
     pairs["x"], pairs["y"], pairs["theta"] = p[:, 3], p[:, 4], p[:, 5]
     res = csm.match_batch(mats, scans, pairs)
+    assert_search_ok(csm, res["status"])
     oms = {}
     for i in range(len(p)):
         s, c, full = int(p[i, 0]), int(p[i, 1]), bool(p[i, 2])
@@ -243,6 +245,7 @@ def test_gpu_matches_fast3d_golden(csm, oracle):
     rows = [_pair3(r) for r in d["pairs"]]
     res = csm.match_batch_3d(mats, nodes, [(s, n, full, ms, npose, spose)
                                            for s, n, full, ms, npose, spose in rows])
+    assert_search_ok(csm, [r.status for r in res])
     oms = None
     for i, (s, n, full, ms, npose, spose) in enumerate(rows):
         single = (mats[s].MatchFullSubmap(npose[1], spose[1], nodes[n], ms) if full
