@@ -303,6 +303,11 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     return lib
 
 
+def strerror(code: int) -> str:
+    """csm_strerror: the text of a C-ABI status code."""
+    return load_library().csm_strerror(code).decode()
+
+
 def _check(code: int, what: str) -> int:
     if code < 0:
         msg = load_library().csm_strerror(code).decode()

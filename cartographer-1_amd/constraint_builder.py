@@ -28,12 +28,13 @@ Ceres unpinned) unless ``refine_with_ceres`` is off.
 from __future__ import annotations
 
 import math
+import sys
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional, Tuple
 
 import numpy as np
 
-from . import (CSM_OK, CeresOptions2D, CeresOptions3D, Context, FastCorrelativeScanMatcher2D,
+from . import (CSM_OK, strerror, CeresOptions2D, CeresOptions3D, Context, FastCorrelativeScanMatcher2D,
                FastCorrelativeScanMatcher3D, ceres_refine_batch, ceres_refine_batch_3d,
                FastCorrelativeScanMatcherOptions2D, FastCorrelativeScanMatcherOptions3D,
                HybridGrid, NodeData3D, ProbabilityGrid, ScanSet, _f32_points, default_context,
@@ -139,6 +140,8 @@ class ConstraintBuilder2D:
         self.constraints_found = 0
         self.global_constraints_searched = 0
         self.global_constraints_found = 0
+        self.constraints_failed = 0  # pairs skipped on a device error status
+        self.last_error = CSM_OK
         self.constraint_scores: List[float] = []
         self.global_constraint_scores: List[float] = []
 
@@ -228,7 +231,15 @@ class ConstraintBuilder2D:
                     refined = {i: tuple(float(v) for v in poses[k]) for k, i in enumerate(ok)}
             finally:
                 scans.close()
+            failed = 0
             for i, (p, r) in enumerate(zip(pending, results)):
+                if int(r["status"]) < 0:
+                    # Not searchable on the device (CSM_ERANGE):
+                    # no constraint, counted, never fatal (as the C++ header).
+                    self.constraints_failed += 1
+                    self.last_error = int(r["status"])
+                    failed += 1
+                    continue
                 if p.full:
                     self.global_constraints_searched += 1
                 else:
@@ -249,6 +260,9 @@ class ConstraintBuilder2D:
                     translation_weight=self.options.loop_closure_translation_weight,
                     rotation_weight=self.options.loop_closure_rotation_weight,
                     score=score)
+            if failed:
+                print(f"ConstraintBuilder2D: {failed} of {len(pending)} pairs skipped "
+                      f"({strerror(self.last_error)})", file=sys.stderr)
         self._finished_nodes = self._started_nodes
 
 
@@ -323,6 +337,8 @@ class ConstraintBuilder3D:
         self.constraints_found = 0
         self.global_constraints_searched = 0
         self.global_constraints_found = 0
+        self.constraints_failed = 0  # pairs skipped on a device error status
+        self.last_error = CSM_OK
         self.constraint_scores: List[float] = []
         self.global_constraint_scores: List[float] = []
         self.rotational_scores: List[float] = []
@@ -428,7 +444,15 @@ class ConstraintBuilder3D:
                                                  self.options.ceres_scan_matcher_options_3d,
                                                  self.context)
                 refined = dict(zip(ok, poses))
+            failed = 0
             for i, (p, r) in enumerate(zip(pending, results)):
+                if int(r["status"]) < 0:
+                    # Not searchable on the device (CSM_ERANGE):
+                    # no constraint, counted, never fatal (as the C++ header).
+                    self.constraints_failed += 1
+                    self.last_error = int(r["status"])
+                    failed += 1
+                    continue
                 if p.full:
                     self.global_constraints_searched += 1
                 else:
@@ -453,4 +477,7 @@ class ConstraintBuilder3D:
                     rotation_weight=self.options.loop_closure_rotation_weight,
                     score=score, rotational_score=float(r["rotational_score"]),
                     low_resolution_score=float(r["low_resolution_score"]))
+            if failed:
+                print(f"ConstraintBuilder3D: {failed} of {len(pending)} pairs skipped "
+                      f"({strerror(self.last_error)})", file=sys.stderr)
         self._finished_nodes = self._started_nodes

@@ -32,7 +32,10 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <memory>
+#include <new>
 #include <string>
 #include <vector>
 
@@ -206,7 +209,21 @@ bool Rigid(Reader r, double* pose7) {
   return ok;
 }
 
+// Largest decompressed message accepted (a 400x400 Submap2D is ~0.5 MB, a
+// 3D submap's two HybridGrids tens of MB). A stream whose message inflates
+// past this is rejected rather than exhausting host memory.
+// CSM_PBSTREAM_MAX_MESSAGE_BYTES lowers (or raises) the limit.
+size_t MaxMessageBytes() {
+  size_t limit = size_t{256} << 20;
+  if (const char* e = std::getenv("CSM_PBSTREAM_MAX_MESSAGE_BYTES")) {
+    const long long v = std::atoll(e);
+    if (v > 0) limit = static_cast<size_t>(v);
+  }
+  return limit;
+}
+
 bool Gunzip(const std::vector<uint8_t>& in, std::string* out) {
+  const size_t limit = MaxMessageBytes();
   z_stream zs;
   std::memset(&zs, 0, sizeof(zs));
   if (inflateInit2(&zs, 16 + MAX_WBITS) != Z_OK) return false;
@@ -223,7 +240,12 @@ bool Gunzip(const std::vector<uint8_t>& in, std::string* out) {
       inflateEnd(&zs);
       return false;
     }
-    out->append(buf, sizeof(buf) - zs.avail_out);
+    const size_t got = sizeof(buf) - zs.avail_out;
+    if (out->size() + got > limit) {
+      inflateEnd(&zs);
+      return false;
+    }
+    out->append(buf, got);
   } while (rc != Z_STREAM_END);
   inflateEnd(&zs);
   return true;
@@ -397,7 +419,9 @@ int ParseSubmap(Reader r, Submap2DRec* s, Submap3DRec* s3) {
 // CompressedPointCloud::ConstIterator::ReadNextPoint
 // (compressed_point_cloud.cc:79-97).
 int Decompress(const std::vector<int32_t>& data, int32_t num_points, std::vector<float>* xyz) {
-  if (num_points < 0) return CSM_EINVAL;
+  // Every point takes one int32 of `data` (plus block headers), so a count
+  // beyond data.size() is corrupt: rejected before allocating.
+  if (num_points < 0 || static_cast<size_t>(num_points) > data.size()) return CSM_EINVAL;
   xyz->resize(static_cast<size_t>(num_points) * 3);
   size_t in = 0;
   int32_t left_in_block = 0, block[3] = {0, 0, 0};
@@ -482,15 +506,31 @@ struct csm_pbstream {
 
 extern "C" {
 
+static int PbstreamOpen(const char* path, csm_pbstream** out);
+
+// No exception crosses the C-ABI: an allocation failure while reading is
+// CSM_ENOMEM, anything else thrown is a malformed stream.
 int csm_pbstream_open(const char* path, csm_pbstream** out) {
   if (!path || !out) return CSM_EINVAL;
   *out = nullptr;
+  try {
+    return PbstreamOpen(path, out);
+  } catch (const std::bad_alloc&) {
+    return CSM_ENOMEM;
+  } catch (...) {
+    return CSM_EINVAL;
+  }
+}
+
+static int PbstreamOpen(const char* path, csm_pbstream** out) {
   FILE* f = std::fopen(path, "rb");
   if (!f) return CSM_EINVAL;
+  std::unique_ptr<FILE, int (*)(FILE*)> file_guard(f, &std::fclose);
   std::fseek(f, 0, SEEK_END);
   const long file_size = std::ftell(f);
   std::fseek(f, 0, SEEK_SET);
-  auto* s = new csm_pbstream();
+  std::unique_ptr<csm_pbstream> owner(new csm_pbstream());
+  csm_pbstream* s = owner.get();
   int rc = CSM_OK;
   uint64_t magic = 0;
   if (!ReadU64(f, &magic) || magic != kMagic) rc = CSM_EINVAL;  // proto_stream.cc:68-73
@@ -543,13 +583,10 @@ int csm_pbstream_open(const char* path, csm_pbstream** out) {
     });
     if (!ok && rc == CSM_OK) rc = CSM_EINVAL;
   }
-  std::fclose(f);
+  file_guard.reset();
   if (rc == CSM_OK && header) rc = CSM_EINVAL;  // no SerializationHeader
-  if (rc != CSM_OK) {
-    delete s;
-    return rc;
-  }
-  *out = s;
+  if (rc != CSM_OK) return rc;
+  *out = owner.release();
   return CSM_OK;
 }
 

@@ -14,7 +14,10 @@ from typing import Dict, List, Optional, Set, Tuple
 
 from .constraint_builder import FixedRatioSampler, rigid2d_compose, rigid2d_inverse
 
-TIME_MIN = -math.inf  # common::Time::min()
+# Times are seconds on the universal time scale; a trajectory pair never
+# connected reads the epoch (0), the value-initialised common::Time of
+# trajectory_connectivity_state.cc:67-70's map.
+TIME_EPOCH = 0.0
 
 
 @dataclass
@@ -55,7 +58,7 @@ class TrajectoryConnectivityState:
     def Connect(self, a: int, b: int, time: float):
         if self.TransitivelyConnected(a, b):
             key = (min(a, b), max(a, b))
-            if self._last.get(key, TIME_MIN) < time:
+            if self._last.get(key, TIME_EPOCH) < time:
                 self._last[key] = time
         else:
             for ia in self._component(a):
@@ -66,7 +69,7 @@ class TrajectoryConnectivityState:
         self._forest[self._find(a)] = self._find(b)
 
     def LastConnectionTime(self, a: int, b: int) -> float:
-        return self._last.get((min(a, b), max(a, b)), TIME_MIN)
+        return self._last.get((min(a, b), max(a, b)), TIME_EPOCH)
 
 
 @dataclass

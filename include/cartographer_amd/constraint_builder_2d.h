@@ -17,6 +17,7 @@
 #define CARTOGRAPHER_AMD_CONSTRAINT_BUILDER_2D_H_
 
 #include <cmath>
+#include <cstdio>
 #include <functional>
 #include <map>
 #include <memory>
@@ -107,6 +108,10 @@ class ConstraintBuilder2D {
   // Metrics (constraint_builder_2d.cc:46-53).
   int64_t constraints_searched = 0, constraints_found = 0;
   int64_t global_constraints_searched = 0, global_constraints_found = 0;
+  // Pairs skipped because the device search returned an error (not counted
+  // as searched), and the last such status.
+  int64_t constraints_failed = 0;
+  int last_error = CSM_OK;
 
  private:
   struct Pending {
@@ -194,10 +199,19 @@ class ConstraintBuilder2D {
                 "csm_ceres2d_refine_batch");
       for (size_t k = 0; k < which.size(); ++k) results[which[k]].pose = out[k];
     }
+    int64_t failed_this_flush = 0;
     for (size_t i = 0; i < pending_.size(); ++i) {
       const Pending& p = pending_[i];
+      if (results[i].status < 0) {
+        // A pair the device path could not search (CSM_ERANGE: a cloud or
+        // window past the kernels' limits) yields no
+        // constraint; it is counted and reported, never fatal.
+        ++constraints_failed;
+        ++failed_this_flush;
+        last_error = results[i].status;
+        continue;
+      }
       (p.full ? global_constraints_searched : constraints_searched) += 1;
-      CheckOk(results[i].status, "ComputeConstraint");
       if (results[i].status != CSM_OK) continue;
       (p.full ? global_constraints_found : constraints_found) += 1;
       const Rigid2d pose{results[i].pose.x, results[i].pose.y, results[i].pose.theta};
@@ -211,6 +225,10 @@ class ConstraintBuilder2D {
       c.score = results[i].score;
       constraints_[p.slot].reset(new Constraint(c));
     }
+    if (failed_this_flush)
+      std::fprintf(stderr, "ConstraintBuilder2D: %lld of %zu pairs skipped (%s)\n",
+                   static_cast<long long>(failed_this_flush), pending_.size(),
+                   csm_strerror(last_error));
     pending_.clear();
     num_finished_nodes_ = num_started_nodes_;
   }

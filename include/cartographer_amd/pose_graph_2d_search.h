@@ -50,7 +50,10 @@ struct PoseGraphSearchOptions {
 // reference's mutex: one thread drives the search here).
 class TrajectoryConnectivityState {
  public:
-  static constexpr double kTimeMin = -std::numeric_limits<double>::infinity();
+  // Times are seconds on the universal time scale (common::Time's epoch is
+  // 0). A pair never connected reads the epoch: last_connection_time_map_'s
+  // value-initialised common::Time (trajectory_connectivity_state.cc:67-70).
+  static constexpr double kEpoch = 0.;
 
   void Add(int trajectory_id) { forest_.emplace(trajectory_id, trajectory_id); }
 
@@ -74,10 +77,10 @@ class TrajectoryConnectivityState {
     return FindSet(a) == FindSet(b);
   }
 
-  // common::Time::min() for pairs never connected (map default).
+  // The epoch for pairs never connected (the map's default value).
   double LastConnectionTime(int a, int b) {
     const auto it = last_connection_.find(std::minmax(a, b));
-    return it == last_connection_.end() ? kTimeMin : it->second;
+    return it == last_connection_.end() ? kEpoch : it->second;
   }
 
  private:

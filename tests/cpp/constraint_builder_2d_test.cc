@@ -72,9 +72,39 @@ static void FindsConstraints() {
   EXPECT(builder.global_constraints_searched == 2 && builder.global_constraints_found == 2);
 }
 
+// A cloud past the device path's limit (more than 16448 points: CSM_ERANGE)
+// is skipped and counted; the other pairs of the flush still produce their
+// constraints and the process does not abort.
+static void SkipsUnsearchablePairs() {
+  ConstraintBuilder2D builder(TestOptions());
+  PointCloud small, huge;
+  small.push_back(0.1f, 0.2f, 0.3f);
+  for (int i = 0; i < 16449; ++i) huge.push_back(0.001f * (i % 100), 0.001f * (i / 100), 0.f);
+  std::vector<uint16_t> cells(100 * 110, 0);
+  Submap2DView submap;
+  submap.grid.resolution = 1.;
+  submap.grid.max_x = 2.;
+  submap.grid.max_y = 3.;
+  submap.grid.num_x_cells = 100;
+  submap.grid.num_y_cells = 110;
+  submap.grid.cells = cells.data();
+  submap.local_pose = Rigid2d{4., 5., 0.};
+  const SubmapId submap_id{0, 1};
+  builder.MaybeAddGlobalConstraint(submap_id, &submap, NodeId{0, 0}, &small);
+  builder.MaybeAddGlobalConstraint(submap_id, &submap, NodeId{0, 1}, &huge);
+  builder.NotifyEndOfNode();
+  ConstraintBuilder2D::Result result;
+  builder.WhenDone([&](const ConstraintBuilder2D::Result& r) { result = r; });
+  EXPECT(result.size() == 1);
+  EXPECT(result.size() == 1 && result[0].node_id.node_index == 0);
+  EXPECT(builder.constraints_failed == 1 && builder.last_error == CSM_ERANGE);
+  EXPECT(builder.global_constraints_searched == 1 && builder.global_constraints_found == 1);
+}
+
 int main() {
   CallsBack();
   FindsConstraints();
+  SkipsUnsearchablePairs();
   if (failures) return 1;
   std::printf("constraint_builder_2d_test: OK\n");
   return 0;

@@ -137,10 +137,39 @@ static void LocatesShiftedWall() {
   EXPECT(builder.constraints_searched == 1);
 }
 
+// A high-resolution cloud past the device limit (8192 points: CSM_ERANGE) is
+// skipped and counted; the other pair of the flush is still searched.
+static void SkipsUnsearchablePairs() {
+  TrajectoryNodeData3D small, huge;
+  small.high_resolution_point_cloud.push_back(0.1f, 0.2f, 0.3f);
+  small.low_resolution_point_cloud.push_back(0.1f, 0.2f, 0.3f);
+  small.rotational_scan_matcher_histogram.assign(3, 0.f);
+  for (int i = 0; i < 8193; ++i)
+    huge.high_resolution_point_cloud.push_back(0.01f * (i % 90), 0.01f * (i / 90), 0.f);
+  huge.low_resolution_point_cloud.push_back(0.1f, 0.2f, 0.3f);
+  huge.rotational_scan_matcher_histogram.assign(3, 0.f);
+  Submap3DView submap;
+  submap.high_resolution_hybrid_grid.resolution = 0.1f;
+  submap.low_resolution_hybrid_grid.resolution = 0.1f;
+  submap.rotational_scan_matcher_histogram.assign(3, 0.f);
+  ConstraintBuilder3D builder(TestOptions());
+  builder.MaybeAddConstraint(SubmapId{0, 1}, &submap, NodeId{0, 0}, &small, Rigid3d::Identity(),
+                             Rigid3d::Identity());
+  builder.MaybeAddConstraint(SubmapId{0, 1}, &submap, NodeId{0, 1}, &huge, Rigid3d::Identity(),
+                             Rigid3d::Identity());
+  builder.NotifyEndOfNode();
+  size_t n = 0;
+  builder.WhenDone([&](const ConstraintBuilder3D::Result& r) { n = r.size(); });
+  EXPECT(n == 1);
+  EXPECT(builder.constraints_failed == 1 && builder.last_error == CSM_ERANGE);
+  EXPECT(builder.constraints_searched == 1 && builder.constraints_found == 1);
+}
+
 int main() {
   CallsBack();
   FindsConstraints();
   LocatesShiftedWall();
+  SkipsUnsearchablePairs();
   if (failures) return 1;
   std::printf("OK\n");
   return 0;

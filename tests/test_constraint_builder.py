@@ -128,6 +128,28 @@ def test_finds_constraints(csm, cb):
 
 
 @pytest.mark.gpu
+def test_skips_unsearchable_pairs(csm, cb, capsys):
+    """A cloud past the device limit (16448 points: CSM_ERANGE) yields no
+    constraint and is counted in constraints_failed, exactly as the C++
+    header does (tests/cpp/constraint_builder_2d_test.cc); the rest of the
+    flush is unaffected and nothing raises."""
+    builder = cb.ConstraintBuilder2D(_test_options(cb))
+    submap = _unknown_submap(csm, cb)
+    small = np.array([[0.1, 0.2, 0.3]], np.float32)
+    i = np.arange(16449)
+    huge = np.stack([0.001 * (i % 100), 0.001 * (i // 100), np.zeros(len(i))], 1).astype(np.float32)
+    builder.MaybeAddGlobalConstraint((0, 1), submap, (0, 0), small)
+    builder.MaybeAddGlobalConstraint((0, 1), submap, (0, 1), huge)
+    builder.NotifyEndOfNode()
+    got = []
+    builder.WhenDone(got.append)
+    assert len(got[0]) == 1 and got[0][0].node_id == (0, 0)
+    assert builder.constraints_failed == 1 and builder.last_error == csm.CSM_ERANGE
+    assert builder.global_constraints_searched == 1 and builder.global_constraints_found == 1
+    assert "1 of 2 pairs skipped" in capsys.readouterr().err
+
+
+@pytest.mark.gpu
 def test_distance_filter_and_sampling(csm, cb):
     opts = _test_options(cb)
     opts.sampling_ratio = 0.5

@@ -209,8 +209,8 @@ def test_empty_stream(csm, tmp_path):
 
 
 @pytest.mark.parametrize("case", ["magic", "no_header", "truncated", "cell_range", "cell_count",
-                                  "cost_order", "missing", "garbage"])
-def test_malformed_streams_fail(csm, tmp_path, case):
+                                  "cost_order", "missing", "garbage", "num_points", "inflate_limit"])
+def test_malformed_streams_fail(csm, tmp_path, case, monkeypatch):
     path = tmp_path / f"{case}.pbstream"
     cells = np.zeros((2, 2), np.uint16)
     good = submap2d_msg(0, 0, [0, 0, 0, 1, 0, 0, 0], grid2d(0.05, 1.0, 1.0, cells))
@@ -240,6 +240,22 @@ def test_malformed_streams_fail(csm, tmp_path, case):
             f.write(struct.pack("<Q", MAGIC))
             f.write(struct.pack("<Q", 4))
             f.write(b"\x1f\x8b\x00\x00")
+    elif case == "num_points":
+        # A node cloud declaring 2^31 - 1 points over a few words of data is
+        # rejected before the loader allocates for the declared count.
+        data, _, _ = compress(np.array([[0.1, 0.2, 0.0]], np.float32))
+        cloud = f_int(1, 2**31 - 1) + f_packed(3, data)
+        nd = (f_int(1, 0) + f_msg(2, quaternion([1, 0, 0, 0])) + f_msg(3, cloud) +
+              f_msg(7, rigid3d([0, 0, 0, 1, 0, 0, 0])))
+        write_stream(path, [f_msg(4, f_msg(1, f_int(1, 0) + f_int(2, 0)) + f_msg(5, nd))])
+    elif case == "inflate_limit":
+        # A message that inflates past the per-message limit (lowered here;
+        # 256 MiB by default) fails instead of filling host memory.
+        monkeypatch.setenv("CSM_PBSTREAM_MAX_MESSAGE_BYTES", "4096")
+        big = submap2d_msg(0, 0, [0, 0, 0, 1, 0, 0, 0],
+                           grid2d(0.05, 1.0, 1.0, np.zeros((64, 64), np.uint16)))
+        assert len(big) > 4096
+        write_stream(path, [big])
     with pytest.raises(csm.CsmError):
         csm.read_pbstream(path)
 

@@ -57,6 +57,26 @@ def test_same_trajectory_is_local_with_relative_pose(pg):
     assert np.allclose(calls[0][3], exp, atol=1e-9)
 
 
+def test_unconnected_trajectory_early_node_is_local(pg):
+    """A never-connected trajectory pair reads the epoch (0) as its last
+    connection time (trajectory_connectivity_state.cc:67-70), so a node of
+    another trajectory earlier than global_constraint_search_after_n_seconds
+    gets a local search (pose_graph_2d.cc:276-282), a later one a global one.
+    Both mirrors run the same script."""
+    ops = [("S", (0, 0), (0.0, 0.0, 0.0)),
+           ("N", (0, 0), 0.0, (0.0, 0.0, 0.0), 1, [(0, 0)]),
+           ("N", (1, 0), 5.0, (0.0, 0.0, 0.0), 0, []),     # t < 10 s: local
+           ("N", (1, 1), 12.0, (0.0, 0.0, 0.0), 0, [])]    # t >= 10 s: global
+    want = [("L", (1, 0), (0, 0)), ("G", (1, 1), (0, 0))]
+    py = _run_python(pg, ops, 1.0, 10.0)
+    assert [c[:3] for c in py if c[0] != "E"] == want
+    _build_cpp_search()
+    out = subprocess.run([CPP_BIN, "1.0", "10.0"], input=_script(ops), capture_output=True,
+                         text=True, timeout=60, check=True).stdout
+    assert [c[:3] for c in _parse_cpp(out) if c[0] != "E"] == want
+    assert pg.TrajectoryConnectivityState().LastConnectionTime(0, 1) == 0.0
+
+
 def test_order_finished_submaps_then_old_nodes(pg):
     """:364-393: the node against every finished submap in SubmapId order, then
     the newly finished submap against older nodes in NodeId order, skipping
@@ -110,7 +130,7 @@ def test_connectivity_joins_components(pg):
     assert t.LastConnectionTime(0, 3) == 7.0 and t.LastConnectionTime(0, 1) == 5.0
     t.Connect(0, 3, 9.0)
     assert t.LastConnectionTime(0, 3) == 9.0 and t.LastConnectionTime(1, 3) == 7.0
-    assert t.LastConnectionTime(0, 9) == -math.inf
+    assert t.LastConnectionTime(0, 9) == 0.0  # the epoch: never connected
     assert t.TransitivelyConnected(0, 3) and not t.TransitivelyConnected(0, 9)
 
 
@@ -190,12 +210,16 @@ def _parse_cpp(text):
     return log
 
 
-def test_cpp_header_and_python_mirror_agree(pg):
+def _build_cpp_search():
     os.makedirs(os.path.dirname(CPP_BIN), exist_ok=True)
     subprocess.check_call(["g++", "-std=c++17", "-O1", "-Wall", "-Werror", "-I",
                            os.path.join(ROOT, "include"), CPP_TEST, "-o", CPP_BIN,
                            "-L", os.path.join(ROOT, "cartographer-1_amd"), "-lcsm_amd",
                            "-Wl,-rpath," + os.path.join(ROOT, "cartographer-1_amd")])
+
+
+def test_cpp_header_and_python_mirror_agree(pg):
+    _build_cpp_search()
     for seed, ratio, after in [(1, 0.003, 10.0), (2, 0.3, 10.0), (3, 1.0, 5.0)]:
         ops = _scenario(seed)
         py = _run_python(pg, ops, ratio, after)
