@@ -28,6 +28,9 @@ import time
 import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
+# Version tag of the search kernel the committed PMC traffic figures belong to
+# (a traffic file recorded on another kernel version is not reported).
+KERNEL_TAG = "v4-r2"
 
 
 def load_pkg():
@@ -55,6 +58,14 @@ def parse():
     p.add_argument("--nodes3d", type=int, default=500)
     p.add_argument("--submaps3d", type=int, default=25, help="3D submaps per GPU (C5: 200 / 8)")
     p.add_argument("--steps3d", type=int, default=3)
+    p.add_argument("--workload", default="c2", choices=["c2", "c3"],
+                   help="c2: 500 x 50 submaps per GPU (weak scaling, default); c3: the fixed "
+                        "2000-node x 1000-submap queue split over the ranks (strong scaling)")
+    p.add_argument("--c3-nodes", type=int, default=2000)
+    p.add_argument("--c3-submaps", type=int, default=1000)
+    p.add_argument("--c3-chunk", type=int, default=8, help="submaps per claimed chunk")
+    p.add_argument("--cpu-pairs", type=int, default=0,
+                   help="CPU baseline sample size (0: sized to --cpu-seconds)")
     return p.parse_args()
 
 
@@ -77,6 +88,8 @@ def main():
 
     csm = load_pkg()
     ctx = csm.Context(device)
+    if args.workload == "c3":
+        return c3_main(csm, ctx, args, rank, world_size, dist)
 
     # ---- synthetic world (identical on every rank) -------------------------
     t0 = time.time()
@@ -207,16 +220,25 @@ def main():
         sys.exit(3)
 
 
-def committed_traffic(args, world_size):
+TRAFFIC_FILES = {"c2": os.path.join("profiles", "r1e", "traffic_c2.json"),
+                 "c3": os.path.join("profiles", "r2", "traffic_c3.json")}
+
+
+def committed_traffic(args, world_size, workload="c2"):
     """HBM-side bytes per search launch from the committed PMC pass
-    (profiles/r1e/traffic_c2.json: rocprofv3 --pmc FETCH_SIZE, x2 gfx950
+    (profiles/*/traffic_*.json: rocprofv3 --pmc FETCH_SIZE, x2 gfx950
     correction). PMC counters cannot be read from inside this process, so the
     figure is reported only when this run's workload is the profiled one."""
-    path = os.path.join(ROOT, "profiles", "r1e", "traffic_c2.json")
+    path = os.path.join(ROOT, TRAFFIC_FILES[workload])
     try:
         t = json.load(open(path))
     except (OSError, ValueError):
         return None
+    if workload == "c3":
+        same = (args.c3_nodes == t["nodes"] and args.c3_submaps == t["submaps"] and
+                args.c3_chunk == t["chunk"] and abs(args.min_score - t["min_score"]) < 1e-9 and
+                args.search_depth == t["search_depth"] and t.get("commit_kernel") == KERNEL_TAG)
+        return t if same else None
     same = (world_size == 1 and args.nodes == t["nodes"] and
             args.submaps_per_rank == t["submaps_per_rank"] and
             abs(args.min_score - t["min_score"]) < 1e-9 and args.search_depth == t["search_depth"])
@@ -548,42 +570,290 @@ def fast3d_bench(csm, ctx, args, rank=0, world_size=1, dist=None, coll_dev=None,
 
 
 def cpu_baseline(world, my_submaps, args):
-    """The oracle restatement (the reference's algorithm and data structures)
-    on host threads, one pair per task as ConstraintBuilder2D schedules them,
-    on a bounded random sample of the same pairs."""
+    """C2 CPU baseline: the oracle restatement (the reference's algorithm and
+    data structures) on host threads, one pair per task as ConstraintBuilder2D
+    schedules them, on a bounded uniform random sample of the same queue."""
+    rng = np.random.RandomState(12345)
+    k = 100000
+    ps = np.asarray(my_submaps)[rng.randint(0, len(my_submaps), k)]
+    pn = rng.randint(0, world.num_nodes, k)
+    return cpu_pairs_2d(world, ps, pn, args, "uniformly sampled (submap, scan) pairs of the same C2 queue")
+
+
+def host_cpu():
+    """The host the CPU baseline runs on: CPU model, logical CPUs, the CPUs
+    this process may run on (affinity) and the cgroup CPU quota."""
+    info = {"model": None, "logical_cpus": os.cpu_count(), "affinity_cpus": None,
+            "cgroup_quota_cpus": None}
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                info["model"] = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        info["affinity_cpus"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        info["affinity_cpus"] = os.cpu_count()
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        if quota != "max":
+            info["cgroup_quota_cpus"] = int(quota) / int(period)
+    except (OSError, ValueError):
+        pass
+    usable = info["affinity_cpus"] or 1
+    if info["cgroup_quota_cpus"]:
+        usable = min(usable, max(1, int(math.ceil(info["cgroup_quota_cpus"]))))
+    info["usable_cpus"] = usable
+    return info
+
+
+def timed_pool(run, threads_options, probe_pairs_per_thread=2):
+    """Picks the thread count for the CPU baseline: a short probe at each
+    candidate (the usable CPUs, and every logical CPU when more are visible);
+    the faster per-pair rate wins. run(k, threads) -> (wall_s, task_seconds)."""
+    best = None
+    probes = []
+    for t in threads_options:
+        k = max(t * probe_pairs_per_thread, 4)
+        wall, _ = run(k, t)
+        probes.append({"threads": t, "pairs": k, "pairs_per_s": k / wall})
+        if best is None or k / wall > best[1]:
+            best = (t, k / wall)
+    return best, probes
+
+
+def summarize_cpu(k, wall, task_s, threads, cpu, probes, what):
+    """pairs/s on the sample, with a 95% interval from the spread of per-pair
+    costs: value * mean / (mean +- 1.96 * sd / sqrt(k))."""
+    mu = float(np.mean(task_s))
+    half = 1.96 * float(np.std(task_s, ddof=1)) / math.sqrt(k) if k > 1 else 0.0
+    value = k / wall
+    lo = value * mu / (mu + half)
+    hi = value * mu / (mu - half) if mu > half else float("inf")
+    return {"value": value, "ci95": [lo, hi], "unit": "pairs/s", "cores": threads,
+            "threads": threads, "kind": "port",
+            "host": {"cpu_model": cpu["model"], "logical_cpus": cpu["logical_cpus"],
+                     "affinity_cpus": cpu["affinity_cpus"],
+                     "cgroup_quota_cpus": cpu["cgroup_quota_cpus"]},
+            "thread_probes": probes,
+            "mean_pair_cpu_s": mu,
+            "sample": f"{k} {what}, {wall:.1f} s wall on {threads} threads "
+                      f"(oracle restatement, -O3 -DNDEBUG, one pair per task)"}
+
+
+def oracle_submaps_2d(o, world, submaps, threads):
+    """Oracle FastCorrelativeScanMatcher2D per submap, built on a thread pool
+    (ctypes releases the GIL; setup, outside any timed region)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    def make(s):
+        return o.fast2d((world.resolution, world.submap_max[s, 0], world.submap_max[s, 1]),
+                        world.submap_cells[s], 7.0, math.radians(30.0), 7)
+    with ThreadPoolExecutor(max_workers=max(1, threads)) as ex:
+        return list(ex.map(make, submaps))
+
+
+def cpu_pairs_2d(world, pair_sub, pair_node, args, what):
+    """CPU baseline on the given (submap, node) pairs: the oracle's
+    MatchFullSubmap, one pair per task on a pool of host threads
+    (ConstraintBuilder2D on common::ThreadPool, thread_pool.cc:80-106)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import ctypes as C
 
     import oracle_lib
     o = oracle_lib.Oracle()
-    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-    rng = np.random.RandomState(12345)
-    subs = [o.fast2d((world.resolution, world.submap_max[s, 0], world.submap_max[s, 1]),
-                     world.submap_cells[s], 7.0, math.radians(30.0), 7) for s in my_submaps]
-    handles = (C.c_void_p * len(subs))(*[s.h for s in subs])
+    cpu = host_cpu()
+    uniq, inv = np.unique(pair_sub, return_inverse=True)
+    subs = oracle_submaps_2d(o, world, uniq, cpu["usable_cpus"])
+    handles = (C.c_void_p * len(subs))(*[m.h for m in subs])
     pts = np.ascontiguousarray(world.points, np.float32)
     offs = np.ascontiguousarray(world.offsets, np.int64)
+    P = C.POINTER
+    cursor = [0]
 
-    def run(k):
-        ps = rng.randint(0, len(subs), k).astype(np.int32)
-        pn = rng.randint(0, world.num_nodes, k).astype(np.int32)
+    def run(k, threads):
+        # Consecutive slices of the (shuffled) sample: probes and the main
+        # run see different pairs of the same distribution.
+        idx = np.arange(cursor[0], cursor[0] + k) % len(inv)
+        cursor[0] += k
+        ps = np.ascontiguousarray(inv[idx], np.int32)
+        pn = np.ascontiguousarray(pair_node[idx], np.int32)
         scores, poses, matched = np.zeros(k, np.float32), np.zeros(3 * k), np.zeros(k, np.int32)
-        P = C.POINTER
+        task = np.zeros(k)
         wall = o.lib.oracle_fast2d_match_pairs(
             handles, pts.ctypes.data_as(P(C.c_float)), offs.ctypes.data_as(P(C.c_int64)),
             ps.ctypes.data_as(P(C.c_int32)), pn.ctypes.data_as(P(C.c_int32)), k, threads,
             args.min_score, scores.ctypes.data_as(P(C.c_float)), poses.ctypes.data_as(P(C.c_double)),
-            matched.ctypes.data_as(P(C.c_int32)))
-        return wall
+            matched.ctypes.data_as(P(C.c_int32)), task.ctypes.data_as(P(C.c_double)))
+        return wall, task
 
-    probe_k = threads
-    wall = run(probe_k)
-    k = max(threads, int(probe_k * args.cpu_seconds / max(wall, 1e-3)))
-    k = min(k, 20000)
-    wall = run(k)
-    return {"value": k / wall, "unit": "pairs/s", "cores": threads, "kind": "port",
-            "sample": f"{k} uniformly sampled (submap, scan) pairs of the same C2 queue, "
-                      f"{wall:.1f} s wall on {threads} threads (oracle, -O3 -DNDEBUG)"}
+    options = [args.cpu_threads] if args.cpu_threads else sorted(
+        {cpu["usable_cpus"], cpu["logical_cpus"] or cpu["usable_cpus"]})
+    (threads, rate), probes = timed_pool(run, options)
+    k = args.cpu_pairs or max(4 * threads, int(rate * args.cpu_seconds))
+    wall, task = run(k, threads)
+    return summarize_cpu(k, wall, task, threads, cpu, probes, what)
+
+
+class ChunkClaimer:
+    """Dynamic work claiming over the ranks: one atomic counter in the
+    process group's store (rank 0's TCPStore), so a rank that finishes early
+    takes the next chunk — the shared-queue balance of the reference's
+    ThreadPool (thread_pool.cc:80-106) across GPUs. Single process: a local
+    counter."""
+
+    def __init__(self, dist, n_chunks):
+        self.dist, self.n = dist, n_chunks
+        self.store = None
+        self.key = None
+        self.local = 0
+        if dist is not None:
+            from torch.distributed import distributed_c10d
+            self.store = distributed_c10d._get_default_store()
+
+    def reset(self, tag):
+        self.key = f"c3_claim_{tag}"
+        self.local = 0
+
+    def claim(self):
+        if self.store is None:
+            c, self.local = self.local, self.local + 1
+            return c
+        return int(self.store.add(self.key, 1)) - 1
+
+
+def c3_main(csm, ctx, args, rank, world_size, dist):
+    """C3: the ConstraintBuilder2D global sweep of BASELINE.json configs[2],
+    2000 nodes x 1000 submaps (2 M MatchFullSubmap pairs, min_score 0.55),
+    as ONE fixed queue split over the ranks (strong scaling). The queue is
+    cut into chunks of --c3-chunk submaps x all nodes; ranks claim chunks
+    dynamically, build the chunk's pyramids on their GPU, search it as one
+    batch and keep the accepted constraints; at the end every rank's records
+    are gathered to rank 0 in submission order (constraint_builder_2d.cc:279-300).
+    A step = the whole queue; pyramid builds are inside the timed region."""
+    cdist = importlib.import_module("cartographer_amd.distributed")
+    N, S, K = args.c3_nodes, args.c3_submaps, args.c3_chunk
+    t0 = time.time()
+    world = csm.SyntheticWorld2D(num_nodes=N, num_submaps=S, submap_cells=400, beams=1080,
+                                 seed=args.seed)
+    gen_s = time.time() - t0
+    opts = csm.FastCorrelativeScanMatcherOptions2D(7.0, math.radians(30.0), 7, args.search_depth)
+    scans = csm.ScanSet(None, ctx, packed=(world.points, world.offsets))
+    n_chunks = (S + K - 1) // K
+    coll_dev = None
+    if dist is not None:
+        import torch
+        coll_dev = torch.device("cuda", torch.cuda.current_device()) \
+            if args.dist_backend == "nccl" else None
+
+    def run_chunk(c):
+        subs = np.arange(c * K, min(S, (c + 1) * K))
+        mats = [csm.FastCorrelativeScanMatcher2D(world.grid(int(s)), opts, ctx) for s in subs]
+        sub_local = np.repeat(np.arange(len(subs), dtype=np.int32), N)
+        node = np.tile(np.arange(N, dtype=np.int32), len(subs))
+        pairs = csm.make_pairs(sub_local, node, args.min_score, full_submap=True)
+        res = csm.match_batch(mats, scans, pairs, ctx)
+        for m in mats:
+            m.close()
+        sub_global = subs[sub_local].astype(np.int64)
+        submission = sub_global * N + node  # queue order: submap-major
+        return res, cdist.make_records(res, submission, sub_global, node)
+
+    for _ in range(args.warmup):  # one chunk: module load, staging buffers
+        run_chunk(rank % n_chunks)
+    claimer = ChunkClaimer(dist, n_chunks)
+    ctx.reset_timing()
+    ctx.enable_timing(True)
+    errors = 0
+    claims = []
+    accepted = 0
+    step_s = []
+    for step in range(args.steps):
+        claimer.reset(step)
+        if dist is not None:
+            dist.barrier()
+            import torch
+            torch.cuda.synchronize()
+        a = time.perf_counter()
+        recs = []
+        mine = 0
+        while True:
+            c = claimer.claim()
+            if c >= n_chunks:
+                break
+            res, rec = run_chunk(c)
+            errors += int((res["status"] < 0).sum())
+            recs.append(rec)
+            mine += 1
+            if rank == 0 and world_size == 1:
+                print(f"c3: chunk {c + 1}/{n_chunks} {time.perf_counter() - a:.1f} s",
+                      file=sys.stderr, flush=True)
+        rec = np.concatenate(recs) if recs else np.zeros((0, cdist.RECORD_WIDTH))
+        out = cdist.gather_records(rec, dist, rank, world_size, coll_dev)
+        if dist is not None:
+            dist.barrier()
+            import torch
+            torch.cuda.synchronize()
+        step_s.append(time.perf_counter() - a)
+        claims.append(mine)
+        if rank == 0:
+            accepted = len(out)
+    ctx.enable_timing(False)
+    tm = ctx.timing()
+    elapsed = cdist.max_over_ranks(sum(step_s), dist, coll_dev)
+    errors = int(cdist.sum_over_ranks(errors, dist, coll_dev))
+    total_pairs = N * S * args.steps
+    kernel_ms = cdist.max_over_ranks(tm.search_kernel_ms, dist, coll_dev)
+    lookups = cdist.sum_over_ranks(tm.search_lookups, dist, coll_dev)
+    launches = cdist.sum_over_ranks(tm.search_launches, dist, coll_dev)
+    achieved = tm.search_lookups / (tm.search_kernel_ms * 1e-3) / 1e9 if tm.search_kernel_ms else 0.0
+    traffic = committed_traffic(args, world_size, "c3")
+    out = {
+        "metric": "loop-closure constraint candidates/sec (node x submap pairs) + ms/scan-match, 2D 5cm grid",
+        "value": total_pairs / elapsed, "unit": "pairs/s", "n_gpus": world_size,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (seeded building world, 1080-beam scans, ray-cast submaps)",
+        "config": {"workload": f"C3: ConstraintBuilder2D global sweep, {N} nodes x {S} submaps "
+                               f"(400x400 @5cm) = {N * S} MatchFullSubmap pairs, one fixed queue over "
+                               f"the ranks, chunks of {K} submaps claimed dynamically, "
+                               f"branch_and_bound_depth=7, min_score={args.min_score:.2f}",
+                   "pairs_per_step": N * S, "search_depth": 0 if args.search_depth == 0 else args.search_depth,
+                   "parallelism": f"dynamic chunk claiming x{world_size}"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": 8000.0, "unit": "GB/s",
+                     "frac": achieved / 8000.0,
+                     "traffic": traffic["traffic_bytes_per_launch"] if traffic else None,
+                     "traffic_source": traffic["source"] if traffic else None,
+                     "kernel": "fast2d_search",
+                     "kernel_ms_avg": tm.search_kernel_ms / max(tm.search_launches, 1),
+                     "algorithmic_bytes_per_launch": tm.search_lookups / max(tm.search_launches, 1)},
+        "accepted_constraints_per_step": accepted,
+        "errors_per_step": errors / args.steps,
+        "stack_high_water": int(tm.stack_high_water),
+        "chunks": n_chunks, "chunks_claimed_rank0": claims,
+        "kernel_s_max_over_ranks": kernel_ms * 1e-3, "search_launches": int(launches),
+        "lookups_per_pair": lookups / max(total_pairs, 1),
+        "setup_s": {"world": gen_s},
+    }
+    if rank == 0 and world_size == 1 and not args.no_cpu:
+        rng = np.random.RandomState(12345)
+        k = args.cpu_pairs or 2000
+        args.cpu_pairs = k
+        ps = rng.randint(0, S, k)
+        pn = rng.randint(0, N, k)
+        out["cpu_baseline"] = cpu_pairs_2d(world, ps, pn, args,
+                                           f"uniformly sampled (submap, node) pairs of the C3 queue")
+        out["speedup_vs_cpu"] = out["value"] / out["cpu_baseline"]["value"]
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+    if errors:
+        print(f"bench: {errors} pair searches returned an error status", file=sys.stderr)
+        sys.exit(3)
 
 
 if __name__ == "__main__":

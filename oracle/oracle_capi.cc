@@ -159,7 +159,7 @@ double oracle_fast2d_match_pairs(void* const* submaps, const float* points,
                                  const int32_t* pair_submap,
                                  const int32_t* pair_node, int64_t num_pairs,
                                  int32_t threads, float min_score, float* scores,
-                                 double* poses, int32_t* matched) {
+                                 double* poses, int32_t* matched, double* task_seconds) {
   std::vector<PointCloud> clouds;
   // Clouds are materialised per task (TrajectoryNode::Data holds them
   // already in the reference; conversion is outside the timed region).
@@ -178,7 +178,11 @@ double oracle_fast2d_match_pairs(void* const* submaps, const float* points,
         const auto* m = static_cast<const FastCorrelativeScanMatcher2D*>(submaps[pair_submap[i]]);
         Rigid2d pose;
         float score = 0.f;
+        const auto ts = std::chrono::steady_clock::now();
         const bool ok = m->MatchFullSubmap(clouds[pair_node[i]], min_score, &score, &pose);
+        if (task_seconds)  // per-task time, for the baseline's confidence interval
+          task_seconds[i] =
+              std::chrono::duration<double>(std::chrono::steady_clock::now() - ts).count();
         matched[i] = ok ? 1 : 0;
         scores[i] = ok ? score : 0.f;
         poses[3 * i] = pose.tx;

@@ -220,7 +220,7 @@ double oracle_fast3d_match_pairs(void** submaps, const float* high, const int64_
                                  const float* low, const int64_t* low_off, const float* hists,
                                  int hsize, const double* node_q, const int32_t* pair_submap,
                                  const int32_t* pair_node, int64_t num_pairs, int threads,
-                                 float min_score, int32_t* matched) {
+                                 float min_score, int32_t* matched, double* task_seconds) {
   std::atomic<int64_t> next{0};
   const auto t0 = std::chrono::steady_clock::now();
   auto work = [&]() {
@@ -231,9 +231,12 @@ double oracle_fast3d_match_pairs(void** submaps, const float* high, const int64_
                low + 3 * low_off[n], static_cast<int>(low_off[n + 1] - low_off[n]),
                hists + static_cast<int64_t>(hsize) * n, hsize, kIdentityQ);
       const double* q = node_q + 4 * n;
+      const auto ts = std::chrono::steady_clock::now();
       const Fast3dResult r = static_cast<Fast3dHandle*>(submaps[pair_submap[i]])->m->MatchFullSubmap(
           Quatd{q[0], q[1], q[2], q[3]}, Quatd{1., 0., 0., 0.}, node, min_score);
       matched[i] = r.matched ? 1 : 0;
+      if (task_seconds)
+        task_seconds[i] = std::chrono::duration<double>(std::chrono::steady_clock::now() - ts).count();
     }
   };
   std::vector<std::thread> pool;

@@ -28,7 +28,7 @@ class Oracle:
             "oracle_fast2d_score_candidate": (I32, [VP, I32, P(D), D, D, P(F), I32, I32, I32,
                                                     I32, I32, P(I32), P(F)]),
             "oracle_fast2d_match_pairs": (D, [P(VP), P(F), P(I64), P(I32), P(I32), I64, I32, F,
-                                              P(F), P(D), P(I32)]),
+                                              P(F), P(D), P(I32), P(D)]),
             "oracle_rt2d_match": (D, [D, D, D, I32, I32, P(C.c_uint16), D, D, D, D, P(D), P(F),
                                       I32, P(D), P(I64)]),
             "oracle_rt2d_time": (D, [D, D, D, I32, I32, P(C.c_uint16), D, D, D, D, P(D), P(F),
@@ -246,7 +246,7 @@ _SIG3D = {
     "oracle_rt3d_score": (F, [VP, P(D), P(D), P(F), I32, I64, P(D)]),
     "oracle_rt3d_window": (None, [P(D), F, P(F), I32, P(I32), P(F), P(I32)]),
     "oracle_fast3d_match_pairs": (D, [P(VP), P(F), P(I64), P(F), P(I64), P(F), I32, P(D),
-                                      P(I32), P(I32), I64, I32, F, P(I32)]),
+                                      P(I32), P(I32), I64, I32, F, P(I32), P(D)]),
     "oracle_rt3d_time": (D, [VP, P(D), P(D), P(F), I32, I64, I64]),
 }
 
