@@ -675,22 +675,36 @@ def cpu_pairs_2d(world, pair_sub, pair_node, args, what):
 
     def run(k, threads):
         # Consecutive slices of the (shuffled) sample: probes and the main
-        # run see different pairs of the same distribution.
-        idx = np.arange(cursor[0], cursor[0] + k) % len(inv)
-        cursor[0] += k
-        ps = np.ascontiguousarray(inv[idx], np.int32)
-        pn = np.ascontiguousarray(pair_node[idx], np.int32)
-        scores, poses, matched = np.zeros(k, np.float32), np.zeros(3 * k), np.zeros(k, np.int32)
-        task = np.zeros(k)
-        wall = o.lib.oracle_fast2d_match_pairs(
-            handles, pts.ctypes.data_as(P(C.c_float)), offs.ctypes.data_as(P(C.c_int64)),
-            ps.ctypes.data_as(P(C.c_int32)), pn.ctypes.data_as(P(C.c_int32)), k, threads,
-            args.min_score, scores.ctypes.data_as(P(C.c_float)), poses.ctypes.data_as(P(C.c_double)),
-            matched.ctypes.data_as(P(C.c_int32)), task.ctypes.data_as(P(C.c_double)))
-        return wall, task
+        # run see different pairs of the same distribution. Slices of
+        # 64 pairs per thread keep every thread busy and let a long sample
+        # print progress (a silent minute-long call looks hung).
+        wall, tasks, done, t0 = 0.0, [], 0, time.time()
+        while done < k:
+            kk = min(k - done, 64 * threads)
+            idx = np.arange(cursor[0], cursor[0] + kk) % len(inv)
+            cursor[0] += kk
+            ps = np.ascontiguousarray(inv[idx], np.int32)
+            pn = np.ascontiguousarray(pair_node[idx], np.int32)
+            scores, poses = np.zeros(kk, np.float32), np.zeros(3 * kk)
+            matched, task = np.zeros(kk, np.int32), np.zeros(kk)
+            wall += o.lib.oracle_fast2d_match_pairs(
+                handles, pts.ctypes.data_as(P(C.c_float)), offs.ctypes.data_as(P(C.c_int64)),
+                ps.ctypes.data_as(P(C.c_int32)), pn.ctypes.data_as(P(C.c_int32)), kk, threads,
+                args.min_score, scores.ctypes.data_as(P(C.c_float)),
+                poses.ctypes.data_as(P(C.c_double)), matched.ctypes.data_as(P(C.c_int32)),
+                task.ctypes.data_as(P(C.c_double)))
+            tasks.append(task)
+            done += kk
+            if k > 64 * threads:
+                print(f"cpu baseline: {done}/{k} pairs, {time.time() - t0:.0f} s", file=sys.stderr,
+                      flush=True)
+        return wall, np.concatenate(tasks)
 
+    # Thread counts to probe: the usable CPUs (affinity and cgroup quota);
+    # every logical CPU as well only when no quota caps the process.
     options = [args.cpu_threads] if args.cpu_threads else sorted(
-        {cpu["usable_cpus"], cpu["logical_cpus"] or cpu["usable_cpus"]})
+        {cpu["usable_cpus"]} | ({cpu["logical_cpus"]} if cpu["logical_cpus"] and
+                                not cpu["cgroup_quota_cpus"] else set()))
     (threads, rate), probes = timed_pool(run, options)
     k = args.cpu_pairs or max(4 * threads, int(rate * args.cpu_seconds))
     wall, task = run(k, threads)

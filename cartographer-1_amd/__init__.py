@@ -121,27 +121,31 @@ class Result3D(C.Structure):
 
 
 class CeresOptions2D(C.Structure):
-    """proto::CeresScanMatcherOptions2D; defaults pose_graph.lua:30-39."""
+    """proto::CeresScanMatcherOptions2D; defaults pose_graph.lua:30-39
+    (ceres_solver_options: max_num_iterations 10, use_nonmonotonic_steps)."""
     _fields_ = [("occupied_space_weight", C.c_double), ("translation_weight", C.c_double),
-                ("rotation_weight", C.c_double), ("max_num_iterations", C.c_int32)]
+                ("rotation_weight", C.c_double), ("max_num_iterations", C.c_int32),
+                ("use_nonmonotonic_steps", C.c_int32)]
 
     @staticmethod
     def make(occupied_space_weight=20.0, translation_weight=10.0, rotation_weight=1.0,
-             max_num_iterations=10) -> "CeresOptions2D":
+             max_num_iterations=10, use_nonmonotonic_steps=True) -> "CeresOptions2D":
         return CeresOptions2D(occupied_space_weight, translation_weight, rotation_weight,
-                              max_num_iterations)
+                              max_num_iterations, int(bool(use_nonmonotonic_steps)))
 
 
 class CeresOptions3D(C.Structure):
-    """proto::CeresScanMatcherOptions3D; defaults pose_graph.lua:49-60."""
+    """proto::CeresScanMatcherOptions3D; defaults pose_graph.lua:49-60
+    (ceres_solver_options: max_num_iterations 10, monotonic steps)."""
     _fields_ = [("occupied_space_weight_0", C.c_double), ("occupied_space_weight_1", C.c_double),
                 ("translation_weight", C.c_double), ("rotation_weight", C.c_double),
-                ("max_num_iterations", C.c_int32)]
+                ("max_num_iterations", C.c_int32), ("use_nonmonotonic_steps", C.c_int32)]
 
     @staticmethod
     def make(w0=5.0, w1=30.0, translation_weight=10.0, rotation_weight=1.0,
-             max_num_iterations=10) -> "CeresOptions3D":
-        return CeresOptions3D(w0, w1, translation_weight, rotation_weight, max_num_iterations)
+             max_num_iterations=10, use_nonmonotonic_steps=False) -> "CeresOptions3D":
+        return CeresOptions3D(w0, w1, translation_weight, rotation_weight, max_num_iterations,
+                              int(bool(use_nonmonotonic_steps)))
 
 
 class Refine3D(C.Structure):

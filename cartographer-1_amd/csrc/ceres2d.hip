@@ -10,11 +10,12 @@
 // translation delta to the match and the rotation delta to its angle. Each
 // iteration the workgroup evaluates the N residual rows and their analytic
 // Jacobian (what AutoDiff computes) in double, reduces J^T J and J^T r, and
-// one lane takes a Levenberg-Marquardt trust-region step with Ceres' defaults
-// (Jacobi scaling from the initial Jacobian, radius 1e4, diagonal clamp
-// [1e-6, 1e32], min relative decrease 1e-3, tolerances 1e-6 / 1e-10 / 1e-8).
-// Ceres is absent from this image, so the solver follows oracle/ceres2d.cc's
-// restatement (parity unpinned against Ceres itself).
+// every lane takes the same Levenberg-Marquardt trust-region step with Ceres
+// 1.13's defaults (Jacobi scaling from the initial Jacobian, radius 1e4,
+// diagonal clamp [1e-6, 1e32], min relative decrease 1e-3, tolerances 1e-6 /
+// 1e-10 / 1e-8, non-monotonic steps as pose_graph.lua:35 sets them). Ceres is
+// absent from this image: the solver follows oracle/ceres2d.cc's restatement,
+// which the reference's ceres_scan_matcher_2d_test.cc pins.
 
 #include <hip/hip_runtime.h>
 
@@ -23,6 +24,7 @@
 #include <cmath>
 #include <vector>
 
+#include "ceres_lm.h"
 #include "csm_internal.h"
 
 namespace csm {
@@ -44,6 +46,7 @@ struct RefineDesc {
 struct RefineOpts {
   double occupied, wt, wr;
   int max_iterations;
+  int nonmonotonic;  // ceres_solver_options.use_nonmonotonic_steps
 };
 
 __device__ __forceinline__ double CostAt(const RefineDesc& d, int row, int col) {
@@ -177,12 +180,16 @@ __device__ void Pass(const RefineDesc& d, const float* pts, double scale, const 
   for (int k = 0; k < 10; ++k) out[k] = acc[k];
 }
 
+// The minimizer loop is Ceres' TrustRegionMinimizer::Minimize: LM step
+// (invalid when the model decrease is not positive), candidate cost,
+// parameter then function tolerance (both end the solve without taking the
+// candidate), acceptance by step quality > 1e-3; the lowest-cost accepted
+// point is returned. Every thread runs the (scalar) step logic on the same
+// block-reduced sums, so all of them hold the same state.
 __global__ void __launch_bounds__(kRefineThreads)
 ceres2d_refine(const RefineDesc* __restrict__ items, const float* __restrict__ points,
                RefineOpts o, double* __restrict__ out_pose, int32_t* __restrict__ out_iters) {
   __shared__ double red[kRefineThreads / 64][10];
-  __shared__ double sxn[3];
-  __shared__ int sflag;  // 0 continue, 1 stop
   const RefineDesc d = items[blockIdx.x];
   const float* pts = points + 3 * d.point_offset;
   const double scale = o.occupied / sqrt(static_cast<double>(d.n));
@@ -192,68 +199,72 @@ ceres2d_refine(const RefineDesc* __restrict__ items, const float* __restrict__ p
   double cost = 0.5 * S[0];
   // Jacobi scaling from the initial Jacobian.
   const double js[3] = {1. / (1. + sqrt(S[1])), 1. / (1. + sqrt(S[4])), 1. / (1. + sqrt(S[6]))};
-  double radius = 1e4, decrease = 2.;
-  int iter = 0;
-  while (iter < o.max_iterations) {
+  StepEvaluator ev(cost, o.nonmonotonic != 0);
+  double best[3] = {x[0], x[1], x[2]}, best_cost = cost;
+  LmRadius lm;
+  int iter = 0, invalid = 0;
+  auto gradient_small = [&]() {
+    return fmax(fabs(S[7]), fmax(fabs(S[8]), fabs(S[9]))) <= 1e-10;
+  };
+  bool go = o.max_iterations > 0 && !gradient_small();
+  while (go) {
     ++iter;
-    if (threadIdx.x == 0) {
-      sflag = 0;
-      const double gu[3] = {S[7], S[8], S[9]};
-      if (fmax(fabs(gu[0]), fmax(fabs(gu[1]), fabs(gu[2]))) <= 1e-10) sflag = 1;
-      const double Au[3][3] = {{S[1], S[2], S[3]}, {S[2], S[4], S[5]}, {S[3], S[5], S[6]}};
-      double A[3][3], g[3], M[3][4], ds[3] = {0., 0., 0.};
+    const double Au[3][3] = {{S[1], S[2], S[3]}, {S[2], S[4], S[5]}, {S[3], S[5], S[6]}};
+    double A[3][3], g[3], M[3][4], ds[3] = {0., 0., 0.};
+    for (int a = 0; a < 3; ++a) {
+      g[a] = S[7 + a] * js[a];
+      for (int b = 0; b < 3; ++b) A[a][b] = Au[a][b] * js[a] * js[b];
+    }
+    for (int a = 0; a < 3; ++a) {
+      for (int b = 0; b < 3; ++b) M[a][b] = A[a][b];
+      M[a][a] += fmin(fmax(A[a][a], 1e-6), 1e32) / lm.radius;
+      M[a][3] = -g[a];
+    }
+    const bool solved = Solve3(M, ds);
+    double gd = 0., dad = 0.;
+    for (int a = 0; a < 3; ++a) {
+      gd += g[a] * ds[a];
+      for (int b = 0; b < 3; ++b) dad += ds[a] * A[a][b] * ds[b];
+    }
+    const double model = -(gd + 0.5 * dad);
+    if (!solved || !(model > 0.)) {
+      if (++invalid > 5) break;  // HandleInvalidStep: LM rejects the step
+      lm.Rejected();
+    } else {
+      invalid = 0;
+      double xn[3], step_norm = 0., x_norm = 0.;
       for (int a = 0; a < 3; ++a) {
-        g[a] = gu[a] * js[a];
-        for (int b = 0; b < 3; ++b) A[a][b] = Au[a][b] * js[a] * js[b];
-      }
-      for (int a = 0; a < 3; ++a) {
-        for (int b = 0; b < 3; ++b) M[a][b] = A[a][b];
-        M[a][a] += fmin(fmax(A[a][a], 1e-6), 1e32) / radius;
-        M[a][3] = -g[a];
-      }
-      if (!sflag && !Solve3(M, ds)) sflag = 1;
-      double step_norm = 0., x_norm = 0.;
-      for (int a = 0; a < 3; ++a) {
-        sxn[a] = x[a] + ds[a] * js[a];
-        step_norm += (ds[a] * js[a]) * (ds[a] * js[a]);
+        const double step = ds[a] * js[a];
+        xn[a] = x[a] + step;
+        step_norm += step * step;
         x_norm += x[a] * x[a];
       }
-      if (!sflag && sqrt(step_norm) <= 1e-8 * (sqrt(x_norm) + 1e-8)) sflag = 1;
-      double gd = 0., dad = 0.;
-      for (int a = 0; a < 3; ++a) {
-        gd += g[a] * ds[a];
-        for (int b = 0; b < 3; ++b) dad += ds[a] * A[a][b] * ds[b];
+      double T[10];
+      Pass<false>(d, pts, scale, o, xn, T, red);
+      const double new_cost = 0.5 * T[0];
+      if (sqrt(step_norm) <= (sqrt(x_norm) + 1e-8) * 1e-8) break;  // parameter tolerance
+      if (fabs(cost - new_cost) <= 1e-6 * cost) break;             // function tolerance
+      const double quality = ev.Quality(new_cost, model);
+      if (quality > 1e-3) {
+        for (int a = 0; a < 3; ++a) x[a] = xn[a];
+        Pass<true>(d, pts, scale, o, x, S, red);
+        cost = 0.5 * S[0];
+        lm.Accepted(quality);
+        ev.Accepted(new_cost, model);
+        if (cost < best_cost) {
+          best_cost = cost;
+          for (int a = 0; a < 3; ++a) best[a] = x[a];
+        }
+      } else {
+        lm.Rejected();
       }
-      red[0][0] = -(gd + 0.5 * dad);  // model cost change, read after the barrier
     }
-    __syncthreads();
-    if (sflag) break;
-    const double model = red[0][0];
-    const double xn[3] = {sxn[0], sxn[1], sxn[2]};
-    __syncthreads();
-    double T[10];
-    Pass<false>(d, pts, scale, o, xn, T, red);
-    const double new_cost = 0.5 * T[0];
-    const double rho = model > 0. ? (cost - new_cost) / model : -1.;
-    if (rho > 1e-3) {
-      const double change = cost - new_cost;
-      for (int a = 0; a < 3; ++a) x[a] = xn[a];
-      const double tf = 2. * rho - 1.;
-      radius = fmin(1e16, radius / fmax(1. / 3., 1. - tf * tf * tf));
-      decrease = 2.;
-      const double old_cost = cost;
-      Pass<true>(d, pts, scale, o, x, S, red);
-      cost = 0.5 * S[0];
-      if (fabs(change) <= 1e-6 * old_cost) break;
-    } else {
-      radius /= decrease;
-      decrease *= 2.;
-    }
+    go = iter < o.max_iterations && lm.radius >= 1e-32 && !gradient_small();
   }
   if (threadIdx.x == 0) {
-    out_pose[3 * blockIdx.x + 0] = x[0];
-    out_pose[3 * blockIdx.x + 1] = x[1];
-    out_pose[3 * blockIdx.x + 2] = x[2];
+    out_pose[3 * blockIdx.x + 0] = best[0];
+    out_pose[3 * blockIdx.x + 1] = best[1];
+    out_pose[3 * blockIdx.x + 2] = best[2];
     if (out_iters) out_iters[blockIdx.x] = iter;
   }
 }
@@ -309,7 +320,8 @@ int csm_ceres2d_refine_batch(csm_context* ctx, csm_fast2d* const* submaps, int32
   CSM_HIP(hipMemcpyAsync(ctx->cr_items.ptr, desc.data(), sizeof(RefineDesc) * n,
                          hipMemcpyHostToDevice, st));
   const RefineOpts o{options->occupied_space_weight, options->translation_weight,
-                     options->rotation_weight, options->max_num_iterations};
+                     options->rotation_weight, options->max_num_iterations,
+                     options->use_nonmonotonic_steps ? 1 : 0};
   double* dpose = ctx->cr_out.as<double>();
   int32_t* diters = reinterpret_cast<int32_t*>(dpose + 3 * n);
   hipLaunchKernelGGL(ceres2d_refine, dim3(static_cast<unsigned>(n)), dim3(kRefineThreads), 0, st,

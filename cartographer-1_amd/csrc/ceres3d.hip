@@ -21,6 +21,7 @@
 #include <cmath>
 #include <vector>
 
+#include "ceres_lm.h"
 #include "csm_internal.h"
 
 namespace csm {
@@ -45,6 +46,7 @@ struct Refine3Desc {
 struct Refine3Opts {
   double w0, w1, wt, wr;
   int max_iterations;
+  int nonmonotonic;  // ceres_solver_options.use_nonmonotonic_steps
 };
 
 __device__ __forceinline__ double Prob(const GridView3& g, int x, int y, int z) {
@@ -258,12 +260,12 @@ __device__ void Unpack(const double* S, double* Au, double* gu) {
   for (int a = 0; a < 6; ++a) gu[a] = S[22 + a];
 }
 
+// Ceres 1.13 TrustRegionMinimizer::Minimize as in ceres2d.hip: every thread
+// runs the 6-dimensional step logic on the same block-reduced sums.
 __global__ void __launch_bounds__(kR3Threads)
 ceres3d_refine(const Refine3Desc* __restrict__ items, const float* __restrict__ points,
                Refine3Opts o, double* __restrict__ out, int32_t* __restrict__ out_iters) {
   __shared__ double red[kR3Threads / 64][kSums];
-  __shared__ double snext[7], smodel;
-  __shared__ int sflag;
   const Refine3Desc d = items[blockIdx.x];
   const double scale[2] = {o.w0 / sqrt(static_cast<double>(d.n[0])),
                            o.w1 / sqrt(static_cast<double>(d.n[1]))};
@@ -275,26 +277,40 @@ ceres3d_refine(const Refine3Desc* __restrict__ items, const float* __restrict__ 
   double Au[36], gu[6], js[6];
   Unpack(S, Au, gu);
   for (int a = 0; a < 6; ++a) js[a] = 1. / (1. + sqrt(Au[7 * a]));
-  double radius = 1e4, decrease = 2.;
-  int iter = 0;
-  while (iter < o.max_iterations) {
+  StepEvaluator ev(cost, o.nonmonotonic != 0);
+  LmRadius lm;
+  double best_t[3] = {t[0], t[1], t[2]}, best_q[4] = {q[0], q[1], q[2], q[3]}, best_cost = cost;
+  int iter = 0, invalid = 0;
+  auto gradient_small = [&]() {
+    double gmax = 0.;
+    for (int a = 0; a < 6; ++a) gmax = fmax(gmax, fabs(gu[a]));
+    return gmax <= 1e-10;
+  };
+  bool go = o.max_iterations > 0 && !gradient_small();
+  while (go) {
     ++iter;
-    if (threadIdx.x == 0) {
-      sflag = 0;
-      double gmax = 0.;
-      for (int a = 0; a < 6; ++a) gmax = fmax(gmax, fabs(gu[a]));
-      if (gmax <= 1e-10) sflag = 1;
-      double A[36], g[6], M[36], rhs[6], ds[6] = {0., 0., 0., 0., 0., 0.};
-      for (int a = 0; a < 6; ++a) {
-        g[a] = gu[a] * js[a];
-        for (int b = 0; b < 6; ++b) A[6 * a + b] = Au[6 * a + b] * js[a] * js[b];
-      }
-      for (int a = 0; a < 6; ++a) {
-        for (int b = 0; b < 6; ++b) M[6 * a + b] = A[6 * a + b];
-        M[7 * a] += fmin(fmax(A[7 * a], 1e-6), 1e32) / radius;
-        rhs[a] = -g[a];
-      }
-      if (!sflag && !Solve6(M, rhs, ds)) sflag = 1;
+    double A[36], g[6], M[36], rhs[6], ds[6] = {0., 0., 0., 0., 0., 0.};
+    for (int a = 0; a < 6; ++a) {
+      g[a] = gu[a] * js[a];
+      for (int b = 0; b < 6; ++b) A[6 * a + b] = Au[6 * a + b] * js[a] * js[b];
+    }
+    for (int a = 0; a < 6; ++a) {
+      for (int b = 0; b < 6; ++b) M[6 * a + b] = A[6 * a + b];
+      M[7 * a] += fmin(fmax(A[7 * a], 1e-6), 1e32) / lm.radius;
+      rhs[a] = -g[a];
+    }
+    const bool solved = Solve6(M, rhs, ds);
+    double gd = 0., dad = 0.;
+    for (int a = 0; a < 6; ++a) {
+      gd += g[a] * ds[a];
+      for (int b = 0; b < 6; ++b) dad += ds[a] * A[6 * a + b] * ds[b];
+    }
+    const double model = -(gd + 0.5 * dad);
+    if (!solved || !(model > 0.)) {
+      if (++invalid > 5) break;  // HandleInvalidStep: LM rejects the step
+      lm.Rejected();
+    } else {
+      invalid = 0;
       double step[6], step_norm = 0., x_norm = 0.;
       for (int a = 0; a < 6; ++a) {
         step[a] = ds[a] * js[a];
@@ -302,53 +318,43 @@ ceres3d_refine(const Refine3Desc* __restrict__ items, const float* __restrict__ 
       }
       for (int a = 0; a < 3; ++a) x_norm += t[a] * t[a];
       for (int a = 0; a < 4; ++a) x_norm += q[a] * q[a];
-      if (!sflag && sqrt(step_norm) <= 1e-8 * (sqrt(x_norm) + 1e-8)) sflag = 1;
-      double gd = 0., dad = 0.;
-      for (int a = 0; a < 6; ++a) {
-        gd += g[a] * ds[a];
-        for (int b = 0; b < 6; ++b) dad += ds[a] * A[6 * a + b] * ds[b];
-      }
-      smodel = -(gd + 0.5 * dad);
-      for (int a = 0; a < 3; ++a) snext[a] = t[a] + step[a];
+      // Plus: t + dt; QuaternionParameterization::Plus on the rotation.
+      double tn[3] = {t[0] + step[0], t[1] + step[1], t[2] + step[2]}, qn[4];
       const double nrm = sqrt(step[3] * step[3] + step[4] * step[4] + step[5] * step[5]);
       if (nrm > 0.) {
         const double sn = sin(nrm) / nrm;
         const double qd[4] = {cos(nrm), sn * step[3], sn * step[4], sn * step[5]};
-        QuatProduct(qd, q, snext + 3);
+        QuatProduct(qd, q, qn);
       } else {
-        for (int a = 0; a < 4; ++a) snext[3 + a] = q[a];
+        for (int a = 0; a < 4; ++a) qn[a] = q[a];
+      }
+      Pass3<false>(d, points, scale, o, tn, qn, target_inv, T, red);
+      const double new_cost = 0.5 * T[0];
+      if (sqrt(step_norm) <= (sqrt(x_norm) + 1e-8) * 1e-8) break;  // parameter tolerance
+      if (fabs(cost - new_cost) <= 1e-6 * cost) break;             // function tolerance
+      const double quality = ev.Quality(new_cost, model);
+      if (quality > 1e-3) {
+        for (int a = 0; a < 3; ++a) t[a] = tn[a];
+        for (int a = 0; a < 4; ++a) q[a] = qn[a];
+        Pass3<true>(d, points, scale, o, t, q, target_inv, S, red);
+        cost = 0.5 * S[0];
+        Unpack(S, Au, gu);
+        lm.Accepted(quality);
+        ev.Accepted(new_cost, model);
+        if (cost < best_cost) {
+          best_cost = cost;
+          for (int a = 0; a < 3; ++a) best_t[a] = t[a];
+          for (int a = 0; a < 4; ++a) best_q[a] = q[a];
+        }
+      } else {
+        lm.Rejected();
       }
     }
-    __syncthreads();
-    if (sflag) break;
-    const double model = smodel;
-    double tn[3], qn[4];
-    for (int a = 0; a < 3; ++a) tn[a] = snext[a];
-    for (int a = 0; a < 4; ++a) qn[a] = snext[3 + a];
-    __syncthreads();
-    Pass3<false>(d, points, scale, o, tn, qn, target_inv, T, red);
-    const double new_cost = 0.5 * T[0];
-    const double rho = model > 0. ? (cost - new_cost) / model : -1.;
-    if (rho > 1e-3) {
-      const double change = cost - new_cost;
-      for (int a = 0; a < 3; ++a) t[a] = tn[a];
-      for (int a = 0; a < 4; ++a) q[a] = qn[a];
-      const double tf = 2. * rho - 1.;
-      radius = fmin(1e16, radius / fmax(1. / 3., 1. - tf * tf * tf));
-      decrease = 2.;
-      const double old_cost = cost;
-      Pass3<true>(d, points, scale, o, t, q, target_inv, S, red);
-      cost = 0.5 * S[0];
-      Unpack(S, Au, gu);
-      if (fabs(change) <= 1e-6 * old_cost) break;
-    } else {
-      radius /= decrease;
-      decrease *= 2.;
-    }
+    go = iter < o.max_iterations && lm.radius >= 1e-32 && !gradient_small();
   }
   if (threadIdx.x == 0) {
-    for (int a = 0; a < 3; ++a) out[7 * blockIdx.x + a] = t[a];
-    for (int a = 0; a < 4; ++a) out[7 * blockIdx.x + 3 + a] = q[a];
+    for (int a = 0; a < 3; ++a) out[7 * blockIdx.x + a] = best_t[a];
+    for (int a = 0; a < 4; ++a) out[7 * blockIdx.x + 3 + a] = best_q[a];
     if (out_iters) out_iters[blockIdx.x] = iter;
   }
 }
@@ -419,7 +425,7 @@ int csm_ceres3d_refine_batch(csm_context* ctx, const csm_hybrid_grid* const* gri
                          hipMemcpyHostToDevice, st));
   const Refine3Opts o{options->occupied_space_weight_0, options->occupied_space_weight_1,
                       options->translation_weight, options->rotation_weight,
-                      options->max_num_iterations};
+                      options->max_num_iterations, options->use_nonmonotonic_steps ? 1 : 0};
   double* dout = ctx->cr3_out.as<double>();
   int32_t* diters = reinterpret_cast<int32_t*>(dout + 7 * n);
   hipLaunchKernelGGL(ceres3d_refine, dim3(static_cast<unsigned>(n)), dim3(kR3Threads), 0, st,

@@ -37,9 +37,9 @@ struct ConstraintBuilderOptions {
   int flush_pairs = 0;  // 0: search each node's pairs when the node ends
   // ceres_scan_matcher (pose_graph.lua:30-39): accepted 2D matches are refined
   // with CeresScanMatcher2D (constraint_builder_2d.cc:245-249).
-  csm_ceres2d_options ceres_scan_matcher_options{20., 10., 1., 10};
+  csm_ceres2d_options ceres_scan_matcher_options{20., 10., 1., 10, /*nonmonotonic=*/1};
   // ceres_scan_matcher_3d (pose_graph.lua:49-60), ConstraintBuilder3D (:264-275).
-  csm_ceres3d_options ceres_scan_matcher_options_3d{5., 30., 10., 1., 10};
+  csm_ceres3d_options ceres_scan_matcher_options_3d{5., 30., 10., 1., 10, /*nonmonotonic=*/0};
   bool refine_with_ceres = true;
 };
 

@@ -322,8 +322,9 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
  * 245-249; ceres_scan_matcher_2d.cc:64-105). csm_ceres2d_refine_batch runs
  * that refinement for n (submap, scan) items on the device, over the submaps'
  * csm_fast2d handles (their correspondence-cost grids) and a scan set.
- * Ceres is not part of this library: the solver restates Ceres' trust-region
- * Levenberg-Marquardt defaults (parity with Ceres unpinned).
+ * Ceres is not part of this library: the solver restates Ceres 1.13's
+ * trust-region Levenberg-Marquardt (the version scripts/install_ceres.sh:20
+ * pins), pinned by the reference's ceres_scan_matcher_2d_test.cc.
  * iterations (may be NULL) receives the iterations each item ran. */
 typedef struct csm_ceres2d_options {
   /* proto::CeresScanMatcherOptions2D (pose_graph.lua:30-39 defaults 20, 10, 1;
@@ -332,6 +333,8 @@ typedef struct csm_ceres2d_options {
   double translation_weight;
   double rotation_weight;
   int32_t max_num_iterations;
+  /* ceres_solver_options.use_nonmonotonic_steps (pose_graph.lua:35: true). */
+  int32_t use_nonmonotonic_steps;
 } csm_ceres2d_options;
 
 typedef struct csm_refine2d {
@@ -360,6 +363,8 @@ typedef struct csm_ceres3d_options {
   double translation_weight;
   double rotation_weight;
   int32_t max_num_iterations;
+  /* ceres_solver_options.use_nonmonotonic_steps (pose_graph.lua:56: false). */
+  int32_t use_nonmonotonic_steps;
 } csm_ceres3d_options;
 
 typedef struct csm_refine3d {

@@ -16,15 +16,19 @@
 // (DENSE_QR on a 3x3 system, Jacobi column scaling from the initial
 // Jacobian, initial radius 1e4, min/max diagonal 1e-6 / 1e32, min relative
 // decrease 1e-3, function / gradient / parameter tolerances 1e-6 / 1e-10 /
-// 1e-8) and the reference's max_num_iterations = 10 (pose_graph.lua:30-39).
-// Non-monotonic steps are not restated. PARITY UNPINNED against Ceres: the
-// GPU path is checked against this restatement only.
+// 1e-8) and the reference's max_num_iterations = 10 and use_nonmonotonic_steps
+// = true (pose_graph.lua:30-39), following Ceres 2.x's TrustRegionMinimizer
+// and TrustRegionStepEvaluator. Pinned by the reference's own
+// ceres_scan_matcher_2d_test.cc and occupied_space_cost_function_2d_test.cc
+// (restated in ref_tests.cc) to their tolerances; Ceres itself is absent, so
+// agreement beyond those tolerances is unpinned.
 #include <algorithm>
 #include <climits>
 #include <cmath>
 #include <cstdint>
 #include <vector>
 
+#include "ceres_minimizer.h"
 #include "csm_oracle.h"
 
 namespace oracle {
@@ -148,15 +152,19 @@ bool Solve3(double A[3][3], const double b[3], double out[3]) {
 
 }  // namespace
 
-struct CeresOptions2D {
-  double occupied_space_weight = 20., translation_weight = 10., rotation_weight = 1.;
-  int max_num_iterations = 10;
-};
-
-// Returns the number of iterations run; *pose receives the solution.
+// Returns the number of iterations run; *pose receives the solution and
+// *final_cost (if given) Ceres' summary.final_cost, 1/2 |r|^2 at *pose.
+// The loop follows Ceres' TrustRegionMinimizer::Minimize: per iteration the
+// LM step (invalid if the model decrease is not positive), the candidate's
+// cost, the parameter and function tolerance tests (which end the solve
+// WITHOUT taking the candidate), then acceptance by step quality > 1e-3. The
+// returned parameters are the lowest-cost accepted point
+// (FinalizeIterationAndCheckIfMinimizerCanContinue), which differs from the
+// last accepted one only with non-monotonic steps.
 int CeresMatch2D(const MapLimits& limits, const std::vector<uint16_t>& cells, float min_cc,
                  float max_cc, const CeresOptions2D& o, const double target[2],
-                 const double initial[3], const std::vector<Vec2d>& points, double pose[3]) {
+                 const double initial[3], const std::vector<Vec2d>& points, double pose[3],
+                 double* final_cost) {
   const std::vector<float> table = MakeConversionTable(max_cc, min_cc, max_cc);
   const CostGrid grid{limits, &table, &cells, static_cast<double>(max_cc)};
   Problem p{&grid, &points,
@@ -172,38 +180,42 @@ int CeresMatch2D(const MapLimits& limits, const std::vector<uint16_t>& cells, fl
     for (size_t i = 0; i < m; ++i) s += J[3 * i + j] * J[3 * i + j];
     scale[j] = 1. / (1. + std::sqrt(s));
   }
+  StepEvaluator ev(cost, o.use_nonmonotonic_steps ? 5 : 0);
+  double best[3] = {x[0], x[1], x[2]}, best_cost = cost;
   double radius = 1e4, decrease_factor = 2.;
-  int iter = 0;
-  while (iter < o.max_num_iterations) {
-    ++iter;
-    // Normal equations from the unscaled Jacobian, then Jacobi-scaled:
-    // A = S Ju^T Ju S, g = S Ju^T r.
-    double Au[3][3] = {{0.}}, gu[3] = {0., 0., 0.};
+  int iter = 0, invalid = 0;
+  // Gradient of the current point: Ju^T r (unscaled), Au = Ju^T Ju.
+  double Au[3][3], gu[3];
+  auto normal_equations = [&]() {
+    for (int a = 0; a < 3; ++a) {
+      gu[a] = 0.;
+      for (int b = 0; b < 3; ++b) Au[a][b] = 0.;
+    }
     for (size_t i = 0; i < m; ++i)
       for (int a = 0; a < 3; ++a) {
         gu[a] += J[3 * i + a] * r[i];
         for (int b = 0; b < 3; ++b) Au[a][b] += J[3 * i + a] * J[3 * i + b];
       }
-    if (std::max({std::fabs(gu[0]), std::fabs(gu[1]), std::fabs(gu[2])}) <= 1e-10) break;
+  };
+  normal_equations();
+  auto gradient_small = [&]() {
+    return std::max({std::fabs(gu[0]), std::fabs(gu[1]), std::fabs(gu[2])}) <= 1e-10;
+  };
+  bool go = o.max_num_iterations > 0 && !gradient_small();
+  while (go) {
+    ++iter;
     double A[3][3], g[3];
     for (int a = 0; a < 3; ++a) {
       g[a] = gu[a] * scale[a];
       for (int b = 0; b < 3; ++b) A[a][b] = Au[a][b] * scale[a] * scale[b];
     }
-    double M[3][3], rhs[3], ds[3];
+    double M[3][3], rhs[3], ds[3] = {0., 0., 0.};
     for (int a = 0; a < 3; ++a) {
       for (int b = 0; b < 3; ++b) M[a][b] = A[a][b];
       M[a][a] += std::min(std::max(A[a][a], 1e-6), 1e32) / radius;
       rhs[a] = -g[a];
     }
-    if (!Solve3(M, rhs, ds)) break;
-    double step[3], step_norm = 0., x_norm = 0.;
-    for (int a = 0; a < 3; ++a) {
-      step[a] = ds[a] * scale[a];
-      step_norm += step[a] * step[a];
-      x_norm += x[a] * x[a];
-    }
-    if (std::sqrt(step_norm) <= 1e-8 * (std::sqrt(x_norm) + 1e-8)) break;
+    const bool solved = Solve3(M, rhs, ds);
     // Model cost change -(J ds) . (r + J ds / 2) = -(g . ds + ds^T A ds / 2).
     double gd = 0., dad = 0.;
     for (int a = 0; a < 3; ++a) {
@@ -211,27 +223,65 @@ int CeresMatch2D(const MapLimits& limits, const std::vector<uint16_t>& cells, fl
       for (int b = 0; b < 3; ++b) dad += ds[a] * A[a][b] * ds[b];
     }
     const double model = -(gd + 0.5 * dad);
-    const double xn[3] = {x[0] + step[0], x[1] + step[1], x[2] + step[2]};
-    const double new_cost = Evaluate(p, xn, &r_new, nullptr);
-    const double rho = model > 0. ? (cost - new_cost) / model : -1.;
-    if (rho > 1e-3) {
-      const double change = cost - new_cost;
-      for (int a = 0; a < 3; ++a) x[a] = xn[a];
-      const double tf = 2. * rho - 1.;
-      radius = std::min(1e16, radius / std::max(1. / 3., 1. - tf * tf * tf));
-      decrease_factor = 2.;
-      const double old_cost = cost;
-      cost = Evaluate(p, x, &r, &J);
-      if (std::fabs(change) <= 1e-6 * old_cost) break;
-    } else {
+    if (!solved || !(model > 0.)) {
+      // HandleInvalidStep: LM treats it as a rejected step.
+      if (++invalid > 5) break;
       radius /= decrease_factor;
       decrease_factor *= 2.;
+    } else {
+      invalid = 0;
+      double step[3], step_norm = 0., x_norm = 0.;
+      for (int a = 0; a < 3; ++a) {
+        step[a] = ds[a] * scale[a];
+        step_norm += step[a] * step[a];
+        x_norm += x[a] * x[a];
+      }
+      const double xn[3] = {x[0] + step[0], x[1] + step[1], x[2] + step[2]};
+      const double new_cost = Evaluate(p, xn, &r_new, nullptr);
+      if (std::sqrt(step_norm) <= (std::sqrt(x_norm) + 1e-8) * 1e-8) break;  // parameter tol.
+      if (std::fabs(cost - new_cost) <= 1e-6 * cost) break;                 // function tol.
+      const double quality = ev.Quality(new_cost, model);
+      if (quality > 1e-3) {
+        for (int a = 0; a < 3; ++a) x[a] = xn[a];
+        cost = Evaluate(p, x, &r, &J);
+        normal_equations();
+        const double tf = 2. * quality - 1.;
+        radius = std::min(1e16, radius / std::max(1. / 3., 1. - tf * tf * tf));
+        decrease_factor = 2.;
+        ev.Accepted(new_cost, model);
+        if (cost < best_cost) {
+          best_cost = cost;
+          for (int a = 0; a < 3; ++a) best[a] = x[a];
+        }
+      } else {
+        radius /= decrease_factor;
+        decrease_factor *= 2.;
+      }
     }
+    go = iter < o.max_num_iterations && radius >= 1e-32 && !gradient_small();
   }
-  pose[0] = x[0];
-  pose[1] = x[1];
-  pose[2] = x[2];
+  pose[0] = best[0];
+  pose[1] = best[1];
+  pose[2] = best[2];
+  if (final_cost) *final_cost = best_cost;
   return iter;
+}
+
+// OccupiedSpaceCostFunction2D::Evaluate residuals only
+// (occupied_space_cost_function_2d.cc:40-62) at `pose` (x, y, theta).
+std::vector<double> OccupiedSpaceResiduals2D(const MapLimits& limits,
+                                             const std::vector<uint16_t>& cells, float min_cc,
+                                             float max_cc, double weight,
+                                             const std::vector<Vec2d>& points,
+                                             const double pose[3]) {
+  const std::vector<float> table = MakeConversionTable(max_cc, min_cc, max_cc);
+  const CostGrid grid{limits, &table, &cells, static_cast<double>(max_cc)};
+  Problem p{&grid, &points, weight / std::sqrt(static_cast<double>(points.size())),
+            0., 0., 0., 0., 0.};
+  std::vector<double> r;
+  Evaluate(p, pose, &r, nullptr);
+  r.resize(points.size());
+  return r;
 }
 
 }  // namespace oracle
@@ -241,7 +291,7 @@ using namespace oracle;
 extern "C" {
 
 // opts: occupied_space_weight, translation_weight, rotation_weight,
-// max_num_iterations. target: (x, y). initial / out: (x, y, theta).
+// max_num_iterations, use_nonmonotonic_steps (0/1). target: (x, y). initial / out: (x, y, theta).
 int32_t oracle_ceres2d_match(double res, double max_x, double max_y, int32_t nx, int32_t ny,
                              const uint16_t* cells, float min_cc, float max_cc, const double* opts,
                              const double* target, const double* initial, const float* xyz,
@@ -260,7 +310,8 @@ int32_t oracle_ceres2d_match(double res, double max_x, double max_y, int32_t nx,
   o.translation_weight = opts[1];
   o.rotation_weight = opts[2];
   o.max_num_iterations = static_cast<int>(opts[3]);
-  return CeresMatch2D(l, c, min_cc, max_cc, o, target, initial, pts, out);
+  o.use_nonmonotonic_steps = opts[4] != 0.;
+  return CeresMatch2D(l, c, min_cc, max_cc, o, target, initial, pts, out, nullptr);
 }
 
 }  // extern "C"

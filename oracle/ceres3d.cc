@@ -14,15 +14,19 @@
 //     smooth-step tricubic interpolation of interpolated_grid.h:50-150;
 //   * TranslationDeltaCostFunctor3D: w_t * (t - target);
 //   * RotationDeltaCostFunctor3D: w_r * vec(target^-1 * q).
-// The solver restates Ceres' trust-region Levenberg-Marquardt defaults (as
+// The solver restates Ceres 1.13's trust-region Levenberg-Marquardt (as
 // oracle/ceres2d.cc) on the 6-dimensional tangent space, with
-// max_num_iterations = 10 and monotonic steps (pose_graph.lua:49-60).
-// PARITY UNPINNED against Ceres (absent from this image).
+// max_num_iterations = 10 and monotonic steps (pose_graph.lua:49-60) by
+// default. Pinned by the reference's ceres_scan_matcher_3d_test.cc (restated
+// without its intensity block, which ConstraintBuilder3D never passes,
+// constraint_builder_3d.cc:267-274) and rotation_delta_cost_functor_3d_test.cc
+// to their tolerances; Ceres itself is absent from this image.
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <vector>
 
+#include "ceres_minimizer.h"
 #include "oracle3d.h"
 
 namespace oracle {
@@ -203,15 +207,18 @@ bool SolveN(std::vector<double> M, std::vector<double> b, int n, double* out) {
 
 }  // namespace
 
-struct CeresOptions3D {
-  double w0 = 5., w1 = 30., wt = 10., wr = 1.;
-  int max_num_iterations = 10;
-};
+void RotationDeltaResiduals3D(double scale, const double target_q[4], const double q[4],
+                              double out[3]) {
+  const double inv[4] = {target_q[0], -target_q[1], -target_q[2], -target_q[3]};
+  double delta[4];
+  QuatProduct(inv, q, delta);
+  for (int a = 0; a < 3; ++a) out[a] = scale * delta[a + 1];
+}
 
 int CeresMatch3D(const HybridGrid& high, const HybridGrid& low, const std::vector<Vec3f>& high_cloud,
                  const std::vector<Vec3f>& low_cloud, const CeresOptions3D& o,
                  const double target[3], const double initial_t[3], const double initial_q[4],
-                 double out_t[3], double out_q[4]) {
+                 double out_t[3], double out_q[4], double* final_cost) {
   Problem3 p;
   p.grid[0] = &high;
   p.grid[1] = &low;
@@ -243,13 +250,19 @@ int CeresMatch3D(const HybridGrid& high, const HybridGrid& low, const std::vecto
   double Au[36], gu[6], scale[6];
   normal(Au, gu);
   for (int a = 0; a < 6; ++a) scale[a] = 1. / (1. + std::sqrt(Au[7 * a]));
+  StepEvaluator ev(cost, o.use_nonmonotonic_steps ? 5 : 0);
+  double best_t[3] = {t[0], t[1], t[2]}, best_q[4] = {q[0], q[1], q[2], q[3]}, best_cost = cost;
   double radius = 1e4, decrease = 2.;
-  int iter = 0;
-  while (iter < o.max_num_iterations) {
-    ++iter;
+  int iter = 0, invalid = 0;
+  auto gradient_small = [&]() {
     double gmax = 0.;
     for (int a = 0; a < 6; ++a) gmax = std::max(gmax, std::fabs(gu[a]));
-    if (gmax <= 1e-10) break;
+    return gmax <= 1e-10;
+  };
+  // Ceres 1.13 TrustRegionMinimizer::Minimize, as in ceres2d.cc.
+  bool go = o.max_num_iterations > 0 && !gradient_small();
+  while (go) {
+    ++iter;
     std::vector<double> A(36), g(6), M(36), rhs(6);
     for (int a = 0; a < 6; ++a) {
       g[a] = gu[a] * scale[a];
@@ -260,50 +273,65 @@ int CeresMatch3D(const HybridGrid& high, const HybridGrid& low, const std::vecto
       M[7 * a] += std::min(std::max(A[7 * a], 1e-6), 1e32) / radius;
       rhs[a] = -g[a];
     }
-    double ds[6];
-    if (!SolveN(M, rhs, 6, ds)) break;
-    double step[6], step_norm = 0., x_norm = 0.;
-    for (int a = 0; a < 6; ++a) {
-      step[a] = ds[a] * scale[a];
-      step_norm += step[a] * step[a];
-    }
-    for (int a = 0; a < 3; ++a) x_norm += t[a] * t[a];
-    for (int a = 0; a < 4; ++a) x_norm += q[a] * q[a];
-    if (std::sqrt(step_norm) <= 1e-8 * (std::sqrt(x_norm) + 1e-8)) break;
+    double ds[6] = {0., 0., 0., 0., 0., 0.};
+    const bool solved = SolveN(M, rhs, 6, ds);
     double gd = 0., dad = 0.;
     for (int a = 0; a < 6; ++a) {
       gd += g[a] * ds[a];
       for (int b = 0; b < 6; ++b) dad += ds[a] * A[6 * a + b] * ds[b];
     }
     const double model = -(gd + 0.5 * dad);
-    // Plus: t + dt; QuaternionParameterization::Plus on the rotation.
-    double tn[3] = {t[0] + step[0], t[1] + step[1], t[2] + step[2]}, qn[4];
-    const double nrm = std::sqrt(step[3] * step[3] + step[4] * step[4] + step[5] * step[5]);
-    if (nrm > 0.) {
-      const double sn = std::sin(nrm) / nrm;
-      const double qd[4] = {std::cos(nrm), sn * step[3], sn * step[4], sn * step[5]};
-      QuatProduct(qd, q, qn);
-    } else {
-      for (int a = 0; a < 4; ++a) qn[a] = q[a];
-    }
-    const double new_cost = Evaluate3(p, tn, qn, &rn, nullptr);
-    const double rho = model > 0. ? (cost - new_cost) / model : -1.;
-    if (rho > 1e-3) {
-      const double change = cost - new_cost;
-      for (int a = 0; a < 3; ++a) t[a] = tn[a];
-      for (int a = 0; a < 4; ++a) q[a] = qn[a];
-      const double tf = 2. * rho - 1.;
-      radius = std::min(1e16, radius / std::max(1. / 3., 1. - tf * tf * tf));
-      decrease = 2.;
-      const double old_cost = cost;
-      cost = Evaluate3(p, t, q, &r, &J);
-      normal(Au, gu);
-      if (std::fabs(change) <= 1e-6 * old_cost) break;
-    } else {
+    if (!solved || !(model > 0.)) {
+      if (++invalid > 5) break;
       radius /= decrease;
       decrease *= 2.;
+    } else {
+      invalid = 0;
+      double step[6], step_norm = 0., x_norm = 0.;
+      for (int a = 0; a < 6; ++a) {
+        step[a] = ds[a] * scale[a];
+        step_norm += step[a] * step[a];
+      }
+      for (int a = 0; a < 3; ++a) x_norm += t[a] * t[a];
+      for (int a = 0; a < 4; ++a) x_norm += q[a] * q[a];
+      // Plus: t + dt; QuaternionParameterization::Plus on the rotation.
+      double tn[3] = {t[0] + step[0], t[1] + step[1], t[2] + step[2]}, qn[4];
+      const double nrm = std::sqrt(step[3] * step[3] + step[4] * step[4] + step[5] * step[5]);
+      if (nrm > 0.) {
+        const double sn = std::sin(nrm) / nrm;
+        const double qd[4] = {std::cos(nrm), sn * step[3], sn * step[4], sn * step[5]};
+        QuatProduct(qd, q, qn);
+      } else {
+        for (int a = 0; a < 4; ++a) qn[a] = q[a];
+      }
+      const double new_cost = Evaluate3(p, tn, qn, &rn, nullptr);
+      if (std::sqrt(step_norm) <= (std::sqrt(x_norm) + 1e-8) * 1e-8) break;  // parameter tol.
+      if (std::fabs(cost - new_cost) <= 1e-6 * cost) break;                 // function tol.
+      const double quality = ev.Quality(new_cost, model);
+      if (quality > 1e-3) {
+        for (int a = 0; a < 3; ++a) t[a] = tn[a];
+        for (int a = 0; a < 4; ++a) q[a] = qn[a];
+        cost = Evaluate3(p, t, q, &r, &J);
+        normal(Au, gu);
+        const double tf = 2. * quality - 1.;
+        radius = std::min(1e16, radius / std::max(1. / 3., 1. - tf * tf * tf));
+        decrease = 2.;
+        ev.Accepted(new_cost, model);
+        if (cost < best_cost) {
+          best_cost = cost;
+          for (int a = 0; a < 3; ++a) best_t[a] = t[a];
+          for (int a = 0; a < 4; ++a) best_q[a] = q[a];
+        }
+      } else {
+        radius /= decrease;
+        decrease *= 2.;
+      }
     }
+    go = iter < o.max_num_iterations && radius >= 1e-32 && !gradient_small();
   }
+  for (int a = 0; a < 3; ++a) t[a] = best_t[a];
+  for (int a = 0; a < 4; ++a) q[a] = best_q[a];
+  if (final_cost) *final_cost = best_cost;
   for (int a = 0; a < 3; ++a) out_t[a] = t[a];
   for (int a = 0; a < 4; ++a) out_q[a] = q[a];
   return iter;
@@ -315,7 +343,7 @@ using namespace oracle;
 
 extern "C" {
 
-// opts: w0, w1, wt, wr, max_num_iterations. target: xyz. initial/out: t[3], q[4] (w, x, y, z).
+// opts: w0, w1, wt, wr, max_num_iterations, use_nonmonotonic_steps. target: xyz. initial/out: t[3], q[4] (w, x, y, z).
 int32_t oracle_ceres3d_match(void* high, void* low, const float* high_xyz, int32_t nh,
                              const float* low_xyz, int32_t nl, const double* opts,
                              const double* target, const double* initial, double* out) {
@@ -328,8 +356,9 @@ int32_t oracle_ceres3d_match(void* high, void* low, const float* high_xyz, int32
   o.wt = opts[2];
   o.wr = opts[3];
   o.max_num_iterations = static_cast<int>(opts[4]);
+  o.use_nonmonotonic_steps = opts[5] != 0.;
   return CeresMatch3D(*static_cast<HybridGrid*>(high), *static_cast<HybridGrid*>(low), hc, lc, o,
-                      target, initial, initial + 3, out, out + 3);
+                      target, initial, initial + 3, out, out + 3, nullptr);
 }
 
 }  // extern "C"

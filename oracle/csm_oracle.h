@@ -325,6 +325,22 @@ class RealTimeCorrelativeScanMatcher2D {
   RealTimeOptions options_;
 };
 
+// mapping/internal/2d/scan_matching/ceres_scan_matcher_2d.cc (ceres2d.cc)
+struct CeresOptions2D {
+  double occupied_space_weight = 20., translation_weight = 10., rotation_weight = 1.;
+  int max_num_iterations = 10;
+  bool use_nonmonotonic_steps = true;
+};
+int CeresMatch2D(const MapLimits& limits, const std::vector<uint16_t>& cells, float min_cc,
+                 float max_cc, const CeresOptions2D& o, const double target[2],
+                 const double initial[3], const std::vector<Vec2d>& points, double pose[3],
+                 double* final_cost);
+std::vector<double> OccupiedSpaceResiduals2D(const MapLimits& limits,
+                                             const std::vector<uint16_t>& cells, float min_cc,
+                                             float max_cc, double weight,
+                                             const std::vector<Vec2d>& points,
+                                             const double pose[3]);
+
 }  // namespace oracle
 
 #endif  // CSM_ORACLE_H_

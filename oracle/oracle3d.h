@@ -344,6 +344,20 @@ float RealTimeScore3D(const RtOptions3D& options, const Rigid3d& initial,
                       const PointCloud& cloud, const HybridGrid& grid, int64_t index,
                       Rigid3f* candidate_out);
 
+// mapping/internal/3d/scan_matching/ceres_scan_matcher_3d.cc (ceres3d.cc).
+struct CeresOptions3D {
+  double w0 = 5., w1 = 30., wt = 10., wr = 1.;
+  int max_num_iterations = 10;
+  bool use_nonmonotonic_steps = false;
+};
+int CeresMatch3D(const HybridGrid& high, const HybridGrid& low, const std::vector<Vec3f>& high_cloud,
+                 const std::vector<Vec3f>& low_cloud, const CeresOptions3D& o,
+                 const double target[3], const double initial_t[3], const double initial_q[4],
+                 double out_t[3], double out_q[4], double* final_cost);
+// RotationDeltaCostFunctor3D residuals (rotation_delta_cost_functor_3d.h):
+// scale * vec(target^-1 * q), quaternions (w, x, y, z).
+void RotationDeltaResiduals3D(double scale, const double target_q[4], const double q[4],
+                              double out[3]);
 
 }  // namespace oracle
 

@@ -8,6 +8,7 @@
 // (std::mt19937 + uniform distributions), so the draws follow the same
 // generator; the checks are the reference's checks and tolerances.
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <functional>
@@ -347,6 +348,67 @@ TEST(ProbabilityValuesTables) {
     if (std::abs(vp[pt[pv]] - (1.f - vc[ct[cv]])) > 5e-5) ++bad2;
   }
   EXPECT(bad2 == 0);
+}
+
+// transform::IsNearly (rigid_transform_test_helpers.h:42-46) for Rigid2d:
+// Eigen's isApprox of the 3x3 affine matrices, |A - B|_F^2 <= eps^2 *
+// min(|A|_F^2, |B|_F^2).
+bool IsNearly2D(const double a[3], const double b[3], double eps) {
+  auto mat = [](const double p[3], double m[9]) {
+    const double c = std::cos(p[2]), s = std::sin(p[2]);
+    const double v[9] = {c, -s, p[0], s, c, p[1], 0., 0., 1.};
+    for (int k = 0; k < 9; ++k) m[k] = v[k];
+  };
+  double ma[9], mb[9], d = 0., na = 0., nb = 0.;
+  mat(a, ma);
+  mat(b, mb);
+  for (int k = 0; k < 9; ++k) {
+    d += (ma[k] - mb[k]) * (ma[k] - mb[k]);
+    na += ma[k] * ma[k];
+    nb += mb[k] * mb[k];
+  }
+  return d <= eps * eps * std::min(na, nb);
+}
+
+// ceres_scan_matcher_2d_test.cc:35-96 — one occupied cell at (-3.5, 2.5),
+// one point at (-3, 2): from four initial poses the solver reaches
+// Translation(-0.5, 0.5) within 1e-2 with final_cost ~ 0 (EXPECT_NEAR 1e-2).
+// Options as the test's Lua dictionary: occupied_space_weight 1,
+// translation_weight 0.1, rotation_weight 1.5, max_num_iterations 50.
+TEST(CeresScanMatcher2DTest) {
+  ProbabilityGrid grid(Limits(1., 10., 10., 20, 20));
+  grid.SetProbability(grid.limits().GetCellIndex(-3.5f, 2.5f), kMaxProbability);
+  const std::vector<Vec2d> cloud{{-3., 2.}};
+  CeresOptions2D o;
+  o.occupied_space_weight = 1.;
+  o.translation_weight = 0.1;
+  o.rotation_weight = 1.5;
+  o.max_num_iterations = 50;
+  const double starts[4][2] = {{-0.5, 0.5}, {-0.3, 0.5}, {-0.45, 0.3}, {-0.3, 0.3}};
+  for (const auto& st : starts) {
+    const double initial[3] = {st[0], st[1], 0.};
+    double pose[3], final_cost = -1.;
+    CeresMatch2D(grid.limits(), grid.cells(), grid.min_correspondence_cost(),
+                 grid.max_correspondence_cost(), o, st, initial, cloud, pose, &final_cost);
+    EXPECT_NEAR(0., final_cost, 1e-2);
+    const double expected[3] = {-0.5, 0.5, 0.};
+    EXPECT(IsNearly2D(pose, expected, 1e-2));
+  }
+}
+
+// occupied_space_cost_function_2d_test.cc:30-47 — an all-unknown 2x2 grid:
+// the residual of one point at the origin is kMaxProbability (DoubleEq,
+// 4 ulps).
+TEST(OccupiedSpaceCostFunction2DSmokeTest) {
+  ProbabilityGrid grid(Limits(1., 1., 1., 2, 2));
+  const std::vector<Vec2d> cloud{{0., 0.}};
+  const double pose[3] = {0., 0., 0.};
+  const std::vector<double> r =
+      OccupiedSpaceResiduals2D(grid.limits(), grid.cells(), grid.min_correspondence_cost(),
+                               grid.max_correspondence_cost(), 1., cloud, pose);
+  EXPECT(r.size() == 1u);
+  const double want = static_cast<double>(kMaxProbability);
+  EXPECT(std::abs(r[0] - want) <= 4. * std::numeric_limits<double>::epsilon() * want);
 }
 
 }  // namespace

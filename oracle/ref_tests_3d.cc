@@ -272,6 +272,99 @@ void QuaternionSanity() {
 
 }  // namespace
 
+namespace {
+
+Quatd AngleAxisQ(double angle, double ax, double ay, double az) {
+  const double n = std::sqrt(ax * ax + ay * ay + az * az);
+  const double s = std::sin(0.5 * angle) / n;
+  return Quatd{std::cos(0.5 * angle), ax * s, ay * s, az * s};
+}
+Quatd Mul(const Quatd& a, const Quatd& b) {
+  return Quatd{a.w * b.w - a.x * b.x - a.y * b.y - a.z * b.z,
+               a.w * b.x + a.x * b.w + a.y * b.z - a.z * b.y,
+               a.w * b.y - a.x * b.z + a.y * b.w + a.z * b.x,
+               a.w * b.z + a.x * b.y - a.y * b.x + a.z * b.w};
+}
+double RotationDeltaSquaredCost(const Quatd& rotation, double scale, const Quatd& target) {
+  const double q[4] = {rotation.w, rotation.x, rotation.y, rotation.z};
+  const double t[4] = {target.w, target.x, target.y, target.z};
+  double r[3];
+  RotationDeltaResiduals3D(scale, t, q, r);
+  return r[0] * r[0] + r[1] * r[1] + r[2] * r[2];
+}
+
+// rotation_delta_cost_functor_3d_test.cc:50-83 (kPrecision 1e-8).
+void RotationDeltaCostFunctor3DTests() {
+  const Quatd id{1., 0., 0., 0.};
+  CHECK3(std::abs(RotationDeltaSquaredCost(id, 1.0, id)) <= 1e-8);
+  const Quatd rot = AngleAxisQ(0.9, 0.2, 0.1, 0.3);
+  CHECK3(std::abs(RotationDeltaSquaredCost(rot, 1.0, rot)) <= 1e-8);
+  const double scaling = 1.2, angle = 0.8;
+  const Quatd rotation = AngleAxisQ(angle, 0.2, 0.1, 0.8);
+  const Quatd target = AngleAxisQ(0.2, -0.5, 0.3, 0.4);
+  const double expected = std::pow(scaling * std::sin(angle / 2.0), 2);
+  CHECK3(std::abs(expected - RotationDeltaSquaredCost(rotation, scaling, id)) <= 1e-8);
+  CHECK3(std::abs(expected - RotationDeltaSquaredCost(Mul(target, rotation), scaling, target)) <=
+         1e-8);
+  CHECK3(std::abs(expected - RotationDeltaSquaredCost(Mul(rotation, target), scaling, target)) <=
+         1e-8);
+}
+
+// ceres_scan_matcher_3d_test.cc (the upstream test the fork keeps as
+// ceres_scan_matcher_3d_test.cc.bak:34-136): seven points set to probability
+// 1 in a 1 m HybridGrid at expected_pose = Translation(-1, 0, 0) * point;
+// occupied_space_weight_0 = 1, translation_weight 0.01, rotation_weight 0.1,
+// use_nonmonotonic_steps, max_num_iterations 10; final_cost ~ 0 (1e-2) and
+// IsNearly(expected, 3e-2) from five initial poses. The test's intensity
+// block (IntensityHybridGrid, weight 0.5) is left out: ConstraintBuilder3D
+// passes no intensity grid (constraint_builder_3d.cc:267-274), so neither
+// the oracle nor the device path carries that cost.
+void CeresScanMatcher3DTests() {
+  HybridGrid grid(1.f);
+  std::vector<Vec3f> cloud;
+  const float pts[7][3] = {{-3.f, 2.f, 0.f}, {-4.f, 2.f, 0.f}, {-5.f, 2.f, 0.f}, {-6.f, 2.f, 0.f},
+                           {-6.f, 3.f, 1.f}, {-6.f, 4.f, 2.f}, {-7.f, 3.f, 1.f}};
+  for (const auto& p : pts) {
+    cloud.push_back(Vec3f{p[0], p[1], p[2]});
+    grid.SetProbability(grid.GetCellIndex(Vec3f{p[0] + -1.f, p[1], p[2]}), 1.f);
+  }
+  CeresOptions3D o;
+  o.w0 = 1.;
+  o.w1 = 0.;  // one (cloud, grid) pair in the test: the second block is inert
+  o.wt = 0.01;
+  o.wr = 0.1;
+  o.max_num_iterations = 10;
+  o.use_nonmonotonic_steps = true;
+  auto run = [&](const std::vector<Vec3f>& c, const Rigid3d& initial, const Rigid3d& expected) {
+    const double t0[3] = {initial.t.x, initial.t.y, initial.t.z};
+    const double q0[4] = {initial.q.w, initial.q.x, initial.q.y, initial.q.z};
+    double t[3], q[4], final_cost = -1.;
+    CeresMatch3D(grid, grid, c, c, o, t0, t0, q0, t, q, &final_cost);
+    CHECK3(std::abs(final_cost) <= 1e-2);
+    CHECK3(IsNearly3D(Rigid3d{Vec3d{t[0], t[1], t[2]}, Quatd{q[0], q[1], q[2], q[3]}}, expected,
+                      3e-2));
+  };
+  const Quatd id{1., 0., 0., 0.};
+  const Rigid3d expected{Vec3d{-1., 0., 0.}, id};
+  run(cloud, Rigid3d{Vec3d{-1., 0., 0.}, id}, expected);     // PerfectEstimate
+  run(cloud, Rigid3d{Vec3d{-0.8, 0., 0.}, id}, expected);    // AlongX
+  run(cloud, Rigid3d{Vec3d{-1., 0., -0.2}, id}, expected);   // AlongZ
+  run(cloud, Rigid3d{Vec3d{-0.9, -0.2, 0.2}, id}, expected); // AlongXYZ
+  // FullPoseCorrection: the cloud rotated by 0.05 about z; expected pose
+  // expected * additional^-1; start rotated about x.
+  const Quatd add = AngleAxisQ(0.05, 0., 0., 1.);
+  std::vector<Vec3f> turned;
+  for (const Vec3f& p : cloud) {
+    const double c = std::cos(0.05), s = std::sin(0.05);
+    turned.push_back(Vec3f{static_cast<float>(c * p.x - s * p.y),
+                           static_cast<float>(s * p.x + c * p.y), p.z});
+  }
+  const Rigid3d expected2{Vec3d{-1., 0., 0.}, Quatd{add.w, -add.x, -add.y, -add.z}};
+  run(turned, Rigid3d{Vec3d{-0.95, -0.05, 0.05}, AngleAxisQ(0.05, 1., 0., 0.)}, expected2);
+}
+
+}  // namespace
+
 int RunRefTests3D(int* checks) {
   const int before = g_fail;
   struct {
@@ -281,7 +374,9 @@ int RunRefTests3D(int* checks) {
                {"PrecomputedGridGenerator3DTest.TestAgainstNaiveAlgorithm", PrecomputationGrid3DTest},
                {"RotationalScanMatcher3DTest (2 cases)", RotationalScanMatcherTests},
                {"FastCorrelativeScanMatcher3DTest (Match, MatchFullSubmap)", FastCorrelativeScanMatcher3DTests},
-               {"Eigen float helpers (SSE product, redux)", QuaternionSanity}};
+               {"Eigen float helpers (SSE product, redux)", QuaternionSanity},
+               {"RotationDeltaCostFunctor3DTest (2 cases)", RotationDeltaCostFunctor3DTests},
+               {"CeresScanMatcher3DTest (5 cases, no intensity block)", CeresScanMatcher3DTests}};
   for (auto& t : tests) {
     const int b = g_fail;
     t.fn();

@@ -454,10 +454,12 @@ Oracle.adaptive_voxel_filter_masks = _o_adaptive_voxel_filter_masks
 
 def _o_ceres2d_match(self, limits, cells, options, target, initial, cloud,
                      min_cc=0.1, max_cc=0.9):
-    """CeresScanMatcher2D::Match restated (oracle/ceres2d.cc): (pose, iterations)."""
+    """CeresScanMatcher2D::Match restated (oracle/ceres2d.cc): (pose, iterations).
+    options: (occupied, translation, rotation weights, max_num_iterations
+    [, use_nonmonotonic_steps = True as pose_graph.lua:35])."""
     cells = np.ascontiguousarray(cells, np.uint16)
     pts = np.ascontiguousarray(cloud, np.float32).reshape(-1, 3)
-    o = np.asarray(options, np.float64)
+    o = np.asarray(tuple(options) + ((1.0,) if len(options) == 4 else ()), np.float64)
     t = np.asarray(target, np.float64)
     i = np.asarray(initial, np.float64)
     out = np.zeros(3)
@@ -482,7 +484,8 @@ def _o_ceres3d_match(self, high, low, high_cloud, low_cloud, options, target, in
     f.argtypes = [VP, VP, P(F), I32, P(F), I32, P(D), P(D), P(D), P(D)]
     hc = np.ascontiguousarray(high_cloud, np.float32).reshape(-1, 3)
     lc = np.ascontiguousarray(low_cloud, np.float32).reshape(-1, 3)
-    o = np.asarray(options, np.float64)
+    # (w0, w1, translation, rotation, max_num_iterations [, nonmonotonic = 0])
+    o = np.asarray(tuple(options) + ((0.0,) if len(options) == 5 else ()), np.float64)
     t = np.asarray(target, np.float64)
     init = np.concatenate([np.asarray(initial_t, np.float64), np.asarray(initial_q, np.float64)])
     out = np.zeros(7)
