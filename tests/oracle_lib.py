@@ -453,10 +453,17 @@ Oracle.adaptive_voxel_filter_masks = _o_adaptive_voxel_filter_masks
 
 
 def _o_ceres2d_match(self, limits, cells, options, target, initial, cloud,
-                     min_cc=0.1, max_cc=0.9):
+                     min_cc=None, max_cc=None):
     """CeresScanMatcher2D::Match restated (oracle/ceres2d.cc): (pose, iterations).
     options: (occupied, translation, rotation weights, max_num_iterations
     [, use_nonmonotonic_steps = True as pose_graph.lua:35])."""
+    # probability_values.h: kMinCorrespondenceCost = 1.f - kMaxProbability,
+    # kMaxCorrespondenceCost = 1.f - kMinProbability, in float.
+    f32 = np.float32
+    if min_cc is None:
+        min_cc = f32(1.0) - (f32(1.0) - f32(0.1))
+    if max_cc is None:
+        max_cc = f32(1.0) - f32(0.1)
     cells = np.ascontiguousarray(cells, np.uint16)
     pts = np.ascontiguousarray(cloud, np.float32).reshape(-1, 3)
     o = np.asarray(tuple(options) + ((1.0,) if len(options) == 4 else ()), np.float64)
