@@ -257,12 +257,29 @@ def rt2d_bench(csm, ctx, args):
     cloud = w.cloud(n)
     for _ in range(10):
         m.Match(init, cloud, g)
-    times = []
+    # Same grid every call (the device keeps its converted copy), then a grid
+    # that changes between calls as local SLAM's matching submap does after
+    # every insertion (one cell toggled: the whole grid is re-uploaded and
+    # re-converted).
+    g2 = csm.ProbabilityGrid(g.resolution, g.max_x, g.max_y, g.cells.copy())
+    g2.cells[0, 0] ^= 1
+    times, times_changed = [], []
+    ctx.reset_timing()
+    ctx.enable_timing(True)
     for _ in range(100):
         a = time.perf_counter()
         m.Match(init, cloud, g)
         times.append(time.perf_counter() - a)
-    res = {"gpu_ms_per_scan_match_median": 1e3 * float(np.median(times)), "points": len(cloud)}
+    ctx.enable_timing(False)
+    kernel_ms = ctx.timing().other_kernel_ms / 100
+    for k in range(100):
+        a = time.perf_counter()
+        m.Match(init, cloud, g2 if k % 2 == 0 else g)
+        times_changed.append(time.perf_counter() - a)
+    res = {"gpu_ms_per_scan_match_median": 1e3 * float(np.median(times)),
+           "gpu_ms_per_scan_match_median_grid_changed": 1e3 * float(np.median(times_changed)),
+           "kernel_ms_per_scan_match": kernel_ms,
+           "points": len(cloud)}
     try:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_lib

@@ -169,6 +169,26 @@ class AdaptiveVoxelFilterOptions(C.Structure):
         return AdaptiveVoxelFilterOptions(max_length, min_num_points, max_range)
 
 
+class LinearBounds(C.Structure):
+    """SearchParameters::LinearBounds (correlative_scan_matcher_2d.h:37-42)."""
+    _fields_ = [("min_x", C.c_int32), ("max_x", C.c_int32), ("min_y", C.c_int32),
+                ("max_y", C.c_int32)]
+
+    def as_tuple(self):
+        return (self.min_x, self.max_x, self.min_y, self.max_y)
+
+
+class SearchParametersC(C.Structure):
+    _fields_ = [("num_angular_perturbations", C.c_int32),
+                ("angular_perturbation_step_size", C.c_double), ("resolution", C.c_double),
+                ("num_scans", C.c_int32), ("num_linear_perturbations", C.c_int32)]
+
+
+class Candidate2DC(C.Structure):
+    _fields_ = [("scan_index", C.c_int32), ("x_index_offset", C.c_int32),
+                ("y_index_offset", C.c_int32), ("score", C.c_float)]
+
+
 class Pair3D(C.Structure):
     _fields_ = [("submap", C.c_int32), ("node", C.c_int32), ("full_submap", C.c_int32),
                 ("min_score", C.c_float), ("node_pose", Pose3D), ("submap_pose", Pose3D)]
@@ -210,6 +230,30 @@ _SIGNATURES = {
                                       C.POINTER(C.c_uint16), C.POINTER(C.c_uint16), C.c_float,
                                       C.c_float, C.POINTER(Pose2D), C.POINTER(C.c_float),
                                       C.c_int32, C.POINTER(C.c_double), C.POINTER(Pose2D)]),
+    "csm_search_parameters_init": (C.c_int, [C.c_double, C.c_double, C.POINTER(C.c_float),
+                                             C.c_int32, C.c_double,
+                                             C.POINTER(SearchParametersC)]),
+    "csm_search_parameters_init_for_testing": (C.c_int, [C.c_int32, C.c_int32, C.c_double,
+                                                         C.c_double,
+                                                         C.POINTER(SearchParametersC)]),
+    "csm_search_parameters_shrink_to_fit": (C.c_int, [C.POINTER(SearchParametersC),
+                                                      C.POINTER(C.c_int32), C.c_int32, C.c_int32,
+                                                      C.c_int32, C.POINTER(LinearBounds)]),
+    "csm_generate_rotated_scans": (C.c_int, [C.POINTER(C.c_float), C.c_int32,
+                                             C.POINTER(SearchParametersC), C.POINTER(C.c_float)]),
+    "csm_discretize_scans": (C.c_int, [C.POINTER(MapLimits), C.POINTER(C.c_float), C.c_int32,
+                                       C.c_int32, C.c_float, C.c_float, C.POINTER(C.c_int32)]),
+    "csm_rt2d_score_candidates": (C.c_int, [C.c_void_p, C.POINTER(RtOptions),
+                                            C.POINTER(MapLimits), C.POINTER(C.c_uint16),
+                                            C.c_float, C.c_float, C.POINTER(C.c_int32),
+                                            C.c_int32, C.c_int32, C.POINTER(SearchParametersC),
+                                            C.POINTER(Candidate2DC), C.c_int64]),
+    "csm_rt2d_score_candidates_tsdf": (C.c_int, [C.c_void_p, C.POINTER(RtOptions),
+                                                 C.POINTER(MapLimits), C.POINTER(C.c_uint16),
+                                                 C.POINTER(C.c_uint16), C.c_float, C.c_float,
+                                                 C.POINTER(C.c_int32), C.c_int32, C.c_int32,
+                                                 C.POINTER(SearchParametersC),
+                                                 C.POINTER(Candidate2DC), C.c_int64]),
     "csm_hybrid_grid_create": (C.c_int, [C.c_void_p, C.c_float, C.POINTER(C.c_int32),
                                          C.POINTER(C.c_uint16), C.c_int64, C.c_int32,
                                          C.POINTER(C.c_void_p)]),
@@ -709,6 +753,138 @@ class RealTimeCorrelativeScanMatcher2D:
                                             _ptr(pts, C.c_float), len(pts), C.byref(score),
                                             C.byref(pose)), "csm_rt2d_match")
         return float(score.value), pose.as_tuple()
+
+    def ScoreCandidates(self, grid, discrete_scans, search_parameters: "SearchParameters",
+                        candidates):
+        """real_time_correlative_scan_matcher_2d.h:75-78 (visible for testing):
+        sets ``score`` on every Candidate2D of ``candidates`` (in place; also
+        returned as a float32 array). ``discrete_scans``: (num_scans, n, 2)
+        int cell indices as DiscretizeScans returns them."""
+        d = np.ascontiguousarray(np.asarray(discrete_scans, np.int32))
+        if d.ndim != 3 or d.shape[2] != 2:
+            raise ValueError("discrete_scans must be (num_scans, points, 2)")
+        o = self.options
+        opts = RtOptions(o.linear_search_window, o.angular_search_window,
+                         o.translation_delta_cost_weight, o.rotation_delta_cost_weight)
+        lim = grid.limits()
+        arr = (Candidate2DC * max(len(candidates), 1))()
+        for i, c in enumerate(candidates):
+            arr[i].scan_index, arr[i].x_index_offset, arr[i].y_index_offset = (
+                c.scan_index, c.x_index_offset, c.y_index_offset)
+        sp = search_parameters._c
+        if isinstance(grid, TSDF2D):
+            tsd = np.ascontiguousarray(grid.tsd_cells, dtype=np.uint16)
+            wgt = np.ascontiguousarray(grid.weight_cells, dtype=np.uint16)
+            _check(self._lib.csm_rt2d_score_candidates_tsdf(
+                self.context.handle, C.byref(opts), C.byref(lim), _ptr(tsd, C.c_uint16),
+                _ptr(wgt, C.c_uint16), grid.truncation_distance, grid.max_weight,
+                _ptr(d, C.c_int32), d.shape[0], d.shape[1], C.byref(sp), arr, len(candidates)),
+                "csm_rt2d_score_candidates_tsdf")
+        else:
+            cells = np.ascontiguousarray(grid.cells, dtype=np.uint16)
+            _check(self._lib.csm_rt2d_score_candidates(
+                self.context.handle, C.byref(opts), C.byref(lim), _ptr(cells, C.c_uint16),
+                grid.min_correspondence_cost, grid.max_correspondence_cost, _ptr(d, C.c_int32),
+                d.shape[0], d.shape[1], C.byref(sp), arr, len(candidates)),
+                "csm_rt2d_score_candidates")
+        scores = np.array([arr[i].score for i in range(len(candidates))], np.float32)
+        for c, v in zip(candidates, scores):
+            c.score = float(v)
+        return scores
+
+
+class SearchParameters:
+    """correlative_scan_matcher_2d.h:35-61: SearchParameters(linear_search_window,
+    angular_search_window, point_cloud, resolution), or the testing constructor
+    ``SearchParameters.for_testing(num_linear, num_angular, step, resolution)``."""
+
+    def __init__(self, linear_search_window, angular_search_window, point_cloud,
+                 resolution, _c=None):
+        lib = load_library()
+        if _c is None:
+            pts = _f32_points(point_cloud)
+            _c = SearchParametersC()
+            _check(lib.csm_search_parameters_init(linear_search_window, angular_search_window,
+                                                  _ptr(pts, C.c_float), len(pts), resolution,
+                                                  C.byref(_c)), "csm_search_parameters_init")
+        self._c = _c
+        L = _c.num_linear_perturbations
+        self.linear_bounds = [LinearBounds(-L, L, -L, L) for _ in range(_c.num_scans)]
+
+    @staticmethod
+    def for_testing(num_linear_perturbations, num_angular_perturbations,
+                    angular_perturbation_step_size, resolution) -> "SearchParameters":
+        c = SearchParametersC()
+        _check(load_library().csm_search_parameters_init_for_testing(
+            num_linear_perturbations, num_angular_perturbations, angular_perturbation_step_size,
+            resolution, C.byref(c)), "csm_search_parameters_init_for_testing")
+        return SearchParameters(0, 0, None, resolution, _c=c)
+
+    num_angular_perturbations = property(lambda self: self._c.num_angular_perturbations)
+    angular_perturbation_step_size = property(lambda self: self._c.angular_perturbation_step_size)
+    resolution = property(lambda self: self._c.resolution)
+    num_scans = property(lambda self: self._c.num_scans)
+
+    def ShrinkToFit(self, discrete_scans, num_x_cells, num_y_cells):
+        """correlative_scan_matcher_2d.cc:68-91 (cell_limits as its two counts)."""
+        d = np.ascontiguousarray(np.asarray(discrete_scans, np.int32))
+        if d.shape[0] != self.num_scans or d.ndim != 3 or d.shape[2] != 2:
+            raise ValueError("discrete_scans must be (num_scans, points, 2)")
+        b = (LinearBounds * self.num_scans)(*self.linear_bounds)
+        _check(load_library().csm_search_parameters_shrink_to_fit(
+            C.byref(self._c), _ptr(d, C.c_int32), d.shape[1], num_x_cells, num_y_cells, b),
+            "csm_search_parameters_shrink_to_fit")
+        self.linear_bounds = [b[i] for i in range(self.num_scans)]
+
+
+@dataclass
+class Candidate2D:
+    """correlative_scan_matcher_2d.h:71-98."""
+    scan_index: int
+    x_index_offset: int
+    y_index_offset: int
+    search_parameters: "SearchParameters"
+    score: float = 0.0
+
+    @property
+    def x(self):
+        return -self.y_index_offset * self.search_parameters.resolution
+
+    @property
+    def y(self):
+        return -self.x_index_offset * self.search_parameters.resolution
+
+    @property
+    def orientation(self):
+        sp = self.search_parameters
+        return (self.scan_index - sp.num_angular_perturbations) * sp.angular_perturbation_step_size
+
+
+def GenerateRotatedScans(point_cloud, search_parameters: SearchParameters) -> np.ndarray:
+    """correlative_scan_matcher_2d.cc:93-108 -> (num_scans, n, 3) float32."""
+    pts = _f32_points(point_cloud)
+    out = np.zeros((search_parameters.num_scans, len(pts), 3), np.float32)
+    _check(load_library().csm_generate_rotated_scans(_ptr(pts, C.c_float), len(pts),
+                                                     C.byref(search_parameters._c),
+                                                     _ptr(out, C.c_float)),
+           "csm_generate_rotated_scans")
+    return out
+
+
+def DiscretizeScans(map_limits: MapLimits, scans, initial_translation) -> np.ndarray:
+    """correlative_scan_matcher_2d.cc:110-127: (num_scans, n, 3) rotated clouds
+    -> (num_scans, n, 2) int32 cell indices (x, y)."""
+    sc = np.ascontiguousarray(np.asarray(scans, np.float32))
+    if sc.ndim != 3 or sc.shape[2] != 3:
+        raise ValueError("scans must be (num_scans, points, 3)")
+    out = np.zeros((sc.shape[0], sc.shape[1], 2), np.int32)
+    _check(load_library().csm_discretize_scans(C.byref(map_limits), _ptr(sc, C.c_float),
+                                               sc.shape[1], sc.shape[0],
+                                               float(np.float32(initial_translation[0])),
+                                               float(np.float32(initial_translation[1])),
+                                               _ptr(out, C.c_int32)),
+           "csm_discretize_scans")
+    return out
 
 
 class ScanSet:

@@ -619,137 +619,4 @@ int csm_fast2d_match_full_submap(const csm_fast2d* m, const float* points_xyz, i
 
 }  // extern "C"
 
-namespace {
 
-// RealTimeCorrelativeScanMatcher2D::Match (real_time_correlative_scan_matcher_2d.cc:117-149)
-// over a ProbabilityGrid (weight_cells == nullptr) or a TSDF2D.
-int Rt2dMatch(csm_context* ctx, const csm_rt_options* o, const csm_map_limits* l,
-              const uint16_t* cells, const uint16_t* weight_cells, float truncation,
-              float max_weight, const csm_pose2d* initial, const float* xyz, int32_t n,
-              double* score, csm_pose2d* pose) {
-  if (!ctx || !o || !l || !cells || !initial || !score || !pose || n <= 0 || !xyz)
-    return CSM_EINVAL;
-  if (l->num_x_cells < 1 || l->num_y_cells < 1 || !(l->resolution > 0.)) return CSM_EINVAL;
-  const bool tsdf = weight_cells != nullptr;
-  if (tsdf && !(truncation > 0.f && max_weight > 0.f)) return CSM_EINVAL;
-  std::lock_guard<std::mutex> lock(ctx->mu);
-  if (EnsureDevice(ctx)) return CSM_EHIP;
-  hipStream_t st = ctx->stream;
-  int rc;
-  // real_time_correlative_scan_matcher_2d.cc:123-130: window on the
-  // pre-rotated cloud.
-  const ZRot pre = MakeZRot(static_cast<float>(initial->theta));
-  const SearchWindow2D w = MakeSearchWindow2D(o->linear_search_window, o->angular_search_window,
-                                              xyz, n, l->resolution, &pre);
-  std::vector<ZRot> table;
-  RotationTable(w, &table);
-  std::vector<float2> rot(table.size());
-  for (size_t i = 0; i < table.size(); ++i) rot[i] = make_float2(table[i].w, table[i].s);
-  const int nx = l->num_x_cells, ny = l->num_y_cells, ncell = nx * ny;
-  const int L = w.num_linear_perturbations;
-  const int side = 2 * L + 1;
-  const int64_t per_rot = static_cast<int64_t>(side) * side;
-  if (per_rot * w.num_scans > 0xffffffffll || static_cast<size_t>(n) * 8 > 60 * 1024)
-    return CSM_ERANGE;
-  if ((rc = ctx->rt_cells.Reserve(sizeof(uint16_t) * ncell))) return rc;
-  if ((rc = ctx->rt_points.Reserve(sizeof(float) * 3 * n))) return rc;
-  if ((rc = ctx->rt_rot.Reserve(sizeof(float2) * rot.size()))) return rc;
-  if ((rc = ctx->rt_best.Reserve(sizeof(unsigned long long)))) return rc;
-  CSM_HIP(hipMemcpyAsync(ctx->rt_cells.ptr, cells, sizeof(uint16_t) * ncell, hipMemcpyHostToDevice, st));
-  if (tsdf) {
-    // tsd_value_converter.cc:22-33: tsd table (min_tsd, min_tsd, max_tsd),
-    // weight table (0, 0, max_weight).
-    if (!ctx->ttab_uploaded || ctx->ttab_key[0] != truncation || ctx->ttab_key[1] != max_weight) {
-      std::vector<float> tab(2 * 32768);
-      ConversionTable(-truncation, -truncation, truncation, tab.data());
-      ConversionTable(0.f, 0.f, max_weight, tab.data() + 32768);
-      if ((rc = ctx->rt_ttab.Reserve(sizeof(float) * 2 * 32768))) return rc;
-      CSM_HIP(hipMemcpyAsync(ctx->rt_ttab.ptr, tab.data(), sizeof(float) * 2 * 32768,
-                             hipMemcpyHostToDevice, st));
-      CSM_HIP(hipStreamSynchronize(st));
-      ctx->ttab_key[0] = truncation;
-      ctx->ttab_key[1] = max_weight;
-      ctx->ttab_uploaded = true;
-    }
-    if ((rc = ctx->rt_wcells.Reserve(sizeof(uint16_t) * ncell))) return rc;
-    if ((rc = ctx->rt_tsdw.Reserve(sizeof(float2) * ncell))) return rc;
-    CSM_HIP(hipMemcpyAsync(ctx->rt_wcells.ptr, weight_cells, sizeof(uint16_t) * ncell,
-                           hipMemcpyHostToDevice, st));
-    CSM_HIP(LaunchCellsToTsdf(ctx->rt_cells.as<uint16_t>(), ctx->rt_wcells.as<uint16_t>(),
-                              ctx->rt_ttab.as<float>(), ctx->rt_ttab.as<float>() + 32768,
-                              ctx->rt_tsdw.as<float2>(), ncell, st));
-  } else {
-    if (!ctx->ptab_uploaded) {
-      ctx->ptab_host.resize(32768);
-      ProbabilityTable(ctx->ptab_host.data());
-      if ((rc = ctx->rt_ptab.Reserve(sizeof(float) * 32768))) return rc;
-      CSM_HIP(hipMemcpyAsync(ctx->rt_ptab.ptr, ctx->ptab_host.data(), sizeof(float) * 32768,
-                             hipMemcpyHostToDevice, st));
-      ctx->ptab_uploaded = true;
-    }
-    if ((rc = ctx->rt_prob.Reserve(sizeof(float) * ncell))) return rc;
-    CSM_HIP(LaunchCellsToProbability(ctx->rt_cells.as<uint16_t>(), ctx->rt_ptab.as<float>(),
-                                     ctx->rt_prob.as<float>(), ncell, st));
-  }
-  CSM_HIP(hipMemcpyAsync(ctx->rt_points.ptr, xyz, sizeof(float) * 3 * n, hipMemcpyHostToDevice, st));
-  CSM_HIP(hipMemcpyAsync(ctx->rt_rot.ptr, rot.data(), sizeof(float2) * rot.size(),
-                         hipMemcpyHostToDevice, st));
-  CSM_HIP(hipMemsetAsync(ctx->rt_best.ptr, 0, sizeof(unsigned long long), st));
-  const int block = 256;
-  if (ctx->timing) CSM_HIP(hipEventRecord(ctx->ev0, st));
-  CSM_HIP(LaunchRt2dScore(dim3(static_cast<unsigned>((per_rot + block - 1) / block), w.num_scans),
-                          block, sizeof(int2) * n, st, tsdf ? nullptr : ctx->rt_prob.as<float>(),
-                          tsdf ? ctx->rt_tsdw.as<float2>() : nullptr, truncation, nx, ny, l->max_x,
-                          l->max_y, l->resolution, ctx->rt_points.as<float>(), n,
-                          ctx->rt_rot.as<float2>(), pre.w, pre.s, static_cast<float>(initial->x),
-                          static_cast<float>(initial->y), L, w.num_angular_perturbations,
-                          w.angular_perturbation_step_size, o->translation_delta_cost_weight,
-                          o->rotation_delta_cost_weight, ctx->rt_best.as<unsigned long long>()));
-  if (ctx->timing) CSM_HIP(hipEventRecord(ctx->ev1, st));
-  unsigned long long key = 0;
-  CSM_HIP(hipMemcpyAsync(&key, ctx->rt_best.ptr, sizeof(key), hipMemcpyDeviceToHost, st));
-  CSM_HIP(hipStreamSynchronize(st));
-  if (ctx->timing) {
-    float ms = 0.f;
-    CSM_HIP(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
-    ctx->t.other_kernel_ms += ms;
-  }
-  if (key == 0) return CSM_EINVAL;
-  const uint32_t bits = static_cast<uint32_t>(key >> 32);
-  float s;
-  std::memcpy(&s, &bits, sizeof(s));
-  const uint32_t idx = 0xffffffffu - static_cast<uint32_t>(key & 0xffffffffu);
-  const int r = static_cast<int>(idx / per_rot);
-  const int t = static_cast<int>(idx % per_rot);
-  const int xo = -L + t / side, yo = -L + t % side;
-  const double cx = -yo * l->resolution, cy = -xo * l->resolution;
-  const double co = (r - w.num_angular_perturbations) * w.angular_perturbation_step_size;
-  pose->x = initial->x + cx;
-  pose->y = initial->y + cy;
-  pose->theta = initial->theta + co;
-  *score = s;
-  return CSM_OK;
-}
-
-}  // namespace
-
-extern "C" {
-
-int csm_rt2d_match(csm_context* ctx, const csm_rt_options* o, const csm_map_limits* l,
-                   const uint16_t* cells, float min_cc, float max_cc, const csm_pose2d* initial,
-                   const float* xyz, int32_t n, double* score, csm_pose2d* pose) {
-  (void)min_cc;
-  (void)max_cc;
-  return Rt2dMatch(ctx, o, l, cells, nullptr, 0.f, 0.f, initial, xyz, n, score, pose);
-}
-
-int csm_rt2d_match_tsdf(csm_context* ctx, const csm_rt_options* o, const csm_map_limits* l,
-                        const uint16_t* tsd_cells, const uint16_t* weight_cells,
-                        float truncation_distance, float max_weight, const csm_pose2d* initial,
-                        const float* xyz, int32_t n, double* score, csm_pose2d* pose) {
-  if (!weight_cells) return CSM_EINVAL;
-  return Rt2dMatch(ctx, o, l, tsd_cells, weight_cells, truncation_distance, max_weight, initial,
-                   xyz, n, score, pose);
-}
-
-}  // extern "C"

@@ -65,6 +65,20 @@ struct PinnedBuf {
   T* as() const { return static_cast<T*>(ptr); }
 };
 
+// RealTimeCorrelativeScanMatcher2D state (rt2d.hip): the converted, padded
+// grid of the last call (re-made only when cells / padding / TSDF
+// parameters change), its host copy for the comparison, conversion tables
+// and per-call scratch.
+struct Rt2dCache {
+  bool valid = false, tsdf = false, tables = false, ttab_ok = false;
+  int nx = 0, ny = 0, P = 0;
+  float truncation = 0.f, max_weight = 0.f;
+  float ttab_key[2] = {0.f, 0.f};
+  std::vector<uint16_t> cells, wcells;
+  DevBuf grid, dcells, ptab, ttab, bases, best, dstage, sink;
+  PinnedBuf stage, stage_cells, host_key;
+};
+
 }  // namespace csm
 
 struct csm_context {
@@ -72,16 +86,11 @@ struct csm_context {
   hipStream_t stream = nullptr;
   std::mutex mu;
   csm::DevBuf submap_desc, pair_desc, rot_table, best, status, counters, pair_order,
-      chunk_prefix, blocks, stats, spill, rt_prob, rt_cells, rt_points, rt_best, rt_rot, rt_ptab,
-      single_points, rt_wcells, rt_tsdw, rt_ttab;
-  // TSDValueConverter tables for the last (truncation, max_weight) uploaded.
-  float ttab_key[2] = {0.f, 0.f};
-  bool ttab_uploaded = false;
+      chunk_prefix, blocks, stats, spill, single_points;
+  csm::Rt2dCache rt2d;
   bool timing = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   csm_timing t{};
-  std::vector<float> ptab_host;
-  bool ptab_uploaded = false;
   double level_cands[csm::kMaxLevels] = {0};
   double level_batches[csm::kMaxLevels] = {0};
   int num_cus = 256;

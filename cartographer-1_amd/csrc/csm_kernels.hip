@@ -8,9 +8,7 @@
 //       (fast_correlative_scan_matcher_2d.cc:264-333) and run an exact
 //       depth-first branch and bound per wave (:335-378) against a per-pair
 //       incumbent shared through a 64-bit atomicMax.
-//   K5  rt2d_score — RealTimeCorrelativeScanMatcher2D::ScoreCandidates
-//       (real_time_correlative_scan_matcher_2d.cc:61-75, 151-176) and the
-//       first-max selection (:142-143).
+// (RealTimeCorrelativeScanMatcher2D's kernels are in rt2d.hip.)
 //
 // Built with -ffp-contract=off; the discretization additionally uses the
 // explicit round-to-nearest intrinsics so no multiply-add is ever fused:
@@ -21,28 +19,11 @@
 #include <algorithm>
 
 #include "csm_device.h"
+#include "geom2d_dev.h"
 
 namespace csm {
 
 // ---------------------------------------------------------------- helpers ---
-
-__device__ __forceinline__ void RotateZDev(float w, float s, float x, float y,
-                                           float* ox, float* oy) {
-  // Eigen QuaternionBase::_transformVector with q.vec = (0, 0, s).
-  const float uvx = __fsub_rn(0.f, __fmul_rn(s, y));
-  const float uvy = __fsub_rn(__fmul_rn(s, x), 0.f);
-  const float ux = __fadd_rn(uvx, uvx);
-  const float uy = __fadd_rn(uvy, uvy);
-  const float cx = __fsub_rn(0.f, __fmul_rn(s, uy));
-  const float cy = __fsub_rn(__fmul_rn(s, ux), 0.f);
-  *ox = __fadd_rn(__fadd_rn(x, __fmul_rn(w, ux)), cx);
-  *oy = __fadd_rn(__fadd_rn(y, __fmul_rn(w, uy)), cy);
-}
-
-// MapLimits::GetCellIndex: lround((max - p) / resolution - 0.5) in double.
-__device__ __forceinline__ double CellCoord(double max_v, float p, double res) {
-  return __builtin_round(__dsub_rn(__ddiv_rn(__dsub_rn(max_v, static_cast<double>(p)), res), 0.5));
-}
 
 __device__ __forceinline__ int WaveSum(int v) {
 #pragma unroll
@@ -1080,91 +1061,8 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
   if (stats && tid == 0) atomicMax(&stats[kStatHighWater], static_cast<unsigned long long>(sh.high_water));
 }
 
-// ---------------------------------------------------------------- K5 -------
-
-// One workgroup per rotated scan; one lane per (x, y) offset of the full
-// (2L+1)^2 window (no ShrinkToFit on this path). Float sums run point by
-// point in the reference order so every candidate score is bit-identical.
-// kTsdf selects the grid: ProbabilityGrid (`prob`, 0.1 outside the limits,
-// real_time_correlative_scan_matcher_2d.cc:61-75) or TSDF2D (`tsdw` = (tsd,
-// weight), (-truncation, 0) outside, :38-59).
-template <bool kTsdf>
-__global__ void rt2d_score(const float* __restrict__ prob,   // ProbabilityGrid as probabilities
-                           const float2* __restrict__ tsdw,  // TSDF2D as (tsd, weight)
-                           float max_cc, int nx, int ny, double max_x, double max_y, double res,
-                           const float* __restrict__ points, int n,
-                           const float2* __restrict__ rot_table, float pre_w, float pre_s,
-                           float tx, float ty, int num_linear, int num_angular,
-                           double step, double wt, double wr,
-                           unsigned long long* __restrict__ best) {
-  extern __shared__ __align__(16) int2 lds_xy[];
-  const int r = blockIdx.y;
-  const float2 q = rot_table[r];
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    float x, y;
-    RotateZDev(pre_w, pre_s, points[3 * i], points[3 * i + 1], &x, &y);
-    RotateZDev(q.x, q.y, x, y, &x, &y);
-    const float px = __fadd_rn(tx, x), py = __fadd_rn(ty, y);
-    double cx = CellCoord(max_y, py, res), cy = CellCoord(max_x, px, res);
-    cx = fmin(fmax(cx, -1e9), 1e9);
-    cy = fmin(fmax(cy, -1e9), 1e9);
-    lds_xy[i] = make_int2(static_cast<int>(cx), static_cast<int>(cy));
-  }
-  __syncthreads();
-  const int side = 2 * num_linear + 1;
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  unsigned long long key = 0;
-  if (t < side * side) {
-    const int xo = -num_linear + t / side;
-    const int yo = -num_linear + t % side;
-    float s = 0.f;
-    if constexpr (kTsdf) {
-      float sw = 0.f;
-      for (int i = 0; i < n; ++i) {
-        const int2 c = lds_xy[i];
-        const int gx = c.x + xo, gy = c.y + yo;
-        const bool in = gx >= 0 && gy >= 0 && gx < nx && gy < ny;
-        const float2 v = in ? tsdw[static_cast<size_t>(gy) * nx + gx] : make_float2(-max_cc, 0.f);
-        const float norm = __fdiv_rn(__fsub_rn(max_cc, fabsf(v.x)), max_cc);
-        s = __fadd_rn(s, __fmul_rn(norm, v.y));
-        sw = __fadd_rn(sw, v.y);
-      }
-      s = sw == 0.f ? 0.f : __fdiv_rn(s, sw);
-    } else {
-      for (int i = 0; i < n; ++i) {
-        const int2 c = lds_xy[i];
-        const int gx = c.x + xo, gy = c.y + yo;
-        const bool in = gx >= 0 && gy >= 0 && gx < nx && gy < ny;
-        s = __fadd_rn(s, in ? prob[static_cast<size_t>(gy) * nx + gx] : 0.1f);
-      }
-      s = __fdiv_rn(s, static_cast<float>(n));
-    }
-    const double cand_x = -yo * res, cand_y = -xo * res;
-    const double theta = (r - num_angular) * step;
-    const double pen = __dadd_rn(__dmul_rn(hypot(cand_x, cand_y), wt), __dmul_rn(fabs(theta), wr));
-    const float score = static_cast<float>(__dmul_rn(static_cast<double>(s), exp(-__dmul_rn(pen, pen))));
-    const unsigned int idx = static_cast<unsigned int>(r * side * side + t);
-    key = (static_cast<unsigned long long>(__float_as_uint(score)) << 32) |
-          static_cast<unsigned long long>(0xffffffffu - idx);
-  }
-  for (int m = 32; m >= 1; m >>= 1) {
-    const unsigned long long o = __shfl_xor(key, m, 64);
-    key = o > key ? o : key;
-  }
-  if ((threadIdx.x & 63) == 0 && key != 0) atomicMax(best, key);
-}
-
-// TSDF2D cells -> (tsd, weight) through TSDValueConverter's tables
-// (tsd_value_converter.h:54-62; bit 15, the update marker, is masked).
-__global__ void cells_to_tsdf(const uint16_t* __restrict__ tsd_cells,
-                              const uint16_t* __restrict__ weight_cells,
-                              const float* __restrict__ tsd_tab, const float* __restrict__ w_tab,
-                              float2* __restrict__ out, int n) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) out[i] = make_float2(tsd_tab[tsd_cells[i] & 0x7fff], w_tab[weight_cells[i] & 0x7fff]);
-}
-
-// Grid cells -> probability (ProbabilityGrid::GetProbability table).
+// Grid cells -> float through a 32768-entry table (ValueConversionTables;
+// the Ceres refinement's correspondence-cost grid).
 __global__ void cells_to_probability(const uint16_t* __restrict__ cells,
                                      const float* __restrict__ ptab,
                                      float* __restrict__ out, int n) {
@@ -1213,30 +1111,6 @@ hipError_t LaunchFast2dSearchV2(int grid, size_t dyn_lds, hipStream_t st, const 
                                 uint2* spill, int npad) {
   hipLaunchKernelGGL(fast2d_search_v4, dim3(grid), dim3(kSearchThreads), dyn_lds, st, submaps, pairs,
                      points, rot_table, queues, counters, best, status, stats, spill, npad);
-  return hipGetLastError();
-}
-
-hipError_t LaunchRt2dScore(dim3 grid, int block, size_t dyn_lds, hipStream_t st, const float* prob,
-                           const float2* tsdw, float max_cc, int nx, int ny, double max_x,
-                           double max_y, double res, const float* points, int n,
-                           const float2* rot_table, float pre_w, float pre_s, float tx, float ty,
-                           int num_linear, int num_angular, double step, double wt, double wr,
-                           unsigned long long* best) {
-  if (tsdw)
-    hipLaunchKernelGGL(rt2d_score<true>, grid, dim3(block), dyn_lds, st, prob, tsdw, max_cc, nx, ny,
-                       max_x, max_y, res, points, n, rot_table, pre_w, pre_s, tx, ty, num_linear,
-                       num_angular, step, wt, wr, best);
-  else
-    hipLaunchKernelGGL(rt2d_score<false>, grid, dim3(block), dyn_lds, st, prob, tsdw, max_cc, nx, ny,
-                       max_x, max_y, res, points, n, rot_table, pre_w, pre_s, tx, ty, num_linear,
-                       num_angular, step, wt, wr, best);
-  return hipGetLastError();
-}
-
-hipError_t LaunchCellsToTsdf(const uint16_t* tsd, const uint16_t* weight, const float* tsd_tab,
-                             const float* w_tab, float2* out, int n, hipStream_t st) {
-  hipLaunchKernelGGL(cells_to_tsdf, dim3((n + 255) / 256), dim3(256), 0, st, tsd, weight, tsd_tab,
-                     w_tab, out, n);
   return hipGetLastError();
 }
 

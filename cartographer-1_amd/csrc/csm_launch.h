@@ -23,14 +23,8 @@ hipError_t LaunchFast2dSearchV2(int grid, size_t dyn_lds, hipStream_t st, const 
                                 const WorkQueues2& queues, unsigned long long* counters,
                                 uint64_t* best, int32_t* status, unsigned long long* stats,
                                 uint2* spill, int npad);
-hipError_t LaunchRt2dScore(dim3 grid, int block, size_t dyn_lds, hipStream_t st, const float* prob,
-                           const float2* tsdw, float max_cc, int nx, int ny, double max_x,
-                           double max_y, double res, const float* points, int n,
-                           const float2* rot_table, float pre_w, float pre_s, float tx, float ty,
-                           int num_linear, int num_angular, double step, double wt, double wr,
-                           unsigned long long* best);
-hipError_t LaunchCellsToTsdf(const uint16_t* tsd, const uint16_t* weight, const float* tsd_tab,
-                             const float* w_tab, float2* out, int n, hipStream_t st);
+
+
 hipError_t LaunchCellsToProbability(const uint16_t* cells, const float* ptab, float* out, int n,
                                     hipStream_t st);
 

@@ -201,6 +201,80 @@ int csm_rt2d_match_tsdf(csm_context* ctx, const csm_rt_options* options,
                         const float* points_xyz, int32_t n, double* score,
                         csm_pose2d* pose);
 
+/* ---- correlative_scan_matcher_2d.h: search-space helpers ---------------------
+ * The free functions and SearchParameters of correlative_scan_matcher_2d.h
+ * (:35-68, .cc:27-127), host-side, with the reference's float/double
+ * arithmetic (the device path computes the same values internally). */
+typedef struct csm_linear_bounds {
+  int32_t min_x, max_x, min_y, max_y;  /* inclusive pixel offsets */
+} csm_linear_bounds;
+
+typedef struct csm_search_parameters {
+  int32_t num_angular_perturbations;
+  double angular_perturbation_step_size;
+  double resolution;
+  int32_t num_scans;
+  /* linear_bounds start as +-num_linear_perturbations for every scan. */
+  int32_t num_linear_perturbations;
+} csm_search_parameters;
+
+/* SearchParameters(linear_search_window, angular_search_window, point_cloud,
+ * resolution) (correlative_scan_matcher_2d.cc:27-52). */
+int csm_search_parameters_init(double linear_search_window, double angular_search_window,
+                               const float* points_xyz, int32_t n, double resolution,
+                               csm_search_parameters* out);
+/* SearchParameters(num_linear_perturbations, num_angular_perturbations,
+ * angular_perturbation_step_size, resolution) — "for testing" (:54-66). */
+int csm_search_parameters_init_for_testing(int32_t num_linear_perturbations,
+                                           int32_t num_angular_perturbations,
+                                           double angular_perturbation_step_size,
+                                           double resolution, csm_search_parameters* out);
+/* SearchParameters::ShrinkToFit (:68-91): bounds (num_scans entries) are
+ * tightened in place against discrete scans (num_scans * points_per_scan
+ * (x, y) cell indices, scan-major) and the grid's cell limits. */
+int csm_search_parameters_shrink_to_fit(const csm_search_parameters* sp,
+                                        const int32_t* discrete_xy, int32_t points_per_scan,
+                                        int32_t num_x_cells, int32_t num_y_cells,
+                                        csm_linear_bounds* bounds);
+/* GenerateRotatedScans (:93-108): out_xyz holds num_scans * n points. */
+int csm_generate_rotated_scans(const float* points_xyz, int32_t n,
+                               const csm_search_parameters* sp, float* out_xyz);
+/* DiscretizeScans (:110-127): num_scans rotated clouds of n points each
+ * (scan-major), translated by (initial_x, initial_y) in float and turned
+ * into cell indices by MapLimits::GetCellIndex; out_xy receives
+ * num_scans * n (x, y) pairs. */
+int csm_discretize_scans(const csm_map_limits* limits, const float* rotated_xyz, int32_t n,
+                         int32_t num_scans, float initial_x, float initial_y, int32_t* out_xy);
+
+/* Candidate2D (correlative_scan_matcher_2d.h:71-98): score is filled in by
+ * ScoreCandidates. */
+typedef struct csm_candidate2d {
+  int32_t scan_index, x_index_offset, y_index_offset;
+  float score;
+} csm_candidate2d;
+
+/* RealTimeCorrelativeScanMatcher2D::ScoreCandidates(grid, discrete_scans,
+ * search_parameters, candidates*) (real_time_correlative_scan_matcher_2d.h:
+ * 75-78, .cc:151-176; visible for testing): every candidate's score =
+ * mean probability of its discrete scan shifted by its offsets, times
+ * exp(-(hypot(x, y) * w_t + |orientation| * w_r)^2) with the candidate's
+ * x, y, orientation from the search parameters. discrete_xy as
+ * csm_discretize_scans writes it. */
+int csm_rt2d_score_candidates(csm_context* ctx, const csm_rt_options* options,
+                              const csm_map_limits* limits, const uint16_t* cells,
+                              float min_correspondence_cost, float max_correspondence_cost,
+                              const int32_t* discrete_xy, int32_t num_scans,
+                              int32_t points_per_scan, const csm_search_parameters* sp,
+                              csm_candidate2d* candidates, int64_t num_candidates);
+/* The same over a TSDF2D (grid arrays as csm_rt2d_match_tsdf). */
+int csm_rt2d_score_candidates_tsdf(csm_context* ctx, const csm_rt_options* options,
+                                   const csm_map_limits* limits, const uint16_t* tsd_cells,
+                                   const uint16_t* weight_cells, float truncation_distance,
+                                   float max_weight, const int32_t* discrete_xy,
+                                   int32_t num_scans, int32_t points_per_scan,
+                                   const csm_search_parameters* sp,
+                                   csm_candidate2d* candidates, int64_t num_candidates);
+
 /* ---- 3D: HybridGrid ----------------------------------------------------------
  * A HybridGrid (mapping/3d/hybrid_grid.h:463-545) crosses the boundary as the
  * list its iterator / ToProto yields (hybrid_grid.h:530-541): cell indices

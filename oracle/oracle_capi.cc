@@ -283,6 +283,84 @@ int32_t oracle_discretize(double res, double max_x, double max_y, int32_t nx,
   return 0;
 }
 
+// ---- correlative_scan_matcher_2d.h helpers (checkers for the csm_search_*,
+// csm_generate_rotated_scans, csm_discretize_scans and
+// csm_rt2d_score_candidates exports) -----------------------------------------
+
+// SearchParameters(lin, ang, cloud, res): num_angular, step, num_scans and
+// the first scan's bounds (all scans start equal).
+int32_t oracle_search_parameters(double lin, double ang, const float* xyz, int32_t n, double res,
+                                 int32_t* num_angular, double* step, int32_t* num_scans,
+                                 int32_t* bounds4) {
+  const SearchParameters sp(lin, ang, ToCloud(xyz, n), res);
+  *num_angular = sp.num_angular_perturbations;
+  *step = sp.angular_perturbation_step_size;
+  *num_scans = sp.num_scans;
+  bounds4[0] = sp.linear_bounds[0].min_x;
+  bounds4[1] = sp.linear_bounds[0].max_x;
+  bounds4[2] = sp.linear_bounds[0].min_y;
+  bounds4[3] = sp.linear_bounds[0].max_y;
+  return 0;
+}
+
+// GenerateRotatedScans with the testing SearchParameters constructor;
+// out: num_scans * n * 3 floats.
+int32_t oracle_generate_rotated_scans(const float* xyz, int32_t n, int32_t num_linear,
+                                      int32_t num_angular, double step, double res, float* out) {
+  const SearchParameters sp(num_linear, num_angular, step, res);
+  const auto scans = GenerateRotatedScans(ToCloud(xyz, n), sp);
+  for (int s = 0; s < sp.num_scans; ++s)
+    for (int i = 0; i < n; ++i) {
+      float* o = out + 3 * (static_cast<int64_t>(s) * n + i);
+      o[0] = scans[s][i].x;
+      o[1] = scans[s][i].y;
+      o[2] = scans[s][i].z;
+    }
+  return sp.num_scans;
+}
+
+// DiscretizeScans of num_scans given clouds (scan-major); out: (x, y) pairs.
+int32_t oracle_discretize_scans(double res, double max_x, double max_y, int32_t nx, int32_t ny,
+                                const float* rotated, int32_t n, int32_t num_scans, float tx,
+                                float ty, int32_t* out) {
+  std::vector<PointCloud> scans(static_cast<size_t>(num_scans));
+  for (int s = 0; s < num_scans; ++s) scans[s] = ToCloud(rotated + 3 * static_cast<int64_t>(s) * n, n);
+  const auto d = DiscretizeScans(ToLimits(res, max_x, max_y, nx, ny), scans, tx, ty);
+  for (int s = 0; s < num_scans; ++s)
+    for (int i = 0; i < n; ++i) {
+      out[2 * (static_cast<int64_t>(s) * n + i)] = d[s][i].x;
+      out[2 * (static_cast<int64_t>(s) * n + i) + 1] = d[s][i].y;
+    }
+  return 0;
+}
+
+// RealTimeCorrelativeScanMatcher2D::ScoreCandidates over a probability grid.
+// discrete: num_scans * n (x, y); cands: (scan, x_off, y_off) triples;
+// sp given as (num_angular, step, res) through the testing constructor.
+int32_t oracle_rt2d_score_candidates(double res, double max_x, double max_y, int32_t nx,
+                                     int32_t ny, const uint16_t* cells, double wt, double wr,
+                                     const int32_t* discrete, int32_t num_scans, int32_t n,
+                                     int32_t num_angular, double step, const int32_t* cands,
+                                     int64_t count, float* out) {
+  const MapLimits l = ToLimits(res, max_x, max_y, nx, ny);
+  ProbabilityGrid g(l, std::vector<uint16_t>(cells, cells + static_cast<size_t>(nx) * ny));
+  RealTimeOptions o;
+  o.translation_delta_cost_weight = wt;
+  o.rotation_delta_cost_weight = wr;
+  std::vector<DiscreteScan2D> scans(static_cast<size_t>(num_scans));
+  for (int s = 0; s < num_scans; ++s)
+    for (int i = 0; i < n; ++i) {
+      const int64_t k = static_cast<int64_t>(s) * n + i;
+      scans[s].push_back(Idx2{discrete[2 * k], discrete[2 * k + 1]});
+    }
+  const SearchParameters sp(0, num_angular, step, res);
+  std::vector<Candidate2D> c;
+  for (int64_t i = 0; i < count; ++i) c.emplace_back(cands[3 * i], cands[3 * i + 1], cands[3 * i + 2], sp);
+  RealTimeCorrelativeScanMatcher2D(o).ScoreCandidates(g, scans, &c);
+  for (int64_t i = 0; i < count; ++i) out[i] = c[i].score;
+  return 0;
+}
+
 }  // extern "C"
 
 // ---- test-grid construction (the reference tests build grids through the

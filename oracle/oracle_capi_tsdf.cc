@@ -97,4 +97,32 @@ double oracle_rt2d_match_tsdf(double res, double max_x, double max_y, int32_t nx
   return s;
 }
 
+// RealTimeScoreCandidatesTSDF (ScoreCandidates over a TSDF2D), arguments as
+// oracle_rt2d_score_candidates.
+int32_t oracle_rt2d_score_candidates_tsdf(double res, double max_x, double max_y, int32_t nx,
+                                          int32_t ny, const uint16_t* tsd, const uint16_t* weight,
+                                          float truncation_distance, float max_weight, double wt,
+                                          double wr, const int32_t* discrete, int32_t num_scans,
+                                          int32_t n, int32_t num_angular, double step,
+                                          const int32_t* cands, int64_t count, float* out) {
+  const size_t cells = static_cast<size_t>(nx) * ny;
+  const TSDF2D t(ToLimitsT(res, max_x, max_y, nx, ny), truncation_distance, max_weight,
+                 std::vector<uint16_t>(tsd, tsd + cells), std::vector<uint16_t>(weight, weight + cells));
+  RealTimeOptions o;
+  o.translation_delta_cost_weight = wt;
+  o.rotation_delta_cost_weight = wr;
+  std::vector<DiscreteScan2D> scans(static_cast<size_t>(num_scans));
+  for (int s = 0; s < num_scans; ++s)
+    for (int i = 0; i < n; ++i) {
+      const int64_t k = static_cast<int64_t>(s) * n + i;
+      scans[s].push_back(Idx2{discrete[2 * k], discrete[2 * k + 1]});
+    }
+  const SearchParameters sp(0, num_angular, step, res);
+  std::vector<Candidate2D> c;
+  for (int64_t i = 0; i < count; ++i) c.emplace_back(cands[3 * i], cands[3 * i + 1], cands[3 * i + 2], sp);
+  RealTimeScoreCandidatesTSDF(o, t, scans, &c);
+  for (int64_t i = 0; i < count; ++i) out[i] = c[i].score;
+  return 0;
+}
+
 }  // extern "C"

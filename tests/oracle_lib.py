@@ -35,6 +35,14 @@ class Oracle:
                                      I32, I32]),
             "oracle_discretize": (I32, [D, D, D, I32, I32, P(D), D, D, P(F), I32, I32, P(I32),
                                         P(I32), P(I32), I64, P(D)]),
+            "oracle_search_parameters": (I32, [D, D, P(F), I32, D, P(I32), P(D), P(I32), P(I32)]),
+            "oracle_generate_rotated_scans": (I32, [P(F), I32, I32, I32, D, D, P(F)]),
+            "oracle_discretize_scans": (I32, [D, D, D, I32, I32, P(F), I32, I32, F, F, P(I32)]),
+            "oracle_rt2d_score_candidates": (I32, [D, D, D, I32, I32, P(C.c_uint16), D, D,
+                                                   P(I32), I32, I32, I32, D, P(I32), I64, P(F)]),
+            "oracle_rt2d_score_candidates_tsdf": (I32, [D, D, D, I32, I32, P(C.c_uint16),
+                                                        P(C.c_uint16), F, F, D, D, P(I32), I32,
+                                                        I32, I32, D, P(I32), I64, P(F)]),
             "oracle_grid_create": (VP, [D, D, D, I32, I32]),
             "oracle_grid_destroy": (None, [VP]),
             "oracle_grid_insert": (None, [VP, F, F, I32, P(F), P(F), I32]),
@@ -502,3 +510,86 @@ def _o_ceres3d_match(self, high, low, high_cloud, low_cloud, options, target, in
 
 
 Oracle.ceres3d_match = _o_ceres3d_match
+
+
+def _o_search_parameters(self, lin, ang, cloud, res):
+    """SearchParameters(lin, ang, cloud, res) restated: (num_angular, step,
+    num_scans, first scan's bounds)."""
+    pts = np.ascontiguousarray(cloud, np.float32).reshape(-1, 3)
+    na, ns = C.c_int32(), C.c_int32()
+    step = C.c_double()
+    b = np.zeros(4, np.int32)
+    self.lib.oracle_search_parameters(lin, ang, _p(pts, F), len(pts), res, C.byref(na),
+                                      C.byref(step), C.byref(ns), _p(b, I32))
+    return na.value, step.value, ns.value, tuple(int(v) for v in b)
+
+
+def _o_generate_rotated_scans(self, cloud, num_linear, num_angular, step, res):
+    pts = np.ascontiguousarray(cloud, np.float32).reshape(-1, 3)
+    out = np.zeros((2 * num_angular + 1, len(pts), 3), np.float32)
+    self.lib.oracle_generate_rotated_scans(_p(pts, F), len(pts), num_linear, num_angular, step,
+                                           res, _p(out, F))
+    return out
+
+
+def _o_discretize_scans(self, limits, scans, tx, ty):
+    """limits: (res, max_x, max_y, nx, ny); scans (num_scans, n, 3)."""
+    sc = np.ascontiguousarray(scans, np.float32)
+    out = np.zeros((sc.shape[0], sc.shape[1], 2), np.int32)
+    self.lib.oracle_discretize_scans(limits[0], limits[1], limits[2], limits[3], limits[4],
+                                     _p(sc, F), sc.shape[1], sc.shape[0], float(np.float32(tx)),
+                                     float(np.float32(ty)), _p(out, I32))
+    return out
+
+
+def _o_rt2d_score_candidates(self, limits, cells, wt, wr, discrete, num_angular, step, cands,
+                             tsdf=None):
+    """ScoreCandidates restated; cands (k, 3) (scan, x_off, y_off). tsdf:
+    (weight_cells, truncation, max_weight) for a TSDF2D (cells = tsd cells)."""
+    d = np.ascontiguousarray(discrete, np.int32)
+    c = np.ascontiguousarray(cands, np.int32).reshape(-1, 3)
+    cells = np.ascontiguousarray(cells, np.uint16)
+    out = np.zeros(len(c), np.float32)
+    if tsdf is None:
+        self.lib.oracle_rt2d_score_candidates(limits[0], limits[1], limits[2], limits[3],
+                                              limits[4], _p(cells, C.c_uint16), wt, wr,
+                                              _p(d, I32), d.shape[0], d.shape[1], num_angular,
+                                              step, _p(c, I32), len(c), _p(out, F))
+    else:
+        w = np.ascontiguousarray(tsdf[0], np.uint16)
+        self.lib.oracle_rt2d_score_candidates_tsdf(limits[0], limits[1], limits[2], limits[3],
+                                                   limits[4], _p(cells, C.c_uint16),
+                                                   _p(w, C.c_uint16), tsdf[1], tsdf[2], wt, wr,
+                                                   _p(d, I32), d.shape[0], d.shape[1],
+                                                   num_angular, step, _p(c, I32), len(c),
+                                                   _p(out, F))
+    return out
+
+
+Oracle.search_parameters = _o_search_parameters
+Oracle.generate_rotated_scans = _o_generate_rotated_scans
+Oracle.discretize_scans = _o_discretize_scans
+Oracle.rt2d_score_candidates = _o_rt2d_score_candidates
+
+
+def _o_discretize(self, limits, cells, initial, lin, ang, cloud, rotated_sp=False):
+    """The matchers' whole window pipeline restated (oracle_discretize):
+    SearchParameters, rotated scans, DiscretizeScans at the initial pose and
+    ShrinkToFit. Returns (num_scans, shrunk bounds (num_scans, 4),
+    discrete scans (num_scans, n, 2), step)."""
+    res, mx, my = limits
+    pts = np.ascontiguousarray(cloud, np.float32).reshape(-1, 3)
+    init = np.asarray(initial, np.float64)
+    ns, step = C.c_int32(), C.c_double()
+    args = (res, mx, my, cells.shape[1], cells.shape[0], _p(init, D), lin, ang, _p(pts, F),
+            len(pts), int(rotated_sp), C.byref(ns))
+    self.lib.oracle_discretize(*args, None, None, 0, C.byref(step))
+    bounds = np.zeros((ns.value, 4), np.int32)
+    out = np.zeros((ns.value, len(pts), 2), np.int32)
+    rc = self.lib.oracle_discretize(*args, _p(bounds, I32), _p(out, I32), out.size,
+                                    C.byref(step))
+    assert rc == 0
+    return ns.value, bounds, out, step.value
+
+
+Oracle.discretize = _o_discretize
