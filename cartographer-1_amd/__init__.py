@@ -260,6 +260,12 @@ _SIGNATURES = {
     "csm_hybrid_grid_destroy": (None, [C.c_void_p]),
     "csm_hybrid_grid_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32),
                                        C.POINTER(C.c_int32)]),
+    "csm_rt3d_window": (C.c_int, [C.POINTER(RtOptions), C.c_float, C.POINTER(C.c_float),
+                                  C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+    "csm_rt3d_score_rotations": (C.c_int, [C.c_void_p, C.POINTER(RtOptions), C.c_void_p,
+                                           C.POINTER(Pose3D), C.POINTER(C.c_float), C.c_int32,
+                                           C.POINTER(C.c_int32), C.c_int32,
+                                           C.POINTER(C.c_float)]),
     "csm_rt3d_match": (C.c_int, [C.c_void_p, C.POINTER(RtOptions), C.c_void_p, C.POINTER(Pose3D),
                                  C.POINTER(C.c_float), C.c_int32, C.POINTER(C.c_float),
                                  C.POINTER(Pose3D)]),

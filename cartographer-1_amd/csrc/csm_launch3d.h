@@ -28,7 +28,8 @@ hipError_t LaunchRt3dScore2( int num_rot, hipStream_t st, const float* pad,
                             const Brick3& gb, float res, const float* points, int n,
                             const float4* rot, const float* rot_angle, const float4* trans,
                             int num_trans, int t_base, double wt, double wr,
-                            unsigned long long* best);
+                            unsigned long long* best, float* scores = nullptr,
+                            int scores_pitch = 0);
 // Items [item_begin, item_begin + num_items) of the yaw list; `large`
 // selects the build for clouds of more than kSmall3dPoints points.
 hipError_t LaunchFast3dSearch(bool large, int grid, hipStream_t st, const Submap3Desc* submaps,

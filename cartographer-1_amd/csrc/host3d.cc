@@ -248,29 +248,39 @@ int csm_hybrid_grid_info(const csm_hybrid_grid* g, int32_t* origin3, int32_t* di
 }
 
 // ------------------------------------------------------------- RTCSM3D --
-int csm_rt3d_match(csm_context* ctx, const csm_rt_options* o, const csm_hybrid_grid* grid,
-                   const csm_pose3d* initial, const float* xyz, int32_t n, float* score,
-                   csm_pose3d* pose) {
-  if (!ctx || !o || !grid || !initial || !score || !pose || n <= 0 || !xyz) return CSM_EINVAL;
-  if (grid->ctx != ctx) return CSM_EINVAL;
-  std::lock_guard<std::mutex> lock(ctx->mu);
-  int rc;
-  if ((rc = EnsureDevice3(ctx))) return rc;
-  // GenerateExhaustiveSearchTransforms (real_time_correlative_scan_matcher_3d.cc:55-95).
-  const float res = grid->resolution;
-  const int L = Lround(o->linear_search_window / res);
+namespace {
+
+// GenerateExhaustiveSearchTransforms (real_time_correlative_scan_matcher_3d.cc:
+// 55-95) composed with the initial pose (:41-42): rotation r = ((rz + A) *
+// na + ry + A) * na + rx + A and translation t = ((z + L) * nl + y + L) * nl +
+// x + L, candidate index t * num_rot + r (the reference's loop order).
+struct Rt3dWindow {
+  int L = 0, A = 0;
+  int64_t nl = 0, na = 0, num_trans = 0, num_rot = 0;
+  std::vector<float4> rot, trans;
+  std::vector<float> angle;
+};
+
+int MakeRt3dWindow(const csm_rt_options* o, float res, const csm_pose3d* initial, const float* xyz,
+                   int32_t n, Rt3dWindow* w) {
+  w->L = Lround(o->linear_search_window / res);
   float max_range = 3.f * res;
   for (int i = 0; i < n; ++i)
     max_range = std::max(NormV(V3{xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2]}), max_range);
   const float step = (1.f - 1e-3f) * std::acos(1.f - (res * res) / (2.f * (max_range * max_range)));
-  const int A = Lround(o->angular_search_window / step);
+  w->A = Lround(o->angular_search_window / step);
+  const int L = w->L, A = w->A;
   if (L < 0 || A < 0 || L > 1000 || A > 1000) return CSM_ERANGE;
-  const int64_t nl = 2 * L + 1, na = 2 * A + 1;
-  const int64_t num_trans = nl * nl * nl, num_rot = na * na * na;
-  if (num_trans * num_rot >= (int64_t{1} << 32) || num_rot > (int64_t{1} << 31)) return CSM_ERANGE;
+  w->nl = 2 * L + 1;
+  w->na = 2 * A + 1;
+  w->num_trans = w->nl * w->nl * w->nl;
+  w->num_rot = w->na * w->na * w->na;
+  if (w->num_trans * w->num_rot >= (int64_t{1} << 32) || w->num_rot > (int64_t{1} << 31))
+    return CSM_ERANGE;
   const R3 init = CastF(*initial);
-  std::vector<float4> rot(num_rot);
-  std::vector<float> rot_angle(num_rot);
+  w->rot.resize(w->num_rot);
+  w->angle.resize(w->num_rot);
+  const int64_t na = w->na, nl = w->nl;
   for (int rz = -A; rz <= A; ++rz)
     for (int ry = -A; ry <= A; ++ry)
       for (int rx = -A; rx <= A; ++rx) {
@@ -279,10 +289,10 @@ int csm_rt3d_match(csm_context* ctx, const csm_rt_options* o, const csm_hybrid_g
                                          static_cast<float>(ry) * step,
                                          static_cast<float>(rz) * step});
         const Q4 q = QNormalized(QMul(init.q, qs));  // initial.cast<float>() * transform
-        rot[r] = make_float4(q.x, q.y, q.z, q.w);
-        rot_angle[r] = GetAngle(qs);
+        w->rot[r] = make_float4(q.x, q.y, q.z, q.w);
+        w->angle[r] = GetAngle(qs);
       }
-  std::vector<float4> trans(num_trans);
+  w->trans.resize(w->num_trans);
   for (int z = -L; z <= L; ++z)
     for (int y = -L; y <= L; ++y)
       for (int x = -L; x <= L; ++x) {
@@ -290,29 +300,41 @@ int csm_rt3d_match(csm_context* ctx, const csm_rt_options* o, const csm_hybrid_g
         const V3 tv{static_cast<float>(x) * res, static_cast<float>(y) * res,
                     static_cast<float>(z) * res};
         const V3 T = Apply(init, tv);
-        trans[t] = make_float4(T.x, T.y, T.z, NormV(tv));
+        w->trans[t] = make_float4(T.x, T.y, T.z, NormV(tv));
       }
+  return CSM_OK;
+}
+
+// Scores the window's candidates over `rot` (num_rot of the window's
+// rotations, angles alongside): the best key (scores == nullptr) or every
+// candidate's score into the device array scores[r * num_trans + t].
+int RunRt3d(csm_context* ctx, const csm_rt_options* o, const csm_hybrid_grid* grid, const float* xyz,
+            int32_t n, const Rt3dWindow& w, const float4* rot, const float* angle,
+            int64_t num_rot, unsigned long long* key, float* dscores) {
   hipStream_t st = ctx->stream;
+  int rc;
+  const float res = grid->resolution;
+  const int64_t num_trans = w.num_trans;
   if ((rc = ctx->rt3_rot.Reserve(sizeof(float4) * num_rot + sizeof(float) * num_rot))) return rc;
   if ((rc = ctx->rt3_trans.Reserve(sizeof(float4) * num_trans))) return rc;
   if ((rc = ctx->rt3_points.Reserve(sizeof(float) * 3 * n))) return rc;
   if ((rc = ctx->rt3_best.Reserve(sizeof(unsigned long long)))) return rc;
   float4* drot = ctx->rt3_rot.as<float4>();
   float* dangle = reinterpret_cast<float*>(drot + num_rot);
-  CSM_HIP(hipMemcpyAsync(drot, rot.data(), sizeof(float4) * num_rot, hipMemcpyHostToDevice, st));
-  CSM_HIP(hipMemcpyAsync(dangle, rot_angle.data(), sizeof(float) * num_rot, hipMemcpyHostToDevice,
-                         st));
-  CSM_HIP(hipMemcpyAsync(ctx->rt3_trans.ptr, trans.data(), sizeof(float4) * num_trans,
+  CSM_HIP(hipMemcpyAsync(drot, rot, sizeof(float4) * num_rot, hipMemcpyHostToDevice, st));
+  CSM_HIP(hipMemcpyAsync(dangle, angle, sizeof(float) * num_rot, hipMemcpyHostToDevice, st));
+  CSM_HIP(hipMemcpyAsync(ctx->rt3_trans.ptr, w.trans.data(), sizeof(float4) * num_trans,
                          hipMemcpyHostToDevice, st));
   CSM_HIP(hipMemcpyAsync(ctx->rt3_points.ptr, xyz, sizeof(float) * 3 * n, hipMemcpyHostToDevice,
                          st));
   CSM_HIP(hipMemsetAsync(ctx->rt3_best.ptr, 0, sizeof(unsigned long long), st));
   const Brick3& gb = grid->brick;
   // v2 addresses the padded brick with 24-bit row products and a 32-bit byte
-  // offset; larger bricks take the v1 kernel.
+  // offset; larger bricks take the v1 kernel (no scoring mode).
   const bool v2 = !std::getenv("CSM_RT3D_V1") &&
                   static_cast<int64_t>(gb.nx + 2) * (gb.ny + 2) * (gb.nz + 2) < (int64_t{1} << 29) &&
                   static_cast<int64_t>(gb.ny + 2) * (gb.nz + 2) < (int64_t{1} << 24);
+  if (dscores && !v2) return CSM_ERANGE;
   if (v2 && !grid->prob_pad_ready) {
     csm_hybrid_grid* g = const_cast<csm_hybrid_grid*>(grid);
     if ((rc = g->prob_pad.Reserve(sizeof(float) * (gb.nx + 2) * (gb.ny + 2) * (gb.nz + 2))))
@@ -320,7 +342,6 @@ int csm_rt3d_match(csm_context* ctx, const csm_rt_options* o, const csm_hybrid_g
     CSM_HIP(LaunchPadProbBrick(grid->prob.as<float>(), gb, g->prob_pad.as<float>(), st));
     g->prob_pad_ready = true;
   }
-
   if (ctx->timing) CSM_HIP(hipEventRecord(ctx->ev0, st));
   for (int64_t t0 = 0; t0 < num_trans; t0 += kRt3dThreads) {
     const int cnt = static_cast<int>(std::min<int64_t>(kRt3dThreads, num_trans - t0));
@@ -329,7 +350,8 @@ int csm_rt3d_match(csm_context* ctx, const csm_rt_options* o, const csm_hybrid_g
                                ctx->rt3_points.as<float>(), n, drot, dangle,
                                ctx->rt3_trans.as<float4>(), cnt, static_cast<int>(t0),
                                o->translation_delta_cost_weight, o->rotation_delta_cost_weight,
-                               ctx->rt3_best.as<unsigned long long>()));
+                               ctx->rt3_best.as<unsigned long long>(), dscores,
+                               static_cast<int>(num_trans)));
     else
       CSM_HIP(LaunchRt3dScore(static_cast<int>(num_rot), st, grid->prob.as<float>(), gb, res,
                               ctx->rt3_points.as<float>(), n, drot, dangle,
@@ -338,8 +360,7 @@ int csm_rt3d_match(csm_context* ctx, const csm_rt_options* o, const csm_hybrid_g
                               ctx->rt3_best.as<unsigned long long>()));
   }
   if (ctx->timing) CSM_HIP(hipEventRecord(ctx->ev1, st));
-  unsigned long long key = 0;
-  CSM_HIP(hipMemcpyAsync(&key, ctx->rt3_best.ptr, sizeof(key), hipMemcpyDeviceToHost, st));
+  if (key) CSM_HIP(hipMemcpyAsync(key, ctx->rt3_best.ptr, sizeof(*key), hipMemcpyDeviceToHost, st));
   CSM_HIP(hipStreamSynchronize(st));
   if (ctx->timing) {
     float ms = 0.f;
@@ -348,17 +369,79 @@ int csm_rt3d_match(csm_context* ctx, const csm_rt_options* o, const csm_hybrid_g
     ctx->t.rt3d_kernel_ms += ms;
     ctx->t.rt3d_lookups += static_cast<double>(num_trans) * num_rot * n;
   }
+  return CSM_OK;
+}
+
+}  // namespace
+
+int csm_rt3d_match(csm_context* ctx, const csm_rt_options* o, const csm_hybrid_grid* grid,
+                   const csm_pose3d* initial, const float* xyz, int32_t n, float* score,
+                   csm_pose3d* pose) {
+  if (!ctx || !o || !grid || !initial || !score || !pose || n <= 0 || !xyz) return CSM_EINVAL;
+  if (grid->ctx != ctx) return CSM_EINVAL;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  int rc;
+  if ((rc = EnsureDevice3(ctx))) return rc;
+  Rt3dWindow w;
+  if ((rc = MakeRt3dWindow(o, grid->resolution, initial, xyz, n, &w))) return rc;
+  unsigned long long key = 0;
+  if ((rc = RunRt3d(ctx, o, grid, xyz, n, w, w.rot.data(), w.angle.data(), w.num_rot, &key,
+                    nullptr)))
+    return rc;
   if (key == 0) return CSM_EHIP;
   const uint32_t low = static_cast<uint32_t>(key & 0xffffffffu);
   const uint32_t idx = 0xffffffffu - low;
-  const int64_t t = idx / num_rot, r = idx % num_rot;
+  const int64_t t = idx / w.num_rot, r = idx % w.num_rot;
   const uint32_t bits = static_cast<uint32_t>(key >> 32);
   float s;
   std::memcpy(&s, &bits, sizeof(s));
   *score = s;
-  const float4 q = rot[r];
-  const float4 T = trans[t];
+  const float4 q = w.rot[r];
+  const float4 T = w.trans[t];
   *pose = ToPose(V3{T.x, T.y, T.z}, Q4{q.w, q.x, q.y, q.z});
+  return CSM_OK;
+}
+
+int csm_rt3d_window(const csm_rt_options* o, float resolution, const float* xyz, int32_t n,
+                    int32_t* num_translations, int32_t* num_rotations) {
+  if (!o || !(resolution > 0.f) || n <= 0 || !xyz) return CSM_EINVAL;
+  const csm_pose3d id{{0., 0., 0.}, {1., 0., 0., 0.}};
+  Rt3dWindow w;
+  int rc;
+  if ((rc = MakeRt3dWindow(o, resolution, &id, xyz, n, &w))) return rc;
+  if (num_translations) *num_translations = static_cast<int32_t>(w.num_trans);
+  if (num_rotations) *num_rotations = static_cast<int32_t>(w.num_rot);
+  return CSM_OK;
+}
+
+int csm_rt3d_score_rotations(csm_context* ctx, const csm_rt_options* o,
+                             const csm_hybrid_grid* grid, const csm_pose3d* initial,
+                             const float* xyz, int32_t n, const int32_t* rotations,
+                             int32_t num_rotations, float* scores) {
+  if (!ctx || !o || !grid || !initial || n <= 0 || !xyz || num_rotations < 0 ||
+      (num_rotations > 0 && (!rotations || !scores)))
+    return CSM_EINVAL;
+  if (grid->ctx != ctx) return CSM_EINVAL;
+  if (num_rotations == 0) return CSM_OK;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  int rc;
+  if ((rc = EnsureDevice3(ctx))) return rc;
+  Rt3dWindow w;
+  if ((rc = MakeRt3dWindow(o, grid->resolution, initial, xyz, n, &w))) return rc;
+  std::vector<float4> rot(static_cast<size_t>(num_rotations));
+  std::vector<float> angle(static_cast<size_t>(num_rotations));
+  for (int32_t k = 0; k < num_rotations; ++k) {
+    if (rotations[k] < 0 || rotations[k] >= w.num_rot) return CSM_EINVAL;
+    rot[k] = w.rot[rotations[k]];
+    angle[k] = w.angle[rotations[k]];
+  }
+  DevBuf dscores;
+  const size_t count = static_cast<size_t>(num_rotations) * w.num_trans;
+  if ((rc = dscores.Reserve(sizeof(float) * count))) return rc;
+  if ((rc = RunRt3d(ctx, o, grid, xyz, n, w, rot.data(), angle.data(), num_rotations, nullptr,
+                    dscores.as<float>())))
+    return rc;
+  CSM_HIP(hipMemcpy(scores, dscores.ptr, sizeof(float) * count, hipMemcpyDeviceToHost));
   return CSM_OK;
 }
 

@@ -226,7 +226,8 @@ rt3d_score2(const float* __restrict__ pad, int pnx, int pny, int pnz, int ox, in
             float res, float inv, const float* __restrict__ points, int n,
             const float4* __restrict__ rot, const float* __restrict__ rot_angle,
             const float4* __restrict__ trans, int num_trans, int t_base, int num_rot, double wt,
-            double wr, unsigned long long* __restrict__ best) {
+            double wr, unsigned long long* __restrict__ best, float* __restrict__ scores,
+            int scores_pitch) {
   __shared__ float4 rp[kRt3Rpb][kRt3Tile];
   __shared__ unsigned long long red[768 / 64];
   const int tid = threadIdx.x;
@@ -308,7 +309,11 @@ rt3d_score2(const float* __restrict__ pad, int pnx, int pny, int pnz, int ox, in
     score = static_cast<float>(static_cast<double>(score) * exp(-(e * e)));
     const unsigned idx = static_cast<unsigned>(t_base + t) * static_cast<unsigned>(num_rot) + r;
     key = (static_cast<unsigned long long>(__float_as_uint(score)) << 32) | (0xffffffffu - idx);
+    // Test-visible scoring of a rotation subset (csm_rt3d_score_rotations):
+    // every candidate's score, no reduction.
+    if (scores) scores[static_cast<int64_t>(r) * scores_pitch + t_base + t] = score;
   }
+  if (scores) return;  // uniform: no reduction in the scoring mode
   for (int m = 32; m > 0; m >>= 1) {
     const unsigned long long o = __shfl_xor(key, m, 64);
     key = o > key ? o : key;
@@ -1314,12 +1319,13 @@ hipError_t LaunchRt3dScore2(int num_rot, hipStream_t st, const float* pad,
                             const Brick3& gb, float res, const float* points, int n,
                             const float4* rot, const float* rot_angle, const float4* trans,
                             int num_trans, int t_base, double wt, double wr,
-                            unsigned long long* best) {
+                            unsigned long long* best, float* scores, int scores_pitch) {
   const int threads = (kRt3Rpb * num_trans + 63) / 64 * 64;
   const int blocks = (num_rot + kRt3Rpb - 1) / kRt3Rpb;
   hipLaunchKernelGGL(rt3d_score2, dim3(blocks), dim3(threads), 0, st, pad, gb.nx + 2, gb.ny + 2,
                      gb.nz + 2, gb.ox, gb.oy, gb.oz, res, 1.f / res, points, n, rot, rot_angle,
-                     trans + t_base, num_trans, t_base, num_rot, wt, wr, best);
+                     trans + t_base, num_trans, t_base, num_rot, wt, wr, best, scores,
+                     scores_pitch);
   return hipGetLastError();
 }
 

@@ -88,6 +88,37 @@ class RealTimeCorrelativeScanMatcher3D:
                                         C.byref(score), C.byref(out)), "csm_rt3d_match")
         return float(score.value), out.as_tuple()
 
+    def _opts(self):
+        o = self.options
+        return RtOptions(o.linear_search_window, o.angular_search_window,
+                         o.translation_delta_cost_weight, o.rotation_delta_cost_weight)
+
+    def window(self, point_cloud, resolution):
+        """GenerateExhaustiveSearchTransforms' window: (num_translations,
+        num_rotations); candidate index = t * num_rotations + r."""
+        pts = _f32_points(point_cloud)
+        nt, nr = C.c_int32(), C.c_int32()
+        opts = self._opts()
+        _check(self._lib.csm_rt3d_window(C.byref(opts), float(resolution), _ptr(pts, C.c_float),
+                                         len(pts), C.byref(nt), C.byref(nr)), "csm_rt3d_window")
+        return nt.value, nr.value
+
+    def score_rotations(self, initial_pose_estimate, point_cloud, grid: HybridGrid, rotations):
+        """Test-visible: ScoreCandidate of every translation for the given
+        rotation indices, by Match's kernel -> (len(rotations), num_translations)."""
+        pts = _f32_points(point_cloud)
+        rot = np.ascontiguousarray(np.asarray(rotations, np.int32))
+        nt, _ = self.window(pts, grid.resolution)
+        out = np.zeros((len(rot), nt), np.float32)
+        opts = self._opts()
+        init = _pose(initial_pose_estimate)
+        _check(self._lib.csm_rt3d_score_rotations(self.context.handle, C.byref(opts), grid.handle,
+                                                  C.byref(init), _ptr(pts, C.c_float), len(pts),
+                                                  _ptr(rot, C.c_int32), len(rot),
+                                                  _ptr(out, C.c_float)),
+               "csm_rt3d_score_rotations")
+        return out
+
 
 @dataclass
 class FastCorrelativeScanMatcherOptions3D:

@@ -308,6 +308,21 @@ int csm_rt3d_match(csm_context* ctx, const csm_rt_options* options, const csm_hy
                    const csm_pose3d* initial, const float* points_xyz, int32_t n, float* score,
                    csm_pose3d* pose);
 
+/* The search window Match uses (GenerateExhaustiveSearchTransforms, :55-95):
+ * (2L+1)^3 translations and (2A+1)^3 rotations for this cloud and grid
+ * resolution. Candidate index = t * num_rotations + r. */
+int csm_rt3d_window(const csm_rt_options* options, float resolution, const float* points_xyz,
+                    int32_t n, int32_t* num_translations, int32_t* num_rotations);
+
+/* Test-visible: ScoreCandidate (:97-113, score after the exp penalty) of
+ * every translation for each of `num_rotations` rotation indices of the
+ * window, computed by the same kernel as Match; scores[k * num_translations
+ * + t] for rotations[k]. */
+int csm_rt3d_score_rotations(csm_context* ctx, const csm_rt_options* options,
+                             const csm_hybrid_grid* grid, const csm_pose3d* initial,
+                             const float* points_xyz, int32_t n, const int32_t* rotations,
+                             int32_t num_rotations, float* scores);
+
 /* ---- FastCorrelativeScanMatcher3D --------------------------------------------
  * proto::FastCorrelativeScanMatcherOptions3D
  * (proto/scan_matching/fast_correlative_scan_matcher_options_3d.proto). */

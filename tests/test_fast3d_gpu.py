@@ -336,3 +336,88 @@ def test_large_clouds_match_oracle(csm, oracle, world3d):
             assert np.float32(single.score) == np.float32(r.score)
             assert single.pose_estimate == r.pose.as_tuple()
     assert res[3].status == csm.CSM_ERANGE
+
+
+def _qmul(a, b):
+    return (a[0] * b[0] - a[1] * b[1] - a[2] * b[2] - a[3] * b[3],
+            a[0] * b[1] + a[1] * b[0] + a[2] * b[3] - a[3] * b[2],
+            a[0] * b[2] - a[1] * b[3] + a[2] * b[0] + a[3] * b[1],
+            a[0] * b[3] + a[1] * b[2] - a[2] * b[1] + a[3] * b[0])
+
+
+def test_rt3d_c4_full_window(csm, oracle):
+    """BASELINE config C4 at its full size: the bench's 64-ring scan (~55k
+    points) against a 0.10 m HybridGrid, +-0.3 m / +-15 deg (343 translations x
+    ~420k rotations, 1.45e8 candidates), yawed initial pose. The whole window
+    is searched on the device; the oracle cannot score 1.45e8 candidates
+    (~27 h), so parity is checked (1) on the winner: the oracle scores the
+    winning candidate index to the same float (exp penalty: 1e-6 relative);
+    (2) on 16 whole rotations scored by Match's kernel (the winner's, the two
+    window corners and 13 seeded ones, 5488 candidates): every one of them
+    equals the oracle's score on a 400-candidate sample including the full
+    winner row, and none beats the winner."""
+    w = csm.SyntheticWorld3D(num_nodes=2, num_submaps=1, world_x=20.0, world_y=20.0, world_z=5.0,
+                             num_boxes=8, max_range=14.0, seed=20250127 + 3)
+    c = int(w.submap_nodes[0])
+    cloud = np.ascontiguousarray(w.raw[c], np.float32)
+    grid = csm.HybridGrid(w.high_resolution, *w.high_cells[0])
+    (tx, ty, tz), q = w.node_in_submap(c, 0)
+    dyaw = math.radians(4.0)
+    q0 = (q[0] * math.cos(dyaw / 2) - q[3] * math.sin(dyaw / 2), 0.0, 0.0,
+          q[3] * math.cos(dyaw / 2) + q[0] * math.sin(dyaw / 2))
+    init = ((tx + 0.12, ty - 0.08, tz + 0.05), q0)
+    opts = (0.3, math.radians(15.0), 0.1, 0.1)
+    m = csm.RealTimeCorrelativeScanMatcher3D(csm.RealTimeCorrelativeScanMatcherOptions(*opts))
+    nt, nr = m.window(cloud, w.high_resolution)
+    assert len(cloud) > 40000 and nt == 343 and nr > 100000
+    score, pose = m.Match(init, cloud, grid)
+    # Recover the winner's (t, r): translations are init * (x, y, z) * res,
+    # rotations init.q * AngleAxis((rx, ry, rz) * step).
+    og = oracle.hybrid_grid(w.high_resolution)
+    og.set_values(*w.high_cells[0])
+    import ctypes as C
+    Lw, Aw, stepw = C.c_int(), C.c_int(), C.c_float()
+    oo = np.asarray(opts, np.float64)
+    oracle.lib.oracle_rt3d_window(oo.ctypes.data_as(C.POINTER(C.c_double)),
+                                  float(w.high_resolution),
+                                  cloud.ctypes.data_as(C.POINTER(C.c_float)), len(cloud),
+                                  C.byref(Lw), C.byref(stepw), C.byref(Aw))
+    L, A, step = Lw.value, Aw.value, float(stepw.value)
+    nl, na = 2 * L + 1, 2 * A + 1
+    assert nl ** 3 == nt and na ** 3 == nr
+    qi = tuple(float(v) for v in init[1])
+    nq = math.sqrt(sum(v * v for v in qi))
+    qi = tuple(v / nq for v in qi)
+    qinv = (qi[0], -qi[1], -qi[2], -qi[3])
+    d = np.asarray(pose[0]) - np.asarray(init[0])
+    v = _qmul(_qmul(qinv, (0.0,) + tuple(d)), qi)[1:]
+    x, y, z = (int(round(c_ / w.high_resolution)) for c_ in v)
+    t = ((z + L) * nl + (y + L)) * nl + (x + L)
+    qs = _qmul(qinv, pose[1])
+    s_ = math.sqrt(sum(c_ * c_ for c_ in qs[1:]))
+    ang = 2 * math.atan2(s_, qs[0])
+    axis = [c_ / s_ for c_ in qs[1:]] if s_ > 0 else [0.0, 0.0, 0.0]
+    rx, ry, rz = (int(round(a_ * ang / step)) for a_ in axis)
+    r = ((rz + A) * na + (ry + A)) * na + (rx + A)
+    win_index = t * nr + r
+    ref_score, ref_pose = oracle.rt3d_score(og, opts, init, cloud, win_index)
+    assert np.allclose(ref_pose[0], pose[0], atol=1e-6) and np.allclose(ref_pose[1], pose[1],
+                                                                        atol=1e-6)
+    assert math.isclose(score, ref_score, rel_tol=1e-6), (score, ref_score)
+    rng = np.random.RandomState(17)
+    rots = [r, 0, nr - 1] + [int(v) for v in rng.randint(0, nr, 13)]
+    scores = m.score_rotations(init, cloud, grid, rots)
+    assert scores.shape == (16, nt)
+    assert scores[0, t] == np.float32(score)
+    # Nothing in the subset beats the winner (ties: the smaller index wins).
+    for k, rr in enumerate(rots):
+        for tt in np.nonzero(scores[k] >= np.float32(score))[0]:
+            assert scores[k, tt] == np.float32(score) and int(tt) * nr + rr >= win_index
+    sample = [(0, tt) for tt in range(nt)] + [(int(k), int(tt)) for k, tt in
+                                              zip(rng.randint(1, 16, 57), rng.randint(0, nt, 57))]
+    exact = 0
+    for k, tt in sample:
+        ref, _ = oracle.rt3d_score(og, opts, init, cloud, tt * nr + rots[k])
+        assert math.isclose(float(scores[k, tt]), ref, rel_tol=1e-6), (k, tt, scores[k, tt], ref)
+        exact += float(scores[k, tt]) == ref
+    assert exact >= 0.95 * len(sample)
