@@ -557,7 +557,8 @@ def fast3d_bench(csm, ctx, args, rank=0, world_size=1, dist=None, coll_dev=None,
             low = np.ascontiguousarray(np.concatenate(w.low), np.float32)
             hists = np.ascontiguousarray(np.stack(w.node_hist), np.float32)
             nq = np.ascontiguousarray([w.node_rotation(i) for i in range(w.num_nodes)], np.float64)
-            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+            cpu = host_cpu()
+            threads = args.cpu_threads or cpu["usable_cpus"]
             rng = np.random.RandomState(777)
             P = C.POINTER
             hv = (C.c_void_p * len(handles))(*handles)
@@ -566,21 +567,23 @@ def fast3d_bench(csm, ctx, args, rank=0, world_size=1, dist=None, coll_dev=None,
                 ps = rng.randint(0, w.num_submaps, k).astype(np.int32)
                 pn = rng.randint(0, w.num_nodes, k).astype(np.int32)
                 matched = np.zeros(k, np.int32)
-                return orc.lib.oracle_fast3d_match_pairs(
+                task = np.zeros(k)
+                wall = orc.lib.oracle_fast3d_match_pairs(
                     hv, high.ctypes.data_as(P(C.c_float)), hoff.ctypes.data_as(P(C.c_int64)),
                     low.ctypes.data_as(P(C.c_float)), loff.ctypes.data_as(P(C.c_int64)),
                     hists.ctypes.data_as(P(C.c_float)), hists.shape[1],
                     nq.ctypes.data_as(P(C.c_double)), ps.ctypes.data_as(P(C.c_int32)),
                     pn.ctypes.data_as(P(C.c_int32)), k, threads, 0.6,
-                    matched.ctypes.data_as(P(C.c_int32)))
+                    matched.ctypes.data_as(P(C.c_int32)), task.ctypes.data_as(P(C.c_double)))
+                return wall, task
 
-            probe = run(threads)
+            probe, _ = run(threads)
             k = min(20000, max(threads, int(threads * 10.0 / max(probe, 1e-3))))
-            sec = run(k)
-            out["cpu_baseline"] = {"value": k / sec, "unit": "pairs/s", "cores": threads,
-                                   "kind": "port",
-                                   "sample": f"{k} uniformly sampled pairs of the same queue, "
-                                             f"{sec:.1f} s on {threads} threads (oracle, -O3)"}
+            sec, task = run(k)
+            cb = summarize_cpu(k, sec, task, threads, cpu, [], "uniformly sampled pairs of the same queue")
+            cb["sample"] = (f"{k} uniformly sampled pairs of the same queue, {sec:.1f} s on "
+                            f"{threads} threads (oracle, -O3)")
+            out["cpu_baseline"] = cb
         except OSError:
             pass
     return out

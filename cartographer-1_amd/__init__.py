@@ -333,6 +333,18 @@ _SIGNATURES = {
                                              C.POINTER(C.c_uint16), C.c_int64]),
     "csm_pbstream_submap3d_histogram": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_float),
                                                   C.c_int32]),
+    "csm_comm_get_unique_id": (C.c_int, [C.POINTER(C.c_uint8)]),
+    "csm_comm_create_rccl": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.POINTER(C.c_uint8),
+                                       C.POINTER(C.c_void_p)]),
+    "csm_comm_create_tcp": (C.c_int, [C.c_int32, C.c_int32, C.c_char_p, C.c_int32,
+                                      C.POINTER(C.c_void_p)]),
+    "csm_comm_destroy": (None, [C.c_void_p]),
+    "csm_comm_rank": (C.c_int32, [C.c_void_p]),
+    "csm_comm_size": (C.c_int32, [C.c_void_p]),
+    "csm_comm_gather": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.POINTER(C.c_int64)]),
+    "csm_comm_gathered": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.POINTER(C.c_int64)]),
+    "csm_comm_allreduce_i64": (C.c_int, [C.c_void_p, C.POINTER(C.c_int64), C.c_int32, C.c_int32]),
+    "csm_comm_barrier": (C.c_int, [C.c_void_p]),
     "csm_strerror": (C.c_char_p, [C.c_int]),
 }
 
@@ -1181,6 +1193,90 @@ class DeviceBuffer:
     def __del__(self):
         try:
             self.free()
+        except Exception:
+            pass
+
+
+COMM_ID_BYTES = 128
+REDUCE_SUM, REDUCE_MAX = 0, 1
+
+
+class Comm:
+    """The C-ABI's multi-GPU hand-off (csm_comm_*): gather of per-rank byte
+    blobs to rank 0 and small integer all-reduces, over RCCL (one process per
+    GPU) or TCP between host processes (CPU tests / rehearsals)."""
+
+    def __init__(self, handle, lib):
+        self.h, self._lib = handle, lib
+
+    @staticmethod
+    def unique_id() -> bytes:
+        lib = load_library()
+        buf = (C.c_uint8 * COMM_ID_BYTES)()
+        _check(lib.csm_comm_get_unique_id(buf), "csm_comm_get_unique_id")
+        return bytes(buf)
+
+    @classmethod
+    def rccl(cls, context: "Context", rank: int, world_size: int, uid: bytes) -> "Comm":
+        lib = load_library()
+        if len(uid) != COMM_ID_BYTES:
+            raise ValueError("RCCL unique id must be 128 bytes")
+        buf = (C.c_uint8 * COMM_ID_BYTES).from_buffer_copy(uid)
+        h = C.c_void_p()
+        _check(lib.csm_comm_create_rccl(context.handle, rank, world_size, buf, C.byref(h)),
+               "csm_comm_create_rccl")
+        return cls(h.value, lib)
+
+    @classmethod
+    def tcp(cls, rank: int, world_size: int, host: str = "127.0.0.1", port: int = 29601) -> "Comm":
+        lib = load_library()
+        h = C.c_void_p()
+        _check(lib.csm_comm_create_tcp(rank, world_size, host.encode(), port, C.byref(h)),
+               "csm_comm_create_tcp")
+        return cls(h.value, lib)
+
+    @property
+    def rank(self) -> int:
+        return int(self._lib.csm_comm_rank(self.h))
+
+    @property
+    def size(self) -> int:
+        return int(self._lib.csm_comm_size(self.h))
+
+    def gather(self, blob: bytes):
+        """Collective. Rank 0 gets the list of every rank's blob (rank order);
+        the other ranks get None."""
+        data = C.create_string_buffer(blob, len(blob)) if blob else None
+        total = C.c_int64()
+        _check(self._lib.csm_comm_gather(self.h, data, len(blob), C.byref(total)), "csm_comm_gather")
+        if self.rank != 0:
+            return None
+        out = C.create_string_buffer(max(total.value, 1))
+        sizes = (C.c_int64 * self.size)()
+        _check(self._lib.csm_comm_gathered(self.h, out, total.value, sizes), "csm_comm_gathered")
+        raw, blobs, at = out.raw, [], 0
+        for n in sizes:
+            blobs.append(raw[at:at + n])
+            at += n
+        return blobs
+
+    def allreduce(self, values, op: int = REDUCE_SUM) -> np.ndarray:
+        v = np.ascontiguousarray(values, np.int64).copy()
+        _check(self._lib.csm_comm_allreduce_i64(self.h, v.ctypes.data_as(C.POINTER(C.c_int64)),
+                                                len(v), op), "csm_comm_allreduce_i64")
+        return v
+
+    def barrier(self):
+        _check(self._lib.csm_comm_barrier(self.h), "csm_comm_barrier")
+
+    def close(self):
+        if self.h:
+            self._lib.csm_comm_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
         except Exception:
             pass
 

@@ -49,7 +49,17 @@ struct SubmapDesc {
   int32_t quad_w[kMaxLevels];
   int32_t quad_h[kMaxLevels];
   int32_t quad_bytes[kMaxLevels];
+  // Scan clustering per child level (DESIGN.md §5 "Clustered entries"):
+  // quad level d holds M_d(c) = max of level 0 over [c, c + 2^d + k - 1)
+  // per axis, k = 2^cshift[d], so one entry per occupied k x k cluster of
+  // scan cells (weighted by its point count) bounds every point in it.
+  // k = 1 at level 0 (exact leaf scores). Quad index X' = cell + offset +
+  // quad_bias[d], quad_bias = (2^d - 1) + (k - 1) + 2^d.
+  int32_t cshift[kMaxLevels];
+  int32_t quad_bias[kMaxLevels];
 };
+
+constexpr int kMaxClusterShift = 3;  // clusters of 1, 2, 4, 8 cells per side
 
 // One (node, submap) search.
 struct PairDesc {
@@ -85,8 +95,8 @@ struct WorkQueues2 {
   int32_t rot_chunk;
 };
 
-constexpr int kStack2 = 2048;   // v4 per-workgroup DFS stack entries in LDS
-constexpr int kSpill2 = 6144;   // further entries per workgroup in global memory
+constexpr int kStack2 = 1024;   // v4 per-workgroup DFS stack entries in LDS
+constexpr int kSpill2 = 7168;   // further entries per workgroup in global memory
 constexpr int kBatchNodes = 64; // nodes expanded per batch (256 children)
 
 // Best leaf per pair, packed for a 64-bit atomicMax:

@@ -42,6 +42,26 @@ int AutoSearchDepth(int configured, int nx, int ny) {
   return std::max(d, configured);
 }
 
+// Scan cluster size per child level (SubmapDesc::cshift): k = 1, 2, 2, 4, 4,
+// 8, ... cells per side (log2), chosen by tools/frontier_sim.py (cluster) on
+// the C2 world: 0.39x the lookups of exact per-level bounds. Level 0 is
+// always exact (k = 1) and k <= 2^level. CSM_CLUSTER="s0,s1,..." overrides.
+void ClusterShifts(int32_t* out) {
+  static const int kDefault[kMaxLevels] = {0, 1, 1, 2, 2, 3, 3, 3, 3, 3, 3, 3};
+  for (int l = 0; l < kMaxLevels; ++l) out[l] = kDefault[l];
+  if (const char* env = std::getenv("CSM_CLUSTER")) {
+    int l = 0;
+    for (const char* c = env; *c && l < kMaxLevels; ++l) {
+      out[l] = std::atoi(c);
+      while (*c && *c != ',') ++c;
+      if (*c == ',') ++c;
+    }
+    for (; l < kMaxLevels; ++l) out[l] = out[l - 1];
+  }
+  for (int l = 0; l < kMaxLevels; ++l)
+    out[l] = std::max(0, std::min({out[l], l, kMaxClusterShift}));
+}
+
 }  // namespace
 }  // namespace csm
 
@@ -237,9 +257,16 @@ int RunBatch(csm_context* ctx, csm_fast2d* const* submaps, int32_t num_submaps,
     wq2.pair_order = wq.pair_order;
     wq2.chunk_prefix = wq.chunk_prefix;
     wq2.block_first = ctx->blocks.as<int32_t>();
-    // rot_chunk * npad cells (4 B) and run counts (1 B), 16-B aligned.
-    const size_t dyn_lds = (static_cast<size_t>(rc) * max_npad * 5 + 15) & ~size_t{15};
-    const int per_cu = std::max(1, std::min(8, static_cast<int>((160 * 1024) / (dyn_lds + 10 * 1024))));
+    // Per rotation: npad raw cells / k = 1 entries and capc cluster-list
+    // entries, 4 B cell + 1 B count each, 16-B aligned. capc = 3/4 npad holds
+    // the three cluster lists of a typical scan (0.55 npad on C2); a list
+    // that does not fit falls back to a finer one in the kernel.
+    int capc = (3 * max_npad / 4 + 63) & ~63;
+    const int lds_cap = 96 * 1024;
+    while (capc > 0 && static_cast<size_t>(rc) * (max_npad + capc) * 5 > lds_cap) capc -= 64;
+    const size_t dyn_lds = (static_cast<size_t>(rc) * (max_npad + capc) * 5 + 15) & ~size_t{15};
+    const size_t static_lds = 12 * 1024;  // V4Shared (8 KiB stack + batch state)
+    const int per_cu = std::max(1, std::min(8, static_cast<int>((160 * 1024) / (dyn_lds + static_lds))));
     const int grid = static_cast<int>(std::min<int64_t>(static_cast<int64_t>(ctx->num_cus) * per_cu,
                                                         std::max<int64_t>(total_chunks, 1)));
     // DFS stack spill: kSpill2 entries per persistent workgroup.
@@ -250,7 +277,7 @@ int RunBatch(csm_context* ctx, csm_fast2d* const* submaps, int32_t num_submaps,
                                  ctx->rot_table.as<float2>(), wq2,
                                  ctx->counters.as<unsigned long long>(), ctx->best.as<uint64_t>(),
                                  ctx->status.as<int32_t>(), ctx->stats.as<unsigned long long>(),
-                                 ctx->spill.as<uint2>(), max_npad));
+                                 ctx->spill.as<uint2>(), max_npad, capc));
   } else {
     const size_t dyn_lds = static_cast<size_t>(rc) * max_npad * sizeof(uint32_t);
     const int grid = static_cast<int>(std::min<int64_t>(static_cast<int64_t>(ctx->num_cus) * 4,
@@ -289,9 +316,9 @@ int RunBatch(csm_context* ctx, csm_fast2d* const* submaps, int32_t num_submaps,
     const unsigned long long* kp = stats_host + 2 + 2 * kMaxLevels;
     if (std::getenv("CSM_PROFILE2D") && (kp[0] | kp[1] | kp[2]))
       std::fprintf(stderr,
-                   "fast2d phases (Mcycles, thread 0 sums): discretize+shrink %.1f control %.1f "
-                   "score %.1f | batches %llu\n",
-                   kp[0] / 1e6, kp[1] / 1e6, kp[2] / 1e6, kp[3]);
+                   "fast2d phases (Mcycles, thread 0 sums): setup %.1f (entry lists %.1f) control "
+                   "%.1f score %.1f\n",
+                   kp[0] / 1e6, kp[3] / 1e6, kp[1] / 1e6, kp[2] / 1e6);
   }
 
   // ---- decode -----------------------------------------------------------------
@@ -453,10 +480,13 @@ int csm_fast2d_create(csm_context* ctx, const csm_map_limits* limits,
     total += (static_cast<size_t>(d.zero_index[l]) + 1 + 255) & ~size_t(255);
   }
   std::vector<size_t> qoffs(depth);
+  ClusterShifts(d.cshift);
   for (int l = 0; l < depth; ++l) {
     const int h = 1 << l;
-    d.quad_w[l] = d.wide_nx[l] + h;
-    d.quad_h[l] = d.wide_ny[l] + h;
+    const int km1 = (1 << d.cshift[l]) - 1;
+    d.quad_bias[l] = (h - 1) + km1 + h;
+    d.quad_w[l] = d.wide_nx[l] + km1 + h;
+    d.quad_h[l] = d.wide_ny[l] + km1 + h;
     d.quad_pws[l] = (d.quad_w[l] + 2 * h - 1) / (2 * h);
     d.quad_pph[l] = (d.quad_h[l] + 2 * h - 1) / (2 * h);
     const size_t qb = static_cast<size_t>(2 * h) * (2 * h) * d.quad_pws[l] * d.quad_pph[l] * 4;
@@ -491,7 +521,7 @@ int csm_fast2d_create(csm_context* ctx, const csm_map_limits* limits,
                                 1 << (l - 1), st));
   }
   for (int l = 0; l < depth; ++l)
-    CSM_HIP(LaunchPyramidQuad(d.level[l], d.wide_nx[l], d.wide_ny[l], l,
+    CSM_HIP(LaunchPyramidQuad(d.level[l], d.wide_nx[l], d.wide_ny[l], l, (1 << d.cshift[l]) - 1,
                               const_cast<uint32_t*>(d.quad[l]), d.quad_w[l], d.quad_h[l],
                               d.quad_pws[l], d.quad_pph[l], d.quad_bytes[l] / 4, st));
   // Correspondence costs (Grid2D::GetCorrespondenceCost, grid_2d.cc) for the

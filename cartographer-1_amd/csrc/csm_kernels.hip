@@ -42,6 +42,26 @@ __device__ __forceinline__ int WaveMax(int v) {
 }
 __device__ __forceinline__ int Uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// Wave-wide max / sum without the LDS crossbar: DPP within each 16-lane row
+// (quad perms, half-row and row mirrors), then the four row results through
+// readlane. Every lane gets the result.
+template <typename Op>
+__device__ __forceinline__ int DppReduce(int v, Op op) {
+  v = op(v, __builtin_amdgcn_update_dpp(v, v, 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
+  v = op(v, __builtin_amdgcn_update_dpp(v, v, 0x4E, 0xF, 0xF, false));   // quad_perm [2,3,0,1]
+  v = op(v, __builtin_amdgcn_update_dpp(v, v, 0x141, 0xF, 0xF, false));  // row_half_mirror
+  v = op(v, __builtin_amdgcn_update_dpp(v, v, 0x140, 0xF, 0xF, false));  // row_mirror
+  const int r0 = __builtin_amdgcn_readlane(v, 0), r1 = __builtin_amdgcn_readlane(v, 16);
+  const int r2 = __builtin_amdgcn_readlane(v, 32), r3 = __builtin_amdgcn_readlane(v, 48);
+  return op(op(r0, r1), op(r2, r3));
+}
+__device__ __forceinline__ int DppMax(int v) {
+  return DppReduce(v, [](int a, int b) { return max(a, b); });
+}
+__device__ __forceinline__ int DppSum(int v) {
+  return DppReduce(v, [](int a, int b) { return a + b; });
+}
+
 __device__ __forceinline__ uint64_t LoadBest(const uint64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -518,15 +538,17 @@ constexpr int kRootChunk = 192;  // virtual roots pushed at a time
 
 // ---------------------------------------------------------------- K1c ------
 
-// Quad layout of level d (h = 2^d): the dword for quad cell (X', Y'),
-// X' < qw = wnx + h, Y' < qh = wny + h, packs the children values of a node
-// whose child (0,0) sits at wide cell (X, Y) = (X' - h, Y' - h):
-// byte0 G(X, Y), byte1 G(X, Y+h), byte2 G(X+h, Y), byte3 G(X+h, Y+h);
-// G = 0 outside the wide grid. Cells are stored polyphase with period
-// P = 2h: plane (X' mod P, Y' mod P), entry (X' / P, Y' / P), row stride pws,
-// plane size pws * pph dwords. Same-level nodes of one rotation sit on one
-// P-lattice, so one point's lookups by sibling nodes are adjacent dwords.
-__global__ void pyramid_quad(const uint8_t* __restrict__ level, int wnx, int wny, int log_h,
+// Quad layout of level d (h = 2^d) for scan clusters of k = km1 + 1 cells
+// per side: M(c) = max of level 0 over [c, c + h + km1) per axis = the max of
+// G_d at c and c + km1 (km1 <= h). M's wide index is m = c + (h - 1) + km1.
+// The dword for quad cell (X', Y'), X' < qw = wnx + km1 + h, Y' < qh, packs
+// the children values of a node whose child (0,0) sits at M-wide cell
+// (X, Y) = (X' - h, Y' - h): byte0 M(X, Y), byte1 M(X, Y+h), byte2 M(X+h, Y),
+// byte3 M(X+h, Y+h); 0 outside. Cells are stored polyphase with period
+// P = 2h: plane (X' mod P, Y' mod P), entry (X' / P, Y' / P), row stride
+// pws, plane size pws * pph dwords. Same-level nodes of one rotation sit on
+// one P-lattice, so one point's lookups by sibling nodes are adjacent dwords.
+__global__ void pyramid_quad(const uint8_t* __restrict__ level, int wnx, int wny, int log_h, int km1,
                              uint32_t* __restrict__ out, int qw, int qh, int pws, int pph,
                              int total) {
   const int o = blockIdx.x * blockDim.x + threadIdx.x;
@@ -544,7 +566,13 @@ __global__ void pyramid_quad(const uint8_t* __restrict__ level, int wnx, int wny
     auto g = [&](int a, int b) -> uint32_t {
       return (a >= 0 && b >= 0 && a < wnx && b < wny) ? level[static_cast<size_t>(b) * wnx + a] : 0u;
     };
-    v = g(X, Y) | (g(X, Y + h) << 8) | (g(X + h, Y) << 16) | (g(X + h, Y + h) << 24);
+    // G_d wide index of M-wide cell m is m - km1.
+    auto m = [&](int a, int b) -> uint32_t {
+      a -= km1;
+      b -= km1;
+      return max(max(g(a, b), g(a + km1, b)), max(g(a, b + km1), g(a + km1, b + km1)));
+    };
+    v = m(X, Y) | (m(X, Y + h) << 8) | (m(X + h, Y) << 16) | (m(X + h, Y + h) << 24);
   }
   out[o] = v;
 }
@@ -552,23 +580,37 @@ __global__ void pyramid_quad(const uint8_t* __restrict__ level, int wnx, int wny
 // ---------------------------------------------------------------- K2-K4 v4 -
 //
 // A workgroup (4 waves) searches a chunk of R rotations of one pair at once.
-// The DFS stack mixes the chunk's rotations; a batch pops up to 16 nodes of
-// one level (best first) and scores their 2x2 children: a lane takes one node
-// and a strided subset of that node's rotated scan, and per point issues ONE
-// dword load from the quad layout that returns all four children's values.
-// The 4 waves split the points and meet in LDS; wave 0 combines, prunes,
-// pushes survivors sorted (best on top) and pops the next batch. Roots are
+// Each rotation's discretized scan becomes up to four entry lists: runs of
+// consecutive points in one cell (k = 1) and runs of consecutive points in
+// one k x k cluster (k = 2, 4, 8), each entry weighted by its point count.
+// A node at level d scores its 2x2 children at level d - 1 over the list of
+// that level's cluster size against quad level d - 1, whose values are
+// widened by k - 1 cells (SubmapDesc::cshift): every point of a cluster lies
+// in [q, q + k), so the cluster's count times the widened max bounds the
+// points' own terms. Leaves (level 0) use k = 1 and the exact values. The
+// bounds are looser than the reference's at coarse levels, so more inner
+// nodes survive, but every leaf that can reach the best sum is still scored
+// exactly: the result is unchanged.
+//
+// The DFS stack mixes the chunk's rotations; a batch pops up to 64 nodes
+// (deepest level first, best bound first): a lane takes one node and a
+// strided subset of that node's list, and per entry issues ONE dword load
+// from the quad layout that returns all four children's values. The 4 waves
+// split the entries and meet in LDS; all waves combine, prune and push
+// survivors sorted (best on top), wave 0 pops the next batch. Roots are
 // virtual nodes one level above the top lattice.
 
 constexpr int kMaxRotChunk = 16;
+constexpr int kLists = kMaxClusterShift + 1;
 
 struct V4Shared {
   uint2 stack[kStack2];  // w0: xo | yo << 16; w1: sum | rot << 22 | level << 27
   int part[kBatchNodes][4];  // children sums, accumulated by the 4 waves (LDS atomics)
-  int n_eff;                  // run-list length shared by the chunk's rotations
-  int run_len[kMaxRotChunk];  // each rotation's own run-list length
+  int list_off[kMaxRotChunk][kLists];  // entry list (rotation, cluster shift): first entry
+  int list_len[kMaxRotChunk][kLists];  // and length; a list that did not fit aliases a finer one
   int node_xo[kBatchNodes], node_yo[kBatchNodes], node_rot[kBatchNodes], node_level[kBatchNodes];
-  int nodes, done;
+  int node_off[kBatchNodes], node_len[kBatchNodes];  // the node's children-level list
+  int nodes, done, batch_len, batch_entries;
   int item_pair, item_chunk, queue;
   int sp;
   uint64_t best;
@@ -577,7 +619,7 @@ struct V4Shared {
   int vny[kMaxRotChunk];
   int root_prefix[kMaxRotChunk + 1];
   int vnext;
-  int range_error, batch_no, high_water;
+  int range_error, batch_no, high_water, long_runs;
   unsigned long long lv_cands[kMaxLevels];
   unsigned long long lv_batches[kMaxLevels];
 };
@@ -592,12 +634,12 @@ __device__ __forceinline__ void StackPut(V4Shared& sh, uint2* spill, int i, uint
   if (i < kStack2) sh.stack[i] = v; else spill[i - kStack2] = v;
 }
 
-// Scores the children of the batch's nodes over the chunk's run lists: entry
-// k of rotation r is a cell (pts) and the number of consecutive scan points
-// that fell into it (cnt, <= 255; 0 for padding). A child's sum is
-// sum_k cnt[k] * value, the reference's per-point sum regrouped.
-__device__ __forceinline__ void V4Score(V4Shared& sh, const uint32_t* pts, const uint8_t* cnt,
-                                        int npad, int n, const SubmapDesc& sm) {
+// Scores the children of the batch's nodes: lane (node, group) walks entries
+// g, g + groups, ... of the node's list (cells, counts). A child's sum is
+// sum_k cnt[k] * value over the list: the reference's per-point sum
+// regrouped at level 0, an upper bound of it at coarser levels.
+__device__ __forceinline__ void V4Score(V4Shared& sh, const uint32_t* cells, const uint8_t* cnts,
+                                        const SubmapDesc& sm) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nodes = Uniform(sh.nodes);
   const int groups = 64 / nodes;
@@ -606,18 +648,19 @@ __device__ __forceinline__ void V4Score(V4Shared& sh, const uint32_t* pts, const
   // Each node scores its children at its own child level: one descriptor
   // spans the whole pyramid, the level is a per-lane byte offset.
   const int level = sh.node_level[node] - 1;
-  const int h = 1 << level;
   const int qw = sm.quad_w[level], qh = sm.quad_h[level];
   const int qoff = sm.quad_off[level];
   const int sft = level + 1, pmask = (2 << level) - 1;
   const int pws4 = sm.quad_pws[level] * 4, ps4 = sm.quad_pws[level] * sm.quad_pph[level] * 4;
   const __amdgpu_buffer_rsrc_t rsrc = LevelRsrc(sm.pyramid_base, Uniform(sm.pyramid_bytes));
-  const uint32_t* P = pts + sh.node_rot[node] * npad;
-  const uint8_t* Cn = cnt + sh.node_rot[node] * npad;
-  const int cx = sh.node_xo[node] + (h - 1) + h;
-  const int cy = sh.node_yo[node] + (h - 1) + h;
-  const int quarter = (n + kWaves - 1) / kWaves;
-  const int s = Uniform(min(n, wave * quarter)), e = Uniform(min(n, wave * quarter + quarter));
+  const int off = sh.node_off[node], len = sh.node_len[node];
+  const uint32_t* P = cells + off;
+  const uint8_t* Cn = cnts + off;
+  const int cx = sh.node_xo[node] + sm.quad_bias[level];
+  const int cy = sh.node_yo[node] + sm.quad_bias[level];
+  const int blen = Uniform(sh.batch_len);
+  const int quarter = (blen + kWaves - 1) / kWaves;
+  const int s = Uniform(min(blen, wave * quarter)), e = Uniform(min(blen, wave * quarter + quarter));
   constexpr int kOOB = 0x7ffffff0;
   constexpr int U = 8;
   uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
@@ -630,8 +673,8 @@ __device__ __forceinline__ void V4Score(V4Shared& sh, const uint32_t* pts, const
     const int b = __umul24(Y >> sft, pws4) + a;
     return valid ? ((X >> sft) << 2) + b : kOOB;
   };
-  // v_dot4_u32_u8 with the run count in one byte of the weight multiplies
-  // that child's byte by the count and accumulates.
+  // v_dot4_u32_u8 with the entry's count in one byte of the weight
+  // multiplies that child's byte by the count and accumulates.
   auto accumulate = [&](uint32_t v, uint32_t c) {
     a0 = __builtin_amdgcn_udot4(v, c, a0, false);
     a1 = __builtin_amdgcn_udot4(v, c << 8, a1, false);
@@ -644,8 +687,11 @@ __device__ __forceinline__ void V4Score(V4Shared& sh, const uint32_t* pts, const
     uint32_t c[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      ad[u] = address(P[i + u * groups + g], true);
-      c[u] = Cn[i + u * groups + g];
+      const int idx = i + u * groups + g;
+      const bool in = idx < len;
+      const int j = in ? idx : 0;
+      ad[u] = address(P[j], in);
+      c[u] = in ? Cn[j] : 0u;
     }
     uint32_t v[U];
 #pragma unroll
@@ -655,10 +701,10 @@ __device__ __forceinline__ void V4Score(V4Shared& sh, const uint32_t* pts, const
   }
   for (; i < e; i += groups) {
     const int idx = i + g;
-    const bool in = idx < e;
-    const uint32_t vv = __builtin_amdgcn_raw_buffer_load_b32(rsrc, address(in ? P[idx] : 0u, in),
-                                                             0, 0);
-    accumulate(vv, in ? Cn[idx] : 0u);
+    const bool in = idx < e && idx < len;
+    const int j = in ? idx : 0;
+    const uint32_t vv = __builtin_amdgcn_raw_buffer_load_b32(rsrc, address(P[j], in), 0, 0);
+    accumulate(vv, in ? Cn[j] : 0u);
   }
   for (int m = nodes; m < 64; m <<= 1) {
     a0 += __shfl_xor(a0, m, 64);
@@ -674,64 +720,76 @@ __device__ __forceinline__ void V4Score(V4Shared& sh, const uint32_t* pts, const
   }
 }
 
-// Run lists (per rotation, in place): consecutive scan points that fall in
-// the same cell become one entry with their count. Wave w compacts rotations
-// w, w + 4, ...; a run longer than 255 points is split so counts fit a byte.
-// Writes each rotation's list length to lens[r]; returns this wave's longest
-// list (wave-uniform).
-__device__ int CompactRuns(uint32_t* pts, uint8_t* cnt, int npad, int n, int nrot, int* lens) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const unsigned long long below = (1ull << lane) - 1;
-  int longest = 0;
-  for (int r = wave; r < nrot; r += kWaves) {
-    uint32_t* P = pts + r * npad;
-    uint8_t* C = cnt + r * npad;
-    int out = 0;                // entries written so far
-    int run_start = 0;          // start of the run open at the block boundary
-    uint32_t last = 0;          // last cell of the previous block
-    int open_k = -1, open_pos = 0;  // the previous block's last entry, count pending
-    for (int base = 0; base < n; base += 64) {
-      const int i = base + lane;
-      const bool in = i < n;
-      const uint32_t v = in ? P[i] : 0u;
-      uint32_t prev = __shfl_up(v, 1, 64);
-      if (lane == 0) prev = last;
-      const bool head0 = in && (i == 0 || v != prev);
-      // Start of each lane's run: inclusive max-scan of head positions.
-      int rs = head0 ? i : -1;
-      for (int d = 1; d < 64; d <<= 1) {
-        const int o = __shfl_up(rs, d, 64);
-        if (lane >= d) rs = max(rs, o);
-      }
-      rs = max(rs, run_start);
-      const bool head = head0 || (in && (i - rs) % 255 == 0);
-      const unsigned long long hm = __ballot(head);
-      const int k = out + __popcll(hm & below);
-      // Close the entry left open by the previous block.
-      if (open_k >= 0 && hm) {
-        const int first = base + static_cast<int>(__ffsll(static_cast<long long>(hm))) - 1;
-        if (lane == 0) C[open_k] = static_cast<uint8_t>(first - open_pos);
+// Cluster key of a packed cell (int16 x | int16 y << 16): both coordinates
+// rounded down to a multiple of 2^shift.
+__device__ __forceinline__ uint32_t ClusterKey(uint32_t p, int shift) {
+  const int x = (static_cast<int16_t>(p & 0xffff) >> shift) << shift;
+  const int y = ((static_cast<int>(p) >> 16) >> shift) << shift;
+  return (static_cast<uint32_t>(x) & 0xffff) | (static_cast<uint32_t>(y) << 16);
+}
+
+// One wave sweeps the n raw cells of a rotation (src) and makes its run list
+// at cluster mask `mask` (both cell coordinates rounded down to a multiple
+// of k = 2^sl: the cell word with the low sl bits of each half cleared):
+// consecutive points with the same key become one entry, the key and the
+// number of points (<= 255: a longer run splits at multiples of 255 from its
+// start). kWrite = false only counts. Writing in place (P == src, mask all
+// ones) is safe: entry k <= point i, and a block's cells are in registers
+// before any write. Per block: one compare and ballot for the run heads, the
+// entry index by mbcnt, the count as the distance to the next head; the
+// 255-split scan runs only in blocks a run can reach 255 in.
+template <bool kWrite>
+__device__ int RunList(const uint32_t* src, int n, uint32_t mask, uint32_t* P, uint8_t* C) {
+  const int lane = threadIdx.x & 63;
+  const unsigned long long upto = (2ull << lane) - 1;  // lanes <= this one (lane 63: all)
+  int out = 0, run_start = 0, open_k = -1, open_pos = 0;
+  uint32_t last = 0;
+  uint32_t nextv = lane < n ? src[lane] : 0u;  // the next block's cells, loaded a block ahead
+  for (int base = 0; base < n; base += 64) {
+    const int i = base + lane;
+    const bool in = i < n;
+    const uint32_t v = nextv;
+    nextv = i + 64 < n ? src[i + 64] : 0u;
+    uint32_t prev = static_cast<uint32_t>(__builtin_amdgcn_update_dpp(
+        0, static_cast<int>(v), 0x138, 0xF, 0xF, false));  // wave_shr:1
+    if (lane == 0) prev = last;
+    const bool head0 = in && (i == 0 || ((v ^ prev) & mask) != 0u);
+    const unsigned long long h0 = __ballot(head0);
+    unsigned long long hm = h0;
+    if (base + 63 - run_start >= 255) {  // a run may pass 255 points in this block
+      const unsigned long long mine = h0 & upto;
+      const int rs = mine ? base + 63 - __clzll(mine) : run_start;
+      hm = __ballot(head0 || (in && i > rs && (i - rs) % 255 == 0));
+    }
+    if (kWrite) {
+      if (open_k >= 0 && hm) {  // close the entry left open by the previous block
+        if (lane == 0) C[open_k] = static_cast<uint8_t>(base + __ffsll(static_cast<long long>(hm)) - 1 - open_pos);
         open_k = -1;
       }
-      if (head) {
-        const unsigned long long above = hm & ~(below | (1ull << lane));
-        P[k] = v;
-        if (above) C[k] = static_cast<uint8_t>(__ffsll(static_cast<long long>(above)) - 1 - lane);
+      if ((hm >> lane) & 1ull) {
+        const int k = out + static_cast<int>(__builtin_amdgcn_mbcnt_hi(
+                                static_cast<uint32_t>(hm >> 32),
+                                __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(hm), 0u)));
+        P[k] = v & mask;
+        const unsigned long long rest = lane < 63 ? hm >> (lane + 1) : 0ull;
+        if (rest) C[k] = static_cast<uint8_t>(__ffsll(static_cast<long long>(rest)));
       }
       if (hm) {
-        const int lastl = 63 - __clzll(hm);
         open_k = out + __popcll(hm) - 1;
-        open_pos = base + lastl;
+        open_pos = base + 63 - __clzll(hm);
       }
-      out += __popcll(hm);
-      run_start = __shfl(rs, 63, 64);
-      last = __shfl(v, 63, 64);
     }
-    if (open_k >= 0 && lane == 0) C[open_k] = static_cast<uint8_t>(n - open_pos);
-    if (lane == 0) lens[r] = out;
-    longest = max(longest, out);
+    out += __popcll(hm);
+    if (h0) run_start = base + 63 - __clzll(h0);
+    last = __builtin_amdgcn_readlane(v, 63);
   }
-  return longest;
+  if (kWrite && open_k >= 0 && lane == 0) C[open_k] = static_cast<uint8_t>(n - open_pos);
+  return out;
+}
+
+__device__ __forceinline__ uint32_t ClusterMask(int sl) {
+  const uint32_t h = (0xffffu << sl) & 0xffffu;
+  return h | (h << 16);
 }
 
 __global__ void __launch_bounds__(kSearchThreads) __attribute__((amdgpu_waves_per_eu(5)))
@@ -744,18 +802,21 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
                  uint64_t* __restrict__ best,
                  int32_t* __restrict__ status,
                  unsigned long long* __restrict__ stats,
-                 uint2* __restrict__ spill_base, int npad) {
-  extern __shared__ __align__(16) uint32_t pts[];  // rot_chunk * npad cells, then counts
+                 uint2* __restrict__ spill_base, int npad, int capc) {
+  // Dynamic LDS: cells, then counts, each rc * (npad + capc) entries. Rotation
+  // r's raw cells (then its k = 1 run list, in place) at r * npad; its
+  // cluster lists packed in [rc * npad + r * capc, + capc).
+  extern __shared__ __align__(16) uint32_t cells[];
   __shared__ V4Shared sh;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int rc = queues.rot_chunk;
-  uint8_t* cnt = reinterpret_cast<uint8_t*>(pts + rc * npad);
+  uint8_t* cnts = reinterpret_cast<uint8_t*>(cells + rc * (npad + capc));
   uint2* spill = spill_base + static_cast<size_t>(blockIdx.x) * kSpill2;
   for (int k = tid; k < kBatchNodes * 4; k += kSearchThreads) sh.part[k >> 2][k & 3] = 0;
   if (tid == 0) sh.high_water = 0;
   unsigned long long local_cands = 0, local_lookups = 0;
 #ifdef CSM_KPROF
-  long long kprof[4] = {0, 0, 0, 0};  // thread 0: discretize, control, score cycles; batches
+  long long kprof[4] = {0, 0, 0, 0};  // thread 0: setup, control, score cycles; lists (part of setup)
 #endif
   if (tid == 0) sh.queue = blockIdx.x % kNumXcd;
   if (tid < kMaxLevels) { sh.lv_cands[tid] = 0; sh.lv_batches[tid] = 0; }
@@ -824,7 +885,8 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
         }
         mnx = min(mnx, ix); mxx = max(mxx, ix);
         mny = min(mny, iy); mxy = max(mxy, iy);
-        pts[r * npad + i] = (static_cast<uint32_t>(ix) & 0xffff) | (static_cast<uint32_t>(iy) << 16);
+        cells[r * npad + i] = (static_cast<uint32_t>(ix) & 0xffff) | (static_cast<uint32_t>(iy) << 16);
+        cnts[r * npad + i] = 1;  // the k = 1 list is the scan itself, one point per entry
       }
       mnx = WaveMin(mnx); mxx = WaveMax(mxx); mny = WaveMin(mny); mxy = WaveMax(mxy);
       if (lane == 0) {
@@ -833,21 +895,86 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
       }
     }
     if (range_error) sh.range_error = 1;
-    if (tid == 0) sh.n_eff = 0;
     __syncthreads();
-    // ---- Run lists; pad every rotation to the longest with empty entries ----
+    // ---- Entry lists: k = 1 is the discretized scan itself (one point per
+    // entry; it scores the leaves only), k = 2, 4, 8 are run lists of cluster
+    // keys. All threads count the runs of all three; the lists are packed
+    // into the rotation's capc region coarsest first (one that does not fit
+    // aliases the next finer list); then one wave per (rotation, list) sweep
+    // writes them -------------------------------------------------------------
     {
-      const int longest = CompactRuns(pts, cnt, npad, n, nrot, sh.run_len);
-      if (lane == 0) atomicMax(&sh.n_eff, longest);
-    }
-    __syncthreads();
-    const int n_eff = Uniform(sh.n_eff);
-    for (int r = 0; r < nrot; ++r)  // past a rotation's own list: out-of-range cell, count 0
-      for (int k = sh.run_len[r] + tid; k < n_eff; k += kSearchThreads) {
-        pts[r * npad + k] = 0x80008000u;
-        cnt[r * npad + k] = 0;
+#ifdef CSM_KPROF
+      const long long t_lists = clock64();
+#endif
+      // A rotation whose coarsest keys repeat 255 points apart may hold a run
+      // past 255 points (split entries): its lists are counted by a sweep.
+      if (tid < nrot * kLists) sh.list_len[tid / kLists][tid % kLists] = tid % kLists == 0 ? n : 0;
+      if (tid == 0) sh.long_runs = 0;
+      __syncthreads();
+      for (int r = 0; r < nrot; ++r) {
+        const uint32_t* raw = cells + r * npad;
+        uint32_t c1 = 0, c23 = 0;  // run heads of k = 2 | k = 4, k = 8 (16-bit fields)
+        bool long_run = false;
+        for (int i = tid; i < n; i += kSearchThreads) {
+          const uint32_t v = raw[i];
+          const uint32_t d = i == 0 ? 0xffffffffu : v ^ raw[i - 1];
+          c1 += (d & ClusterMask(1)) != 0u;
+          c23 += ((d & ClusterMask(2)) != 0u) | (static_cast<uint32_t>((d & ClusterMask(3)) != 0u) << 16);
+          long_run |= i >= 255 && ((v ^ raw[i - 255]) & ClusterMask(kMaxClusterShift)) == 0u;
+        }
+        c1 = DppSum(c1);
+        c23 = DppSum(c23);
+        if (lane == 0) {
+          atomicAdd(&sh.list_len[r][1], static_cast<int>(c1));
+          atomicAdd(&sh.list_len[r][2], static_cast<int>(c23 & 0xffff));
+          atomicAdd(&sh.list_len[r][3], static_cast<int>(c23 >> 16));
+        }
+        if (__ballot(long_run) && lane == 0) atomicOr(&sh.long_runs, 1 << r);
       }
-    __syncthreads();
+      __syncthreads();
+      if (const int lr = sh.long_runs) {
+        for (int t = wave; t < nrot * kMaxClusterShift; t += kWaves) {
+          const int r = t / kMaxClusterShift, sl = 1 + t % kMaxClusterShift;
+          if (lr >> r & 1) {
+            const int len = RunList<false>(cells + r * npad, n, ClusterMask(sl), nullptr, nullptr);
+            if (lane == 0) sh.list_len[r][sl] = len;
+          }
+        }
+        __syncthreads();
+      }
+      if (tid < nrot) {
+        const int r = tid;
+        sh.list_off[r][0] = r * npad;
+        int used = 0;
+        int off[kLists] = {r * npad, -1, -1, -1};
+        for (int sl = kMaxClusterShift; sl >= 1; --sl)
+          if (used + sh.list_len[r][sl] <= capc) {
+            off[sl] = rc * npad + r * capc + used;
+            used += sh.list_len[r][sl];
+          }
+        for (int sl = 1; sl < kLists; ++sl) {
+          if (off[sl] >= 0) {
+            sh.list_off[r][sl] = off[sl];
+          } else {  // does not fit: the finer list bounds this level too
+            sh.list_off[r][sl] = sh.list_off[r][sl - 1];
+            sh.list_len[r][sl] = sh.list_len[r][sl - 1] | (1 << 30);
+          }
+        }
+      }
+      __syncthreads();
+      for (int t = wave; t < nrot * kMaxClusterShift; t += kWaves) {
+        const int r = t / kMaxClusterShift, sl = 1 + t % kMaxClusterShift;
+        if (!(sh.list_len[r][sl] & (1 << 30)))
+          RunList<true>(cells + r * npad, n, ClusterMask(sl), cells + sh.list_off[r][sl],
+                        cnts + sh.list_off[r][sl]);
+      }
+      __syncthreads();
+      if (tid < nrot * kLists) sh.list_len[tid / kLists][tid % kLists] &= ~(1 << 30);
+      __syncthreads();
+#ifdef CSM_KPROF
+      if (tid == 0) kprof[3] += clock64() - t_lists;
+#endif
+    }
     // ---- ShrinkToFit per rotation; root counts ------------------------------
     if (tid < nrot) {
       const int r = tid;
@@ -924,19 +1051,19 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
               atomicMax(reinterpret_cast<unsigned long long*>(&sh.best), key);
             }
           }
-          // Inner survivors: deepest level first, then best bound, on top.
-          // Rank among survivors by counting larger keys (lane ids make keys
-          // distinct); each survivor writes its own entry.
+          // Inner survivors: deepest level on top (the batch pop takes the
+          // top 64 entries at once, so order within a level is immaterial
+          // there). Rank = survivors of deeper levels + same-level survivors
+          // in lower lanes; one ballot per distinct level (usually one).
           const bool push = keep && clvl > 0;
-          const uint32_t skey = push ? ((static_cast<uint32_t>(15 - clvl) << 28) |
-                                        (static_cast<uint32_t>(sum) << 6) | static_cast<uint32_t>(lane))
-                                     : 0u;
           const unsigned long long pm = __ballot(push);
           const int kept = __popcll(pm);
           int rank = 0;
-          for (unsigned long long m = pm; m; m &= m - 1) {
-            const int jl = static_cast<int>(__ffsll(static_cast<long long>(m))) - 1;
-            rank += static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(skey), jl)) > skey;
+          for (unsigned long long rem = pm; rem;) {
+            const int l0 = __builtin_amdgcn_readlane(clvl, static_cast<int>(__ffsll(static_cast<long long>(rem))) - 1);
+            const unsigned long long same = __ballot(push && clvl == l0);
+            if (push) rank += clvl > l0 ? __popcll(same) : (clvl == l0 ? __popcll(same & ((1ull << lane) - 1)) : 0);
+            rem &= ~same;
           }
           int sp = 0;
           if (lane == 0 && kept > 0) {
@@ -945,8 +1072,7 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
           }
           sp = __shfl(sp, 0, 64);
           // Entries past the LDS stack go to this workgroup's spill region in
-          // global memory (StackPut); past that the pair is flagged (the
-          // bound is ~2.8k entries: <= 256 pushed per level).
+          // global memory (StackPut); past that the pair is flagged.
           if (push && sp + kept <= kStack2 + kSpill2)
             StackPut(sh, spill, sp + kept - 1 - rank, make_uint2(
                 (static_cast<uint32_t>(xo) & 0xffff) | (static_cast<uint32_t>(yo) << 16),
@@ -976,13 +1102,13 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
           sp = vc;
           if (lane == 0) sh.vnext = v0 + vc;
         }
-        // (c) Pop the next batch: up to 16 same-level nodes, best first.
+        // (c) Pop the next batch: up to 64 nodes, best first.
         if (lane == 0 && (sh.batch_no++ & 7) == 0) {
           const uint64_t fresh = LoadBest(pair_best);
           if (fresh > sh.best) sh.best = fresh;
         }
         const uint32_t cur_sum = static_cast<uint32_t>(sh.best >> kSumShift);
-        int nodes = 0;
+        int nodes = 0, blen = 0, bent = 0;
         if (sp > 0) {
           // Up to 64 entries from the top (any level); expand a power of two
           // of the unpruned ones, discard pruned ones passed over.
@@ -996,22 +1122,32 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
           int take = __popcll(inm);
           if (ne > 0) {
             nodes = 1 << (31 - __clz(ne));
-            unsigned long long m = em;
-            for (int k = 1; k < nodes; ++k) m &= m - 1;
-            take = static_cast<int>(__ffsll(static_cast<long long>(m)));
             const int rank = __popcll(em & ((1ull << lane) - 1));
+            // Entries up to the nodes-th expandable one are taken.
+            take = static_cast<int>(__ffsll(static_cast<long long>(
+                __ballot(expandable && rank == nodes - 1))));
+            int len = 0;
             if (expandable && lane < take) {
+              const int r = (ent.y >> 22) & 0x1f, lvl = static_cast<int>(ent.y >> 27);
+              const int sl = sm.cshift[lvl - 1];
+              len = sh.list_len[r][sl];
               sh.node_xo[rank] = static_cast<int16_t>(ent.x & 0xffff);
               sh.node_yo[rank] = static_cast<int>(ent.x) >> 16;
-              sh.node_rot[rank] = (ent.y >> 22) & 0x1f;
-              sh.node_level[rank] = static_cast<int>(ent.y >> 27);
+              sh.node_rot[rank] = r;
+              sh.node_level[rank] = lvl;
+              sh.node_off[rank] = sh.list_off[r][sl];
+              sh.node_len[rank] = len;
             }
+            blen = DppMax(len);
+            bent = DppSum(len);
           }
           sp -= take;
         }
         if (lane == 0) {
           sh.sp = sp;
           sh.nodes = nodes;
+          sh.batch_len = blen;
+          sh.batch_entries = bent;
           sh.done = (nodes == 0 && sp == 0 && sh.vnext >= vtotal) ? 1 : 0;
         }
       }
@@ -1021,16 +1157,15 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
         const long long now = clock64();
         kprof[1] += now - t_mark;
         t_mark = now;
-        kprof[3] += 1;
       }
 #endif
       const int nodes = Uniform(sh.nodes);
       const int done = Uniform(sh.done);
       if (done) break;
       if (nodes > 0) {
-        V4Score(sh, pts, cnt, npad, n_eff, sm);
+        V4Score(sh, cells, cnts, sm);
         local_cands += 4 * nodes;
-        local_lookups += static_cast<unsigned long long>(4 * nodes) * n;
+        local_lookups += 4ull * static_cast<unsigned>(Uniform(sh.batch_entries));
         if (tid < nodes) {
           const int cl = sh.node_level[tid] - 1;
           atomicAdd(&sh.lv_cands[cl], 4ull);
@@ -1097,10 +1232,11 @@ hipError_t LaunchFast2dSearch(int grid, size_t dyn_lds, hipStream_t st, const Su
   return hipGetLastError();
 }
 
-hipError_t LaunchPyramidQuad(const uint8_t* level, int wnx, int wny, int log_h, uint32_t* out,
-                             int qw, int qh, int pws, int pph, int total, hipStream_t st) {
+hipError_t LaunchPyramidQuad(const uint8_t* level, int wnx, int wny, int log_h, int km1,
+                             uint32_t* out, int qw, int qh, int pws, int pph, int total,
+                             hipStream_t st) {
   hipLaunchKernelGGL(pyramid_quad, dim3((total + 255) / 256), dim3(256), 0, st, level, wnx, wny,
-                     log_h, out, qw, qh, pws, pph, total);
+                     log_h, km1, out, qw, qh, pws, pph, total);
   return hipGetLastError();
 }
 
@@ -1108,9 +1244,9 @@ hipError_t LaunchFast2dSearchV2(int grid, size_t dyn_lds, hipStream_t st, const 
                                 const PairDesc* pairs, const float* points, const float2* rot_table,
                                 const WorkQueues2& queues, unsigned long long* counters,
                                 uint64_t* best, int32_t* status, unsigned long long* stats,
-                                uint2* spill, int npad) {
+                                uint2* spill, int npad, int capc) {
   hipLaunchKernelGGL(fast2d_search_v4, dim3(grid), dim3(kSearchThreads), dyn_lds, st, submaps, pairs,
-                     points, rot_table, queues, counters, best, status, stats, spill, npad);
+                     points, rot_table, queues, counters, best, status, stats, spill, npad, capc);
   return hipGetLastError();
 }
 

@@ -16,13 +16,14 @@ hipError_t LaunchFast2dSearch(int grid, size_t dyn_lds, hipStream_t st, const Su
                               const PairDesc* pairs, const float* points, const float2* rot_table,
                               const WorkQueues& queues, unsigned long long* counters,
                               uint64_t* best, int32_t* status, unsigned long long* stats);
-hipError_t LaunchPyramidQuad(const uint8_t* level, int wnx, int wny, int log_h, uint32_t* out,
-                             int qw, int qh, int pws, int pph, int total, hipStream_t st);
+hipError_t LaunchPyramidQuad(const uint8_t* level, int wnx, int wny, int log_h, int km1,
+                             uint32_t* out, int qw, int qh, int pws, int pph, int total,
+                             hipStream_t st);
 hipError_t LaunchFast2dSearchV2(int grid, size_t dyn_lds, hipStream_t st, const SubmapDesc* submaps,
                                 const PairDesc* pairs, const float* points, const float2* rot_table,
                                 const WorkQueues2& queues, unsigned long long* counters,
                                 uint64_t* best, int32_t* status, unsigned long long* stats,
-                                uint2* spill, int npad);
+                                uint2* spill, int npad, int capc);
 
 
 hipError_t LaunchCellsToProbability(const uint16_t* cells, const float* ptab, float* out, int n,

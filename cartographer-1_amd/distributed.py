@@ -103,6 +103,34 @@ def gather_records(rec: np.ndarray, dist=None, rank: int = 0, world_size: int = 
     return allrec[np.argsort(allrec[:, 0], kind="stable")]
 
 
+def gather_records_comm(rec: np.ndarray, comm) -> Optional[np.ndarray]:
+    """gather_records over the C-ABI communicator (csm_comm_gather: RCCL or
+    TCP): each rank's float64 record block as one blob; rank 0 concatenates
+    them in rank order and sorts by submission index. None on other ranks."""
+    width = rec.shape[1]
+    blobs = comm.gather(np.ascontiguousarray(rec, np.float64).tobytes())
+    if blobs is None:
+        return None
+    allrec = np.concatenate([np.frombuffer(b, np.float64).reshape(-1, width) for b in blobs])
+    return allrec[np.argsort(allrec[:, 0], kind="stable")]
+
+
+def make_comm(csm, context, rank: int, world_size: int, store=None, backend: str = "rccl",
+              port: int = 29611):
+    """The C-ABI communicator of this rank: RCCL with rank 0's unique id
+    shared through ``store`` (torch.distributed's TCPStore), or TCP to
+    127.0.0.1:``port`` (host processes, gloo rehearsals)."""
+    if backend == "rccl":
+        if rank == 0:
+            uid = csm.Comm.unique_id()
+            if store is not None:
+                store.set("csm_comm_id", uid)
+        else:
+            uid = bytes(store.get("csm_comm_id"))
+        return csm.Comm.rccl(context, rank, world_size, uid)
+    return csm.Comm.tcp(rank, world_size, "127.0.0.1", port)
+
+
 def max_over_ranks(value: float, dist=None, device=None) -> float:
     """The slowest rank's wall time (bench timing contract)."""
     if dist is None:

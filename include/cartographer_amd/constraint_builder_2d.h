@@ -13,6 +13,13 @@
 // CeresScanMatcher2D restatement of ComputeConstraint (:245-249;
 // csm_ceres2d_refine_batch, parity with Ceres unpinned) unless
 // options.refine_with_ceres is off.
+//
+// Multi-GPU (set_communicator): every rank makes the same calls; a rank
+// searches only the pairs of the submaps it owns (ShardOwner) on its own
+// device, and WhenDone gathers the accepted constraints to rank 0 in
+// submission order (constraint_gather.h). Rank 0's callback gets the whole
+// result, the other ranks' callbacks an empty one; the metric counters are
+// summed over the ranks at every WhenDone.
 #ifndef CARTOGRAPHER_AMD_CONSTRAINT_BUILDER_2D_H_
 #define CARTOGRAPHER_AMD_CONSTRAINT_BUILDER_2D_H_
 
@@ -25,6 +32,7 @@
 #include <vector>
 
 #include "constraint_builder_common.h"
+#include "constraint_gather.h"
 #include "scan_matching.h"
 
 namespace cartographer_amd {
@@ -67,6 +75,10 @@ class ConstraintBuilder2D {
     if (scans_) csm_scan_set_destroy(scans_);
   }
 
+  // Shards the search over the ranks of `comm` (not owned; outlives the
+  // builder). Call before the first MaybeAdd*.
+  void set_communicator(csm_comm* comm) { comm_ = comm; }
+
   void MaybeAddConstraint(const SubmapId& submap_id, const Submap2DView* submap,
                           const NodeId& node_id, const PointCloud* cloud,
                           const Rigid2d& initial_relative_pose) {
@@ -92,8 +104,12 @@ class ConstraintBuilder2D {
   void WhenDone(const std::function<void(const Result&)>& callback) {
     Flush();
     Result result;
-    for (auto& c : constraints_)
-      if (c) result.push_back(*c);
+    if (comm_ && csm_comm_size(comm_) > 1) {
+      GatherToRoot(&result);
+    } else {
+      for (auto& c : constraints_)
+        if (c) result.push_back(*c);
+    }
     constraints_.clear();
     callback(result);
   }
@@ -124,8 +140,62 @@ class ConstraintBuilder2D {
     size_t slot;
   };
 
+  bool Owned(const SubmapId& id) const {
+    return !comm_ || csm_comm_size(comm_) <= 1 ||
+           ShardOwner(id.trajectory_id, id.submap_index, csm_comm_size(comm_)) ==
+               csm_comm_rank(comm_);
+  }
+
+  // Rank 0 receives every rank's accepted constraints in slot order; the
+  // metric deltas since the last WhenDone are summed over the ranks.
+  void GatherToRoot(Result* result) {
+    std::vector<ConstraintRecord> local;
+    for (size_t slot = 0; slot < constraints_.size(); ++slot) {
+      const Constraint* c = constraints_[slot].get();
+      if (!c) continue;
+      ConstraintRecord r{};
+      r.slot = static_cast<int64_t>(slot);
+      r.submap_trajectory = c->submap_id.trajectory_id;
+      r.submap_index = c->submap_id.submap_index;
+      r.node_trajectory = c->node_id.trajectory_id;
+      r.node_index = c->node_id.node_index;
+      r.x = c->relative_pose.x;
+      r.y = c->relative_pose.y;
+      r.theta = c->relative_pose.theta;
+      r.score = c->score;
+      r.tag = static_cast<int32_t>(c->tag);
+      local.push_back(r);
+    }
+    const std::vector<ConstraintRecord> all = GatherConstraintRecords(comm_, local);
+    int64_t d[5] = {constraints_searched - reduced_[0], constraints_found - reduced_[1],
+                    global_constraints_searched - reduced_[2],
+                    global_constraints_found - reduced_[3], constraints_failed - reduced_[4]};
+    CommCheck(csm_comm_allreduce_i64(comm_, d, 5, CSM_REDUCE_SUM), "csm_comm_allreduce_i64");
+    int64_t* counters[5] = {&constraints_searched, &constraints_found, &global_constraints_searched,
+                            &global_constraints_found, &constraints_failed};
+    for (int k = 0; k < 5; ++k) {
+      reduced_[k] += d[k];
+      *counters[k] = reduced_[k];
+    }
+    for (const ConstraintRecord& r : all) {
+      Constraint c;
+      c.submap_id = SubmapId{r.submap_trajectory, r.submap_index};
+      c.node_id = NodeId{r.node_trajectory, r.node_index};
+      c.relative_pose = Rigid2d{r.x, r.y, r.theta};
+      c.translation_weight = options_.loop_closure_translation_weight;
+      c.rotation_weight = options_.loop_closure_rotation_weight;
+      c.tag = static_cast<Constraint::Tag>(r.tag);
+      c.score = r.score;
+      result->push_back(c);
+    }
+  }
+
   void Enqueue(const SubmapId& submap_id, const Submap2DView* submap, const NodeId& node_id,
                const PointCloud* cloud, bool full, const Rigid2d& initial) {
+    if (!Owned(submap_id)) {  // another rank searches it; the slot keeps submission order
+      constraints_.emplace_back();
+      return;
+    }
     if (!matchers_.count(submap_id))  // DispatchScanMatcherConstruction
       matchers_.emplace(submap_id, std::make_shared<FastCorrelativeScanMatcher2D>(
                                        submap->grid, options_.fast_correlative_scan_matcher_options,
@@ -241,6 +311,8 @@ class ConstraintBuilder2D {
   std::vector<Pending> pending_;
   csm_scan_set* scans_ = nullptr;
   int num_started_nodes_ = 0, num_finished_nodes_ = 0;
+  csm_comm* comm_ = nullptr;
+  int64_t reduced_[5] = {0, 0, 0, 0, 0};  // counter totals over ranks at the last WhenDone
 };
 
 }  // namespace cartographer_amd

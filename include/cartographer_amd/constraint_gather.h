@@ -1,0 +1,73 @@
+// Sharding of the constraint search across ranks (one process per GPU) and
+// the hand-off of accepted constraints to rank 0.
+//
+// Every rank makes the same sequence of builder calls (the SLAM front end is
+// replicated, or replays the same node stream), so every rank assigns the same
+// submission slot to every pair; a rank searches only the pairs of the
+// submaps it owns. At WhenDone the ranks' accepted constraints travel to rank
+// 0 as fixed-width records over csm_comm_gather (RCCL over xGMI, or TCP between
+// host processes) and rank 0 orders them by slot, which is the order the
+// reference's WhenDone delivers (constraint_builder_2d.cc:279-300: results
+// are appended in submission order, failures dropped).
+#ifndef CARTOGRAPHER_AMD_CONSTRAINT_GATHER_H_
+#define CARTOGRAPHER_AMD_CONSTRAINT_GATHER_H_
+
+#include <algorithm>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "../csm_amd.h"
+
+namespace cartographer_amd {
+
+// One accepted constraint on the wire (64 bytes, no padding).
+struct ConstraintRecord {
+  int64_t slot;  // submission index of the pair
+  int32_t submap_trajectory, submap_index, node_trajectory, node_index;
+  double x, y, theta;  // relative pose, submap <- node
+  float score;
+  int32_t tag;
+  int64_t reserved;  // zero
+};
+static_assert(sizeof(ConstraintRecord) == 64, "ConstraintRecord is a fixed wire format");
+
+// The rank that searches a submap's pairs: submaps are dealt round robin in
+// creation order, so every rank gets a share of each region of the map.
+inline int ShardOwner(int trajectory_id, int submap_index, int world_size) {
+  const uint64_t h = static_cast<uint64_t>(static_cast<uint32_t>(trajectory_id)) * 0x9E3779B1u +
+                     static_cast<uint32_t>(submap_index);
+  return static_cast<int>(h % static_cast<uint64_t>(world_size));
+}
+
+inline void CommCheck(int code, const char* what) {
+  if (code != CSM_OK) {
+    std::fprintf(stderr, "F %s: %s (%d)\n", what, csm_strerror(code), code);
+    std::abort();
+  }
+}
+
+// Collective over `comm`: rank 0 returns every rank's records sorted by slot
+// (slots are unique across ranks); the other ranks return an empty vector.
+inline std::vector<ConstraintRecord> GatherConstraintRecords(
+    csm_comm* comm, const std::vector<ConstraintRecord>& local) {
+  int64_t total = 0;
+  CommCheck(csm_comm_gather(comm, local.data(),
+                            static_cast<int64_t>(local.size() * sizeof(ConstraintRecord)), &total),
+            "csm_comm_gather");
+  std::vector<ConstraintRecord> all;
+  if (csm_comm_rank(comm) != 0) return all;
+  all.resize(static_cast<size_t>(total) / sizeof(ConstraintRecord));
+  std::vector<int64_t> sizes(static_cast<size_t>(csm_comm_size(comm)));
+  CommCheck(csm_comm_gathered(comm, all.data(), total, sizes.data()), "csm_comm_gathered");
+  std::stable_sort(all.begin(), all.end(), [](const ConstraintRecord& a, const ConstraintRecord& b) {
+    return a.slot < b.slot;
+  });
+  return all;
+}
+
+}  // namespace cartographer_amd
+
+#endif  // CARTOGRAPHER_AMD_CONSTRAINT_GATHER_H_

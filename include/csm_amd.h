@@ -571,6 +571,39 @@ int csm_pbstream_submap3d_grid(const csm_pbstream* stream, int32_t index, int32_
 int csm_pbstream_submap3d_histogram(const csm_pbstream* stream, int32_t index, float* histogram,
                                     int32_t capacity);
 
+/* ---- Multi-GPU hand-off ------------------------------------
+ * The constraint queue shards across ranks (one process per GPU) with no
+ * data-path collective; the one exchange is gathering every rank's accepted
+ * constraints to rank 0 for the CPU pose-graph solve, where WhenDone's
+ * submission order is restored (constraint_builder_2d.cc:279-300 delivers
+ * results in submission order through one callback). The reference runs one
+ * process and has no counterpart; these calls are what a sharded
+ * ConstraintBuilder2D (include/cartographer_amd/constraint_builder_2d.h,
+ * set_communicator) uses. Transports: RCCL over xGMI (rank r on its context's
+ * device; rank 0 makes the id with csm_comm_get_unique_id and the caller
+ * distributes it) or TCP between host processes (CPU tests, rehearsals). */
+#define CSM_COMM_ID_BYTES 128
+#define CSM_REDUCE_SUM 0
+#define CSM_REDUCE_MAX 1
+typedef struct csm_comm csm_comm;
+int csm_comm_get_unique_id(uint8_t* id /* CSM_COMM_ID_BYTES */);
+int csm_comm_create_rccl(csm_context* ctx, int32_t rank, int32_t world_size, const uint8_t* id,
+                         csm_comm** out);
+/* Rank 0 listens on `port`; the others connect to root_host:port. */
+int csm_comm_create_tcp(int32_t rank, int32_t world_size, const char* root_host, int32_t port,
+                        csm_comm** out);
+void csm_comm_destroy(csm_comm* comm);
+int32_t csm_comm_rank(const csm_comm* comm);
+int32_t csm_comm_size(const csm_comm* comm);
+/* Collective: every rank contributes send_bytes; rank 0 keeps all blobs in
+ * rank order (total in *total_bytes, 0 on other ranks) and copies them out
+ * with csm_comm_gathered (sizes: world_size entries, bytes per rank). */
+int csm_comm_gather(csm_comm* comm, const void* send, int64_t send_bytes, int64_t* total_bytes);
+int csm_comm_gathered(const csm_comm* comm, void* out, int64_t capacity, int64_t* sizes);
+/* Collective: element-wise sum or max over ranks, in place. */
+int csm_comm_allreduce_i64(csm_comm* comm, int64_t* values, int32_t count, int32_t op);
+int csm_comm_barrier(csm_comm* comm);
+
 /* Human-readable text for a return code. */
 const char* csm_strerror(int code);
 

@@ -1,0 +1,215 @@
+// The sharded ConstraintBuilder2D (set_communicator) and the record gather it
+// uses (constraint_gather.h), run as separate processes over the C-ABI's TCP
+// transport.
+//
+//   distributed_builder_test gather <world> <port>
+//       CPU only: forks <world> ranks; each gathers interleaved-slot records
+//       to rank 0, which checks the slot order and contents. Exit 0 = pass.
+//   distributed_builder_test builder <rank> <world> <port>
+//       GPU: a synthetic two-room map (6 submaps, 10 nodes), every node
+//       matched globally against every submap and locally against nearby
+//       ones, the builder sharded over <world> ranks (world 1: no
+//       communicator). Rank 0 prints one line per constraint of WhenDone's
+//       result, in order, then the summed counters; tests/test_distributed.py
+//       compares the world-2 output with the world-1 output.
+#include <sys/wait.h>
+#include <unistd.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "cartographer_amd/constraint_builder_2d.h"
+
+using namespace cartographer_amd;
+
+static int GatherMain(int world, int port) {
+  std::vector<pid_t> kids;
+  for (int rank = 1; rank < world; ++rank) {
+    const pid_t p = fork();
+    if (p == 0) {
+      csm_comm* comm = nullptr;
+      if (csm_comm_create_tcp(rank, world, "127.0.0.1", port, &comm) != CSM_OK) _exit(2);
+      std::vector<ConstraintRecord> mine;
+      for (int k = 0; k < 5 + rank; ++k) {
+        ConstraintRecord r{};
+        r.slot = static_cast<int64_t>(k) * world + rank;
+        r.submap_index = rank;
+        r.node_index = k;
+        r.x = 0.5 * k;
+        r.score = 0.25f * rank;
+        mine.push_back(r);
+      }
+      const auto all = GatherConstraintRecords(comm, mine);
+      csm_comm_destroy(comm);
+      _exit(all.empty() ? 0 : 3);
+    }
+    kids.push_back(p);
+  }
+  csm_comm* comm = nullptr;
+  if (csm_comm_create_tcp(0, world, "127.0.0.1", port, &comm) != CSM_OK) return 2;
+  std::vector<ConstraintRecord> mine;
+  for (int k = 0; k < 5; ++k) {
+    ConstraintRecord r{};
+    r.slot = static_cast<int64_t>(k) * world;
+    r.node_index = k;
+    r.x = 0.5 * k;
+    mine.push_back(r);
+  }
+  const auto all = GatherConstraintRecords(comm, mine);
+  csm_comm_destroy(comm);
+  int bad = 0;
+  size_t expect = 0;
+  for (int r = 0; r < world; ++r) expect += 5 + r;
+  if (all.size() != expect) ++bad;
+  for (size_t i = 0; i < all.size(); ++i) {
+    const ConstraintRecord& r = all[i];
+    if (i && all[i - 1].slot >= r.slot) ++bad;
+    const int rank = static_cast<int>(r.slot % world), k = static_cast<int>(r.slot / world);
+    if (r.submap_index != rank || r.node_index != k || r.x != 0.5 * k || r.score != 0.25f * rank)
+      ++bad;
+  }
+  for (pid_t p : kids) {
+    int st = 0;
+    waitpid(p, &st, 0);
+    if (!WIFEXITED(st) || WEXITSTATUS(st) != 0) ++bad;
+  }
+  if (bad) {
+    std::fprintf(stderr, "gather: %d failures\n", bad);
+    return 1;
+  }
+  std::printf("gather OK\n");
+  return 0;
+}
+
+// Two rooms joined by a door, 5 cm cells; walls are occupied (low
+// correspondence cost), the inside free, the outside unknown.
+struct World {
+  double res = 0.05;
+  std::vector<std::vector<uint16_t>> cells;
+  std::vector<Submap2DView> submaps;
+  std::vector<PointCloud> clouds;
+  std::vector<Rigid2d> node_poses;
+};
+
+static bool OnWall(double x, double y) {
+  auto near = [](double a, double b) { return std::fabs(a - b) < 0.06; };
+  const bool outer = (near(x, 0.) || near(x, 8.)) && y >= 0. && y <= 4.;
+  const bool outer_y = (near(y, 0.) || near(y, 4.)) && x >= 0. && x <= 8.;
+  const bool middle = near(x, 4.) && y >= 0. && y <= 4. && !(y > 1.6 && y < 2.4);
+  const bool box = near(y, 1.) && x > 1.5 && x < 2.5;
+  return outer || outer_y || middle || box;
+}
+
+static World MakeWorld() {
+  World w;
+  const int n = 200;  // 10 m x 10 m submaps
+  const double centers[6][2] = {{2, 2}, {4, 2}, {6, 2}, {3, 1.5}, {5, 2.5}, {4, 3}};
+  w.cells.resize(6);
+  for (int s = 0; s < 6; ++s) {
+    Submap2DView v;
+    v.grid.resolution = w.res;
+    v.grid.max_x = centers[s][0] + 5.;
+    v.grid.max_y = centers[s][1] + 5.;
+    v.grid.num_x_cells = n;
+    v.grid.num_y_cells = n;
+    auto& c = w.cells[s];
+    c.assign(n * n, 0);
+    for (int yi = 0; yi < n; ++yi)
+      for (int xi = 0; xi < n; ++xi) {
+        // Cell (xi, yi): x index along -y, y index along -x (MapLimits).
+        const double px = v.grid.max_x - w.res * (yi + 0.5);
+        const double py = v.grid.max_y - w.res * (xi + 0.5);
+        uint16_t val = 0;
+        if (OnWall(px, py)) val = 1;  // cost 0.1
+        else if (px > 0. && px < 8. && py > 0. && py < 4.) val = 28000;
+        // Only part of the map is known to each submap.
+        if (std::hypot(px - centers[s][0], py - centers[s][1]) > 3.5) val = 0;
+        c[yi * n + xi] = val;
+      }
+    v.grid.cells = c.data();
+    v.local_pose = Rigid2d{0., 0., 0.};
+    w.submaps.push_back(v);
+  }
+  // Nodes: simple ray casts against the walls from poses inside the rooms.
+  for (int k = 0; k < 10; ++k) {
+    const Rigid2d pose{1. + 0.6 * k, 1.5 + 0.1 * (k % 4), 0.3 * k};
+    PointCloud pc;
+    for (int b = 0; b < 360; ++b) {
+      const double a = 2. * M_PI * b / 360.;
+      for (double r = 0.1; r < 9.; r += 0.02) {
+        const double gx = pose.x + r * std::cos(a), gy = pose.y + r * std::sin(a);
+        if (OnWall(gx, gy)) {
+          // Point in the node frame.
+          const double dx = gx - pose.x, dy = gy - pose.y;
+          const double c = std::cos(-pose.theta), s = std::sin(-pose.theta);
+          pc.push_back(static_cast<float>(c * dx - s * dy), static_cast<float>(s * dx + c * dy), 0.f);
+          break;
+        }
+      }
+    }
+    w.clouds.push_back(pc);
+    w.node_poses.push_back(pose);
+  }
+  return w;
+}
+
+static int BuilderMain(int rank, int world, int port) {
+  csm_comm* comm = nullptr;
+  if (world > 1 && csm_comm_create_tcp(rank, world, "127.0.0.1", port, &comm) != CSM_OK) {
+    std::fprintf(stderr, "comm create failed\n");
+    return 2;
+  }
+  const World w = MakeWorld();
+  ConstraintBuilderOptions o;
+  o.sampling_ratio = 1.;
+  o.min_score = 0.5f;
+  o.global_localization_min_score = 0.55f;
+  o.max_constraint_distance = 15.;
+  ConstraintBuilder2D builder(o);
+  if (comm) builder.set_communicator(comm);
+  for (int k = 0; k < static_cast<int>(w.clouds.size()); ++k) {
+    for (int s = 0; s < static_cast<int>(w.submaps.size()); ++s) {
+      const SubmapId sid{0, s};
+      const NodeId nid{0, k};
+      if ((k + s) % 3 == 0) {
+        builder.MaybeAddGlobalConstraint(sid, &w.submaps[s], nid, &w.clouds[k]);
+      } else {
+        // Initial relative pose: the true pose, perturbed.
+        const Rigid2d rel{w.node_poses[k].x + 0.1, w.node_poses[k].y - 0.05,
+                          w.node_poses[k].theta + 0.03};
+        builder.MaybeAddConstraint(sid, &w.submaps[s], nid, &w.clouds[k], rel);
+      }
+    }
+    builder.NotifyEndOfNode();
+  }
+  ConstraintBuilder2D::Result result;
+  builder.WhenDone([&](const ConstraintBuilder2D::Result& r) { result = r; });
+  if (rank == 0) {
+    for (const Constraint& c : result)
+      std::printf("c %d %d %.9f %.9f %.9f %.7f\n", c.submap_id.submap_index, c.node_id.node_index,
+                  c.relative_pose.x, c.relative_pose.y, c.relative_pose.theta, c.score);
+    std::printf("counters %lld %lld %lld %lld %lld\n",
+                static_cast<long long>(builder.constraints_searched),
+                static_cast<long long>(builder.constraints_found),
+                static_cast<long long>(builder.global_constraints_searched),
+                static_cast<long long>(builder.global_constraints_found),
+                static_cast<long long>(builder.constraints_failed));
+  } else if (!result.empty()) {
+    std::fprintf(stderr, "rank %d got a non-empty result\n", rank);
+    return 1;
+  }
+  if (comm) csm_comm_destroy(comm);
+  return 0;
+}
+
+int main(int argc, char** argv) {
+  if (argc == 4 && std::string(argv[1]) == "gather") return GatherMain(std::atoi(argv[2]), std::atoi(argv[3]));
+  if (argc == 5 && std::string(argv[1]) == "builder")
+    return BuilderMain(std::atoi(argv[2]), std::atoi(argv[3]), std::atoi(argv[4]));
+  std::fprintf(stderr, "usage: %s gather <world> <port> | builder <rank> <world> <port>\n", argv[0]);
+  return 2;
+}

@@ -150,3 +150,53 @@ def test_synthetic_3d_shard_is_the_full_worlds_submaps(csm):
         assert np.array_equal(full.submap_hist[2 + j], part.submap_hist[j])
     for i in range(8):
         assert np.array_equal(full.high[i], part.high[i])
+
+
+# ---- the C++ sharded ConstraintBuilder2D over the C-ABI communicator -------
+
+DIST_SRC = os.path.join(ROOT, "tests", "cpp", "distributed_builder_test.cc")
+DIST_BIN = os.path.join(ROOT, "tests", "cpp", "_build", "distributed_builder_test")
+
+
+def _build_dist():
+    import subprocess
+    os.makedirs(os.path.dirname(DIST_BIN), exist_ok=True)
+    libdir = os.path.join(ROOT, "cartographer-1_amd")
+    subprocess.check_call(["g++", "-std=c++17", "-O1", "-Wall", "-Werror",
+                           "-I", os.path.join(ROOT, "include"), DIST_SRC, "-o", DIST_BIN,
+                           "-L", libdir, "-lcsm_amd", "-Wl,-rpath," + libdir])
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_cpp_record_gather_tcp(csm, world):
+    """GatherConstraintRecords over the TCP transport, <world> forked ranks:
+    rank 0 gets every rank's records in slot (submission) order."""
+    import subprocess
+    _build_dist()
+    out = subprocess.run([DIST_BIN, "gather", str(world), str(_free_port())],
+                         capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    assert "gather OK" in out.stdout
+
+
+@pytest.mark.gpu
+def test_cpp_sharded_builder_matches_single_rank(csm):
+    """The C++ ConstraintBuilder2D sharded over 2 ranks (two processes on the
+    one GPU, TCP transport) delivers on rank 0 exactly what the single-rank
+    builder delivers: same constraints, same (submission) order, same summed
+    counters."""
+    import subprocess
+    _build_dist()
+    single = subprocess.run([DIST_BIN, "builder", "0", "1", "0"], capture_output=True, text=True,
+                            timeout=120)
+    assert single.returncode == 0, single.stderr
+    port = str(_free_port())
+    procs = [subprocess.Popen([DIST_BIN, "builder", str(r), "2", port], stdout=subprocess.PIPE,
+                              stderr=subprocess.PIPE, text=True) for r in range(2)]
+    outs = [p.communicate(timeout=120) for p in procs]
+    for p, (o, e) in zip(procs, outs):
+        assert p.returncode == 0, e
+    lines = single.stdout.strip().splitlines()
+    assert sum(1 for l in lines if l.startswith("c ")) >= 5, single.stdout
+    assert outs[0][0].strip().splitlines() == lines
+    assert outs[1][0].strip() == ""
