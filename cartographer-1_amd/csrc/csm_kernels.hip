@@ -620,6 +620,10 @@ struct V4Shared {
   int root_prefix[kMaxRotChunk + 1];
   int vnext;
   int range_error, batch_no, high_water, long_runs;
+  // The submap's per-level quad layout (SubmapDesc), cached per item so the
+  // batch loop reads LDS, not lane-divergent global loads: quad_w, quad_h,
+  // quad_off, 4 * quad_pws, plane bytes, quad_bias, cshift.
+  int lv[kMaxLevels][8];
   unsigned long long lv_cands[kMaxLevels];
   unsigned long long lv_batches[kMaxLevels];
 };
@@ -648,16 +652,15 @@ __device__ __forceinline__ void V4Score(V4Shared& sh, const uint32_t* cells, con
   // Each node scores its children at its own child level: one descriptor
   // spans the whole pyramid, the level is a per-lane byte offset.
   const int level = sh.node_level[node] - 1;
-  const int qw = sm.quad_w[level], qh = sm.quad_h[level];
-  const int qoff = sm.quad_off[level];
+  const int* L = sh.lv[level];
+  const int qw = L[0], qh = L[1], qoff = L[2], pws4 = L[3], ps4 = L[4];
   const int sft = level + 1, pmask = (2 << level) - 1;
-  const int pws4 = sm.quad_pws[level] * 4, ps4 = sm.quad_pws[level] * sm.quad_pph[level] * 4;
   const __amdgpu_buffer_rsrc_t rsrc = LevelRsrc(sm.pyramid_base, Uniform(sm.pyramid_bytes));
   const int off = sh.node_off[node], len = sh.node_len[node];
   const uint32_t* P = cells + off;
   const uint8_t* Cn = cnts + off;
-  const int cx = sh.node_xo[node] + sm.quad_bias[level];
-  const int cy = sh.node_yo[node] + sm.quad_bias[level];
+  const int cx = sh.node_xo[node] + L[5];
+  const int cy = sh.node_yo[node] + L[5];
   const int blen = Uniform(sh.batch_len);
   const int quarter = (blen + kWaves - 1) / kWaves;
   const int s = Uniform(min(blen, wave * quarter)), e = Uniform(min(blen, wave * quarter + quarter));
@@ -681,6 +684,9 @@ __device__ __forceinline__ void V4Score(V4Shared& sh, const uint32_t* cells, con
     a2 = __builtin_amdgcn_udot4(v, c << 16, a2, false);
     a3 = __builtin_amdgcn_udot4(v, c << 24, a3, false);
   };
+  // U entries per lane in flight, then the remainder one at a time: every
+  // issued load costs texture-path cycles even when its lanes are out of
+  // range, so the tail issues no more loads than it needs.
   int i = s;
   for (; i + U * groups <= e; i += U * groups) {
     int ad[U];
@@ -862,6 +868,16 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
 #endif
     if (tid < kMaxRotChunk * 4) sh.mm[tid >> 2][tid & 3] = (tid & 1) ? -0x7fffffff : 0x7fffffff;
     if (tid == 0) sh.range_error = 0;
+    if (tid < sm.levels) {
+      const int d = tid;
+      sh.lv[d][0] = sm.quad_w[d];
+      sh.lv[d][1] = sm.quad_h[d];
+      sh.lv[d][2] = sm.quad_off[d];
+      sh.lv[d][3] = sm.quad_pws[d] * 4;
+      sh.lv[d][4] = sm.quad_pws[d] * sm.quad_pph[d] * 4;
+      sh.lv[d][5] = sm.quad_bias[d];
+      sh.lv[d][6] = sm.cshift[d];
+    }
     __syncthreads();
     bool range_error = false;
     for (int r = 0; r < nrot; ++r) {
@@ -1129,7 +1145,7 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
             int len = 0;
             if (expandable && lane < take) {
               const int r = (ent.y >> 22) & 0x1f, lvl = static_cast<int>(ent.y >> 27);
-              const int sl = sm.cshift[lvl - 1];
+              const int sl = sh.lv[lvl - 1][6];
               len = sh.list_len[r][sl];
               sh.node_xo[rank] = static_cast<int16_t>(ent.x & 0xffff);
               sh.node_yo[rank] = static_cast<int>(ent.x) >> 16;
