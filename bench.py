@@ -30,7 +30,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 # Version tag of the search kernel the committed PMC traffic figures belong to
 # (a traffic file recorded on another kernel version is not reported).
-KERNEL_TAG = "v4-r2"
+KERNEL_TAG = "v5-clusters"
 
 
 def load_pkg():
@@ -118,9 +118,10 @@ def main():
         coll_dev = torch.device("cuda", device) if args.dist_backend == "nccl" else None
     sub_global = np.asarray(my_submaps, np.int64)[sub_local]
 
+    gather, gather_transport = make_gather(csm, ctx, args, rank, world_size, dist, coll_dev)
+
     def gather_constraints(res):
-        rec = cdist.make_records(res, submission, sub_global, node_idx)
-        return cdist.gather_records(rec, dist, rank, world_size, coll_dev)
+        return gather(cdist.make_records(res, submission, sub_global, node_idx))
 
     def barrier_sync():
         if dist is not None:
@@ -180,13 +181,19 @@ def main():
                                f"{args.nodes} scans x {args.submaps_per_rank} submaps per GPU "
                                "(400x400 @5cm), branch_and_bound_depth=7, min_score=%.2f" % args.min_score,
                    "pairs_per_step_per_gpu": n_pairs, "search_depth": matchers[0].options.search_depth,
-                   "parallelism": f"submap-sharded x{world_size}"},
+                   "parallelism": f"submap-sharded x{world_size}",
+                   "gather": gather_transport},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
                      "frac": achieved / peak,
                      "traffic": traffic["traffic_bytes_per_launch"] if traffic else None,
                      "traffic_source": traffic["source"] if traffic else None,
                      "kernel": "fast2d_search", "kernel_ms_avg": kernel_ms_avg,
-                     "algorithmic_bytes_per_launch": bytes_per_launch},
+                     "algorithmic_bytes_per_launch": bytes_per_launch,
+                     "bytes_definition": "4 B per quad-dword gather the search issues (one "
+                                         "per node x scan entry, 4 children each)",
+                     # SURVEY §8(d)'s figure: candidates scored x N points x 1 B
+                     "candidate_equivalent_bytes_per_launch": tm.search_candidates /
+                     max(tm.search_launches, 1) * float(np.diff(world.offsets).mean())},
         "accepted_constraints_per_step": accepted,
         "errors_per_step": errors / args.steps,
         "stack_high_water": int(tm.stack_high_water),
@@ -206,7 +213,8 @@ def main():
     if rank == 0 and world_size == 1 and not args.no_3d:
         out["rt3d"] = rt3d_bench(csm, ctx, args)
     if not args.no_3d:  # collective over ranks: the C5 sweep, submap-sharded
-        f3 = fast3d_bench(csm, ctx, args, rank, world_size, dist, coll_dev, barrier_sync, cdist)
+        f3 = fast3d_bench(csm, ctx, args, rank, world_size, dist, coll_dev, barrier_sync, cdist,
+                          gather)
         if rank == 0:
             out["fast3d"] = f3
     if rank == 0:
@@ -220,7 +228,7 @@ def main():
         sys.exit(3)
 
 
-TRAFFIC_FILES = {"c2": os.path.join("profiles", "r1e", "traffic_c2.json"),
+TRAFFIC_FILES = {"c2": os.path.join("profiles", "r2", "traffic_c2.json"),
                  "c3": os.path.join("profiles", "r2", "traffic_c3.json")}
 
 
@@ -241,8 +249,32 @@ def committed_traffic(args, world_size, workload="c2"):
         return t if same else None
     same = (world_size == 1 and args.nodes == t["nodes"] and
             args.submaps_per_rank == t["submaps_per_rank"] and
-            abs(args.min_score - t["min_score"]) < 1e-9 and args.search_depth == t["search_depth"])
+            abs(args.min_score - t["min_score"]) < 1e-9 and args.search_depth == t["search_depth"]
+            and t.get("commit_kernel") == KERNEL_TAG)
     return t if same else None
+
+
+def make_gather(csm, ctx, args, rank, world_size, dist, coll_dev):
+    """Rank-0 gather of accepted-constraint records for N > 1: the C-ABI
+    communicator (csm_comm_gather over RCCL; TCP for gloo rehearsals), whose
+    unique id travels through torch.distributed's store. Falls back to the
+    torch.distributed gather if the communicator cannot be created.
+    Returns (gather(rec) -> sorted records on rank 0, transport name)."""
+    cdist = importlib.import_module("cartographer_amd.distributed")
+    if dist is None:
+        return (lambda rec: cdist.gather_records(rec)), "local"
+    try:
+        from torch.distributed import distributed_c10d
+        store = distributed_c10d._get_default_store()
+        backend = "rccl" if args.dist_backend == "nccl" else "tcp"
+        port = int(os.environ.get("MASTER_PORT", "29500")) + 17
+        comm = cdist.make_comm(csm, ctx, rank, world_size, store, backend, port)
+        return (lambda rec: cdist.gather_records_comm(rec, comm)), f"csm_comm_{backend}"
+    except Exception as e:  # noqa: BLE001 - any failure: the torch path still works
+        print(f"bench: csm_comm unavailable ({e}); gathering with torch.distributed",
+              file=sys.stderr)
+        return (lambda rec: cdist.gather_records(rec, dist, rank, world_size, coll_dev)), \
+            "torch.distributed"
 
 
 def rt2d_bench(csm, ctx, args):
@@ -452,7 +484,7 @@ def rt3d_bench(csm, ctx, args):
 
 
 def fast3d_bench(csm, ctx, args, rank=0, world_size=1, dist=None, coll_dev=None,
-                 barrier_sync=lambda: None, cdist=None):
+                 barrier_sync=lambda: None, cdist=None, gather=None):
     """C5: FastCorrelativeScanMatcher3D::MatchFullSubmap over nodes3d nodes x
     (submaps3d x world_size) submaps, submap-sharded: each rank builds and
     searches its submaps3d submaps of the same world against every node (the
@@ -483,7 +515,8 @@ def fast3d_bench(csm, ctx, args, rank=0, world_size=1, dist=None, coll_dev=None,
         res = csm.match_batch_3d(mats, nodes, pairs, ctx)
         rec = cdist.make_records_3d(res, submission, sub_global, nod) if cdist else None
         if cdist is not None:
-            rec = cdist.gather_records(rec, dist, rank, world_size, coll_dev)
+            rec = gather(rec) if gather is not None else \
+                cdist.gather_records(rec, dist, rank, world_size, coll_dev)
         return res, rec
 
     step()  # warm-up at full size (staging buffers)
@@ -795,6 +828,7 @@ def c3_main(csm, ctx, args, rank, world_size, dist):
         submission = sub_global * N + node  # queue order: submap-major
         return res, cdist.make_records(res, submission, sub_global, node)
 
+    gather, gather_transport = make_gather(csm, ctx, args, rank, world_size, dist, coll_dev)
     for _ in range(args.warmup):  # one chunk: module load, staging buffers
         run_chunk(rank % n_chunks)
     claimer = ChunkClaimer(dist, n_chunks)
@@ -825,7 +859,7 @@ def c3_main(csm, ctx, args, rank, world_size, dist):
                 print(f"c3: chunk {c + 1}/{n_chunks} {time.perf_counter() - a:.1f} s",
                       file=sys.stderr, flush=True)
         rec = np.concatenate(recs) if recs else np.zeros((0, cdist.RECORD_WIDTH))
-        out = cdist.gather_records(rec, dist, rank, world_size, coll_dev)
+        out = gather(rec)
         if dist is not None:
             dist.barrier()
             import torch
@@ -855,7 +889,8 @@ def c3_main(csm, ctx, args, rank, world_size, dist):
                                f"the ranks, chunks of {K} submaps claimed dynamically, "
                                f"branch_and_bound_depth=7, min_score={args.min_score:.2f}",
                    "pairs_per_step": N * S, "search_depth": 0 if args.search_depth == 0 else args.search_depth,
-                   "parallelism": f"dynamic chunk claiming x{world_size}"},
+                   "parallelism": f"dynamic chunk claiming x{world_size}",
+                   "gather": gather_transport},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": 8000.0, "unit": "GB/s",
                      "frac": achieved / 8000.0,
                      "traffic": traffic["traffic_bytes_per_launch"] if traffic else None,

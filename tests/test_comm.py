@@ -102,3 +102,17 @@ def test_comm_rejects_bad_arguments(csm):
     assert lib.csm_comm_create_tcp(0, 0, b"127.0.0.1", 1234, C.byref(h)) == csm.CSM_EINVAL
     assert lib.csm_comm_create_tcp(1, 2, None, 1234, C.byref(h)) == csm.CSM_EINVAL
     assert lib.csm_comm_gather(None, None, 0, None) == csm.CSM_EINVAL
+
+
+@pytest.mark.gpu
+def test_rccl_single_rank(csm):
+    """The RCCL transport on the box's one GPU: loading librccl through
+    dlopen and ncclCommInitRank at world_size 1 (the collectives themselves
+    short-circuit at one rank; N > 1 runs them in bench.py)."""
+    ctx = csm.Context(0)
+    comm = csm.Comm.rccl(ctx, 0, 1, csm.Comm.unique_id())
+    assert (comm.rank, comm.size) == (0, 1)
+    assert comm.gather(b"\x01\x02\x03") == [b"\x01\x02\x03"]
+    assert comm.allreduce([5, -2], csm.REDUCE_MAX).tolist() == [5, -2]
+    comm.barrier()
+    comm.close()

@@ -1,0 +1,48 @@
+#!/bin/bash
+# Round-2 measurement set on one MI355X box. Usage: tools/gpu_measure.sh OUT STAGE...
+#   tests   pytest -m gpu (all GPU tests)
+#   bench   bench.py defaults (C2 + C1 + voxel + Ceres + C4 + C5, CPU baselines)
+#   trace   rocprofv3 --kernel-trace --stats of the C2 leg alone
+#   pmc     rocprofv3 --pmc passes on the C2 leg (one counter group per pass)
+#   gloo2   2-rank rehearsal (torch.distributed.run, gloo, both ranks on the GPU)
+#   c3      bench.py --workload c3 (2000 x 1000 queue, 1 GPU) + CPU baseline
+set -u
+OUT=$1; shift
+R=${GRAFT_REPO_ROOT:-$PWD}
+mkdir -p $R/$OUT
+cd $R
+for st in "$@"; do
+  echo "== $st $(date +%T)"
+  case $st in
+    tests)
+      timeout -k 10 400 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
+        > $OUT/gpu_tests.log 2>&1 || { tail -30 $OUT/gpu_tests.log; exit 1; } ;;
+    bench)
+      timeout -k 10 500 python -u bench.py > $OUT/bench_full.json 2> $OUT/bench_full.err \
+        || { tail -30 $OUT/bench_full.err; exit 1; } ;;
+    trace)
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $R/$OUT/trace \
+        -o c2 --output-format csv -- python3 $R/bench.py --no-cpu --no-rt --no-3d --steps 1 --warmup 1 \
+        > $R/$OUT/trace.json 2> $R/$OUT/trace.err) || { tail -20 $OUT/trace.err; exit 1; } ;;
+    pmc)
+      mkdir -p $OUT/pmc
+      i=0
+      for g in "TA_TA_BUSY_sum GRBM_GUI_ACTIVE" "TA_BUFFER_READ_WAVEFRONTS_sum TD_TD_BUSY_sum" \
+               "TCC_HIT_sum TCC_MISS_sum" "FETCH_SIZE"; do
+        (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 150 rocprofv3 --pmc $g -d $R/$OUT/pmc/p$i -o run \
+          --output-format csv -- python3 $R/bench.py --no-cpu --no-rt --no-3d --steps 1 --warmup 0 \
+          > $R/$OUT/pmc/p$i.log 2>&1) || { echo "pmc pass $i failed"; tail -5 $OUT/pmc/p$i.log; exit 1; }
+        i=$((i+1))
+      done
+      python3 tools/pmc_sum.py $OUT/pmc fast2d_search_v4 > $OUT/pmc/pmc_c2_summary.txt ;;
+    gloo2)
+      timeout -k 10 400 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+        --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --dist-backend gloo --no-cpu --no-rt \
+        --steps 1 --warmup 1 > $OUT/rehearsal_2rank.json 2> $OUT/rehearsal_2rank.err \
+        || { tail -30 $OUT/rehearsal_2rank.err; exit 1; } ;;
+    c3)
+      timeout -k 10 1000 python -u bench.py --workload c3 > $OUT/bench_c3.json 2> $OUT/bench_c3.err \
+        || { tail -30 $OUT/bench_c3.err; exit 1; } ;;
+  esac
+done
+echo "== done $(date +%T)"

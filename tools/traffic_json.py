@@ -1,0 +1,38 @@
+"""Writes profiles/<round>/traffic_<workload>.json from a FETCH_SIZE pass
+(rocprofv3 --pmc FETCH_SIZE, its own pass, no tracing) of the C2/C3 bench leg:
+HBM-side bytes per fast2d_search_v4 launch = FETCH_SIZE (KB) x 1024 x 2 (the
+gfx950 x2 correction of MI355X_MICROARCH.md's HBM/rocprofv3 section).
+
+    python tools/traffic_json.py PMC_DIR OUT_JSON KERNEL_TAG LAUNCH_MS [workload args...]
+"""
+import collections
+import csv
+import glob
+import json
+import sys
+
+
+def main():
+    pmc, out, tag, launch_ms = sys.argv[1], sys.argv[2], sys.argv[3], float(sys.argv[4])
+    per = collections.defaultdict(float)
+    launches = set()
+    for f in glob.glob(f"{pmc}/**/*counter_collection.csv", recursive=True):
+        for r in csv.DictReader(open(f)):
+            if "fast2d_search_v4" in r.get("Kernel_Name", "") and r["Counter_Name"] == "FETCH_SIZE":
+                per[r.get("Dispatch_Id", "0")] += float(r["Counter_Value"])
+                launches.add(r.get("Dispatch_Id", "0"))
+    if not per:
+        sys.exit("no FETCH_SIZE rows for fast2d_search_v4")
+    kb = sum(per.values()) / len(per)
+    t = {"kernel": "fast2d_search_v4 (scan clusters)", "commit_kernel": tag,
+         "workload": "C2 bench.py --no-cpu --no-rt --no-3d --steps 1 --warmup 0",
+         "nodes": 500, "submaps_per_rank": 50, "min_score": 0.55, "search_depth": 0,
+         "launches": len(per), "fetch_size_kb_per_launch": kb, "gfx950_fetch_correction": 2.0,
+         "traffic_bytes_per_launch": kb * 1024 * 2.0, "launch_ms": launch_ms,
+         "source": f"rocprofv3 --pmc FETCH_SIZE (own pass, no tracing); {pmc}"}
+    json.dump(t, open(out, "w"), indent=1)
+    print(json.dumps(t))
+
+
+if __name__ == "__main__":
+    main()
