@@ -207,6 +207,7 @@ def main():
     if rank == 0 and world_size == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(world, my_submaps, args)
     if rank == 0 and world_size == 1 and not args.no_rt:
+        out["dropin"] = dropin_bench(csm, ctx, matchers, scans, world, args)
         out["voxel_filter"] = voxel_filter_bench(csm, ctx, world, args)
         out["ceres2d"] = ceres_bench(csm, ctx, world, matchers, scans, pairs, res, my_submaps,
                                      node_idx, sub_local, args)
@@ -323,6 +324,40 @@ def rt2d_bench(csm, ctx, args):
     except OSError:
         pass
     return res
+
+
+def dropin_bench(csm, ctx, matchers, scans, world, args):
+    """The drop-in's real call patterns on the C2 world (pyramids resident):
+    ConstraintBuilder2D flushing one finished node against every submap (one
+    batch of len(matchers) MatchFullSubmap pairs per node, INTEGRATION.md
+    Option B), and Option A's single MatchFullSubmap calls (one pair per
+    call, the reference's Task granularity)."""
+    nodes = min(20, args.nodes)
+    k = len(matchers)
+    sub = np.arange(k, dtype=np.int32)
+    for _ in range(2):  # warm-up
+        csm.match_batch(matchers, scans, csm.make_pairs(sub, np.zeros(k, np.int32), args.min_score,
+                                                        full_submap=True), ctx)
+    flush_ms = []
+    for nd in range(nodes):
+        pairs = csm.make_pairs(sub, np.full(k, nd, np.int32), args.min_score, full_submap=True)
+        a = time.perf_counter()
+        csm.match_batch(matchers, scans, pairs, ctx)
+        flush_ms.append((time.perf_counter() - a) * 1e3)
+    single_ms = []
+    for j in range(20):
+        m, cloud = matchers[j % k], world.cloud(j % args.nodes)
+        a = time.perf_counter()
+        m.MatchFullSubmap(cloud, args.min_score)
+        single_ms.append((time.perf_counter() - a) * 1e3)
+    return {"per_node_flush": {"pairs_per_flush": k, "flushes": nodes,
+                               "ms_per_flush_median": float(np.median(flush_ms)),
+                               "pairs_per_s": k / (float(np.median(flush_ms)) * 1e-3)},
+            "single_call": {"calls": len(single_ms),
+                            "ms_per_match_full_submap_median": float(np.median(single_ms)),
+                            "pairs_per_s": 1e3 / float(np.median(single_ms))},
+            "note": "through the Python ctypes mirror; the batch path re-uploads the pairs and "
+                    "rotation tables per call"}
 
 
 def voxel_filter_bench(csm, ctx, world, args):
