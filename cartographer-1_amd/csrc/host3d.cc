@@ -16,8 +16,11 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <condition_variable>
 #include <cstring>
+#include <functional>
 #include <memory>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -614,7 +617,8 @@ namespace {
 
 struct PairPrep {
   Pair3Desc desc{};
-  std::vector<Yaw3Desc> yaws;
+  const Yaw3Desc* yaws = nullptr;  // this pair's discrete scans, in the batch's pinned staging
+  int num_yaws = 0;
   int status = CSM_OK;
   // Phase 1 results: the discrete-scan yaws and their rotational inputs.
   int angular_window = 0;
@@ -625,7 +629,18 @@ struct PairPrep {
 
 // MatchWithSearchParameters' host half up to the rotational scores
 // (fast_correlative_scan_matcher_3d.cc:127-199, GenerateDiscreteScans :246-276).
-void PreparePair(const csm_fast3d* m, const csm_node3d& node, const csm_pair3d& p,
+// Largest point norm of a node's high-resolution cloud (float, point order):
+// both the full-submap window (:215-222) and the angular step (:258-270)
+// take it; computed once per node per batch.
+float MaxNorm(const csm_node3d& node) {
+  float m = 0.f;
+  for (int i = 0; i < node.num_high_resolution; ++i)
+    m = std::max(m, NormV(V3{node.high_resolution_xyz[3 * i], node.high_resolution_xyz[3 * i + 1],
+                             node.high_resolution_xyz[3 * i + 2]}));
+  return m;
+}
+
+void PreparePair(const csm_fast3d* m, const csm_node3d& node, const csm_pair3d& p, float max_norm,
                  PairPrep* out) {
   const csm_fast3d_options& o = m->options;
   const float res = m->resolution;
@@ -637,11 +652,7 @@ void PreparePair(const csm_fast3d* m, const csm_node3d& node, const csm_pair3d& 
   double ang;
   R3 node_pose, submap_pose;
   if (p.full_submap) {
-    float maxd = 0.f;
-    for (int i = 0; i < n; ++i)
-      maxd = std::max(maxd, NormV(V3{node.high_resolution_xyz[3 * i],
-                                     node.high_resolution_xyz[3 * i + 1],
-                                     node.high_resolution_xyz[3 * i + 2]}));
+    const float maxd = max_norm;
     wxy = wz = (m->width_in_voxels + 1) / 2 + LroundF(maxd / res + 0.5f);
     ang = M_PI;
     csm_pose3d a = p.node_pose, b = p.submap_pose;
@@ -686,11 +697,7 @@ void PreparePair(const csm_fast3d* m, const csm_node3d& node, const csm_pair3d& 
   d.min_low_resolution_score = static_cast<float>(o.min_low_resolution_score);
   d.min_sum = MinAcceptedSum(p.min_score, std::max(n, 1));
   // Angular steps (:258-270).
-  float max_range = 3.f * res;
-  for (int i = 0; i < n; ++i)
-    max_range = std::max(NormV(V3{node.high_resolution_xyz[3 * i], node.high_resolution_xyz[3 * i + 1],
-                                  node.high_resolution_xyz[3 * i + 2]}),
-                         max_range);
+  const float max_range = n > 0 ? std::max(3.f * res, max_norm) : 3.f * res;
   out->astep = (1.f - 1e-2f) * std::acos(1.f - (res * res) / (2.f * (max_range * max_range)));
   out->angular_window = Lround(ang / out->astep);
   if (out->angular_window > kMax3dYaws / 2) {
@@ -710,22 +717,37 @@ void PreparePair(const csm_fast3d* m, const csm_node3d& node, const csm_pair3d& 
   out->node_q = node_pose.q;
 }
 
-// GenerateDiscreteScans :277-294 given the rotational scores of the pair.
-// The discrete scans of the yaws that passed the rotational filter (k in
-// increasing order, with their scores; yaw_compact on the device).
-void BuildYaws(const csm_fast3d* m, const int32_t* ks, const float* scores, int count,
-               PairPrep* out) {
-  (void)m;
-  const int A = out->angular_window;
+// Leaf key layout (kernels3d.hip LeafId): sum bits + yaw + 2 x xy + z bits;
+// CSM_ERANGE when a pair with `count` discrete scans does not fit 63 bits.
+void KeyBits(int count, PairPrep* out) {
   Pair3Desc& d = out->desc;
-  out->yaws.reserve(count);
+  auto bits = [](int64_t v) {
+    int b = 0;
+    while ((int64_t{1} << b) <= v) ++b;
+    return std::max(b, 1);
+  };
+  d.bits_xy = bits(2 * d.wxy);
+  d.bits_z = bits(2 * d.wz);
+  const int yaw_bits = bits(static_cast<int64_t>(count));
+  d.key_shift = yaw_bits + 2 * d.bits_xy + d.bits_z;
+  const int sum_bits = bits(static_cast<int64_t>(d.num_points) * 255);
+  if (d.key_shift + sum_bits > 63) out->status = CSM_ERANGE;
+}
+
+// GenerateDiscreteScans :277-294 given the rotational scores of the pair:
+// the discrete scans of the yaws that passed the rotational filter (k in
+// increasing order, with their scores; yaw_compact on the device), written
+// straight into the batch's pinned staging at `dst`.
+void BuildYaws(const int32_t* ks, const float* scores, int count, int32_t pair,
+               const PairPrep& prep, Yaw3Desc* dst) {
+  const int A = prep.angular_window;
   for (int j = 0; j < count; ++j) {
     const int k = ks[j];
-    const float angle = static_cast<float>(k - A) * out->astep;
+    const float angle = static_cast<float>(k - A) * prep.astep;
     const Q4 yaw = AngleAxisToQuat(V3{0.f, 0.f, angle});
-    const Q4 q = QMul(QMul(out->submap_inv, yaw), out->node_q);
+    const Q4 q = QMul(QMul(prep.submap_inv, yaw), prep.node_q);
     const Q4 qn = QNormalized(QMul(Q4{1.f, 0.f, 0.f, 0.f}, q));  // GetPoseFromCandidate
-    Yaw3Desc y{};
+    Yaw3Desc& y = dst[j];
     y.qw = q.w;
     y.qx = q.x;
     y.qy = q.y;
@@ -734,39 +756,97 @@ void BuildYaws(const csm_fast3d* m, const int32_t* ks, const float* scores, int 
     y.nx = qn.x;
     y.ny = qn.y;
     y.nz = qn.z;
-    y.tx = out->node_to_submap.t.x;
-    y.ty = out->node_to_submap.t.y;
-    y.tz = out->node_to_submap.t.z;
+    y.tx = prep.node_to_submap.t.x;
+    y.ty = prep.node_to_submap.t.y;
+    y.tz = prep.node_to_submap.t.z;
     y.rotational_score = scores[j];
-    y.yaw_id = static_cast<int32_t>(out->yaws.size());  // increasing angle order
-    out->yaws.push_back(y);
+    y.pair = pair;
+    y.yaw_id = j;  // increasing angle order
   }
-  // Leaf key layout (kernels3d.hip LeafId): sum bits + yaw + 2 x xy + z bits.
-  auto bits = [](int64_t v) {
-    int b = 0;
-    while ((int64_t{1} << b) <= v) ++b;
-    return std::max(b, 1);
-  };
-  d.bits_xy = bits(2 * d.wxy);
-  d.bits_z = bits(2 * d.wz);
-  const int yaw_bits = bits(static_cast<int64_t>(out->yaws.size()));
-  d.key_shift = yaw_bits + 2 * d.bits_xy + d.bits_z;
-  const int sum_bits = bits(static_cast<int64_t>(d.num_points) * 255);
-  if (d.key_shift + sum_bits > 63) out->status = CSM_ERANGE;
 }
+
+// A persistent pool of host workers for the batch's per-pair host phases
+// (spawning threads per phase cost ~1 ms per phase on the GPU box).
+class HostPool {
+ public:
+  static HostPool& Get() {
+    static HostPool pool;
+    return pool;
+  }
+  // Runs f(i) for i in [0, num) on the workers and the calling thread.
+  void Run(int64_t num, const std::function<void(int64_t)>& f) {
+    if (num <= 0) return;
+    std::unique_lock<std::mutex> lock(mu_);  // one batch phase at a time
+    {
+      std::lock_guard<std::mutex> g(state_);
+      f_ = &f;
+      num_ = num;
+      next_.store(0);
+      active_ = static_cast<int>(workers_.size());
+      ++epoch_;
+    }
+    cv_.notify_all();
+    Work(f, num);
+    std::unique_lock<std::mutex> g(state_);
+    done_.wait(g, [&] { return active_ == 0; });
+    f_ = nullptr;
+  }
+  ~HostPool() {
+    {
+      std::lock_guard<std::mutex> g(state_);
+      stop_ = true;
+      ++epoch_;
+    }
+    cv_.notify_all();
+    for (auto& t : workers_) t.join();
+  }
+
+ private:
+  HostPool() {
+    const int nt = static_cast<int>(
+        std::max<unsigned>(1, std::min<unsigned>(16, std::thread::hardware_concurrency())));
+    for (int t = 1; t < nt; ++t) workers_.emplace_back([this] { Loop(); });
+  }
+  void Work(const std::function<void(int64_t)>& f, int64_t num) {
+    for (int64_t i = next_.fetch_add(1); i < num; i = next_.fetch_add(1)) f(i);
+  }
+  void Loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      const std::function<void(int64_t)>* f;
+      int64_t num;
+      {
+        std::unique_lock<std::mutex> g(state_);
+        cv_.wait(g, [&] { return stop_ || epoch_ != seen; });
+        if (stop_) return;
+        seen = epoch_;
+        f = f_;
+        num = num_;
+      }
+      Work(*f, num);
+      std::lock_guard<std::mutex> g(state_);
+      if (--active_ == 0) done_.notify_one();
+    }
+  }
+  std::mutex mu_, state_;
+  std::condition_variable cv_, done_;
+  std::vector<std::thread> workers_;
+  const std::function<void(int64_t)>* f_ = nullptr;
+  int64_t num_ = 0;
+  std::atomic<int64_t> next_{0};
+  int active_ = 0;
+  uint64_t epoch_ = 0;
+  bool stop_ = false;
+};
 
 template <typename F>
 void ParallelPairs(int64_t num, F&& f) {
-  std::atomic<int64_t> next{0};
-  const int nt = static_cast<int>(
-      std::max<unsigned>(1, std::min<unsigned>(16, std::thread::hardware_concurrency())));
-  auto work = [&]() {
-    for (int64_t i = next.fetch_add(1); i < num; i = next.fetch_add(1)) f(i);
-  };
-  std::vector<std::thread> pool;
-  for (int t = 1; t < std::min<int64_t>(nt, num); ++t) pool.emplace_back(work);
-  work();
-  for (auto& t : pool) t.join();
+  if (num < 64) {  // not worth waking the pool
+    for (int64_t i = 0; i < num; ++i) f(i);
+    return;
+  }
+  const std::function<void(int64_t)> fn = f;
+  HostPool::Get().Run(num, fn);
 }
 
 }  // namespace
@@ -812,7 +892,15 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
     }
   }
   lap(0);
-  // Phase 1 (host, parallel): search windows, angular steps, initial yaws.
+  // Phase 1 (host, parallel): per-node cloud extents, then search windows,
+  // angular steps, initial yaws per pair.
+  std::vector<float> max_norm(num_nodes, 0.f);
+  std::vector<int32_t> used_nodes;
+  for (int32_t nd = 0; nd < num_nodes; ++nd)
+    if (hoff[nd] >= 0) used_nodes.push_back(nd);
+  ParallelPairs(static_cast<int64_t>(used_nodes.size()), [&](int64_t j) {
+    max_norm[used_nodes[j]] = MaxNorm(nodes[used_nodes[j]]);
+  });
   std::vector<PairPrep> prep(static_cast<size_t>(num_pairs));
   ParallelPairs(num_pairs, [&](int64_t i) {
     if (results[i].status != CSM_NO_MATCH) return;
@@ -823,7 +911,7 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
       prep[i].status = CSM_EINVAL;
       return;
     }
-    PreparePair(submaps[p.submap], nd, p, &prep[i]);
+    PreparePair(submaps[p.submap], nd, p, max_norm[p.node], &prep[i]);
   });
   lap(1);
   if (prof3 && num_pairs > 0) {
@@ -840,7 +928,11 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
     std::fprintf(stderr, " | pair0 w %d/%d T %d\n", prep[0].desc.wxy, prep[0].desc.wz,
                  prep[0].desc.top_nx * prep[0].desc.top_ny * prep[0].desc.top_nz);
   }
-  // Phase 2 (device): rotational scores of every (pair, yaw).
+  // Phase 2 (device): rotational scores of every (pair, yaw); the passing
+  // yaws (k, score) per pair come back compacted (yk, ys from yaw_src[i]).
+  std::vector<int32_t> yk;
+  std::vector<float> ys;
+  std::vector<int64_t> yaw_src(static_cast<size_t>(num_pairs), 0);
   {
     std::vector<float> hists;
     std::vector<int64_t> node_hist(num_nodes, -1), sub_hist(num_submaps, -1);
@@ -876,8 +968,6 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
       rp_pair.push_back(i);
     }
     std::vector<int2> range(rp.size());
-    std::vector<int32_t> yk;
-    std::vector<float> ys;
     if (!rp.empty()) {
       std::lock_guard<std::mutex> lock(ctx->mu);
       int rc;
@@ -918,12 +1008,12 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
       }
     }
     lap(2);
-    // Phase 3 (host, parallel): discrete-scan poses of the yaws that pass.
-    ParallelPairs(static_cast<int64_t>(rp_pair.size()), [&](int64_t j) {
+    for (size_t j = 0; j < rp_pair.size(); ++j) {
       const int64_t i = rp_pair[j];
-      BuildYaws(submaps[pairs[i].submap], yk.data() + range[j].x, ys.data() + range[j].x,
-                range[j].y, &prep[i]);
-    });
+      prep[i].num_yaws = range[j].y;
+      yaw_src[i] = range[j].x;
+      KeyBits(range[j].y, &prep[i]);
+    }
   }
   lap(3);
   std::vector<Submap3Desc> sdesc(num_submaps);
@@ -948,7 +1038,7 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
     d.point_offset = hoff[pairs[i].node];
     d.low_offset = loff[pairs[i].node];
     d.yaw_begin = ny;
-    d.num_yaws = static_cast<int32_t>(prep[i].yaws.size());
+    d.num_yaws = prep[i].num_yaws;
     ny += d.num_yaws;
     pdesc.push_back(d);
     pair_of.push_back(i);
@@ -979,16 +1069,16 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
   CSM_HIP(hipMemcpyAsync(dsub, sdesc.data(), sizeof(Submap3Desc) * num_submaps,
                          hipMemcpyHostToDevice, st));
   if (ny > 0) {
-    // Yaw descriptors written in parallel straight into pinned staging.
+    // Discrete-scan poses of the yaws that pass, built in parallel straight
+    // into pinned staging (the decode reads them from there).
     if ((rc = ctx->f3_host_yaws.Reserve(sizeof(Yaw3Desc) * ny))) return rc;
     Yaw3Desc* hy = ctx->f3_host_yaws.as<Yaw3Desc>();
     ParallelPairs(np, [&](int64_t dp) {
-      const std::vector<Yaw3Desc>& ys = prep[pair_of[dp]].yaws;
+      const int64_t i = pair_of[dp];
       Yaw3Desc* o = hy + pdesc[dp].yaw_begin;
-      for (size_t k = 0; k < ys.size(); ++k) {
-        o[k] = ys[k];
-        o[k].pair = static_cast<int32_t>(dp);
-      }
+      BuildYaws(yk.data() + yaw_src[i], ys.data() + yaw_src[i], prep[i].num_yaws,
+                static_cast<int32_t>(dp), prep[i], o);
+      prep[i].yaws = o;
     });
     CSM_HIP(hipMemcpyAsync(ctx->f3_yaws.ptr, hy, sizeof(Yaw3Desc) * ny, hipMemcpyHostToDevice, st));
   }
