@@ -30,6 +30,13 @@ hipError_t LaunchRt3dScore2( int num_rot, hipStream_t st, const float* pad,
                             int num_trans, int t_base, double wt, double wr,
                             unsigned long long* best, float* scores = nullptr,
                             int scores_pitch = 0);
+// rt3d_score3 (same padded brick; byte offsets below 2^24): pre-scaled points
+// and translations, eps = bound on the fast cell coordinate's error.
+hipError_t LaunchRt3dScore3(int num_rot, hipStream_t st, const float* pad, const Brick3& gb,
+                            float res, float eps, const float* points, int n, const float4* rot,
+                            const float* rot_angle, const float4* trans, int num_trans, int t_base,
+                            double wt, double wr, unsigned long long* best, float* scores,
+                            int scores_pitch);
 // Items [item_begin, item_begin + num_items) of the yaw list; `large`
 // selects the build for clouds of more than kSmall3dPoints points.
 hipError_t LaunchFast3dSearch(bool large, int grid, hipStream_t st, const Submap3Desc* submaps,

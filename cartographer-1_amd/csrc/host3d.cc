@@ -345,10 +345,32 @@ int RunRt3d(csm_context* ctx, const csm_rt_options* o, const csm_hybrid_grid* gr
     CSM_HIP(LaunchPadProbBrick(grid->prob.as<float>(), gb, g->prob_pad.as<float>(), st));
     g->prob_pad_ready = true;
   }
+  // v3 when the padded brick's byte offsets are exact in float (< 2^24).
+  const bool v3 = v2 && !std::getenv("CSM_RT3D_V2") &&
+                  4 * static_cast<int64_t>(gb.nx + 2) * (gb.ny + 2) * (gb.nz + 2) < (int64_t{1} << 24);
+  // |(a' + tr') - fl(fl(a + tr) / res)| <= 2.5 * 2^-23 * (|a| + |tr|) / res
+  // (rt3d_score3); the threshold takes 4 * 2^-23 * (A + T + 1).
+  float eps = 0.f;
+  if (v3) {
+    float amax = 0.f, tmax = 0.f;
+    for (int i = 0; i < n; ++i)
+      amax = std::max(amax, NormV(V3{xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2]}));
+    for (const float4& t : w.trans)
+      tmax = std::max({tmax, std::fabs(t.x), std::fabs(t.y), std::fabs(t.z)});
+    eps = static_cast<float>(4.0 * std::ldexp(1.0, -23) *
+                             (static_cast<double>(amax) * 1.001 / res + tmax / res + 1.0));
+  }
   if (ctx->timing) CSM_HIP(hipEventRecord(ctx->ev0, st));
   for (int64_t t0 = 0; t0 < num_trans; t0 += kRt3dThreads) {
     const int cnt = static_cast<int>(std::min<int64_t>(kRt3dThreads, num_trans - t0));
-    if (v2)
+    if (v3)
+      CSM_HIP(LaunchRt3dScore3(static_cast<int>(num_rot), st, grid->prob_pad.as<float>(), gb, res,
+                               eps, ctx->rt3_points.as<float>(), n, drot, dangle,
+                               ctx->rt3_trans.as<float4>(), cnt, static_cast<int>(t0),
+                               o->translation_delta_cost_weight, o->rotation_delta_cost_weight,
+                               ctx->rt3_best.as<unsigned long long>(), dscores,
+                               static_cast<int>(num_trans)));
+    else if (v2)
       CSM_HIP(LaunchRt3dScore2(static_cast<int>(num_rot), st, grid->prob_pad.as<float>(), gb, res,
                                ctx->rt3_points.as<float>(), n, drot, dangle,
                                ctx->rt3_trans.as<float4>(), cnt, static_cast<int>(t0),

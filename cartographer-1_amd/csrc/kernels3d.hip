@@ -327,6 +327,112 @@ rt3d_score2(const float* __restrict__ pad, int pnx, int pny, int pnz, int ox, in
   }
 }
 
+// RTCSM3D, v3 (bricks under 2^22 cells): same candidates, sums and key as
+// v2, about half the VALU per lookup (the v2 kernel is VALU-bound at ~33
+// instructions per lookup):
+//  * the rotated points are stored pre-scaled, a' = a * (1 / res), and each
+//    thread holds its translation pre-scaled, tr' = tr * (1 / res): a cell
+//    coordinate is rint(a' + tr') (one add, not an add and a multiply);
+//  * one rounding-safety test per lookup: the largest |y - rint(y)| of the
+//    three axes against 0.5 - eps, eps an absolute bound on |(a' + tr') -
+//    fl(fl(a + tr) / res)| from the magnitudes of a' and tr' (host, per
+//    launch); lookups within eps of a half-integer take the exact IEEE path
+//    (the point is re-rotated from the cloud, RoundDiv per axis);
+//  * the clamp into the padded brick runs on the rounded coordinates with
+//    per-thread bounds, and the byte offset is three exact float FMAs.
+__global__ void __launch_bounds__(768)
+rt3d_score3(const float* __restrict__ pad, int pnx, int pny, int pnz, int ox, int oy, int oz,
+            float res, float inv, float eps, const float* __restrict__ points, int n,
+            const float4* __restrict__ rot, const float* __restrict__ rot_angle,
+            const float4* __restrict__ trans, int num_trans, int t_base, int num_rot, double wt,
+            double wr, unsigned long long* __restrict__ best, float* __restrict__ scores,
+            int scores_pitch) {
+  __shared__ float4 rp[kRt3Rpb][kRt3Tile];
+  __shared__ unsigned long long red[768 / 64];
+  const int tid = threadIdx.x;
+  const int sub = tid / num_trans;
+  const int t = tid - sub * num_trans;
+  const int r = blockIdx.x * kRt3Rpb + sub;
+  const bool active = sub < kRt3Rpb && r < num_rot;
+  const float4 tr = active ? trans[t] : make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4* my = rp[active ? sub : 0];
+  const float4 q = rot[min(r, num_rot - 1)];
+  const float tsx = __fmul_rn(tr.x, inv), tsy = __fmul_rn(tr.y, inv), tsz = __fmul_rn(tr.z, inv);
+  // Padded cell (ix + bx, iy + by, iz + bz), each coordinate clamped into
+  // [0, pn - 1]: the rounded coordinate clamps into [-b, pn - 1 - b].
+  const float bx = static_cast<float>(1 - ox), by = static_cast<float>(1 - oy),
+              bz = static_cast<float>(1 - oz);
+  const float lx = -bx, ly = -by, lz = -bz;
+  const float hx = static_cast<float>(pnx - 1) - bx, hy = static_cast<float>(pny - 1) - by,
+              hz = static_cast<float>(pnz - 1) - bz;
+  const float sx = 4.f, sy = 4.f * static_cast<float>(pnx),
+              sz = 4.f * static_cast<float>(pnx) * static_cast<float>(pny);
+  const float base = 4.f * ((bz * static_cast<float>(pny) + by) * static_cast<float>(pnx) + bx);
+  const float half = 0.5f - eps;
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(pad), 0, static_cast<int>(4u * pnx * pny * pnz), 0x00020000);
+  float sum = 0.f;
+  for (int tb = 0; tb < n; tb += kRt3Tile) {
+    const int cnt = min(kRt3Tile, n - tb);
+    __syncthreads();
+    for (int i = tid; i < kRt3Rpb * cnt; i += blockDim.x) {
+      const int s2 = i / cnt, j = i - s2 * cnt;
+      const int rr = min(blockIdx.x * kRt3Rpb + s2, num_rot - 1);
+      const float4 qq = rot[rr];
+      const float* p = points + 3 * static_cast<int64_t>(tb + j);
+      float ox_, oy_, oz_;
+      Rotate3(qq.w, qq.x, qq.y, qq.z, p[0], p[1], p[2], &ox_, &oy_, &oz_);
+      rp[s2][j] = make_float4(__fmul_rn(ox_, inv), __fmul_rn(oy_, inv), __fmul_rn(oz_, inv), 0.f);
+    }
+    __syncthreads();
+    if (active) {
+      for (int i = 0; i < cnt; ++i) {
+        const float4 a = my[i];
+        const float yx = __fadd_rn(a.x, tsx), yy = __fadd_rn(a.y, tsy), yz = __fadd_rn(a.z, tsz);
+        float rx = rintf(yx), ry = rintf(yy), rz = rintf(yz);
+        const float dm = fmaxf(fmaxf(fabsf(__fsub_rn(yx, rx)), fabsf(__fsub_rn(yy, ry))),
+                               fabsf(__fsub_rn(yz, rz)));
+        if (dm >= half) {  // rare: the IEEE quotient of the reference decides
+          const float* p = points + 3 * static_cast<int64_t>(tb + i);
+          float ax, ay, az;
+          Rotate3(q.w, q.x, q.y, q.z, p[0], p[1], p[2], &ax, &ay, &az);
+          rx = static_cast<float>(RoundDiv(__fadd_rn(ax, tr.x), res, inv));
+          ry = static_cast<float>(RoundDiv(__fadd_rn(ay, tr.y), res, inv));
+          rz = static_cast<float>(RoundDiv(__fadd_rn(az, tr.z), res, inv));
+        }
+        rx = __builtin_amdgcn_fmed3f(rx, lx, hx);
+        ry = __builtin_amdgcn_fmed3f(ry, ly, hy);
+        rz = __builtin_amdgcn_fmed3f(rz, lz, hz);
+        // Exact: every term is an integer below 2^24.
+        const float off = fmaf(rz, sz, fmaf(ry, sy, fmaf(rx, sx, base)));
+        sum = __fadd_rn(sum, __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                                 rsrc, static_cast<int>(off), 0, 0)));
+      }
+    }
+  }
+  unsigned long long key = 0;
+  if (active) {
+    float score = __fdiv_rn(sum, static_cast<float>(n));
+    const double e = static_cast<double>(tr.w) * wt + static_cast<double>(rot_angle[r]) * wr;
+    score = static_cast<float>(static_cast<double>(score) * exp(-(e * e)));
+    const unsigned idx = static_cast<unsigned>(t_base + t) * static_cast<unsigned>(num_rot) + r;
+    key = (static_cast<unsigned long long>(__float_as_uint(score)) << 32) | (0xffffffffu - idx);
+    if (scores) scores[static_cast<int64_t>(r) * scores_pitch + t_base + t] = score;
+  }
+  if (scores) return;  // uniform: no reduction in the scoring mode
+  for (int m = 32; m > 0; m >>= 1) {
+    const unsigned long long o = __shfl_xor(key, m, 64);
+    key = o > key ? o : key;
+  }
+  if ((tid & 63) == 0) red[tid >> 6] = key;
+  __syncthreads();
+  if (tid == 0) {
+    unsigned long long k = red[0];
+    for (int w = 1; w < static_cast<int>(blockDim.x / 64); ++w) k = red[w] > k ? red[w] : k;
+    atomicMax(best, k);
+  }
+}
+
 // ------------------------------------------------------------ FastCSM3D ----
 //
 // Persistent workgroups pull (pair, yaw) items from a global counter. Per
@@ -1324,6 +1430,20 @@ hipError_t LaunchRt3dScore2(int num_rot, hipStream_t st, const float* pad,
   const int blocks = (num_rot + kRt3Rpb - 1) / kRt3Rpb;
   hipLaunchKernelGGL(rt3d_score2, dim3(blocks), dim3(threads), 0, st, pad, gb.nx + 2, gb.ny + 2,
                      gb.nz + 2, gb.ox, gb.oy, gb.oz, res, 1.f / res, points, n, rot, rot_angle,
+                     trans + t_base, num_trans, t_base, num_rot, wt, wr, best, scores,
+                     scores_pitch);
+  return hipGetLastError();
+}
+
+hipError_t LaunchRt3dScore3(int num_rot, hipStream_t st, const float* pad, const Brick3& gb,
+                            float res, float eps, const float* points, int n, const float4* rot,
+                            const float* rot_angle, const float4* trans, int num_trans, int t_base,
+                            double wt, double wr, unsigned long long* best, float* scores,
+                            int scores_pitch) {
+  const int threads = (kRt3Rpb * num_trans + 63) / 64 * 64;
+  const int blocks = (num_rot + kRt3Rpb - 1) / kRt3Rpb;
+  hipLaunchKernelGGL(rt3d_score3, dim3(blocks), dim3(threads), 0, st, pad, gb.nx + 2, gb.ny + 2,
+                     gb.nz + 2, gb.ox, gb.oy, gb.oz, res, 1.f / res, eps, points, n, rot, rot_angle,
                      trans + t_base, num_trans, t_base, num_rot, wt, wr, best, scores,
                      scores_pitch);
   return hipGetLastError();
