@@ -185,8 +185,7 @@ def main():
                    "gather": gather_transport},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
                      "frac": achieved / peak,
-                     "traffic": traffic["traffic_bytes_per_launch"] if traffic else None,
-                     "traffic_source": traffic["source"] if traffic else None,
+                     **traffic_fields(traffic, kernel_ms_avg, peak),
                      "kernel": "fast2d_search", "kernel_ms_avg": kernel_ms_avg,
                      "algorithmic_bytes_per_launch": bytes_per_launch,
                      "bytes_definition": "4 B per quad-dword gather the search issues (one "
@@ -229,8 +228,19 @@ def main():
         sys.exit(3)
 
 
-TRAFFIC_FILES = {"c2": os.path.join("profiles", "r2", "traffic_c2.json"),
-                 "c3": os.path.join("profiles", "r2", "traffic_c3.json")}
+TRAFFIC_FILES = {"c2": os.path.join("profiles", "r2b", "traffic_c2.json"),
+                 "c3": os.path.join("profiles", "r2d", "traffic_c3.json")}
+
+
+def traffic_fields(traffic, kernel_ms_avg, peak):
+    """roofline.traffic (HBM-side bytes per launch from the committed PMC
+    pass) and the rate / fraction of peak it implies at this run's measured
+    launch duration, next to the algorithmic figures."""
+    if not traffic or not kernel_ms_avg:
+        return {"traffic": None, "traffic_source": None, "traffic_GBps": None, "traffic_frac": None}
+    gbps = traffic["traffic_bytes_per_launch"] / (kernel_ms_avg * 1e-3) / 1e9
+    return {"traffic": traffic["traffic_bytes_per_launch"], "traffic_source": traffic["source"],
+            "traffic_GBps": gbps, "traffic_frac": gbps / peak}
 
 
 def committed_traffic(args, world_size, workload="c2"):
@@ -244,8 +254,9 @@ def committed_traffic(args, world_size, workload="c2"):
     except (OSError, ValueError):
         return None
     if workload == "c3":
-        same = (args.c3_nodes == t["nodes"] and args.c3_submaps == t["submaps"] and
-                args.c3_chunk == t["chunk"] and abs(args.min_score - t["min_score"]) < 1e-9 and
+        # Per-launch traffic of chunk launches (chunk x all nodes); the PMC
+        # pass may cover the first chunks of the queue only.
+        same = (args.c3_nodes == t["nodes"] and args.c3_chunk == t["chunk"] and abs(args.min_score - t["min_score"]) < 1e-9 and
                 args.search_depth == t["search_depth"] and t.get("commit_kernel") == KERNEL_TAG)
         return t if same else None
     same = (world_size == 1 and args.nodes == t["nodes"] and
@@ -928,8 +939,8 @@ def c3_main(csm, ctx, args, rank, world_size, dist):
                    "gather": gather_transport},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": 8000.0, "unit": "GB/s",
                      "frac": achieved / 8000.0,
-                     "traffic": traffic["traffic_bytes_per_launch"] if traffic else None,
-                     "traffic_source": traffic["source"] if traffic else None,
+                     **traffic_fields(traffic, tm.search_kernel_ms / max(tm.search_launches, 1),
+                                      8000.0),
                      "kernel": "fast2d_search",
                      "kernel_ms_avg": tm.search_kernel_ms / max(tm.search_launches, 1),
                      "algorithmic_bytes_per_launch": tm.search_lookups / max(tm.search_launches, 1)},

@@ -6,6 +6,8 @@
 #   pmc     rocprofv3 --pmc passes on the C2 leg (one counter group per pass)
 #   gloo2   2-rank rehearsal (torch.distributed.run, gloo, both ranks on the GPU)
 #   c3      bench.py --workload c3 (2000 x 1000 queue, 1 GPU) + CPU baseline
+#   c3trace rocprofv3 --kernel-trace --stats of the whole C3 queue (one step, no CPU leg)
+#   c3pmc   FETCH_SIZE pass on the first 64 submaps of the C3 queue (8 chunk launches)
 set -u
 OUT=$1; shift
 R=${GRAFT_REPO_ROOT:-$PWD}
@@ -43,6 +45,17 @@ for st in "$@"; do
     c3)
       timeout -k 10 1000 python -u bench.py --workload c3 > $OUT/bench_c3.json 2> $OUT/bench_c3.err \
         || { tail -30 $OUT/bench_c3.err; exit 1; } ;;
+    c3trace)
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $R/$OUT/c3trace \
+        -o c3 --output-format csv -- python3 -u $R/bench.py --workload c3 --no-cpu --steps 1 --warmup 1 \
+        > $R/$OUT/c3trace.json 2> $R/$OUT/c3trace.err) || { tail -20 $OUT/c3trace.err; exit 1; } ;;
+    c3pmc)
+      mkdir -p $OUT/c3pmc
+      (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d $R/$OUT/c3pmc/p0 -o run \
+        --output-format csv -- python3 $R/bench.py --workload c3 --c3-submaps 64 --no-cpu --steps 1 --warmup 0 \
+        > $R/$OUT/c3pmc/p0.json 2> $R/$OUT/c3pmc/p0.log) || { echo "c3 pmc pass failed"; tail -5 $OUT/c3pmc/p0.log; exit 1; }
+      ms=$(python3 -c "import json,sys; print(json.loads([l for l in open('$OUT/c3pmc/p0.json') if l.startswith('{')][-1])['roofline']['kernel_ms_avg'])" 2>/dev/null || echo 0)
+      python3 tools/traffic_json.py $OUT/c3pmc $OUT/traffic_c3.json v5-clusters $ms c3 2000 8 64 ;;
   esac
 done
 echo "== done $(date +%T)"

@@ -3,7 +3,7 @@
 HBM-side bytes per fast2d_search_v4 launch = FETCH_SIZE (KB) x 1024 x 2 (the
 gfx950 x2 correction of MI355X_MICROARCH.md's HBM/rocprofv3 section).
 
-    python tools/traffic_json.py PMC_DIR OUT_JSON KERNEL_TAG LAUNCH_MS [workload args...]
+    python tools/traffic_json.py PMC_DIR OUT_JSON KERNEL_TAG LAUNCH_MS [c3 NODES CHUNK SUBMAPS]
 """
 import collections
 import csv
@@ -30,6 +30,13 @@ def main():
          "launches": len(per), "fetch_size_kb_per_launch": kb, "gfx950_fetch_correction": 2.0,
          "traffic_bytes_per_launch": kb * 1024 * 2.0, "launch_ms": launch_ms,
          "source": f"rocprofv3 --pmc FETCH_SIZE (own pass, no tracing); {pmc}"}
+    if len(sys.argv) > 5 and sys.argv[5] == "c3":
+        nodes, chunk, submaps = (int(v) for v in sys.argv[6:9])
+        del t["submaps_per_rank"]
+        t.update({"workload": f"C3 chunk launches: bench.py --workload c3 --c3-submaps {submaps} "
+                              f"--no-cpu --steps 1 --warmup 0 (the first {submaps} submaps of the "
+                              f"2000 x 1000 queue)",
+                  "nodes": nodes, "chunk": chunk, "submaps": submaps})
     json.dump(t, open(out, "w"), indent=1)
     print(json.dumps(t))
 
