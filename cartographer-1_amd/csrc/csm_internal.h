@@ -97,7 +97,11 @@ struct csm_context {
   // 3D path scratch (host3d.cc).
   csm::DevBuf rt3_rot, rt3_trans, rt3_points, rt3_best, f3_pairs, f3_yaws, f3_points,
       f3_low_points, f3_best, f3_status, f3_counter, f3_items, f3_scores, f3_spill;
-  csm::PinnedBuf f3_host_yaws;
+  csm::PinnedBuf f3_host_yaws, f3_host_points;
+  // Side stream for the 3D batch's cloud upload (overlaps the rotational
+  // scores on `stream`); the search waits on f3_points_ready.
+  hipStream_t f3_copy_stream = nullptr;
+  hipEvent_t f3_points_ready = nullptr;
   // Voxel filter scratch (voxel_filter.hip).
   csm::DevBuf vf_points, vf_offsets, vf_keep, vf_counts;
   // CeresScanMatcher2D refinement scratch (ceres2d.hip).

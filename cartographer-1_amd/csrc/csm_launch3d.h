@@ -66,6 +66,28 @@ hipError_t LaunchYawCompact(const void* pairs, int num_pairs, const float* score
                             unsigned* cursor, int2* range, int32_t* out_k, float* out_s,
                             hipStream_t st);
 
+// Discrete-scan poses of the passing yaws (GenerateDiscreteScans :277-294),
+// one record per device pair (in device pair order): the pair's fixed
+// rotations and translation, the angular step and window, where its passing
+// (k, score) lists start in the compacted arrays, and where its Yaw3Desc
+// records go.
+struct YawBuild3 {
+  float siw, six, siy, siz;  // submap_pose.rotation().inverse()
+  float nqw, nqx, nqy, nqz;  // node_pose.rotation()
+  float tx, ty, tz;          // (submap^-1 * node).translation()
+  float astep;
+  int32_t window, src, yaw_begin, num;
+};
+// A yaw whose float sin/cos rounding the device cannot decide: the host
+// rebuilds it with the reference's libm.
+struct YawFlag3 {
+  int32_t dp, j, k;
+  float score;
+};
+constexpr int kYawFlagCap = 4096;
+hipError_t LaunchYawBuild(const YawBuild3* items, int num_pairs, const int32_t* k, const float* s,
+                          Yaw3Desc* out, unsigned* flag_count, YawFlag3* flags, hipStream_t st);
+
 }  // namespace csm
 
 #endif  // CSM_LAUNCH3D_H_

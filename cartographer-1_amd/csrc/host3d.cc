@@ -639,7 +639,6 @@ namespace {
 
 struct PairPrep {
   Pair3Desc desc{};
-  const Yaw3Desc* yaws = nullptr;  // this pair's discrete scans, in the batch's pinned staging
   int num_yaws = 0;
   int status = CSM_OK;
   // Phase 1 results: the discrete-scan yaws and their rotational inputs.
@@ -889,9 +888,10 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
     hms[k] += std::chrono::duration<double, std::milli>(now - ht).count();
     ht = now;
   };
-  // Nodes: pack clouds (only nodes some pair references).
+  // Nodes: offsets of the clouds some pair references (packed below).
   std::vector<int64_t> hoff(num_nodes, -1), loff(num_nodes, -1);
-  std::vector<float> hpts, lpts;
+  std::vector<int32_t> used_nodes;
+  int64_t nh = 0, nl = 0;
   for (int64_t i = 0; i < num_pairs; ++i) {
     results[i] = csm_result3d{};
     results[i].status = CSM_NO_MATCH;
@@ -907,19 +907,48 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
       continue;
     }
     if (hoff[p.node] < 0) {
-      hoff[p.node] = static_cast<int64_t>(hpts.size() / 3);
-      hpts.insert(hpts.end(), nd.high_resolution_xyz, nd.high_resolution_xyz + 3 * nd.num_high_resolution);
-      loff[p.node] = static_cast<int64_t>(lpts.size() / 3);
-      lpts.insert(lpts.end(), nd.low_resolution_xyz, nd.low_resolution_xyz + 3 * nd.num_low_resolution);
+      hoff[p.node] = nh;
+      loff[p.node] = nl;
+      nh += nd.num_high_resolution;
+      nl += nd.num_low_resolution;
+      used_nodes.push_back(p.node);
     }
   }
+  // One lock for the whole device section: the clouds uploaded here are read
+  // by the search below.
+  std::unique_lock<std::mutex> ctx_lock(ctx->mu);
+  {
+    int rc;
+    if ((rc = EnsureDevice3(ctx))) return rc;
+    if (!ctx->f3_copy_stream) {
+      CSM_HIP(hipStreamCreateWithFlags(&ctx->f3_copy_stream, hipStreamNonBlocking));
+      CSM_HIP(hipEventCreateWithFlags(&ctx->f3_points_ready, hipEventDisableTiming));
+    }
+    if ((rc = ctx->f3_host_points.Reserve(sizeof(float) * 3 * std::max<int64_t>(nh + nl, 1))))
+      return rc;
+    if ((rc = ctx->f3_points.Reserve(sizeof(float) * 3 * std::max<int64_t>(nh, 1)))) return rc;
+    if ((rc = ctx->f3_low_points.Reserve(sizeof(float) * 3 * std::max<int64_t>(nl, 1)))) return rc;
+  }
+  float* const hstage = ctx->f3_host_points.as<float>();
+  float* const lstage = hstage + 3 * nh;
+  ParallelPairs(static_cast<int64_t>(used_nodes.size()), [&](int64_t j) {
+    const csm_node3d& nd = nodes[used_nodes[j]];
+    std::memcpy(hstage + 3 * hoff[used_nodes[j]], nd.high_resolution_xyz,
+                sizeof(float) * 3 * nd.num_high_resolution);
+    std::memcpy(lstage + 3 * loff[used_nodes[j]], nd.low_resolution_xyz,
+                sizeof(float) * 3 * nd.num_low_resolution);
+  });
+  if (nh > 0)
+    CSM_HIP(hipMemcpyAsync(ctx->f3_points.ptr, hstage, sizeof(float) * 3 * nh, hipMemcpyHostToDevice,
+                           ctx->f3_copy_stream));
+  if (nl > 0)
+    CSM_HIP(hipMemcpyAsync(ctx->f3_low_points.ptr, lstage, sizeof(float) * 3 * nl,
+                           hipMemcpyHostToDevice, ctx->f3_copy_stream));
+  CSM_HIP(hipEventRecord(ctx->f3_points_ready, ctx->f3_copy_stream));
   lap(0);
   // Phase 1 (host, parallel): per-node cloud extents, then search windows,
   // angular steps, initial yaws per pair.
   std::vector<float> max_norm(num_nodes, 0.f);
-  std::vector<int32_t> used_nodes;
-  for (int32_t nd = 0; nd < num_nodes; ++nd)
-    if (hoff[nd] >= 0) used_nodes.push_back(nd);
   ParallelPairs(static_cast<int64_t>(used_nodes.size()), [&](int64_t j) {
     max_norm[used_nodes[j]] = MaxNorm(nodes[used_nodes[j]]);
   });
@@ -954,6 +983,9 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
   // yaws (k, score) per pair come back compacted (yk, ys from yaw_src[i]).
   std::vector<int32_t> yk;
   std::vector<float> ys;
+  unsigned kept = 0;
+  const int32_t* dev_k = nullptr;
+  const float* dev_s = nullptr;
   std::vector<int64_t> yaw_src(static_cast<size_t>(num_pairs), 0);
   {
     std::vector<float> hists;
@@ -991,9 +1023,7 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
     }
     std::vector<int2> range(rp.size());
     if (!rp.empty()) {
-      std::lock_guard<std::mutex> lock(ctx->mu);
       int rc;
-      if ((rc = EnsureDevice3(ctx))) return rc;
       hipStream_t st = ctx->stream;
       if ((rc = ctx->f3_items.Reserve(sizeof(RotPair3Host) * rp.size() +
                                       sizeof(float) * std::max<size_t>(hists.size(), 1))))
@@ -1016,18 +1046,14 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
       CSM_HIP(LaunchRotScores(drp, static_cast<int>(rp.size()), max_yaws, dh, dscores, st));
       CSM_HIP(LaunchYawCompact(drp, static_cast<int>(rp.size()), dscores, dcursor, drange, dk, ds,
                                st));
-      unsigned kept = 0;
       CSM_HIP(hipMemcpyAsync(range.data(), drange, sizeof(int2) * rp.size(),
                              hipMemcpyDeviceToHost, st));
       CSM_HIP(hipMemcpyAsync(&kept, dcursor, sizeof(unsigned), hipMemcpyDeviceToHost, st));
       CSM_HIP(hipStreamSynchronize(st));
-      yk.resize(std::max(kept, 1u));
-      ys.resize(std::max(kept, 1u));
-      if (kept > 0) {
-        CSM_HIP(hipMemcpyAsync(yk.data(), dk, sizeof(int32_t) * kept, hipMemcpyDeviceToHost, st));
-        CSM_HIP(hipMemcpyAsync(ys.data(), ds, sizeof(float) * kept, hipMemcpyDeviceToHost, st));
-        CSM_HIP(hipStreamSynchronize(st));
-      }
+      // The passing (k, score) lists stay on the device (f3_scores) for the
+      // yaw_build kernel; the host reads them back with the results.
+      dev_k = dk;
+      dev_s = ds;
     }
     lap(2);
     for (size_t j = 0; j < rp_pair.size(); ++j) {
@@ -1067,16 +1093,15 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
     if (pass == 0) ny_small = ny;
   }
   const int np = static_cast<int>(pdesc.size());
-  if (np == 0) return CSM_OK;
-  std::lock_guard<std::mutex> lock(ctx->mu);
-  int rc;
-  if ((rc = EnsureDevice3(ctx))) return rc;
   hipStream_t st = ctx->stream;
+  if (np == 0) {
+    CSM_HIP(hipStreamSynchronize(ctx->f3_copy_stream));  // staging is reused by the next batch
+    return CSM_OK;
+  }
+  int rc;
   if ((rc = ctx->f3_pairs.Reserve(sizeof(Pair3Desc) * np + sizeof(Submap3Desc) * num_submaps)))
     return rc;
   if ((rc = ctx->f3_yaws.Reserve(sizeof(Yaw3Desc) * std::max(ny, 1)))) return rc;
-  if ((rc = ctx->f3_points.Reserve(sizeof(float) * std::max<size_t>(hpts.size(), 3)))) return rc;
-  if ((rc = ctx->f3_low_points.Reserve(sizeof(float) * std::max<size_t>(lpts.size(), 3)))) return rc;
   if ((rc = ctx->f3_best.Reserve(sizeof(unsigned long long) * np + sizeof(float) * np))) return rc;
   if ((rc = ctx->f3_status.Reserve(sizeof(int32_t) * np))) return rc;
   if ((rc = ctx->f3_counter.Reserve(8 + 16 * sizeof(unsigned long long)))) return rc;
@@ -1091,25 +1116,64 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
   CSM_HIP(hipMemcpyAsync(dsub, sdesc.data(), sizeof(Submap3Desc) * num_submaps,
                          hipMemcpyHostToDevice, st));
   if (ny > 0) {
-    // Discrete-scan poses of the yaws that pass, built in parallel straight
-    // into pinned staging (the decode reads them from there).
-    if ((rc = ctx->f3_host_yaws.Reserve(sizeof(Yaw3Desc) * ny))) return rc;
-    Yaw3Desc* hy = ctx->f3_host_yaws.as<Yaw3Desc>();
-    ParallelPairs(np, [&](int64_t dp) {
-      const int64_t i = pair_of[dp];
-      Yaw3Desc* o = hy + pdesc[dp].yaw_begin;
-      BuildYaws(yk.data() + yaw_src[i], ys.data() + yaw_src[i], prep[i].num_yaws,
-                static_cast<int32_t>(dp), prep[i], o);
-      prep[i].yaws = o;
-    });
-    CSM_HIP(hipMemcpyAsync(ctx->f3_yaws.ptr, hy, sizeof(Yaw3Desc) * ny, hipMemcpyHostToDevice, st));
+    // Discrete-scan poses of the yaws that pass, built on the device from the
+    // compacted (k, score) lists; the few yaws whose float sin / cos rounding
+    // the device cannot decide are rebuilt here with libm and patched in.
+    std::vector<YawBuild3> yb(static_cast<size_t>(np));
+    for (int dp = 0; dp < np; ++dp) {
+      const PairPrep& pr = prep[pair_of[dp]];
+      YawBuild3& b = yb[dp];
+      b.siw = pr.submap_inv.w;
+      b.six = pr.submap_inv.x;
+      b.siy = pr.submap_inv.y;
+      b.siz = pr.submap_inv.z;
+      b.nqw = pr.node_q.w;
+      b.nqx = pr.node_q.x;
+      b.nqy = pr.node_q.y;
+      b.nqz = pr.node_q.z;
+      b.tx = pr.node_to_submap.t.x;
+      b.ty = pr.node_to_submap.t.y;
+      b.tz = pr.node_to_submap.t.z;
+      b.astep = pr.astep;
+      b.window = pr.angular_window;
+      b.src = static_cast<int32_t>(yaw_src[pair_of[dp]]);
+      b.yaw_begin = pdesc[dp].yaw_begin;
+      b.num = pdesc[dp].num_yaws;
+    }
+    // f3_items held the rotational-score inputs, which are consumed (synced).
+    if ((rc = ctx->f3_items.Reserve(sizeof(YawBuild3) * np + sizeof(YawFlag3) * kYawFlagCap + 16)))
+      return rc;
+    YawBuild3* dyb = ctx->f3_items.as<YawBuild3>();
+    YawFlag3* dflags = reinterpret_cast<YawFlag3*>(dyb + np);
+    unsigned* dflag_count = reinterpret_cast<unsigned*>(dflags + kYawFlagCap);
+    CSM_HIP(hipMemcpyAsync(dyb, yb.data(), sizeof(YawBuild3) * np, hipMemcpyHostToDevice, st));
+    CSM_HIP(hipMemsetAsync(dflag_count, 0, sizeof(unsigned), st));
+    CSM_HIP(LaunchYawBuild(dyb, np, dev_k, dev_s, ctx->f3_yaws.as<Yaw3Desc>(), dflag_count, dflags,
+                           st));
+    unsigned nflag = 0;
+    YawFlag3 flags[64];
+    CSM_HIP(hipMemcpyAsync(&nflag, dflag_count, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+    CSM_HIP(hipMemcpyAsync(flags, dflags, sizeof(flags), hipMemcpyDeviceToHost, st));
+    CSM_HIP(hipStreamSynchronize(st));
+    if (nflag > 0) {
+      std::vector<YawFlag3> all(flags, flags + std::min<unsigned>(nflag, 64));
+      if (nflag > 64) {
+        if (nflag > static_cast<unsigned>(kYawFlagCap)) return CSM_ERANGE;  // never seen: ~2^-16 per yaw
+        all.resize(nflag);
+        CSM_HIP(hipMemcpy(all.data(), dflags, sizeof(YawFlag3) * nflag, hipMemcpyDeviceToHost));
+      }
+      if ((rc = ctx->f3_host_yaws.Reserve(sizeof(Yaw3Desc) * all.size()))) return rc;
+      Yaw3Desc* hy = ctx->f3_host_yaws.as<Yaw3Desc>();
+      for (size_t f = 0; f < all.size(); ++f) {
+        const YawFlag3& fl = all[f];
+        BuildYaws(&fl.k, &fl.score, 1, fl.dp, prep[pair_of[fl.dp]], &hy[f]);
+        hy[f].yaw_id = fl.j;
+        CSM_HIP(hipMemcpyAsync(ctx->f3_yaws.as<Yaw3Desc>() + pdesc[fl.dp].yaw_begin + fl.j, &hy[f],
+                               sizeof(Yaw3Desc), hipMemcpyHostToDevice, st));
+      }
+    }
   }
-  if (!hpts.empty())
-    CSM_HIP(hipMemcpyAsync(ctx->f3_points.ptr, hpts.data(), sizeof(float) * hpts.size(),
-                           hipMemcpyHostToDevice, st));
-  if (!lpts.empty())
-    CSM_HIP(hipMemcpyAsync(ctx->f3_low_points.ptr, lpts.data(), sizeof(float) * lpts.size(),
-                           hipMemcpyHostToDevice, st));
+  CSM_HIP(hipStreamWaitEvent(st, ctx->f3_points_ready, 0));
   CSM_HIP(hipMemsetAsync(dbest, 0, sizeof(unsigned long long) * np, st));
   CSM_HIP(hipMemsetAsync(ctx->f3_status.ptr, 0, sizeof(int32_t) * np, st));
   CSM_HIP(hipMemsetAsync(ctx->f3_counter.ptr, 0, 8 + 16 * sizeof(unsigned long long), st));
@@ -1147,6 +1211,12 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
   CSM_HIP(hipMemcpyAsync(stat.data(), ctx->f3_status.ptr, sizeof(int32_t) * np,
                          hipMemcpyDeviceToHost, st));
   CSM_HIP(hipMemcpyAsync(prof, dstats, sizeof(prof), hipMemcpyDeviceToHost, st));
+  yk.resize(std::max(kept, 1u));
+  ys.resize(std::max(kept, 1u));
+  if (kept > 0) {
+    CSM_HIP(hipMemcpyAsync(yk.data(), dev_k, sizeof(int32_t) * kept, hipMemcpyDeviceToHost, st));
+    CSM_HIP(hipMemcpyAsync(ys.data(), dev_s, sizeof(float) * kept, hipMemcpyDeviceToHost, st));
+  }
   CSM_HIP(hipStreamSynchronize(st));
   if (ctx->timing) {
     float ms = 0.f;
@@ -1190,7 +1260,9 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
     const int ox =
         static_cast<int>((id >> (d.bits_z + d.bits_xy)) & ((1ull << d.bits_xy) - 1)) - d.wxy;
     const int yaw = static_cast<int>(id >> (d.bits_z + 2 * d.bits_xy));
-    const Yaw3Desc& y = prep[i].yaws[yaw];
+    // The winning discrete scan, rebuilt exactly as the device built it.
+    Yaw3Desc y;
+    BuildYaws(yk.data() + yaw_src[i] + yaw, ys.data() + yaw_src[i] + yaw, 1, dp, prep[i], &y);
     const float res = submaps[d.submap]->resolution;
     const V3 t0 = Rotate(Q4{1.f, 0.f, 0.f, 0.f}, V3{y.tx, y.ty, y.tz});
     const V3 t{t0.x + res * static_cast<float>(ox), t0.y + res * static_cast<float>(oy),

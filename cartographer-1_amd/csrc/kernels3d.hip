@@ -6,8 +6,10 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 #include "csm_device3d.h"
+#include "csm_launch3d.h"
 
 namespace csm {
 
@@ -340,6 +342,7 @@ rt3d_score2(const float* __restrict__ pad, int pnx, int pny, int pnz, int ox, in
 //    (the point is re-rotated from the cloud, RoundDiv per axis);
 //  * the clamp into the padded brick runs on the rounded coordinates with
 //    per-thread bounds, and the byte offset is three exact float FMAs.
+template <int U>
 __global__ void __launch_bounds__(768)
 rt3d_score3(const float* __restrict__ pad, int pnx, int pny, int pnz, int ox, int oy, int oz,
             float res, float inv, float eps, const float* __restrict__ points, int n,
@@ -386,27 +389,63 @@ rt3d_score3(const float* __restrict__ pad, int pnx, int pny, int pnz, int ox, in
     }
     __syncthreads();
     if (active) {
-      for (int i = 0; i < cnt; ++i) {
+      // Cell coordinates of point i for this thread's translation, with the
+      // rounding-safety test; the rare lookups within eps of a half-integer
+      // take the reference's IEEE quotient (the point re-rotated from the
+      // cloud, RoundDiv per axis).
+      auto cell = [&](int i, float* rx, float* ry, float* rz) {
         const float4 a = my[i];
         const float yx = __fadd_rn(a.x, tsx), yy = __fadd_rn(a.y, tsy), yz = __fadd_rn(a.z, tsz);
-        float rx = rintf(yx), ry = rintf(yy), rz = rintf(yz);
-        const float dm = fmaxf(fmaxf(fabsf(__fsub_rn(yx, rx)), fabsf(__fsub_rn(yy, ry))),
-                               fabsf(__fsub_rn(yz, rz)));
-        if (dm >= half) {  // rare: the IEEE quotient of the reference decides
-          const float* p = points + 3 * static_cast<int64_t>(tb + i);
-          float ax, ay, az;
-          Rotate3(q.w, q.x, q.y, q.z, p[0], p[1], p[2], &ax, &ay, &az);
-          rx = static_cast<float>(RoundDiv(__fadd_rn(ax, tr.x), res, inv));
-          ry = static_cast<float>(RoundDiv(__fadd_rn(ay, tr.y), res, inv));
-          rz = static_cast<float>(RoundDiv(__fadd_rn(az, tr.z), res, inv));
-        }
+        *rx = rintf(yx);
+        *ry = rintf(yy);
+        *rz = rintf(yz);
+        const float dm = fmaxf(fmaxf(fabsf(__fsub_rn(yx, *rx)), fabsf(__fsub_rn(yy, *ry))),
+                               fabsf(__fsub_rn(yz, *rz)));
+        return dm;
+      };
+      auto exact = [&](int i, float* rx, float* ry, float* rz) {
+        const float* p = points + 3 * static_cast<int64_t>(tb + i);
+        float ax, ay, az;
+        Rotate3(q.w, q.x, q.y, q.z, p[0], p[1], p[2], &ax, &ay, &az);
+        *rx = static_cast<float>(RoundDiv(__fadd_rn(ax, tr.x), res, inv));
+        *ry = static_cast<float>(RoundDiv(__fadd_rn(ay, tr.y), res, inv));
+        *rz = static_cast<float>(RoundDiv(__fadd_rn(az, tr.z), res, inv));
+      };
+      auto offset = [&](float rx, float ry, float rz) {
         rx = __builtin_amdgcn_fmed3f(rx, lx, hx);
         ry = __builtin_amdgcn_fmed3f(ry, ly, hy);
         rz = __builtin_amdgcn_fmed3f(rz, lz, hz);
         // Exact: every term is an integer below 2^24.
-        const float off = fmaf(rz, sz, fmaf(ry, sy, fmaf(rx, sx, base)));
+        return static_cast<int>(fmaf(rz, sz, fmaf(ry, sy, fmaf(rx, sx, base))));
+      };
+      // U points per step: their U gathers are issued together and added in
+      // point order afterwards (the same float sum, U loads in flight).
+      int i = 0;
+      for (; i + U <= cnt; i += U) {
+        float rx[U], ry[U], rz[U], dm[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) dm[u] = cell(i + u, &rx[u], &ry[u], &rz[u]);
+        float dmax = dm[0];
+#pragma unroll
+        for (int u = 1; u < U; ++u) dmax = fmaxf(dmax, dm[u]);
+        if (dmax >= half) {
+#pragma unroll
+          for (int u = 0; u < U; ++u)
+            if (dm[u] >= half) exact(i + u, &rx[u], &ry[u], &rz[u]);
+        }
+        float v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          v[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+              rsrc, offset(rx[u], ry[u], rz[u]), 0, 0));
+#pragma unroll
+        for (int u = 0; u < U; ++u) sum = __fadd_rn(sum, v[u]);
+      }
+      for (; i < cnt; ++i) {
+        float rx, ry, rz;
+        if (cell(i, &rx, &ry, &rz) >= half) exact(i, &rx, &ry, &rz);
         sum = __fadd_rn(sum, __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
-                                 rsrc, static_cast<int>(off), 0, 0)));
+                                 rsrc, offset(rx, ry, rz), 0, 0)));
       }
     }
   }
@@ -1294,16 +1333,74 @@ __device__ __forceinline__ float PacketSum(F v, int n) {
   return r;
 }
 
-__global__ void rot_scores(const RotPair3* __restrict__ pairs, int num_pairs,
-                           const float* __restrict__ hists, float* __restrict__ out) {
+// Two sums over the same terms in one pass, each in PacketSum's order.
+template <typename F>
+__device__ __forceinline__ float2 PacketSum2(F v, int n) {
+  const int a2 = (n / 8) * 8, a1 = (n / 4) * 4;
+  auto add = [](float2 a, float2 b) { return make_float2(__fadd_rn(a.x, b.x), __fadd_rn(a.y, b.y)); };
+  if (a1 == 0) {
+    if (n == 0) return make_float2(0.f, 0.f);
+    float2 r = v(0);
+    for (int i = 1; i < n; ++i) r = add(r, v(i));
+    return r;
+  }
+  float2 p0 = v(0), p1 = v(1), p2 = v(2), p3 = v(3);
+  if (a1 > 4) {
+    float2 q0 = v(4), q1 = v(5), q2 = v(6), q3 = v(7);
+    for (int i = 8; i < a2; i += 8) {
+      p0 = add(p0, v(i));
+      p1 = add(p1, v(i + 1));
+      p2 = add(p2, v(i + 2));
+      p3 = add(p3, v(i + 3));
+      q0 = add(q0, v(i + 4));
+      q1 = add(q1, v(i + 5));
+      q2 = add(q2, v(i + 6));
+      q3 = add(q3, v(i + 7));
+    }
+    p0 = add(p0, q0);
+    p1 = add(p1, q1);
+    p2 = add(p2, q2);
+    p3 = add(p3, q3);
+    if (a1 > a2) {
+      p0 = add(p0, v(a2));
+      p1 = add(p1, v(a2 + 1));
+      p2 = add(p2, v(a2 + 2));
+      p3 = add(p3, v(a2 + 3));
+    }
+  }
+  float2 r = add(add(p0, p2), add(p1, p3));
+  for (int i = a1; i < n; ++i) r = add(r, v(i));
+  return r;
+}
+
+// One block per (pair, 64 yaws): both histograms staged in LDS, the submap
+// norm computed once per block, the rotated bucket index wrapped by a
+// compare instead of '%', and the scan norm and the dot product summed in
+// one pass (each still in the packet order of its own Eigen reduction).
+constexpr int kRotThreads = 64;
+
+__global__ void __launch_bounds__(kRotThreads)
+rot_scores(const RotPair3* __restrict__ pairs, int num_pairs, const float* __restrict__ hists,
+           float* __restrict__ out) {
+  __shared__ float hs[kMaxHistogram + 1], ss[kMaxHistogram];
+  __shared__ float submap_norm_sh;
   const int p = blockIdx.y;
   if (p >= num_pairs) return;
   const RotPair3 rp = pairs[p];
-  const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k > 2 * rp.window) return;
+  if (static_cast<int>(blockIdx.x) * kRotThreads > 2 * rp.window) return;
   const int n = rp.size;
-  const float* h = hists + rp.node_hist;
-  const float* sub = hists + rp.submap_hist;
+  const int tid = threadIdx.x;
+  for (int i = tid; i < n; i += kRotThreads) {
+    hs[i] = hists[rp.node_hist + i];
+    ss[i] = hists[rp.submap_hist + i];
+  }
+  if (tid == 0 && n > 0) hs[n] = hists[rp.node_hist];  // h[(n - 1 + 1 + full) mod n] at full = 0
+  __syncthreads();
+  if (tid == 0)
+    submap_norm_sh = sqrtf(PacketSum([&](int i) { return __fmul_rn(ss[i], ss[i]); }, n));
+  __syncthreads();
+  const int k = blockIdx.x * kRotThreads + tid;
+  if (k > 2 * rp.window) return;
   const float angle = __fadd_rn(rp.yaw0, __fmul_rn(static_cast<float>(k - rp.window), rp.step));
   int full = 0;
   float fraction = 0.f;
@@ -1313,18 +1410,118 @@ __global__ void rot_scores(const RotPair3* __restrict__ pairs, int num_pairs,
     full = static_cast<int>(roundf(__fsub_rn(rb, 0.5f)));
     fraction = __fsub_rn(rb, static_cast<float>(full));
     while (full < 0) full += n;
+    full %= n;  // (i + full) mod n below is i + full, less n past the end
   }
   const float one_minus = __fsub_rn(1.f, fraction);
-  auto rot = [&](int i) {
-    return __fadd_rn(__fmul_rn(fraction, h[(i + 1 + full) % n]), __fmul_rn(one_minus, h[(i + full) % n]));
-  };
-  const float scan_norm = sqrtf(PacketSum([&](int i) { const float r = rot(i); return __fmul_rn(r, r); }, n));
-  const float submap_norm = sqrtf(PacketSum([&](int i) { return __fmul_rn(sub[i], sub[i]); }, n));
-  const float normalization = __fmul_rn(scan_norm, submap_norm);
+  // hs[n] repeats hs[0], so j + 1 needs no second wrap when j = n - 1.
+  const float2 sums = PacketSum2([&](int i) {
+    int j = i + full;
+    j -= j >= n ? n : 0;
+    const float r = __fadd_rn(__fmul_rn(fraction, hs[j + 1]), __fmul_rn(one_minus, hs[j]));
+    return make_float2(__fmul_rn(r, r), __fmul_rn(ss[i], r));
+  }, n);
+  const float scan_norm = sqrtf(sums.x);
+  const float normalization = __fmul_rn(scan_norm, submap_norm_sh);
   float score = 1.f;
-  if (!(normalization < 1e-3f))
-    score = __fdiv_rn(PacketSum([&](int i) { return __fmul_rn(sub[i], rot(i)); }, n), normalization);
+  if (!(normalization < 1e-3f)) score = __fdiv_rn(sums.y, normalization);
   out[rp.out + k] = score;
+}
+
+// GenerateDiscreteScans :277-294 on the device for the passing yaws, with
+// the float arithmetic of the host restatement (host3d.cc BuildYaws):
+// angle = (k - A) * step, AngleAxisToQuat through double sin / cos of
+// norm / 2 rounded to float, Eigen's SSE quaternion products, the normalized
+// rotation of GetPoseFromCandidate. The device's double sin / cos may differ
+// from libm's in the last ulps; a float rounding of them is kept only when
+// the double value lies farther than 2^-40 relative from a float rounding
+// boundary (both results are then on the same side), otherwise the yaw is
+// flagged and the host rebuilds it.
+__device__ __forceinline__ bool NearFloatBoundary(double v) {
+  v = fabs(v);  // round-to-nearest-even is symmetric (cos < 0 past |angle| = pi)
+  const float f = static_cast<float>(v);
+  if (!(f >= 1.2e-38f) || !(f < 3.0e38f)) return true;  // zero, subnormal, huge: the host decides
+  const double fd = static_cast<double>(f);
+  const double up = static_cast<double>(__int_as_float(__float_as_int(f) + 1));
+  const double dn = static_cast<double>(__int_as_float(__float_as_int(f) - 1));
+  const double d = fmin(fabs(v - 0.5 * (fd + up)), fabs(v - 0.5 * (fd + dn)));
+  return d <= fabs(v) * 0x1p-40;
+}
+
+__device__ __forceinline__ float4 QMulDev(float4 a, float4 b) {  // (w, x, y, z) in (x, y, z, w)
+  // a.w*b.w - a.x*b.x - (a.z*b.z + a.y*b.y), ... : host3d.cc QMul term order.
+  const float w = __fsub_rn(__fsub_rn(__fmul_rn(a.x, b.x), __fmul_rn(a.y, b.y)),
+                            __fadd_rn(__fmul_rn(a.w, b.w), __fmul_rn(a.z, b.z)));
+  const float x = __fadd_rn(__fsub_rn(__fmul_rn(a.y, b.x), __fmul_rn(a.w, b.z)),
+                            __fadd_rn(__fmul_rn(a.z, b.w), __fmul_rn(a.x, b.y)));
+  const float y = __fadd_rn(__fsub_rn(__fmul_rn(a.z, b.x), __fmul_rn(a.y, b.w)),
+                            __fadd_rn(__fmul_rn(a.w, b.y), __fmul_rn(a.x, b.z)));
+  const float z = __fadd_rn(__fsub_rn(__fmul_rn(a.w, b.x), __fmul_rn(a.z, b.y)),
+                            __fadd_rn(__fmul_rn(a.y, b.z), __fmul_rn(a.x, b.w)));
+  return make_float4(w, x, y, z);
+}
+
+__global__ void __launch_bounds__(64)
+yaw_build(const YawBuild3* __restrict__ items, const int32_t* __restrict__ ks,
+          const float* __restrict__ ss, Yaw3Desc* __restrict__ out, unsigned* __restrict__ flag_count,
+          YawFlag3* __restrict__ flags) {
+  const int dp = blockIdx.x;
+  const YawBuild3 it = items[dp];
+  // Quaternions held as float4 (x = w, y = x, z = y, w = z).
+  const float4 si = make_float4(it.siw, it.six, it.siy, it.siz);
+  const float4 nq = make_float4(it.nqw, it.nqx, it.nqy, it.nqz);
+  for (int j = threadIdx.x; j < it.num; j += 64) {
+    const int k = ks[it.src + j];
+    const float score = ss[it.src + j];
+    const float angle = __fmul_rn(static_cast<float>(k - it.window), it.astep);
+    // AngleAxisToQuat(V3{0, 0, angle}).
+    float scale = 0.5f, w = 1.f;
+    const float sq = __fadd_rn(__fmul_rn(0.f, 0.f), __fadd_rn(__fmul_rn(0.f, 0.f), __fmul_rn(angle, angle)));
+    bool flag = false;
+    if (static_cast<double>(sq) > 1e-8) {
+      const float norm = sqrtf(sq);
+      const double h = static_cast<double>(norm) / 2.;
+      const double sv = sin(h) / static_cast<double>(norm), cv = cos(h);
+      flag = NearFloatBoundary(sv) || NearFloatBoundary(cv);
+      scale = static_cast<float>(sv);
+      w = static_cast<float>(cv);
+    }
+    const float4 yaw = make_float4(w, __fmul_rn(scale, 0.f), __fmul_rn(scale, 0.f), __fmul_rn(scale, angle));
+    const float4 q = QMulDev(QMulDev(si, yaw), nq);
+    float4 qn = QMulDev(make_float4(1.f, 0.f, 0.f, 0.f), q);
+    const float n2 = __fadd_rn(__fadd_rn(__fmul_rn(qn.y, qn.y), __fmul_rn(qn.w, qn.w)),
+                               __fadd_rn(__fmul_rn(qn.z, qn.z), __fmul_rn(qn.x, qn.x)));
+    if (n2 > 0.f) {
+      const float n = sqrtf(n2);
+      qn = make_float4(__fdiv_rn(qn.x, n), __fdiv_rn(qn.y, n), __fdiv_rn(qn.z, n), __fdiv_rn(qn.w, n));
+    }
+    Yaw3Desc y;
+    y.qw = q.x;
+    y.qx = q.y;
+    y.qy = q.z;
+    y.qz = q.w;
+    y.nw = qn.x;
+    y.nx = qn.y;
+    y.ny = qn.z;
+    y.nz = qn.w;
+    y.tx = it.tx;
+    y.ty = it.ty;
+    y.tz = it.tz;
+    y.rotational_score = score;
+    y.pair = dp;
+    y.yaw_id = j;
+    out[it.yaw_begin + j] = y;
+    if (flag) {
+      const unsigned f = atomicAdd(flag_count, 1u);
+      if (f < static_cast<unsigned>(kYawFlagCap)) {
+        YawFlag3 r;
+        r.dp = dp;
+        r.j = j;
+        r.k = k;
+        r.score = score;
+        flags[f] = r;
+      }
+    }
+  }
 }
 
 // The yaws of each pair whose rotational score passes (the filter of
@@ -1442,7 +1639,7 @@ hipError_t LaunchRt3dScore3(int num_rot, hipStream_t st, const float* pad, const
                             int scores_pitch) {
   const int threads = (kRt3Rpb * num_trans + 63) / 64 * 64;
   const int blocks = (num_rot + kRt3Rpb - 1) / kRt3Rpb;
-  hipLaunchKernelGGL(rt3d_score3, dim3(blocks), dim3(threads), 0, st, pad, gb.nx + 2, gb.ny + 2,
+  hipLaunchKernelGGL(rt3d_score3<4>, dim3(blocks), dim3(threads), 0, st, pad, gb.nx + 2, gb.ny + 2,
                      gb.nz + 2, gb.ox, gb.oy, gb.oz, res, 1.f / res, eps, points, n, rot, rot_angle,
                      trans + t_base, num_trans, t_base, num_rot, wt, wr, best, scores,
                      scores_pitch);
@@ -1478,9 +1675,17 @@ hipError_t LaunchFast3dFinalize(int num_pairs, hipStream_t st, const Submap3Desc
 hipError_t LaunchRotScores(const void* pairs, int num_pairs, int max_yaws, const float* hists,
                            float* out, hipStream_t st) {
   if (num_pairs <= 0 || max_yaws <= 0) return hipSuccess;
-  const int threads = 64;
+  const int threads = kRotThreads;
   hipLaunchKernelGGL(rot_scores, dim3((max_yaws + threads - 1) / threads, num_pairs), dim3(threads),
                      0, st, static_cast<const RotPair3*>(pairs), num_pairs, hists, out);
+  return hipGetLastError();
+}
+
+hipError_t LaunchYawBuild(const YawBuild3* items, int num_pairs, const int32_t* k, const float* s,
+                          Yaw3Desc* out, unsigned* flag_count, YawFlag3* flags, hipStream_t st) {
+  if (num_pairs <= 0) return hipSuccess;
+  hipLaunchKernelGGL(yaw_build, dim3(num_pairs), dim3(64), 0, st, items, k, s, out, flag_count,
+                     flags);
   return hipGetLastError();
 }
 
