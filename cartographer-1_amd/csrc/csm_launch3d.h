@@ -37,6 +37,20 @@ hipError_t LaunchRt3dScore3(int num_rot, hipStream_t st, const float* pad, const
                             const float* rot_angle, const float4* trans, int num_trans, int t_base,
                             double wt, double wr, unsigned long long* best, float* scores,
                             int scores_pitch);
+// rt3d_score4: lanes = 64 rotations of a 4 x 4 x 4 block of the angular
+// lattice (rot / rot_index in block order, index -1 for holes), waves =
+// translations. `pad` is the brick padded by P cells per side (LaunchPadProbBrick
+// with P); points whose scaled rotation lies outside [safe_lo, safe_hi] take
+// the clamped path.
+constexpr int kRt4Waves = 8, kRt4Tw = 2, kRt4Tile = 32;
+hipError_t LaunchPadProbBrickP(const float* prob, const Brick3& gb, int P, float* out,
+                               hipStream_t st);
+hipError_t LaunchRt3dScore4(int num_blocks, hipStream_t st, const float* pad, const Brick3& gb,
+                            int P, float res, float eps, float4 safe_lo, float4 safe_hi,
+                            const float* points, int n, const float4* rot, const int* rot_index,
+                            const float* rot_angle, const float4* trans, int num_trans,
+                            int num_rot, double wt, double wr, unsigned long long* best,
+                            float* scores, int scores_pitch);
 // Items [item_begin, item_begin + num_items) of the yaw list; `large`
 // selects the build for clouds of more than kSmall3dPoints points.
 hipError_t LaunchFast3dSearch(bool large, int grid, hipStream_t st, const Submap3Desc* submaps,

@@ -313,7 +313,7 @@ int MakeRt3dWindow(const csm_rt_options* o, float res, const csm_pose3d* initial
 // candidate's score into the device array scores[r * num_trans + t].
 int RunRt3d(csm_context* ctx, const csm_rt_options* o, const csm_hybrid_grid* grid, const float* xyz,
             int32_t n, const Rt3dWindow& w, const float4* rot, const float* angle,
-            int64_t num_rot, unsigned long long* key, float* dscores) {
+            int64_t num_rot, unsigned long long* key, float* dscores, bool lattice) {
   hipStream_t st = ctx->stream;
   int rc;
   const float res = grid->resolution;
@@ -345,13 +345,26 @@ int RunRt3d(csm_context* ctx, const csm_rt_options* o, const csm_hybrid_grid* gr
     CSM_HIP(LaunchPadProbBrick(grid->prob.as<float>(), gb, g->prob_pad.as<float>(), st));
     g->prob_pad_ready = true;
   }
+  // v4 (rotation lanes) over a brick padded by P cells, P = the translation
+  // lattice's reach in cells + 2, when its byte offsets are exact in float.
+  int P = 0;
+  {
+    float reach = 0.f;
+    const float4 c = w.trans[w.num_trans / 2];  // the centre: initial translation
+    for (const float4& t : w.trans)
+      reach = std::max({reach, std::fabs(t.x - c.x), std::fabs(t.y - c.y), std::fabs(t.z - c.z)});
+    P = static_cast<int>(std::ceil(reach / res)) + 2;
+  }
+  const bool v4 = v2 && !std::getenv("CSM_RT3D_V3") && !std::getenv("CSM_RT3D_V2") &&
+                  4 * static_cast<int64_t>(gb.nx + 2 * P) * (gb.ny + 2 * P) * (gb.nz + 2 * P) <
+                      (int64_t{1} << 24);
   // v3 when the padded brick's byte offsets are exact in float (< 2^24).
-  const bool v3 = v2 && !std::getenv("CSM_RT3D_V2") &&
+  const bool v3 = v2 && !v4 && !std::getenv("CSM_RT3D_V2") &&
                   4 * static_cast<int64_t>(gb.nx + 2) * (gb.ny + 2) * (gb.nz + 2) < (int64_t{1} << 24);
   // |(a' + tr') - fl(fl(a + tr) / res)| <= 2.5 * 2^-23 * (|a| + |tr|) / res
   // (rt3d_score3); the threshold takes 4 * 2^-23 * (A + T + 1).
   float eps = 0.f;
-  if (v3) {
+  if (v3 || v4) {
     float amax = 0.f, tmax = 0.f;
     for (int i = 0; i < n; ++i)
       amax = std::max(amax, NormV(V3{xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2]}));
@@ -360,8 +373,83 @@ int RunRt3d(csm_context* ctx, const csm_rt_options* o, const csm_hybrid_grid* gr
     eps = static_cast<float>(4.0 * std::ldexp(1.0, -23) *
                              (static_cast<double>(amax) * 1.001 / res + tmax / res + 1.0));
   }
-  if (ctx->timing) CSM_HIP(hipEventRecord(ctx->ev0, st));
-  for (int64_t t0 = 0; t0 < num_trans; t0 += kRt3dThreads) {
+  if (v4) {
+    csm_hybrid_grid* g = const_cast<csm_hybrid_grid*>(grid);
+    if (g->prob_wide_pad != P) {
+      if ((rc = g->prob_wide.Reserve(sizeof(float) * (gb.nx + 2 * P) * (gb.ny + 2 * P) *
+                                     (gb.nz + 2 * P))))
+        return rc;
+      CSM_HIP(LaunchPadProbBrickP(grid->prob.as<float>(), gb, P, g->prob_wide.as<float>(), st));
+      g->prob_wide_pad = P;
+    }
+    // Rotations in 4 x 4 x 4 blocks of the (rx, ry, rz) lattice (one block
+    // per 64 lanes; holes past the lattice edge carry index -1), or in the
+    // given order for a subset.
+    std::vector<float4> brot;
+    std::vector<int32_t> bidx;
+    if (lattice) {
+      const int64_t na = w.na, nb = (na + 3) / 4;
+      brot.assign(static_cast<size_t>(nb * nb * nb * 64), make_float4(0.f, 0.f, 0.f, 1.f));
+      bidx.assign(brot.size(), -1);
+      int64_t slot = 0;
+      for (int64_t bz = 0; bz < nb; ++bz)
+        for (int64_t by = 0; by < nb; ++by)
+          for (int64_t bx = 0; bx < nb; ++bx)
+            for (int lane = 0; lane < 64; ++lane, ++slot) {
+              const int64_t rx = 4 * bx + (lane & 3), ry = 4 * by + ((lane >> 2) & 3),
+                            rz = 4 * bz + (lane >> 4);
+              if (rx >= na || ry >= na || rz >= na) continue;
+              const int64_t r = (rz * na + ry) * na + rx;
+              brot[slot] = rot[r];
+              bidx[slot] = static_cast<int32_t>(r);
+            }
+    } else {
+      brot.assign(static_cast<size_t>((num_rot + 63) / 64 * 64), make_float4(0.f, 0.f, 0.f, 1.f));
+      bidx.assign(brot.size(), -1);
+      for (int64_t r = 0; r < num_rot; ++r) {
+        brot[r] = rot[r];
+        bidx[r] = static_cast<int32_t>(r);
+      }
+    }
+    // The scaled rotated point a' keeps rint(a' + t') inside the padded box
+    // for every translation t' when a' + min t' >= lo and a' + max t' <= hi
+    // per axis (a margin covers the add's rounding).
+    float tmin[3] = {0.f, 0.f, 0.f}, tmax3[3] = {0.f, 0.f, 0.f};
+    const float inv = 1.f / res;
+    for (int64_t t = 0; t < num_trans; ++t) {
+      const float v[3] = {w.trans[t].x * inv, w.trans[t].y * inv, w.trans[t].z * inv};
+      for (int a = 0; a < 3; ++a) {
+        tmin[a] = t == 0 ? v[a] : std::min(tmin[a], v[a]);
+        tmax3[a] = t == 0 ? v[a] : std::max(tmax3[a], v[a]);
+      }
+    }
+    const int org[3] = {gb.ox, gb.oy, gb.oz}, dim[3] = {gb.nx, gb.ny, gb.nz};
+    float lo[3], hi[3];
+    for (int a = 0; a < 3; ++a) {
+      lo[a] = static_cast<float>(org[a] - P) - tmin[a] + 0.01f;
+      hi[a] = static_cast<float>(org[a] - P + dim[a] + 2 * P - 1) - tmax3[a] - 0.01f;
+    }
+    const size_t rot_bytes = sizeof(float4) * brot.size() + sizeof(int32_t) * bidx.size();
+    if ((rc = ctx->rt3_rot4.Reserve(rot_bytes))) return rc;
+    float4* drot4 = ctx->rt3_rot4.as<float4>();
+    int32_t* didx = reinterpret_cast<int32_t*>(drot4 + brot.size());
+    CSM_HIP(hipMemcpyAsync(drot4, brot.data(), sizeof(float4) * brot.size(), hipMemcpyHostToDevice,
+                           st));
+    CSM_HIP(hipMemcpyAsync(didx, bidx.data(), sizeof(int32_t) * bidx.size(), hipMemcpyHostToDevice,
+                           st));
+    if (ctx->timing) CSM_HIP(hipEventRecord(ctx->ev0, st));
+    CSM_HIP(LaunchRt3dScore4(static_cast<int>(brot.size() / 64), st, grid->prob_wide.as<float>(), gb,
+                             P, res, eps, make_float4(lo[0], lo[1], lo[2], 0.f),
+                             make_float4(hi[0], hi[1], hi[2], 0.f), ctx->rt3_points.as<float>(), n,
+                             drot4, didx, dangle, ctx->rt3_trans.as<float4>(),
+                             static_cast<int>(num_trans), static_cast<int>(num_rot),
+                             o->translation_delta_cost_weight, o->rotation_delta_cost_weight,
+                             ctx->rt3_best.as<unsigned long long>(), dscores,
+                             static_cast<int>(num_trans)));
+  } else if (ctx->timing) {
+    CSM_HIP(hipEventRecord(ctx->ev0, st));
+  }
+  for (int64_t t0 = 0; t0 < num_trans && !v4; t0 += kRt3dThreads) {
     const int cnt = static_cast<int>(std::min<int64_t>(kRt3dThreads, num_trans - t0));
     if (v3)
       CSM_HIP(LaunchRt3dScore3(static_cast<int>(num_rot), st, grid->prob_pad.as<float>(), gb, res,
@@ -411,7 +499,7 @@ int csm_rt3d_match(csm_context* ctx, const csm_rt_options* o, const csm_hybrid_g
   if ((rc = MakeRt3dWindow(o, grid->resolution, initial, xyz, n, &w))) return rc;
   unsigned long long key = 0;
   if ((rc = RunRt3d(ctx, o, grid, xyz, n, w, w.rot.data(), w.angle.data(), w.num_rot, &key,
-                    nullptr)))
+                    nullptr, true)))
     return rc;
   if (key == 0) return CSM_EHIP;
   const uint32_t low = static_cast<uint32_t>(key & 0xffffffffu);
@@ -464,7 +552,7 @@ int csm_rt3d_score_rotations(csm_context* ctx, const csm_rt_options* o,
   const size_t count = static_cast<size_t>(num_rotations) * w.num_trans;
   if ((rc = dscores.Reserve(sizeof(float) * count))) return rc;
   if ((rc = RunRt3d(ctx, o, grid, xyz, n, w, rot.data(), angle.data(), num_rotations, nullptr,
-                    dscores.as<float>())))
+                    dscores.as<float>(), false)))
     return rc;
   CSM_HIP(hipMemcpy(scores, dscores.ptr, sizeof(float) * count, hipMemcpyDeviceToHost));
   return CSM_OK;

@@ -197,13 +197,13 @@ rt3d_score(const float* __restrict__ prob, Brick3 gb, float res, float inv,
 //    7^3 translations, against 343 of 384).
 constexpr int kRt3Rpb = 2;
 
-__global__ void pad_prob_brick(const float* __restrict__ prob, Brick3 gb, float* __restrict__ out) {
+__global__ void pad_prob_brick(const float* __restrict__ prob, Brick3 gb, int P, float* __restrict__ out) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  const int px = gb.nx + 2, py = gb.ny + 2, pz = gb.nz + 2;
+  const int px = gb.nx + 2 * P, py = gb.ny + 2 * P, pz = gb.nz + 2 * P;
   if (i >= static_cast<int64_t>(px) * py * pz) return;
-  const int x = static_cast<int>(i % px) - 1;
-  const int y = static_cast<int>((i / px) % py) - 1;
-  const int z = static_cast<int>(i / (static_cast<int64_t>(px) * py)) - 1;
+  const int x = static_cast<int>(i % px) - P;
+  const int y = static_cast<int>((i / px) % py) - P;
+  const int z = static_cast<int>(i / (static_cast<int64_t>(px) * py)) - P;
   float v = 0.1f;
   if (x >= 0 && x < gb.nx && y >= 0 && y < gb.ny && z >= 0 && z < gb.nz)
     v = prob[(static_cast<int64_t>(z) * gb.ny + y) * gb.nx + x];
@@ -468,6 +468,136 @@ rt3d_score3(const float* __restrict__ pad, int pnx, int pny, int pnz, int ox, in
   if (tid == 0) {
     unsigned long long k = red[0];
     for (int w = 1; w < static_cast<int>(blockDim.x / 64); ++w) k = red[w] > k ? red[w] : k;
+    atomicMax(best, k);
+  }
+}
+
+// RTCSM3D, v4: the same candidates, cell rule, sums and key as v3, with the
+// lanes of a wave on 64 ROTATIONS (a 4 x 4 x 4 block of the angular lattice)
+// and the waves on translations (kRt4Tw each). For one point and one
+// translation, neighbouring rotations move the point by about a cell at the
+// scan's maximum range and by a fraction of one nearer in, so a gather
+// touches ~4 cache lines instead of the ~15 of 64 translations of one
+// rotation (tools/rt3d_lines_sim.py). Each lane rotates the points of a tile
+// by its own rotation into LDS (shared by the workgroup's translations). The
+// brick is padded by P cells of 0.1 per side; a point whose scaled rotation
+// lies inside [safe_lo, safe_hi] (host: the padded box shrunk by every
+// translation's reach) needs no clamp for any translation, the others and
+// the rounding band take the clamped, exact path.
+__global__ void __launch_bounds__(64 * kRt4Waves)
+rt3d_score4(const float* __restrict__ pad, int pnx, int pny, int pnz, float bx, float by, float bz,
+            float res, float inv, float eps, float4 safe_lo, float4 safe_hi,
+            const float* __restrict__ points, int n, const float4* __restrict__ rot,
+            const int* __restrict__ rot_index, const float* __restrict__ rot_angle,
+            const float4* __restrict__ trans, int num_trans, int num_rot, double wt, double wr,
+            unsigned long long* __restrict__ best, float* __restrict__ scores, int scores_pitch) {
+  __shared__ float4 rp[kRt4Tile][64];
+  __shared__ unsigned long long red[kRt4Waves];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int slot = blockIdx.x * 64 + lane;
+  const int ri = rot_index[slot];
+  const float4 q = rot[slot];  // (x, y, z, w); identity in holes
+  const int t0 = (blockIdx.y * kRt4Waves + wave) * kRt4Tw;
+  float tsx[kRt4Tw], tsy[kRt4Tw], tsz[kRt4Tw];
+  float4 tr[kRt4Tw];
+#pragma unroll
+  for (int u = 0; u < kRt4Tw; ++u) {
+    tr[u] = trans[min(t0 + u, num_trans - 1)];
+    tsx[u] = __fmul_rn(tr[u].x, inv);
+    tsy[u] = __fmul_rn(tr[u].y, inv);
+    tsz[u] = __fmul_rn(tr[u].z, inv);
+  }
+  const float lx = -bx, ly = -by, lz = -bz;
+  const float hx = static_cast<float>(pnx - 1) - bx, hy = static_cast<float>(pny - 1) - by,
+              hz = static_cast<float>(pnz - 1) - bz;
+  const float sx = 4.f, sy = 4.f * static_cast<float>(pnx),
+              sz = 4.f * static_cast<float>(pnx) * static_cast<float>(pny);
+  const float base = 4.f * ((bz * static_cast<float>(pny) + by) * static_cast<float>(pnx) + bx);
+  const float half = 0.5f - eps;
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(pad), 0, static_cast<int>(4u * pnx * pny * pnz), 0x00020000);
+  float sum[kRt4Tw];
+#pragma unroll
+  for (int u = 0; u < kRt4Tw; ++u) sum[u] = 0.f;
+  for (int tb = 0; tb < n; tb += kRt4Tile) {
+    const int cnt = min(kRt4Tile, n - tb);
+    __syncthreads();
+    for (int j = wave; j < cnt; j += kRt4Waves) {
+      const float* p = points + 3 * static_cast<int64_t>(tb + j);
+      float ax, ay, az;
+      Rotate3(q.w, q.x, q.y, q.z, p[0], p[1], p[2], &ax, &ay, &az);
+      const float sxv = __fmul_rn(ax, inv), syv = __fmul_rn(ay, inv), szv = __fmul_rn(az, inv);
+      const bool inside = sxv >= safe_lo.x && sxv <= safe_hi.x && syv >= safe_lo.y &&
+                          syv <= safe_hi.y && szv >= safe_lo.z && szv <= safe_hi.z;
+      rp[j][lane] = make_float4(sxv, syv, szv, inside ? 0.f : 1.f);
+    }
+    __syncthreads();
+    for (int i = 0; i < cnt; ++i) {
+      const float4 a = rp[i][lane];
+      float rx[kRt4Tw], ry[kRt4Tw], rz[kRt4Tw], dm[kRt4Tw];
+      float dmax = a.w;  // 1 outside the safe box: the clamped path
+#pragma unroll
+      for (int u = 0; u < kRt4Tw; ++u) {
+        const float yx = __fadd_rn(a.x, tsx[u]), yy = __fadd_rn(a.y, tsy[u]),
+                    yz = __fadd_rn(a.z, tsz[u]);
+        rx[u] = rintf(yx);
+        ry[u] = rintf(yy);
+        rz[u] = rintf(yz);
+        dm[u] = fmaxf(fmaxf(fabsf(__fsub_rn(yx, rx[u])), fabsf(__fsub_rn(yy, ry[u]))),
+                      fabsf(__fsub_rn(yz, rz[u])));
+        dmax = fmaxf(dmax, dm[u]);
+      }
+      if (dmax >= half) {  // rare: exact quotient and / or clamp
+        const float* p = points + 3 * static_cast<int64_t>(tb + i);
+        float ax, ay, az;
+        Rotate3(q.w, q.x, q.y, q.z, p[0], p[1], p[2], &ax, &ay, &az);
+#pragma unroll
+        for (int u = 0; u < kRt4Tw; ++u) {
+          if (dm[u] >= half) {
+            rx[u] = static_cast<float>(RoundDiv(__fadd_rn(ax, tr[u].x), res, inv));
+            ry[u] = static_cast<float>(RoundDiv(__fadd_rn(ay, tr[u].y), res, inv));
+            rz[u] = static_cast<float>(RoundDiv(__fadd_rn(az, tr[u].z), res, inv));
+          }
+          rx[u] = __builtin_amdgcn_fmed3f(rx[u], lx, hx);
+          ry[u] = __builtin_amdgcn_fmed3f(ry[u], ly, hy);
+          rz[u] = __builtin_amdgcn_fmed3f(rz[u], lz, hz);
+        }
+      }
+      float v[kRt4Tw];
+#pragma unroll
+      for (int u = 0; u < kRt4Tw; ++u) {
+        // Exact: every term is an integer below 2^24.
+        const float off = fmaf(rz[u], sz, fmaf(ry[u], sy, fmaf(rx[u], sx, base)));
+        v[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, static_cast<int>(off), 0, 0));
+      }
+#pragma unroll
+      for (int u = 0; u < kRt4Tw; ++u) sum[u] = __fadd_rn(sum[u], v[u]);
+    }
+  }
+  unsigned long long key = 0;
+#pragma unroll
+  for (int u = 0; u < kRt4Tw; ++u) {
+    const int t = t0 + u;
+    if (ri < 0 || t >= num_trans) continue;
+    float score = __fdiv_rn(sum[u], static_cast<float>(n));
+    const double e = static_cast<double>(tr[u].w) * wt + static_cast<double>(rot_angle[ri]) * wr;
+    score = static_cast<float>(static_cast<double>(score) * exp(-(e * e)));
+    const unsigned idx = static_cast<unsigned>(t) * static_cast<unsigned>(num_rot) + ri;
+    const unsigned long long k =
+        (static_cast<unsigned long long>(__float_as_uint(score)) << 32) | (0xffffffffu - idx);
+    key = k > key ? k : key;
+    if (scores) scores[static_cast<int64_t>(ri) * scores_pitch + t] = score;
+  }
+  if (scores) return;  // uniform: no reduction in the scoring mode
+  for (int m = 32; m > 0; m >>= 1) {
+    const unsigned long long o = __shfl_xor(key, m, 64);
+    key = o > key ? o : key;
+  }
+  if (lane == 0) red[wave] = key;
+  __syncthreads();
+  if (tid == 0) {
+    unsigned long long k = red[0];
+    for (int w = 1; w < kRt4Waves; ++w) k = red[w] > k ? red[w] : k;
     atomicMax(best, k);
   }
 }
@@ -1612,9 +1742,31 @@ hipError_t LaunchRt3dScore(int num_rot, hipStream_t st, const float* prob, const
 }
 
 hipError_t LaunchPadProbBrick(const float* prob, const Brick3& gb, float* out, hipStream_t st) {
-  const int64_t total = static_cast<int64_t>(gb.nx + 2) * (gb.ny + 2) * (gb.nz + 2);
+  return LaunchPadProbBrickP(prob, gb, 1, out, st);
+}
+
+hipError_t LaunchPadProbBrickP(const float* prob, const Brick3& gb, int P, float* out,
+                               hipStream_t st) {
+  const int64_t total =
+      static_cast<int64_t>(gb.nx + 2 * P) * (gb.ny + 2 * P) * (gb.nz + 2 * P);
   hipLaunchKernelGGL(pad_prob_brick, dim3(static_cast<unsigned>((total + 255) / 256)), dim3(256), 0,
-                     st, prob, gb, out);
+                     st, prob, gb, P, out);
+  return hipGetLastError();
+}
+
+hipError_t LaunchRt3dScore4(int num_blocks, hipStream_t st, const float* pad, const Brick3& gb,
+                            int P, float res, float eps, float4 safe_lo, float4 safe_hi,
+                            const float* points, int n, const float4* rot, const int* rot_index,
+                            const float* rot_angle, const float4* trans, int num_trans,
+                            int num_rot, double wt, double wr, unsigned long long* best,
+                            float* scores, int scores_pitch) {
+  const int per = kRt4Waves * kRt4Tw;
+  hipLaunchKernelGGL(rt3d_score4, dim3(num_blocks, (num_trans + per - 1) / per), dim3(64 * kRt4Waves),
+                     0, st, pad, gb.nx + 2 * P, gb.ny + 2 * P, gb.nz + 2 * P,
+                     static_cast<float>(P - gb.ox), static_cast<float>(P - gb.oy),
+                     static_cast<float>(P - gb.oz), res, 1.f / res, eps, safe_lo, safe_hi, points, n,
+                     rot, rot_index, rot_angle, trans, num_trans, num_rot, wt, wr, best, scores,
+                     scores_pitch);
   return hipGetLastError();
 }
 
