@@ -95,7 +95,7 @@ struct csm_context {
   double level_batches[csm::kMaxLevels] = {0};
   int num_cus = 256;
   // 3D path scratch (host3d.cc).
-  csm::DevBuf rt3_rot, rt3_rot4, rt3_trans, rt3_points, rt3_best, f3_pairs, f3_yaws, f3_points,
+  csm::DevBuf rt3_rot, rt3_rot4, rt3_cols, rt3_trans, rt3_points, rt3_best, f3_pairs, f3_yaws, f3_points,
       f3_low_points, f3_best, f3_status, f3_counter, f3_items, f3_scores, f3_spill;
   csm::PinnedBuf f3_host_yaws, f3_host_points;
   // Side stream for the 3D batch's cloud upload (overlaps the rotational
@@ -142,6 +142,8 @@ struct csm_hybrid_grid {
   bool prob_pad_ready = false;
   csm::DevBuf prob_wide;  // padded by prob_wide_pad 0.1 cells per side (rt3d_score4)
   int prob_wide_pad = 0;
+  csm::DevBuf prob_col;   // padded by prob_col_pad cells, z fastest (rt3d_score5)
+  int prob_col_pad = 0;
 };
 
 #endif  // CSM_INTERNAL_H_

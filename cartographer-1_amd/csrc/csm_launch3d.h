@@ -51,6 +51,19 @@ hipError_t LaunchRt3dScore4(int num_blocks, hipStream_t st, const float* pad, co
                             const float* rot_angle, const float4* trans, int num_trans,
                             int num_rot, double wt, double wr, unsigned long long* best,
                             float* scores, int scores_pitch);
+// rt3d_score5: v4's rotation blocks, one wave per (x, y) column of the
+// translation lattice (nl = 2L + 1 in {3, 5, 7} z steps), over the brick
+// padded by P and stored z fastest (LaunchPadProbBrickZ). col_t0[c] = the
+// scaled translation of step 0 of column c, col_thr[c] = per-axis rounding
+// thresholds of the column test.
+hipError_t LaunchPadProbBrickZ(const float* prob, const Brick3& gb, int P, float* out,
+                               hipStream_t st);
+hipError_t LaunchRt3dScore5(int nl, int num_blocks, hipStream_t st, const float* col,
+                            const Brick3& gb, int P, float res, float eps, float4 safe_lo,
+                            float4 safe_hi, const float* points, int n, const float4* rot,
+                            const int* rot_index, const float* rot_angle, const float4* trans,
+                            const float4* col_t0, const float4* col_thr, int num_rot, double wt,
+                            double wr, unsigned long long* best, float* scores, int scores_pitch);
 // Items [item_begin, item_begin + num_items) of the yaw list; `large`
 // selects the build for clouds of more than kSmall3dPoints points.
 hipError_t LaunchFast3dSearch(bool large, int grid, hipStream_t st, const Submap3Desc* submaps,

@@ -437,6 +437,63 @@ int RunRt3d(csm_context* ctx, const csm_rt_options* o, const csm_hybrid_grid* gr
                            st));
     CSM_HIP(hipMemcpyAsync(didx, bidx.data(), sizeof(int32_t) * bidx.size(), hipMemcpyHostToDevice,
                            st));
+    // v5 (column gathers) for 3-, 5- and 7-step z columns.
+    const int nl = static_cast<int>(w.nl);
+    const bool v5 = !std::getenv("CSM_RT3D_V4") && (nl == 3 || nl == 5 || nl == 7);
+    if (v5) {
+      csm_hybrid_grid* g = const_cast<csm_hybrid_grid*>(grid);
+      if (g->prob_col_pad != P) {
+        if ((rc = g->prob_col.Reserve(sizeof(float) * (gb.nx + 2 * P) * (gb.ny + 2 * P) *
+                                      (gb.nz + 2 * P))))
+          return rc;
+        CSM_HIP(LaunchPadProbBrickZ(grid->prob.as<float>(), gb, P, g->prob_col.as<float>(), st));
+        g->prob_col_pad = P;
+      }
+      // Per column: step 0's scaled translation and the per-axis thresholds
+      // half - drift - allowance (drift: the largest |t'(k) - t'(0) - k e_z|;
+      // allowance: the two float adds' rounding, 2^-22 (|a'| + |t'| + 1)).
+      float amax = 0.f, tmaxs = 0.f;
+      for (int i = 0; i < n; ++i)
+        amax = std::max(amax, NormV(V3{xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2]}));
+      for (int64_t t = 0; t < num_trans; ++t)
+        tmaxs = std::max({tmaxs, std::fabs(w.trans[t].x * inv), std::fabs(w.trans[t].y * inv),
+                          std::fabs(w.trans[t].z * inv)});
+      const float allow = static_cast<float>(
+          std::ldexp(1.0, -22) * (static_cast<double>(amax) * 1.001 / res + tmaxs + 1.0));
+      const float half = 0.5f - eps;
+      const int cols = nl * nl;
+      std::vector<float4> ct0(static_cast<size_t>(cols)), cth(static_cast<size_t>(cols));
+      for (int c = 0; c < cols; ++c) {
+        const float4 T0 = w.trans[c];
+        const float b0[3] = {T0.x * inv, T0.y * inv, T0.z * inv};
+        float dev[3] = {0.f, 0.f, 0.f};
+        for (int k = 1; k < nl; ++k) {
+          const float4 T = w.trans[static_cast<int64_t>(k) * cols + c];
+          const float bk[3] = {T.x * inv, T.y * inv, T.z * inv};
+          dev[0] = std::max(dev[0], std::fabs(bk[0] - b0[0]));
+          dev[1] = std::max(dev[1], std::fabs(bk[1] - b0[1]));
+          dev[2] = std::max(dev[2], std::fabs(static_cast<float>(
+                                        static_cast<double>(bk[2]) - b0[2] - k)));
+        }
+        ct0[c] = make_float4(b0[0], b0[1], b0[2], 0.f);
+        cth[c] = make_float4(half - dev[0] - allow, half - dev[1] - allow, half - dev[2] - allow,
+                             0.f);
+      }
+      if ((rc = ctx->rt3_cols.Reserve(sizeof(float4) * 2 * cols))) return rc;
+      float4* dct0 = ctx->rt3_cols.as<float4>();
+      CSM_HIP(hipMemcpyAsync(dct0, ct0.data(), sizeof(float4) * cols, hipMemcpyHostToDevice, st));
+      CSM_HIP(hipMemcpyAsync(dct0 + cols, cth.data(), sizeof(float4) * cols, hipMemcpyHostToDevice,
+                             st));
+      if (ctx->timing) CSM_HIP(hipEventRecord(ctx->ev0, st));
+      CSM_HIP(LaunchRt3dScore5(nl, static_cast<int>(brot.size() / 64), st, grid->prob_col.as<float>(),
+                               gb, P, res, eps, make_float4(lo[0], lo[1], lo[2], 0.f),
+                               make_float4(hi[0], hi[1], hi[2], 0.f), ctx->rt3_points.as<float>(),
+                               n, drot4, didx, dangle, ctx->rt3_trans.as<float4>(), dct0,
+                               dct0 + cols, static_cast<int>(num_rot),
+                               o->translation_delta_cost_weight, o->rotation_delta_cost_weight,
+                               ctx->rt3_best.as<unsigned long long>(), dscores,
+                               static_cast<int>(num_trans)));
+    } else {
     if (ctx->timing) CSM_HIP(hipEventRecord(ctx->ev0, st));
     CSM_HIP(LaunchRt3dScore4(static_cast<int>(brot.size() / 64), st, grid->prob_wide.as<float>(), gb,
                              P, res, eps, make_float4(lo[0], lo[1], lo[2], 0.f),
@@ -446,6 +503,7 @@ int RunRt3d(csm_context* ctx, const csm_rt_options* o, const csm_hybrid_grid* gr
                              o->translation_delta_cost_weight, o->rotation_delta_cost_weight,
                              ctx->rt3_best.as<unsigned long long>(), dscores,
                              static_cast<int>(num_trans)));
+    }
   } else if (ctx->timing) {
     CSM_HIP(hipEventRecord(ctx->ev0, st));
   }

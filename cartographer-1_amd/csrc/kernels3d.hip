@@ -602,6 +602,153 @@ rt3d_score4(const float* __restrict__ pad, int pnx, int pny, int pnz, float bx, 
   }
 }
 
+// RTCSM3D, v5 (column gathers): as v4 — lanes on a 4 x 4 x 4 block of
+// rotations — but each wave takes one (x, y) column of the translation
+// lattice with all NL of its z steps, over a padded brick stored z-fastest.
+// The kernels above are bound by the texture address path (TA/TD 91-99%
+// busy at ~23-26 cycles per 64-lane dword gather, profiles/r2d/pmc_rt3d):
+// the per-instruction cost, not bytes or lines. Along a z column the cell of
+// step k is the cell of step 0 plus k in z whenever the rounding of step 0
+// clears the column's drift (host: per column and axis, the largest
+// |t'(k) - t'(0) - k e_z| plus a rounding allowance), so one lane fetches its
+// NL cells with one or two 16-byte loads and adds them to NL sums in point
+// order. A lookup that fails the column test (or a point outside the safe
+// box) takes v3's per-step path: fast rounding or the IEEE quotient, clamp.
+template <int NL>
+__global__ void __launch_bounds__(64 * NL)
+rt3d_score5(const float* __restrict__ col, int pnx, int pny, int pnz, float bx, float by, float bz,
+            float res, float inv, float eps, float4 safe_lo, float4 safe_hi,
+            const float* __restrict__ points, int n, const float4* __restrict__ rot,
+            const int* __restrict__ rot_index, const float* __restrict__ rot_angle,
+            const float4* __restrict__ trans, const float4* __restrict__ col_t0,
+            const float4* __restrict__ col_thr, int num_rot, double wt, double wr,
+            unsigned long long* __restrict__ best, float* __restrict__ scores, int scores_pitch) {
+  __shared__ float4 rp[kRt4Tile][64];
+  __shared__ unsigned long long red[NL];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int slot = blockIdx.x * 64 + lane;
+  const int ri = rot_index[slot];
+  const float4 q = rot[slot];
+  const int c = blockIdx.y * NL + wave;  // column (y, x) of the lattice
+  constexpr int kCols = NL * NL;
+  const float4 t0 = col_t0[c], th = col_thr[c];
+  const float lx = -bx, ly = -by, lz = -bz;
+  const float hx = static_cast<float>(pnx - 1) - bx, hy = static_cast<float>(pny - 1) - by,
+              hz = static_cast<float>(pnz - 1) - bz;
+  // z-fastest: byte offset 4 * (((x + bx) * pny + (y + by)) * pnz + (z + bz)).
+  const float sx = 4.f * static_cast<float>(pny) * static_cast<float>(pnz),
+              sy = 4.f * static_cast<float>(pnz), sz = 4.f;
+  const float base = 4.f * ((bx * static_cast<float>(pny) + by) * static_cast<float>(pnz) + bz);
+  const float half = 0.5f - eps;
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(col), 0, static_cast<int>(4u * pnx * pny * pnz), 0x00020000);
+  float sum[NL];
+#pragma unroll
+  for (int k = 0; k < NL; ++k) sum[k] = 0.f;
+  for (int tb = 0; tb < n; tb += kRt4Tile) {
+    const int cnt = min(kRt4Tile, n - tb);
+    __syncthreads();
+    for (int j = wave; j < cnt; j += NL) {
+      const float* p = points + 3 * static_cast<int64_t>(tb + j);
+      float ax, ay, az;
+      Rotate3(q.w, q.x, q.y, q.z, p[0], p[1], p[2], &ax, &ay, &az);
+      const float sxv = __fmul_rn(ax, inv), syv = __fmul_rn(ay, inv), szv = __fmul_rn(az, inv);
+      const bool inside = sxv >= safe_lo.x && sxv <= safe_hi.x && syv >= safe_lo.y &&
+                          syv <= safe_hi.y && szv >= safe_lo.z && szv <= safe_hi.z;
+      rp[j][lane] = make_float4(sxv, syv, szv, inside ? 0.f : 1.f);
+    }
+    __syncthreads();
+    for (int i = 0; i < cnt; ++i) {
+      const float4 a = rp[i][lane];
+      const float yx = __fadd_rn(a.x, t0.x), yy = __fadd_rn(a.y, t0.y), yz = __fadd_rn(a.z, t0.z);
+      const float rx = rintf(yx), ry = rintf(yy), rz = rintf(yz);
+      // Column test: every step's rounding is step 0's (+k in z), clear of the band.
+      const float m = fmaxf(fmaxf(__fsub_rn(fabsf(__fsub_rn(yx, rx)), th.x),
+                                  __fsub_rn(fabsf(__fsub_rn(yy, ry)), th.y)),
+                            fmaxf(__fsub_rn(fabsf(__fsub_rn(yz, rz)), th.z), __fsub_rn(a.w, 0.5f)));
+      float v[NL];
+      if (m < 0.f) {
+        const float off = fmaf(rz, sz, fmaf(ry, sy, fmaf(rx, sx, base)));  // exact (< 2^24)
+        const int o = static_cast<int>(off);
+        const auto lo4 = __builtin_amdgcn_raw_buffer_load_b128(rsrc, o, 0, 0);
+#pragma unroll
+        for (int k = 0; k < NL && k < 4; ++k) v[k] = __uint_as_float(lo4[k]);
+        if constexpr (NL > 4) {
+          const auto hi4 = __builtin_amdgcn_raw_buffer_load_b128(rsrc, o + 16, 0, 0);
+#pragma unroll
+          for (int k = 4; k < NL; ++k) v[k] = __uint_as_float(hi4[k - 4]);
+        }
+      } else {  // rare: v3's per-step path
+        const float* p = points + 3 * static_cast<int64_t>(tb + i);
+        float ax, ay, az;
+        Rotate3(q.w, q.x, q.y, q.z, p[0], p[1], p[2], &ax, &ay, &az);
+#pragma unroll
+        for (int k = 0; k < NL; ++k) {
+          const float4 tr = trans[k * kCols + c];
+          const float tx = __fmul_rn(tr.x, inv), ty = __fmul_rn(tr.y, inv), tz = __fmul_rn(tr.z, inv);
+          const float ux = __fadd_rn(a.x, tx), uy = __fadd_rn(a.y, ty), uz = __fadd_rn(a.z, tz);
+          float ox = rintf(ux), oy = rintf(uy), oz = rintf(uz);
+          const float dm = fmaxf(fmaxf(fabsf(__fsub_rn(ux, ox)), fabsf(__fsub_rn(uy, oy))),
+                                 fabsf(__fsub_rn(uz, oz)));
+          if (dm >= half) {
+            ox = static_cast<float>(RoundDiv(__fadd_rn(ax, tr.x), res, inv));
+            oy = static_cast<float>(RoundDiv(__fadd_rn(ay, tr.y), res, inv));
+            oz = static_cast<float>(RoundDiv(__fadd_rn(az, tr.z), res, inv));
+          }
+          ox = __builtin_amdgcn_fmed3f(ox, lx, hx);
+          oy = __builtin_amdgcn_fmed3f(oy, ly, hy);
+          oz = __builtin_amdgcn_fmed3f(oz, lz, hz);
+          const float off = fmaf(oz, sz, fmaf(oy, sy, fmaf(ox, sx, base)));
+          v[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, static_cast<int>(off), 0, 0));
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < NL; ++k) sum[k] = __fadd_rn(sum[k], v[k]);
+    }
+  }
+  unsigned long long key = 0;
+#pragma unroll
+  for (int k = 0; k < NL; ++k) {
+    const int t = k * kCols + c;
+    if (ri < 0) continue;
+    float score = __fdiv_rn(sum[k], static_cast<float>(n));
+    const double e = static_cast<double>(trans[t].w) * wt + static_cast<double>(rot_angle[ri]) * wr;
+    score = static_cast<float>(static_cast<double>(score) * exp(-(e * e)));
+    const unsigned idx = static_cast<unsigned>(t) * static_cast<unsigned>(num_rot) + ri;
+    const unsigned long long kk =
+        (static_cast<unsigned long long>(__float_as_uint(score)) << 32) | (0xffffffffu - idx);
+    key = kk > key ? kk : key;
+    if (scores) scores[static_cast<int64_t>(ri) * scores_pitch + t] = score;
+  }
+  if (scores) return;  // uniform: no reduction in the scoring mode
+  for (int mm = 32; mm > 0; mm >>= 1) {
+    const unsigned long long o = __shfl_xor(key, mm, 64);
+    key = o > key ? o : key;
+  }
+  if (lane == 0) red[wave] = key;
+  __syncthreads();
+  if (tid == 0) {
+    unsigned long long k = red[0];
+    for (int w = 1; w < NL; ++w) k = red[w] > k ? red[w] : k;
+    atomicMax(best, k);
+  }
+}
+
+// The brick padded by P cells of 0.1 per side, z fastest (rt3d_score5).
+__global__ void pad_prob_brick_zfast(const float* __restrict__ prob, Brick3 gb, int P,
+                                     float* __restrict__ out) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const int px = gb.nx + 2 * P, py = gb.ny + 2 * P, pz = gb.nz + 2 * P;
+  if (i >= static_cast<int64_t>(px) * py * pz) return;
+  const int z = static_cast<int>(i % pz) - P;
+  const int y = static_cast<int>((i / pz) % py) - P;
+  const int x = static_cast<int>(i / (static_cast<int64_t>(pz) * py)) - P;
+  float v = 0.1f;
+  if (x >= 0 && x < gb.nx && y >= 0 && y < gb.ny && z >= 0 && z < gb.nz)
+    v = prob[(static_cast<int64_t>(z) * gb.ny + y) * gb.nx + x];
+  out[i] = v;
+}
+
 // ------------------------------------------------------------ FastCSM3D ----
 //
 // Persistent workgroups pull (pair, yaw) items from a global counter. Per
@@ -1751,6 +1898,39 @@ hipError_t LaunchPadProbBrickP(const float* prob, const Brick3& gb, int P, float
       static_cast<int64_t>(gb.nx + 2 * P) * (gb.ny + 2 * P) * (gb.nz + 2 * P);
   hipLaunchKernelGGL(pad_prob_brick, dim3(static_cast<unsigned>((total + 255) / 256)), dim3(256), 0,
                      st, prob, gb, P, out);
+  return hipGetLastError();
+}
+
+hipError_t LaunchPadProbBrickZ(const float* prob, const Brick3& gb, int P, float* out,
+                               hipStream_t st) {
+  const int64_t total =
+      static_cast<int64_t>(gb.nx + 2 * P) * (gb.ny + 2 * P) * (gb.nz + 2 * P);
+  hipLaunchKernelGGL(pad_prob_brick_zfast, dim3(static_cast<unsigned>((total + 255) / 256)), dim3(256),
+                     0, st, prob, gb, P, out);
+  return hipGetLastError();
+}
+
+hipError_t LaunchRt3dScore5(int nl, int num_blocks, hipStream_t st, const float* col,
+                            const Brick3& gb, int P, float res, float eps, float4 safe_lo,
+                            float4 safe_hi, const float* points, int n, const float4* rot,
+                            const int* rot_index, const float* rot_angle, const float4* trans,
+                            const float4* col_t0, const float4* col_thr, int num_rot, double wt,
+                            double wr, unsigned long long* best, float* scores, int scores_pitch) {
+  const float fbx = static_cast<float>(P - gb.ox), fby = static_cast<float>(P - gb.oy),
+              fbz = static_cast<float>(P - gb.oz);
+  const int px = gb.nx + 2 * P, py = gb.ny + 2 * P, pz = gb.nz + 2 * P;
+#define CSM_RT5(NLV)                                                                              \
+  hipLaunchKernelGGL(rt3d_score5<NLV>, dim3(num_blocks, NLV), dim3(64 * NLV), 0, st, col, px, py, \
+                     pz, fbx, fby, fbz, res, 1.f / res, eps, safe_lo, safe_hi, points, n, rot,    \
+                     rot_index, rot_angle, trans, col_t0, col_thr, num_rot, wt, wr, best, scores, \
+                     scores_pitch)
+  switch (nl) {
+    case 3: CSM_RT5(3); break;
+    case 5: CSM_RT5(5); break;
+    case 7: CSM_RT5(7); break;
+    default: return hipErrorInvalidValue;
+  }
+#undef CSM_RT5
   return hipGetLastError();
 }
 
