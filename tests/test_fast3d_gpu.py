@@ -247,6 +247,29 @@ def test_rt3d_dense_scene(csm, oracle):
         assert pose == ref_pose
 
 
+@pytest.mark.parametrize("window", [0.1, 0.2, 0.3])
+def test_rt3d_column_kernel_tilted_initial(csm, oracle, window):
+    """The column-gather kernel (rt3d_score5, 3-, 5- and 7-step z columns)
+    under an initial pose with roll and pitch: the translation lattice's z
+    columns drift in x and y, so many lookups fail the column test and take
+    the per-step exact path. Same score and pose as the oracle."""
+    rng = np.random.default_rng(11)
+    cloud = rng.uniform(-4, 4, (400, 3)).astype(np.float32) * np.float32([1, 1, 0.4])
+    og = oracle.hybrid_grid(0.1)
+    og.insert((0, 0, 0), cloud, 0.7, 0.4, 5)
+    opts = (window, math.radians(1.5), 0.1, 0.1)
+    g = gpu_grid(csm, og)
+    m = csm.RealTimeCorrelativeScanMatcher3D(csm.RealTimeCorrelativeScanMatcherOptions(*opts))
+    roll, pitch = math.radians(8.0), math.radians(-5.0)
+    q = (math.cos(roll / 2) * math.cos(pitch / 2), math.sin(roll / 2) * math.cos(pitch / 2),
+         math.cos(roll / 2) * math.sin(pitch / 2), -math.sin(roll / 2) * math.sin(pitch / 2))
+    for initial in [((0.04, -0.02, 0.03), q), ((0.0, 0.0, 0.0), quat_z(0.2))]:
+        score, pose = m.Match(initial, cloud, g)
+        ref_score, ref_pose, idx, n = oracle.rt3d_match(og, opts, initial, cloud)
+        assert math.isclose(score, ref_score, rel_tol=1e-6), (score, ref_score)
+        assert pose == ref_pose
+
+
 # ------------------------------------------------- synthetic world (C5 shape) --
 @pytest.fixture(scope="module")
 def world3d(csm):
