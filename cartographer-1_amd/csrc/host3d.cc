@@ -1301,10 +1301,28 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
     CSM_HIP(hipMemcpyAsync(&nflag, dflag_count, sizeof(unsigned), hipMemcpyDeviceToHost, st));
     CSM_HIP(hipMemcpyAsync(flags, dflags, sizeof(flags), hipMemcpyDeviceToHost, st));
     CSM_HIP(hipStreamSynchronize(st));
+    // CSM_YAW_HOST_BUILD (tests): the host path for every yaw.
+    if (nflag > static_cast<unsigned>(kYawFlagCap) || std::getenv("CSM_YAW_HOST_BUILD")) {
+      // More undecided roundings than the flag list holds (~2^-15 per value,
+      // so only in batches of ~10^8 yaws): rebuild every yaw on the host.
+      std::vector<int32_t> hk(std::max(kept, 1u));
+      std::vector<float> hs(std::max(kept, 1u));
+      CSM_HIP(hipMemcpyAsync(hk.data(), dev_k, sizeof(int32_t) * kept, hipMemcpyDeviceToHost, st));
+      CSM_HIP(hipMemcpyAsync(hs.data(), dev_s, sizeof(float) * kept, hipMemcpyDeviceToHost, st));
+      CSM_HIP(hipStreamSynchronize(st));
+      if ((rc = ctx->f3_host_yaws.Reserve(sizeof(Yaw3Desc) * ny))) return rc;
+      Yaw3Desc* hy = ctx->f3_host_yaws.as<Yaw3Desc>();
+      ParallelPairs(np, [&](int64_t dp) {
+        const int64_t i = pair_of[dp];
+        BuildYaws(hk.data() + yaw_src[i], hs.data() + yaw_src[i], prep[i].num_yaws,
+                  static_cast<int32_t>(dp), prep[i], hy + pdesc[dp].yaw_begin);
+      });
+      CSM_HIP(hipMemcpyAsync(ctx->f3_yaws.ptr, hy, sizeof(Yaw3Desc) * ny, hipMemcpyHostToDevice, st));
+      nflag = 0;
+    }
     if (nflag > 0) {
       std::vector<YawFlag3> all(flags, flags + std::min<unsigned>(nflag, 64));
       if (nflag > 64) {
-        if (nflag > static_cast<unsigned>(kYawFlagCap)) return CSM_ERANGE;  // never seen: ~2^-16 per yaw
         all.resize(nflag);
         CSM_HIP(hipMemcpy(all.data(), dflags, sizeof(YawFlag3) * nflag, hipMemcpyDeviceToHost));
       }

@@ -238,7 +238,13 @@ def test_oracle_reproduces_rt3d_golden(oracle):
 
 
 @pytest.mark.gpu
-def test_gpu_matches_fast3d_golden(csm, oracle):
+@pytest.mark.parametrize("yaw_build", ["device", "host"])
+def test_gpu_matches_fast3d_golden(csm, oracle, yaw_build, monkeypatch):
+    """Both discrete-scan pose paths: built on the device (yaw_build, libm
+    fix-ups for undecided roundings) and the host path that a flag-list
+    overflow falls back to (CSM_YAW_HOST_BUILD forces it)."""
+    if yaw_build == "host":
+        monkeypatch.setenv("CSM_YAW_HOST_BUILD", "1")
     from test_fast3d_gpu import assert_same_result
     d = _load("fast3d_c5.npz")
     o = csm.FastCorrelativeScanMatcherOptions3D(*[int(v) if i < 2 else float(v)
