@@ -1077,12 +1077,16 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
   }
   float* const hstage = ctx->f3_host_points.as<float>();
   float* const lstage = hstage + 3 * nh;
+  // Per node, in one pass: its clouds into the pinned staging and its
+  // high-resolution cloud's largest norm (phase 1 below).
+  std::vector<float> max_norm(num_nodes, 0.f);
   ParallelPairs(static_cast<int64_t>(used_nodes.size()), [&](int64_t j) {
     const csm_node3d& nd = nodes[used_nodes[j]];
     std::memcpy(hstage + 3 * hoff[used_nodes[j]], nd.high_resolution_xyz,
                 sizeof(float) * 3 * nd.num_high_resolution);
     std::memcpy(lstage + 3 * loff[used_nodes[j]], nd.low_resolution_xyz,
                 sizeof(float) * 3 * nd.num_low_resolution);
+    max_norm[used_nodes[j]] = MaxNorm(nd);
   });
   if (nh > 0)
     CSM_HIP(hipMemcpyAsync(ctx->f3_points.ptr, hstage, sizeof(float) * 3 * nh, hipMemcpyHostToDevice,
@@ -1094,10 +1098,6 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
   lap(0);
   // Phase 1 (host, parallel): per-node cloud extents, then search windows,
   // angular steps, initial yaws per pair.
-  std::vector<float> max_norm(num_nodes, 0.f);
-  ParallelPairs(static_cast<int64_t>(used_nodes.size()), [&](int64_t j) {
-    max_norm[used_nodes[j]] = MaxNorm(nodes[used_nodes[j]]);
-  });
   std::vector<PairPrep> prep(static_cast<size_t>(num_pairs));
   ParallelPairs(num_pairs, [&](int64_t i) {
     if (results[i].status != CSM_NO_MATCH) return;
