@@ -3,17 +3,21 @@
 Metric (BASELINE.json): loop-closure constraint candidates/sec (node x submap
 pairs) + ms/scan-match, 2D 5 cm grid.
 
-Workload per rank (BASELINE config C2): 500 synthetic 1080-beam scans x 50
-submaps (400x400 @ 5 cm), FastCorrelativeScanMatcher2D::MatchFullSubmap,
-branch_and_bound_depth 7, min_score 0.55 = 25,000 pairs per step. With N
-GPUs the world has 50*N submaps and rank r owns submaps [50r, 50r+50): the
-constraint queue is sharded by submap with no data-path collective (weak
-scaling); accepted constraints are gathered to rank 0 over RCCL each step
-(the hand-off to the CPU pose-graph solve), ordered by submission index.
+Headline workload (default, BASELINE config C3 = the north-star queue):
+ConstraintBuilder2D's global loop-closure sweep, 2000 synthetic 1080-beam
+nodes x 1000 submaps (400x400 @ 5 cm), FastCorrelativeScanMatcher2D::
+MatchFullSubmap, branch_and_bound_depth 7, min_score 0.55: one fixed queue of
+2 M pairs. A step is one twentieth of it (50 submaps x 2000 nodes = 100,000
+pairs), so `--steps 20` covers the whole queue once. Inside the timed region
+the ranks claim chunks of submaps from the queue dynamically (csm_comm's
+rank-0 counter table, the reference's shared ThreadPool queue), build each
+chunk's pyramids on their GPU, search it as one batch, and finally gather
+the accepted constraints to rank 0 in submission order (RCCL). Node clouds
+are resident in HBM before timing; submap pyramids are built inside it.
 
-A step = one pass of the search over the rank's 25,000 pairs, inputs resident
-in HBM (pyramids and clouds uploaded before timing). The secondary number is
-RealTimeCorrelativeScanMatcher2D::Match ms/scan-match at config C1.
+Secondary lines (rank 0, one GPU): C2 (500 x 50), C1 RTCSM2D ms/scan-match,
+the drop-in's call patterns, voxel filter, Ceres refinement, C4 RTCSM3D and
+C5 FastCSM3D (500 nodes x 200 submaps, split over the ranks).
 
 Prints ONE JSON line on rank 0.
 """
@@ -42,8 +46,12 @@ def load_pkg():
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=2)
-    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--workload", default="c3", choices=["c2", "c3"],
+                   help="c3 (default): the fixed 2000-node x 1000-submap queue, a step = one "
+                        "--c3-slice of it, claimed dynamically over the ranks; c2: 500 x 50 "
+                        "submaps per GPU (weak scaling)")
     p.add_argument("--nodes", type=int, default=500)
     p.add_argument("--submaps-per-rank", type=int, default=50)
     p.add_argument("--min-score", type=float, default=0.55)
@@ -51,21 +59,20 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=20.0)
     p.add_argument("--cpu-threads", type=int, default=0)
     p.add_argument("--no-cpu", action="store_true")
-    p.add_argument("--no-rt", action="store_true")
+    p.add_argument("--no-rt", action="store_true", help="skip the secondary 2D legs")
     p.add_argument("--seed", type=int, default=20250127)
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
     p.add_argument("--no-3d", action="store_true")
     p.add_argument("--nodes3d", type=int, default=500)
-    p.add_argument("--submaps3d", type=int, default=25, help="3D submaps per GPU (C5: 200 / 8)")
+    p.add_argument("--submaps3d", type=int, default=200,
+                   help="C5 submaps in total, split over the ranks")
     p.add_argument("--steps3d", type=int, default=3)
-    p.add_argument("--workload", default="c2", choices=["c2", "c3"],
-                   help="c2: 500 x 50 submaps per GPU (weak scaling, default); c3: the fixed "
-                        "2000-node x 1000-submap queue split over the ranks (strong scaling)")
     p.add_argument("--c3-nodes", type=int, default=2000)
     p.add_argument("--c3-submaps", type=int, default=1000)
-    p.add_argument("--c3-chunk", type=int, default=8, help="submaps per claimed chunk")
+    p.add_argument("--c3-slice", type=int, default=50, help="submaps of the queue per step")
+    p.add_argument("--c3-chunk", type=int, default=4, help="submaps per claimed chunk")
     p.add_argument("--cpu-pairs", type=int, default=0,
-                   help="CPU baseline sample size (0: sized to --cpu-seconds)")
+                   help="CPU baseline sample size (0: 2000 for C3, sized to --cpu-seconds for C2)")
     return p.parse_args()
 
 
@@ -76,6 +83,7 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     device = local_rank
+    coll_dev = None
     if world_size > 1:
         import torch
         import torch.distributed as tdist
@@ -85,19 +93,74 @@ def main():
         torch.cuda.set_device(device)
         tdist.init_process_group(args.dist_backend)
         dist = tdist
+        coll_dev = torch.device("cuda", device) if args.dist_backend == "nccl" else None
 
     csm = load_pkg()
     ctx = csm.Context(device)
-    if args.workload == "c3":
-        return c3_main(csm, ctx, args, rank, world_size, dist)
+    comm, transport = make_comm_checked(csm, ctx, args, rank, world_size, dist, coll_dev)
+    cdist = importlib.import_module("cartographer_amd.distributed")
+    if comm is not None:
+        def gather(rec):
+            return cdist.gather_records_comm(rec, comm)
+    else:
+        def gather(rec):
+            return cdist.gather_records(rec)
 
-    # ---- synthetic world (identical on every rank) -------------------------
+    def barrier_sync():
+        if dist is not None:
+            dist.barrier()
+            import torch
+            torch.cuda.synchronize()
+
+    if args.workload == "c3":
+        out, errors = c3_run(csm, ctx, args, rank, world_size, dist, coll_dev, comm, gather,
+                             transport, barrier_sync)
+    else:
+        out, errors = c2_run(csm, ctx, args, rank, world_size, dist, coll_dev, gather, transport,
+                             barrier_sync, headline=True)
+    if rank == 0 and world_size == 1 and not args.no_rt:
+        if args.workload == "c3":
+            c2, c2_errors = c2_run(csm, ctx, args, rank, world_size, dist, coll_dev, gather,
+                                   transport, barrier_sync, headline=False)
+            errors += c2_errors
+            out["c2"] = c2
+        out["rt2d"] = rt2d_bench(csm, ctx, args)
+    if rank == 0 and world_size == 1 and not args.no_3d:
+        out["rt3d"] = rt3d_bench(csm, ctx, args)
+    if not args.no_3d:  # collective over ranks: the C5 sweep, submap-sharded
+        f3 = fast3d_bench(csm, ctx, args, rank, world_size, dist, coll_dev, barrier_sync, cdist,
+                          gather)
+        if rank == 0:
+            out["fast3d"] = f3
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+    if comm is not None:
+        comm.close()
+    if dist is not None:
+        dist.destroy_process_group()
+    failed = errors + (out.get("fast3d", {}).get("errors_per_step", 0) if rank == 0 else 0)
+    if failed:
+        print(f"bench: {failed} pair searches returned an error status", file=sys.stderr)
+        sys.exit(3)
+
+
+def c2_run(csm, ctx, args, rank, world_size, dist, coll_dev, gather, transport, barrier_sync,
+           headline):
+    """Config C2: 500 scans x 50 submaps per GPU, submap-sharded (weak
+    scaling). As the headline (--workload c2) it carries the roofline and its
+    CPU baseline; as a secondary line (default run) one step, plus the
+    drop-in's call patterns, the voxel filter and the Ceres refinement on its
+    world. Returns (result dict, pairs with error statuses per step)."""
+    cdist = importlib.import_module("cartographer_amd.distributed")
+    steps = args.steps if headline else 1
+    warmup = args.warmup if headline else 1
     t0 = time.time()
     world = csm.SyntheticWorld2D(num_nodes=args.nodes,
                                  num_submaps=args.submaps_per_rank * world_size,
                                  submap_cells=400, beams=1080, seed=args.seed)
     gen_s = time.time() - t0
-    cdist = importlib.import_module("cartographer_amd.distributed")
     my_submaps = cdist.shard_submaps(world.num_submaps, rank, world_size, args.submaps_per_rank)
     opts = csm.FastCorrelativeScanMatcherOptions2D(7.0, math.radians(30.0), 7, args.search_depth)
     t0 = time.time()
@@ -111,26 +174,13 @@ def main():
     # ConstraintBuilder2D::WhenDone ordering on rank 0 (constraint_builder_2d.cc:285-288).
     submission = (np.int64(rank) * len(pairs) + np.arange(len(pairs), dtype=np.int64))
     n_pairs = len(pairs)
-
-    coll_dev = None
-    if dist is not None:
-        import torch
-        coll_dev = torch.device("cuda", device) if args.dist_backend == "nccl" else None
     sub_global = np.asarray(my_submaps, np.int64)[sub_local]
-
-    gather, gather_transport = make_gather(csm, ctx, args, rank, world_size, dist, coll_dev)
 
     def gather_constraints(res):
         return gather(cdist.make_records(res, submission, sub_global, node_idx))
 
-    def barrier_sync():
-        if dist is not None:
-            dist.barrier()
-            import torch
-            torch.cuda.synchronize()
-
     # ---- warmup + timed steps ------------------------------------------------
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         res = csm.match_batch(matchers, scans, pairs, ctx)
         gather_constraints(res)
     ctx.reset_timing()
@@ -139,7 +189,7 @@ def main():
     t_start = time.perf_counter()
     accepted = 0
     errors = 0  # pairs whose search returned an error status (never counted as work)
-    for _ in range(args.steps):
+    for _ in range(steps):
         res = csm.match_batch(matchers, scans, pairs, ctx)
         errors += int((res["status"] < 0).sum())
         rec = gather_constraints(res)
@@ -152,26 +202,25 @@ def main():
     lv_cands, lv_batches = ctx.level_stats()
     elapsed = cdist.max_over_ranks(elapsed, dist, coll_dev)
     errors = int(cdist.sum_over_ranks(errors, dist, coll_dev))
-    total_pairs = n_pairs * world_size * args.steps
+    total_pairs = n_pairs * world_size * steps
     value = total_pairs / elapsed
 
-    # Roofline of the dominant kernel (fast2d_search): algorithmic bytes per
-    # launch = candidates scored x points x 1 B (uint8 pyramid lookups).
+    # Roofline of the dominant kernel (fast2d_search_v4): issued bytes per
+    # launch (4 B per quad-dword gather) over its HIP-event duration.
     kernel_ms_avg = tm.search_kernel_ms / max(tm.search_launches, 1)
     bytes_per_launch = tm.search_lookups / max(tm.search_launches, 1)
     achieved = bytes_per_launch / (kernel_ms_avg * 1e-3) / 1e9 if kernel_ms_avg > 0 else 0.0
     peak = 8000.0
-
-    traffic = committed_traffic(args, world_size)
+    traffic = committed_traffic(args, world_size) if headline else None
 
     out = {
         "metric": "loop-closure constraint candidates/sec (node x submap pairs) + ms/scan-match, 2D 5cm grid",
         "value": value,
         "unit": "pairs/s",
         "n_gpus": world_size,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": elapsed / args.steps * 1e3,
+        "steps": steps,
+        "warmup": warmup,
+        "ms_per_step": elapsed / steps * 1e3,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -182,50 +231,44 @@ def main():
                                "(400x400 @5cm), branch_and_bound_depth=7, min_score=%.2f" % args.min_score,
                    "pairs_per_step_per_gpu": n_pairs, "search_depth": matchers[0].options.search_depth,
                    "parallelism": f"submap-sharded x{world_size}",
-                   "gather": gather_transport},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
-                     "frac": achieved / peak,
-                     **traffic_fields(traffic, kernel_ms_avg, peak),
-                     "kernel": "fast2d_search", "kernel_ms_avg": kernel_ms_avg,
-                     "algorithmic_bytes_per_launch": bytes_per_launch,
-                     "bytes_definition": "4 B per quad-dword gather the search issues (one "
-                                         "per node x scan entry, 4 children each)",
-                     # SURVEY §8(d)'s figure: candidates scored x N points x 1 B
-                     "candidate_equivalent_bytes_per_launch": tm.search_candidates /
-                     max(tm.search_launches, 1) * float(np.diff(world.offsets).mean())},
+                   "gather": transport},
+        "roofline": roofline_fields(tm, achieved, peak, traffic, kernel_ms_avg, bytes_per_launch,
+                                    tm.search_candidates / max(tm.search_launches, 1) *
+                                    float(np.diff(world.offsets).mean())),
         "accepted_constraints_per_step": accepted,
-        "errors_per_step": errors / args.steps,
+        "errors_per_step": errors / steps,
         "stack_high_water": int(tm.stack_high_water),
-        "search_levels": {"candidates_per_pair": [c / max(n_pairs * args.steps, 1) for c in lv_cands],
+        "search_levels": {"candidates_per_pair": [c / max(n_pairs * steps, 1) for c in lv_cands],
                           "mean_lanes_per_batch": [c / b if b else 0 for c, b in zip(lv_cands, lv_batches)]},
         "setup_s": {"world": gen_s, "pyramids_and_upload": build_s},
     }
-
-    if rank == 0 and world_size == 1 and not args.no_rt:
-        out["rt2d"] = rt2d_bench(csm, ctx, args)
-    if rank == 0 and world_size == 1 and not args.no_cpu:
+    if not headline:
+        for k in ("metric", "higher_is_better", "vs_baseline", "dtype", "data"):
+            out.pop(k)
+    if rank == 0 and world_size == 1 and headline and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(world, my_submaps, args)
     if rank == 0 and world_size == 1 and not args.no_rt:
         out["dropin"] = dropin_bench(csm, ctx, matchers, scans, world, args)
         out["voxel_filter"] = voxel_filter_bench(csm, ctx, world, args)
         out["ceres2d"] = ceres_bench(csm, ctx, world, matchers, scans, pairs, res, my_submaps,
                                      node_idx, sub_local, args)
-    if rank == 0 and world_size == 1 and not args.no_3d:
-        out["rt3d"] = rt3d_bench(csm, ctx, args)
-    if not args.no_3d:  # collective over ranks: the C5 sweep, submap-sharded
-        f3 = fast3d_bench(csm, ctx, args, rank, world_size, dist, coll_dev, barrier_sync, cdist,
-                          gather)
-        if rank == 0:
-            out["fast3d"] = f3
-    if rank == 0:
-        print(json.dumps(out), flush=True)
-    if dist is not None:
-        dist.barrier()
-        dist.destroy_process_group()
-    failed = errors + (out.get("fast3d", {}).get("errors_per_step", 0) if rank == 0 else 0)
-    if failed:
-        print(f"bench: {failed} pair searches returned an error status", file=sys.stderr)
-        sys.exit(3)
+    for m in matchers:
+        m.close()
+    scans.close()
+    return out, errors
+
+
+def roofline_fields(tm, achieved, peak, traffic, kernel_ms_avg, bytes_per_launch,
+                    candidate_bytes):
+    return {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
+            "frac": achieved / peak,
+            **traffic_fields(traffic, kernel_ms_avg, peak),
+            "kernel": "fast2d_search", "kernel_ms_avg": kernel_ms_avg,
+            "algorithmic_bytes_per_launch": bytes_per_launch,
+            "bytes_definition": "4 B per quad-dword gather the search issues (one "
+                                "per node x scan entry, 4 children each)",
+            # SURVEY §8(d)'s figure: candidates scored x N points x 1 B
+            "candidate_equivalent_bytes_per_launch": candidate_bytes}
 
 
 TRAFFIC_FILES = {"c2": os.path.join("profiles", "r2b", "traffic_c2.json"),
@@ -266,27 +309,51 @@ def committed_traffic(args, world_size, workload="c2"):
     return t if same else None
 
 
-def make_gather(csm, ctx, args, rank, world_size, dist, coll_dev):
-    """Rank-0 gather of accepted-constraint records for N > 1: the C-ABI
-    communicator (csm_comm_gather over RCCL; TCP for gloo rehearsals), whose
-    unique id travels through torch.distributed's store. Falls back to the
-    torch.distributed gather if the communicator cannot be created.
-    Returns (gather(rec) -> sorted records on rank 0, transport name)."""
-    cdist = importlib.import_module("cartographer_amd.distributed")
+def make_comm_checked(csm, ctx, args, rank, world_size, dist, coll_dev):
+    """The C-ABI communicator for N > 1 (csm_comm over RCCL; TCP for gloo
+    rehearsals), with its work-claiming table opened. Rank 0 makes the RCCL
+    unique id and hands it out through torch.distributed's store (an error
+    sentinel if it cannot, so peers do not wait out the store's timeout).
+    Every rank reports whether its communicator came up, and the ranks agree
+    (all_reduce MIN) before any of them uses it: if one failed, ALL exit
+    non-zero. There is no fallback transport, so a scaling run either
+    measures the product path or fails visibly.
+    Returns (comm or None at N = 1, transport name)."""
     if dist is None:
-        return (lambda rec: cdist.gather_records(rec)), "local"
+        return None, "local"
+    import torch
+    from torch.distributed import distributed_c10d
+    store = distributed_c10d._get_default_store()
+    backend = "rccl" if args.dist_backend == "nccl" else "tcp"
+    base = int(os.environ.get("MASTER_PORT", "29500"))
+    comm, err = None, None
     try:
-        from torch.distributed import distributed_c10d
-        store = distributed_c10d._get_default_store()
-        backend = "rccl" if args.dist_backend == "nccl" else "tcp"
-        port = int(os.environ.get("MASTER_PORT", "29500")) + 17
-        comm = cdist.make_comm(csm, ctx, rank, world_size, store, backend, port)
-        return (lambda rec: cdist.gather_records_comm(rec, comm)), f"csm_comm_{backend}"
-    except Exception as e:  # noqa: BLE001 - any failure: the torch path still works
-        print(f"bench: csm_comm unavailable ({e}); gathering with torch.distributed",
-              file=sys.stderr)
-        return (lambda rec: cdist.gather_records(rec, dist, rank, world_size, coll_dev)), \
-            "torch.distributed"
+        if backend == "rccl":
+            if rank == 0:
+                try:
+                    uid = csm.Comm.unique_id()
+                except Exception:
+                    store.set("csm_comm_id", b"ERROR")
+                    raise
+                store.set("csm_comm_id", uid)
+            else:
+                uid = bytes(store.get("csm_comm_id"))
+                if uid == b"ERROR":
+                    raise RuntimeError("rank 0 could not make the RCCL unique id")
+            comm = csm.Comm.rccl(ctx, rank, world_size, uid)
+        else:
+            comm = csm.Comm.tcp(rank, world_size, "127.0.0.1", base + 17)
+        comm.claim_open("127.0.0.1", base + 19)
+    except Exception as e:  # noqa: BLE001 - reported below, then every rank exits
+        err = e
+    ok = torch.tensor([0 if err else 1], dtype=torch.int64,
+                      device=coll_dev if coll_dev is not None else torch.device("cpu"))
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    if int(ok.item()) != 1:
+        print(f"bench: rank {rank}: csm_comm ({backend}) not available on every rank"
+              + (f": {err}" if err else ""), file=sys.stderr, flush=True)
+        sys.exit(4)
+    return comm, f"csm_comm_{backend}"
 
 
 def rt2d_bench(csm, ctx, args):
@@ -531,16 +598,18 @@ def rt3d_bench(csm, ctx, args):
 
 def fast3d_bench(csm, ctx, args, rank=0, world_size=1, dist=None, coll_dev=None,
                  barrier_sync=lambda: None, cdist=None, gather=None):
-    """C5: FastCorrelativeScanMatcher3D::MatchFullSubmap over nodes3d nodes x
-    (submaps3d x world_size) submaps, submap-sharded: each rank builds and
-    searches its submaps3d submaps of the same world against every node (the
-    8-GPU sweep of 500 x 200 is 500 x 25 per GPU), pose_graph.lua 3D options,
-    global_localization_min_score 0.6. Accepted constraints are gathered to
-    rank 0 each step; value = all ranks' pairs / the slowest rank's time."""
+    """C5 (BASELINE.json configs[4]): FastCorrelativeScanMatcher3D::MatchFullSubmap
+    over nodes3d nodes x submaps3d submaps (500 x 200) of one world, split by
+    submap over the ranks (strong scaling): rank r builds and searches
+    submaps [r S / N, (r + 1) S / N) against every node, pose_graph.lua 3D
+    options, global_localization_min_score 0.6. Accepted constraints are
+    gathered to rank 0 each step in submission order; value = all pairs / the
+    slowest rank's time."""
     t0 = time.time()
-    w = csm.SyntheticWorld3D(num_nodes=args.nodes3d, num_submaps=args.submaps3d * world_size,
-                             submap_range=(rank * args.submaps3d, args.submaps3d),
-                             seed=args.seed + 5)
+    S3 = args.submaps3d
+    b0, b1 = rank * S3 // world_size, (rank + 1) * S3 // world_size
+    w = csm.SyntheticWorld3D(num_nodes=args.nodes3d, num_submaps=S3,
+                             submap_range=(b0, b1 - b0), seed=args.seed + 5)
     gen = time.time() - t0
     o = csm.FastCorrelativeScanMatcherOptions3D()
     grids = [(csm.HybridGrid(w.high_resolution, *w.high_cells[s], context=ctx),
@@ -554,8 +623,8 @@ def fast3d_bench(csm, ctx, args, rank=0, world_size=1, dist=None, coll_dev=None,
     nod = np.tile(np.arange(w.num_nodes), w.num_submaps)
     rot = np.array([w.node_rotation(n) for n in range(w.num_nodes)])
     pairs = csm.make_pairs_3d(sub, nod, 0.6, True, node_q=rot[nod])
-    submission = np.int64(rank) * len(pairs) + np.arange(len(pairs), dtype=np.int64)
     sub_global = w.submap_ids[sub].astype(np.int64)
+    submission = sub_global * w.num_nodes + nod  # queue order: submap-major
 
     def step():
         res = csm.match_batch_3d(mats, nodes, pairs, ctx)
@@ -581,12 +650,12 @@ def fast3d_bench(csm, ctx, args, rank=0, world_size=1, dist=None, coll_dev=None,
     ctx.enable_timing(False)
     if cdist is not None:
         wall = cdist.max_over_ranks(wall, dist, coll_dev)
-    total = len(pairs) * world_size * reps
-    out = {"config": f"C5: MatchFullSubmap, {w.num_nodes} nodes x {w.num_submaps} submaps per GPU "
-                     f"({w.num_submaps * world_size} total; 0.10/0.45 m grids, ~200-point clouds, "
+    total = w.num_nodes * S3 * reps
+    out = {"config": f"C5: MatchFullSubmap, {w.num_nodes} nodes x {S3} submaps split over "
+                     f"{world_size} GPU(s) (0.10/0.45 m grids, ~200-point clouds, "
                      "120-bucket histograms), branch_and_bound_depth 8, full_resolution_depth 3",
-           "pairs_per_step": len(pairs) * world_size, "steps": reps, "value": total / wall,
-           "unit": "pairs/s", "n_gpus": world_size, "scaling": "weak",
+           "pairs_per_step": w.num_nodes * S3, "steps": reps, "value": total / wall,
+           "unit": "pairs/s", "n_gpus": world_size, "scaling": "strong",
            "accepted_per_step": int(len(rec)) if rec is not None else int((res3["status"] == 0).sum()),
            "ms_per_step": wall / reps * 1e3,
            "errors_per_step": errors3 / reps, "stack_high_water": int(tm.stack_high_water),
@@ -810,42 +879,20 @@ def cpu_pairs_2d(world, pair_sub, pair_node, args, what):
     return summarize_cpu(k, wall, task, threads, cpu, probes, what)
 
 
-class ChunkClaimer:
-    """Dynamic work claiming over the ranks: one atomic counter in the
-    process group's store (rank 0's TCPStore), so a rank that finishes early
-    takes the next chunk — the shared-queue balance of the reference's
-    ThreadPool (thread_pool.cc:80-106) across GPUs. Single process: a local
-    counter."""
-
-    def __init__(self, dist, n_chunks):
-        self.dist, self.n = dist, n_chunks
-        self.store = None
-        self.key = None
-        self.local = 0
-        if dist is not None:
-            from torch.distributed import distributed_c10d
-            self.store = distributed_c10d._get_default_store()
-
-    def reset(self, tag):
-        self.key = f"c3_claim_{tag}"
-        self.local = 0
-
-    def claim(self):
-        if self.store is None:
-            c, self.local = self.local, self.local + 1
-            return c
-        return int(self.store.add(self.key, 1)) - 1
-
-
-def c3_main(csm, ctx, args, rank, world_size, dist):
-    """C3: the ConstraintBuilder2D global sweep of BASELINE.json configs[2],
-    2000 nodes x 1000 submaps (2 M MatchFullSubmap pairs, min_score 0.55),
-    as ONE fixed queue split over the ranks (strong scaling). The queue is
-    cut into chunks of --c3-chunk submaps x all nodes; ranks claim chunks
-    dynamically, build the chunk's pyramids on their GPU, search it as one
-    batch and keep the accepted constraints; at the end every rank's records
-    are gathered to rank 0 in submission order (constraint_builder_2d.cc:279-300).
-    A step = the whole queue; pyramid builds are inside the timed region."""
+def c3_run(csm, ctx, args, rank, world_size, dist, coll_dev, comm, gather, transport,
+           barrier_sync):
+    """C3 (BASELINE.json configs[2], the north-star queue): ConstraintBuilder2D's
+    global sweep, 2000 nodes x 1000 submaps = 2 M MatchFullSubmap pairs,
+    min_score 0.55, as ONE fixed queue (constraint_builder_2d.cc:102-111, swept
+    by pose_graph_2d.cc:379-392). Step k is the queue's slice of --c3-slice
+    submaps starting at submap k * slice (mod 1000): 20 steps = the whole
+    queue. The timed region's K slices are cut into chunks of --c3-chunk
+    submaps x all nodes; every rank claims chunks through csm_comm_fetch_add
+    (the rank-0 counter table: the shared queue of common::ThreadPool,
+    thread_pool.cc:80-106), builds the chunk's pyramids on its GPU, searches it
+    as one batch and keeps the accepted constraints; at the end the records
+    go to rank 0 in submission order (constraint_builder_2d.cc:279-300) over
+    RCCL. Warmup steps run one chunk each, untimed."""
     cdist = importlib.import_module("cartographer_amd.distributed")
     N, S, K = args.c3_nodes, args.c3_submaps, args.c3_chunk
     t0 = time.time()
@@ -854,15 +901,13 @@ def c3_main(csm, ctx, args, rank, world_size, dist):
     gen_s = time.time() - t0
     opts = csm.FastCorrelativeScanMatcherOptions2D(7.0, math.radians(30.0), 7, args.search_depth)
     scans = csm.ScanSet(None, ctx, packed=(world.points, world.offsets))
-    n_chunks = (S + K - 1) // K
-    coll_dev = None
-    if dist is not None:
-        import torch
-        coll_dev = torch.device("cuda", torch.cuda.current_device()) \
-            if args.dist_backend == "nccl" else None
+    slice_ = args.c3_slice
+    # The timed queue: steps x slice submaps, in queue order (wrapping after S).
+    queue = (np.arange(args.steps * slice_) % S).astype(np.int64)
+    chunks = [queue[i:i + K] for i in range(0, len(queue), K)]
+    n_chunks = len(chunks)
 
-    def run_chunk(c):
-        subs = np.arange(c * K, min(S, (c + 1) * K))
+    def run_chunk(subs, base):
         mats = [csm.FastCorrelativeScanMatcher2D(world.grid(int(s)), opts, ctx) for s in subs]
         sub_local = np.repeat(np.arange(len(subs), dtype=np.int32), N)
         node = np.tile(np.arange(N, dtype=np.int32), len(subs))
@@ -870,60 +915,51 @@ def c3_main(csm, ctx, args, rank, world_size, dist):
         res = csm.match_batch(mats, scans, pairs, ctx)
         for m in mats:
             m.close()
-        sub_global = subs[sub_local].astype(np.int64)
-        submission = sub_global * N + node  # queue order: submap-major
+        sub_global = np.asarray(subs, np.int64)[sub_local]
+        submission = base + np.arange(len(pairs), dtype=np.int64)  # queue order: submap-major
         return res, cdist.make_records(res, submission, sub_global, node)
 
-    gather, gather_transport = make_gather(csm, ctx, args, rank, world_size, dist, coll_dev)
-    for _ in range(args.warmup):  # one chunk: module load, staging buffers
-        run_chunk(rank % n_chunks)
-    claimer = ChunkClaimer(dist, n_chunks)
+    def claim(key):
+        if comm is None:
+            claim.local[key] = claim.local.get(key, 0) + 1
+            return claim.local[key] - 1
+        return comm.fetch_add(key, 1)
+    claim.local = {}
+
+    for w in range(args.warmup):  # one chunk each: module load, staging buffers
+        run_chunk(chunks[(rank + w) % n_chunks], 0)
     ctx.reset_timing()
     ctx.enable_timing(True)
-    errors = 0
-    claims = []
-    accepted = 0
-    step_s = []
-    for step in range(args.steps):
-        claimer.reset(step)
-        if dist is not None:
-            dist.barrier()
-            import torch
-            torch.cuda.synchronize()
-        a = time.perf_counter()
-        recs = []
-        mine = 0
-        while True:
-            c = claimer.claim()
-            if c >= n_chunks:
-                break
-            res, rec = run_chunk(c)
-            errors += int((res["status"] < 0).sum())
-            recs.append(rec)
-            mine += 1
-            if rank == 0 and world_size == 1:
-                print(f"c3: chunk {c + 1}/{n_chunks} {time.perf_counter() - a:.1f} s",
-                      file=sys.stderr, flush=True)
-        rec = np.concatenate(recs) if recs else np.zeros((0, cdist.RECORD_WIDTH))
-        out = gather(rec)
-        if dist is not None:
-            dist.barrier()
-            import torch
-            torch.cuda.synchronize()
-        step_s.append(time.perf_counter() - a)
-        claims.append(mine)
-        if rank == 0:
-            accepted = len(out)
+    barrier_sync()
+    t_start = time.perf_counter()
+    errors, mine, recs = 0, 0, []
+    while True:
+        c = claim(1)  # key 1: the timed queue's head
+        if c >= n_chunks:
+            break
+        res, rec = run_chunk(chunks[c], np.int64(c) * K * N)
+        errors += int((res["status"] < 0).sum())
+        recs.append(rec)
+        mine += 1
+        if rank == 0 and (c % 10 == 0 or world_size == 1):
+            print(f"c3: chunk {c + 1}/{n_chunks} {time.perf_counter() - t_start:.1f} s",
+                  file=sys.stderr, flush=True)
+    allrec = gather(np.concatenate(recs) if recs else np.zeros((0, cdist.RECORD_WIDTH)))
+    barrier_sync()
+    elapsed = time.perf_counter() - t_start
     ctx.enable_timing(False)
     tm = ctx.timing()
-    elapsed = cdist.max_over_ranks(sum(step_s), dist, coll_dev)
+    lv_cands, lv_batches = ctx.level_stats()
+    accepted = len(allrec) if rank == 0 else 0
+    elapsed = cdist.max_over_ranks(elapsed, dist, coll_dev)
     errors = int(cdist.sum_over_ranks(errors, dist, coll_dev))
-    total_pairs = N * S * args.steps
-    kernel_ms = cdist.max_over_ranks(tm.search_kernel_ms, dist, coll_dev)
-    lookups = cdist.sum_over_ranks(tm.search_lookups, dist, coll_dev)
-    launches = cdist.sum_over_ranks(tm.search_launches, dist, coll_dev)
-    achieved = tm.search_lookups / (tm.search_kernel_ms * 1e-3) / 1e9 if tm.search_kernel_ms else 0.0
+    total_pairs = len(queue) * N
+    kernel_ms_avg = tm.search_kernel_ms / max(tm.search_launches, 1)
+    bytes_per_launch = tm.search_lookups / max(tm.search_launches, 1)
+    achieved = bytes_per_launch / (kernel_ms_avg * 1e-3) / 1e9 if kernel_ms_avg else 0.0
     traffic = committed_traffic(args, world_size, "c3")
+    claimed = cdist.sum_over_ranks(mine, dist, coll_dev)
+    chunks_max = cdist.max_over_ranks(mine, dist, coll_dev)
     out = {
         "metric": "loop-closure constraint candidates/sec (node x submap pairs) + ms/scan-match, 2D 5cm grid",
         "value": total_pairs / elapsed, "unit": "pairs/s", "n_gpus": world_size,
@@ -931,44 +967,40 @@ def c3_main(csm, ctx, args, rank, world_size, dist):
         "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u8",
         "data": "synthetic (seeded building world, 1080-beam scans, ray-cast submaps)",
         "config": {"workload": f"C3: ConstraintBuilder2D global sweep, {N} nodes x {S} submaps "
-                               f"(400x400 @5cm) = {N * S} MatchFullSubmap pairs, one fixed queue over "
-                               f"the ranks, chunks of {K} submaps claimed dynamically, "
-                               f"branch_and_bound_depth=7, min_score={args.min_score:.2f}",
-                   "pairs_per_step": N * S, "search_depth": 0 if args.search_depth == 0 else args.search_depth,
+                               f"(400x400 @5cm) = {N * S} MatchFullSubmap pairs in one fixed queue; "
+                               f"a step = {slice_} submaps x {N} nodes of it ({slice_ * N} pairs), "
+                               f"chunks of {K} submaps claimed dynamically by the ranks, pyramids "
+                               f"built inside the timed region, branch_and_bound_depth=7, "
+                               f"min_score={args.min_score:.2f}",
+                   "pairs_per_step": slice_ * N, "queue_pairs_timed": total_pairs,
+                   "covers_whole_queue": bool(len(np.unique(queue)) == S),
+                   "search_depth": args.search_depth,
                    "parallelism": f"dynamic chunk claiming x{world_size}",
-                   "gather": gather_transport},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": 8000.0, "unit": "GB/s",
-                     "frac": achieved / 8000.0,
-                     **traffic_fields(traffic, tm.search_kernel_ms / max(tm.search_launches, 1),
-                                      8000.0),
-                     "kernel": "fast2d_search",
-                     "kernel_ms_avg": tm.search_kernel_ms / max(tm.search_launches, 1),
-                     "algorithmic_bytes_per_launch": tm.search_lookups / max(tm.search_launches, 1)},
-        "accepted_constraints_per_step": accepted,
+                   "gather": transport},
+        "roofline": roofline_fields(tm, achieved, 8000.0, traffic, kernel_ms_avg, bytes_per_launch,
+                                    tm.search_candidates / max(tm.search_launches, 1) *
+                                    float(np.diff(world.offsets).mean())),
+        "accepted_constraints": accepted,
         "errors_per_step": errors / args.steps,
         "stack_high_water": int(tm.stack_high_water),
-        "chunks": n_chunks, "chunks_claimed_rank0": claims,
-        "kernel_s_max_over_ranks": kernel_ms * 1e-3, "search_launches": int(launches),
-        "lookups_per_pair": lookups / max(total_pairs, 1),
+        "chunks": n_chunks, "chunks_claimed": int(claimed), "chunks_max_rank": int(chunks_max),
+        "kernel_s_rank0": tm.search_kernel_ms * 1e-3, "search_launches_rank0": int(tm.search_launches),
+        "search_levels": {"candidates_per_pair": [c / max(mine * K * N, 1) for c in lv_cands],
+                          "mean_lanes_per_batch": [c / b if b else 0 for c, b in zip(lv_cands, lv_batches)]},
         "setup_s": {"world": gen_s},
     }
     if rank == 0 and world_size == 1 and not args.no_cpu:
         rng = np.random.RandomState(12345)
         k = args.cpu_pairs or 2000
-        args.cpu_pairs = k
+        args_c = argparse.Namespace(**vars(args))
+        args_c.cpu_pairs = k
         ps = rng.randint(0, S, k)
         pn = rng.randint(0, N, k)
-        out["cpu_baseline"] = cpu_pairs_2d(world, ps, pn, args,
-                                           f"uniformly sampled (submap, node) pairs of the C3 queue")
+        out["cpu_baseline"] = cpu_pairs_2d(world, ps, pn, args_c,
+                                           "uniformly sampled (submap, node) pairs of the C3 queue")
         out["speedup_vs_cpu"] = out["value"] / out["cpu_baseline"]["value"]
-    if rank == 0:
-        print(json.dumps(out), flush=True)
-    if dist is not None:
-        dist.barrier()
-        dist.destroy_process_group()
-    if errors:
-        print(f"bench: {errors} pair searches returned an error status", file=sys.stderr)
-        sys.exit(3)
+    scans.close()
+    return out, errors
 
 
 if __name__ == "__main__":

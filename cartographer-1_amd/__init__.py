@@ -345,6 +345,8 @@ _SIGNATURES = {
     "csm_comm_gathered": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.POINTER(C.c_int64)]),
     "csm_comm_allreduce_i64": (C.c_int, [C.c_void_p, C.POINTER(C.c_int64), C.c_int32, C.c_int32]),
     "csm_comm_barrier": (C.c_int, [C.c_void_p]),
+    "csm_comm_claim_open": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int32]),
+    "csm_comm_fetch_add": (C.c_int, [C.c_void_p, C.c_int64, C.c_int64, C.POINTER(C.c_int64)]),
     "csm_strerror": (C.c_char_p, [C.c_int]),
 }
 
@@ -1268,6 +1270,17 @@ class Comm:
 
     def barrier(self):
         _check(self._lib.csm_comm_barrier(self.h), "csm_comm_barrier")
+
+    def claim_open(self, host: str = "127.0.0.1", port: int = 29621):
+        """Collective: starts the rank-0 counter table for fetch_add (the
+        shared work queue of common::ThreadPool across ranks)."""
+        _check(self._lib.csm_comm_claim_open(self.h, host.encode(), port), "csm_comm_claim_open")
+
+    def fetch_add(self, key: int, delta: int = 1) -> int:
+        """Counter `key` before adding `delta`, atomic across ranks."""
+        old = C.c_int64()
+        _check(self._lib.csm_comm_fetch_add(self.h, key, delta, C.byref(old)), "csm_comm_fetch_add")
+        return int(old.value)
 
     def close(self):
         if self.h:

@@ -23,9 +23,13 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
+#include <map>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -112,7 +116,28 @@ bool RecvAll(int fd, void* p, size_t n, int timeout_ms) {
   return true;
 }
 
+// Connection set-up (connect / accept) gives up after this long.
 constexpr int kTcpTimeoutMs = 120000;
+
+// Data receives of the collectives wait for the slowest rank: a rank reaches a
+// gather only after its own share of the search, and at C3 scale ranks run
+// for minutes, so the default is no limit (-1). CSM_COMM_TIMEOUT_MS bounds it
+// (tests use a short one to exercise a late rank).
+int DataTimeoutMs() {
+  static const int v = [] {
+    const char* e = std::getenv("CSM_COMM_TIMEOUT_MS");
+    if (!e || !*e) return -1;
+    const long t = std::strtol(e, nullptr, 10);
+    return t > 0 ? static_cast<int>(std::min<long>(t, 0x7fffffff)) : -1;
+  }();
+  return v;
+}
+
+struct ClaimService;
+void DestroyClaims(ClaimService* s);
+struct ClaimDeleter {
+  void operator()(ClaimService* s) const { DestroyClaims(s); }
+};
 
 }  // namespace
 
@@ -129,8 +154,11 @@ struct csm_comm {
   // The root's last gather: every rank's blob in rank order, and the sizes.
   std::vector<char> gathered;
   std::vector<int64_t> sizes;
+  // Dynamic work claiming (csm_comm_claim_open); destroyed before the sockets.
+  std::unique_ptr<ClaimService, ClaimDeleter> claims;
 
   ~csm_comm() {
+    claims.reset();
     if (nccl && Rccl()) Rccl()->CommDestroy(nccl);
     for (int fd : peers)
       if (fd >= 0) ::close(fd);
@@ -207,7 +235,7 @@ int TcpGather(csm_comm* c, const void* send, int64_t bytes) {
   c->sizes.assign(c->size, 0);
   c->sizes[0] = bytes;
   for (int r = 1; r < c->size; ++r)
-    if (!RecvAll(c->peers[r], &c->sizes[r], sizeof(int64_t), kTcpTimeoutMs) || c->sizes[r] < 0)
+    if (!RecvAll(c->peers[r], &c->sizes[r], sizeof(int64_t), DataTimeoutMs()) || c->sizes[r] < 0)
       return CSM_EINVAL;
   int64_t total = 0;
   for (int64_t v : c->sizes) total += v;
@@ -216,7 +244,7 @@ int TcpGather(csm_comm* c, const void* send, int64_t bytes) {
   int64_t at = bytes;
   for (int r = 1; r < c->size; ++r) {
     if (c->sizes[r] > 0 &&
-        !RecvAll(c->peers[r], c->gathered.data() + at, static_cast<size_t>(c->sizes[r]), kTcpTimeoutMs))
+        !RecvAll(c->peers[r], c->gathered.data() + at, static_cast<size_t>(c->sizes[r]), DataTimeoutMs()))
       return CSM_EINVAL;
     at += c->sizes[r];
   }
@@ -226,12 +254,12 @@ int TcpGather(csm_comm* c, const void* send, int64_t bytes) {
 int TcpAllreduce(csm_comm* c, int64_t* v, int n, int op) {
   const size_t b = sizeof(int64_t) * static_cast<size_t>(n);
   if (c->rank != 0) {
-    if (!SendAll(c->root_fd, v, b) || !RecvAll(c->root_fd, v, b, kTcpTimeoutMs)) return CSM_EINVAL;
+    if (!SendAll(c->root_fd, v, b) || !RecvAll(c->root_fd, v, b, DataTimeoutMs())) return CSM_EINVAL;
     return CSM_OK;
   }
   std::vector<int64_t> o(static_cast<size_t>(n));
   for (int r = 1; r < c->size; ++r) {
-    if (!RecvAll(c->peers[r], o.data(), b, kTcpTimeoutMs)) return CSM_EINVAL;
+    if (!RecvAll(c->peers[r], o.data(), b, DataTimeoutMs())) return CSM_EINVAL;
     for (int i = 0; i < n; ++i) v[i] = op == CSM_REDUCE_MAX ? std::max(v[i], o[i]) : v[i] + o[i];
   }
   for (int r = 1; r < c->size; ++r)
@@ -244,23 +272,47 @@ int TcpAllreduce(csm_comm* c, int64_t* v, int n, int op) {
     if ((x) != 0) return CSM_EHIP;      \
   } while (0)
 
+// Every failure a rank can hit locally (staging allocation) is exchanged
+// before any payload moves, so either all ranks move data or all return the
+// same error; no rank is left blocked in a Send or Recv. The count buffer is
+// allocated when the communicator is created (kCountWords), so the count
+// exchange itself never depends on an allocation.
+constexpr int kCountWords = 64;
+
 int RcclGather(csm_comm* c, const void* send, int64_t bytes) {
   RcclApi* R = Rccl();
   hipStream_t st = c->ctx->stream;
   if (hipSetDevice(c->ctx->device) != hipSuccess) return CSM_EHIP;
-  int rc;
-  if ((rc = c->d_counts.Reserve(sizeof(int64_t) * (c->size + 1)))) return rc;
+  if (c->size + 2 > kCountWords) return CSM_ERANGE;  // same on every rank
   int64_t* dc = c->d_counts.as<int64_t>();
-  CSM_HIP(hipMemcpyAsync(dc + c->size, &bytes, sizeof(int64_t), hipMemcpyHostToDevice, st));
+  // A peer that cannot stage its payload reports -1 instead of its size.
+  int64_t mine = bytes;
+  if (c->rank != 0 && bytes > 0 && c->d_send.Reserve(static_cast<size_t>(bytes)) != CSM_OK) mine = -1;
+  CSM_HIP(hipMemcpyAsync(dc + c->size, &mine, sizeof(int64_t), hipMemcpyHostToDevice, st));
   NCCL_OK(R->AllGather(dc + c->size, dc, 1, kNcclInt64, c->nccl, st));
   std::vector<int64_t> sz(c->size);
   CSM_HIP(hipMemcpyAsync(sz.data(), dc, sizeof(int64_t) * c->size, hipMemcpyDeviceToHost, st));
   CSM_HIP(hipStreamSynchronize(st));
   int64_t total = 0;
-  for (int64_t v : sz) total += v;
+  bool failed = false;
+  for (int64_t v : sz) {
+    failed |= v < 0;
+    total += std::max<int64_t>(v, 0);
+  }
+  if (failed) return CSM_ENOMEM;  // every rank saw the same -1
+  // The root stages the receive side, then tells every rank whether it could.
+  int64_t root_fail = 0;
+  if (c->rank == 0 && total > bytes && c->d_recv.Reserve(static_cast<size_t>(total)) != CSM_OK)
+    root_fail = 1;
+  if (total > sz[0]) {  // some peer has a payload: agree on the root's staging
+    CSM_HIP(hipMemcpyAsync(dc + c->size + 1, &root_fail, sizeof(int64_t), hipMemcpyHostToDevice, st));
+    NCCL_OK(R->AllReduce(dc + c->size + 1, dc + c->size + 1, 1, kNcclInt64, kNcclMax, c->nccl, st));
+    CSM_HIP(hipMemcpyAsync(&root_fail, dc + c->size + 1, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    CSM_HIP(hipStreamSynchronize(st));
+    if (root_fail) return CSM_ENOMEM;
+  }
   if (c->rank != 0) {
     if (bytes == 0) return CSM_OK;
-    if ((rc = c->d_send.Reserve(static_cast<size_t>(bytes)))) return rc;
     CSM_HIP(hipMemcpyAsync(c->d_send.ptr, send, static_cast<size_t>(bytes), hipMemcpyHostToDevice, st));
     NCCL_OK(R->Send(c->d_send.ptr, static_cast<size_t>(bytes), kNcclInt8, 0, c->nccl, st));
     CSM_HIP(hipStreamSynchronize(st));
@@ -270,7 +322,6 @@ int RcclGather(csm_comm* c, const void* send, int64_t bytes) {
   c->gathered.resize(static_cast<size_t>(total));
   if (bytes > 0) std::memcpy(c->gathered.data(), send, static_cast<size_t>(bytes));
   if (total == bytes) return CSM_OK;
-  if ((rc = c->d_recv.Reserve(static_cast<size_t>(total)))) return rc;
   char* dr = static_cast<char*>(c->d_recv.ptr);
   NCCL_OK(R->GroupStart());
   int64_t at = bytes;
@@ -285,18 +336,124 @@ int RcclGather(csm_comm* c, const void* send, int64_t bytes) {
   return CSM_OK;
 }
 
+// In pieces of kCountWords through the buffer allocated at creation.
 int RcclAllreduce(csm_comm* c, int64_t* v, int n, int op) {
   RcclApi* R = Rccl();
   hipStream_t st = c->ctx->stream;
   if (hipSetDevice(c->ctx->device) != hipSuccess) return CSM_EHIP;
-  int rc;
-  if ((rc = c->d_counts.Reserve(sizeof(int64_t) * std::max(n, c->size + 1)))) return rc;
   int64_t* d = c->d_counts.as<int64_t>();
-  CSM_HIP(hipMemcpyAsync(d, v, sizeof(int64_t) * n, hipMemcpyHostToDevice, st));
-  NCCL_OK(R->AllReduce(d, d, static_cast<size_t>(n), kNcclInt64,
-                       op == CSM_REDUCE_MAX ? kNcclMax : kNcclSum, c->nccl, st));
-  CSM_HIP(hipMemcpyAsync(v, d, sizeof(int64_t) * n, hipMemcpyDeviceToHost, st));
-  CSM_HIP(hipStreamSynchronize(st));
+  for (int at = 0; at < n; at += kCountWords) {
+    const int k = std::min(kCountWords, n - at);
+    CSM_HIP(hipMemcpyAsync(d, v + at, sizeof(int64_t) * k, hipMemcpyHostToDevice, st));
+    NCCL_OK(R->AllReduce(d, d, static_cast<size_t>(k), kNcclInt64,
+                         op == CSM_REDUCE_MAX ? kNcclMax : kNcclSum, c->nccl, st));
+    CSM_HIP(hipMemcpyAsync(v + at, d, sizeof(int64_t) * k, hipMemcpyDeviceToHost, st));
+    CSM_HIP(hipStreamSynchronize(st));
+  }
+  return CSM_OK;
+}
+
+// ---- Dynamic work claiming ------------------------------------------------------
+// The reference balances one task per pair on a shared queue
+// (common/thread_pool.cc:80-106: idle workers pop the next task). Across
+// processes the queue head is a table of counters on rank 0, served by a host
+// thread: a peer sends (key, delta) and gets the counter's value before the
+// add. Rank 0's own claims take the same mutex without a round trip. The
+// transport is host TCP for RCCL communicators too: a claim is 24 bytes, and
+// there is no device atomic shared between processes that RCCL exposes.
+struct ClaimService {
+  std::mutex mu;
+  std::map<int64_t, int64_t> counters;
+  int listen_fd = -1;
+  int wake[2] = {-1, -1};  // self-pipe: destroy wakes the server's poll
+  std::vector<int> peers;  // rank 0: one socket per peer; others: [0] = to the root
+  std::thread server;
+
+  int64_t FetchAddLocal(int64_t key, int64_t delta) {
+    std::lock_guard<std::mutex> lock(mu);
+    int64_t& v = counters[key];
+    const int64_t old = v;
+    v += delta;
+    return old;
+  }
+
+  void Serve() {
+    std::vector<pollfd> fds;
+    for (;;) {
+      fds.clear();
+      fds.push_back(pollfd{wake[0], POLLIN, 0});
+      for (int fd : peers)
+        if (fd >= 0) fds.push_back(pollfd{fd, POLLIN, 0});
+      if (fds.size() == 1) return;  // every peer has gone
+      if (::poll(fds.data(), fds.size(), -1) < 0) return;
+      if (fds[0].revents) return;
+      for (size_t k = 1; k < fds.size(); ++k) {
+        if (!fds[k].revents) continue;
+        int64_t req[2];
+        if (!RecvAll(fds[k].fd, req, sizeof(req), kTcpTimeoutMs)) {
+          for (int& fd : peers)
+            if (fd == fds[k].fd) { ::close(fd); fd = -1; }
+          continue;
+        }
+        const int64_t old = FetchAddLocal(req[0], req[1]);
+        if (!SendAll(fds[k].fd, &old, sizeof(old))) {
+          for (int& fd : peers)
+            if (fd == fds[k].fd) { ::close(fd); fd = -1; }
+        }
+      }
+    }
+  }
+
+  ~ClaimService() {
+    if (wake[1] >= 0) {
+      const char b = 1;
+      (void)!::write(wake[1], &b, 1);
+    }
+    if (server.joinable()) server.join();
+    for (int fd : peers)
+      if (fd >= 0) ::close(fd);
+    for (int fd : wake)
+      if (fd >= 0) ::close(fd);
+  }
+};
+
+int ClaimOpen(csm_comm* c, const char* host, int port) {
+  auto svc = std::make_unique<ClaimService>();
+  if (c->size > 1) {
+    // The same rendezvous as the TCP transport, on its own port.
+    csm_comm tmp;
+    tmp.rank = c->rank;
+    tmp.size = c->size;
+    const int rc = TcpConnect(&tmp, host, port);
+    if (rc) return rc;
+    if (c->rank == 0) {
+      svc->peers = tmp.peers;
+      tmp.peers.clear();
+      if (::pipe(svc->wake) != 0) return CSM_EINVAL;
+      ClaimService* raw = svc.get();
+      svc->server = std::thread([raw] { raw->Serve(); });
+    } else {
+      svc->peers.assign(1, tmp.root_fd);
+      tmp.root_fd = -1;
+    }
+  }
+  c->claims.reset(svc.release());
+  return CSM_OK;
+}
+
+void DestroyClaims(ClaimService* s) { delete s; }
+
+int ClaimFetchAdd(csm_comm* c, int64_t key, int64_t delta, int64_t* old) {
+  ClaimService* s = c->claims.get();
+  if (c->rank == 0 || c->size == 1) {
+    *old = s->FetchAddLocal(key, delta);
+    return CSM_OK;
+  }
+  // One request in flight per rank; callers on several threads take turns.
+  std::lock_guard<std::mutex> lock(s->mu);
+  const int64_t req[2] = {key, delta};
+  if (!SendAll(s->peers[0], req, sizeof(req)) || !RecvAll(s->peers[0], old, sizeof(*old), DataTimeoutMs()))
+    return CSM_EINVAL;
   return CSM_OK;
 }
 
@@ -329,6 +486,7 @@ int csm_comm_create_rccl(csm_context* ctx, int32_t rank, int32_t world_size, con
   std::memcpy(u.internal, id, kIdBytes);
   // ncclCommInitRank(comm, nranks, ncclUniqueId (128 B by value), rank)
   using Init = int (*)(ncclComm_p*, int, UniqueId, int);
+  if (c->d_counts.Reserve(sizeof(int64_t) * kCountWords)) return CSM_ENOMEM;
   if (reinterpret_cast<Init>(R->CommInitRank)(&c->nccl, world_size, u, rank) != 0)
     return CSM_EHIP;
   *out = c.release();
@@ -392,6 +550,17 @@ int csm_comm_allreduce_i64(csm_comm* c, int64_t* values, int32_t count, int32_t 
 int csm_comm_barrier(csm_comm* c) {
   int64_t v = 0;
   return csm_comm_allreduce_i64(c, &v, 1, CSM_REDUCE_SUM);
+}
+
+int csm_comm_claim_open(csm_comm* c, const char* root_host, int32_t port) {
+  if (!c || c->claims || (c->size > 1 && (port <= 0 || port > 65535 || (c->rank != 0 && !root_host))))
+    return CSM_EINVAL;
+  return ClaimOpen(c, root_host, port);
+}
+
+int csm_comm_fetch_add(csm_comm* c, int64_t key, int64_t delta, int64_t* old_value) {
+  if (!c || !c->claims || !old_value) return CSM_EINVAL;
+  return ClaimFetchAdd(c, key, delta, old_value);
 }
 
 }  // extern "C"

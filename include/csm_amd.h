@@ -603,6 +603,16 @@ int csm_comm_gathered(const csm_comm* comm, void* out, int64_t capacity, int64_t
 /* Collective: element-wise sum or max over ranks, in place. */
 int csm_comm_allreduce_i64(csm_comm* comm, int64_t* values, int32_t count, int32_t op);
 int csm_comm_barrier(csm_comm* comm);
+/* Dynamic work claiming: the shared queue of the reference's
+ * common::ThreadPool (thread_pool.cc:80-106, idle workers take the next task;
+ * ConstraintBuilder2D schedules one task per pair, constraint_builder_2d.cc:102-111)
+ * stretched over ranks. claim_open is collective: rank 0 serves a table of
+ * int64 counters from a host thread on `port`, the others connect to
+ * root_host:port (any transport; a world of 1 keeps the table locally).
+ * fetch_add is NOT collective: *old_value = counter[key], counter[key] += delta,
+ * atomically across ranks; counters start at 0. */
+int csm_comm_claim_open(csm_comm* comm, const char* root_host, int32_t port);
+int csm_comm_fetch_add(csm_comm* comm, int64_t key, int64_t delta, int64_t* old_value);
 
 /* Human-readable text for a return code. */
 const char* csm_strerror(int code);
