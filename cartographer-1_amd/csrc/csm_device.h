@@ -57,6 +57,17 @@ struct SubmapDesc {
   // quad_bias[d], quad_bias = (2^d - 1) + (k - 1) + 2^d.
   int32_t cshift[kMaxLevels];
   int32_t quad_bias[kMaxLevels];
+  // Plane kind per level: entry bytes 4 = quad (above), 16 = hex, 0 = none.
+  // Hex layout (search kernel v5): a node of a level L >= 2 in hex_mask
+  // scores its 16 grandchildren at level c = L - 2, offsets (a h, b h),
+  // a, b in 0..3, h = 2^c, from ONE 16-byte entry: dword a, byte b =
+  // M_c(X + a h, Y + b h), X' = cell + offset + quad_bias[c] with quad_bias =
+  // (h - 1) + (k - 1) + 3h, polyphase with period P = 4h (the lattice nodes of
+  // level c + 2 sit on). Only the levels the node chain reaches get a plane
+  // (virtual roots at levels: quad into levels - 1; then L -> L - 2 for hex
+  // levels, L -> L - 1 otherwise).
+  int32_t quad_es[kMaxLevels];
+  int32_t hex_mask;  // bit L: nodes of level L expand two levels at once (0: v4)
 };
 
 constexpr int kMaxClusterShift = 3;  // clusters of 1, 2, 4, 8 cells per side
@@ -97,7 +108,7 @@ struct WorkQueues2 {
 
 constexpr int kStack2 = 1024;   // v4 per-workgroup DFS stack entries in LDS
 constexpr int kSpill2 = 7168;   // further entries per workgroup in global memory
-constexpr int kBatchNodes = 64; // nodes expanded per batch (256 children)
+constexpr int kBatchNodes = 64; // nodes expanded per batch (256 children; hex: 1024)
 
 // Best leaf per pair, packed for a 64-bit atomicMax:
 //   [63:42] level-0 integer sum (22 bits)

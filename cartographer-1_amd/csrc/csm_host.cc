@@ -96,7 +96,10 @@ int RunBatch(csm_context* ctx, csm_fast2d* const* submaps, int32_t num_submaps,
   for (int i = 0; i < num_submaps; ++i) {
     if (!submaps[i] || submaps[i]->ctx != ctx) return CSM_EINVAL;
     sdesc[i] = submaps[i]->desc;
+    // One launch serves one kernel: v4 (no hex levels) or v5 (fixed at create).
+    if ((sdesc[i].hex_mask != 0) != (sdesc[0].hex_mask != 0)) return CSM_EINVAL;
   }
+  const bool hex = num_submaps > 0 && sdesc[0].hex_mask != 0;
   std::vector<PairDesc> pdesc;
   std::vector<int64_t> pair_src;  // pdesc index -> pair index
   std::vector<float2> rot_host;
@@ -265,8 +268,15 @@ int RunBatch(csm_context* ctx, csm_fast2d* const* submaps, int32_t num_submaps,
     const int lds_cap = 96 * 1024;
     while (capc > 0 && static_cast<size_t>(rc) * (max_npad + capc) * 5 > lds_cap) capc -= 64;
     const size_t dyn_lds = (static_cast<size_t>(rc) * (max_npad + capc) * 5 + 15) & ~size_t{15};
-    const size_t static_lds = 12 * 1024;  // V4Shared (8 KiB stack + batch state)
-    const int per_cu = std::max(1, std::min(8, static_cast<int>((160 * 1024) / (dyn_lds + static_lds))));
+    // V4Shared: 8 KiB stack + batch state (v5: a 4 KiB stack + 4 KiB of
+    // 16-child sums). CSM_WG_PER_CU caps the workgroups per CU (A/B runs).
+    const size_t static_lds = 12 * 1024 + 512;
+    // Node order: FIFO (level by level, the default) or LIFO (depth-first,
+    // CSM_SEARCH_ORDER=lifo).
+    const char* order_env = std::getenv("CSM_SEARCH_ORDER");
+    const bool fifo = !(order_env && std::strcmp(order_env, "lifo") == 0);
+    int per_cu = std::max(1, std::min(8, static_cast<int>((160 * 1024) / (dyn_lds + static_lds))));
+    if (const char* w = std::getenv("CSM_WG_PER_CU")) per_cu = std::max(1, std::min(per_cu, std::atoi(w)));
     const int grid = static_cast<int>(std::min<int64_t>(static_cast<int64_t>(ctx->num_cus) * per_cu,
                                                         std::max<int64_t>(total_chunks, 1)));
     // DFS stack spill: kSpill2 entries per persistent workgroup.
@@ -277,7 +287,7 @@ int RunBatch(csm_context* ctx, csm_fast2d* const* submaps, int32_t num_submaps,
                                  ctx->rot_table.as<float2>(), wq2,
                                  ctx->counters.as<unsigned long long>(), ctx->best.as<uint64_t>(),
                                  ctx->status.as<int32_t>(), ctx->stats.as<unsigned long long>(),
-                                 ctx->spill.as<uint2>(), max_npad, capc));
+                                 ctx->spill.as<uint2>(), max_npad, capc, hex, fifo));
   } else {
     const size_t dyn_lds = static_cast<size_t>(rc) * max_npad * sizeof(uint32_t);
     const int grid = static_cast<int>(std::min<int64_t>(static_cast<int64_t>(ctx->num_cus) * 4,
@@ -461,6 +471,31 @@ int csm_fast2d_create(csm_context* ctx, const csm_map_limits* limits,
                                         : AutoSearchDepth(options->branch_and_bound_depth, nx, ny);
   depth = std::max(depth, options->branch_and_bound_depth);
   depth = std::min(depth, kMaxLevels);
+  // Node levels that expand two levels at once (search kernel v5, hex
+  // planes; SubmapDesc::hex_mask): by default the top level and the one two
+  // below it (measured best on C2). CSM_SEARCH_KERNEL=4: none
+  // (v4, quad planes only); =5: every even level >= 2; CSM_HEX_LEVELS="8,6"
+  // lists them (experiments).
+  uint32_t hex_mask = 0;
+  {
+    const char* kenv = std::getenv("CSM_SEARCH_KERNEL");
+    const int kf = kenv ? std::atoi(kenv) : 0;
+    if (kf == 5) {
+      for (int l = 2; l < depth; l += 2) hex_mask |= 1u << l;
+    } else if (kf != 4 && kf != 2) {
+      for (int l : {depth - 1, depth - 3})
+        if (l >= 2) hex_mask |= 1u << l;
+    }
+    if (const char* lv = std::getenv("CSM_HEX_LEVELS")) {
+      hex_mask = 0;
+      for (const char* c = lv; *c;) {
+        const int l = std::atoi(c);
+        if (l >= 2 && l < depth) hex_mask |= 1u << l;
+        while (*c && *c != ',') ++c;
+        if (*c == ',') ++c;
+      }
+    }
+  }
   m->options.search_depth = depth;
   std::vector<uint8_t> qtab(32768);
   if (!QuantizationTable(min_cc, max_cc, qtab.data())) return CSM_EINVAL;
@@ -482,23 +517,55 @@ int csm_fast2d_create(csm_context* ctx, const csm_map_limits* limits,
     offs[l] = total;
     total += (static_cast<size_t>(d.zero_index[l]) + 1 + 255) & ~size_t(255);
   }
+  const size_t rowmajor = total;
   std::vector<size_t> qoffs(depth);
   ClusterShifts(d.cshift);
-  for (int l = 0; l < depth; ++l) {
-    const int h = 1 << l;
-    const int km1 = (1 << d.cshift[l]) - 1;
-    d.quad_bias[l] = (h - 1) + km1 + h;
-    d.quad_w[l] = d.wide_nx[l] + km1 + h;
-    d.quad_h[l] = d.wide_ny[l] + km1 + h;
-    d.quad_pws[l] = (d.quad_w[l] + 2 * h - 1) / (2 * h);
-    d.quad_pph[l] = (d.quad_h[l] + 2 * h - 1) / (2 * h);
-    const size_t qb = static_cast<size_t>(2 * h) * (2 * h) * d.quad_pws[l] * d.quad_pph[l] * 4;
-    if (qb > 0x7fffff00u) return CSM_ERANGE;
-    d.quad_bytes[l] = static_cast<int32_t>(qb);
-    qoffs[l] = total;
-    total += (qb + 255) & ~size_t(255);
+  size_t widen_bytes = 0;  // scratch for the widened levels the hex planes are made from
+  // Plane layout (SubmapDesc::quad_es): the levels the node chain reaches
+  // (virtual roots -> quad plane of the top level; a node level L in the
+  // mask -> hex plane of L - 2, any other -> quad plane of L - 1). A layout
+  // past the 2^31-byte buffer range falls back to quad planes only.
+  auto layout = [&](uint32_t mask) {
+    int kind[kMaxLevels] = {0};
+    kind[depth - 1] = 4;
+    for (int L = depth - 1; L >= 1;) {
+      if (L >= 2 && ((mask >> L) & 1u)) {
+        kind[L - 2] = 16;
+        L -= 2;
+      } else {
+        kind[L - 1] = 4;
+        L -= 1;
+      }
+    }
+    total = rowmajor;
+    widen_bytes = 0;
+    for (int l = 0; l < depth; ++l) {
+      const int h = 1 << l;
+      const int km1 = (1 << d.cshift[l]) - 1;
+      const bool hexl = kind[l] == 16;
+      const int reach = hexl ? 3 * h : h, period = hexl ? 4 * h : 2 * h;
+      d.quad_es[l] = kind[l];
+      d.quad_bias[l] = (h - 1) + km1 + reach;
+      d.quad_w[l] = d.wide_nx[l] + km1 + reach;
+      d.quad_h[l] = d.wide_ny[l] + km1 + reach;
+      d.quad_pws[l] = (d.quad_w[l] + period - 1) / period;
+      d.quad_pph[l] = (d.quad_h[l] + period - 1) / period;
+      const size_t qb = static_cast<size_t>(period) * period * d.quad_pws[l] * d.quad_pph[l] * kind[l];
+      if (qb > 0x7fffff00u) return false;
+      d.quad_bytes[l] = static_cast<int32_t>(qb);
+      qoffs[l] = total;
+      total += (qb + 255) & ~size_t(255);
+      if (hexl)
+        widen_bytes = std::max(widen_bytes, static_cast<size_t>(d.wide_nx[l] + km1) *
+                                                (d.wide_ny[l] + km1));
+    }
+    return total <= 0x7fffff00u;
+  };
+  if (!layout(hex_mask)) {
+    if (!hex_mask || !layout(0)) return CSM_ERANGE;
+    hex_mask = 0;
   }
-  if (total > 0x7fffff00u) return CSM_ERANGE;
+  d.hex_mask = static_cast<int32_t>(hex_mask);
   int rc;
   if ((rc = m->pyramid.Reserve(total))) return rc;
   d.pyramid_base = m->pyramid.as<uint8_t>();
@@ -523,10 +590,19 @@ int csm_fast2d_create(csm_context* ctx, const csm_map_limits* limits,
                                 const_cast<uint8_t*>(d.level[l]), d.wide_nx[l], d.wide_ny[l],
                                 1 << (l - 1), st));
   }
-  for (int l = 0; l < depth; ++l)
-    CSM_HIP(LaunchPyramidQuad(d.level[l], d.wide_nx[l], d.wide_ny[l], l, (1 << d.cshift[l]) - 1,
-                              const_cast<uint32_t*>(d.quad[l]), d.quad_w[l], d.quad_h[l],
-                              d.quad_pws[l], d.quad_pph[l], d.quad_bytes[l] / 4, st));
+  DevBuf dwiden;
+  if (widen_bytes && (rc = dwiden.Reserve(widen_bytes))) return rc;
+  for (int l = 0; l < depth; ++l) {
+    const int km1 = (1 << d.cshift[l]) - 1;
+    if (d.quad_es[l] == 4)
+      CSM_HIP(LaunchPyramidQuad(d.level[l], d.wide_nx[l], d.wide_ny[l], l, km1,
+                                const_cast<uint32_t*>(d.quad[l]), d.quad_w[l], d.quad_h[l],
+                                d.quad_pws[l], d.quad_pph[l], d.quad_bytes[l] / 4, st));
+    else if (d.quad_es[l] == 16)
+      CSM_HIP(LaunchPyramidHex(d.level[l], d.wide_nx[l], d.wide_ny[l], l, km1, dwiden.as<uint8_t>(),
+                               const_cast<uint32_t*>(d.quad[l]), d.quad_w[l], d.quad_h[l],
+                               d.quad_pws[l], d.quad_pph[l], d.quad_bytes[l] / 16, st));
+  }
   // Correspondence costs (Grid2D::GetCorrespondenceCost, grid_2d.cc) for the
   // CeresScanMatcher2D refinement: the value table with unknown -> max_cc.
   {

@@ -577,6 +577,57 @@ __global__ void pyramid_quad(const uint8_t* __restrict__ level, int wnx, int wny
   out[o] = v;
 }
 
+// The widened level M (row-major, mw = wnx + km1 by mh = wny + km1): M-wide
+// cell (X, Y) is the max of G_d at wide cells {X - km1, X} x {Y - km1, Y}
+// (level 0 over [c, c + h + km1) per axis), 0 outside. Input of pyramid_hex.
+__global__ void pyramid_widen(const uint8_t* __restrict__ level, int wnx, int wny, int km1,
+                              uint8_t* __restrict__ out, int mw, int mh) {
+  const int x = blockIdx.x * blockDim.x + threadIdx.x;
+  const int y = blockIdx.y;
+  if (x >= mw || y >= mh) return;
+  auto g = [&](int a, int b) -> uint32_t {
+    return (a >= 0 && b >= 0 && a < wnx && b < wny) ? level[static_cast<size_t>(b) * wnx + a] : 0u;
+  };
+  const int a = x - km1, b = y - km1;
+  out[static_cast<size_t>(y) * mw + x] =
+      static_cast<uint8_t>(max(max(g(a, b), g(a + km1, b)), max(g(a, b + km1), g(a + km1, b + km1))));
+}
+
+// Hex layout of level d (h = 2^d, search kernel v5): the 16-byte entry for
+// hex cell (X', Y'), X' < qw = mw + 3h, packs the 16 grandchildren values of a
+// level-(d + 2) node whose child (0,0) sits at M-wide cell (X, Y) =
+// (X' - 3h, Y' - 3h): dword a, byte b = M(X + a h, Y + b h); 0 outside.
+// Polyphase with period P = 4h: plane (X' mod P, Y' mod P), entry
+// (X' / P, Y' / P), so sibling nodes' lookups of one point are adjacent
+// entries.
+__global__ void pyramid_hex(const uint8_t* __restrict__ mlev, int mw, int mh, int log_h,
+                            uint4* __restrict__ out, int qw, int qh, int pws, int pph, int total) {
+  const int o = blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= total) return;
+  const int h = 1 << log_h;
+  const int s = log_h + 2, p = 4 * h;
+  const int ps = pws * pph;
+  const int pi = o / ps, k = o - pi * ps;
+  const int fx = pi & (p - 1), fy = pi >> s;
+  const int ky = k / pws, kx = k - ky * pws;
+  const int xq = (kx << s) + fx, yq = (ky << s) + fy;
+  uint4 v = make_uint4(0u, 0u, 0u, 0u);
+  if (xq < qw && yq < qh) {
+    const int X = xq - 3 * h, Y = yq - 3 * h;
+    auto m = [&](int a, int b) -> uint32_t {
+      return (a >= 0 && b >= 0 && a < mw && b < mh) ? mlev[static_cast<size_t>(b) * mw + a] : 0u;
+    };
+    uint32_t w[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      const int xa = X + a * h;
+      w[a] = m(xa, Y) | (m(xa, Y + h) << 8) | (m(xa, Y + 2 * h) << 16) | (m(xa, Y + 3 * h) << 24);
+    }
+    v = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+  out[o] = v;
+}
+
 // ---------------------------------------------------------------- K2-K4 v4 -
 //
 // A workgroup (4 waves) searches a chunk of R rotations of one pair at once.
@@ -603,9 +654,19 @@ __global__ void pyramid_quad(const uint8_t* __restrict__ level, int wnx, int wny
 constexpr int kMaxRotChunk = 16;
 constexpr int kLists = kMaxClusterShift + 1;
 
+// kKids: children sums per node, 4 (quad batches only, v4) or 16 (v5: hex
+// batches, and the virtual roots' quad batches in the first 4 columns).
+template <int kKids>
 struct V4Shared {
-  uint2 stack[kStack2];  // w0: xo | yo << 16; w1: sum | rot << 22 | level << 27
-  int part[kBatchNodes][4];  // children sums, accumulated by the 4 waves (LDS atomics)
+  // LDS part of the DFS stack (v5: half, so its 16-child sums fit the same
+  // LDS budget as v4's); the rest spills to global memory.
+  static constexpr int kStackLds = kKids == 16 ? kStack2 / 2 : kStack2;
+  static constexpr int kStackCapacity = kStackLds + kSpill2;
+  uint2 stack[kStackLds];  // w0: xo | yo << 16; w1: sum | rot << 22 | level << 27
+  int part[kBatchNodes][kKids];  // children sums, accumulated by the 4 waves (LDS atomics)
+  int batch_hex;                 // the batch's nodes score 16 grandchildren (v5)
+  int head;                      // FIFO: LDS ring position of the oldest entry
+  int ovf;                       // FIFO: entries in the global overflow stack
   int list_off[kMaxRotChunk][kLists];  // entry list (rotation, cluster shift): first entry
   int list_len[kMaxRotChunk][kLists];  // and length; a list that did not fit aliases a finer one
   int node_xo[kBatchNodes], node_yo[kBatchNodes], node_rot[kBatchNodes], node_level[kBatchNodes];
@@ -628,21 +689,24 @@ struct V4Shared {
   unsigned long long lv_batches[kMaxLevels];
 };
 
-// The DFS stack: entries [0, kStack2) in LDS, [kStack2, kStack2 + kSpill2)
+// The DFS stack: entries [0, kStackLds) in LDS, [kStackLds, kStackLds + kSpill2)
 // in the workgroup's spill region (global memory; the workgroup's own waves
 // write and read it, ordered by the __syncthreads between phases).
-__device__ __forceinline__ uint2 StackGet(const V4Shared& sh, const uint2* spill, int i) {
-  return i < kStack2 ? sh.stack[i] : spill[i - kStack2];
+template <typename Shared>
+__device__ __forceinline__ uint2 StackGet(const Shared& sh, const uint2* spill, int i) {
+  return i < Shared::kStackLds ? sh.stack[i] : spill[i - Shared::kStackLds];
 }
-__device__ __forceinline__ void StackPut(V4Shared& sh, uint2* spill, int i, uint2 v) {
-  if (i < kStack2) sh.stack[i] = v; else spill[i - kStack2] = v;
+template <typename Shared>
+__device__ __forceinline__ void StackPut(Shared& sh, uint2* spill, int i, uint2 v) {
+  if (i < Shared::kStackLds) sh.stack[i] = v; else spill[i - Shared::kStackLds] = v;
 }
 
 // Scores the children of the batch's nodes: lane (node, group) walks entries
 // g, g + groups, ... of the node's list (cells, counts). A child's sum is
 // sum_k cnt[k] * value over the list: the reference's per-point sum
 // regrouped at level 0, an upper bound of it at coarser levels.
-__device__ __forceinline__ void V4Score(V4Shared& sh, const uint32_t* cells, const uint8_t* cnts,
+template <typename Shared>
+__device__ __forceinline__ void V4Score(Shared& sh, const uint32_t* cells, const uint8_t* cnts,
                                         const SubmapDesc& sm) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nodes = Uniform(sh.nodes);
@@ -726,6 +790,92 @@ __device__ __forceinline__ void V4Score(V4Shared& sh, const uint32_t* cells, con
   }
 }
 
+// Hex batches (v5): a node at level L scores its 16 grandchildren at level
+// c = L - 2, (xo + a h, yo + b h), a, b in 0..3, h = 2^c, over the list of
+// level c's cluster size, with ONE 16-byte load per entry from level c's hex
+// plane (dword a, byte b). The intermediate level's pruning is skipped: its
+// bounds are only ever >= the grandchildren's, so the search still visits
+// every leaf that can reach the best sum.
+template <typename Shared>
+__device__ __forceinline__ void V4ScoreHex(Shared& sh, const uint32_t* cells, const uint8_t* cnts,
+                                           const SubmapDesc& sm) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nodes = Uniform(sh.nodes);
+  const int groups = 64 / nodes;
+  const int node = lane & (nodes - 1);
+  const int g = lane / nodes;
+  const int level = sh.node_level[node] - 2;
+  const int* L = sh.lv[level];
+  const int qw = L[0], qh = L[1], qoff = L[2], pws16 = L[3], ps16 = L[4];
+  const int sft = level + 2, pmask = (4 << level) - 1;
+  const __amdgpu_buffer_rsrc_t rsrc = LevelRsrc(sm.pyramid_base, Uniform(sm.pyramid_bytes));
+  const int off = sh.node_off[node], len = sh.node_len[node];
+  const uint32_t* P = cells + off;
+  const uint8_t* Cn = cnts + off;
+  const int cx = sh.node_xo[node] + L[5];
+  const int cy = sh.node_yo[node] + L[5];
+  const int blen = Uniform(sh.batch_len);
+  const int quarter = (blen + kWaves - 1) / kWaves;
+  const int s = Uniform(min(blen, wave * quarter)), e = Uniform(min(blen, wave * quarter + quarter));
+  constexpr int kOOB = 0x7ffffff0;
+  constexpr int U = 4;
+  uint32_t acc[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) acc[j] = 0u;
+  auto address = [&](uint32_t p, bool in) {
+    const int X = static_cast<int16_t>(p & 0xffff) + cx;
+    const int Y = (static_cast<int>(p) >> 16) + cy;
+    const bool valid = in && static_cast<unsigned>(X) < static_cast<unsigned>(qw) &&
+                       static_cast<unsigned>(Y) < static_cast<unsigned>(qh);
+    const int a = __umul24((((Y & pmask) << sft) | (X & pmask)), ps16) + qoff;
+    const int b = __umul24(Y >> sft, pws16) + a;
+    return valid ? ((X >> sft) << 4) + b : kOOB;
+  };
+  // Child (a, b) accumulates byte b of dword a times the entry's count.
+  auto accumulate = [&](const decltype(__builtin_amdgcn_raw_buffer_load_b128(rsrc, 0, 0, 0))& v,
+                        uint32_t c) {
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+        acc[4 * a + b] = __builtin_amdgcn_udot4(v[a], c << (8 * b), acc[4 * a + b], false);
+    }
+  };
+  int i = s;
+  for (; i + U * groups <= e; i += U * groups) {
+    int ad[U];
+    uint32_t c[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int idx = i + u * groups + g;
+      const bool in = idx < len;
+      const int j = in ? idx : 0;
+      ad[u] = address(P[j], in);
+      c[u] = in ? Cn[j] : 0u;
+    }
+    decltype(__builtin_amdgcn_raw_buffer_load_b128(rsrc, 0, 0, 0)) v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, ad[u], 0, 0);
+#pragma unroll
+    for (int u = 0; u < U; ++u) accumulate(v[u], c[u]);
+  }
+  for (; i < e; i += groups) {
+    const int idx = i + g;
+    const bool in = idx < e && idx < len;
+    const int j = in ? idx : 0;
+    const auto vv = __builtin_amdgcn_raw_buffer_load_b128(rsrc, address(P[j], in), 0, 0);
+    accumulate(vv, in ? Cn[j] : 0u);
+  }
+  for (int m = nodes; m < 64; m <<= 1) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc[j] += __shfl_xor(acc[j], m, 64);
+  }
+  if (lane < nodes) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) atomicAdd(&sh.part[lane][j], static_cast<int>(acc[j]));
+  }
+}
+
 // Cluster key of a packed cell (int16 x | int16 y << 16): both coordinates
 // rounded down to a multiple of 2^shift.
 __device__ __forceinline__ uint32_t ClusterKey(uint32_t p, int shift) {
@@ -798,6 +948,15 @@ __device__ __forceinline__ uint32_t ClusterMask(int sl) {
   return h | (h << 16);
 }
 
+// kHex = false: v4 (every node scores its 4 children from the quad planes).
+// kHex = true: v5 (nodes of the levels in SubmapDesc::hex_mask score their
+// 16 grandchildren from hex planes, the others their 4 children from quad
+// planes; a batch holds one kind).
+//
+// kFifo = false: the stack is LIFO with the deepest level on top (depth-first,
+// early leaves). kFifo = true: a FIFO ring (level by level: batches fill up
+// with the whole frontier of a level; leaves come last).
+template <bool kHex, bool kFifo>
 __global__ void __launch_bounds__(kSearchThreads) __attribute__((amdgpu_waves_per_eu(5)))
 fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
                  const PairDesc* __restrict__ pairs,
@@ -812,13 +971,15 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
   // Dynamic LDS: cells, then counts, each rc * (npad + capc) entries. Rotation
   // r's raw cells (then its k = 1 run list, in place) at r * npad; its
   // cluster lists packed in [rc * npad + r * capc, + capc).
+  constexpr int kKids = kHex ? 16 : 4;
   extern __shared__ __align__(16) uint32_t cells[];
-  __shared__ V4Shared sh;
+  __shared__ V4Shared<kKids> sh;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int rc = queues.rot_chunk;
   uint8_t* cnts = reinterpret_cast<uint8_t*>(cells + rc * (npad + capc));
   uint2* spill = spill_base + static_cast<size_t>(blockIdx.x) * kSpill2;
-  for (int k = tid; k < kBatchNodes * 4; k += kSearchThreads) sh.part[k >> 2][k & 3] = 0;
+  for (int k = tid; k < kBatchNodes * kKids; k += kSearchThreads) sh.part[k / kKids][k % kKids] = 0;
+  if (tid == 0) sh.batch_hex = 0;
   if (tid == 0) sh.high_water = 0;
   unsigned long long local_cands = 0, local_lookups = 0;
 #ifdef CSM_KPROF
@@ -861,6 +1022,7 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
     const int nrot = min(rc, pd.num_scans - rot0);
     const int top_level = sm.levels - 1;
     const int step = 1 << top_level;
+    const uint32_t hex_mask = kHex ? static_cast<uint32_t>(Uniform(sm.hex_mask)) : 0u;
 
     // ---- K2: discretize the chunk's rotated scans into LDS ----------------
 #ifdef CSM_KPROF
@@ -873,8 +1035,8 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
       sh.lv[d][0] = sm.quad_w[d];
       sh.lv[d][1] = sm.quad_h[d];
       sh.lv[d][2] = sm.quad_off[d];
-      sh.lv[d][3] = sm.quad_pws[d] * 4;
-      sh.lv[d][4] = sm.quad_pws[d] * sm.quad_pph[d] * 4;
+      sh.lv[d][3] = sm.quad_pws[d] * sm.quad_es[d];
+      sh.lv[d][4] = sm.quad_pws[d] * sm.quad_pph[d] * sm.quad_es[d];
       sh.lv[d][5] = sm.quad_bias[d];
       sh.lv[d][6] = sm.cshift[d];
     }
@@ -911,6 +1073,9 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
       }
     }
     if (range_error) sh.range_error = 1;
+#ifdef CSM_DBG
+    if (range_error) printf("discretize range\n");
+#endif
     __syncthreads();
     // ---- Entry lists: k = 1 is the discretized scan itself (one point per
     // entry; it scores the leaves only), k = 2, 4, 8 are run lists of cluster
@@ -1010,6 +1175,8 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
       for (int r = 0; r < nrot; ++r) sh.root_prefix[r + 1] += sh.root_prefix[r];
       sh.vnext = 0;
       sh.sp = 0;
+      sh.ovf = 0;
+      sh.head = 0;
       sh.best = LoadBest(pair_best);
       sh.batch_no = 0;
       sh.nodes = 0;
@@ -1031,19 +1198,24 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
         // (a) Combine the previous batch: prune, record leaves, push survivors.
         // 16 nodes' children per pass (one per lane); the waves take the
         // passes in parallel and claim stack space atomically.
+        // Hex batches: 4 nodes' 16 grandchildren per pass, child c = (a, b)
+        // at (xo + a h, yo + b h), a = c >> 2, b = c & 3.
         const int pn = sh.nodes;
-        for (int pass = wave; pass * 16 < pn; pass += kWaves) {
-          const int nd = pass * 16 + (lane >> 2), c = lane & 3;
+        const bool hexb = kHex && sh.batch_hex;
+        const int lk = hexb ? 4 : 2;  // log2 children per node
+        const int per_pass = 64 >> lk;
+        for (int pass = wave; pass * per_pass < pn; pass += kWaves) {
+          const int nd = pass * per_pass + (lane >> lk), c = lane & ((1 << lk) - 1);
           int sum = 0, xo = 0, yo = 0, r = 0, clvl = 0;
           bool exists = false;
           if (nd < pn) {
-            clvl = sh.node_level[nd] - 1;
+            clvl = sh.node_level[nd] - (hexb ? 2 : 1);
             const int h = 1 << clvl;
             sum = sh.part[nd][c];
             sh.part[nd][c] = 0;
             r = sh.node_rot[nd];
-            xo = sh.node_xo[nd] + ((c & 2) ? h : 0);
-            yo = sh.node_yo[nd] + ((c & 1) ? h : 0);
+            xo = sh.node_xo[nd] + (c >> (lk >> 1)) * h;
+            yo = sh.node_yo[nd] + (c & ((1 << (lk >> 1)) - 1)) * h;
             exists = xo <= sh.bounds[r][1] && yo <= sh.bounds[r][3];
           }
           const uint64_t cur = sh.best;
@@ -1052,8 +1224,12 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
           // Leaves (child level 0) update the incumbent.
           uint64_t key = 0;
           if (keep && clvl == 0) {
-            if (xo < -kOffsetLimit || xo > kOffsetLimit || yo < -kOffsetLimit || yo > kOffsetLimit)
+            if (xo < -kOffsetLimit || xo > kOffsetLimit || yo < -kOffsetLimit || yo > kOffsetLimit) {
               atomicOr(&status[pair_index], kStatusRange);
+#ifdef CSM_DBG
+              printf("leaf range xo %d yo %d\n", xo, yo);
+#endif
+            }
             else
               key = PackLeafKey(sum, rot0 + r, xo, yo);
           }
@@ -1075,7 +1251,8 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
           const unsigned long long pm = __ballot(push);
           const int kept = __popcll(pm);
           int rank = 0;
-          for (unsigned long long rem = pm; rem;) {
+          if (kFifo) rank = __popcll(pm & ((1ull << lane) - 1));
+          for (unsigned long long rem = kFifo ? 0ull : pm; rem;) {
             const int l0 = __builtin_amdgcn_readlane(clvl, static_cast<int>(__ffsll(static_cast<long long>(rem))) - 1);
             const unsigned long long same = __ballot(push && clvl == l0);
             if (push) rank += clvl > l0 ? __popcll(same) : (clvl == l0 ? __popcll(same & ((1ull << lane) - 1)) : 0);
@@ -1087,25 +1264,49 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
             atomicMax(&sh.high_water, sp + kept);
           }
           sp = __shfl(sp, 0, 64);
-          // Entries past the LDS stack go to this workgroup's spill region in
-          // global memory (StackPut); past that the pair is flagged.
-          if (push && sp + kept <= kStack2 + kSpill2)
-            StackPut(sh, spill, sp + kept - 1 - rank, make_uint2(
-                (static_cast<uint32_t>(xo) & 0xffff) | (static_cast<uint32_t>(yo) << 16),
-                static_cast<uint32_t>(sum) | (static_cast<uint32_t>(r) << 22) |
-                    (static_cast<uint32_t>(clvl) << 27)));
-          if (lane == 0 && sp + kept > kStack2 + kSpill2) atomicOr(&status[pair_index], kStatusRange);
+          const uint2 entry = make_uint2(
+              (static_cast<uint32_t>(xo) & 0xffff) | (static_cast<uint32_t>(yo) << 16),
+              static_cast<uint32_t>(sum) | (static_cast<uint32_t>(r) << 22) |
+                  (static_cast<uint32_t>(clvl) << 27));
+          if (kFifo) {
+            // Ring slots past the LDS ring's capacity go to the workgroup's
+            // overflow stack in global memory (popped when the ring is
+            // empty); past that the pair is flagged.
+            constexpr int kRing = decltype(sh)::kStackLds;
+            const int slot = sp + rank;
+            if (push && slot < kRing) sh.stack[(sh.head + slot) & (kRing - 1)] = entry;
+            const bool over = push && slot >= kRing;
+            const unsigned long long om = __ballot(over);
+            if (om) {
+              int ob = 0;
+              if (lane == 0) ob = atomicAdd(&sh.ovf, __popcll(om));
+              ob = __shfl(ob, 0, 64) + __popcll(om & ((1ull << lane) - 1));
+              if (over && ob < kSpill2) spill[ob] = entry;
+              if (over && ob >= kSpill2) atomicOr(&status[pair_index], kStatusRange);
+#ifdef CSM_DBG
+              if (over && ob >= kSpill2 && (lane == 0 || ob == kSpill2)) printf("ovf overflow ob %d sp %d kept %d head %d\n", ob, sp, kept, sh.head);
+#endif
+            }
+          } else {
+            // Entries past the LDS stack go to this workgroup's spill region
+            // in global memory (StackPut); past that the pair is flagged.
+            if (push && sp + kept <= sh.kStackCapacity) StackPut(sh, spill, sp + kept - 1 - rank, entry);
+            if (lane == 0 && sp + kept > sh.kStackCapacity) atomicOr(&status[pair_index], kStatusRange);
+          }
         }
       }
       __syncthreads();
       if (wave == 0) {
         // (b) Refill roots when the stack is empty. (An overflowed stack has
         // flagged the pair; its result is discarded.)
-        int sp = min(sh.sp, kStack2 + kSpill2);
-        if (sp == 0 && sh.vnext < vtotal) {
+        constexpr int kRing = decltype(sh)::kStackLds;
+        int sp = min(sh.sp, kFifo ? kRing : sh.kStackCapacity);
+        int ovf = kFifo ? min(sh.ovf, kSpill2) : 0;
+        if (sp == 0 && ovf == 0 && sh.vnext < vtotal) {
           const int v0 = sh.vnext, vc = min(kRootChunk, vtotal - v0);
+          if (kFifo && lane == 0) sh.head = 0;  // empty ring: restart at slot 0
           for (int k = lane; k < vc; k += 64) {
-            const int v = v0 + vc - 1 - k;  // lowest root index on top
+            const int v = kFifo ? v0 + k : v0 + vc - 1 - k;  // lowest root index first
             int r = 0;
             while (sh.root_prefix[r + 1] <= v) ++r;
             const int lv = v - sh.root_prefix[r];
@@ -1125,12 +1326,35 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
         }
         const uint32_t cur_sum = static_cast<uint32_t>(sh.best >> kSumShift);
         int nodes = 0, blen = 0, bent = 0;
-        if (sp > 0) {
+        if (sp > 0 || ovf > 0) {
           // Up to 64 entries from the top (any level); expand a power of two
-          // of the unpruned ones, discard pruned ones passed over.
+          // of the unpruned ones, discard pruned ones passed over. FIFO: from
+          // the overflow stack's top while it holds entries (the deepest ones:
+          // depth-first until it drains, which bounds the frontier the way
+          // the LIFO order does), else from the ring's head.
           uint2 ent = make_uint2(0, 0);
-          const bool in = lane < kBatchNodes && lane < sp;
-          if (in) ent = StackGet(sh, spill, sp - 1 - lane);
+          const bool from_ring = !kFifo || ovf == 0;
+          bool in = lane < kBatchNodes && lane < (from_ring ? sp : ovf);
+          const int head = kFifo ? Uniform(sh.head) : 0;
+          if (in) {
+            if (!kFifo)
+              ent = StackGet(sh, spill, sp - 1 - lane);
+            else if (from_ring)
+              ent = sh.stack[(head + lane) & (kRing - 1)];
+            else
+              ent = spill[ovf - 1 - lane];
+          }
+          bool hexb = false;
+          if (kHex) {
+            // One kind per batch: the entries down to the first of the other
+            // kind (quad vs hex node level, SubmapDesc::hex_mask) than the top
+            // entry.
+            const bool hx = (hex_mask >> (ent.y >> 27)) & 1;
+            const bool top_hx = __builtin_amdgcn_readlane(static_cast<int>(hx), 0) != 0;
+            const unsigned long long other = __ballot(in && hx != top_hx);
+            if (other) in = in && lane < static_cast<int>(__ffsll(static_cast<long long>(other))) - 1;
+            hexb = top_hx;
+          }
           const unsigned long long inm = __ballot(in);
           const bool expandable = in && (ent.y & 0x3fffff) >= cur_sum;
           const unsigned long long em = __ballot(expandable);
@@ -1145,7 +1369,7 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
             int len = 0;
             if (expandable && lane < take) {
               const int r = (ent.y >> 22) & 0x1f, lvl = static_cast<int>(ent.y >> 27);
-              const int sl = sh.lv[lvl - 1][6];
+              const int sl = sh.lv[lvl - (hexb ? 2 : 1)][6];
               len = sh.list_len[r][sl];
               sh.node_xo[rank] = static_cast<int16_t>(ent.x & 0xffff);
               sh.node_yo[rank] = static_cast<int>(ent.x) >> 16;
@@ -1157,14 +1381,17 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
             blen = DppMax(len);
             bent = DppSum(len);
           }
-          sp -= take;
+          if (from_ring) sp -= take; else ovf -= take;
+          if (kHex && lane == 0) sh.batch_hex = hexb ? 1 : 0;
+          if (kFifo && from_ring && lane == 0) sh.head = (head + take) & (kRing - 1);
         }
         if (lane == 0) {
           sh.sp = sp;
           sh.nodes = nodes;
           sh.batch_len = blen;
           sh.batch_entries = bent;
-          sh.done = (nodes == 0 && sp == 0 && sh.vnext >= vtotal) ? 1 : 0;
+          if (kFifo) sh.ovf = ovf;
+          sh.done = (nodes == 0 && sp == 0 && ovf == 0 && sh.vnext >= vtotal) ? 1 : 0;
         }
       }
       __syncthreads();
@@ -1179,12 +1406,19 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
       const int done = Uniform(sh.done);
       if (done) break;
       if (nodes > 0) {
-        V4Score(sh, cells, cnts, sm);
-        local_cands += 4 * nodes;
-        local_lookups += 4ull * static_cast<unsigned>(Uniform(sh.batch_entries));
+        // Algorithmic bytes: 4 per quad-dword gather, 16 per hex gather.
+        const bool hexb = kHex && Uniform(sh.batch_hex);
+        if (hexb)
+          V4ScoreHex(sh, cells, cnts, sm);
+        else
+          V4Score(sh, cells, cnts, sm);
+        const int kids = hexb ? 16 : 4;
+        local_cands += kids * nodes;
+        local_lookups += static_cast<unsigned long long>(kids) *
+                         static_cast<unsigned>(Uniform(sh.batch_entries));
         if (tid < nodes) {
-          const int cl = sh.node_level[tid] - 1;
-          atomicAdd(&sh.lv_cands[cl], 4ull);
+          const int cl = sh.node_level[tid] - (hexb ? 2 : 1);
+          atomicAdd(&sh.lv_cands[cl], static_cast<unsigned long long>(kids));
           if (tid == 0) atomicAdd(&sh.lv_batches[cl], 1ull);
         }
       }
@@ -1260,9 +1494,27 @@ hipError_t LaunchFast2dSearchV2(int grid, size_t dyn_lds, hipStream_t st, const 
                                 const PairDesc* pairs, const float* points, const float2* rot_table,
                                 const WorkQueues2& queues, unsigned long long* counters,
                                 uint64_t* best, int32_t* status, unsigned long long* stats,
-                                uint2* spill, int npad, int capc) {
-  hipLaunchKernelGGL(fast2d_search_v4, dim3(grid), dim3(kSearchThreads), dyn_lds, st, submaps, pairs,
-                     points, rot_table, queues, counters, best, status, stats, spill, npad, capc);
+                                uint2* spill, int npad, int capc, bool hex, bool fifo) {
+#define CSM_LAUNCH_V4(H, F)                                                                        \
+  hipLaunchKernelGGL((fast2d_search_v4<H, F>), dim3(grid), dim3(kSearchThreads), dyn_lds, st,     \
+                     submaps, pairs, points, rot_table, queues, counters, best, status, stats,     \
+                     spill, npad, capc)
+  if (hex && fifo) CSM_LAUNCH_V4(true, true);
+  else if (hex) CSM_LAUNCH_V4(true, false);
+  else if (fifo) CSM_LAUNCH_V4(false, true);
+  else CSM_LAUNCH_V4(false, false);
+#undef CSM_LAUNCH_V4
+  return hipGetLastError();
+}
+
+hipError_t LaunchPyramidHex(const uint8_t* level, int wnx, int wny, int log_h, int km1,
+                            uint8_t* scratch, uint32_t* out, int qw, int qh, int pws, int pph,
+                            int total, hipStream_t st) {
+  const int mw = wnx + km1, mh = wny + km1;
+  hipLaunchKernelGGL(pyramid_widen, dim3((mw + 255) / 256, mh), dim3(256), 0, st, level, wnx, wny, km1,
+                     scratch, mw, mh);
+  hipLaunchKernelGGL(pyramid_hex, dim3((total + 255) / 256), dim3(256), 0, st, scratch, mw, mh, log_h,
+                     reinterpret_cast<uint4*>(out), qw, qh, pws, pph, total);
   return hipGetLastError();
 }
 

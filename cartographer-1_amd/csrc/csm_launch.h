@@ -23,7 +23,12 @@ hipError_t LaunchFast2dSearchV2(int grid, size_t dyn_lds, hipStream_t st, const 
                                 const PairDesc* pairs, const float* points, const float2* rot_table,
                                 const WorkQueues2& queues, unsigned long long* counters,
                                 uint64_t* best, int32_t* status, unsigned long long* stats,
-                                uint2* spill, int npad, int capc);
+                                uint2* spill, int npad, int capc, bool hex, bool fifo);
+// Widened level (into scratch, (wnx + km1) x (wny + km1) bytes), then its hex
+// plane (total = 16-byte entries).
+hipError_t LaunchPyramidHex(const uint8_t* level, int wnx, int wny, int log_h, int km1,
+                            uint8_t* scratch, uint32_t* out, int qw, int qh, int pws, int pph,
+                            int total, hipStream_t st);
 
 
 hipError_t LaunchCellsToProbability(const uint16_t* cells, const float* ptab, float* out, int n,

@@ -21,6 +21,7 @@
 #define CSM_ORACLE_H_
 
 #include <cstdint>
+#include <array>
 #include <vector>
 
 namespace oracle {
@@ -275,6 +276,14 @@ class FastCorrelativeScanMatcher2D {
   bool MatchFullSubmap(const PointCloud& cloud, float min_score, float* score,
                        Rigid2d* pose, MatchStats2D* stats = nullptr) const;
   const PrecomputationGrid2D& Level(int i) const { return grids_[i]; }
+  // Test-only (tie statistics): every leaf {scan_index, x_off, y_off} whose
+  // score equals the maximum leaf score, when that maximum beats min_score
+  // (the set the reference's DFS picks its first-visited member from), and
+  // the reference's own pick in *picked. Empty if nothing beats min_score.
+  std::vector<std::array<int, 3>> TiedMaxLeaves(bool full_submap, const Rigid2d& initial,
+                                                const PointCloud& cloud, float min_score,
+                                                size_t max_out,
+                                                std::array<int, 3>* picked) const;
   int max_depth() const { return static_cast<int>(grids_.size()) - 1; }
   const MapLimits& limits() const { return limits_; }
 
@@ -289,6 +298,9 @@ class FastCorrelativeScanMatcher2D {
                        const std::vector<DiscreteScan2D>& scans,
                        std::vector<Candidate2D>* candidates,
                        MatchStats2D* stats) const;
+  void CollectTies(const std::vector<DiscreteScan2D>& scans, const SearchParameters& sp,
+                   const std::vector<Candidate2D>& candidates, int depth, float best,
+                   size_t max_out, std::vector<std::array<int, 3>>* out) const;
   Candidate2D BranchAndBound(const std::vector<DiscreteScan2D>& scans,
                              const SearchParameters& sp,
                              const std::vector<Candidate2D>& candidates,

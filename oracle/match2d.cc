@@ -337,6 +337,69 @@ Candidate2D FastCorrelativeScanMatcher2D::BranchAndBound(
   return best;
 }
 
+// Test-only tie enumeration (not part of the reference): the same window,
+// discretization and lowest-resolution candidates as MatchWithSearchParameters
+// (fast_correlative_scan_matcher_2d.cc:227-262), BranchAndBound for the
+// maximum, then a second walk that keeps every node whose bound reaches that
+// maximum and collects the leaves scoring exactly it. Equal float scores are
+// equal integer sums (ToScore is strictly monotone, SURVEY §8a hazard 13).
+std::vector<std::array<int, 3>> FastCorrelativeScanMatcher2D::TiedMaxLeaves(
+    bool full_submap, const Rigid2d& initial_in, const PointCloud& cloud,
+    float min_score, size_t max_out, std::array<int, 3>* picked) const {
+  Rigid2d initial = initial_in;
+  double lin = options_.linear_search_window, ang = options_.angular_search_window;
+  if (full_submap) {
+    lin = 1e6 * limits_.resolution;
+    ang = M_PI;
+    const double half = 0.5 * limits_.resolution;
+    initial.tx = limits_.max_x - half * limits_.cells.num_y_cells;
+    initial.ty = limits_.max_y - half * limits_.cells.num_x_cells;
+    initial.angle = 0.;
+  }
+  SearchParameters sp(lin, ang, cloud, limits_.resolution);
+  Rigid3f pre;
+  pre.q = QuatFromAngleAxisF(static_cast<float>(initial.angle), 0.f, 0.f, 1.f);
+  const std::vector<PointCloud> rotated_scans =
+      GenerateRotatedScans(TransformPointCloud(cloud, pre), sp);
+  const std::vector<DiscreteScan2D> discrete =
+      DiscretizeScans(limits_, rotated_scans, static_cast<float>(initial.tx),
+                      static_cast<float>(initial.ty));
+  sp.ShrinkToFit(discrete, limits_.cells);
+  std::vector<Candidate2D> lowest = GenerateLowestResolutionCandidates(sp);
+  ScoreCandidates(grids_[max_depth()], discrete, &lowest, nullptr);
+  const Candidate2D best = BranchAndBound(discrete, sp, lowest, max_depth(), min_score, nullptr);
+  std::vector<std::array<int, 3>> out;
+  if (!(best.score > min_score)) return out;
+  *picked = {best.scan_index, best.x_index_offset, best.y_index_offset};
+  CollectTies(discrete, sp, lowest, max_depth(), best.score, max_out, &out);
+  return out;
+}
+
+void FastCorrelativeScanMatcher2D::CollectTies(
+    const std::vector<DiscreteScan2D>& scans, const SearchParameters& sp,
+    const std::vector<Candidate2D>& candidates, int depth, float best, size_t max_out,
+    std::vector<std::array<int, 3>>* out) const {
+  for (const Candidate2D& c : candidates) {
+    if (c.score < best || out->size() >= max_out) break;  // sorted, descending
+    if (depth == 0) {
+      out->push_back({c.scan_index, c.x_index_offset, c.y_index_offset});
+      continue;
+    }
+    std::vector<Candidate2D> children;
+    const LinearBounds& b = sp.linear_bounds[c.scan_index];
+    const int half = 1 << (depth - 1);
+    for (int dx : {0, half}) {
+      if (c.x_index_offset + dx > b.max_x) break;
+      for (int dy : {0, half}) {
+        if (c.y_index_offset + dy > b.max_y) break;
+        children.emplace_back(c.scan_index, c.x_index_offset + dx, c.y_index_offset + dy, sp);
+      }
+    }
+    ScoreCandidates(grids_[depth - 1], scans, &children, nullptr);
+    CollectTies(scans, sp, children, depth - 1, best, max_out, out);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // real_time_correlative_scan_matcher_2d.cc:81-115
 std::vector<Candidate2D>

@@ -151,6 +151,28 @@ int32_t oracle_fast2d_score_candidate(void* h, int32_t full_submap,
   return 0;
 }
 
+// Tie statistics (tests/tools only): the leaves tied at the maximum score
+// (up to max_out, as scan, x_off, y_off triples) and the reference's pick.
+// Returns the number of tied leaves (0: no match above min_score).
+int32_t oracle_fast2d_tie_leaves(void* h, int32_t full_submap, const double* initial,
+                                 const float* xyz, int32_t n, float min_score,
+                                 int32_t max_out, int32_t* leaves, int32_t* picked) {
+  const auto* m = static_cast<FastCorrelativeScanMatcher2D*>(h);
+  Rigid2d init;
+  if (initial) {
+    init.tx = initial[0];
+    init.ty = initial[1];
+    init.angle = initial[2];
+  }
+  std::array<int, 3> pick{0, 0, 0};
+  const auto ties = m->TiedMaxLeaves(full_submap != 0, init, ToCloud(xyz, n), min_score,
+                                     static_cast<size_t>(max_out), &pick);
+  for (size_t i = 0; i < ties.size(); ++i)
+    for (int k = 0; k < 3; ++k) leaves[3 * i + k] = ties[i][k];
+  for (int k = 0; k < 3; ++k) picked[k] = pick[k];
+  return static_cast<int32_t>(ties.size());
+}
+
 // CPU baseline: pairs (submap index, node index) matched with
 // MatchFullSubmap on `threads` workers pulling pairs FIFO. Returns wall
 // seconds; matched[i] = 1 on success.

@@ -27,6 +27,7 @@ class Oracle:
             "oracle_fast2d_match": (I32, [VP, P(D), P(F), I32, F, P(F), P(D), P(I64)]),
             "oracle_fast2d_score_candidate": (I32, [VP, I32, P(D), D, D, P(F), I32, I32, I32,
                                                     I32, I32, P(I32), P(F)]),
+            "oracle_fast2d_tie_leaves": (I32, [VP, I32, P(D), P(F), I32, F, I32, P(I32), P(I32)]),
             "oracle_fast2d_match_pairs": (D, [P(VP), P(F), P(I64), P(I32), P(I32), I64, I32, F,
                                               P(F), P(D), P(I32), P(D)]),
             "oracle_rt2d_match": (D, [D, D, D, I32, I32, P(C.c_uint16), D, D, D, D, P(D), P(F),
@@ -216,6 +217,20 @@ class OracleFast2D:
         r = self.o.lib.oracle_fast2d_match(self.h, _p(init, D), _p(pts, F), len(pts), min_score,
                                            C.byref(score), _p(pose, D), _p(stats, I64))
         return r == 0, score.value, tuple(pose), stats
+
+    def tie_leaves(self, full_submap, initial, cloud, min_score, max_out=4096):
+        """Leaves tied at the maximum score as (scan, x_off, y_off) rows, and
+        the reference's pick among them (None, None if no match)."""
+        pts = np.ascontiguousarray(cloud, np.float32)
+        init = np.asarray(initial if initial is not None else (0, 0, 0), np.float64)
+        out = np.zeros((max_out, 3), np.int32)
+        pick = np.zeros(3, np.int32)
+        k = self.o.lib.oracle_fast2d_tie_leaves(self.h, 1 if full_submap else 0, _p(init, D),
+                                                _p(pts, F), len(pts), min_score, max_out,
+                                                _p(out, I32), _p(pick, I32))
+        if k == 0:
+            return None, None
+        return out[:k].copy(), tuple(int(v) for v in pick)
 
     def score_candidate(self, full_submap, initial, cloud, scan_index, x_off, y_off, depth=0):
         pts = np.ascontiguousarray(cloud, np.float32)

@@ -146,11 +146,26 @@ def world(csm):
     return csm.SyntheticWorld2D(num_nodes=64, num_submaps=8, decimate_to=200, seed=20250127)
 
 
-@pytest.fixture(params=["v2", "v1"])
+SEARCH_KERNELS = {"v5": {}, "v5-all-hex": {"CSM_SEARCH_KERNEL": "5"},
+                  "v5-mixed-lifo": {"CSM_HEX_LEVELS": "8,6,3", "CSM_SEARCH_ORDER": "lifo"},
+                  "v4": {"CSM_SEARCH_KERNEL": "4"},
+                  "v4-lifo": {"CSM_SEARCH_KERNEL": "4", "CSM_SEARCH_ORDER": "lifo"},
+                  "v1": {"CSM_SEARCH_KERNEL": "1"}}
+
+
+@pytest.fixture(params=list(SEARCH_KERNELS))
 def search_kernel(request, monkeypatch):
-    """Both search kernels: v2 (lanes = candidates, polyphase pyramid) and
-    v1 (lanes = points, row-major pyramid; used above ~10k points)."""
-    monkeypatch.setenv("CSM_SEARCH_KERNEL", request.param[1])
+    """Every search kernel and node order: v5 (the default: hex planes for the
+    top level and the one two below, quad planes elsewhere, FIFO node order),
+    v5 with every even level hex, hex levels mixed into quad ones under the
+    depth-first LIFO order, v4 (quad planes only) in both orders, and v1
+    (lanes = points, row-major pyramid; used above ~8k points). The plane
+    layout is fixed when a matcher is created, so the variables are set
+    before."""
+    for var in ("CSM_SEARCH_KERNEL", "CSM_HEX_LEVELS", "CSM_SEARCH_ORDER"):
+        monkeypatch.delenv(var, raising=False)
+    for var, val in SEARCH_KERNELS[request.param].items():
+        monkeypatch.setenv(var, val)
     return request.param
 
 
@@ -262,7 +277,7 @@ def _run_list_clouds(world):
     return [np.ascontiguousarray(c, np.float32) for c in clouds]
 
 
-def test_run_lists_parity(csm, oracle, world):
+def test_run_lists_parity(csm, oracle, world, search_kernel):
     """Run-list compaction (consecutive points in one cell scored once with
     their count) leaves every score and pose unchanged, through the batch path
     with ragged clouds in one batch."""
@@ -287,31 +302,3 @@ def test_run_lists_parity(csm, oracle, world):
         kinds.append(assert_fast_parity(oracle, om, limits, g.cells, gpu, ref, True,
                                         full_submap_center(limits, g.cells), c))
     assert kinds.count("nomatch") < len(kinds)
-
-
-@pytest.mark.parametrize("mode", ["0", "2"])
-def test_batch_selection_modes_parity(csm, oracle, world, mode, monkeypatch):
-    """The v4 kernel's other batch-selection modes (CSM_MIXED_LEVELS: 0 =
-    same-level runs from the stack top, 2 = one (rotation, level) group from
-    a 128-entry window, capped at kBatchNodes) keep parity with the oracle."""
-    monkeypatch.setenv("CSM_MIXED_LEVELS", mode)
-    opts = csm.FastCorrelativeScanMatcherOptions2D(7.0, math.radians(30), 7)
-    mats = [csm.FastCorrelativeScanMatcher2D(world.grid(s), opts) for s in range(8)]
-    scans = csm.ScanSet(None, packed=(world.points, world.offsets))
-    pairs_sn = [(s, int(world.submap_nodes[s])) for s in range(8)] + [(1, 3), (2, 40), (5, 17)]
-    pairs = csm.make_pairs([p[0] for p in pairs_sn], [p[1] for p in pairs_sn], 0.55)
-    res = csm.match_batch(mats, scans, pairs)
-    assert_search_ok(csm, res["status"])
-    matched = 0
-    for k, (s, n) in enumerate(pairs_sn):
-        g = world.grid(s)
-        limits = (g.resolution, g.max_x, g.max_y)
-        om = oracle.fast2d(limits, g.cells, 7.0, math.radians(30), 7)
-        cloud = world.cloud(n)
-        ref = om.match_full_submap(cloud, 0.55)
-        gpu = (res[k]["status"] == 0, float(res[k]["score"]),
-               (res[k]["x"], res[k]["y"], res[k]["theta"]))
-        assert_fast_parity(oracle, om, limits, g.cells, gpu, ref, True,
-                           full_submap_center(limits, g.cells), cloud)
-        matched += int(gpu[0])
-    assert matched >= 3

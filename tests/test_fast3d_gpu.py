@@ -203,6 +203,25 @@ RT_CLOUD = np.array([[-3, 2, 0], [-4, 2, 0], [-5, 2, 0], [-6, 2, 0], [-6, 3, 1],
                      [-7, 3, 1]], np.float32)
 
 
+# Every RTCSM3D kernel the host can select (host3d.cc RunRt3d): v5 (column
+# gathers, the default for 3-, 5- and 7-step z columns), v4 (rotation lanes,
+# other windows), v3 / v2 (bricks too large for v4's / v3's float byte
+# offsets) and v1 (bricks past v2's 2^29 cells). The variables force the
+# fallbacks on small inputs; the last two tests reach v4 and v2 unforced.
+RT3D_KERNELS = {"v5": None, "v4": "CSM_RT3D_V4", "v3": "CSM_RT3D_V3", "v2": "CSM_RT3D_V2",
+                "v1": "CSM_RT3D_V1"}
+
+
+@pytest.fixture(params=list(RT3D_KERNELS))
+def rt3d_kernel(request, monkeypatch):
+    for var in RT3D_KERNELS.values():
+        if var:
+            monkeypatch.delenv(var, raising=False)
+    if RT3D_KERNELS[request.param]:
+        monkeypatch.setenv(RT3D_KERNELS[request.param], "1")
+    return request.param
+
+
 @pytest.mark.parametrize("initial", [
     ((-1.0, 0.0, 0.0), (1, 0, 0, 0)),        # PerfectEstimate
     ((-0.8, 0.0, 0.0), (1, 0, 0, 0)),        # AlongX
@@ -213,7 +232,7 @@ RT_CLOUD = np.array([[-3, 2, 0], [-4, 2, 0], [-5, 2, 0], [-6, 2, 0], [-6, 3, 1],
     ((-1.0, 0.0, 0.0), (math.cos(0.4 / 180 * math.pi), 0, math.sin(0.4 / 180 * math.pi),
                         math.sin(0.4 / 180 * math.pi))),  # unnormalized axis (0, 1, 1)
 ])
-def test_rt3d_reference_cases(csm, oracle, initial):
+def test_rt3d_reference_cases(csm, oracle, initial, rt3d_kernel):
     """real_time_correlative_scan_matcher_3d_test.cc:34-117 on the GPU."""
     og = oracle.hybrid_grid(0.1)
     for p in RT_CLOUD:
@@ -229,7 +248,7 @@ def test_rt3d_reference_cases(csm, oracle, initial):
     assert np.allclose(pose[0], (-1, 0, 0), atol=1e-3)
 
 
-def test_rt3d_dense_scene(csm, oracle):
+def test_rt3d_dense_scene(csm, oracle, rt3d_kernel):
     """A few hundred points, a 0.1 m grid built by the 3D inserter, and a
     +-0.2 m / +-2 deg window: many candidates, every one scored in float in
     the reference order."""
@@ -248,7 +267,7 @@ def test_rt3d_dense_scene(csm, oracle):
 
 
 @pytest.mark.parametrize("window", [0.1, 0.2, 0.3])
-def test_rt3d_column_kernel_tilted_initial(csm, oracle, window):
+def test_rt3d_column_kernel_tilted_initial(csm, oracle, window, rt3d_kernel):
     """The column-gather kernel (rt3d_score5, 3-, 5- and 7-step z columns)
     under an initial pose with roll and pitch: the translation lattice's z
     columns drift in x and y, so many lookups fail the column test and take
@@ -266,6 +285,53 @@ def test_rt3d_column_kernel_tilted_initial(csm, oracle, window):
     for initial in [((0.04, -0.02, 0.03), q), ((0.0, 0.0, 0.0), quat_z(0.2))]:
         score, pose = m.Match(initial, cloud, g)
         ref_score, ref_pose, idx, n = oracle.rt3d_match(og, opts, initial, cloud)
+        assert math.isclose(score, ref_score, rel_tol=1e-6), (score, ref_score)
+        assert pose == ref_pose
+
+
+def test_rt3d_nine_step_window(csm, oracle, rt3d_kernel):
+    """+-0.4 m at 0.1 m: 9-step z columns, which v5 does not take (the host
+    selects v4 unforced), under a tilted and a yawed initial pose."""
+    rng = np.random.default_rng(19)
+    cloud = rng.uniform(-4, 4, (300, 3)).astype(np.float32) * np.float32([1, 1, 0.4])
+    og = oracle.hybrid_grid(0.1)
+    og.insert((0, 0, 0), cloud, 0.7, 0.4, 5)
+    opts = (0.4, math.radians(1.0), 0.1, 0.1)
+    g = gpu_grid(csm, og)
+    m = csm.RealTimeCorrelativeScanMatcher3D(csm.RealTimeCorrelativeScanMatcherOptions(*opts))
+    nt, _ = m.window(cloud, 0.1)
+    assert nt == 9 ** 3
+    roll = math.radians(6.0)
+    for initial in [((0.05, -0.03, 0.02), (math.cos(roll / 2), math.sin(roll / 2), 0.0, 0.0)),
+                    ((0.0, 0.0, 0.0), quat_z(0.1))]:
+        score, pose = m.Match(initial, cloud, g)
+        ref_score, ref_pose, _, _ = oracle.rt3d_match(og, opts, initial, cloud)
+        assert math.isclose(score, ref_score, rel_tol=1e-6), (score, ref_score)
+        assert pose == ref_pose
+
+
+@pytest.mark.parametrize("kernel", ["v2", "v1"])
+def test_rt3d_large_brick(csm, oracle, kernel, monkeypatch):
+    """A HybridGrid whose known cells span 30 x 30 x 6 m at 0.1 m (5.5e6
+    voxels, a 22 MB float brick): past v4's and v3's 2^24-byte float offsets,
+    so the host selects v2 unforced (and v1 when forced)."""
+    for var in RT3D_KERNELS.values():
+        if var:
+            monkeypatch.delenv(var, raising=False)
+    if kernel == "v1":
+        monkeypatch.setenv("CSM_RT3D_V1", "1")
+    rng = np.random.default_rng(29)
+    cloud = rng.uniform(-4, 4, (250, 3)).astype(np.float32) * np.float32([1, 1, 0.4])
+    og = oracle.hybrid_grid(0.1)
+    og.insert((0, 0, 0), cloud, 0.7, 0.4, 5)
+    og.set_probability(-150, -150, -30, 0.6)
+    og.set_probability(150, 150, 30, 0.6)
+    g = gpu_grid(csm, og)
+    opts = (0.2, math.radians(1.0), 0.1, 0.1)
+    m = csm.RealTimeCorrelativeScanMatcher3D(csm.RealTimeCorrelativeScanMatcherOptions(*opts))
+    for initial in [((0.04, -0.02, 0.03), quat_z(0.02)), ((0.0, 0.0, 0.0), (1, 0, 0, 0))]:
+        score, pose = m.Match(initial, cloud, g)
+        ref_score, ref_pose, _, _ = oracle.rt3d_match(og, opts, initial, cloud)
         assert math.isclose(score, ref_score, rel_tol=1e-6), (score, ref_score)
         assert pose == ref_pose
 
