@@ -265,18 +265,24 @@ int RunBatch(csm_context* ctx, csm_fast2d* const* submaps, int32_t num_submaps,
     // the three cluster lists of a typical scan (0.55 npad on C2); a list
     // that does not fit falls back to a finer one in the kernel.
     int capc = (3 * max_npad / 4 + 63) & ~63;
+    if (const char* ce = std::getenv("CSM_CAPC_PCT"))  // A/B: cluster-list room, % of npad
+      capc = std::max(64, (std::atoi(ce) * max_npad / 100 + 63) & ~63);
     const int lds_cap = 96 * 1024;
-    while (capc > 0 && static_cast<size_t>(rc) * (max_npad + capc) * 5 > lds_cap) capc -= 64;
-    const size_t dyn_lds = (static_cast<size_t>(rc) * (max_npad + capc) * 5 + 15) & ~size_t{15};
-    // V4Shared: 8 KiB stack + batch state (v5: a 4 KiB stack + 4 KiB of
-    // 16-child sums). CSM_WG_PER_CU caps the workgroups per CU (A/B runs).
-    const size_t static_lds = 12 * 1024 + 512;
+    // Per rotation: npad raw cells (4 B) + capc cluster entries (4 B cell + 1 B count).
+    auto dyn_bytes = [&](int cap) { return static_cast<size_t>(rc) * (max_npad * 4 + cap * 5); };
+    while (capc > 0 && dyn_bytes(capc) > lds_cap) capc -= 64;
+    const size_t dyn_lds = (dyn_bytes(capc) + 15) & ~size_t{15};
     // Node order: FIFO (level by level, the default) or LIFO (depth-first,
     // CSM_SEARCH_ORDER=lifo).
     const char* order_env = std::getenv("CSM_SEARCH_ORDER");
     const bool fifo = !(order_env && std::strcmp(order_env, "lifo") == 0);
-    int per_cu = std::max(1, std::min(8, static_cast<int>((160 * 1024) / (dyn_lds + static_lds))));
+    // Workgroups per CU: what registers and LDS allow (the runtime's
+    // occupancy query). CSM_WG_PER_CU caps it (A/B runs).
+    int per_cu = std::max(1, std::min(8, Fast2dSearchV2BlocksPerCu(hex, fifo, dyn_lds)));
     if (const char* w = std::getenv("CSM_WG_PER_CU")) per_cu = std::max(1, std::min(per_cu, std::atoi(w)));
+    if (std::getenv("CSM_PROFILE2D"))
+      std::fprintf(stderr, "fast2d launch: %s %s, %d rotations per item, %zu B dynamic LDS (capc %d), %d workgroups per CU\n",
+                   hex ? "v5" : "v4", fifo ? "fifo" : "lifo", rc, dyn_lds, capc, per_cu);
     const int grid = static_cast<int>(std::min<int64_t>(static_cast<int64_t>(ctx->num_cus) * per_cu,
                                                         std::max<int64_t>(total_chunks, 1)));
     // DFS stack spill: kSpill2 entries per persistent workgroup.

@@ -658,9 +658,12 @@ constexpr int kLists = kMaxClusterShift + 1;
 // batches, and the virtual roots' quad batches in the first 4 columns).
 template <int kKids>
 struct V4Shared {
-  // LDS part of the DFS stack (v5: half, so its 16-child sums fit the same
-  // LDS budget as v4's); the rest spills to global memory.
-  static constexpr int kStackLds = kKids == 16 ? kStack2 / 2 : kStack2;
+  // LDS part of the DFS stack (v5: a quarter, so 6 workgroups fit a CU's
+  // LDS with their 16-child sums); the rest spills to global memory.
+#ifndef CSM_V4_RING
+#define CSM_V4_RING 0  // LDS stack entries (0: 1024 for v4, 256 for v5)
+#endif
+  static constexpr int kStackLds = CSM_V4_RING ? CSM_V4_RING : (kKids == 16 ? kStack2 / 4 : kStack2);
   static constexpr int kStackCapacity = kStackLds + kSpill2;
   uint2 stack[kStackLds];  // w0: xo | yo << 16; w1: sum | rot << 22 | level << 27
   int part[kBatchNodes][kKids];  // children sums, accumulated by the 4 waves (LDS atomics)
@@ -707,7 +710,7 @@ __device__ __forceinline__ void StackPut(Shared& sh, uint2* spill, int i, uint2 
 // regrouped at level 0, an upper bound of it at coarser levels.
 template <typename Shared>
 __device__ __forceinline__ void V4Score(Shared& sh, const uint32_t* cells, const uint8_t* cnts,
-                                        const SubmapDesc& sm) {
+                                        int raw_end, const SubmapDesc& sm) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nodes = Uniform(sh.nodes);
   const int groups = 64 / nodes;
@@ -722,7 +725,10 @@ __device__ __forceinline__ void V4Score(Shared& sh, const uint32_t* cells, const
   const __amdgpu_buffer_rsrc_t rsrc = LevelRsrc(sm.pyramid_base, Uniform(sm.pyramid_bytes));
   const int off = sh.node_off[node], len = sh.node_len[node];
   const uint32_t* P = cells + off;
-  const uint8_t* Cn = cnts + off;
+  // Raw scans (cells [0, raw_end)) weigh every entry 1 and store no counts;
+  // cluster lists keep theirs at cnts[offset - raw_end].
+  const bool raw = off < raw_end;
+  const uint8_t* Cn = cnts + (raw ? 0 : off - raw_end);
   const int cx = sh.node_xo[node] + L[5];
   const int cy = sh.node_yo[node] + L[5];
   const int blen = Uniform(sh.batch_len);
@@ -761,7 +767,7 @@ __device__ __forceinline__ void V4Score(Shared& sh, const uint32_t* cells, const
       const bool in = idx < len;
       const int j = in ? idx : 0;
       ad[u] = address(P[j], in);
-      c[u] = in ? Cn[j] : 0u;
+      c[u] = in ? (raw ? 1u : Cn[j]) : 0u;
     }
     uint32_t v[U];
 #pragma unroll
@@ -774,7 +780,7 @@ __device__ __forceinline__ void V4Score(Shared& sh, const uint32_t* cells, const
     const bool in = idx < e && idx < len;
     const int j = in ? idx : 0;
     const uint32_t vv = __builtin_amdgcn_raw_buffer_load_b32(rsrc, address(P[j], in), 0, 0);
-    accumulate(vv, in ? Cn[j] : 0u);
+    accumulate(vv, in ? (raw ? 1u : Cn[j]) : 0u);
   }
   for (int m = nodes; m < 64; m <<= 1) {
     a0 += __shfl_xor(a0, m, 64);
@@ -798,7 +804,7 @@ __device__ __forceinline__ void V4Score(Shared& sh, const uint32_t* cells, const
 // every leaf that can reach the best sum.
 template <typename Shared>
 __device__ __forceinline__ void V4ScoreHex(Shared& sh, const uint32_t* cells, const uint8_t* cnts,
-                                           const SubmapDesc& sm) {
+                                           int raw_end, const SubmapDesc& sm) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nodes = Uniform(sh.nodes);
   const int groups = 64 / nodes;
@@ -811,7 +817,10 @@ __device__ __forceinline__ void V4ScoreHex(Shared& sh, const uint32_t* cells, co
   const __amdgpu_buffer_rsrc_t rsrc = LevelRsrc(sm.pyramid_base, Uniform(sm.pyramid_bytes));
   const int off = sh.node_off[node], len = sh.node_len[node];
   const uint32_t* P = cells + off;
-  const uint8_t* Cn = cnts + off;
+  // Raw scans (cells [0, raw_end)) weigh every entry 1 and store no counts;
+  // cluster lists keep theirs at cnts[offset - raw_end].
+  const bool raw = off < raw_end;
+  const uint8_t* Cn = cnts + (raw ? 0 : off - raw_end);
   const int cx = sh.node_xo[node] + L[5];
   const int cy = sh.node_yo[node] + L[5];
   const int blen = Uniform(sh.batch_len);
@@ -851,7 +860,7 @@ __device__ __forceinline__ void V4ScoreHex(Shared& sh, const uint32_t* cells, co
       const bool in = idx < len;
       const int j = in ? idx : 0;
       ad[u] = address(P[j], in);
-      c[u] = in ? Cn[j] : 0u;
+      c[u] = in ? (raw ? 1u : Cn[j]) : 0u;
     }
     decltype(__builtin_amdgcn_raw_buffer_load_b128(rsrc, 0, 0, 0)) v[U];
 #pragma unroll
@@ -864,7 +873,7 @@ __device__ __forceinline__ void V4ScoreHex(Shared& sh, const uint32_t* cells, co
     const bool in = idx < e && idx < len;
     const int j = in ? idx : 0;
     const auto vv = __builtin_amdgcn_raw_buffer_load_b128(rsrc, address(P[j], in), 0, 0);
-    accumulate(vv, in ? Cn[j] : 0u);
+    accumulate(vv, in ? (raw ? 1u : Cn[j]) : 0u);
   }
   for (int m = nodes; m < 64; m <<= 1) {
 #pragma unroll
@@ -956,8 +965,13 @@ __device__ __forceinline__ uint32_t ClusterMask(int sl) {
 // kFifo = false: the stack is LIFO with the deepest level on top (depth-first,
 // early leaves). kFifo = true: a FIFO ring (level by level: batches fill up
 // with the whole frontier of a level; leaves come last).
+#ifndef CSM_V4_WAVES
+// Waves per SIMD the register budget targets: 6 workgroups per CU (v5 with
+// its 256-entry LDS ring fits 6 in LDS too; measured best).
+#define CSM_V4_WAVES 6
+#endif
 template <bool kHex, bool kFifo>
-__global__ void __launch_bounds__(kSearchThreads) __attribute__((amdgpu_waves_per_eu(5)))
+__global__ void __launch_bounds__(kSearchThreads) __attribute__((amdgpu_waves_per_eu(CSM_V4_WAVES)))
 fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
                  const PairDesc* __restrict__ pairs,
                  const float* __restrict__ points,
@@ -968,15 +982,18 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
                  int32_t* __restrict__ status,
                  unsigned long long* __restrict__ stats,
                  uint2* __restrict__ spill_base, int npad, int capc) {
-  // Dynamic LDS: cells, then counts, each rc * (npad + capc) entries. Rotation
-  // r's raw cells (then its k = 1 run list, in place) at r * npad; its
-  // cluster lists packed in [rc * npad + r * capc, + capc).
+  // Dynamic LDS: cells, rc * (npad + capc) words, then the cluster lists'
+  // counts, rc * capc bytes. Rotation r's raw cells at r * npad; its cluster
+  // lists packed in [rc * npad + r * capc, + capc).
   constexpr int kKids = kHex ? 16 : 4;
   extern __shared__ __align__(16) uint32_t cells[];
   __shared__ V4Shared<kKids> sh;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int rc = queues.rot_chunk;
+  // Counts of the cluster lists only (the raw scans weigh 1): entry at cell
+  // offset o has its count at cnts[o - rc * npad].
   uint8_t* cnts = reinterpret_cast<uint8_t*>(cells + rc * (npad + capc));
+  const int raw_end = rc * npad;
   uint2* spill = spill_base + static_cast<size_t>(blockIdx.x) * kSpill2;
   for (int k = tid; k < kBatchNodes * kKids; k += kSearchThreads) sh.part[k / kKids][k % kKids] = 0;
   if (tid == 0) sh.batch_hex = 0;
@@ -1064,7 +1081,6 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
         mnx = min(mnx, ix); mxx = max(mxx, ix);
         mny = min(mny, iy); mxy = max(mxy, iy);
         cells[r * npad + i] = (static_cast<uint32_t>(ix) & 0xffff) | (static_cast<uint32_t>(iy) << 16);
-        cnts[r * npad + i] = 1;  // the k = 1 list is the scan itself, one point per entry
       }
       mnx = WaveMin(mnx); mxx = WaveMax(mxx); mny = WaveMin(mny); mxy = WaveMax(mxy);
       if (lane == 0) {
@@ -1147,7 +1163,7 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
         const int r = t / kMaxClusterShift, sl = 1 + t % kMaxClusterShift;
         if (!(sh.list_len[r][sl] & (1 << 30)))
           RunList<true>(cells + r * npad, n, ClusterMask(sl), cells + sh.list_off[r][sl],
-                        cnts + sh.list_off[r][sl]);
+                        cnts + (sh.list_off[r][sl] - raw_end));
       }
       __syncthreads();
       if (tid < nrot * kLists) sh.list_len[tid / kLists][tid % kLists] &= ~(1 << 30);
@@ -1409,9 +1425,9 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
         // Algorithmic bytes: 4 per quad-dword gather, 16 per hex gather.
         const bool hexb = kHex && Uniform(sh.batch_hex);
         if (hexb)
-          V4ScoreHex(sh, cells, cnts, sm);
+          V4ScoreHex(sh, cells, cnts, raw_end, sm);
         else
-          V4Score(sh, cells, cnts, sm);
+          V4Score(sh, cells, cnts, raw_end, sm);
         const int kids = hexb ? 16 : 4;
         local_cands += kids * nodes;
         local_lookups += static_cast<unsigned long long>(kids) *
@@ -1505,6 +1521,20 @@ hipError_t LaunchFast2dSearchV2(int grid, size_t dyn_lds, hipStream_t st, const 
   else CSM_LAUNCH_V4(false, false);
 #undef CSM_LAUNCH_V4
   return hipGetLastError();
+}
+
+int Fast2dSearchV2BlocksPerCu(bool hex, bool fifo, size_t dyn_lds) {
+  int blocks = 0;
+  hipError_t e;
+  if (hex && fifo)
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fast2d_search_v4<true, true>, kSearchThreads, dyn_lds);
+  else if (hex)
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fast2d_search_v4<true, false>, kSearchThreads, dyn_lds);
+  else if (fifo)
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fast2d_search_v4<false, true>, kSearchThreads, dyn_lds);
+  else
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fast2d_search_v4<false, false>, kSearchThreads, dyn_lds);
+  return e == hipSuccess ? blocks : 0;
 }
 
 hipError_t LaunchPyramidHex(const uint8_t* level, int wnx, int wny, int log_h, int km1,

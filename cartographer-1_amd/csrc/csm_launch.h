@@ -24,6 +24,9 @@ hipError_t LaunchFast2dSearchV2(int grid, size_t dyn_lds, hipStream_t st, const 
                                 const WorkQueues2& queues, unsigned long long* counters,
                                 uint64_t* best, int32_t* status, unsigned long long* stats,
                                 uint2* spill, int npad, int capc, bool hex, bool fifo);
+// Resident workgroups per CU of the v4/v5 search kernel at this dynamic LDS
+// size (registers and LDS; 0 if the query fails).
+int Fast2dSearchV2BlocksPerCu(bool hex, bool fifo, size_t dyn_lds);
 // Widened level (into scratch, (wnx + km1) x (wny + km1) bytes), then its hex
 // plane (total = 16-byte entries).
 hipError_t LaunchPyramidHex(const uint8_t* level, int wnx, int wny, int log_h, int km1,
