@@ -82,7 +82,8 @@ class Timing(C.Structure):
                 ("other_kernel_ms", C.c_double), ("rt3d_kernel_ms", C.c_double),
                 ("rt3d_lookups", C.c_double), ("fast3d_kernel_ms", C.c_double),
                 ("fast3d_launches", C.c_int64), ("fast3d_lookups", C.c_double),
-                ("search_errors", C.c_int64), ("stack_high_water", C.c_int64)]
+                ("search_errors", C.c_int64), ("stack_high_water", C.c_int64),
+                ("tied_pairs", C.c_int64), ("ties_unresolved", C.c_int64)]
 
 
 class Pose3D(C.Structure):

@@ -83,7 +83,16 @@ struct PairDesc {
   int32_t max_rejected_sum; // prune / reject sums <= this value
   float tx, ty;             // initial translation, narrowed to float
   float pre_w, pre_s;       // initial rotation quaternion (z axis)
+  int32_t collect;          // 1: tie enumeration, record every leaf with sum collect_sum
+  int32_t collect_sum;
 };
+
+// Tie resolution (csm_host.cc ResolveTies): one workgroup per (pair,
+// rotation) scores `count` queries (level, x_off, y_off) at queries[first..].
+struct ScoreJob {
+  int32_t pair, rot, first, count;
+};
+constexpr int kTieCap = 4096;  // tied leaves recorded per pair
 
 // Per-XCD work queues over rotation chunks of pairs.
 struct WorkQueues {
@@ -121,6 +130,12 @@ CSM_HD inline uint64_t PackLeafKey(uint32_t sum, int rot, int xo, int yo) {
   const uint64_t idx = (uint64_t(rot) << 28) | (uint64_t(xo + 8192) << 14) |
                        uint64_t(yo + 8192);
   return (uint64_t(sum) << kSumShift) | (~idx & kTieMask);
+}
+// The same leaf as (sum, index) with the index NOT inverted: the per-pair
+// atomicMax of these keeps the tied maximum with the largest index, so a pair
+// has more than one maximal leaf iff its two keys differ.
+CSM_HD inline uint64_t HighLeafKey(uint64_t key) {
+  return (key & ~kTieMask) | (~key & kTieMask);
 }
 CSM_HD inline void UnpackLeafKey(uint64_t key, uint32_t* sum, int* rot, int* xo, int* yo) {
   *sum = static_cast<uint32_t>(key >> kSumShift);

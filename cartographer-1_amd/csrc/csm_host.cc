@@ -17,6 +17,8 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <set>
+#include <array>
 #include <tuple>
 #include <vector>
 
@@ -86,6 +88,416 @@ const std::pair<SearchWindow2D, std::vector<ZRot>>& WindowFor(
   std::vector<ZRot> table;
   RotationTable(w, &table);
   return s->windows.emplace(key, std::make_pair(w, std::move(table))).first->second;
+}
+
+struct SearchPlan {
+  bool use_v2 = true, hex = false, fifo = true;
+  int rc = 2, max_npad = 64;
+};
+
+// One search launch over `pdesc` (the submap descriptors and the rotation
+// table are on the device already). init_best: per-pair starting best keys
+// (tie enumeration: the pair's maximum, so only nodes reaching it expand and
+// every leaf at it is recorded, PairDesc::collect_sum); null = 0.
+int LaunchSearch(csm_context* ctx, csm_scan_set* scans, const std::vector<PairDesc>& pdesc,
+                 const std::vector<uint64_t>* init_best, const SearchPlan& plan, bool timed,
+                 std::vector<uint64_t>* keys, std::vector<uint64_t>* keys_hi,
+                 std::vector<int32_t>* stat, unsigned long long* stats_host,
+                 std::vector<uint2>* ties = nullptr, std::vector<int32_t>* tie_counts = nullptr) {
+  const int np = static_cast<int>(pdesc.size());
+  const int rc = plan.rc;
+  // Per-XCD queues: submap s -> queue s % 8 so a submap's pyramid stays in
+  // one XCD's L2; pairs within a queue in submap order.
+  std::vector<std::vector<int32_t>> q(kNumXcd);
+  for (int i = 0; i < np; ++i) q[pdesc[i].submap % kNumXcd].push_back(i);
+  std::vector<int32_t> order;
+  std::vector<int64_t> prefix;
+  WorkQueues wq{};
+  wq.rot_chunk = rc;
+  int64_t running = 0;
+  for (int x = 0; x < kNumXcd; ++x) {
+    std::stable_sort(q[x].begin(), q[x].end(),
+                     [&](int a, int b) { return pdesc[a].submap < pdesc[b].submap; });
+    wq.queue_begin[x] = static_cast<int32_t>(order.size());
+    const int64_t qstart = running;
+    for (int pi : q[x]) {
+      order.push_back(pi);
+      prefix.push_back(running);
+      running += (pdesc[pi].num_scans + rc - 1) / rc;
+    }
+    wq.queue_chunks[x] = running - qstart;
+  }
+  wq.queue_begin[kNumXcd] = static_cast<int32_t>(order.size());
+  prefix.push_back(running);
+
+  int rcode;
+  if ((rcode = ctx->pair_desc.Reserve(sizeof(PairDesc) * np))) return rcode;
+  if ((rcode = ctx->best.Reserve(sizeof(uint64_t) * np))) return rcode;
+  if ((rcode = ctx->best_hi.Reserve(sizeof(uint64_t) * np))) return rcode;
+  if ((rcode = ctx->status.Reserve(sizeof(int32_t) * np))) return rcode;
+  if ((rcode = ctx->counters.Reserve(sizeof(unsigned long long) * kNumXcd))) return rcode;
+  if ((rcode = ctx->pair_order.Reserve(sizeof(int32_t) * order.size()))) return rcode;
+  if ((rcode = ctx->chunk_prefix.Reserve(sizeof(int64_t) * prefix.size()))) return rcode;
+  if ((rcode = ctx->stats.Reserve(sizeof(unsigned long long) * kStatsWords))) return rcode;
+  if ((rcode = ctx->tie_count.Reserve(sizeof(int32_t) * np))) return rcode;
+  if (ties && (rcode = ctx->ties.Reserve(sizeof(uint2) * kTieCap * static_cast<size_t>(np))))
+    return rcode;
+  hipStream_t st = ctx->stream;
+  CSM_HIP(hipMemcpyAsync(ctx->pair_desc.ptr, pdesc.data(), sizeof(PairDesc) * np,
+                         hipMemcpyHostToDevice, st));
+  CSM_HIP(hipMemcpyAsync(ctx->pair_order.ptr, order.data(), sizeof(int32_t) * order.size(),
+                         hipMemcpyHostToDevice, st));
+  CSM_HIP(hipMemcpyAsync(ctx->chunk_prefix.ptr, prefix.data(), sizeof(int64_t) * prefix.size(),
+                         hipMemcpyHostToDevice, st));
+  if (init_best)
+    CSM_HIP(hipMemcpyAsync(ctx->best.ptr, init_best->data(), sizeof(uint64_t) * np,
+                           hipMemcpyHostToDevice, st));
+  else
+    CSM_HIP(hipMemsetAsync(ctx->best.ptr, 0, sizeof(uint64_t) * np, st));
+  CSM_HIP(hipMemsetAsync(ctx->best_hi.ptr, 0, sizeof(uint64_t) * np, st));
+  CSM_HIP(hipMemsetAsync(ctx->status.ptr, 0, sizeof(int32_t) * np, st));
+  CSM_HIP(hipMemsetAsync(ctx->tie_count.ptr, 0, sizeof(int32_t) * np, st));
+  CSM_HIP(hipMemsetAsync(ctx->counters.ptr, 0, sizeof(unsigned long long) * kNumXcd, st));
+  CSM_HIP(hipMemsetAsync(ctx->stats.ptr, 0, sizeof(unsigned long long) * kStatsWords, st));
+  wq.pair_order = ctx->pair_order.as<int32_t>();
+  wq.chunk_prefix = ctx->chunk_prefix.as<int64_t>();
+
+  // ---- launch: persistent workgroups ----------------------------------------
+  const int64_t total_chunks = running;
+  const int max_npad = plan.max_npad;
+  if (timed) CSM_HIP(hipEventRecord(ctx->ev0, st));
+  if (plan.use_v2) {
+    // Block table: for every 64 chunks of a queue, the first pair_order entry.
+    std::vector<int32_t> blocks;
+    WorkQueues2 wq2{};
+    wq2.rot_chunk = rc;
+    for (int x = 0; x < kNumXcd; ++x) {
+      wq2.queue_begin[x] = wq.queue_begin[x];
+      wq2.queue_chunks[x] = wq.queue_chunks[x];
+      wq2.block_offset[x] = static_cast<int32_t>(blocks.size());
+      const int64_t qstart = prefix[wq.queue_begin[x]];
+      int e = wq.queue_begin[x];
+      for (int64_t c = 0; c < wq.queue_chunks[x]; c += 64) {
+        while (prefix[e + 1] - qstart <= c) ++e;
+        blocks.push_back(e);
+      }
+    }
+    wq2.queue_begin[kNumXcd] = wq.queue_begin[kNumXcd];
+    if ((rcode = ctx->blocks.Reserve(sizeof(int32_t) * std::max<size_t>(blocks.size(), 1))))
+      return rcode;
+    if (!blocks.empty())
+      CSM_HIP(hipMemcpyAsync(ctx->blocks.ptr, blocks.data(), sizeof(int32_t) * blocks.size(),
+                             hipMemcpyHostToDevice, st));
+    wq2.pair_order = wq.pair_order;
+    wq2.chunk_prefix = wq.chunk_prefix;
+    wq2.block_first = ctx->blocks.as<int32_t>();
+    // Per rotation: npad raw cells and capc cluster-list entries. capc =
+    // 3/4 npad holds the three cluster lists of a typical scan (0.55 npad on
+    // C2); a list that does not fit falls back to a finer one in the kernel.
+    int capc = (3 * max_npad / 4 + 63) & ~63;
+    if (const char* ce = std::getenv("CSM_CAPC_PCT"))  // A/B: cluster-list room, % of npad
+      capc = std::max(64, (std::atoi(ce) * max_npad / 100 + 63) & ~63);
+    const int lds_cap = 96 * 1024;
+    // Per rotation: npad raw cells (4 B) + capc cluster entries (4 B cell + 1 B count).
+    auto dyn_bytes = [&](int cap) { return static_cast<size_t>(rc) * (max_npad * 4 + cap * 5); };
+    while (capc > 0 && dyn_bytes(capc) > lds_cap) capc -= 64;
+    const size_t dyn_lds = (dyn_bytes(capc) + 15) & ~size_t{15};
+    // Workgroups per CU: what registers and LDS allow (the runtime's
+    // occupancy query). CSM_WG_PER_CU caps it (A/B runs).
+    int per_cu = std::max(1, std::min(8, Fast2dSearchV2BlocksPerCu(plan.hex, plan.fifo, dyn_lds)));
+    if (const char* w = std::getenv("CSM_WG_PER_CU")) per_cu = std::max(1, std::min(per_cu, std::atoi(w)));
+    if (std::getenv("CSM_PROFILE2D") && !init_best)
+      std::fprintf(stderr, "fast2d launch: %s %s, %d rotations per item, %zu B dynamic LDS (capc %d), %d workgroups per CU\n",
+                   plan.hex ? "v5" : "v4", plan.fifo ? "fifo" : "lifo", rc, dyn_lds, capc, per_cu);
+    const int grid = static_cast<int>(std::min<int64_t>(static_cast<int64_t>(ctx->num_cus) * per_cu,
+                                                        std::max<int64_t>(total_chunks, 1)));
+    // DFS stack spill: kSpill2 entries per persistent workgroup.
+    if ((rcode = ctx->spill.Reserve(sizeof(uint2) * kSpill2 * static_cast<size_t>(grid))))
+      return rcode;
+    CSM_HIP(LaunchFast2dSearchV2(grid, dyn_lds, st, ctx->submap_desc.as<SubmapDesc>(),
+                                 ctx->pair_desc.as<PairDesc>(), scans->points.as<float>(),
+                                 ctx->rot_table.as<float2>(), wq2,
+                                 ctx->counters.as<unsigned long long>(), ctx->best.as<uint64_t>(),
+                                 ctx->status.as<int32_t>(), ctx->stats.as<unsigned long long>(),
+                                 ctx->spill.as<uint2>(), max_npad, capc, plan.hex, plan.fifo,
+                                 ctx->best_hi.as<uint64_t>(), ties ? ctx->ties.as<uint2>() : nullptr,
+                                 ctx->tie_count.as<int32_t>()));
+  } else {
+    const size_t dyn_lds = static_cast<size_t>(rc) * max_npad * sizeof(uint32_t);
+    const int grid = static_cast<int>(std::min<int64_t>(static_cast<int64_t>(ctx->num_cus) * 4,
+                                                        std::max<int64_t>(total_chunks, 1)));
+    CSM_HIP(LaunchFast2dSearch(grid, dyn_lds, st, ctx->submap_desc.as<SubmapDesc>(),
+                               ctx->pair_desc.as<PairDesc>(), scans->points.as<float>(),
+                               ctx->rot_table.as<float2>(), wq,
+                               ctx->counters.as<unsigned long long>(), ctx->best.as<uint64_t>(),
+                               ctx->status.as<int32_t>(), ctx->stats.as<unsigned long long>()));
+  }
+  if (timed) CSM_HIP(hipEventRecord(ctx->ev1, st));
+  keys->resize(np);
+  keys_hi->resize(np);
+  stat->resize(np);
+  CSM_HIP(hipMemcpyAsync(keys->data(), ctx->best.ptr, sizeof(uint64_t) * np, hipMemcpyDeviceToHost, st));
+  CSM_HIP(hipMemcpyAsync(keys_hi->data(), ctx->best_hi.ptr, sizeof(uint64_t) * np,
+                         hipMemcpyDeviceToHost, st));
+  CSM_HIP(hipMemcpyAsync(stat->data(), ctx->status.ptr, sizeof(int32_t) * np, hipMemcpyDeviceToHost, st));
+  CSM_HIP(hipMemcpyAsync(stats_host, ctx->stats.ptr, sizeof(unsigned long long) * kStatsWords,
+                         hipMemcpyDeviceToHost, st));
+  if (ties) {
+    ties->resize(static_cast<size_t>(kTieCap) * np);
+    tie_counts->resize(np);
+    CSM_HIP(hipMemcpyAsync(ties->data(), ctx->ties.ptr, sizeof(uint2) * ties->size(),
+                           hipMemcpyDeviceToHost, st));
+    CSM_HIP(hipMemcpyAsync(tie_counts->data(), ctx->tie_count.ptr, sizeof(int32_t) * np,
+                           hipMemcpyDeviceToHost, st));
+  }
+  CSM_HIP(hipStreamSynchronize(st));
+  return CSM_OK;
+}
+
+// ShrinkToFit bounds (correlative_scan_matcher_2d.cc:73-91) of rotation r of
+// a pair, from the scan discretized on the host with the device's arithmetic
+// (two z rotations in Eigen's order, the float translation add, GetCellIndex
+// in double, map_limits.h:69-75).
+void RotationBounds(const csm_scan_set* scans, const PairDesc& d, const SubmapDesc& sm,
+                    const ZRot& rot, int b[4]) {
+  int mnx = 0x7fffffff, mxx = -0x7fffffff, mny = 0x7fffffff, mxy = -0x7fffffff;
+  const ZRot pre{d.pre_w, d.pre_s};
+  const float* p = scans->host_points.data() + 3 * d.point_offset;
+  for (int i = 0; i < d.num_points; ++i) {
+    float x, y;
+    RotateZ(pre, p[3 * i], p[3 * i + 1], &x, &y);
+    RotateZ(rot, x, y, &x, &y);
+    const float px = d.tx + x, py = d.ty + y;
+    const int ix = static_cast<int>(std::round((sm.max_y - static_cast<double>(py)) / sm.resolution - 0.5));
+    const int iy = static_cast<int>(std::round((sm.max_x - static_cast<double>(px)) / sm.resolution - 0.5));
+    mnx = std::min(mnx, ix); mxx = std::max(mxx, ix);
+    mny = std::min(mny, iy); mxy = std::max(mxy, iy);
+  }
+  b[0] = std::max(-d.num_linear, std::min(0, -mxx));
+  b[1] = std::min(d.num_linear, std::max(0, sm.nx - 1 - mnx));
+  b[2] = std::max(-d.num_linear, std::min(0, -mxy));
+  b[3] = std::min(d.num_linear, std::max(0, sm.ny - 1 - mny));
+}
+
+// Exactly tied maxima. The device keeps the smallest (rotation, x, y) leaf;
+// the reference keeps the FIRST maximal leaf its depth-first search visits
+// (std::max keeps the incumbent on equal scores and later subtrees whose
+// bound does not exceed it are cut, fast_correlative_scan_matcher_2d.cc:
+// 344-376). It visits a node's children (<= 4, std::sort = insertion sort:
+// stable) by descending score, equal scores in generation order (x, then y;
+// :353-366), and the lowest-resolution candidates in the order std::sort
+// (introsort, not stable) leaves their generation order (scan, x, y;
+// :276-312) in. So among tied leaves the reference's pick is the one whose
+// chain of ancestors, top level first, comes first in those orders. For a
+// pair whose two witness keys show a tie: (1) a second search with the
+// maximum as its starting best records every leaf at it; (2) the ancestors'
+// exact bounds at the reference's depth are scored on the device
+// (fast2d_score_queries); (3) when two tied leaves descend from different
+// lowest-resolution candidates of equal score, the pair's whole
+// lowest-resolution list is scored and sorted with the same std::sort and
+// comparison, which reproduces the reference's permutation. No oracle and no
+// CPU scoring is involved.
+int ResolveTies(csm_context* ctx, csm_fast2d* const* submaps, csm_scan_set* scans,
+                const std::vector<PairDesc>& pdesc, const std::vector<float2>& rot_host,
+                const SearchPlan& plan, const std::vector<int32_t>& stat,
+                const std::vector<uint64_t>& keys_hi, std::vector<uint64_t>* keys) {
+  std::vector<int> tied;
+  for (int k = 0; k < static_cast<int>(pdesc.size()); ++k) {
+    const uint64_t key = (*keys)[k];
+    if ((stat[k] & kStatusRange) || key == 0) continue;
+    const int64_t sum = static_cast<int64_t>(key >> kSumShift);
+    if (sum <= pdesc[k].max_rejected_sum) continue;
+    if ((keys_hi[k] >> kSumShift) == (key >> kSumShift) && keys_hi[k] != HighLeafKey(key))
+      tied.push_back(k);
+  }
+  if (tied.empty()) return CSM_OK;
+  ctx->t.tied_pairs += static_cast<int64_t>(tied.size());
+  // (1) Every leaf at the maximum.
+  std::vector<PairDesc> pd2;
+  std::vector<uint64_t> init;
+  for (int k : tied) {
+    PairDesc d = pdesc[k];
+    d.collect = 1;
+    d.collect_sum = static_cast<int32_t>((*keys)[k] >> kSumShift);
+    pd2.push_back(d);
+    init.push_back(static_cast<uint64_t>(d.collect_sum) << kSumShift);
+  }
+  std::vector<uint64_t> k2, kh2;
+  std::vector<int32_t> st2, counts;
+  std::vector<uint2> ties;
+  unsigned long long stats2[kStatsWords] = {0};
+  int rc;
+  if ((rc = LaunchSearch(ctx, scans, pd2, &init, plan, false, &k2, &kh2, &st2, stats2, &ties,
+                         &counts)))
+    return rc;
+  auto zrot = [&](const PairDesc& d, int r) {
+    const float2 z = rot_host[d.rot_offset + r];
+    return ZRot{z.x, z.y};
+  };
+  // (2) Ancestors at the reference's depth D: level d node of a leaf is
+  // (b0 + ((x - b0) >> d << d), b2 + ((y - b2) >> d << d)).
+  struct Tie {
+    int k, t, depth, leaves_first, leaves_count;
+  };
+  std::vector<Tie> work;
+  std::vector<int3> leaves;          // (rot, x, y)
+  std::vector<ScoreJob> jobs;
+  std::vector<int4> queries;
+  std::vector<int> leaf_query;       // per leaf: first of its D - 1 ancestor queries
+  for (size_t t = 0; t < tied.size(); ++t) {
+    const int k = tied[t];
+    const int cnt = counts[t];
+    if ((st2[t] & kStatusRange) || cnt > kTieCap || cnt < 2) {
+      ctx->t.ties_unresolved += 1;
+      continue;
+    }
+    const PairDesc& d = pdesc[k];
+    const csm_fast2d* m = submaps[d.submap];
+    Tie w{k, static_cast<int>(t), m->options.branch_and_bound_depth,
+          static_cast<int>(leaves.size()), cnt};
+    std::map<int, std::vector<int>> by_rot;
+    for (int i = 0; i < cnt; ++i) {
+      const uint2 e = ties[static_cast<size_t>(t) * kTieCap + i];
+      const int r = static_cast<int>(e.x);
+      const int x = static_cast<int16_t>(e.y & 0xffff), y = static_cast<int>(e.y) >> 16;
+      leaves.push_back(make_int3(r, x, y));
+      by_rot[r].push_back(w.leaves_first + i);
+    }
+    leaf_query.resize(leaves.size(), -1);
+    const int T = w.depth - 1;
+    for (auto& [r, idx] : by_rot) {
+      int b[4];
+      RotationBounds(scans, d, m->desc, zrot(d, r), b);
+      if (T < 1) continue;
+      ScoreJob job{static_cast<int32_t>(t), r, static_cast<int32_t>(queries.size()), 0};
+      for (int li : idx) {
+        leaf_query[li] = static_cast<int>(queries.size());
+        for (int lv = 1; lv <= T; ++lv) {
+          const int ax = b[0] + (((leaves[li].y - b[0]) >> lv) << lv);
+          const int ay = b[2] + (((leaves[li].z - b[2]) >> lv) << lv);
+          queries.push_back(make_int4(lv, ax, ay, 0));
+        }
+      }
+      job.count = static_cast<int32_t>(queries.size()) - job.first;
+      jobs.push_back(job);
+    }
+    work.push_back(w);
+  }
+  auto score = [&](const std::vector<ScoreJob>& js, const std::vector<int4>& qs,
+                   std::vector<int32_t>* sums) -> int {
+    sums->assign(qs.size(), 0);
+    if (js.empty()) return CSM_OK;
+    int r2;
+    if ((r2 = ctx->sq_jobs.Reserve(sizeof(ScoreJob) * js.size()))) return r2;
+    if ((r2 = ctx->sq_queries.Reserve(sizeof(int4) * qs.size()))) return r2;
+    if ((r2 = ctx->sq_sums.Reserve(sizeof(int32_t) * qs.size()))) return r2;
+    hipStream_t st = ctx->stream;
+    CSM_HIP(hipMemcpyAsync(ctx->sq_jobs.ptr, js.data(), sizeof(ScoreJob) * js.size(),
+                           hipMemcpyHostToDevice, st));
+    CSM_HIP(hipMemcpyAsync(ctx->sq_queries.ptr, qs.data(), sizeof(int4) * qs.size(),
+                           hipMemcpyHostToDevice, st));
+    CSM_HIP(LaunchFast2dScoreQueries(static_cast<int>(js.size()), plan.max_npad, st,
+                                     ctx->submap_desc.as<SubmapDesc>(), ctx->pair_desc.as<PairDesc>(),
+                                     scans->points.as<float>(), ctx->rot_table.as<float2>(),
+                                     ctx->sq_jobs.as<ScoreJob>(), ctx->sq_queries.as<int4>(),
+                                     ctx->sq_sums.as<int32_t>()));
+    CSM_HIP(hipMemcpyAsync(sums->data(), ctx->sq_sums.ptr, sizeof(int32_t) * qs.size(),
+                           hipMemcpyDeviceToHost, st));
+    CSM_HIP(hipStreamSynchronize(st));
+    return CSM_OK;
+  };
+  // The jobs index pd2 (ctx->pair_desc holds it after the second search).
+  std::vector<int32_t> sums;
+  if ((rc = score(jobs, queries, &sums))) return rc;
+  for (const Tie& w : work) {
+    const PairDesc& d = pdesc[w.k];
+    const PairDesc& d2 = pd2[w.t];
+    const csm_fast2d* m = submaps[d.submap];
+    const int T = w.depth - 1;
+    // (x, y, score) of leaf li's level-lv ancestor; the score as
+    // ScoreCandidates stores it (ToScore(sum / n), compared as floats).
+    auto anc = [&](int li, int lv) {
+      const int4 q = queries[leaf_query[li] + lv - 1];
+      return std::make_tuple(q.y, q.z,
+                             SumToScore(sums[leaf_query[li] + lv - 1], d.num_points, m->min_s, m->max_s));
+    };
+    // (3) Top-level positions, only if two distinct top ancestors tie.
+    std::map<std::tuple<int, int, int>, int64_t> top_pos;  // (rot, x, y) -> sorted position
+    bool need_perm = T == 0;
+    if (T >= 1) {
+      std::map<float, std::set<std::tuple<int, int, int>>> top_by_sum;
+      for (int i = 0; i < w.leaves_count; ++i) {
+        const int li = w.leaves_first + i;
+        const auto [x, y, s] = anc(li, T);
+        top_by_sum[s].insert({leaves[li].x, x, y});
+      }
+      for (auto& [s, nodes] : top_by_sum) need_perm |= nodes.size() > 1;
+    }
+    if (need_perm) {
+      // The pair's whole lowest-resolution list in generation order.
+      const int step = 1 << T;
+      std::vector<ScoreJob> tj;
+      std::vector<int4> tq;
+      std::vector<int64_t> rot_first(d.num_scans + 1, 0);
+      std::vector<std::array<int, 4>> rb(d.num_scans);
+      for (int r = 0; r < d.num_scans; ++r) {
+        int b[4];
+        RotationBounds(scans, d, m->desc, zrot(d, r), b);
+        rb[r] = {b[0], b[1], b[2], b[3]};
+        ScoreJob job{w.t, r, static_cast<int32_t>(tq.size()), 0};
+        for (int x = b[0]; x <= b[1]; x += step)
+          for (int y = b[2]; y <= b[3]; y += step) tq.push_back(make_int4(T, x, y, 0));
+        job.count = static_cast<int32_t>(tq.size()) - job.first;
+        rot_first[r + 1] = static_cast<int64_t>(tq.size());
+        if (job.count) tj.push_back(job);
+      }
+      std::vector<int32_t> ts;
+      if ((rc = score(tj, tq, &ts))) return rc;
+      // ScoreCandidates: score = ToScore(sum / n), then
+      // std::sort(greater<Candidate2D>) — the same algorithm and the same
+      // comparisons give the same permutation for any element type.
+      std::vector<std::pair<float, int64_t>> lst(tq.size());
+      for (size_t i = 0; i < tq.size(); ++i)
+        lst[i] = {SumToScore(ts[i], d.num_points, m->min_s, m->max_s), static_cast<int64_t>(i)};
+      std::sort(lst.begin(), lst.end(),
+                [](const std::pair<float, int64_t>& a, const std::pair<float, int64_t>& b) {
+                  return a.first > b.first;
+                });
+      std::vector<int64_t> pos(lst.size());
+      for (size_t i = 0; i < lst.size(); ++i) pos[lst[i].second] = static_cast<int64_t>(i);
+      for (int i = 0; i < w.leaves_count; ++i) {
+        const int li = w.leaves_first + i;
+        const int r = leaves[li].x;
+        int x = leaves[li].y, y = leaves[li].z;
+        if (T >= 1) std::tie(x, y, std::ignore) = anc(li, T);
+        const int ny = (rb[r][3] - rb[r][2] + step) / step;
+        const int64_t idx = rot_first[r] + static_cast<int64_t>((x - rb[r][0]) / step) * ny + (y - rb[r][2]) / step;
+        top_pos[{r, x, y}] = pos[idx];
+      }
+    }
+    // The reference's visiting order of two tied leaves.
+    auto first = [&](int a, int b) {
+      for (int lv = T; lv >= 1; --lv) {
+        const auto [ax, ay, as] = anc(a, lv);
+        const auto [bx, by, bs] = anc(b, lv);
+        const int ra = leaves[a].x, rb2 = leaves[b].x;
+        if (ra == rb2 && ax == bx && ay == by) continue;
+        if (as != bs) return as > bs;
+        if (lv == T) return top_pos.at({ra, ax, ay}) < top_pos.at({rb2, bx, by});
+        return std::make_pair(ax, ay) < std::make_pair(bx, by);
+      }
+      if (T == 0)
+        return top_pos.at({leaves[a].x, leaves[a].y, leaves[a].z}) <
+               top_pos.at({leaves[b].x, leaves[b].y, leaves[b].z});
+      return std::make_pair(leaves[a].y, leaves[a].z) < std::make_pair(leaves[b].y, leaves[b].z);
+    };
+    int best = w.leaves_first;
+    for (int i = 1; i < w.leaves_count; ++i)
+      if (first(w.leaves_first + i, best)) best = w.leaves_first + i;
+    (*keys)[w.k] = PackLeafKey(static_cast<uint32_t>(d2.collect_sum), leaves[best].x,
+                               leaves[best].y, leaves[best].z);
+  }
+  return CSM_OK;
 }
 
 int RunBatch(csm_context* ctx, csm_fast2d* const* submaps, int32_t num_submaps,
@@ -168,154 +580,38 @@ int RunBatch(csm_context* ctx, csm_fast2d* const* submaps, int32_t num_submaps,
 
   const char* forced_env = std::getenv("CSM_SEARCH_KERNEL");
   const int forced = forced_env ? std::atoi(forced_env) : 0;
-  // The v4 kernel keeps rot_chunk discretized scans (4 B/point) in LDS;
+  SearchPlan plan;
+  // The v4/v5 kernel keeps rot_chunk discretized scans (4 B/point) in LDS;
   // above ~8k points per scan the v1 kernel (lanes = points) is used.
-  const bool use_v2 = forced == 2 || (forced != 1 && max_npad <= 8192);
+  plan.use_v2 = forced == 2 || (forced != 1 && max_npad <= 8192);
+  plan.hex = hex;
+  plan.max_npad = max_npad;
   const char* rc_env = std::getenv("CSM_ROT_CHUNK");
   const int v4_budget = 9 * 1024;  // C2 (1088 padded points): 2 rotations per chunk, the measured best
   const int v4_rc = rc_env ? std::max(1, std::min(16, std::atoi(rc_env)))
                            : std::max(1, std::min(8, v4_budget / (max_npad * 4)));
   const int lds_budget = 40 * 1024;
-  const int rc = use_v2 ? v4_rc : std::max(1, std::min(16, lds_budget / (max_npad * 4)));
+  plan.rc = plan.use_v2 ? v4_rc : std::max(1, std::min(16, lds_budget / (max_npad * 4)));
+  // Node order: FIFO (level by level, the default) or LIFO (depth-first,
+  // CSM_SEARCH_ORDER=lifo).
+  const char* order_env = std::getenv("CSM_SEARCH_ORDER");
+  plan.fifo = !(order_env && std::strcmp(order_env, "lifo") == 0);
 
-  // Per-XCD queues: submap s -> queue s % 8 so a submap's pyramid stays in
-  // one XCD's L2; pairs within a queue in submap order.
-  std::vector<std::vector<int32_t>> q(kNumXcd);
-  for (int i = 0; i < np; ++i) q[pdesc[i].submap % kNumXcd].push_back(i);
-  // Rebalance: if a queue is much larger than the mean, spill whole submaps.
-  std::vector<int32_t> order;
-  std::vector<int64_t> prefix;
-  WorkQueues wq{};
-  wq.rot_chunk = rc;
-  int64_t running = 0;
-  for (int x = 0; x < kNumXcd; ++x) {
-    std::stable_sort(q[x].begin(), q[x].end(),
-                     [&](int a, int b) { return pdesc[a].submap < pdesc[b].submap; });
-    wq.queue_begin[x] = static_cast<int32_t>(order.size());
-    const int64_t qstart = running;
-    for (int pi : q[x]) {
-      order.push_back(pi);
-      prefix.push_back(running);
-      running += (pdesc[pi].num_scans + rc - 1) / rc;
-    }
-    wq.queue_chunks[x] = running - qstart;
-  }
-  wq.queue_begin[kNumXcd] = static_cast<int32_t>(order.size());
-  prefix.push_back(running);
-
-  // ---- uploads ---------------------------------------------------------------
+  // ---- uploads shared by the search and the tie resolution ------------------
   int rcode;
   if ((rcode = ctx->submap_desc.Reserve(sizeof(SubmapDesc) * num_submaps))) return rcode;
-  if ((rcode = ctx->pair_desc.Reserve(sizeof(PairDesc) * np))) return rcode;
   if ((rcode = ctx->rot_table.Reserve(sizeof(float2) * rot_host.size()))) return rcode;
-  if ((rcode = ctx->best.Reserve(sizeof(uint64_t) * np))) return rcode;
-  if ((rcode = ctx->status.Reserve(sizeof(int32_t) * np))) return rcode;
-  if ((rcode = ctx->counters.Reserve(sizeof(unsigned long long) * kNumXcd))) return rcode;
-  if ((rcode = ctx->pair_order.Reserve(sizeof(int32_t) * order.size()))) return rcode;
-  if ((rcode = ctx->chunk_prefix.Reserve(sizeof(int64_t) * prefix.size()))) return rcode;
-  if ((rcode = ctx->stats.Reserve(sizeof(unsigned long long) * kStatsWords))) return rcode;
   hipStream_t st = ctx->stream;
   CSM_HIP(hipMemcpyAsync(ctx->submap_desc.ptr, sdesc.data(), sizeof(SubmapDesc) * num_submaps,
                          hipMemcpyHostToDevice, st));
-  CSM_HIP(hipMemcpyAsync(ctx->pair_desc.ptr, pdesc.data(), sizeof(PairDesc) * np,
-                         hipMemcpyHostToDevice, st));
   CSM_HIP(hipMemcpyAsync(ctx->rot_table.ptr, rot_host.data(), sizeof(float2) * rot_host.size(),
                          hipMemcpyHostToDevice, st));
-  CSM_HIP(hipMemcpyAsync(ctx->pair_order.ptr, order.data(), sizeof(int32_t) * order.size(),
-                         hipMemcpyHostToDevice, st));
-  CSM_HIP(hipMemcpyAsync(ctx->chunk_prefix.ptr, prefix.data(), sizeof(int64_t) * prefix.size(),
-                         hipMemcpyHostToDevice, st));
-  CSM_HIP(hipMemsetAsync(ctx->best.ptr, 0, sizeof(uint64_t) * np, st));
-  CSM_HIP(hipMemsetAsync(ctx->status.ptr, 0, sizeof(int32_t) * np, st));
-  CSM_HIP(hipMemsetAsync(ctx->counters.ptr, 0, sizeof(unsigned long long) * kNumXcd, st));
-  CSM_HIP(hipMemsetAsync(ctx->stats.ptr, 0, sizeof(unsigned long long) * kStatsWords, st));
-  wq.pair_order = ctx->pair_order.as<int32_t>();
-  wq.chunk_prefix = ctx->chunk_prefix.as<int64_t>();
-
-  // ---- launch: persistent workgroups ----------------------------------------
-  const int64_t total_chunks = running;
-  if (ctx->timing) CSM_HIP(hipEventRecord(ctx->ev0, st));
-  if (use_v2) {
-    // Block table: for every 64 chunks of a queue, the first pair_order entry.
-    std::vector<int32_t> blocks;
-    WorkQueues2 wq2{};
-    wq2.rot_chunk = rc;
-    for (int x = 0; x < kNumXcd; ++x) {
-      wq2.queue_begin[x] = wq.queue_begin[x];
-      wq2.queue_chunks[x] = wq.queue_chunks[x];
-      wq2.block_offset[x] = static_cast<int32_t>(blocks.size());
-      const int64_t qstart = prefix[wq.queue_begin[x]];
-      int e = wq.queue_begin[x];
-      for (int64_t c = 0; c < wq.queue_chunks[x]; c += 64) {
-        while (prefix[e + 1] - qstart <= c) ++e;
-        blocks.push_back(e);
-      }
-    }
-    wq2.queue_begin[kNumXcd] = wq.queue_begin[kNumXcd];
-    if ((rcode = ctx->blocks.Reserve(sizeof(int32_t) * std::max<size_t>(blocks.size(), 1))))
-      return rcode;
-    if (!blocks.empty())
-      CSM_HIP(hipMemcpyAsync(ctx->blocks.ptr, blocks.data(), sizeof(int32_t) * blocks.size(),
-                             hipMemcpyHostToDevice, st));
-    wq2.pair_order = wq.pair_order;
-    wq2.chunk_prefix = wq.chunk_prefix;
-    wq2.block_first = ctx->blocks.as<int32_t>();
-    // Per rotation: npad raw cells / k = 1 entries and capc cluster-list
-    // entries, 4 B cell + 1 B count each, 16-B aligned. capc = 3/4 npad holds
-    // the three cluster lists of a typical scan (0.55 npad on C2); a list
-    // that does not fit falls back to a finer one in the kernel.
-    int capc = (3 * max_npad / 4 + 63) & ~63;
-    if (const char* ce = std::getenv("CSM_CAPC_PCT"))  // A/B: cluster-list room, % of npad
-      capc = std::max(64, (std::atoi(ce) * max_npad / 100 + 63) & ~63);
-    const int lds_cap = 96 * 1024;
-    // Per rotation: npad raw cells (4 B) + capc cluster entries (4 B cell + 1 B count).
-    auto dyn_bytes = [&](int cap) { return static_cast<size_t>(rc) * (max_npad * 4 + cap * 5); };
-    while (capc > 0 && dyn_bytes(capc) > lds_cap) capc -= 64;
-    const size_t dyn_lds = (dyn_bytes(capc) + 15) & ~size_t{15};
-    // Node order: FIFO (level by level, the default) or LIFO (depth-first,
-    // CSM_SEARCH_ORDER=lifo).
-    const char* order_env = std::getenv("CSM_SEARCH_ORDER");
-    const bool fifo = !(order_env && std::strcmp(order_env, "lifo") == 0);
-    // Workgroups per CU: what registers and LDS allow (the runtime's
-    // occupancy query). CSM_WG_PER_CU caps it (A/B runs).
-    int per_cu = std::max(1, std::min(8, Fast2dSearchV2BlocksPerCu(hex, fifo, dyn_lds)));
-    if (const char* w = std::getenv("CSM_WG_PER_CU")) per_cu = std::max(1, std::min(per_cu, std::atoi(w)));
-    if (std::getenv("CSM_PROFILE2D"))
-      std::fprintf(stderr, "fast2d launch: %s %s, %d rotations per item, %zu B dynamic LDS (capc %d), %d workgroups per CU\n",
-                   hex ? "v5" : "v4", fifo ? "fifo" : "lifo", rc, dyn_lds, capc, per_cu);
-    const int grid = static_cast<int>(std::min<int64_t>(static_cast<int64_t>(ctx->num_cus) * per_cu,
-                                                        std::max<int64_t>(total_chunks, 1)));
-    // DFS stack spill: kSpill2 entries per persistent workgroup.
-    if ((rcode = ctx->spill.Reserve(sizeof(uint2) * kSpill2 * static_cast<size_t>(grid))))
-      return rcode;
-    CSM_HIP(LaunchFast2dSearchV2(grid, dyn_lds, st, ctx->submap_desc.as<SubmapDesc>(),
-                                 ctx->pair_desc.as<PairDesc>(), scans->points.as<float>(),
-                                 ctx->rot_table.as<float2>(), wq2,
-                                 ctx->counters.as<unsigned long long>(), ctx->best.as<uint64_t>(),
-                                 ctx->status.as<int32_t>(), ctx->stats.as<unsigned long long>(),
-                                 ctx->spill.as<uint2>(), max_npad, capc, hex, fifo));
-  } else {
-    const size_t dyn_lds = static_cast<size_t>(rc) * max_npad * sizeof(uint32_t);
-    const int grid = static_cast<int>(std::min<int64_t>(static_cast<int64_t>(ctx->num_cus) * 4,
-                                                        std::max<int64_t>(total_chunks, 1)));
-    CSM_HIP(LaunchFast2dSearch(grid, dyn_lds, st, ctx->submap_desc.as<SubmapDesc>(),
-                               ctx->pair_desc.as<PairDesc>(), scans->points.as<float>(),
-                               ctx->rot_table.as<float2>(), wq,
-                               ctx->counters.as<unsigned long long>(), ctx->best.as<uint64_t>(),
-                               ctx->status.as<int32_t>(), ctx->stats.as<unsigned long long>()));
-  }
-  if (ctx->timing) CSM_HIP(hipEventRecord(ctx->ev1, st));
-
-  std::vector<uint64_t> keys(np);
-  std::vector<int32_t> stat(np);
+  std::vector<uint64_t> keys, keys_hi;
+  std::vector<int32_t> stat;
   unsigned long long stats_host[kStatsWords] = {0};
-  CSM_HIP(hipMemcpyAsync(keys.data(), ctx->best.ptr, sizeof(uint64_t) * np,
-                         hipMemcpyDeviceToHost, st));
-  CSM_HIP(hipMemcpyAsync(stat.data(), ctx->status.ptr, sizeof(int32_t) * np,
-                         hipMemcpyDeviceToHost, st));
-  CSM_HIP(hipMemcpyAsync(stats_host, ctx->stats.ptr, sizeof(stats_host),
-                         hipMemcpyDeviceToHost, st));
-  CSM_HIP(hipStreamSynchronize(st));
+  if ((rcode = LaunchSearch(ctx, scans, pdesc, nullptr, plan, ctx->timing, &keys, &keys_hi, &stat,
+                            stats_host)))
+    return rcode;
   if (ctx->timing) {
     float ms = 0.f;
     CSM_HIP(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
@@ -336,6 +632,11 @@ int RunBatch(csm_context* ctx, csm_fast2d* const* submaps, int32_t num_submaps,
                    "%.1f score %.1f\n",
                    kp[0] / 1e6, kp[3] / 1e6, kp[1] / 1e6, kp[2] / 1e6);
   }
+
+  // ---- exactly tied maxima: the reference's pick (ResolveTies) ---------------
+  if (plan.use_v2 && (rcode = ResolveTies(ctx, submaps, scans, pdesc, rot_host, plan, stat, keys_hi,
+                                           &keys)))
+    return rcode;
 
   // ---- decode -----------------------------------------------------------------
   for (int k = 0; k < np; ++k) {

@@ -86,7 +86,8 @@ struct csm_context {
   hipStream_t stream = nullptr;
   std::mutex mu;
   csm::DevBuf submap_desc, pair_desc, rot_table, best, status, counters, pair_order,
-      chunk_prefix, blocks, stats, spill, single_points;
+      chunk_prefix, blocks, stats, spill, single_points, best_hi, ties, tie_count, sq_jobs,
+      sq_queries, sq_sums;
   csm::Rt2dCache rt2d;
   bool timing = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;

@@ -981,7 +981,9 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
                  uint64_t* __restrict__ best,
                  int32_t* __restrict__ status,
                  unsigned long long* __restrict__ stats,
-                 uint2* __restrict__ spill_base, int npad, int capc) {
+                 uint2* __restrict__ spill_base, int npad, int capc,
+                 uint64_t* __restrict__ best_hi, uint2* __restrict__ ties,
+                 int32_t* __restrict__ tie_count) {
   // Dynamic LDS: cells, rc * (npad + capc) words, then the cluster lists'
   // counts, rc * capc bytes. Rotation r's raw cells at r * npad; its cluster
   // lists packed in [rc * npad + r * capc, + capc).
@@ -1034,6 +1036,7 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
     const SubmapDesc& sm = submaps[pd.submap];
     const int n = pd.num_points;
     const int s_min = pd.max_rejected_sum;
+    const int collect_sum = pd.collect ? pd.collect_sum : -1;
     uint64_t* pair_best = best + pair_index;
     const int rot0 = Uniform(sh.item_chunk) * rc;
     const int nrot = min(rc, pd.num_scans - rot0);
@@ -1248,16 +1251,31 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
             }
             else
               key = PackLeafKey(sum, rot0 + r, xo, yo);
+            // Tie enumeration: every leaf at the pair's maximum sum.
+            if (collect_sum >= 0 && key != 0 && sum == collect_sum) {
+              const int slot = atomicAdd(&tie_count[pair_index], 1);
+              if (slot < kTieCap)
+                ties[static_cast<size_t>(pair_index) * kTieCap + slot] = make_uint2(
+                    static_cast<uint32_t>(rot0 + r),
+                    (static_cast<uint32_t>(xo) & 0xffff) | (static_cast<uint32_t>(yo) << 16));
+            }
           }
           if (__ballot(key != 0)) {  // wave-uniform: any leaf this pass
+            uint64_t hi = key ? HighLeafKey(key) : 0;
             for (int m = 32; m >= 1; m >>= 1) {
               const uint64_t o = __shfl_xor(key, m, 64);
               key = o > key ? o : key;
+              const uint64_t oh = __shfl_xor(hi, m, 64);
+              hi = oh > hi ? oh : hi;
             }
             if (lane == 0 && key > cur) {
               atomicMax(reinterpret_cast<unsigned long long*>(pair_best), key);
               atomicMax(reinterpret_cast<unsigned long long*>(&sh.best), key);
             }
+            // The largest-index leaf at the running maximum: a second maximal
+            // leaf shows as a different index at the final sum (ResolveTies).
+            if (lane == 0 && static_cast<uint32_t>(hi >> kSumShift) >= cur_sum)
+              atomicMax(reinterpret_cast<unsigned long long*>(best_hi + pair_index), hi);
           }
           // Inner survivors: deepest level on top (the batch pop takes the
           // top 64 entries at once, so order within a level is immaterial
@@ -1462,6 +1480,47 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
   if (stats && tid == 0) atomicMax(&stats[kStatHighWater], static_cast<unsigned long long>(sh.high_water));
 }
 
+// Tie resolution (csm_host.cc ResolveTies): exact level-d sums of listed
+// candidates, ScoreCandidates' integer sums (fast_correlative_scan_matcher_2d.cc
+// :314-333) over the row-major levels. One workgroup per (pair, rotation)
+// job: the rotation's scan is discretized into LDS exactly as the search
+// discretizes it (padding cells lie off every level), then each wave sums its
+// queries (level, x_off, y_off) over the points.
+__global__ void __launch_bounds__(256)
+fast2d_score_queries(const SubmapDesc* __restrict__ submaps, const PairDesc* __restrict__ pairs,
+                     const float* __restrict__ points, const float2* __restrict__ rot_table,
+                     const ScoreJob* __restrict__ jobs, const int4* __restrict__ queries,
+                     int32_t* __restrict__ sums, int npad) {
+  extern __shared__ __align__(16) uint32_t cells[];
+  const ScoreJob job = jobs[blockIdx.x];
+  const PairDesc pd = pairs[job.pair];
+  const SubmapDesc& sm = submaps[pd.submap];
+  const float2 q = rot_table[pd.rot_offset + job.rot];
+  for (int i = threadIdx.x; i < npad; i += blockDim.x) {
+    uint32_t c = 0x80008000u;  // (-32768, -32768): outside every level
+    if (i < pd.num_points) {
+      const float* p = points + 3 * (pd.point_offset + i);
+      float x, y;
+      RotateZDev(pd.pre_w, pd.pre_s, p[0], p[1], &x, &y);
+      RotateZDev(q.x, q.y, x, y, &x, &y);
+      const float px = __fadd_rn(pd.tx, x);
+      const float py = __fadd_rn(pd.ty, y);
+      const double cx = CellCoord(sm.max_y, py, sm.resolution);
+      const double cy = CellCoord(sm.max_x, px, sm.resolution);
+      if (fabs(cx) <= kIndexLimit && fabs(cy) <= kIndexLimit)
+        c = (static_cast<uint32_t>(static_cast<int>(cx)) & 0xffff) |
+            (static_cast<uint32_t>(static_cast<int>(cy)) << 16);
+    }
+    cells[i] = c;
+  }
+  __syncthreads();
+  for (int k = threadIdx.x >> 6; k < job.count; k += blockDim.x >> 6) {
+    const int4 qu = queries[job.first + k];
+    const int s = ScoreOne(cells, npad, MakeView(sm, qu.x), qu.y, qu.z);
+    if ((threadIdx.x & 63) == 0) sums[job.first + k] = s;
+  }
+}
+
 // Grid cells -> float through a 32768-entry table (ValueConversionTables;
 // the Ceres refinement's correspondence-cost grid).
 __global__ void cells_to_probability(const uint16_t* __restrict__ cells,
@@ -1510,16 +1569,26 @@ hipError_t LaunchFast2dSearchV2(int grid, size_t dyn_lds, hipStream_t st, const 
                                 const PairDesc* pairs, const float* points, const float2* rot_table,
                                 const WorkQueues2& queues, unsigned long long* counters,
                                 uint64_t* best, int32_t* status, unsigned long long* stats,
-                                uint2* spill, int npad, int capc, bool hex, bool fifo) {
+                                uint2* spill, int npad, int capc, bool hex, bool fifo,
+                                uint64_t* best_hi, uint2* ties, int32_t* tie_count) {
 #define CSM_LAUNCH_V4(H, F)                                                                        \
   hipLaunchKernelGGL((fast2d_search_v4<H, F>), dim3(grid), dim3(kSearchThreads), dyn_lds, st,     \
                      submaps, pairs, points, rot_table, queues, counters, best, status, stats,     \
-                     spill, npad, capc)
+                     spill, npad, capc, best_hi, ties, tie_count)
   if (hex && fifo) CSM_LAUNCH_V4(true, true);
   else if (hex) CSM_LAUNCH_V4(true, false);
   else if (fifo) CSM_LAUNCH_V4(false, true);
   else CSM_LAUNCH_V4(false, false);
 #undef CSM_LAUNCH_V4
+  return hipGetLastError();
+}
+
+hipError_t LaunchFast2dScoreQueries(int num_jobs, int npad, hipStream_t st, const SubmapDesc* submaps,
+                                    const PairDesc* pairs, const float* points,
+                                    const float2* rot_table, const ScoreJob* jobs,
+                                    const int4* queries, int32_t* sums) {
+  hipLaunchKernelGGL(fast2d_score_queries, dim3(num_jobs), dim3(256), sizeof(uint32_t) * npad, st,
+                     submaps, pairs, points, rot_table, jobs, queries, sums, npad);
   return hipGetLastError();
 }
 

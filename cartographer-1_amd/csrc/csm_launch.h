@@ -23,7 +23,12 @@ hipError_t LaunchFast2dSearchV2(int grid, size_t dyn_lds, hipStream_t st, const 
                                 const PairDesc* pairs, const float* points, const float2* rot_table,
                                 const WorkQueues2& queues, unsigned long long* counters,
                                 uint64_t* best, int32_t* status, unsigned long long* stats,
-                                uint2* spill, int npad, int capc, bool hex, bool fifo);
+                                uint2* spill, int npad, int capc, bool hex, bool fifo,
+                                uint64_t* best_hi, uint2* ties, int32_t* tie_count);
+hipError_t LaunchFast2dScoreQueries(int num_jobs, int npad, hipStream_t st, const SubmapDesc* submaps,
+                                    const PairDesc* pairs, const float* points,
+                                    const float2* rot_table, const ScoreJob* jobs,
+                                    const int4* queries, int32_t* sums);
 // Resident workgroups per CU of the v4/v5 search kernel at this dynamic LDS
 // size (registers and LDS; 0 if the query fails).
 int Fast2dSearchV2BlocksPerCu(bool hex, bool fifo, size_t dyn_lds);

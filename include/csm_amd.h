@@ -101,6 +101,12 @@ typedef struct csm_timing {
    * (entries) any workgroup reached (2D and 3D). */
   int64_t search_errors;
   int64_t stack_high_water;
+  /* 2D searches whose maximum was reached by more than one leaf (the
+   * reference's pick among them is restored, DESIGN.md §2 "Ties"), and those
+   * left at the smallest (rotation, x, y) leaf because more than 4096 leaves
+   * tied (counted whether or not timing is enabled). */
+  int64_t tied_pairs;
+  int64_t ties_unresolved;
 } csm_timing;
 void csm_context_enable_timing(csm_context* ctx, int32_t enable);
 void csm_context_get_timing(csm_context* ctx, csm_timing* out);

@@ -37,7 +37,12 @@ def full_submap_center(limits, cells):
     return (mx - half * cells.shape[0], my - half * cells.shape[1], 0.0)
 
 
-def assert_fast_parity(oracle, om, limits, cells, gpu, ref, full, init, cloud):
+def assert_fast_parity(oracle, om, limits, cells, gpu, ref, full, init, cloud, ties_ok=False):
+    """Same match decision, bit-identical score and the reference's pose. The
+    v4/v5 kernels restore the reference's pick among exactly tied leaves
+    (csm_host.cc ResolveTies), so the pose must be identical; only the v1
+    kernel (clouds past 8192 points) keeps the smallest tied leaf
+    (ties_ok=True), which is then checked to score exactly the maximum."""
     g_ok, g_score, g_pose = gpu
     o_ok, o_score, o_pose = ref[:3]
     assert g_ok == o_ok, (gpu, ref[:3])
@@ -46,6 +51,7 @@ def assert_fast_parity(oracle, om, limits, cells, gpu, ref, full, init, cloud):
     assert np.float32(g_score) == np.float32(o_score), (g_score, o_score)
     if tuple(g_pose) == tuple(o_pose):
         return "exact"
+    assert ties_ok, ("pose differs from the reference's pick", g_pose, o_pose)
     # Exact tie: recover the GPU leaf (scan index, offsets) and score it.
     res = limits[0]
     lin, ang = (1e6 * res, math.pi) if full else (om.lin, om.ang)
@@ -109,7 +115,8 @@ def test_correct_pose_match(csm, oracle, search_kernel):
         init = (0.0, 0.0, 0.0)
         gpu = m.Match(init, cloud, 0.1)
         ref = om.match(init, cloud, 0.1)
-        kinds.append(assert_fast_parity(oracle, om, limits, cells, gpu, ref, False, init, cloud))
+        kinds.append(assert_fast_parity(oracle, om, limits, cells, gpu, ref, False, init, cloud,
+                                        ties_ok=search_kernel == "v1"))
         assert gpu[0] and gpu[1] > 0.1
         # The reference test's own acceptance: pose within IsNearly 0.03.
         assert abs(gpu[2][0] - expected[0]) < 0.1 and abs(gpu[2][1] - expected[1]) < 0.1
@@ -137,7 +144,8 @@ def test_full_submap_matching(csm, oracle, search_kernel):
         gpu = m.MatchFullSubmap(cloud, 0.1)
         ref = om.match_full_submap(cloud, 0.1)
         init = full_submap_center(limits, cells)
-        assert_fast_parity(oracle, om, limits, cells, gpu, ref, True, init, cloud)
+        assert_fast_parity(oracle, om, limits, cells, gpu, ref, True, init, cloud,
+                           ties_ok=search_kernel == "v1")
         assert gpu[0]
 
 
@@ -191,7 +199,7 @@ def test_synthetic_full_submap_pairs(csm, oracle, world, depth_mode, search_kern
         gpu = (res[k]["status"] == 0, float(res[k]["score"]),
                (res[k]["x"], res[k]["y"], res[k]["theta"]))
         assert_fast_parity(oracle, om, limits, g.cells, gpu, ref, True,
-                           full_submap_center(limits, g.cells), cloud)
+                           full_submap_center(limits, g.cells), cloud, ties_ok=search_kernel == "v1")
         matched += int(gpu[0])
     assert matched >= 3
 
@@ -230,7 +238,8 @@ def test_match_window_mode_parity(csm, oracle, world, search_kernel):
         cloud = world.cloud(n)
         gpu = m.Match(init, cloud, 0.55)
         ref = om.match(init, cloud, 0.55)
-        assert_fast_parity(oracle, om, limits, g.cells, gpu, ref, False, init, cloud)
+        assert_fast_parity(oracle, om, limits, g.cells, gpu, ref, False, init, cloud,
+                           ties_ok=search_kernel == "v1")
 
 
 def test_edge_cases(csm, oracle, search_kernel):
@@ -246,7 +255,8 @@ def test_edge_cases(csm, oracle, search_kernel):
     om = oracle.fast2d(limits, cells, 0.5, 0.3, 4)
     gpu = m.MatchFullSubmap(cloud, 0.0)
     ref = om.match_full_submap(cloud, 0.0)
-    assert_fast_parity(oracle, om, limits, cells, gpu, ref, True, full_submap_center(limits, cells), cloud)
+    assert_fast_parity(oracle, om, limits, cells, gpu, ref, True, full_submap_center(limits, cells), cloud,
+                       ties_ok=search_kernel == "v1")
     # min_score above every attainable score: no match.
     assert m.MatchFullSubmap(cloud, 0.95)[0] is False
     # 1x1 grid.
@@ -256,7 +266,7 @@ def test_edge_cases(csm, oracle, search_kernel):
     gpu = m1.Match((0.0, 0.0, 0.0), cloud, 0.0)
     ref = om1.match((0.0, 0.0, 0.0), cloud, 0.0)
     assert_fast_parity(oracle, om1, (0.05, 0.05, 0.05), np.full((1, 1), 20000, np.uint16), gpu, ref,
-                       False, (0.0, 0.0, 0.0), cloud)
+                       False, (0.0, 0.0, 0.0), cloud, ties_ok=search_kernel == "v1")
 
 
 def _run_list_clouds(world):
@@ -300,5 +310,6 @@ def test_run_lists_parity(csm, oracle, world, search_kernel):
                (float(res[k]["x"]), float(res[k]["y"]), float(res[k]["theta"])))
         ref = om.match_full_submap(c, 0.3)
         kinds.append(assert_fast_parity(oracle, om, limits, g.cells, gpu, ref, True,
-                                        full_submap_center(limits, g.cells), c))
+                                        full_submap_center(limits, g.cells), c,
+                                        ties_ok=search_kernel == "v1"))
     assert kinds.count("nomatch") < len(kinds)

@@ -24,7 +24,7 @@ def main():
     if not per:
         sys.exit("no FETCH_SIZE rows for fast2d_search_v4")
     kb = sum(per.values()) / len(per)
-    t = {"kernel": "fast2d_search_v4 (scan clusters)", "commit_kernel": tag,
+    t = {"kernel": "fast2d_search_v4 (v5: FIFO order, hex planes, scan clusters)", "commit_kernel": tag,
          "workload": "C2 bench.py --no-cpu --no-rt --no-3d --steps 1 --warmup 0",
          "nodes": 500, "submaps_per_rank": 50, "min_score": 0.55, "search_depth": 0,
          "launches": len(per), "fetch_size_kb_per_launch": kb, "gfx950_fetch_correction": 2.0,
@@ -37,6 +37,9 @@ def main():
                               f"--no-cpu --steps 1 --warmup 0 (the first {submaps} submaps of the "
                               f"2000 x 1000 queue)",
                   "nodes": nodes, "chunk": chunk, "submaps": submaps})
+        t["workload"] = (f"C3 chunk launches: bench.py --no-cpu --no-rt --no-3d --steps 1 --warmup 0 "
+                         f"--c3-slice {submaps} (the first {submaps} submaps of the 2000 x 1000 queue, "
+                         f"{chunk}-submap chunks)")
     json.dump(t, open(out, "w"), indent=1)
     print(json.dumps(t))
 
