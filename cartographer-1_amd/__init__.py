@@ -259,6 +259,10 @@ _SIGNATURES = {
                                          C.POINTER(C.c_uint16), C.c_int64, C.c_int32,
                                          C.POINTER(C.c_void_p)]),
     "csm_hybrid_grid_destroy": (None, [C.c_void_p]),
+    "csm_hybrid_grid_get_probability": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32), C.c_int64,
+                                                  C.POINTER(C.c_float)]),
+    "csm_hybrid_grid_interpolate": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.c_int64,
+                                              C.POINTER(C.c_double)]),
     "csm_hybrid_grid_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32),
                                        C.POINTER(C.c_int32)]),
     "csm_rt3d_window": (C.c_int, [C.POINTER(RtOptions), C.c_float, C.POINTER(C.c_float),

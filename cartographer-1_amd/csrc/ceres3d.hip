@@ -359,6 +359,40 @@ ceres3d_refine(const Refine3Desc* __restrict__ items, const float* __restrict__ 
   }
 }
 
+// Test-visible lookups on a device grid (csm_hybrid_grid_get_probability /
+// _interpolate): the same Prob / Interpolate the refinement kernel uses.
+__global__ void grid_probability(GridView3 g, const int32_t* __restrict__ ijk, int64_t n,
+                                 float* __restrict__ out) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = static_cast<float>(Prob(g, ijk[3 * i], ijk[3 * i + 1], ijk[3 * i + 2]));
+}
+__global__ void grid_interpolate(GridView3 g, const double* __restrict__ xyz, int64_t n,
+                                 double* __restrict__ out) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = Interpolate(g, xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2], nullptr);
+}
+
+template <typename In, typename Out, typename K>
+int GridLookup(const csm_hybrid_grid* g, const In* in, int64_t n, Out* out, K kernel) {
+  if (!g || n < 0 || (n > 0 && (!in || !out))) return CSM_EINVAL;
+  if (n == 0) return CSM_OK;
+  csm_context* ctx = g->ctx;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  if (hipSetDevice(ctx->device) != hipSuccess) return CSM_EHIP;
+  DevBuf din, dout;
+  int rc;
+  if ((rc = din.Reserve(sizeof(In) * 3 * n)) || (rc = dout.Reserve(sizeof(Out) * n))) return rc;
+  hipStream_t st = ctx->stream;
+  CSM_HIP(hipMemcpyAsync(din.ptr, in, sizeof(In) * 3 * n, hipMemcpyHostToDevice, st));
+  const GridView3 view{g->prob.as<float>(), g->brick, g->resolution};
+  hipLaunchKernelGGL(kernel, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, st, view,
+                     din.as<In>(), n, dout.as<Out>());
+  CSM_HIP(hipGetLastError());
+  CSM_HIP(hipMemcpyAsync(out, dout.ptr, sizeof(Out) * n, hipMemcpyDeviceToHost, st));
+  CSM_HIP(hipStreamSynchronize(st));
+  return CSM_OK;
+}
+
 }  // namespace
 }  // namespace csm
 
@@ -441,6 +475,16 @@ int csm_ceres3d_refine_batch(csm_context* ctx, const csm_hybrid_grid* const* gri
     for (int a = 0; a < 4; ++a) out[i].q[a] = host[7 * i + 3 + a];
   }
   return CSM_OK;
+}
+
+int csm_hybrid_grid_get_probability(const csm_hybrid_grid* g, const int32_t* xyz_indices, int64_t n,
+                                    float* out) {
+  return csm::GridLookup(g, xyz_indices, n, out, csm::grid_probability);
+}
+
+int csm_hybrid_grid_interpolate(const csm_hybrid_grid* g, const double* xyz, int64_t n,
+                                double* out) {
+  return csm::GridLookup(g, xyz, n, out, csm::grid_interpolate);
 }
 
 }  // extern "C"

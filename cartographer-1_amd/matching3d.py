@@ -49,6 +49,25 @@ class HybridGrid:
         _check(self._lib.csm_hybrid_grid_info(self.handle, o, d, C.byref(g)), "csm_hybrid_grid_info")
         return tuple(o), tuple(d), g.value
 
+    def get_probability(self, indices):
+        """HybridGrid::GetProbability at cell indices (n, 3), on the device."""
+        idx = np.ascontiguousarray(np.asarray(indices, np.int32).reshape(-1, 3))
+        out = np.zeros(len(idx), np.float32)
+        _check(self._lib.csm_hybrid_grid_get_probability(self.handle, _ptr(idx, C.c_int32), len(idx),
+                                                         _ptr(out, C.c_float)),
+               "csm_hybrid_grid_get_probability")
+        return out
+
+    def interpolate(self, points):
+        """InterpolatedProbabilityGrid::GetInterpolatedValue at points (n, 3),
+        on the device (the CeresScanMatcher3D kernel's interpolation)."""
+        xyz = np.ascontiguousarray(np.asarray(points, np.float64).reshape(-1, 3))
+        out = np.zeros(len(xyz), np.float64)
+        _check(self._lib.csm_hybrid_grid_interpolate(self.handle, _ptr(xyz, C.c_double), len(xyz),
+                                                     _ptr(out, C.c_double)),
+               "csm_hybrid_grid_interpolate")
+        return out
+
     def close(self):
         if getattr(self, "handle", None):
             self._lib.csm_hybrid_grid_destroy(self.handle)

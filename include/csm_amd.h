@@ -299,6 +299,15 @@ void csm_hybrid_grid_destroy(csm_hybrid_grid* g);
 /* Bounding box origin / extent of the device brick and the grid size. */
 int csm_hybrid_grid_info(const csm_hybrid_grid* g, int32_t* origin3, int32_t* dims3,
                          int32_t* grid_size);
+/* Test-visible lookups on the device grid, with the kernels' own code:
+ * HybridGrid::GetProbability at n cell indices (hybrid_grid.h:496-499; unknown
+ * cells give kMinProbability), and InterpolatedProbabilityGrid::
+ * GetInterpolatedValue at n points (interpolated_grid.h:48-105, the
+ * CeresScanMatcher3D cost's interpolation). */
+int csm_hybrid_grid_get_probability(const csm_hybrid_grid* g, const int32_t* xyz_indices, int64_t n,
+                                    float* out);
+int csm_hybrid_grid_interpolate(const csm_hybrid_grid* g, const double* xyz, int64_t n,
+                                double* out);
 
 /* transform::Rigid3d: translation and rotation quaternion (w, x, y, z). */
 typedef struct csm_pose3d {

@@ -41,7 +41,11 @@ struct Step {
   double db() const { return -2. * ttt + 3. * tt; }
 };
 
-// InterpolatedGrid::GetInterpolatedValue and its gradient in (x, y, z).
+}  // namespace
+
+// InterpolatedGrid::GetInterpolatedValue and its gradient in (x, y, z)
+// (interpolated_grid.h:48-105; tests pin it with interpolated_grid_test.cc
+// and the fork's hybrid_test.txt).
 double Interpolate(const HybridGrid& g, double x, double y, double z, double grad[3]) {
   const float res = g.resolution();
   // CenterOfLowerVoxel (:118-134): the point is cast to float first.
@@ -79,6 +83,8 @@ double Interpolate(const HybridGrid& g, double x, double y, double z, double gra
   }
   return v;
 }
+
+namespace {
 
 // Eigen _transformVector: v + w * uv + q.vec x uv, uv = 2 q.vec x v; and its
 // derivative in (w, x, y, z) (3 x 4, row-major).

@@ -163,6 +163,10 @@ class HybridGrid : public HybridGridBase3<uint16_t> {
   std::vector<uint16_t*> update_indices_;
 };
 
+// InterpolatedProbabilityGrid::GetInterpolatedValue (interpolated_grid.h:48-105)
+// and its gradient (grad may be null); ceres3d.cc.
+double Interpolate(const HybridGrid& g, double x, double y, double z, double grad[3]);
+
 // range_data_inserter_3d.cc:100-136 (hits, then the last num_free_space_voxels
 // misses of every ray).
 class RangeDataInserter3D {

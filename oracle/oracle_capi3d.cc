@@ -65,6 +65,22 @@ int64_t oracle_hgrid_cells(void* g, int32_t* ijk, uint16_t* values, int64_t capa
   return n;
 }
 int oracle_hgrid_grid_size(void* g) { return static_cast<HybridGrid*>(g)->grid_size(); }
+// InterpolatedProbabilityGrid::GetInterpolatedValue at n points (x, y, z).
+void oracle_hgrid_interpolate(void* g, const double* xyz, int64_t n, double* out) {
+  const auto* h = static_cast<HybridGrid*>(g);
+  for (int64_t i = 0; i < n; ++i)
+    out[i] = Interpolate(*h, xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2], nullptr);
+}
+// HybridGridBase::GetCellIndex (float division, lround) of n points.
+void oracle_hgrid_cell_index(void* g, const float* xyz, int64_t n, int32_t* out) {
+  const auto* h = static_cast<HybridGrid*>(g);
+  for (int64_t i = 0; i < n; ++i) {
+    const Idx3 c = h->GetCellIndex(Vec3f{xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2]});
+    out[3 * i] = c.x;
+    out[3 * i + 1] = c.y;
+    out[3 * i + 2] = c.z;
+  }
+}
 float oracle_hgrid_probability(void* g, int x, int y, int z) {
   return static_cast<HybridGrid*>(g)->GetProbability(Idx3{x, y, z});
 }

@@ -416,6 +416,7 @@ TEST(OccupiedSpaceCostFunction2DSmokeTest) {
 int RunRefTests3D(int* checks);    // ref_tests_3d.cc
 int RunRefTestsTSDF(int* checks);  // ref_tests_tsdf.cc
 int RunRefTestsVoxel(int* checks);  // ref_tests_voxel.cc
+int RunRefTestsGrids(int* checks);  // ref_tests_grids.cc
 
 int main() {
   for (const TestCase& t : Registry()) {
@@ -424,12 +425,13 @@ int main() {
     t.fn();
     std::printf("%-70s %s\n", t.name, g_failures == before ? "OK" : "FAILED");
   }
-  int checks3d = 0, checks_tsdf = 0, checks_voxel = 0;
+  int checks3d = 0, checks_tsdf = 0, checks_voxel = 0, checks_grids = 0;
   const int failures3d = RunRefTests3D(&checks3d);
   const int failures_tsdf = RunRefTestsTSDF(&checks_tsdf);
   const int failures_voxel = RunRefTestsVoxel(&checks_voxel);
-  const int failures = g_failures + failures3d + failures_tsdf + failures_voxel;
-  std::printf("checks: %d (2D) + %d (3D) + %d (TSDF) + %d (voxel filter), failures: %d\n",
-              g_checks, checks3d, checks_tsdf, checks_voxel, failures);
+  const int failures_grids = RunRefTestsGrids(&checks_grids);
+  const int failures = g_failures + failures3d + failures_tsdf + failures_voxel + failures_grids;
+  std::printf("checks: %d (2D) + %d (3D) + %d (TSDF) + %d (voxel filter) + %d (grids), failures: %d\n",
+              g_checks, checks3d, checks_tsdf, checks_voxel, checks_grids, failures);
   return failures == 0 ? 0 : 1;
 }

@@ -254,6 +254,8 @@ _SIG3D = {
     "oracle_hgrid_cells": (I64, [VP, P(I32), P(C.c_uint16), I64]),
     "oracle_hgrid_grid_size": (I32, [VP]),
     "oracle_hgrid_probability": (F, [VP, I32, I32, I32]),
+    "oracle_hgrid_interpolate": (None, [VP, P(D), I64, P(D)]),
+    "oracle_hgrid_cell_index": (None, [VP, P(F), I64, P(I32)]),
     "oracle_histogram": (None, [P(F), I32, I32, P(F)]),
     "oracle_rotational_match": (None, [P(F), P(F), I32, F, P(F), I32, P(F)]),
     "oracle_fast3d_create": (VP, [VP, VP, P(F), I32, P(D)]),
@@ -317,6 +319,18 @@ class OracleHybridGrid:
 
     def probability(self, x, y, z):
         return self.o.lib.oracle_hgrid_probability(self.h, x, y, z)
+
+    def interpolate(self, points):
+        xyz = np.ascontiguousarray(np.asarray(points, np.float64).reshape(-1, 3))
+        out = np.zeros(len(xyz))
+        self.o.lib.oracle_hgrid_interpolate(self.h, _p(xyz, D), len(xyz), _p(out, D))
+        return out
+
+    def cell_index(self, points):
+        xyz = np.ascontiguousarray(np.asarray(points, np.float32).reshape(-1, 3))
+        out = np.zeros((len(xyz), 3), np.int32)
+        self.o.lib.oracle_hgrid_cell_index(self.h, _p(xyz, F), len(xyz), _p(out, I32))
+        return out
 
 
 class OracleFast3D:
