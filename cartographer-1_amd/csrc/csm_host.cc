@@ -221,7 +221,7 @@ int LaunchSearch(csm_context* ctx, csm_scan_set* scans, const std::vector<PairDe
                                  ctx->status.as<int32_t>(), ctx->stats.as<unsigned long long>(),
                                  ctx->spill.as<uint2>(), max_npad, capc, plan.hex, plan.fifo,
                                  ctx->best_hi.as<uint64_t>(), ties ? ctx->ties.as<uint2>() : nullptr,
-                                 ctx->tie_count.as<int32_t>()));
+                                 ctx->tie_count.as<int32_t>(), ties != nullptr));
   } else {
     const size_t dyn_lds = static_cast<size_t>(rc) * max_npad * sizeof(uint32_t);
     const int grid = static_cast<int>(std::min<int64_t>(static_cast<int64_t>(ctx->num_cus) * 4,

@@ -970,7 +970,9 @@ __device__ __forceinline__ uint32_t ClusterMask(int sl) {
 // its 256-entry LDS ring fits 6 in LDS too; measured best).
 #define CSM_V4_WAVES 6
 #endif
-template <bool kHex, bool kFifo>
+// kCollect: the tie-enumeration launch (PairDesc::collect_sum, csm_host.cc
+// ResolveTies), its own symbol so profiles tell it from the search.
+template <bool kHex, bool kFifo, bool kCollect>
 __global__ void __launch_bounds__(kSearchThreads) __attribute__((amdgpu_waves_per_eu(CSM_V4_WAVES)))
 fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
                  const PairDesc* __restrict__ pairs,
@@ -1036,7 +1038,7 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
     const SubmapDesc& sm = submaps[pd.submap];
     const int n = pd.num_points;
     const int s_min = pd.max_rejected_sum;
-    const int collect_sum = pd.collect ? pd.collect_sum : -1;
+    const int collect_sum = kCollect ? pd.collect_sum : -1;
     uint64_t* pair_best = best + pair_index;
     const int rot0 = Uniform(sh.item_chunk) * rc;
     const int nrot = min(rc, pd.num_scans - rot0);
@@ -1570,15 +1572,22 @@ hipError_t LaunchFast2dSearchV2(int grid, size_t dyn_lds, hipStream_t st, const 
                                 const WorkQueues2& queues, unsigned long long* counters,
                                 uint64_t* best, int32_t* status, unsigned long long* stats,
                                 uint2* spill, int npad, int capc, bool hex, bool fifo,
-                                uint64_t* best_hi, uint2* ties, int32_t* tie_count) {
-#define CSM_LAUNCH_V4(H, F)                                                                        \
-  hipLaunchKernelGGL((fast2d_search_v4<H, F>), dim3(grid), dim3(kSearchThreads), dyn_lds, st,     \
+                                uint64_t* best_hi, uint2* ties, int32_t* tie_count, bool collect) {
+#define CSM_LAUNCH_V4(H, F, K)                                                                     \
+  hipLaunchKernelGGL((fast2d_search_v4<H, F, K>), dim3(grid), dim3(kSearchThreads), dyn_lds, st,  \
                      submaps, pairs, points, rot_table, queues, counters, best, status, stats,     \
                      spill, npad, capc, best_hi, ties, tie_count)
-  if (hex && fifo) CSM_LAUNCH_V4(true, true);
-  else if (hex) CSM_LAUNCH_V4(true, false);
-  else if (fifo) CSM_LAUNCH_V4(false, true);
-  else CSM_LAUNCH_V4(false, false);
+  if (collect) {
+    if (hex && fifo) CSM_LAUNCH_V4(true, true, true);
+    else if (hex) CSM_LAUNCH_V4(true, false, true);
+    else if (fifo) CSM_LAUNCH_V4(false, true, true);
+    else CSM_LAUNCH_V4(false, false, true);
+  } else {
+    if (hex && fifo) CSM_LAUNCH_V4(true, true, false);
+    else if (hex) CSM_LAUNCH_V4(true, false, false);
+    else if (fifo) CSM_LAUNCH_V4(false, true, false);
+    else CSM_LAUNCH_V4(false, false, false);
+  }
 #undef CSM_LAUNCH_V4
   return hipGetLastError();
 }
@@ -1596,13 +1605,13 @@ int Fast2dSearchV2BlocksPerCu(bool hex, bool fifo, size_t dyn_lds) {
   int blocks = 0;
   hipError_t e;
   if (hex && fifo)
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fast2d_search_v4<true, true>, kSearchThreads, dyn_lds);
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fast2d_search_v4<true, true, false>, kSearchThreads, dyn_lds);
   else if (hex)
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fast2d_search_v4<true, false>, kSearchThreads, dyn_lds);
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fast2d_search_v4<true, false, false>, kSearchThreads, dyn_lds);
   else if (fifo)
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fast2d_search_v4<false, true>, kSearchThreads, dyn_lds);
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fast2d_search_v4<false, true, false>, kSearchThreads, dyn_lds);
   else
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fast2d_search_v4<false, false>, kSearchThreads, dyn_lds);
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fast2d_search_v4<false, false, false>, kSearchThreads, dyn_lds);
   return e == hipSuccess ? blocks : 0;
 }
 

@@ -24,7 +24,7 @@ hipError_t LaunchFast2dSearchV2(int grid, size_t dyn_lds, hipStream_t st, const 
                                 const WorkQueues2& queues, unsigned long long* counters,
                                 uint64_t* best, int32_t* status, unsigned long long* stats,
                                 uint2* spill, int npad, int capc, bool hex, bool fifo,
-                                uint64_t* best_hi, uint2* ties, int32_t* tie_count);
+                                uint64_t* best_hi, uint2* ties, int32_t* tie_count, bool collect);
 hipError_t LaunchFast2dScoreQueries(int num_jobs, int npad, hipStream_t st, const SubmapDesc* submaps,
                                     const PairDesc* pairs, const float* points,
                                     const float2* rot_table, const ScoreJob* jobs,

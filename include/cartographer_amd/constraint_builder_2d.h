@@ -19,7 +19,7 @@
 // device, and WhenDone gathers the accepted constraints to rank 0 in
 // submission order (constraint_gather.h). Rank 0's callback gets the whole
 // result, the other ranks' callbacks an empty one; the metric counters are
-// summed over the ranks at every WhenDone.
+// summed over the ranks and last_error reduced over them at every WhenDone.
 #ifndef CARTOGRAPHER_AMD_CONSTRAINT_BUILDER_2D_H_
 #define CARTOGRAPHER_AMD_CONSTRAINT_BUILDER_2D_H_
 
@@ -149,6 +149,8 @@ class ConstraintBuilder2D {
   // Rank 0 receives every rank's accepted constraints in slot order; the
   // metric deltas since the last WhenDone are summed over the ranks.
   void GatherToRoot(Result* result) {
+    CheckSameSubmissions(comm_, static_cast<int64_t>(constraints_.size()));
+    last_error = ReduceLastError(comm_, last_error);
     std::vector<ConstraintRecord> local;
     for (size_t slot = 0; slot < constraints_.size(); ++slot) {
       const Constraint* c = constraints_[slot].get();

@@ -15,6 +15,15 @@
 // batch by the CeresScanMatcher3D restatement (:264-275;
 // csm_ceres3d_refine_batch, parity with Ceres unpinned) unless
 // options.refine_with_ceres is off.
+//
+// Multi-GPU (set_communicator), as ConstraintBuilder2D: every rank makes the
+// same calls; a rank builds matchers for and searches only the submaps it
+// owns (ShardOwner) on its own device; WhenDone gathers the accepted
+// constraints to rank 0 as ConstraintRecord3D in submission order
+// (constraint_gather.h), sums the counters and reduces last_error over the
+// ranks. The score lists (constraint_scores, global_constraint_scores,
+// rotational_scores, low_resolution_scores) are appended at WhenDone from the
+// delivered result, in submission order, so on rank 0 they cover every rank.
 #ifndef CARTOGRAPHER_AMD_CONSTRAINT_BUILDER_3D_H_
 #define CARTOGRAPHER_AMD_CONSTRAINT_BUILDER_3D_H_
 
@@ -27,6 +36,7 @@
 #include <vector>
 
 #include "constraint_builder_common.h"
+#include "constraint_gather.h"
 #include "scan_matching_3d.h"
 
 namespace cartographer_amd {
@@ -46,6 +56,7 @@ struct Constraint3D {
   double translation_weight = 0., rotation_weight = 0.;
   enum Tag { INTRA_SUBMAP, INTER_SUBMAP } tag = INTER_SUBMAP;
   float score = 0.f, rotational_score = 0.f, low_resolution_score = 0.f;
+  bool global = false;  // found by MaybeAddGlobalConstraint (the metrics split)
 };
 
 class ConstraintBuilder3D {
@@ -55,6 +66,10 @@ class ConstraintBuilder3D {
   explicit ConstraintBuilder3D(const ConstraintBuilderOptions& options,
                                csm_context* context = nullptr)
       : options_(options), context_(context ? context : ThreadContext()) {}
+
+  // Shards the search over the ranks of `comm` (not owned; outlives the
+  // builder). Call before the first MaybeAdd*.
+  void set_communicator(csm_comm* comm) { comm_ = comm; }
 
   void MaybeAddConstraint(const SubmapId& submap_id, const Submap3DView* submap,
                           const NodeId& node_id, const TrajectoryNodeData3D* constant_data,
@@ -85,9 +100,19 @@ class ConstraintBuilder3D {
   void WhenDone(const std::function<void(const Result&)>& callback) {
     Flush();
     Result result;
-    for (auto& c : constraints_)
-      if (c) result.push_back(*c);
+    if (comm_ && csm_comm_size(comm_) > 1) {
+      GatherToRoot(&result);
+    } else {
+      for (auto& c : constraints_)
+        if (c) result.push_back(*c);
+    }
     constraints_.clear();
+    // The score metrics (constraint_builder_3d.cc:46-59), submission order.
+    for (const Constraint3D& c : result) {
+      (c.global ? global_constraint_scores : constraint_scores).push_back(c.score);
+      rotational_scores.push_back(c.rotational_score);
+      low_resolution_scores.push_back(c.low_resolution_score);
+    }
     callback(result);
   }
 
@@ -126,9 +151,75 @@ class ConstraintBuilder3D {
     size_t slot;
   };
 
+  bool Owned(const SubmapId& id) const {
+    return !comm_ || csm_comm_size(comm_) <= 1 ||
+           ShardOwner(id.trajectory_id, id.submap_index, csm_comm_size(comm_)) ==
+               csm_comm_rank(comm_);
+  }
+
+  // Rank 0 receives every rank's accepted constraints in slot order; the
+  // metric counter deltas since the last WhenDone are summed over the ranks.
+  void GatherToRoot(Result* result) {
+    CheckSameSubmissions(comm_, static_cast<int64_t>(constraints_.size()));
+    last_error = ReduceLastError(comm_, last_error);
+    std::vector<ConstraintRecord3D> local;
+    for (size_t slot = 0; slot < constraints_.size(); ++slot) {
+      const Constraint3D* c = constraints_[slot].get();
+      if (!c) continue;
+      ConstraintRecord3D r{};
+      r.slot = static_cast<int64_t>(slot);
+      r.submap_trajectory = c->submap_id.trajectory_id;
+      r.submap_index = c->submap_id.submap_index;
+      r.node_trajectory = c->node_id.trajectory_id;
+      r.node_index = c->node_id.node_index;
+      for (int a = 0; a < 3; ++a) r.t[a] = c->relative_pose.t[a];
+      const Quaterniond& q = c->relative_pose.rotation;
+      r.q[0] = q.w;
+      r.q[1] = q.x;
+      r.q[2] = q.y;
+      r.q[3] = q.z;
+      r.score = c->score;
+      r.rotational_score = c->rotational_score;
+      r.low_resolution_score = c->low_resolution_score;
+      r.tag = static_cast<int32_t>(c->tag);
+      r.global = c->global ? 1 : 0;
+      local.push_back(r);
+    }
+    const std::vector<ConstraintRecord3D> all = GatherRecords(comm_, local);
+    int64_t d[5] = {constraints_searched - reduced_[0], constraints_found - reduced_[1],
+                    global_constraints_searched - reduced_[2],
+                    global_constraints_found - reduced_[3], constraints_failed - reduced_[4]};
+    CommCheck(csm_comm_allreduce_i64(comm_, d, 5, CSM_REDUCE_SUM), "csm_comm_allreduce_i64");
+    int64_t* counters[5] = {&constraints_searched, &constraints_found, &global_constraints_searched,
+                            &global_constraints_found, &constraints_failed};
+    for (int k = 0; k < 5; ++k) {
+      reduced_[k] += d[k];
+      *counters[k] = reduced_[k];
+    }
+    for (const ConstraintRecord3D& r : all) {
+      Constraint3D c;
+      c.submap_id = SubmapId{r.submap_trajectory, r.submap_index};
+      c.node_id = NodeId{r.node_trajectory, r.node_index};
+      for (int a = 0; a < 3; ++a) c.relative_pose.t[a] = r.t[a];
+      c.relative_pose.rotation = Quaterniond{r.q[0], r.q[1], r.q[2], r.q[3]};
+      c.translation_weight = options_.loop_closure_translation_weight;
+      c.rotation_weight = options_.loop_closure_rotation_weight;
+      c.tag = static_cast<Constraint3D::Tag>(r.tag);
+      c.score = r.score;
+      c.rotational_score = r.rotational_score;
+      c.low_resolution_score = r.low_resolution_score;
+      c.global = r.global != 0;
+      result->push_back(c);
+    }
+  }
+
   void Enqueue(const SubmapId& submap_id, const Submap3DView* submap, const NodeId& node_id,
                const TrajectoryNodeData3D* data, bool full, const Rigid3d& node_pose,
                const Rigid3d& submap_pose) {
+    if (!Owned(submap_id)) {  // another rank searches it; the slot keeps submission order
+      constraints_.emplace_back();
+      return;
+    }
     if (!matchers_.count(submap_id)) {  // DispatchScanMatcherConstruction
       auto m = std::make_shared<SubmapScanMatcher>();
       m->high.reset(new HybridGrid3D(submap->high_resolution_hybrid_grid, context_));
@@ -226,9 +317,6 @@ class ConstraintBuilder3D {
       (p.full ? global_constraints_searched : constraints_searched) += 1;
       if (results[i].status != CSM_OK) continue;
       (p.full ? global_constraints_found : constraints_found) += 1;
-      (p.full ? global_constraint_scores : constraint_scores).push_back(results[i].score);
-      rotational_scores.push_back(results[i].rotational_score);
-      low_resolution_scores.push_back(results[i].low_resolution_score);
       Constraint3D c;
       c.submap_id = p.submap_id;
       c.node_id = p.node_id;
@@ -239,6 +327,7 @@ class ConstraintBuilder3D {
       c.score = results[i].score;
       c.rotational_score = results[i].rotational_score;
       c.low_resolution_score = results[i].low_resolution_score;
+      c.global = p.full;
       constraints_[p.slot].reset(new Constraint3D(c));
     }
     if (failed_this_flush)
@@ -256,6 +345,8 @@ class ConstraintBuilder3D {
   std::vector<std::unique_ptr<Constraint3D>> constraints_;
   std::vector<Pending> pending_;
   int num_started_nodes_ = 0, num_finished_nodes_ = 0;
+  csm_comm* comm_ = nullptr;
+  int64_t reduced_[5] = {0, 0, 0, 0, 0};  // counter totals over ranks at the last WhenDone
 };
 
 }  // namespace cartographer_amd

@@ -34,8 +34,27 @@ struct ConstraintRecord {
 };
 static_assert(sizeof(ConstraintRecord) == 64, "ConstraintRecord is a fixed wire format");
 
-// The rank that searches a submap's pairs: submaps are dealt round robin in
-// creation order, so every rank gets a share of each region of the map.
+// One accepted 3D constraint on the wire (104 bytes, no padding): the 2D
+// fields with a Rigid3d pose and FastCorrelativeScanMatcher3D::Result's three
+// scores; `global` marks MaybeAddGlobalConstraint pairs (the metrics split).
+struct ConstraintRecord3D {
+  int64_t slot;
+  int32_t submap_trajectory, submap_index, node_trajectory, node_index;
+  double t[3], q[4];  // relative pose, submap <- node; q = (w, x, y, z)
+  float score, rotational_score, low_resolution_score;
+  int32_t tag;
+  int32_t global;
+  int32_t reserved;  // zero
+};
+static_assert(sizeof(ConstraintRecord3D) == 104, "ConstraintRecord3D is a fixed wire format");
+
+// The rank that searches a submap's pairs: (trajectory_id * 0x9E3779B1 +
+// submap_index) mod world_size, i.e. round robin over the submaps of one
+// trajectory with a per-trajectory offset, so every rank gets a share of each
+// region of the map. Every rank must make the identical sequence of builder
+// calls (MaybeAdd*, NotifyEndOfNode, and with them the samplers' pulses):
+// slots are assigned by that sequence, and WhenDone checks that every rank
+// holds the same number of slots (CheckSameSubmissions).
 inline int ShardOwner(int trajectory_id, int submap_index, int world_size) {
   const uint64_t h = static_cast<uint64_t>(static_cast<uint32_t>(trajectory_id)) * 0x9E3779B1u +
                      static_cast<uint32_t>(submap_index);
@@ -51,21 +70,46 @@ inline void CommCheck(int code, const char* what) {
 
 // Collective over `comm`: rank 0 returns every rank's records sorted by slot
 // (slots are unique across ranks); the other ranks return an empty vector.
-inline std::vector<ConstraintRecord> GatherConstraintRecords(
-    csm_comm* comm, const std::vector<ConstraintRecord>& local) {
+template <typename Record>
+std::vector<Record> GatherRecords(csm_comm* comm, const std::vector<Record>& local) {
   int64_t total = 0;
-  CommCheck(csm_comm_gather(comm, local.data(),
-                            static_cast<int64_t>(local.size() * sizeof(ConstraintRecord)), &total),
+  CommCheck(csm_comm_gather(comm, local.data(), static_cast<int64_t>(local.size() * sizeof(Record)),
+                            &total),
             "csm_comm_gather");
-  std::vector<ConstraintRecord> all;
+  std::vector<Record> all;
   if (csm_comm_rank(comm) != 0) return all;
-  all.resize(static_cast<size_t>(total) / sizeof(ConstraintRecord));
+  all.resize(static_cast<size_t>(total) / sizeof(Record));
   std::vector<int64_t> sizes(static_cast<size_t>(csm_comm_size(comm)));
   CommCheck(csm_comm_gathered(comm, all.data(), total, sizes.data()), "csm_comm_gathered");
-  std::stable_sort(all.begin(), all.end(), [](const ConstraintRecord& a, const ConstraintRecord& b) {
-    return a.slot < b.slot;
-  });
+  std::stable_sort(all.begin(), all.end(),
+                   [](const Record& a, const Record& b) { return a.slot < b.slot; });
   return all;
+}
+
+inline std::vector<ConstraintRecord> GatherConstraintRecords(
+    csm_comm* comm, const std::vector<ConstraintRecord>& local) {
+  return GatherRecords(comm, local);
+}
+
+// Collective: aborts unless every rank assigned the same number of slots
+// since the last WhenDone (diverging submission streams would make rank 0
+// mix or reorder constraints silently).
+inline void CheckSameSubmissions(csm_comm* comm, int64_t slots) {
+  int64_t v[2] = {slots, -slots};
+  CommCheck(csm_comm_allreduce_i64(comm, v, 2, CSM_REDUCE_MAX), "csm_comm_allreduce_i64");
+  if (v[0] != -v[1]) {
+    std::fprintf(stderr, "F ranks submitted different pair sequences (%lld to %lld slots)\n",
+                 static_cast<long long>(-v[1]), static_cast<long long>(v[0]));
+    std::abort();
+  }
+}
+
+// Collective: the builder's last error over the ranks (error codes are
+// negative: the most negative wins; CSM_OK only if no rank saw an error).
+inline int ReduceLastError(csm_comm* comm, int last_error) {
+  int64_t v = -static_cast<int64_t>(last_error);
+  CommCheck(csm_comm_allreduce_i64(comm, &v, 1, CSM_REDUCE_MAX), "csm_comm_allreduce_i64");
+  return static_cast<int>(-v);
 }
 
 }  // namespace cartographer_amd

@@ -5,6 +5,11 @@
 //   distributed_builder_test gather <world> <port>
 //       CPU only: forks <world> ranks; each gathers interleaved-slot records
 //       to rank 0, which checks the slot order and contents. Exit 0 = pass.
+//   distributed_builder_test gather3d <world> <port>
+//       The same with the 3D records (ConstraintRecord3D).
+//   distributed_builder_test diverge <world> <port>
+//       CPU only: rank 1 submits one pair more than the others; WhenDone's
+//       submission check must abort every rank (exit 0 = they all aborted).
 //   distributed_builder_test builder <rank> <world> <port>
 //       GPU: a synthetic two-room map (6 submaps, 10 nodes), every node
 //       matched globally against every submap and locally against nearby
@@ -12,10 +17,14 @@
 //       communicator). Rank 0 prints one line per constraint of WhenDone's
 //       result, in order, then the summed counters; tests/test_distributed.py
 //       compares the world-2 output with the world-1 output.
+//   distributed_builder_test builder3d <rank> <world> <port>
+//       GPU: the same for ConstraintBuilder3D on walls of voxels (4 submaps,
+//       6 nodes, local and global pairs), plus the score metric lists.
 #include <sys/wait.h>
 #include <unistd.h>
 
 #include <cmath>
+#include <csignal>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -23,6 +32,7 @@
 #include <vector>
 
 #include "cartographer_amd/constraint_builder_2d.h"
+#include "cartographer_amd/constraint_builder_3d.h"
 
 using namespace cartographer_amd;
 
@@ -82,6 +92,113 @@ static int GatherMain(int world, int port) {
     return 1;
   }
   std::printf("gather OK\n");
+  return 0;
+}
+
+static int Gather3DMain(int world, int port) {
+  auto make = [&](int rank) {
+    std::vector<ConstraintRecord3D> mine;
+    for (int k = 0; k < 3 + 2 * rank; ++k) {
+      ConstraintRecord3D r{};
+      r.slot = static_cast<int64_t>(k) * world + rank;
+      r.submap_index = rank;
+      r.node_index = k;
+      r.t[0] = 0.5 * k;
+      r.q[0] = 1.;
+      r.q[3] = 0.125 * rank;
+      r.score = 0.25f * rank;
+      r.rotational_score = 0.5f;
+      r.low_resolution_score = 0.125f * k;
+      r.global = k & 1;
+      mine.push_back(r);
+    }
+    return mine;
+  };
+  std::vector<pid_t> kids;
+  for (int rank = 1; rank < world; ++rank) {
+    const pid_t p = fork();
+    if (p == 0) {
+      csm_comm* comm = nullptr;
+      if (csm_comm_create_tcp(rank, world, "127.0.0.1", port, &comm) != CSM_OK) _exit(2);
+      const auto all = GatherRecords(comm, make(rank));
+      csm_comm_destroy(comm);
+      _exit(all.empty() ? 0 : 3);
+    }
+    kids.push_back(p);
+  }
+  csm_comm* comm = nullptr;
+  if (csm_comm_create_tcp(0, world, "127.0.0.1", port, &comm) != CSM_OK) return 2;
+  const auto all = GatherRecords(comm, make(0));
+  csm_comm_destroy(comm);
+  int bad = 0;
+  size_t expect = 0;
+  for (int r = 0; r < world; ++r) expect += 3 + 2 * r;
+  if (all.size() != expect) ++bad;
+  for (size_t i = 0; i < all.size(); ++i) {
+    const ConstraintRecord3D& r = all[i];
+    if (i && all[i - 1].slot >= r.slot) ++bad;
+    const int rank = static_cast<int>(r.slot % world), k = static_cast<int>(r.slot / world);
+    if (r.submap_index != rank || r.node_index != k || r.t[0] != 0.5 * k || r.q[3] != 0.125 * rank ||
+        r.score != 0.25f * rank || r.low_resolution_score != 0.125f * k || r.global != (k & 1))
+      ++bad;
+  }
+  for (pid_t p : kids) {
+    int st = 0;
+    waitpid(p, &st, 0);
+    if (!WIFEXITED(st) || WEXITSTATUS(st) != 0) ++bad;
+  }
+  if (bad) {
+    std::fprintf(stderr, "gather3d: %d failures\n", bad);
+    return 1;
+  }
+  std::printf("gather3d OK\n");
+  return 0;
+}
+
+// Every rank runs a builder whose pairs all target submaps another rank owns
+// (so nothing is searched), and rank 1 submits one pair more. WhenDone's
+// CheckSameSubmissions must abort on every rank (tests/test_distributed.py
+// also checks the message).
+static int DivergeMain(int world, int port) {
+  std::vector<pid_t> kids;
+  for (int rank = 0; rank < world; ++rank) {
+    const pid_t p = fork();
+    if (p == 0) {
+      csm_comm* comm = nullptr;
+      if (csm_comm_create_tcp(rank, world, "127.0.0.1", port, &comm) != CSM_OK) _exit(2);
+      ConstraintBuilderOptions o;
+      // No pair is searched on any rank here (every pair targets a submap
+      // the rank does not own), so no device context is ever used: a
+      // placeholder keeps the test on the CPU.
+      ConstraintBuilder2D builder(o, reinterpret_cast<csm_context*>(uintptr_t{1}));
+      builder.set_communicator(comm);
+      // Submaps owned by no rank but 0 never run a search on the others; the
+      // slot count is what the check compares. Rank 0 adds nothing it owns.
+      Submap2DView dummy;
+      PointCloud cloud;
+      const int extra = rank == 1 ? 1 : 0;
+      for (int k = 0; k < 3 + extra; ++k) {
+        int s = 0;
+        while (ShardOwner(0, s, world) == rank) ++s;  // a submap this rank does not search
+        builder.MaybeAddGlobalConstraint(SubmapId{0, s}, &dummy, NodeId{0, k}, &cloud);
+      }
+      builder.NotifyEndOfNode();
+      builder.WhenDone([](const ConstraintBuilder2D::Result&) {});
+      _exit(0);  // not reached: the check aborts
+    }
+    kids.push_back(p);
+  }
+  int aborted = 0;
+  for (pid_t p : kids) {
+    int st = 0;
+    waitpid(p, &st, 0);
+    aborted += WIFSIGNALED(st) && WTERMSIG(st) == SIGABRT;
+  }
+  if (aborted != world) {
+    std::fprintf(stderr, "diverge: %d of %d ranks aborted\n", aborted, world);
+    return 1;
+  }
+  std::printf("diverge OK\n");
   return 0;
 }
 
@@ -206,10 +323,116 @@ static int BuilderMain(int rank, int world, int port) {
   return 0;
 }
 
+// Walls of occupied voxels (x = +-1.5 m, y = 2 m) shifted per submap; the
+// nodes see them from shifted poses. Local pairs (identity poses) and global
+// pairs (rotations only) over 4 submaps x 6 nodes.
+static Submap3DView WallSubmap(int s) {
+  Submap3DView submap;
+  const int dx = s % 2, dy = s / 2;
+  for (HybridGridView* g : {&submap.high_resolution_hybrid_grid, &submap.low_resolution_hybrid_grid}) {
+    g->resolution = 0.1f;
+    for (int y = -20; y <= 20; ++y)
+      for (int z = -5; z <= 5; ++z)
+        for (int x : {15, -15}) {
+          g->xyz.insert(g->xyz.end(), {x + dx, y + dy, z});
+          g->values.push_back(32767);
+        }
+    for (int x = -14; x <= 14; ++x)
+      for (int z = -5; z <= 5; ++z) {
+        g->xyz.insert(g->xyz.end(), {x + dx, 20 + dy, z});
+        g->values.push_back(30000 - 1000 * s);
+      }
+  }
+  submap.rotational_scan_matcher_histogram.assign(3, 0.f);
+  return submap;
+}
+
+static TrajectoryNodeData3D WallNode(int k) {
+  TrajectoryNodeData3D node;
+  const float sx = -0.3f + 0.1f * (k % 3), sy = 0.2f - 0.1f * (k / 3);
+  for (int z = -5; z <= 5; ++z) {
+    for (int y = -15; y <= 15; y += 3) {
+      node.high_resolution_point_cloud.push_back(1.5f + sx, 0.1f * y + sy, 0.1f * z);
+      node.high_resolution_point_cloud.push_back(-1.5f + sx, 0.1f * y + sy, 0.1f * z);
+    }
+    for (int x = -10; x <= 10; x += 4)
+      node.high_resolution_point_cloud.push_back(0.1f * x + sx, 2.0f + sy, 0.1f * z);
+  }
+  node.low_resolution_point_cloud = node.high_resolution_point_cloud;
+  node.rotational_scan_matcher_histogram.assign(3, 0.f);
+  return node;
+}
+
+static int Builder3DMain(int rank, int world, int port) {
+  csm_comm* comm = nullptr;
+  if (world > 1 && csm_comm_create_tcp(rank, world, "127.0.0.1", port, &comm) != CSM_OK) {
+    std::fprintf(stderr, "comm create failed\n");
+    return 2;
+  }
+  std::vector<Submap3DView> submaps;
+  for (int s = 0; s < 4; ++s) submaps.push_back(WallSubmap(s));
+  std::vector<TrajectoryNodeData3D> nodes;
+  for (int k = 0; k < 6; ++k) nodes.push_back(WallNode(k));
+  ConstraintBuilderOptions o;
+  o.sampling_ratio = 1.;
+  o.min_score = 0.5f;
+  o.global_localization_min_score = 0.5f;
+  o.fast_correlative_scan_matcher_options_3d.min_rotational_score = 0.;
+  o.fast_correlative_scan_matcher_options_3d.linear_xy_search_window = 0.6;
+  o.fast_correlative_scan_matcher_options_3d.linear_z_search_window = 0.2;
+  o.fast_correlative_scan_matcher_options_3d.angular_search_window = 0.05;
+  ConstraintBuilder3D builder(o);
+  if (comm) builder.set_communicator(comm);
+  for (int k = 0; k < 6; ++k) {
+    for (int s = 0; s < 4; ++s) {
+      if ((k + s) % 4 == 0)
+        builder.MaybeAddGlobalConstraint(SubmapId{0, s}, &submaps[s], NodeId{0, k}, &nodes[k],
+                                         Quaterniond::Identity(), Quaterniond::Identity());
+      else
+        builder.MaybeAddConstraint(SubmapId{0, s}, &submaps[s], NodeId{0, k}, &nodes[k],
+                                   Rigid3d::Identity(), Rigid3d::Identity());
+    }
+    builder.NotifyEndOfNode();
+  }
+  ConstraintBuilder3D::Result result;
+  builder.WhenDone([&](const ConstraintBuilder3D::Result& r) { result = r; });
+  if (rank == 0) {
+    for (const Constraint3D& c : result)
+      std::printf("c %d %d %.9f %.9f %.9f %.9f %.9f %.9f %.9f %.7f %.7f %.7f %d\n",
+                  c.submap_id.submap_index, c.node_id.node_index, c.relative_pose.t[0],
+                  c.relative_pose.t[1], c.relative_pose.t[2], c.relative_pose.rotation.w,
+                  c.relative_pose.rotation.x, c.relative_pose.rotation.y,
+                  c.relative_pose.rotation.z, c.score, c.rotational_score, c.low_resolution_score,
+                  c.global ? 1 : 0);
+    std::printf("counters %lld %lld %lld %lld %lld %d\n",
+                static_cast<long long>(builder.constraints_searched),
+                static_cast<long long>(builder.constraints_found),
+                static_cast<long long>(builder.global_constraints_searched),
+                static_cast<long long>(builder.global_constraints_found),
+                static_cast<long long>(builder.constraints_failed), builder.last_error);
+    std::printf("scores %zu %zu %zu %zu\n", builder.constraint_scores.size(),
+                builder.global_constraint_scores.size(), builder.rotational_scores.size(),
+                builder.low_resolution_scores.size());
+  } else if (!result.empty()) {
+    std::fprintf(stderr, "rank %d got a non-empty result\n", rank);
+    return 1;
+  }
+  if (comm) csm_comm_destroy(comm);
+  return 0;
+}
+
 int main(int argc, char** argv) {
   if (argc == 4 && std::string(argv[1]) == "gather") return GatherMain(std::atoi(argv[2]), std::atoi(argv[3]));
+  if (argc == 4 && std::string(argv[1]) == "gather3d")
+    return Gather3DMain(std::atoi(argv[2]), std::atoi(argv[3]));
+  if (argc == 4 && std::string(argv[1]) == "diverge")
+    return DivergeMain(std::atoi(argv[2]), std::atoi(argv[3]));
   if (argc == 5 && std::string(argv[1]) == "builder")
     return BuilderMain(std::atoi(argv[2]), std::atoi(argv[3]), std::atoi(argv[4]));
-  std::fprintf(stderr, "usage: %s gather <world> <port> | builder <rank> <world> <port>\n", argv[0]);
+  if (argc == 5 && std::string(argv[1]) == "builder3d")
+    return Builder3DMain(std::atoi(argv[2]), std::atoi(argv[3]), std::atoi(argv[4]));
+  std::fprintf(stderr,
+               "usage: %s gather|gather3d|diverge <world> <port> | builder|builder3d <rank> <world> <port>\n",
+               argv[0]);
   return 2;
 }

@@ -179,6 +179,54 @@ def test_cpp_record_gather_tcp(csm, world):
     assert "gather OK" in out.stdout
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_cpp_record_gather_3d_tcp(csm, world):
+    """GatherRecords<ConstraintRecord3D> (the sharded ConstraintBuilder3D's
+    hand-off) over TCP: rank 0 gets every rank's 3D records in slot order."""
+    import subprocess
+    _build_dist()
+    out = subprocess.run([DIST_BIN, "gather3d", str(world), str(_free_port())],
+                         capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    assert "gather3d OK" in out.stdout
+
+
+def test_cpp_diverging_submissions_abort(csm):
+    """A rank that submits a different pair sequence makes WhenDone abort on
+    every rank (CheckSameSubmissions), instead of rank 0 mixing constraints."""
+    import subprocess
+    _build_dist()
+    out = subprocess.run([DIST_BIN, "diverge", "3", str(_free_port())],
+                         capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    assert "diverge OK" in out.stdout
+    assert out.stderr.count("ranks submitted different pair sequences") == 3, out.stderr
+
+
+@pytest.mark.gpu
+def test_cpp_sharded_builder_3d_matches_single_rank(csm):
+    """The C++ ConstraintBuilder3D sharded over 2 ranks (two processes on the
+    one GPU, TCP transport) delivers on rank 0 what the single-rank builder
+    delivers: same constraints in submission order, same summed counters and
+    the same score metric lists (constraint_builder_3d.cc:200-305)."""
+    import subprocess
+    _build_dist()
+    single = subprocess.run([DIST_BIN, "builder3d", "0", "1", "0"], capture_output=True, text=True,
+                            timeout=120)
+    assert single.returncode == 0, single.stderr
+    port = str(_free_port())
+    procs = [subprocess.Popen([DIST_BIN, "builder3d", str(r), "2", port], stdout=subprocess.PIPE,
+                              stderr=subprocess.PIPE, text=True) for r in range(2)]
+    outs = [p.communicate(timeout=120) for p in procs]
+    for p, (o, e) in zip(procs, outs):
+        assert p.returncode == 0, e
+    lines = single.stdout.strip().splitlines()
+    assert sum(1 for l in lines if l.startswith("c ")) >= 4, single.stdout
+    assert any(l.startswith("c ") and l.endswith(" 1") for l in lines), single.stdout  # a global one
+    assert outs[0][0].strip().splitlines() == lines
+    assert outs[1][0].strip() == ""
+
+
 @pytest.mark.gpu
 def test_cpp_sharded_builder_matches_single_rank(csm):
     """The C++ ConstraintBuilder2D sharded over 2 ranks (two processes on the

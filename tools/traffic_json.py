@@ -18,7 +18,11 @@ def main():
     launches = set()
     for f in glob.glob(f"{pmc}/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
-            if "fast2d_search_v4" in r.get("Kernel_Name", "") and r["Counter_Name"] == "FETCH_SIZE":
+            # The search's own symbol (the tie-enumeration launches are the
+            # kCollect = true instantiation).
+            name = r.get("Kernel_Name", "")
+            if "fast2d_search_v4" in name and "true>" not in name.split(",")[2] and \
+                    r["Counter_Name"] == "FETCH_SIZE":
                 per[r.get("Dispatch_Id", "0")] += float(r["Counter_Value"])
                 launches.add(r.get("Dispatch_Id", "0"))
     if not per:
