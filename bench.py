@@ -34,7 +34,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 # Version tag of the search kernel the committed PMC traffic figures belong to
 # (a traffic file recorded on another kernel version is not reported).
-KERNEL_TAG = "v5-clusters"
+KERNEL_TAG = "v5-fifo-hex-w6"
 
 
 def load_pkg():
@@ -265,14 +265,15 @@ def roofline_fields(tm, achieved, peak, traffic, kernel_ms_avg, bytes_per_launch
             **traffic_fields(traffic, kernel_ms_avg, peak),
             "kernel": "fast2d_search", "kernel_ms_avg": kernel_ms_avg,
             "algorithmic_bytes_per_launch": bytes_per_launch,
-            "bytes_definition": "4 B per quad-dword gather the search issues (one "
-                                "per node x scan entry, 4 children each)",
+            "bytes_definition": "4 B per quad-dword gather and 16 B per hex gather the "
+                                "search issues (one per node x scan entry: 4 children or "
+                                "16 grandchildren each)",
             # SURVEY §8(d)'s figure: candidates scored x N points x 1 B
             "candidate_equivalent_bytes_per_launch": candidate_bytes}
 
 
-TRAFFIC_FILES = {"c2": os.path.join("profiles", "r2b", "traffic_c2.json"),
-                 "c3": os.path.join("profiles", "r2d", "traffic_c3.json")}
+TRAFFIC_FILES = {"c2": os.path.join("profiles", "r3c", "traffic_c2.json"),
+                 "c3": os.path.join("profiles", "r3c", "traffic_c3.json")}
 
 
 def traffic_fields(traffic, kernel_ms_avg, peak):
@@ -907,17 +908,30 @@ def c3_run(csm, ctx, args, rank, world_size, dist, coll_dev, comm, gather, trans
     chunks = [queue[i:i + K] for i in range(0, len(queue), K)]
     n_chunks = len(chunks)
 
+    phase = {"pyramids": 0.0, "search": 0.0, "close": 0.0, "records": 0.0}
+    profile = bool(os.environ.get("C3_PROFILE"))
+
     def run_chunk(subs, base):
+        t0 = time.perf_counter()
         mats = [csm.FastCorrelativeScanMatcher2D(world.grid(int(s)), opts, ctx) for s in subs]
         sub_local = np.repeat(np.arange(len(subs), dtype=np.int32), N)
         node = np.tile(np.arange(N, dtype=np.int32), len(subs))
         pairs = csm.make_pairs(sub_local, node, args.min_score, full_submap=True)
+        t1 = time.perf_counter()
         res = csm.match_batch(mats, scans, pairs, ctx)
+        t2 = time.perf_counter()
         for m in mats:
             m.close()
+        t3 = time.perf_counter()
         sub_global = np.asarray(subs, np.int64)[sub_local]
         submission = base + np.arange(len(pairs), dtype=np.int64)  # queue order: submap-major
-        return res, cdist.make_records(res, submission, sub_global, node)
+        rec = cdist.make_records(res, submission, sub_global, node)
+        if profile:
+            phase["pyramids"] += t1 - t0
+            phase["search"] += t2 - t1
+            phase["close"] += t3 - t2
+            phase["records"] += time.perf_counter() - t3
+        return res, rec
 
     def claim(key):
         if comm is None:
@@ -944,6 +958,9 @@ def c3_run(csm, ctx, args, rank, world_size, dist, coll_dev, comm, gather, trans
         if rank == 0 and (c % 10 == 0 or world_size == 1):
             print(f"c3: chunk {c + 1}/{n_chunks} {time.perf_counter() - t_start:.1f} s",
                   file=sys.stderr, flush=True)
+    if profile:
+        print("c3 host phases (s): " + ", ".join(f"{k} {v:.2f}" for k, v in phase.items())
+              + f"; kernel {ctx.timing().search_kernel_ms * 1e-3:.2f}", file=sys.stderr, flush=True)
     allrec = gather(np.concatenate(recs) if recs else np.zeros((0, cdist.RECORD_WIDTH)))
     barrier_sync()
     elapsed = time.perf_counter() - t_start

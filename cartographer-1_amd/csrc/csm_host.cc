@@ -76,6 +76,33 @@ int EnsureDevice(csm_context* ctx) {
   return hipSetDevice(ctx->device) == hipSuccess ? CSM_OK : CSM_EHIP;
 }
 
+// The context's pool of device buffers from destroyed matchers: the smallest
+// one holding n bytes (and at most twice that) is reused, else a new one is
+// allocated. Callers hold ctx->mu.
+int PoolTake(csm_context* ctx, size_t n, DevBuf* out) {
+  int best = -1;
+  for (int i = 0; i < static_cast<int>(ctx->buf_pool.size()); ++i) {
+    const size_t b = ctx->buf_pool[i].second;
+    if (b >= n && b <= 2 * n + 4096 && (best < 0 || b < ctx->buf_pool[best].second)) best = i;
+  }
+  if (best < 0) return out->Reserve(n);
+  out->ptr = ctx->buf_pool[best].first;
+  out->bytes = ctx->buf_pool[best].second;
+  ctx->buf_pool.erase(ctx->buf_pool.begin() + best);
+  return CSM_OK;
+}
+void PoolGive(csm_context* ctx, DevBuf* b) {
+  constexpr size_t kMaxPooled = 32;
+  if (!b->ptr) return;
+  if (ctx->buf_pool.size() >= kMaxPooled) {
+    (void)hipFree(ctx->buf_pool.front().first);
+    ctx->buf_pool.erase(ctx->buf_pool.begin());
+  }
+  ctx->buf_pool.emplace_back(b->ptr, b->bytes);
+  b->ptr = nullptr;
+  b->bytes = 0;
+}
+
 const std::pair<SearchWindow2D, std::vector<ZRot>>& WindowFor(
     csm_scan_set* s, int scan, double lin, double ang, double res) {
   const auto key = std::make_tuple(scan, ang, lin, res);
@@ -216,7 +243,7 @@ int LaunchSearch(csm_context* ctx, csm_scan_set* scans, const std::vector<PairDe
       return rcode;
     CSM_HIP(LaunchFast2dSearchV2(grid, dyn_lds, st, ctx->submap_desc.as<SubmapDesc>(),
                                  ctx->pair_desc.as<PairDesc>(), scans->points.as<float>(),
-                                 ctx->rot_table.as<float2>(), wq2,
+                                 scans->rot_dev.as<float2>(), wq2,
                                  ctx->counters.as<unsigned long long>(), ctx->best.as<uint64_t>(),
                                  ctx->status.as<int32_t>(), ctx->stats.as<unsigned long long>(),
                                  ctx->spill.as<uint2>(), max_npad, capc, plan.hex, plan.fifo,
@@ -228,7 +255,7 @@ int LaunchSearch(csm_context* ctx, csm_scan_set* scans, const std::vector<PairDe
                                                         std::max<int64_t>(total_chunks, 1)));
     CSM_HIP(LaunchFast2dSearch(grid, dyn_lds, st, ctx->submap_desc.as<SubmapDesc>(),
                                ctx->pair_desc.as<PairDesc>(), scans->points.as<float>(),
-                               ctx->rot_table.as<float2>(), wq,
+                               scans->rot_dev.as<float2>(), wq,
                                ctx->counters.as<unsigned long long>(), ctx->best.as<uint64_t>(),
                                ctx->status.as<int32_t>(), ctx->stats.as<unsigned long long>()));
   }
@@ -398,7 +425,7 @@ int ResolveTies(csm_context* ctx, csm_fast2d* const* submaps, csm_scan_set* scan
                            hipMemcpyHostToDevice, st));
     CSM_HIP(LaunchFast2dScoreQueries(static_cast<int>(js.size()), plan.max_npad, st,
                                      ctx->submap_desc.as<SubmapDesc>(), ctx->pair_desc.as<PairDesc>(),
-                                     scans->points.as<float>(), ctx->rot_table.as<float2>(),
+                                     scans->points.as<float>(), scans->rot_dev.as<float2>(),
                                      ctx->sq_jobs.as<ScoreJob>(), ctx->sq_queries.as<int4>(),
                                      ctx->sq_sums.as<int32_t>()));
     CSM_HIP(hipMemcpyAsync(sums->data(), ctx->sq_sums.ptr, sizeof(int32_t) * qs.size(),
@@ -514,8 +541,9 @@ int RunBatch(csm_context* ctx, csm_fast2d* const* submaps, int32_t num_submaps,
   const bool hex = num_submaps > 0 && sdesc[0].hex_mask != 0;
   std::vector<PairDesc> pdesc;
   std::vector<int64_t> pair_src;  // pdesc index -> pair index
-  std::vector<float2> rot_host;
-  std::map<const void*, int32_t> rot_offsets;  // table ptr -> offset
+  // Rotation tables live on the scan set's device table, appended once per
+  // (scan, window) and kept across batches (csm_scan_set::rot_all).
+  std::vector<float2>& rot_host = scans->rot_all;
   int max_npad = 64;
   for (int64_t i = 0; i < num_pairs; ++i) {
     const csm_pair2d& p = pairs[i];
@@ -549,12 +577,12 @@ int RunBatch(csm_context* ctx, csm_fast2d* const* submaps, int32_t num_submaps,
     }
     const auto& win = WindowFor(scans, p.scan, lin, ang, res);
     if (win.first.num_scans > kMaxRotations) { results[i].status = CSM_ERANGE; continue; }
-    auto ro = rot_offsets.find(&win);
+    auto ro = scans->rot_offsets.find(&win);
     int32_t off;
-    if (ro == rot_offsets.end()) {
+    if (ro == scans->rot_offsets.end()) {
       off = static_cast<int32_t>(rot_host.size());
       for (const ZRot& z : win.second) rot_host.push_back(make_float2(z.w, z.s));
-      rot_offsets.emplace(&win, off);
+      scans->rot_offsets.emplace(&win, off);
     } else {
       off = ro->second;
     }
@@ -600,12 +628,18 @@ int RunBatch(csm_context* ctx, csm_fast2d* const* submaps, int32_t num_submaps,
   // ---- uploads shared by the search and the tie resolution ------------------
   int rcode;
   if ((rcode = ctx->submap_desc.Reserve(sizeof(SubmapDesc) * num_submaps))) return rcode;
-  if ((rcode = ctx->rot_table.Reserve(sizeof(float2) * rot_host.size()))) return rcode;
+  if (rot_host.size() > scans->rot_uploaded) {  // new windows since the last batch
+    const size_t want = sizeof(float2) * rot_host.size();
+    if (want > scans->rot_dev.bytes && (rcode = scans->rot_dev.Reserve(want + want / 2))) return rcode;
+  }
   hipStream_t st = ctx->stream;
   CSM_HIP(hipMemcpyAsync(ctx->submap_desc.ptr, sdesc.data(), sizeof(SubmapDesc) * num_submaps,
                          hipMemcpyHostToDevice, st));
-  CSM_HIP(hipMemcpyAsync(ctx->rot_table.ptr, rot_host.data(), sizeof(float2) * rot_host.size(),
-                         hipMemcpyHostToDevice, st));
+  if (rot_host.size() > scans->rot_uploaded) {
+    CSM_HIP(hipMemcpyAsync(scans->rot_dev.ptr, rot_host.data(), sizeof(float2) * rot_host.size(),
+                           hipMemcpyHostToDevice, st));
+    scans->rot_uploaded = rot_host.size();
+  }
   std::vector<uint64_t> keys, keys_hi;
   std::vector<int32_t> stat;
   unsigned long long stats_host[kStatsWords] = {0};
@@ -804,8 +838,24 @@ int csm_fast2d_create(csm_context* ctx, const csm_map_limits* limits,
     }
   }
   m->options.search_depth = depth;
-  std::vector<uint8_t> qtab(32768);
-  if (!QuantizationTable(min_cc, max_cc, qtab.data())) return CSM_EINVAL;
+  hipStream_t st = ctx->stream;
+  int rc;
+  // Quantization and correspondence-cost tables, kept on the device for the
+  // last (min_cc, max_cc).
+  if (ctx->f2_tab_key[0] != min_cc || ctx->f2_tab_key[1] != max_cc) {
+    std::vector<uint8_t> qtab(32768);
+    if (!QuantizationTable(min_cc, max_cc, qtab.data())) return CSM_EINVAL;
+    std::vector<float> ctab(32768);
+    ConversionTable(max_cc, min_cc, max_cc, ctab.data());
+    if ((rc = ctx->f2_qtab.Reserve(32768)) || (rc = ctx->f2_ctab.Reserve(sizeof(float) * 32768)))
+      return rc;
+    CSM_HIP(hipMemcpyAsync(ctx->f2_qtab.ptr, qtab.data(), 32768, hipMemcpyHostToDevice, st));
+    CSM_HIP(hipMemcpyAsync(ctx->f2_ctab.ptr, ctab.data(), sizeof(float) * 32768,
+                           hipMemcpyHostToDevice, st));
+    CSM_HIP(hipStreamSynchronize(st));
+    ctx->f2_tab_key[0] = min_cc;
+    ctx->f2_tab_key[1] = max_cc;
+  }
 
   SubmapDesc& d = m->desc;
   d.max_x = limits->max_x;
@@ -873,8 +923,7 @@ int csm_fast2d_create(csm_context* ctx, const csm_map_limits* limits,
     hex_mask = 0;
   }
   d.hex_mask = static_cast<int32_t>(hex_mask);
-  int rc;
-  if ((rc = m->pyramid.Reserve(total))) return rc;
+  if ((rc = PoolTake(ctx, total, &m->pyramid))) return rc;
   d.pyramid_base = m->pyramid.as<uint8_t>();
   d.pyramid_bytes = static_cast<int32_t>(total);
   for (int l = 0; l < depth; ++l) {
@@ -883,12 +932,10 @@ int csm_fast2d_create(csm_context* ctx, const csm_map_limits* limits,
     d.quad_off[l] = static_cast<int32_t>(qoffs[l]);
   }
 
-  DevBuf dcells, dq;
+  DevBuf& dcells = ctx->f2_cells;
+  const DevBuf& dq = ctx->f2_qtab;
   if ((rc = dcells.Reserve(sizeof(uint16_t) * nx * ny))) return rc;
-  if ((rc = dq.Reserve(32768))) return rc;
-  hipStream_t st = ctx->stream;
   CSM_HIP(hipMemcpyAsync(dcells.ptr, cells, sizeof(uint16_t) * nx * ny, hipMemcpyHostToDevice, st));
-  CSM_HIP(hipMemcpyAsync(dq.ptr, qtab.data(), 32768, hipMemcpyHostToDevice, st));
   const int n0 = nx * ny;
   CSM_HIP(LaunchPyramidLevel0(dcells.as<uint16_t>(), dq.as<uint8_t>(),
                               const_cast<uint8_t*>(d.level[0]), n0, st));
@@ -897,7 +944,7 @@ int csm_fast2d_create(csm_context* ctx, const csm_map_limits* limits,
                                 const_cast<uint8_t*>(d.level[l]), d.wide_nx[l], d.wide_ny[l],
                                 1 << (l - 1), st));
   }
-  DevBuf dwiden;
+  DevBuf& dwiden = ctx->f2_widen;
   if (widen_bytes && (rc = dwiden.Reserve(widen_bytes))) return rc;
   for (int l = 0; l < depth; ++l) {
     const int km1 = (1 << d.cshift[l]) - 1;
@@ -912,24 +959,22 @@ int csm_fast2d_create(csm_context* ctx, const csm_map_limits* limits,
   }
   // Correspondence costs (Grid2D::GetCorrespondenceCost, grid_2d.cc) for the
   // CeresScanMatcher2D refinement: the value table with unknown -> max_cc.
-  {
-    std::vector<float> ctab(32768);
-    ConversionTable(max_cc, min_cc, max_cc, ctab.data());
-    DevBuf dtab;
-    if ((rc = dtab.Reserve(sizeof(float) * 32768))) return rc;
-    if ((rc = m->cost.Reserve(sizeof(float) * n0))) return rc;
-    CSM_HIP(hipMemcpyAsync(dtab.ptr, ctab.data(), sizeof(float) * 32768, hipMemcpyHostToDevice, st));
-    CSM_HIP(LaunchCellsToProbability(dcells.as<uint16_t>(), dtab.as<float>(), m->cost.as<float>(),
-                                     n0, st));
-    CSM_HIP(hipStreamSynchronize(st));  // dcells/dq/dtab are freed on return
-  }
+  if ((rc = PoolTake(ctx, sizeof(float) * n0, &m->cost))) return rc;
+  CSM_HIP(LaunchCellsToProbability(dcells.as<uint16_t>(), ctx->f2_ctab.as<float>(),
+                                   m->cost.as<float>(), n0, st));
+  // The cells are read from the caller's memory and the context's scratch
+  // is reused by the next create: finish before returning.
+  CSM_HIP(hipStreamSynchronize(st));
   *out = m.release();
   return CSM_OK;
 }
 
 void csm_fast2d_destroy(csm_fast2d* m) {
   if (!m) return;
+  std::lock_guard<std::mutex> lock(m->ctx->mu);
   (void)hipSetDevice(m->ctx->device);
+  PoolGive(m->ctx, &m->pyramid);  // reused by the next csm_fast2d_create
+  PoolGive(m->ctx, &m->cost);
   delete m;
 }
 

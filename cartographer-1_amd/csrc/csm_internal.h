@@ -85,7 +85,7 @@ struct csm_context {
   int device = 0;
   hipStream_t stream = nullptr;
   std::mutex mu;
-  csm::DevBuf submap_desc, pair_desc, rot_table, best, status, counters, pair_order,
+  csm::DevBuf submap_desc, pair_desc, best, status, counters, pair_order,
       chunk_prefix, blocks, stats, spill, single_points, best_hi, ties, tie_count, sq_jobs,
       sq_queries, sq_sums;
   csm::Rt2dCache rt2d;
@@ -107,6 +107,15 @@ struct csm_context {
   csm::DevBuf vf_points, vf_offsets, vf_keep, vf_counts;
   // CeresScanMatcher2D refinement scratch (ceres2d.hip).
   csm::DevBuf cr_items, cr_out, cr3_items, cr3_points, cr3_out;
+  // csm_fast2d_create: device buffers of destroyed matchers kept for reuse
+  // (pyramids, cost grids: a sweep creates and destroys thousands), scratch,
+  // and the quantization / cost tables of the last (min_cc, max_cc).
+  std::vector<std::pair<void*, size_t>> buf_pool;
+  csm::DevBuf f2_cells, f2_widen, f2_qtab, f2_ctab;
+  float f2_tab_key[2] = {-1.f, -1.f};
+  ~csm_context() {
+    for (auto& b : buf_pool) (void)hipFree(b.first);
+  }
 };
 
 // One submap's device data (csm_host.cc builds it).
@@ -129,6 +138,12 @@ struct csm_scan_set {
   std::map<std::tuple<int, double, double, double>,
            std::pair<csm::SearchWindow2D, std::vector<csm::ZRot>>>
       windows;
+  // Their device copy, appended as batches meet new windows: (w, s) per
+  // rotation, the offset of each window's table, and how much is uploaded.
+  std::vector<float2> rot_all;
+  std::map<const void*, int32_t> rot_offsets;
+  csm::DevBuf rot_dev;
+  size_t rot_uploaded = 0;
 };
 
 // A HybridGrid on the device (host3d.cc builds it).
