@@ -11,13 +11,17 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <limits>
 #include <map>
 #include <memory>
 #include <mutex>
 #include <set>
+#include <thread>
 #include <array>
 #include <tuple>
 #include <vector>
@@ -436,72 +440,139 @@ int ResolveTies(csm_context* ctx, csm_fast2d* const* submaps, csm_scan_set* scan
   // The jobs index pd2 (ctx->pair_desc holds it after the second search).
   std::vector<int32_t> sums;
   if ((rc = score(jobs, queries, &sums))) return rc;
-  for (const Tie& w : work) {
+  // Per tie: the leaves that can come first. The reference visits the
+  // lowest-resolution candidates by descending score, so only leaves under a
+  // top-level ancestor of the highest score compete; the top-level order is
+  // needed only when two distinct such ancestors share that score.
+  struct Cand {
+    std::vector<int> live;  // leaf indices under a highest-score top ancestor
+    bool need_perm = false;
+    std::vector<std::array<int, 4>> rb;  // per rotation bounds (need_perm)
+    std::vector<int64_t> rot_first;      // per rotation first lattice index
+    std::vector<int64_t> pos;            // lattice index -> sorted position
+  };
+  std::vector<Cand> cand(work.size());
+  auto anc_of = [&](const Tie& w, int li, int lv) {
     const PairDesc& d = pdesc[w.k];
-    const PairDesc& d2 = pd2[w.t];
     const csm_fast2d* m = submaps[d.submap];
+    const int4 q = queries[leaf_query[li] + lv - 1];
+    return std::make_tuple(q.y, q.z,
+                           SumToScore(sums[leaf_query[li] + lv - 1], d.num_points, m->min_s, m->max_s));
+  };
+  for (size_t wi = 0; wi < work.size(); ++wi) {
+    const Tie& w = work[wi];
+    Cand& c = cand[wi];
     const int T = w.depth - 1;
-    // (x, y, score) of leaf li's level-lv ancestor; the score as
-    // ScoreCandidates stores it (ToScore(sum / n), compared as floats).
-    auto anc = [&](int li, int lv) {
-      const int4 q = queries[leaf_query[li] + lv - 1];
-      return std::make_tuple(q.y, q.z,
-                             SumToScore(sums[leaf_query[li] + lv - 1], d.num_points, m->min_s, m->max_s));
-    };
-    // (3) Top-level positions, only if two distinct top ancestors tie.
-    std::map<std::tuple<int, int, int>, int64_t> top_pos;  // (rot, x, y) -> sorted position
-    bool need_perm = T == 0;
-    if (T >= 1) {
-      std::map<float, std::set<std::tuple<int, int, int>>> top_by_sum;
-      for (int i = 0; i < w.leaves_count; ++i) {
-        const int li = w.leaves_first + i;
-        const auto [x, y, s] = anc(li, T);
-        top_by_sum[s].insert({leaves[li].x, x, y});
-      }
-      for (auto& [s, nodes] : top_by_sum) need_perm |= nodes.size() > 1;
+    if (T == 0) {  // the top-level list is the leaves themselves
+      for (int i = 0; i < w.leaves_count; ++i) c.live.push_back(w.leaves_first + i);
+      c.need_perm = true;
+      continue;
     }
-    if (need_perm) {
-      // The pair's whole lowest-resolution list in generation order.
-      const int step = 1 << T;
-      std::vector<ScoreJob> tj;
-      std::vector<int4> tq;
-      std::vector<int64_t> rot_first(d.num_scans + 1, 0);
-      std::vector<std::array<int, 4>> rb(d.num_scans);
-      for (int r = 0; r < d.num_scans; ++r) {
-        int b[4];
-        RotationBounds(scans, d, m->desc, zrot(d, r), b);
-        rb[r] = {b[0], b[1], b[2], b[3]};
+    float top = -std::numeric_limits<float>::infinity();
+    for (int i = 0; i < w.leaves_count; ++i) top = std::max(top, std::get<2>(anc_of(w, w.leaves_first + i, T)));
+    std::set<std::tuple<int, int, int>> nodes;
+    for (int i = 0; i < w.leaves_count; ++i) {
+      const int li = w.leaves_first + i;
+      const auto [x, y, sc] = anc_of(w, li, T);
+      if (sc != top) continue;
+      c.live.push_back(li);
+      nodes.insert({leaves[li].x, x, y});
+    }
+    c.need_perm = nodes.size() > 1;
+  }
+  // (3) The whole lowest-resolution list of every pair that needs the
+  // top-level permutation: bounds of all its rotations on the device, every
+  // lattice node scored in one launch, each list sorted on its own thread.
+  std::vector<int> perm;
+  for (size_t wi = 0; wi < work.size(); ++wi)
+    if (cand[wi].need_perm) perm.push_back(static_cast<int>(wi));
+  if (!perm.empty()) {
+    std::vector<int2> bjobs;
+    for (int wi : perm)
+      for (int r = 0; r < pdesc[work[wi].k].num_scans; ++r) bjobs.push_back(make_int2(work[wi].t, r));
+    if ((rc = ctx->sq_jobs.Reserve(sizeof(int2) * bjobs.size()))) return rc;
+    if ((rc = ctx->sq_sums.Reserve(sizeof(int4) * bjobs.size()))) return rc;
+    hipStream_t st = ctx->stream;
+    std::vector<int4> bounds(bjobs.size());
+    CSM_HIP(hipMemcpyAsync(ctx->sq_jobs.ptr, bjobs.data(), sizeof(int2) * bjobs.size(),
+                           hipMemcpyHostToDevice, st));
+    CSM_HIP(LaunchFast2dRotationBounds(static_cast<int>(bjobs.size()), st, ctx->submap_desc.as<SubmapDesc>(),
+                                       ctx->pair_desc.as<PairDesc>(), scans->points.as<float>(),
+                                       scans->rot_dev.as<float2>(), ctx->sq_jobs.as<int2>(),
+                                       ctx->sq_sums.as<int4>()));
+    CSM_HIP(hipMemcpyAsync(bounds.data(), ctx->sq_sums.ptr, sizeof(int4) * bjobs.size(),
+                           hipMemcpyDeviceToHost, st));
+    CSM_HIP(hipStreamSynchronize(st));
+    std::vector<ScoreJob> tj;
+    std::vector<int4> tq;
+    std::vector<int64_t> base(perm.size());
+    size_t bi = 0;
+    for (size_t pi = 0; pi < perm.size(); ++pi) {
+      const Tie& w = work[perm[pi]];
+      Cand& c = cand[perm[pi]];
+      const int n = pdesc[w.k].num_scans;
+      const int T = w.depth - 1, step = 1 << T;
+      base[pi] = static_cast<int64_t>(tq.size());
+      c.rb.resize(n);
+      c.rot_first.assign(n + 1, 0);
+      for (int r = 0; r < n; ++r, ++bi) {
+        const int4 b = bounds[bi];
+        c.rb[r] = {b.x, b.y, b.z, b.w};
         ScoreJob job{w.t, r, static_cast<int32_t>(tq.size()), 0};
-        for (int x = b[0]; x <= b[1]; x += step)
-          for (int y = b[2]; y <= b[3]; y += step) tq.push_back(make_int4(T, x, y, 0));
+        for (int x = b.x; x <= b.y; x += step)
+          for (int y = b.z; y <= b.w; y += step) tq.push_back(make_int4(T, x, y, 0));
         job.count = static_cast<int32_t>(tq.size()) - job.first;
-        rot_first[r + 1] = static_cast<int64_t>(tq.size());
+        c.rot_first[r + 1] = static_cast<int64_t>(tq.size()) - base[pi];
         if (job.count) tj.push_back(job);
       }
-      std::vector<int32_t> ts;
-      if ((rc = score(tj, tq, &ts))) return rc;
-      // ScoreCandidates: score = ToScore(sum / n), then
-      // std::sort(greater<Candidate2D>) — the same algorithm and the same
-      // comparisons give the same permutation for any element type.
-      std::vector<std::pair<float, int64_t>> lst(tq.size());
-      for (size_t i = 0; i < tq.size(); ++i)
-        lst[i] = {SumToScore(ts[i], d.num_points, m->min_s, m->max_s), static_cast<int64_t>(i)};
+    }
+    std::vector<int32_t> ts;
+    if ((rc = score(tj, tq, &ts))) return rc;
+    // ScoreCandidates: score = ToScore(sum / n), then
+    // std::sort(greater<Candidate2D>) — the same algorithm and the same
+    // comparisons give the same permutation for any element type.
+    auto sort_one = [&](size_t pi) {
+      const Tie& w = work[perm[pi]];
+      Cand& c = cand[perm[pi]];
+      const PairDesc& d = pdesc[w.k];
+      const csm_fast2d* m = submaps[d.submap];
+      const int64_t n = c.rot_first.back();
+      std::vector<std::pair<float, int64_t>> lst(n);
+      for (int64_t i = 0; i < n; ++i)
+        lst[i] = {SumToScore(ts[base[pi] + i], d.num_points, m->min_s, m->max_s), i};
       std::sort(lst.begin(), lst.end(),
                 [](const std::pair<float, int64_t>& a, const std::pair<float, int64_t>& b) {
                   return a.first > b.first;
                 });
-      std::vector<int64_t> pos(lst.size());
-      for (size_t i = 0; i < lst.size(); ++i) pos[lst[i].second] = static_cast<int64_t>(i);
-      for (int i = 0; i < w.leaves_count; ++i) {
-        const int li = w.leaves_first + i;
-        const int r = leaves[li].x;
-        int x = leaves[li].y, y = leaves[li].z;
-        if (T >= 1) std::tie(x, y, std::ignore) = anc(li, T);
-        const int ny = (rb[r][3] - rb[r][2] + step) / step;
-        const int64_t idx = rot_first[r] + static_cast<int64_t>((x - rb[r][0]) / step) * ny + (y - rb[r][2]) / step;
-        top_pos[{r, x, y}] = pos[idx];
-      }
+      c.pos.resize(n);
+      for (int64_t i = 0; i < n; ++i) c.pos[lst[i].second] = i;
+    };
+    const size_t nthreads = std::min<size_t>(perm.size(), 8);
+    if (nthreads <= 1) {
+      for (size_t pi = 0; pi < perm.size(); ++pi) sort_one(pi);
+    } else {
+      std::vector<std::thread> pool;
+      std::atomic<size_t> next{0};
+      for (size_t i = 0; i < nthreads; ++i)
+        pool.emplace_back([&] {
+          for (size_t pi; (pi = next.fetch_add(1)) < perm.size();) sort_one(pi);
+        });
+      for (auto& th : pool) th.join();
     }
+  }
+  for (size_t wi = 0; wi < work.size(); ++wi) {
+    const Tie& w = work[wi];
+    const Cand& c = cand[wi];
+    const PairDesc& d2 = pd2[w.t];
+    const int T = w.depth - 1;
+    const int step = 1 << T;
+    auto anc = [&](int li, int lv) { return anc_of(w, li, lv); };
+    // Sorted position of the top-level node (rot, x, y).
+    auto top_pos = [&](int r, int x, int y) {
+      const int ny = (c.rb[r][3] - c.rb[r][2] + step) / step;
+      return c.pos[c.rot_first[r] + static_cast<int64_t>((x - c.rb[r][0]) / step) * ny +
+                   (y - c.rb[r][2]) / step];
+    };
     // The reference's visiting order of two tied leaves.
     auto first = [&](int a, int b) {
       for (int lv = T; lv >= 1; --lv) {
@@ -510,17 +581,17 @@ int ResolveTies(csm_context* ctx, csm_fast2d* const* submaps, csm_scan_set* scan
         const int ra = leaves[a].x, rb2 = leaves[b].x;
         if (ra == rb2 && ax == bx && ay == by) continue;
         if (as != bs) return as > bs;
-        if (lv == T) return top_pos.at({ra, ax, ay}) < top_pos.at({rb2, bx, by});
+        if (lv == T) return top_pos(ra, ax, ay) < top_pos(rb2, bx, by);
         return std::make_pair(ax, ay) < std::make_pair(bx, by);
       }
       if (T == 0)
-        return top_pos.at({leaves[a].x, leaves[a].y, leaves[a].z}) <
-               top_pos.at({leaves[b].x, leaves[b].y, leaves[b].z});
+        return top_pos(leaves[a].x, leaves[a].y, leaves[a].z) <
+               top_pos(leaves[b].x, leaves[b].y, leaves[b].z);
       return std::make_pair(leaves[a].y, leaves[a].z) < std::make_pair(leaves[b].y, leaves[b].z);
     };
-    int best = w.leaves_first;
-    for (int i = 1; i < w.leaves_count; ++i)
-      if (first(w.leaves_first + i, best)) best = w.leaves_first + i;
+    int best = c.live[0];
+    for (size_t i = 1; i < c.live.size(); ++i)
+      if (first(c.live[i], best)) best = c.live[i];
     (*keys)[w.k] = PackLeafKey(static_cast<uint32_t>(d2.collect_sum), leaves[best].x,
                                leaves[best].y, leaves[best].z);
   }
@@ -531,6 +602,11 @@ int RunBatch(csm_context* ctx, csm_fast2d* const* submaps, int32_t num_submaps,
              csm_scan_set* scans, const csm_pair2d* pairs, int64_t num_pairs,
              csm_result2d* results) {
   // ---- host preparation ---------------------------------------------------
+  const bool prof = std::getenv("CSM_PROFILE2D") != nullptr;
+  const auto t_start = std::chrono::steady_clock::now();
+  auto ms_since = [](std::chrono::steady_clock::time_point t) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+  };
   std::vector<SubmapDesc> sdesc(num_submaps);
   for (int i = 0; i < num_submaps; ++i) {
     if (!submaps[i] || submaps[i]->ctx != ctx) return CSM_EINVAL;
@@ -643,6 +719,8 @@ int RunBatch(csm_context* ctx, csm_fast2d* const* submaps, int32_t num_submaps,
   std::vector<uint64_t> keys, keys_hi;
   std::vector<int32_t> stat;
   unsigned long long stats_host[kStatsWords] = {0};
+  const double prep_ms = ms_since(t_start);
+  const auto t_search = std::chrono::steady_clock::now();
   if ((rcode = LaunchSearch(ctx, scans, pdesc, nullptr, plan, ctx->timing, &keys, &keys_hi, &stat,
                             stats_host)))
     return rcode;
@@ -668,9 +746,14 @@ int RunBatch(csm_context* ctx, csm_fast2d* const* submaps, int32_t num_submaps,
   }
 
   // ---- exactly tied maxima: the reference's pick (ResolveTies) ---------------
+  const double search_ms = ms_since(t_search);
+  const auto t_ties = std::chrono::steady_clock::now();
+  const int64_t tied_before = ctx->t.tied_pairs;
   if (plan.use_v2 && (rcode = ResolveTies(ctx, submaps, scans, pdesc, rot_host, plan, stat, keys_hi,
                                            &keys)))
     return rcode;
+  const double ties_ms = ms_since(t_ties);
+  const auto t_decode = std::chrono::steady_clock::now();
 
   // ---- decode -----------------------------------------------------------------
   for (int k = 0; k < np; ++k) {
@@ -713,6 +796,12 @@ int RunBatch(csm_context* ctx, csm_fast2d* const* submaps, int32_t num_submaps,
     results[i].pose.y = init.y + cy;
     results[i].pose.theta = init.theta + co;
   }
+  if (prof)
+    std::fprintf(stderr,
+                 "fast2d batch host (ms): prep %.2f, search + readback %.2f, ties %.2f (%lld pairs), "
+                 "decode %.2f; %d pairs\n",
+                 prep_ms, search_ms, ties_ms, static_cast<long long>(ctx->t.tied_pairs - tied_before),
+                 ms_since(t_decode), np);
   return CSM_OK;
 }
 

@@ -1523,6 +1523,51 @@ fast2d_score_queries(const SubmapDesc* __restrict__ submaps, const PairDesc* __r
   }
 }
 
+// ShrinkToFit bounds (correlative_scan_matcher_2d.cc:73-91) of one (pair,
+// rotation) per workgroup, from the scan discretized exactly as the search
+// discretizes it: (min_x, max_x, min_y, max_y) after the linear window clamp.
+__global__ void __launch_bounds__(256)
+fast2d_rotation_bounds(const SubmapDesc* __restrict__ submaps, const PairDesc* __restrict__ pairs,
+                       const float* __restrict__ points, const float2* __restrict__ rot_table,
+                       const int2* __restrict__ jobs, int4* __restrict__ bounds) {
+  __shared__ int mm[4];
+  const int2 job = jobs[blockIdx.x];
+  const PairDesc pd = pairs[job.x];
+  const SubmapDesc& sm = submaps[pd.submap];
+  const float2 q = rot_table[pd.rot_offset + job.y];
+  if (threadIdx.x == 0) {
+    mm[0] = 0x7fffffff; mm[1] = -0x7fffffff; mm[2] = 0x7fffffff; mm[3] = -0x7fffffff;
+  }
+  __syncthreads();
+  int mnx = 0x7fffffff, mxx = -0x7fffffff, mny = 0x7fffffff, mxy = -0x7fffffff;
+  for (int i = threadIdx.x; i < pd.num_points; i += blockDim.x) {
+    const float* p = points + 3 * (pd.point_offset + i);
+    float x, y;
+    RotateZDev(pd.pre_w, pd.pre_s, p[0], p[1], &x, &y);
+    RotateZDev(q.x, q.y, x, y, &x, &y);
+    const float px = __fadd_rn(pd.tx, x);
+    const float py = __fadd_rn(pd.ty, y);
+    const double cx = CellCoord(sm.max_y, py, sm.resolution);
+    const double cy = CellCoord(sm.max_x, px, sm.resolution);
+    const int ix = fabs(cx) > kIndexLimit ? 0 : static_cast<int>(cx);
+    const int iy = fabs(cy) > kIndexLimit ? 0 : static_cast<int>(cy);
+    mnx = min(mnx, ix); mxx = max(mxx, ix);
+    mny = min(mny, iy); mxy = max(mxy, iy);
+  }
+  mnx = WaveMin(mnx); mxx = WaveMax(mxx); mny = WaveMin(mny); mxy = WaveMax(mxy);
+  if ((threadIdx.x & 63) == 0) {
+    atomicMin(&mm[0], mnx); atomicMax(&mm[1], mxx);
+    atomicMin(&mm[2], mny); atomicMax(&mm[3], mxy);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int lo_x = min(0, -mm[1]), hi_x = max(0, sm.nx - 1 - mm[0]);
+    const int lo_y = min(0, -mm[3]), hi_y = max(0, sm.ny - 1 - mm[2]);
+    bounds[blockIdx.x] = make_int4(max(-pd.num_linear, lo_x), min(pd.num_linear, hi_x),
+                                   max(-pd.num_linear, lo_y), min(pd.num_linear, hi_y));
+  }
+}
+
 // Grid cells -> float through a 32768-entry table (ValueConversionTables;
 // the Ceres refinement's correspondence-cost grid).
 __global__ void cells_to_probability(const uint16_t* __restrict__ cells,
@@ -1598,6 +1643,14 @@ hipError_t LaunchFast2dScoreQueries(int num_jobs, int npad, hipStream_t st, cons
                                     const int4* queries, int32_t* sums) {
   hipLaunchKernelGGL(fast2d_score_queries, dim3(num_jobs), dim3(256), sizeof(uint32_t) * npad, st,
                      submaps, pairs, points, rot_table, jobs, queries, sums, npad);
+  return hipGetLastError();
+}
+
+hipError_t LaunchFast2dRotationBounds(int num_jobs, hipStream_t st, const SubmapDesc* submaps,
+                                      const PairDesc* pairs, const float* points,
+                                      const float2* rot_table, const int2* jobs, int4* bounds) {
+  hipLaunchKernelGGL(fast2d_rotation_bounds, dim3(num_jobs), dim3(256), 0, st, submaps, pairs, points,
+                     rot_table, jobs, bounds);
   return hipGetLastError();
 }
 

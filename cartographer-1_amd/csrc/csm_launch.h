@@ -29,6 +29,10 @@ hipError_t LaunchFast2dScoreQueries(int num_jobs, int npad, hipStream_t st, cons
                                     const PairDesc* pairs, const float* points,
                                     const float2* rot_table, const ScoreJob* jobs,
                                     const int4* queries, int32_t* sums);
+// ShrinkToFit bounds of (pair, rotation) jobs (ResolveTies).
+hipError_t LaunchFast2dRotationBounds(int num_jobs, hipStream_t st, const SubmapDesc* submaps,
+                                      const PairDesc* pairs, const float* points,
+                                      const float2* rot_table, const int2* jobs, int4* bounds);
 // Resident workgroups per CU of the v4/v5 search kernel at this dynamic LDS
 // size (registers and LDS; 0 if the query fails).
 int Fast2dSearchV2BlocksPerCu(bool hex, bool fifo, size_t dyn_lds);

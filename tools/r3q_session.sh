@@ -1,0 +1,8 @@
+set -u
+O=gpurun_out/r3q
+mkdir -p $O
+bash tools/gpu_measure.sh $O tests || exit 1
+tail -2 $O/gpu_tests.log
+CSM_PROFILE2D=1 C3_PROFILE=1 timeout -k 10 300 python -u bench.py --no-cpu --no-rt --no-3d --steps 2 --warmup 1 --c3-slice 16 > $O/c3_small.json 2> $O/c3_small.err || { tail -20 $O/c3_small.err; exit 1; }
+grep -E "host phases|ties" $O/c3_small.err | tail -30
+python3 -c "import json; d=json.loads(open('$O/c3_small.json').read().strip().splitlines()[-1]); print(d['value'], d['roofline']['kernel_ms_avg'], d['ms_per_step'])"
