@@ -272,8 +272,8 @@ def roofline_fields(tm, achieved, peak, traffic, kernel_ms_avg, bytes_per_launch
             "candidate_equivalent_bytes_per_launch": candidate_bytes}
 
 
-TRAFFIC_FILES = {"c2": os.path.join("profiles", "r3c", "traffic_c2.json"),
-                 "c3": os.path.join("profiles", "r3c", "traffic_c3.json")}
+TRAFFIC_FILES = {"c2": os.path.join("profiles", "r3r", "traffic_c2.json"),
+                 "c3": os.path.join("profiles", "r3r", "traffic_c3.json")}
 
 
 def traffic_fields(traffic, kernel_ms_avg, peak):
