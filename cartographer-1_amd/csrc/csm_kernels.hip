@@ -965,6 +965,12 @@ __device__ __forceinline__ uint32_t ClusterMask(int sl) {
 // kFifo = false: the stack is LIFO with the deepest level on top (depth-first,
 // early leaves). kFifo = true: a FIFO ring (level by level: batches fill up
 // with the whole frontier of a level; leaves come last).
+#ifndef CSM_XFAST
+// Children and roots enter the stack x-fastest, so consecutive lanes of the
+// next batch score nodes adjacent in x: adjacent entries of a polyphase plane
+// (DESIGN.md §5).
+#define CSM_XFAST 1
+#endif
 #ifndef CSM_V4_WAVES
 // Waves per SIMD the register budget targets: 6 workgroups per CU (v5 with
 // its 256-entry LDS ring fits 6 in LDS too; measured best).
@@ -1226,7 +1232,11 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
         const int lk = hexb ? 4 : 2;  // log2 children per node
         const int per_pass = 64 >> lk;
         for (int pass = wave; pass * per_pass < pn; pass += kWaves) {
-          const int nd = pass * per_pass + (lane >> lk), c = lane & ((1 << lk) - 1);
+          const int nd = pass * per_pass + (lane >> lk), cl = lane & ((1 << lk) - 1);
+          // Child c = (a, b) at (xo + a h, yo + b h) sits in lane (b, a)
+          // order when CSM_XFAST (x fastest), else (a, b).
+          const int hb = lk >> 1;
+          const int c = CSM_XFAST ? (((cl & ((1 << hb) - 1)) << hb) | (cl >> hb)) : cl;
           int sum = 0, xo = 0, yo = 0, r = 0, clvl = 0;
           bool exists = false;
           if (nd < pn) {
@@ -1346,8 +1356,14 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
             int r = 0;
             while (sh.root_prefix[r + 1] <= v) ++r;
             const int lv = v - sh.root_prefix[r];
-            const int xo = sh.bounds[r][0] + (lv / sh.vny[r]) * 2 * step;
-            const int yo = sh.bounds[r][2] + (lv % sh.vny[r]) * 2 * step;
+            int xi = lv / sh.vny[r], yi = lv % sh.vny[r];
+            if (CSM_XFAST) {
+              const int vnx = (sh.root_prefix[r + 1] - sh.root_prefix[r]) / sh.vny[r];
+              xi = lv % vnx;
+              yi = lv / vnx;
+            }
+            const int xo = sh.bounds[r][0] + xi * 2 * step;
+            const int yo = sh.bounds[r][2] + yi * 2 * step;
             sh.stack[k] = make_uint2((static_cast<uint32_t>(xo) & 0xffff) | (static_cast<uint32_t>(yo) << 16),
                                      0x3fffffu | (static_cast<uint32_t>(r) << 22) |
                                          (static_cast<uint32_t>(top_level + 1) << 27));

@@ -15,9 +15,10 @@
 // options.refine_with_ceres is off.
 //
 // Multi-GPU (set_communicator): every rank makes the same calls; a rank
-// searches only the pairs of the submaps it owns (ShardOwner) on its own
-// device, and WhenDone gathers the accepted constraints to rank 0 in
-// submission order (constraint_gather.h). Rank 0's callback gets the whole
+// searches only the pairs of the submaps it owns (ShardOwner, Sharding::kStatic)
+// or the chunks of each flush it claims (Sharding::kClaim) on its own device,
+// and WhenDone gathers the accepted constraints to rank 0 in submission order
+// (constraint_gather.h). Rank 0's callback gets the whole
 // result, the other ranks' callbacks an empty one; the metric counters are
 // summed over the ranks and last_error reduced over them at every WhenDone.
 #ifndef CARTOGRAPHER_AMD_CONSTRAINT_BUILDER_2D_H_
@@ -76,8 +77,16 @@ class ConstraintBuilder2D {
   }
 
   // Shards the search over the ranks of `comm` (not owned; outlives the
-  // builder). Call before the first MaybeAdd*.
-  void set_communicator(csm_comm* comm) { comm_ = comm; }
+  // builder). Call before the first MaybeAdd*. kClaim needs
+  // csm_comm_claim_open on `comm`; builders that share a communicator in
+  // kClaim mode need distinct `claim_namespace`s (their counters' keys).
+  void set_communicator(csm_comm* comm, Sharding sharding = Sharding::kStatic,
+                        int chunk_submaps = 4, int claim_namespace = 0) {
+    comm_ = comm;
+    sharding_ = sharding;
+    chunk_submaps_ = chunk_submaps;
+    claim_key_ = static_cast<int64_t>(claim_namespace) << 40;
+  }
 
   void MaybeAddConstraint(const SubmapId& submap_id, const Submap2DView* submap,
                           const NodeId& node_id, const PointCloud* cloud,
@@ -127,6 +136,8 @@ class ConstraintBuilder2D {
   // Pairs skipped because the device search returned an error (not counted
   // as searched), and the last such status.
   int64_t constraints_failed = 0;
+  // Sharding::kClaim: chunks this rank searched (not summed over ranks).
+  int64_t chunks_claimed = 0;
   int last_error = CSM_OK;
 
  private:
@@ -140,10 +151,21 @@ class ConstraintBuilder2D {
     size_t slot;
   };
 
+  bool Claiming() const {
+    return comm_ && csm_comm_size(comm_) > 1 && sharding_ == Sharding::kClaim;
+  }
   bool Owned(const SubmapId& id) const {
-    return !comm_ || csm_comm_size(comm_) <= 1 ||
+    return !comm_ || csm_comm_size(comm_) <= 1 || sharding_ == Sharding::kClaim ||
            ShardOwner(id.trajectory_id, id.submap_index, csm_comm_size(comm_)) ==
                csm_comm_rank(comm_);
+  }
+
+  // DispatchScanMatcherConstruction (constraint_builder_2d.cc:165-186).
+  void EnsureMatcher(const SubmapId& submap_id, const Submap2DView* submap) {
+    if (!matchers_.count(submap_id))
+      matchers_.emplace(submap_id, std::make_shared<FastCorrelativeScanMatcher2D>(
+                                       submap->grid, options_.fast_correlative_scan_matcher_options,
+                                       context_));
   }
 
   // Rank 0 receives every rank's accepted constraints in slot order; the
@@ -198,10 +220,7 @@ class ConstraintBuilder2D {
       constraints_.emplace_back();
       return;
     }
-    if (!matchers_.count(submap_id))  // DispatchScanMatcherConstruction
-      matchers_.emplace(submap_id, std::make_shared<FastCorrelativeScanMatcher2D>(
-                                       submap->grid, options_.fast_correlative_scan_matcher_options,
-                                       context_));
+    if (!Claiming()) EnsureMatcher(submap_id, submap);  // claimed chunks build theirs
     constraints_.emplace_back();
     pending_.push_back(Pending{submap_id, submap, node_id, cloud, full, initial,
                                constraints_.size() - 1});
@@ -212,6 +231,23 @@ class ConstraintBuilder2D {
       num_finished_nodes_ = num_started_nodes_;
       return;
     }
+    if (Claiming()) {
+      const std::vector<std::vector<size_t>> chunks = ClaimChunks(pending_, chunk_submaps_);
+      ForClaimedChunks(comm_, claim_key_++, chunks.size(), [&](size_t c) {
+        ++chunks_claimed;
+        Search(chunks[c]);
+      });
+    } else {
+      std::vector<size_t> all(pending_.size());
+      for (size_t i = 0; i < all.size(); ++i) all[i] = i;
+      Search(all);
+    }
+    pending_.clear();
+    num_finished_nodes_ = num_started_nodes_;
+  }
+
+  // Searches (and refines) pending_[which] as one batch.
+  void Search(const std::vector<size_t>& which_pending) {
     std::vector<float> xyz;
     std::vector<int64_t> offsets{0};
     std::vector<csm_fast2d*> handles;
@@ -219,7 +255,9 @@ class ConstraintBuilder2D {
     std::map<const PointCloud*, int32_t> scan_of;  // a node's cloud uploads once
     std::vector<csm_pair2d> pairs;
     std::vector<std::shared_ptr<FastCorrelativeScanMatcher2D>> keep;
-    for (const Pending& p : pending_) {
+    for (size_t i : which_pending) {
+      const Pending& p = pending_[i];
+      EnsureMatcher(p.submap_id, p.submap);
       auto m = matchers_.at(p.submap_id);
       auto s = slot_of.find(p.submap_id);
       if (s == slot_of.end()) {
@@ -272,8 +310,8 @@ class ConstraintBuilder2D {
       for (size_t k = 0; k < which.size(); ++k) results[which[k]].pose = out[k];
     }
     int64_t failed_this_flush = 0;
-    for (size_t i = 0; i < pending_.size(); ++i) {
-      const Pending& p = pending_[i];
+    for (size_t i = 0; i < which_pending.size(); ++i) {
+      const Pending& p = pending_[which_pending[i]];
       if (results[i].status < 0) {
         // A pair the device path could not search (CSM_ERANGE: a cloud or
         // window past the kernels' limits) yields no
@@ -299,10 +337,8 @@ class ConstraintBuilder2D {
     }
     if (failed_this_flush)
       std::fprintf(stderr, "ConstraintBuilder2D: %lld of %zu pairs skipped (%s)\n",
-                   static_cast<long long>(failed_this_flush), pending_.size(),
+                   static_cast<long long>(failed_this_flush), which_pending.size(),
                    csm_strerror(last_error));
-    pending_.clear();
-    num_finished_nodes_ = num_started_nodes_;
   }
 
   ConstraintBuilderOptions options_;
@@ -314,6 +350,9 @@ class ConstraintBuilder2D {
   csm_scan_set* scans_ = nullptr;
   int num_started_nodes_ = 0, num_finished_nodes_ = 0;
   csm_comm* comm_ = nullptr;
+  Sharding sharding_ = Sharding::kStatic;
+  int chunk_submaps_ = 4;
+  int64_t claim_key_ = 0;                  // kClaim: the next flush's counter
   int64_t reduced_[5] = {0, 0, 0, 0, 0};  // counter totals over ranks at the last WhenDone
 };
 

@@ -18,7 +18,8 @@
 //
 // Multi-GPU (set_communicator), as ConstraintBuilder2D: every rank makes the
 // same calls; a rank builds matchers for and searches only the submaps it
-// owns (ShardOwner) on its own device; WhenDone gathers the accepted
+// owns (ShardOwner, Sharding::kStatic) or the chunks of each flush it claims
+// (Sharding::kClaim) on its own device; WhenDone gathers the accepted
 // constraints to rank 0 as ConstraintRecord3D in submission order
 // (constraint_gather.h), sums the counters and reduces last_error over the
 // ranks. The score lists (constraint_scores, global_constraint_scores,
@@ -68,8 +69,16 @@ class ConstraintBuilder3D {
       : options_(options), context_(context ? context : ThreadContext()) {}
 
   // Shards the search over the ranks of `comm` (not owned; outlives the
-  // builder). Call before the first MaybeAdd*.
-  void set_communicator(csm_comm* comm) { comm_ = comm; }
+  // builder). Call before the first MaybeAdd*. kClaim needs
+  // csm_comm_claim_open on `comm`; builders that share a communicator in
+  // kClaim mode need distinct `claim_namespace`s.
+  void set_communicator(csm_comm* comm, Sharding sharding = Sharding::kStatic,
+                        int chunk_submaps = 4, int claim_namespace = 1) {
+    comm_ = comm;
+    sharding_ = sharding;
+    chunk_submaps_ = chunk_submaps;
+    claim_key_ = static_cast<int64_t>(claim_namespace) << 40;
+  }
 
   void MaybeAddConstraint(const SubmapId& submap_id, const Submap3DView* submap,
                           const NodeId& node_id, const TrajectoryNodeData3D* constant_data,
@@ -129,6 +138,8 @@ class ConstraintBuilder3D {
   // Pairs skipped because the device search returned an error (not counted
   // as searched), and the last such status.
   int64_t constraints_failed = 0;
+  // Sharding::kClaim: chunks this rank searched (not summed over ranks).
+  int64_t chunks_claimed = 0;
   int last_error = CSM_OK;
   std::vector<float> constraint_scores, global_constraint_scores;
   std::vector<float> rotational_scores, low_resolution_scores;
@@ -144,6 +155,7 @@ class ConstraintBuilder3D {
 
   struct Pending {
     SubmapId submap_id;
+    const Submap3DView* submap;
     NodeId node_id;
     const TrajectoryNodeData3D* data;
     bool full;
@@ -151,8 +163,11 @@ class ConstraintBuilder3D {
     size_t slot;
   };
 
+  bool Claiming() const {
+    return comm_ && csm_comm_size(comm_) > 1 && sharding_ == Sharding::kClaim;
+  }
   bool Owned(const SubmapId& id) const {
-    return !comm_ || csm_comm_size(comm_) <= 1 ||
+    return !comm_ || csm_comm_size(comm_) <= 1 || sharding_ == Sharding::kClaim ||
            ShardOwner(id.trajectory_id, id.submap_index, csm_comm_size(comm_)) ==
                csm_comm_rank(comm_);
   }
@@ -220,18 +235,22 @@ class ConstraintBuilder3D {
       constraints_.emplace_back();
       return;
     }
-    if (!matchers_.count(submap_id)) {  // DispatchScanMatcherConstruction
-      auto m = std::make_shared<SubmapScanMatcher>();
-      m->high.reset(new HybridGrid3D(submap->high_resolution_hybrid_grid, context_));
-      m->low.reset(new HybridGrid3D(submap->low_resolution_hybrid_grid, context_));
-      m->matcher.reset(new FastCorrelativeScanMatcher3D(
-          *m->high, m->low.get(), &submap->rotational_scan_matcher_histogram,
-          options_.fast_correlative_scan_matcher_options_3d, context_));
-      matchers_.emplace(submap_id, std::move(m));
-    }
+    if (!Claiming()) EnsureMatcher(submap_id, submap);  // claimed chunks build theirs
     constraints_.emplace_back();
-    pending_.push_back(Pending{submap_id, node_id, data, full, node_pose, submap_pose,
+    pending_.push_back(Pending{submap_id, submap, node_id, data, full, node_pose, submap_pose,
                                constraints_.size() - 1});
+  }
+
+  // DispatchScanMatcherConstruction (constraint_builder_3d.cc:170-198).
+  void EnsureMatcher(const SubmapId& submap_id, const Submap3DView* submap) {
+    if (matchers_.count(submap_id)) return;
+    auto m = std::make_shared<SubmapScanMatcher>();
+    m->high.reset(new HybridGrid3D(submap->high_resolution_hybrid_grid, context_));
+    m->low.reset(new HybridGrid3D(submap->low_resolution_hybrid_grid, context_));
+    m->matcher.reset(new FastCorrelativeScanMatcher3D(
+        *m->high, m->low.get(), &submap->rotational_scan_matcher_histogram,
+        options_.fast_correlative_scan_matcher_options_3d, context_));
+    matchers_.emplace(submap_id, std::move(m));
   }
 
   void Flush() {
@@ -239,16 +258,35 @@ class ConstraintBuilder3D {
       num_finished_nodes_ = num_started_nodes_;
       return;
     }
+    if (Claiming()) {
+      const std::vector<std::vector<size_t>> chunks = ClaimChunks(pending_, chunk_submaps_);
+      ForClaimedChunks(comm_, claim_key_++, chunks.size(), [&](size_t c) {
+        ++chunks_claimed;
+        Search(chunks[c]);
+      });
+    } else {
+      std::vector<size_t> all(pending_.size());
+      for (size_t i = 0; i < all.size(); ++i) all[i] = i;
+      Search(all);
+    }
+    pending_.clear();
+    num_finished_nodes_ = num_started_nodes_;
+  }
+
+  // Searches (and refines) pending_[which] as one batch.
+  void Search(const std::vector<size_t>& which_pending) {
     std::vector<csm_fast3d*> handles;
     std::vector<std::shared_ptr<SubmapScanMatcher>> keep;
     std::map<SubmapId, int> slot_of;
     std::map<const TrajectoryNodeData3D*, int32_t> node_of;  // a node's data uploads once
     std::vector<csm_node3d> nodes;
     std::vector<csm_pair3d> pairs;
-    for (const Pending& p : pending_) {
+    for (size_t i : which_pending) {
+      const Pending& p = pending_[i];
       auto s = slot_of.find(p.submap_id);
       if (s == slot_of.end()) {
         s = slot_of.emplace(p.submap_id, static_cast<int>(handles.size())).first;
+        EnsureMatcher(p.submap_id, p.submap);
         auto m = matchers_.at(p.submap_id);
         handles.push_back(m->matcher->handle());
         keep.push_back(m);
@@ -303,8 +341,8 @@ class ConstraintBuilder3D {
       for (size_t k = 0; k < which.size(); ++k) results[which[k]].pose = out[k];
     }
     int64_t failed_this_flush = 0;
-    for (size_t i = 0; i < pending_.size(); ++i) {
-      const Pending& p = pending_[i];
+    for (size_t i = 0; i < which_pending.size(); ++i) {
+      const Pending& p = pending_[which_pending[i]];
       if (results[i].status < 0) {
         // A pair the device path could not search (CSM_ERANGE: a cloud or
         // window past the kernels' limits) yields no
@@ -332,10 +370,8 @@ class ConstraintBuilder3D {
     }
     if (failed_this_flush)
       std::fprintf(stderr, "ConstraintBuilder3D: %lld of %zu pairs skipped (%s)\n",
-                   static_cast<long long>(failed_this_flush), pending_.size(),
+                   static_cast<long long>(failed_this_flush), which_pending.size(),
                    csm_strerror(last_error));
-    pending_.clear();
-    num_finished_nodes_ = num_started_nodes_;
   }
 
   ConstraintBuilderOptions options_;
@@ -346,6 +382,9 @@ class ConstraintBuilder3D {
   std::vector<Pending> pending_;
   int num_started_nodes_ = 0, num_finished_nodes_ = 0;
   csm_comm* comm_ = nullptr;
+  Sharding sharding_ = Sharding::kStatic;
+  int chunk_submaps_ = 4;
+  int64_t claim_key_ = 0;                  // kClaim: the next flush's counter
   int64_t reduced_[5] = {0, 0, 0, 0, 0};  // counter totals over ranks at the last WhenDone
 };
 

@@ -17,6 +17,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <vector>
 
 #include "../csm_amd.h"
@@ -65,6 +66,52 @@ inline void CommCheck(int code, const char* what) {
   if (code != CSM_OK) {
     std::fprintf(stderr, "F %s: %s (%d)\n", what, csm_strerror(code), code);
     std::abort();
+  }
+}
+
+// How a sharded builder splits its pairs over the ranks.
+//   kStatic: by submap (ShardOwner). A rank builds and keeps only the
+//            matchers of its own submaps; no exchange until WhenDone.
+//   kClaim:  dynamically, the reference's shared task queue
+//            (common/thread_pool.cc:80-106) stretched over ranks: every flush's
+//            pairs are cut into chunks of `chunk_submaps` submaps (submaps in
+//            first-submission order) and idle ranks claim the next chunk with
+//            csm_comm_fetch_add (the communicator needs csm_comm_claim_open).
+//            A rank builds the matchers of the submaps it claims, on first
+//            claim. Balances uneven pair costs; each rank may end up holding
+//            any submap's matcher.
+enum class Sharding { kStatic, kClaim };
+
+// A flush's pending pairs (anything with a `submap_id`) grouped into claim
+// chunks: indices into `pending`, chunk_submaps submaps per chunk.
+template <typename Pending>
+std::vector<std::vector<size_t>> ClaimChunks(const std::vector<Pending>& pending, int chunk_submaps) {
+  std::vector<std::vector<size_t>> by_submap;
+  std::map<decltype(pending[0].submap_id), size_t> index;
+  for (size_t i = 0; i < pending.size(); ++i) {
+    auto it = index.emplace(pending[i].submap_id, by_submap.size()).first;
+    if (it->second == by_submap.size()) by_submap.emplace_back();
+    by_submap[it->second].push_back(i);
+  }
+  const size_t per = static_cast<size_t>(chunk_submaps < 1 ? 1 : chunk_submaps);
+  std::vector<std::vector<size_t>> chunks;
+  for (size_t s = 0; s < by_submap.size(); ++s) {
+    if (s % per == 0) chunks.emplace_back();
+    chunks.back().insert(chunks.back().end(), by_submap[s].begin(), by_submap[s].end());
+  }
+  return chunks;
+}
+
+// Claims chunks of counter `key` until they run out, calling fn(chunk index)
+// for each one this rank wins. Not collective; every rank must call it with
+// the same key and count for the queue to drain.
+template <typename Fn>
+void ForClaimedChunks(csm_comm* comm, int64_t key, size_t num_chunks, Fn fn) {
+  for (;;) {
+    int64_t c = 0;
+    CommCheck(csm_comm_fetch_add(comm, key, 1, &c), "csm_comm_fetch_add");
+    if (c < 0 || static_cast<size_t>(c) >= num_chunks) return;
+    fn(static_cast<size_t>(c));
   }
 }
 

@@ -20,6 +20,10 @@
 //   distributed_builder_test builder3d <rank> <world> <port>
 //       GPU: the same for ConstraintBuilder3D on walls of voxels (4 submaps,
 //       6 nodes, local and global pairs), plus the score metric lists.
+//   distributed_builder_test builder-claim|builder3d-claim <rank> <world> <port>
+//       The same with Sharding::kClaim (one-submap chunks claimed through
+//       csm_comm_fetch_add, claim service on port + 1); every rank prints
+//       "claimed <n>" to stderr.
 #include <sys/wait.h>
 #include <unistd.h>
 
@@ -274,12 +278,23 @@ static World MakeWorld() {
   return w;
 }
 
-static int BuilderMain(int rank, int world, int port) {
+// Connects rank `rank` of `world` (none for a world of 1); with `claim`, also
+// opens the claim service on port + 1.
+static csm_comm* Connect(int rank, int world, int port, bool claim) {
   csm_comm* comm = nullptr;
   if (world > 1 && csm_comm_create_tcp(rank, world, "127.0.0.1", port, &comm) != CSM_OK) {
     std::fprintf(stderr, "comm create failed\n");
-    return 2;
+    std::exit(2);
   }
+  if (comm && claim && csm_comm_claim_open(comm, "127.0.0.1", port + 1) != CSM_OK) {
+    std::fprintf(stderr, "claim open failed\n");
+    std::exit(2);
+  }
+  return comm;
+}
+
+static int BuilderMain(int rank, int world, int port, bool claim) {
+  csm_comm* comm = Connect(rank, world, port, claim);
   const World w = MakeWorld();
   ConstraintBuilderOptions o;
   o.sampling_ratio = 1.;
@@ -287,7 +302,7 @@ static int BuilderMain(int rank, int world, int port) {
   o.global_localization_min_score = 0.55f;
   o.max_constraint_distance = 15.;
   ConstraintBuilder2D builder(o);
-  if (comm) builder.set_communicator(comm);
+  if (comm) builder.set_communicator(comm, claim ? Sharding::kClaim : Sharding::kStatic, 1);
   for (int k = 0; k < static_cast<int>(w.clouds.size()); ++k) {
     for (int s = 0; s < static_cast<int>(w.submaps.size()); ++s) {
       const SubmapId sid{0, s};
@@ -319,6 +334,7 @@ static int BuilderMain(int rank, int world, int port) {
     std::fprintf(stderr, "rank %d got a non-empty result\n", rank);
     return 1;
   }
+  if (claim) std::fprintf(stderr, "claimed %lld\n", static_cast<long long>(builder.chunks_claimed));
   if (comm) csm_comm_destroy(comm);
   return 0;
 }
@@ -363,12 +379,8 @@ static TrajectoryNodeData3D WallNode(int k) {
   return node;
 }
 
-static int Builder3DMain(int rank, int world, int port) {
-  csm_comm* comm = nullptr;
-  if (world > 1 && csm_comm_create_tcp(rank, world, "127.0.0.1", port, &comm) != CSM_OK) {
-    std::fprintf(stderr, "comm create failed\n");
-    return 2;
-  }
+static int Builder3DMain(int rank, int world, int port, bool claim) {
+  csm_comm* comm = Connect(rank, world, port, claim);
   std::vector<Submap3DView> submaps;
   for (int s = 0; s < 4; ++s) submaps.push_back(WallSubmap(s));
   std::vector<TrajectoryNodeData3D> nodes;
@@ -382,7 +394,7 @@ static int Builder3DMain(int rank, int world, int port) {
   o.fast_correlative_scan_matcher_options_3d.linear_z_search_window = 0.2;
   o.fast_correlative_scan_matcher_options_3d.angular_search_window = 0.05;
   ConstraintBuilder3D builder(o);
-  if (comm) builder.set_communicator(comm);
+  if (comm) builder.set_communicator(comm, claim ? Sharding::kClaim : Sharding::kStatic, 1);
   for (int k = 0; k < 6; ++k) {
     for (int s = 0; s < 4; ++s) {
       if ((k + s) % 4 == 0)
@@ -417,6 +429,7 @@ static int Builder3DMain(int rank, int world, int port) {
     std::fprintf(stderr, "rank %d got a non-empty result\n", rank);
     return 1;
   }
+  if (claim) std::fprintf(stderr, "claimed %lld\n", static_cast<long long>(builder.chunks_claimed));
   if (comm) csm_comm_destroy(comm);
   return 0;
 }
@@ -427,12 +440,16 @@ int main(int argc, char** argv) {
     return Gather3DMain(std::atoi(argv[2]), std::atoi(argv[3]));
   if (argc == 4 && std::string(argv[1]) == "diverge")
     return DivergeMain(std::atoi(argv[2]), std::atoi(argv[3]));
-  if (argc == 5 && std::string(argv[1]) == "builder")
-    return BuilderMain(std::atoi(argv[2]), std::atoi(argv[3]), std::atoi(argv[4]));
-  if (argc == 5 && std::string(argv[1]) == "builder3d")
-    return Builder3DMain(std::atoi(argv[2]), std::atoi(argv[3]), std::atoi(argv[4]));
+  if (argc == 5) {
+    const std::string m = argv[1];
+    const int rank = std::atoi(argv[2]), world = std::atoi(argv[3]), port = std::atoi(argv[4]);
+    if (m == "builder" || m == "builder-claim") return BuilderMain(rank, world, port, m != "builder");
+    if (m == "builder3d" || m == "builder3d-claim")
+      return Builder3DMain(rank, world, port, m != "builder3d");
+  }
   std::fprintf(stderr,
-               "usage: %s gather|gather3d|diverge <world> <port> | builder|builder3d <rank> <world> <port>\n",
+               "usage: %s gather|gather3d|diverge <world> <port> | "
+               "builder|builder3d|builder-claim|builder3d-claim <rank> <world> <port>\n",
                argv[0]);
   return 2;
 }

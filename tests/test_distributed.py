@@ -203,10 +203,26 @@ def test_cpp_diverging_submissions_abort(csm):
     assert out.stderr.count("ranks submitted different pair sequences") == 3, out.stderr
 
 
+def _run_ranks(mode, world):
+    import subprocess
+    port = str(_free_port())
+    procs = [subprocess.Popen([DIST_BIN, mode, str(r), str(world), port], stdout=subprocess.PIPE,
+                              stderr=subprocess.PIPE, text=True) for r in range(world)]
+    outs = [p.communicate(timeout=180) for p in procs]
+    for p, (o, e) in zip(procs, outs):
+        assert p.returncode == 0, e
+    if mode.endswith("-claim"):
+        claimed = [int(l.split()[1]) for _, e in outs for l in e.splitlines() if l.startswith("claimed ")]
+        assert len(claimed) == world and sum(claimed) > 0, [e for _, e in outs]
+    return outs
+
+
 @pytest.mark.gpu
-def test_cpp_sharded_builder_3d_matches_single_rank(csm):
+@pytest.mark.parametrize("mode,world", [("builder3d", 2), ("builder3d-claim", 2)])
+def test_cpp_sharded_builder_3d_matches_single_rank(csm, mode, world):
     """The C++ ConstraintBuilder3D sharded over 2 ranks (two processes on the
-    one GPU, TCP transport) delivers on rank 0 what the single-rank builder
+    one GPU, TCP transport; by submap owner, or by chunks claimed through
+    csm_comm_fetch_add) delivers on rank 0 what the single-rank builder
     delivers: same constraints in submission order, same summed counters and
     the same score metric lists (constraint_builder_3d.cc:200-305)."""
     import subprocess
@@ -214,37 +230,29 @@ def test_cpp_sharded_builder_3d_matches_single_rank(csm):
     single = subprocess.run([DIST_BIN, "builder3d", "0", "1", "0"], capture_output=True, text=True,
                             timeout=120)
     assert single.returncode == 0, single.stderr
-    port = str(_free_port())
-    procs = [subprocess.Popen([DIST_BIN, "builder3d", str(r), "2", port], stdout=subprocess.PIPE,
-                              stderr=subprocess.PIPE, text=True) for r in range(2)]
-    outs = [p.communicate(timeout=120) for p in procs]
-    for p, (o, e) in zip(procs, outs):
-        assert p.returncode == 0, e
+    outs = _run_ranks(mode, world)
     lines = single.stdout.strip().splitlines()
     assert sum(1 for l in lines if l.startswith("c ")) >= 4, single.stdout
     assert any(l.startswith("c ") and l.endswith(" 1") for l in lines), single.stdout  # a global one
     assert outs[0][0].strip().splitlines() == lines
-    assert outs[1][0].strip() == ""
+    assert all(o.strip() == "" for o, _ in outs[1:])
 
 
 @pytest.mark.gpu
-def test_cpp_sharded_builder_matches_single_rank(csm):
-    """The C++ ConstraintBuilder2D sharded over 2 ranks (two processes on the
-    one GPU, TCP transport) delivers on rank 0 exactly what the single-rank
-    builder delivers: same constraints, same (submission) order, same summed
-    counters."""
+@pytest.mark.parametrize("mode,world", [("builder", 2), ("builder-claim", 2), ("builder-claim", 3)])
+def test_cpp_sharded_builder_matches_single_rank(csm, mode, world):
+    """The C++ ConstraintBuilder2D sharded over 2-3 ranks (processes on the
+    one GPU, TCP transport; Sharding::kStatic by submap owner, or
+    Sharding::kClaim with one-submap chunks claimed dynamically) delivers on
+    rank 0 exactly what the single-rank builder delivers: same constraints,
+    same (submission) order, same summed counters."""
     import subprocess
     _build_dist()
     single = subprocess.run([DIST_BIN, "builder", "0", "1", "0"], capture_output=True, text=True,
                             timeout=120)
     assert single.returncode == 0, single.stderr
-    port = str(_free_port())
-    procs = [subprocess.Popen([DIST_BIN, "builder", str(r), "2", port], stdout=subprocess.PIPE,
-                              stderr=subprocess.PIPE, text=True) for r in range(2)]
-    outs = [p.communicate(timeout=120) for p in procs]
-    for p, (o, e) in zip(procs, outs):
-        assert p.returncode == 0, e
+    outs = _run_ranks(mode, world)
     lines = single.stdout.strip().splitlines()
     assert sum(1 for l in lines if l.startswith("c ")) >= 5, single.stdout
     assert outs[0][0].strip().splitlines() == lines
-    assert outs[1][0].strip() == ""
+    assert all(o.strip() == "" for o, _ in outs[1:])
