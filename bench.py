@@ -15,7 +15,8 @@ chunk's pyramids on their GPU, search it as one batch, and finally gather
 the accepted constraints to rank 0 in submission order (RCCL). Node clouds
 are resident in HBM before timing; submap pyramids are built inside it.
 
-Secondary lines (rank 0, one GPU): C2 (500 x 50), C1 RTCSM2D ms/scan-match,
+Secondary lines (rank 0, one GPU): C2 (500 x 50), the same C2 queue at
+min_score 0.65 (a low-acceptance sweep), C1 RTCSM2D ms/scan-match,
 the drop-in's call patterns, voxel filter, Ceres refinement, C4 RTCSM3D and
 C5 FastCSM3D (500 nodes x 200 submaps, split over the ranks).
 
@@ -124,6 +125,16 @@ def main():
                                    transport, barrier_sync, headline=False)
             errors += c2_errors
             out["c2"] = c2
+            # The same C2 queue at a stricter min_score: a low-acceptance sweep,
+            # closer to a real loop-closure queue where most pairs fail.
+            strict = argparse.Namespace(**{**vars(args), "min_score": 0.65})
+            c2s, c2s_errors = c2_run(csm, ctx, strict, rank, world_size, dist, coll_dev, gather,
+                                     transport, barrier_sync, headline=False, extras=False)
+            errors += c2s_errors
+            out["c2_strict"] = {k: c2s[k] for k in ("value", "unit", "ms_per_step", "config",
+                                                    "accepted_constraints_per_step",
+                                                    "errors_per_step")}
+            out["c2_strict"]["kernel_ms"] = c2s["roofline"]["kernel_ms_avg"]
         out["rt2d"] = rt2d_bench(csm, ctx, args)
     if rank == 0 and world_size == 1 and not args.no_3d:
         out["rt3d"] = rt3d_bench(csm, ctx, args)
@@ -147,7 +158,7 @@ def main():
 
 
 def c2_run(csm, ctx, args, rank, world_size, dist, coll_dev, gather, transport, barrier_sync,
-           headline):
+           headline, extras=True):
     """Config C2: 500 scans x 50 submaps per GPU, submap-sharded (weak
     scaling). As the headline (--workload c2) it carries the roofline and its
     CPU baseline; as a secondary line (default run) one step, plus the
@@ -238,6 +249,7 @@ def c2_run(csm, ctx, args, rank, world_size, dist, coll_dev, gather, transport, 
         "accepted_constraints_per_step": accepted,
         "errors_per_step": errors / steps,
         "stack_high_water": int(tm.stack_high_water),
+        "tied_pairs": int(tm.tied_pairs), "ties_unresolved": int(tm.ties_unresolved),
         "search_levels": {"candidates_per_pair": [c / max(n_pairs * steps, 1) for c in lv_cands],
                           "mean_lanes_per_batch": [c / b if b else 0 for c, b in zip(lv_cands, lv_batches)]},
         "setup_s": {"world": gen_s, "pyramids_and_upload": build_s},
@@ -247,7 +259,7 @@ def c2_run(csm, ctx, args, rank, world_size, dist, coll_dev, gather, transport, 
             out.pop(k)
     if rank == 0 and world_size == 1 and headline and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(world, my_submaps, args)
-    if rank == 0 and world_size == 1 and not args.no_rt:
+    if rank == 0 and world_size == 1 and not args.no_rt and extras:
         out["dropin"] = dropin_bench(csm, ctx, matchers, scans, world, args)
         out["voxel_filter"] = voxel_filter_bench(csm, ctx, world, args)
         out["ceres2d"] = ceres_bench(csm, ctx, world, matchers, scans, pairs, res, my_submaps,
@@ -435,8 +447,8 @@ def dropin_bench(csm, ctx, matchers, scans, world, args):
             "single_call": {"calls": len(single_ms),
                             "ms_per_match_full_submap_median": float(np.median(single_ms)),
                             "pairs_per_s": 1e3 / float(np.median(single_ms))},
-            "note": "through the Python ctypes mirror; the batch path re-uploads the pairs and "
-                    "rotation tables per call"}
+            "note": "through the Python ctypes mirror; a batch uploads its pair descriptors, the "
+                    "scan set's rotation tables are built once and kept on the device"}
 
 
 def voxel_filter_bench(csm, ctx, world, args):
@@ -1001,6 +1013,9 @@ def c3_run(csm, ctx, args, rank, world_size, dist, coll_dev, comm, gather, trans
         "errors_per_step": errors / args.steps,
         "stack_high_water": int(tm.stack_high_water),
         "chunks": n_chunks, "chunks_claimed": int(claimed), "chunks_max_rank": int(chunks_max),
+        # Pairs with exactly tied maxima (resolved to the reference's pick,
+        # csm_host.cc ResolveTies) and any left at the smallest-key leaf.
+        "tied_pairs_rank0": int(tm.tied_pairs), "ties_unresolved_rank0": int(tm.ties_unresolved),
         "kernel_s_rank0": tm.search_kernel_ms * 1e-3, "search_launches_rank0": int(tm.search_launches),
         "search_levels": {"candidates_per_pair": [c / max(mine * K * N, 1) for c in lv_cands],
                           "mean_lanes_per_batch": [c / b if b else 0 for c, b in zip(lv_cands, lv_batches)]},

@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--k", default="1,2,2,4,4,8,8,8,8")
     ap.add_argument("--depth", type=int, default=9)
     ap.add_argument("--min-score", type=float, default=0.55)
+    ap.add_argument("--dive", type=int, default=0,
+                    help="greedy dive incumbent from every n-th rotation (0: off)")
     args = ap.parse_args()
     ks = [int(v) for v in args.k.split(",")]
     import __graft_entry__ as ge
@@ -42,7 +44,7 @@ def main():
     half = args.pairs // 2
     pairs = [(s, int(world.submap_nodes[s])) for s in rng.choice(50, half, replace=False)]
     pairs += list(zip(rng.randint(0, 50, args.pairs - half), rng.randint(0, 500, args.pairs - half)))
-    tot = {"matched": [0, 0, 0], "unmatched": [0, 0, 0]}  # gathers at s_min, at S, pairs
+    tot = {"matched": [0, 0, 0, 0], "unmatched": [0, 0, 0, 0]}  # gathers at s_min, at S, pairs, at dive
     for pi, (s, nd) in enumerate(pairs):
         g = world.grid(int(s))
         cells = g.cells
@@ -80,6 +82,47 @@ def main():
             s_min += 1
         S = int(round((score - 0.1) / 0.8 * 255 * n)) if ok else None
         kind = "matched" if ok else "unmatched"
+
+        def entries(r):
+            ix, iy = disc[r, :, 0].astype(np.int64), disc[r, :, 1].astype(np.int64)
+            ent = []
+            for c in range(D):
+                k = ks[c]
+                if c == 0:
+                    ent.append((ix, iy, np.ones(n, np.int64), 1))
+                    continue
+                qx, qy = (ix // k) * k, (iy // k) * k
+                key = qx * 100000 + qy
+                head = np.ones(n, bool)
+                head[1:] = key[1:] != key[:-1]
+                idx = np.nonzero(head)[0]
+                cnt = np.diff(np.append(idx, n))
+                ent.append((qx[idx], qy[idx], cnt.astype(np.int64), (1 << c) + k - 1))
+            return ent
+
+        # Greedy dive per rotation: from the best top-level node, the best
+        # child at every level down to a leaf (exact leaf sum).
+        S_dive = 0
+        if args.dive:
+            for r in range(0, ns, args.dive):
+                ent = entries(r)
+                bx0, bx1, by0, by1 = bounds[r]
+                st = 1 << (D - 1)
+                fx, fy = [a.ravel() for a in np.meshgrid(np.arange(bx0, bx1 + 1, st),
+                                                         np.arange(by0, by1 + 1, st), indexing="ij")]
+                d = D - 1
+                while True:
+                    sc = score_e(ent[d], fx, fy)
+                    b = int(np.argmax(sc))
+                    if d == 0:
+                        S_dive = max(S_dive, int(sc[b]))
+                        break
+                    hh = 1 << (d - 1)
+                    cx_ = np.array([fx[b] + a * hh for a in range(2) for bb in range(2)])
+                    cy_ = np.array([fy[b] + bb * hh for a in range(2) for bb in range(2)])
+                    okc = (cx_ <= bx1) & (cy_ <= by1)
+                    fx, fy = cx_[okc], cy_[okc]
+                    d -= 1
         for r in np.linspace(0, ns - 1, args.rots).astype(int):
             ix, iy = disc[r, :, 0].astype(np.int64), disc[r, :, 1].astype(np.int64)
             ent = []
@@ -97,7 +140,8 @@ def main():
                 ent.append((qx[idx], qy[idx], cnt.astype(np.int64), (1 << c) + k - 1))
             bx0, bx1, by0, by1 = bounds[r]
             st = 1 << (D - 1)
-            for slot, thr in ((0, s_min), (1, None if S is None else S - 1)):
+            for slot, thr in ((0, s_min), (1, None if S is None else S - 1),
+                              (3, max(s_min, S_dive - 1) if args.dive else None)):
                 if thr is None:
                     continue
                 fx, fy = [a.ravel() for a in np.meshgrid(np.arange(bx0, bx1 + 1, st),
@@ -121,11 +165,13 @@ def main():
             if S is None:
                 tot[kind][1] += 0
         tot[kind][2] += 1
-        print(f"pair {pi} ({s},{nd}) {kind} score {score:.3f} rotations {ns}", flush=True)
-    for kind, (a, b, npairs) in tot.items():
+        print(f"pair {pi} ({s},{nd}) {kind} score {score:.3f} rotations {ns} S {S} dive {S_dive} "
+              f"s_min {s_min}", flush=True)
+    for kind, (a, b, npairs, dv) in tot.items():
         if npairs:
             print(f"{kind}: {npairs} pairs, gathers/pair at s_min {a / npairs:.3g}"
-                  + (f", at S {b / npairs:.3g} ({b / a:.2f}x)" if b else ""))
+                  + (f", at S {b / npairs:.3g} ({b / a:.2f}x)" if b else "")
+                  + (f", at the best dive {dv / npairs:.3g} ({dv / a:.2f}x)" if dv else ""))
 
 
 if __name__ == "__main__":
