@@ -48,13 +48,14 @@ int AutoSearchDepth(int configured, int nx, int ny) {
   return std::max(d, configured);
 }
 
-// Scan cluster size per child level (SubmapDesc::cshift): k = 1, 2, 4, 4, 4,
+// Scan cluster size per child level (SubmapDesc::cshift): k = 1, 1, 4, 4, 4,
 // 8, ... cells per side (log2), first chosen by tools/frontier_sim.py
 // (cluster) on the C2 world (0.39x the lookups of exact per-level bounds),
-// then level 2's k = 4 by GPU A/B with kernel v5 (profiles/r3t). Level 0 is
-// always exact (k = 1) and k <= 2^level. CSM_CLUSTER="s0,s1,..." overrides.
+// then by GPU A/B with kernel v5: level 2 at k = 4 (profiles/r3t), level 1 on
+// the raw scan so no k = 2 list is built (profiles/r3w). Level 0 is always
+// exact (k = 1) and k <= 2^level. CSM_CLUSTER="s0,s1,..." overrides.
 void ClusterShifts(int32_t* out) {
-  static const int kDefault[kMaxLevels] = {0, 1, 2, 2, 2, 3, 3, 3, 3, 3, 3, 3};
+  static const int kDefault[kMaxLevels] = {0, 0, 2, 2, 2, 3, 3, 3, 3, 3, 3, 3};
   for (int l = 0; l < kMaxLevels; ++l) out[l] = kDefault[l];
   if (const char* env = std::getenv("CSM_CLUSTER")) {
     int l = 0;

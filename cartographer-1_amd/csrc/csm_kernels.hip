@@ -713,9 +713,13 @@ __device__ __forceinline__ void V4Score(Shared& sh, const uint32_t* cells, const
                                         int raw_end, const SubmapDesc& sm) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nodes = Uniform(sh.nodes);
-  const int groups = 64 / nodes;
-  const int node = lane & (nodes - 1);
-  const int g = lane / nodes;
+  // Lane -> (node, entry group): node = lane mod pw, pw = nodes rounded up to
+  // a power of two; the lanes of the pw - nodes missing nodes sit out.
+  const int pw = nodes <= 1 ? 1 : 1 << (32 - __clz(nodes - 1));
+  const int groups = 64 / pw;
+  const bool active = (lane & (pw - 1)) < nodes;
+  const int node = active ? lane & (pw - 1) : 0;
+  const int g = lane / pw;
   // Each node scores its children at its own child level: one descriptor
   // spans the whole pyramid, the level is a per-lane byte offset.
   const int level = sh.node_level[node] - 1;
@@ -757,32 +761,34 @@ __device__ __forceinline__ void V4Score(Shared& sh, const uint32_t* cells, const
   // U entries per lane in flight, then the remainder one at a time: every
   // issued load costs texture-path cycles even when its lanes are out of
   // range, so the tail issues no more loads than it needs.
-  int i = s;
-  for (; i + U * groups <= e; i += U * groups) {
-    int ad[U];
-    uint32_t c[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int idx = i + u * groups + g;
-      const bool in = idx < len;
-      const int j = in ? idx : 0;
-      ad[u] = address(P[j], in);
-      c[u] = in ? (raw ? 1u : Cn[j]) : 0u;
+  if (active) {  // the missing nodes' lanes issue no loads
+    int i = s;
+    for (; i + U * groups <= e; i += U * groups) {
+      int ad[U];
+      uint32_t c[U];
+  #pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int idx = i + u * groups + g;
+        const bool in = idx < len;
+        const int j = in ? idx : 0;
+        ad[u] = address(P[j], in);
+        c[u] = in ? (raw ? 1u : Cn[j]) : 0u;
+      }
+      uint32_t v[U];
+  #pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, ad[u], 0, 0);
+  #pragma unroll
+      for (int u = 0; u < U; ++u) accumulate(v[u], c[u]);
     }
-    uint32_t v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) v[u] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, ad[u], 0, 0);
-#pragma unroll
-    for (int u = 0; u < U; ++u) accumulate(v[u], c[u]);
+    for (; i < e; i += groups) {
+      const int idx = i + g;
+      const bool in = idx < e && idx < len;
+      const int j = in ? idx : 0;
+      const uint32_t vv = __builtin_amdgcn_raw_buffer_load_b32(rsrc, address(P[j], in), 0, 0);
+      accumulate(vv, in ? (raw ? 1u : Cn[j]) : 0u);
+    }
   }
-  for (; i < e; i += groups) {
-    const int idx = i + g;
-    const bool in = idx < e && idx < len;
-    const int j = in ? idx : 0;
-    const uint32_t vv = __builtin_amdgcn_raw_buffer_load_b32(rsrc, address(P[j], in), 0, 0);
-    accumulate(vv, in ? (raw ? 1u : Cn[j]) : 0u);
-  }
-  for (int m = nodes; m < 64; m <<= 1) {
+  for (int m = pw; m < 64; m <<= 1) {
     a0 += __shfl_xor(a0, m, 64);
     a1 += __shfl_xor(a1, m, 64);
     a2 += __shfl_xor(a2, m, 64);
@@ -807,9 +813,11 @@ __device__ __forceinline__ void V4ScoreHex(Shared& sh, const uint32_t* cells, co
                                            int raw_end, const SubmapDesc& sm) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nodes = Uniform(sh.nodes);
-  const int groups = 64 / nodes;
-  const int node = lane & (nodes - 1);
-  const int g = lane / nodes;
+  const int pw = nodes <= 1 ? 1 : 1 << (32 - __clz(nodes - 1));  // as V4Score
+  const int groups = 64 / pw;
+  const bool active = (lane & (pw - 1)) < nodes;
+  const int node = active ? lane & (pw - 1) : 0;
+  const int g = lane / pw;
   const int level = sh.node_level[node] - 2;
   const int* L = sh.lv[level];
   const int qw = L[0], qh = L[1], qoff = L[2], pws16 = L[3], ps16 = L[4];
@@ -850,32 +858,34 @@ __device__ __forceinline__ void V4ScoreHex(Shared& sh, const uint32_t* cells, co
         acc[4 * a + b] = __builtin_amdgcn_udot4(v[a], c << (8 * b), acc[4 * a + b], false);
     }
   };
-  int i = s;
-  for (; i + U * groups <= e; i += U * groups) {
-    int ad[U];
-    uint32_t c[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int idx = i + u * groups + g;
-      const bool in = idx < len;
-      const int j = in ? idx : 0;
-      ad[u] = address(P[j], in);
-      c[u] = in ? (raw ? 1u : Cn[j]) : 0u;
+  if (active) {  // the missing nodes' lanes issue no loads
+    int i = s;
+    for (; i + U * groups <= e; i += U * groups) {
+      int ad[U];
+      uint32_t c[U];
+  #pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int idx = i + u * groups + g;
+        const bool in = idx < len;
+        const int j = in ? idx : 0;
+        ad[u] = address(P[j], in);
+        c[u] = in ? (raw ? 1u : Cn[j]) : 0u;
+      }
+      decltype(__builtin_amdgcn_raw_buffer_load_b128(rsrc, 0, 0, 0)) v[U];
+  #pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, ad[u], 0, 0);
+  #pragma unroll
+      for (int u = 0; u < U; ++u) accumulate(v[u], c[u]);
     }
-    decltype(__builtin_amdgcn_raw_buffer_load_b128(rsrc, 0, 0, 0)) v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) v[u] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, ad[u], 0, 0);
-#pragma unroll
-    for (int u = 0; u < U; ++u) accumulate(v[u], c[u]);
+    for (; i < e; i += groups) {
+      const int idx = i + g;
+      const bool in = idx < e && idx < len;
+      const int j = in ? idx : 0;
+      const auto vv = __builtin_amdgcn_raw_buffer_load_b128(rsrc, address(P[j], in), 0, 0);
+      accumulate(vv, in ? (raw ? 1u : Cn[j]) : 0u);
+    }
   }
-  for (; i < e; i += groups) {
-    const int idx = i + g;
-    const bool in = idx < e && idx < len;
-    const int j = in ? idx : 0;
-    const auto vv = __builtin_amdgcn_raw_buffer_load_b128(rsrc, address(P[j], in), 0, 0);
-    accumulate(vv, in ? (raw ? 1u : Cn[j]) : 0u);
-  }
-  for (int m = nodes; m < 64; m <<= 1) {
+  for (int m = pw; m < 64; m <<= 1) {
 #pragma unroll
     for (int j = 0; j < 16; ++j) acc[j] += __shfl_xor(acc[j], m, 64);
   }
@@ -965,6 +975,12 @@ __device__ __forceinline__ uint32_t ClusterMask(int sl) {
 // kFifo = false: the stack is LIFO with the deepest level on top (depth-first,
 // early leaves). kFifo = true: a FIFO ring (level by level: batches fill up
 // with the whole frontier of a level; leaves come last).
+#ifndef CSM_POW2_BATCH
+// 1: a batch takes a power of two of the expandable entries (every lane
+// busy); 0: all of them, up to 64 (fewer, fuller batches; lanes of a
+// non-power-of-two count partly idle).
+#define CSM_POW2_BATCH 0
+#endif
 #ifndef CSM_XFAST
 // Children and roots enter the stack x-fastest, so consecutive lanes of the
 // next batch score nodes adjacent in x: adjacent entries of a polyphase plane
@@ -1150,13 +1166,17 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
         }
         __syncthreads();
       }
+      // The cluster sizes some level scores with (SubmapDesc::cshift); an
+      // unused list is not written and aliases the next finer one.
+      uint32_t used_sl = 0;
+      for (int d = 0; d < sm.levels; ++d) used_sl |= 1u << sh.lv[d][6];
       if (tid < nrot) {
         const int r = tid;
         sh.list_off[r][0] = r * npad;
         int used = 0;
         int off[kLists] = {r * npad, -1, -1, -1};
         for (int sl = kMaxClusterShift; sl >= 1; --sl)
-          if (used + sh.list_len[r][sl] <= capc) {
+          if ((used_sl >> sl & 1u) && used + sh.list_len[r][sl] <= capc) {
             off[sl] = rc * npad + r * capc + used;
             used += sh.list_len[r][sl];
           }
@@ -1170,8 +1190,15 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
         }
       }
       __syncthreads();
-      for (int t = wave; t < nrot * kMaxClusterShift; t += kWaves) {
-        const int r = t / kMaxClusterShift, sl = 1 + t % kMaxClusterShift;
+      // Tasks (rotation, used list) dealt to the waves.
+      const int nused = __popc(used_sl & 0xeu);
+      for (int t = wave; t < nrot * nused; t += kWaves) {
+        const int r = t / nused;
+        int sl = 0;
+        for (int k = t % nused, m = used_sl & 0xe; k >= 0; --k) {
+          sl = __ffs(m) - 1;
+          m &= m - 1;
+        }
         if (!(sh.list_len[r][sl] & (1 << 30)))
           RunList<true>(cells + r * npad, n, ClusterMask(sl), cells + sh.list_off[r][sl],
                         cnts + (sh.list_off[r][sl] - raw_end));
@@ -1413,7 +1440,7 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
           const int ne = __popcll(em);
           int take = __popcll(inm);
           if (ne > 0) {
-            nodes = 1 << (31 - __clz(ne));
+            nodes = CSM_POW2_BATCH ? 1 << (31 - __clz(ne)) : ne;
             const int rank = __popcll(em & ((1ull << lane) - 1));
             // Entries up to the nodes-th expandable one are taken.
             take = static_cast<int>(__ffsll(static_cast<long long>(
