@@ -688,8 +688,6 @@ struct V4Shared {
   // batch loop reads LDS, not lane-divergent global loads: quad_w, quad_h,
   // quad_off, 4 * quad_pws, plane bytes, quad_bias, cshift.
   int lv[kMaxLevels][8];
-  unsigned long long lv_cands[kMaxLevels];
-  unsigned long long lv_batches[kMaxLevels];
 };
 
 // The DFS stack: entries [0, kStackLds) in LDS, [kStackLds, kStackLds + kSpill2)
@@ -1029,7 +1027,7 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
   long long kprof[4] = {0, 0, 0, 0};  // thread 0: setup, control, score cycles; lists (part of setup)
 #endif
   if (tid == 0) sh.queue = blockIdx.x % kNumXcd;
-  if (tid < kMaxLevels) { sh.lv_cands[tid] = 0; sh.lv_batches[tid] = 0; }
+  unsigned long long lv_cands = 0, lv_batches = 0;  // wave 0, lane l: child level l
   int tries = 0;
   __syncthreads();
   for (;;) {
@@ -1085,6 +1083,7 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
       sh.lv[d][6] = sm.cshift[d];
     }
     __syncthreads();
+    const double inv_res = 1.0 / sm.resolution;  // CellCoordFast
     bool range_error = false;
     for (int r = 0; r < nrot; ++r) {
       const float2 q = rot_table[pd.rot_offset + rot0 + r];
@@ -1096,8 +1095,8 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
         RotateZDev(q.x, q.y, x, y, &x, &y);
         const float px = __fadd_rn(pd.tx, x);
         const float py = __fadd_rn(pd.ty, y);
-        const double cx = CellCoord(sm.max_y, py, sm.resolution);
-        const double cy = CellCoord(sm.max_x, px, sm.resolution);
+        const double cx = CellCoordFast(sm.max_y, py, sm.resolution, inv_res);
+        const double cy = CellCoordFast(sm.max_x, px, sm.resolution, inv_res);
         int ix = 0, iy = 0;
         if (fabs(cx) > kIndexLimit || fabs(cy) > kIndexLimit) {
           range_error = true;
@@ -1459,6 +1458,19 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
             }
             blen = DppMax(len);
             bent = DppSum(len);
+            // Per child level: candidates scored and batches (lane l counts
+            // level l; one pass per distinct level, usually one).
+            const bool took = expandable && lane < take;
+            const int cl = static_cast<int>(ent.y >> 27) - (hexb ? 2 : 1);
+            for (unsigned long long tm = __ballot(took); tm;) {
+              const int l0 = __builtin_amdgcn_readlane(cl, static_cast<int>(__ffsll(static_cast<long long>(tm))) - 1);
+              const unsigned long long same = __ballot(took && cl == l0);
+              if (lane == l0) {
+                lv_cands += static_cast<unsigned long long>((hexb ? 16 : 4) * __popcll(same));
+                lv_batches += 1;
+              }
+              tm &= ~same;
+            }
           }
           if (from_ring) sp -= take; else ovf -= take;
           if (kHex && lane == 0) sh.batch_hex = hexb ? 1 : 0;
@@ -1495,11 +1507,6 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
         local_cands += kids * nodes;
         local_lookups += static_cast<unsigned long long>(kids) *
                          static_cast<unsigned>(Uniform(sh.batch_entries));
-        if (tid < nodes) {
-          const int cl = sh.node_level[tid] - (hexb ? 2 : 1);
-          atomicAdd(&sh.lv_cands[cl], static_cast<unsigned long long>(kids));
-          if (tid == 0) atomicAdd(&sh.lv_batches[cl], 1ull);
-        }
       }
       __syncthreads();
 #ifdef CSM_KPROF
@@ -1518,9 +1525,9 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
     for (int k = 0; k < 4; ++k) atomicAdd(&stats[2 + 2 * kMaxLevels + k], static_cast<unsigned long long>(kprof[k]));
 #endif
   }
-  if (stats && tid < kMaxLevels) {
-    atomicAdd(&stats[2 + tid], sh.lv_cands[tid]);
-    atomicAdd(&stats[2 + kMaxLevels + tid], sh.lv_batches[tid]);
+  if (stats && tid < kMaxLevels) {  // wave 0's lane l: level l
+    atomicAdd(&stats[2 + tid], lv_cands);
+    atomicAdd(&stats[2 + kMaxLevels + tid], lv_batches);
   }
   if (stats && tid == 0) atomicMax(&stats[kStatHighWater], static_cast<unsigned long long>(sh.high_water));
 }

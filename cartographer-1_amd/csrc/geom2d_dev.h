@@ -30,6 +30,20 @@ __device__ __forceinline__ double CellCoord(double max_v, float p, double res) {
       __dsub_rn(__ddiv_rn(__dsub_rn(max_v, static_cast<double>(p)), res), 0.5));
 }
 
+// CellCoord from the double reciprocal of the resolution: q' = (max - p) *
+// fl(1/res) is within 2^-52 relative (< 2.2e-10 absolute for |q'| < 2^20) of
+// the IEEE quotient q. Away from an integer by more than that, q and q' have
+// the same floor, fl(q) - 0.5 is exact and not a half-integer, and lround
+// gives floor(q); within 1e-9 of an integer, or for |q'| >= 2^20, the exact
+// CellCoord decides. Same result as CellCoord for every input.
+__device__ __forceinline__ double CellCoordFast(double max_v, float p, double res, double inv_res) {
+  const double d = __dsub_rn(max_v, static_cast<double>(p));
+  const double q = __dmul_rn(d, inv_res);
+  const double k = floor(q);
+  if (fabs(q) < 1048576.0 && q - k > 1e-9 && (k + 1.0) - q > 1e-9) return k;
+  return __builtin_round(__dsub_rn(__ddiv_rn(d, res), 0.5));
+}
+
 }  // namespace csm
 
 #endif  // CSM_GEOM2D_DEV_H_
