@@ -651,6 +651,12 @@ __global__ void pyramid_hex(const uint8_t* __restrict__ mlev, int mw, int mh, in
 // survivors sorted (best on top), wave 0 pops the next batch. Roots are
 // virtual nodes one level above the top lattice.
 
+#ifndef CSM_U_QUAD
+#define CSM_U_QUAD 8  // quad gathers in flight per lane (V4Score)
+#endif
+#ifndef CSM_U_HEX
+#define CSM_U_HEX 4   // hex gathers in flight per lane (V4ScoreHex)
+#endif
 constexpr int kMaxRotChunk = 16;
 constexpr int kLists = kMaxClusterShift + 1;
 
@@ -737,7 +743,7 @@ __device__ __forceinline__ void V4Score(Shared& sh, const uint32_t* cells, const
   const int quarter = (blen + kWaves - 1) / kWaves;
   const int s = Uniform(min(blen, wave * quarter)), e = Uniform(min(blen, wave * quarter + quarter));
   constexpr int kOOB = 0x7ffffff0;
-  constexpr int U = 8;
+  constexpr int U = CSM_U_QUAD;
   uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
   auto address = [&](uint32_t p, bool in) {
     const int X = static_cast<int16_t>(p & 0xffff) + cx;
@@ -833,7 +839,7 @@ __device__ __forceinline__ void V4ScoreHex(Shared& sh, const uint32_t* cells, co
   const int quarter = (blen + kWaves - 1) / kWaves;
   const int s = Uniform(min(blen, wave * quarter)), e = Uniform(min(blen, wave * quarter + quarter));
   constexpr int kOOB = 0x7ffffff0;
-  constexpr int U = 4;
+  constexpr int U = CSM_U_HEX;
   uint32_t acc[16];
 #pragma unroll
   for (int j = 0; j < 16; ++j) acc[j] = 0u;
