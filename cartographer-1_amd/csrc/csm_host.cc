@@ -745,6 +745,18 @@ int RunBatch(csm_context* ctx, csm_fast2d* const* submaps, int32_t num_submaps,
                    "fast2d phases (Mcycles, thread 0 sums): setup %.1f (entry lists %.1f) control "
                    "%.1f score %.1f\n",
                    kp[0] / 1e6, kp[3] / 1e6, kp[1] / 1e6, kp[2] / 1e6);
+    const unsigned long long* kl = stats_host + kStatLines;
+    bool any_lines = false;
+    for (int l = 0; l < kMaxLevels; ++l) any_lines |= kl[kMaxLevels + l] != 0;
+    if (std::getenv("CSM_PROFILE2D") && any_lines) {
+      std::fprintf(stderr, "fast2d lines per gather by child level:");
+      for (int l = 0; l < kMaxLevels; ++l)
+        if (kl[kMaxLevels + l])
+          std::fprintf(stderr, " L%d %.1f (%.3g instr)", l,
+                       static_cast<double>(kl[l]) / kl[kMaxLevels + l],
+                       static_cast<double>(kl[kMaxLevels + l]));
+      std::fprintf(stderr, "\n");
+    }
   }
 
   // ---- exactly tied maxima: the reference's pick (ResolveTies) ---------------

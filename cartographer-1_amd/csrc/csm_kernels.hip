@@ -694,6 +694,9 @@ struct V4Shared {
   // batch loop reads LDS, not lane-divergent global loads: quad_w, quad_h,
   // quad_off, 4 * quad_pws, plane bytes, quad_bias, cshift.
   int lv[kMaxLevels][8];
+#ifdef CSM_KPROF
+  unsigned long long kp_lines[kMaxLevels], kp_instr[kMaxLevels];
+#endif
 };
 
 // The DFS stack: entries [0, kStackLds) in LDS, [kStackLds, kStackLds + kSpill2)
@@ -707,6 +710,31 @@ template <typename Shared>
 __device__ __forceinline__ void StackPut(Shared& sh, uint2* spill, int i, uint2 v) {
   if (i < Shared::kStackLds) sh.stack[i] = v; else spill[i - Shared::kStackLds] = v;
 }
+
+#ifdef CSM_KPROF
+// Distinct 128-byte lines among the executing lanes' in-range addresses of
+// one gather (instrumentation only: 63 shuffles).
+template <typename Shared>
+__device__ void CountLines(Shared& sh, int level, int ad, int oob) {
+  const int lane = threadIdx.x & 63;
+  const bool valid = ad != oob;
+  const int line = valid ? (ad >> 7) : -1 - lane;
+  bool first = valid;
+  for (int j = 1; j < 64; ++j) {
+    const int o = __shfl(line, (lane + 64 - j) & 63, 64);
+    if (lane >= j && o == line) first = false;
+  }
+  const int n = __popcll(__ballot(first));
+  const int lv = __builtin_amdgcn_readfirstlane(level);
+  if (__builtin_amdgcn_readfirstlane(lane) == lane) {
+    atomicAdd(&sh.kp_lines[lv], static_cast<unsigned long long>(n));
+    atomicAdd(&sh.kp_instr[lv], 1ull);
+  }
+}
+#define CSM_COUNT_LINES(lvl, ad, oob) CountLines(sh, (lvl), (ad), (oob))
+#else
+#define CSM_COUNT_LINES(lvl, ad, oob)
+#endif
 
 // Scores the children of the batch's nodes: lane (node, group) walks entries
 // g, g + groups, ... of the node's list (cells, counts). A child's sum is
@@ -778,6 +806,7 @@ __device__ __forceinline__ void V4Score(Shared& sh, const uint32_t* cells, const
         ad[u] = address(P[j], in);
         c[u] = in ? (raw ? 1u : Cn[j]) : 0u;
       }
+      for (int u = 0; u < U; ++u) CSM_COUNT_LINES(level, ad[u], kOOB);
       uint32_t v[U];
   #pragma unroll
       for (int u = 0; u < U; ++u) v[u] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, ad[u], 0, 0);
@@ -875,6 +904,7 @@ __device__ __forceinline__ void V4ScoreHex(Shared& sh, const uint32_t* cells, co
         ad[u] = address(P[j], in);
         c[u] = in ? (raw ? 1u : Cn[j]) : 0u;
       }
+      for (int u = 0; u < U; ++u) CSM_COUNT_LINES(level, ad[u], kOOB);
       decltype(__builtin_amdgcn_raw_buffer_load_b128(rsrc, 0, 0, 0)) v[U];
   #pragma unroll
       for (int u = 0; u < U; ++u) v[u] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, ad[u], 0, 0);
@@ -1034,6 +1064,9 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
 #endif
   if (tid == 0) sh.queue = blockIdx.x % kNumXcd;
   unsigned long long lv_cands = 0, lv_batches = 0;  // wave 0, lane l: child level l
+#ifdef CSM_KPROF
+  if (tid < kMaxLevels) { sh.kp_lines[tid] = 0; sh.kp_instr[tid] = 0; }
+#endif
   int tries = 0;
   __syncthreads();
   for (;;) {
@@ -1536,6 +1569,12 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
     atomicAdd(&stats[2 + kMaxLevels + tid], lv_batches);
   }
   if (stats && tid == 0) atomicMax(&stats[kStatHighWater], static_cast<unsigned long long>(sh.high_water));
+#ifdef CSM_KPROF
+  if (stats && tid < kMaxLevels) {
+    atomicAdd(&stats[kStatLines + tid], sh.kp_lines[tid]);
+    atomicAdd(&stats[kStatLines + kMaxLevels + tid], sh.kp_instr[tid]);
+  }
+#endif
 }
 
 // Tie resolution (csm_host.cc ResolveTies): exact level-d sums of listed

@@ -40,6 +40,18 @@ def lines_current(ex, ey, nx_, ny_, P, es, W):
     return addr >> 7  # [node, entry]
 
 
+def lines_polytile(ex, ey, nx_, ny_, P, es, W, tx, ty):
+    # polyphase period P as lines_current, each plane tiled tx x ty entries per line
+    pw = W // P + 2
+    X = ex[None, :] + nx_[:, None] + 3 * P
+    Y = ey[None, :] + ny_[:, None] + 3 * P
+    plane = (Y % P) * P + (X % P)
+    u, v = X // P, Y // P
+    tpr = pw // tx + 2
+    addr = plane * (tpr * tpr * 128 * 4) + ((v // ty) * tpr + u // tx) * 128 + ((v % ty) * tx + u % tx) * es
+    return addr >> 7
+
+
 def lines_residue(ex, ey, nx_, ny_, k, es, tx, ty, W):
     X = ex[None, :] + nx_[:, None] + 3 * 64
     Y = ey[None, :] + ny_[:, None] + 3 * 64
@@ -152,8 +164,11 @@ def main_survivors():
                 ex, ey = ent[c][0], ent[c][1]
                 P = (4 << (L - 2)) if hexp else (2 << (L - 1))
                 es = 16 if hexp else 4
+                tiles = (4, 2) if hexp else (8, 4)
                 for key, lines, G in [
                         ("current", lines_current(ex, ey, nx_, ny_, P, es, W), 64),
+                        ("current lanes, polyphase planes tiled 4x2 / 8x4",
+                         lines_polytile(ex, ey, nx_, ny_, P, es, W, *tiles), 64),
                         ("residue 4x2/8x4 tiles, 8 nodes x 8 entries",
                          lines_residue(ex, ey, nx_, ny_, k, es, *((4, 2) if hexp else (8, 4)), W), 8),
                         ("residue 4x2/8x4 tiles, 4 nodes x 16 entries",
