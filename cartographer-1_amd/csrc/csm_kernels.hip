@@ -1015,6 +1015,9 @@ __device__ __forceinline__ uint32_t ClusterMask(int sl) {
 // non-power-of-two count partly idle).
 #define CSM_POW2_BATCH 0
 #endif
+#ifndef CSM_LIFO_LEVEL
+#define CSM_LIFO_LEVEL 2  // FIFO order: levels pushed depth-first (0: none; profiles/r3an)
+#endif
 #ifndef CSM_XFAST
 // Children and roots enter the stack x-fastest, so consecutive lanes of the
 // next batch score nodes adjacent in x: adjacent entries of a polyphase plane
@@ -1359,7 +1362,12 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
           // there). Rank = survivors of deeper levels + same-level survivors
           // in lower lanes; one ballot per distinct level (usually one).
           const bool push = keep && clvl > 0;
-          const unsigned long long pm = __ballot(push);
+          // FIFO: nodes at levels <= CSM_LIFO_LEVEL go to the overflow stack,
+          // popped first and deepest first, so an item reaches its leaves
+          // (and an incumbent) early while the upper levels keep full
+          // level-by-level batches.
+          const bool deep = kFifo && push && clvl <= CSM_LIFO_LEVEL;
+          const unsigned long long pm = __ballot(push && !deep);
           const int kept = __popcll(pm);
           int rank = 0;
           if (kFifo) rank = __popcll(pm & ((1ull << lane) - 1));
@@ -1385,8 +1393,8 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
             // empty); past that the pair is flagged.
             constexpr int kRing = decltype(sh)::kStackLds;
             const int slot = sp + rank;
-            if (push && slot < kRing) sh.stack[(sh.head + slot) & (kRing - 1)] = entry;
-            const bool over = push && slot >= kRing;
+            if (push && !deep && slot < kRing) sh.stack[(sh.head + slot) & (kRing - 1)] = entry;
+            const bool over = (push && !deep && slot >= kRing) || deep;
             const unsigned long long om = __ballot(over);
             if (om) {
               int ob = 0;
