@@ -1015,6 +1015,9 @@ __device__ __forceinline__ uint32_t ClusterMask(int sl) {
 // non-power-of-two count partly idle).
 #define CSM_POW2_BATCH 0
 #endif
+#ifndef CSM_BEST_REFRESH
+#define CSM_BEST_REFRESH 1  // batches between reads of the pair's global best (power of 2; profiles/r3ap)
+#endif
 #ifndef CSM_LIFO_LEVEL
 #define CSM_LIFO_LEVEL 2  // FIFO order: levels pushed depth-first (0: none; profiles/r3an)
 #endif
@@ -1445,7 +1448,7 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
           if (lane == 0) sh.vnext = v0 + vc;
         }
         // (c) Pop the next batch: up to 64 nodes, best first.
-        if (lane == 0 && (sh.batch_no++ & 7) == 0) {
+        if (lane == 0 && (sh.batch_no++ & (CSM_BEST_REFRESH - 1)) == 0) {
           const uint64_t fresh = LoadBest(pair_best);
           if (fresh > sh.best) sh.best = fresh;
         }
