@@ -35,7 +35,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 # Version tag of the search kernel the committed PMC traffic figures belong to
 # (a traffic file recorded on another kernel version is not reported).
-KERNEL_TAG = "v5-full-batch"
+KERNEL_TAG = "v5-hybrid-refresh"
 
 
 def load_pkg():
@@ -284,8 +284,8 @@ def roofline_fields(tm, achieved, peak, traffic, kernel_ms_avg, bytes_per_launch
             "candidate_equivalent_bytes_per_launch": candidate_bytes}
 
 
-TRAFFIC_FILES = {"c2": os.path.join("profiles", "r3ae", "traffic_c2.json"),
-                 "c3": os.path.join("profiles", "r3ae", "traffic_c3.json")}
+TRAFFIC_FILES = {"c2": os.path.join("profiles", "r3ar", "traffic_c2.json"),
+                 "c3": os.path.join("profiles", "r3ar", "traffic_c3.json")}
 
 
 def traffic_fields(traffic, kernel_ms_avg, peak):
