@@ -7,6 +7,9 @@
 //       to rank 0, which checks the slot order and contents. Exit 0 = pass.
 //   distributed_builder_test gather3d <world> <port>
 //       The same with the 3D records (ConstraintRecord3D).
+//   distributed_builder_test claimloop <world> <port>
+//       CPU only: Sharding::kClaim's chunking and claim loop over TCP
+//       (ClaimChunks, ForClaimedChunks): every chunk claimed once.
 //   distributed_builder_test diverge <world> <port>
 //       CPU only: rank 1 submits one pair more than the others; WhenDone's
 //       submission check must abort every rank (exit 0 = they all aborted).
@@ -27,8 +30,10 @@
 #include <sys/wait.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cmath>
 #include <csignal>
+#include <set>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -156,6 +161,95 @@ static int Gather3DMain(int world, int port) {
     return 1;
   }
   std::printf("gather3d OK\n");
+  return 0;
+}
+
+// Sharding::kClaim's queue logic without a device: <world> forked ranks run
+// ForClaimedChunks over three flushes of a synthetic pending list (ClaimChunks
+// groups it by submap, 2 submaps per chunk) and gather the (flush, chunk)
+// pairs they claimed; rank 0 checks that every chunk of every flush was
+// claimed exactly once and that each chunk holds exactly its submaps' pairs.
+struct FakePending {
+  SubmapId submap_id;
+  int index;
+};
+
+static std::vector<FakePending> FakeFlush(int flush) {
+  std::vector<FakePending> p;
+  for (int k = 0; k < 17 + 5 * flush; ++k)
+    p.push_back(FakePending{SubmapId{k % 3, (k * 7 + flush) % (4 + flush)}, k});
+  return p;
+}
+
+static int ClaimLoopMain(int world, int port) {
+  auto body = [&](int rank) -> int {
+    csm_comm* comm = nullptr;
+    if (csm_comm_create_tcp(rank, world, "127.0.0.1", port, &comm) != CSM_OK) return 2;
+    if (csm_comm_claim_open(comm, "127.0.0.1", port + 1) != CSM_OK) return 2;
+    std::vector<ConstraintRecord> mine;
+    for (int flush = 0; flush < 3; ++flush) {
+      const auto pending = FakeFlush(flush);
+      const auto chunks = ClaimChunks(pending, 2);
+      ForClaimedChunks(comm, (int64_t{7} << 40) + flush, chunks.size(), [&](size_t c) {
+        for (size_t i : chunks[c]) {
+          ConstraintRecord r{};
+          r.slot = flush * 1000 + pending[i].index;
+          r.submap_trajectory = flush;
+          r.submap_index = static_cast<int32_t>(c);
+          r.node_index = rank;
+          mine.push_back(r);
+        }
+        usleep(1000 * (c % 3));  // uneven chunk costs
+      });
+    }
+    std::sort(mine.begin(), mine.end(),
+              [](const ConstraintRecord& a, const ConstraintRecord& b) { return a.slot < b.slot; });
+    const auto all = GatherConstraintRecords(comm, mine);
+    csm_comm_destroy(comm);
+    if (rank != 0) return all.empty() ? 0 : 3;
+    int bad = 0;
+    size_t expect = 0;
+    for (int flush = 0; flush < 3; ++flush) {
+      const auto pending = FakeFlush(flush);
+      const auto chunks = ClaimChunks(pending, 2);
+      expect += pending.size();
+      std::vector<int> chunk_of(pending.size(), -1);
+      for (size_t c = 0; c < chunks.size(); ++c) {
+        std::set<SubmapId> subs;
+        for (size_t i : chunks[c]) {
+          chunk_of[i] = static_cast<int>(c);
+          subs.insert(pending[i].submap_id);
+        }
+        if (subs.size() > 2) ++bad;  // at most chunk_submaps submaps per chunk
+      }
+      for (int c : chunk_of) bad += c < 0;  // every pair in some chunk
+      for (const ConstraintRecord& r : all)
+        if (r.submap_trajectory == flush && chunk_of[r.slot - flush * 1000] != r.submap_index) ++bad;
+    }
+    if (all.size() != expect) ++bad;  // each pair exactly once
+    for (size_t i = 1; i < all.size(); ++i) bad += all[i - 1].slot >= all[i].slot;
+    std::set<int> ranks;
+    for (const ConstraintRecord& r : all) ranks.insert(r.node_index);
+    std::printf("claimloop: %zu pairs over %zu ranks\n", all.size(), ranks.size());
+    return bad ? 1 : 0;
+  };
+  std::vector<pid_t> kids;
+  for (int rank = 1; rank < world; ++rank) {
+    const pid_t p = fork();
+    if (p == 0) _exit(body(rank));
+    kids.push_back(p);
+  }
+  int rc = body(0);
+  for (pid_t p : kids) {
+    int st = 0;
+    waitpid(p, &st, 0);
+    if (!WIFEXITED(st) || WEXITSTATUS(st) != 0) rc = rc ? rc : 4;
+  }
+  if (rc) {
+    std::fprintf(stderr, "claimloop failed (%d)\n", rc);
+    return 1;
+  }
+  std::printf("claimloop OK\n");
   return 0;
 }
 
@@ -438,6 +532,8 @@ int main(int argc, char** argv) {
   if (argc == 4 && std::string(argv[1]) == "gather") return GatherMain(std::atoi(argv[2]), std::atoi(argv[3]));
   if (argc == 4 && std::string(argv[1]) == "gather3d")
     return Gather3DMain(std::atoi(argv[2]), std::atoi(argv[3]));
+  if (argc == 4 && std::string(argv[1]) == "claimloop")
+    return ClaimLoopMain(std::atoi(argv[2]), std::atoi(argv[3]));
   if (argc == 4 && std::string(argv[1]) == "diverge")
     return DivergeMain(std::atoi(argv[2]), std::atoi(argv[3]));
   if (argc == 5) {
@@ -448,7 +544,7 @@ int main(int argc, char** argv) {
       return Builder3DMain(rank, world, port, m != "builder3d");
   }
   std::fprintf(stderr,
-               "usage: %s gather|gather3d|diverge <world> <port> | "
+               "usage: %s gather|gather3d|claimloop|diverge <world> <port> | "
                "builder|builder3d|builder-claim|builder3d-claim <rank> <world> <port>\n",
                argv[0]);
   return 2;

@@ -191,6 +191,20 @@ def test_cpp_record_gather_3d_tcp(csm, world):
     assert "gather3d OK" in out.stdout
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_cpp_claim_loop_tcp(csm, world):
+    """Sharding::kClaim's queue without a device: <world> forked ranks claim
+    the chunks of three flushes (ClaimChunks groups pending pairs by submap)
+    through csm_comm_fetch_add; rank 0 receives every pair exactly once, in
+    submission order, each from the chunk that holds its submap."""
+    import subprocess
+    _build_dist()
+    out = subprocess.run([DIST_BIN, "claimloop", str(world), str(_free_port())],
+                         capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    assert "claimloop OK" in out.stdout
+
+
 def test_cpp_diverging_submissions_abort(csm):
     """A rank that submits a different pair sequence makes WhenDone abort on
     every rank (CheckSameSubmissions), instead of rank 0 mixing constraints."""
