@@ -71,7 +71,9 @@ def parse():
     p.add_argument("--c3-nodes", type=int, default=2000)
     p.add_argument("--c3-submaps", type=int, default=1000)
     p.add_argument("--c3-slice", type=int, default=50, help="submaps of the queue per step")
-    p.add_argument("--c3-chunk", type=int, default=4, help="submaps per claimed chunk")
+    p.add_argument("--c3-chunk", type=int, default=0,
+                   help="submaps per claimed chunk (0: 4 on one GPU, 2 on several, so the "
+                        "ranks' last claims end closer together)")
     p.add_argument("--cpu-pairs", type=int, default=0,
                    help="CPU baseline sample size (0: 2000 for C3, sized to --cpu-seconds for C2)")
     return p.parse_args()
@@ -907,7 +909,8 @@ def c3_run(csm, ctx, args, rank, world_size, dist, coll_dev, comm, gather, trans
     go to rank 0 in submission order (constraint_builder_2d.cc:279-300) over
     RCCL. Warmup steps run one chunk each, untimed."""
     cdist = importlib.import_module("cartographer_amd.distributed")
-    N, S, K = args.c3_nodes, args.c3_submaps, args.c3_chunk
+    N, S = args.c3_nodes, args.c3_submaps
+    K = args.c3_chunk = args.c3_chunk or (4 if world_size == 1 else 2)
     t0 = time.time()
     world = csm.SyntheticWorld2D(num_nodes=N, num_submaps=S, submap_cells=400, beams=1080,
                                  seed=args.seed)
