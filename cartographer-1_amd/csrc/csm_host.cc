@@ -611,7 +611,9 @@ int RunBatch(csm_context* ctx, csm_fast2d* const* submaps, int32_t num_submaps,
   };
   std::vector<SubmapDesc> sdesc(num_submaps);
   for (int i = 0; i < num_submaps; ++i) {
-    if (!submaps[i] || submaps[i]->ctx != ctx) return CSM_EINVAL;
+    // Any context on this device: a second context may build the next
+    // batch's pyramids on its own stream while this one searches.
+    if (!submaps[i] || submaps[i]->ctx->device != ctx->device) return CSM_EINVAL;
     sdesc[i] = submaps[i]->desc;
     // One launch serves one kernel: v4 (no hex levels) or v5 (fixed at create).
     if ((sdesc[i].hex_mask != 0) != (sdesc[0].hex_mask != 0)) return CSM_EINVAL;

@@ -175,6 +175,9 @@ typedef struct csm_result2d {
   csm_pose2d pose;
 } csm_result2d;
 
+/* The submap handles may come from any context on ctx's device (e.g. one
+ * whose stream builds the next batch's pyramids while ctx searches); the
+ * scan set is ctx's. */
 int csm_fast2d_match_batch(csm_context* ctx, csm_fast2d* const* submaps,
                            int32_t num_submaps, const csm_scan_set* scans,
                            const csm_pair2d* pairs, int64_t num_pairs,
