@@ -539,11 +539,14 @@ int ResolveTies(csm_context* ctx, csm_fast2d* const* submaps, csm_scan_set* scan
       const PairDesc& d = pdesc[w.k];
       const csm_fast2d* m = submaps[d.submap];
       const int64_t n = c.rot_first.back();
-      std::vector<std::pair<float, int64_t>> lst(n);
+      // 8-byte elements (the comparisons, and so the permutation, are the
+      // same whatever the element carries).
+      std::vector<std::pair<float, int32_t>> lst(n);
       for (int64_t i = 0; i < n; ++i)
-        lst[i] = {SumToScore(ts[base[pi] + i], d.num_points, m->min_s, m->max_s), i};
+        lst[i] = {SumToScore(ts[base[pi] + i], d.num_points, m->min_s, m->max_s),
+                  static_cast<int32_t>(i)};
       std::sort(lst.begin(), lst.end(),
-                [](const std::pair<float, int64_t>& a, const std::pair<float, int64_t>& b) {
+                [](const std::pair<float, int32_t>& a, const std::pair<float, int32_t>& b) {
                   return a.first > b.first;
                 });
       c.pos.resize(n);
@@ -728,9 +731,11 @@ int RunBatch(csm_context* ctx, csm_fast2d* const* submaps, int32_t num_submaps,
   if ((rcode = LaunchSearch(ctx, scans, pdesc, nullptr, plan, ctx->timing, &keys, &keys_hi, &stat,
                             stats_host)))
     return rcode;
+  float kernel_ms = 0.f;
   if (ctx->timing) {
     float ms = 0.f;
     CSM_HIP(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+    kernel_ms = ms;
     ctx->t.search_kernel_ms += ms;
     ctx->t.search_launches += 1;
     ctx->t.search_candidates += static_cast<double>(stats_host[0]);
@@ -814,10 +819,10 @@ int RunBatch(csm_context* ctx, csm_fast2d* const* submaps, int32_t num_submaps,
   }
   if (prof)
     std::fprintf(stderr,
-                 "fast2d batch host (ms): prep %.2f, search + readback %.2f, ties %.2f (%lld pairs), "
-                 "decode %.2f; %d pairs\n",
-                 prep_ms, search_ms, ties_ms, static_cast<long long>(ctx->t.tied_pairs - tied_before),
-                 ms_since(t_decode), np);
+                 "fast2d batch host (ms): prep %.2f, search + readback %.2f (kernel %.2f), ties %.2f "
+                 "(%lld pairs), decode %.2f; %d pairs\n",
+                 prep_ms, search_ms, kernel_ms, ties_ms,
+                 static_cast<long long>(ctx->t.tied_pairs - tied_before), ms_since(t_decode), np);
   return CSM_OK;
 }
 
