@@ -345,6 +345,12 @@ int ResolveTies(csm_context* ctx, csm_fast2d* const* submaps, csm_scan_set* scan
   }
   if (tied.empty()) return CSM_OK;
   ctx->t.tied_pairs += static_cast<int64_t>(tied.size());
+  const bool prof = std::getenv("CSM_PROFILE2D") != nullptr;
+  auto now = [] { return std::chrono::steady_clock::now(); };
+  auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+    return std::chrono::duration<double, std::milli>(b - a).count();
+  };
+  const auto tp0 = now();
   // (1) Every leaf at the maximum.
   std::vector<PairDesc> pd2;
   std::vector<uint64_t> init;
@@ -439,6 +445,7 @@ int ResolveTies(csm_context* ctx, csm_fast2d* const* submaps, csm_scan_set* scan
     CSM_HIP(hipStreamSynchronize(st));
     return CSM_OK;
   };
+  const auto tp1 = now();
   // The jobs index pd2 (ctx->pair_desc holds it after the second search).
   std::vector<int32_t> sums;
   if ((rc = score(jobs, queries, &sums))) return rc;
@@ -482,6 +489,8 @@ int ResolveTies(csm_context* ctx, csm_fast2d* const* submaps, csm_scan_set* scan
     }
     c.need_perm = nodes.size() > 1;
   }
+  const auto tp2 = now();
+  auto tp3 = tp2, tp4 = tp2;
   // (3) The whole lowest-resolution list of every pair that needs the
   // top-level permutation: bounds of all its rotations on the device, every
   // lattice node scored in one launch, each list sorted on its own thread.
@@ -528,8 +537,10 @@ int ResolveTies(csm_context* ctx, csm_fast2d* const* submaps, csm_scan_set* scan
         if (job.count) tj.push_back(job);
       }
     }
+    tp3 = now();
     std::vector<int32_t> ts;
     if ((rc = score(tj, tq, &ts))) return rc;
+    tp4 = now();
     // ScoreCandidates: score = ToScore(sum / n), then
     // std::sort(greater<Candidate2D>) — the same algorithm and the same
     // comparisons give the same permutation for any element type.
@@ -565,6 +576,7 @@ int ResolveTies(csm_context* ctx, csm_fast2d* const* submaps, csm_scan_set* scan
       for (auto& th : pool) th.join();
     }
   }
+  const auto tp5 = now();
   for (size_t wi = 0; wi < work.size(); ++wi) {
     const Tie& w = work[wi];
     const Cand& c = cand[wi];
@@ -600,6 +612,12 @@ int ResolveTies(csm_context* ctx, csm_fast2d* const* submaps, csm_scan_set* scan
     (*keys)[w.k] = PackLeafKey(static_cast<uint32_t>(d2.collect_sum), leaves[best].x,
                                leaves[best].y, leaves[best].z);
   }
+  if (prof)
+    std::fprintf(stderr,
+                 "ties (ms): collect search %.2f, ancestors %.2f, bounds + lattice %.2f, "
+                 "lattice scores %.2f, sorts %.2f, picks %.2f; %zu tied, %zu need the order\n",
+                 ms(tp0, tp1), ms(tp1, tp2), ms(tp2, tp3), ms(tp3, tp4), ms(tp4, tp5),
+                 ms(tp5, now()), tied.size(), perm.size());
   return CSM_OK;
 }
 

@@ -1604,6 +1604,7 @@ fast2d_score_queries(const SubmapDesc* __restrict__ submaps, const PairDesc* __r
   const PairDesc pd = pairs[job.pair];
   const SubmapDesc& sm = submaps[pd.submap];
   const float2 q = rot_table[pd.rot_offset + job.rot];
+  const double inv_res = 1.0 / sm.resolution;  // CellCoordFast
   for (int i = threadIdx.x; i < npad; i += blockDim.x) {
     uint32_t c = 0x80008000u;  // (-32768, -32768): outside every level
     if (i < pd.num_points) {
@@ -1613,8 +1614,8 @@ fast2d_score_queries(const SubmapDesc* __restrict__ submaps, const PairDesc* __r
       RotateZDev(q.x, q.y, x, y, &x, &y);
       const float px = __fadd_rn(pd.tx, x);
       const float py = __fadd_rn(pd.ty, y);
-      const double cx = CellCoord(sm.max_y, py, sm.resolution);
-      const double cy = CellCoord(sm.max_x, px, sm.resolution);
+      const double cx = CellCoordFast(sm.max_y, py, sm.resolution, inv_res);
+      const double cy = CellCoordFast(sm.max_x, px, sm.resolution, inv_res);
       if (fabs(cx) <= kIndexLimit && fabs(cy) <= kIndexLimit)
         c = (static_cast<uint32_t>(static_cast<int>(cx)) & 0xffff) |
             (static_cast<uint32_t>(static_cast<int>(cy)) << 16);
@@ -1646,6 +1647,7 @@ fast2d_rotation_bounds(const SubmapDesc* __restrict__ submaps, const PairDesc* _
   }
   __syncthreads();
   int mnx = 0x7fffffff, mxx = -0x7fffffff, mny = 0x7fffffff, mxy = -0x7fffffff;
+  const double inv_res = 1.0 / sm.resolution;  // CellCoordFast
   for (int i = threadIdx.x; i < pd.num_points; i += blockDim.x) {
     const float* p = points + 3 * (pd.point_offset + i);
     float x, y;
@@ -1653,8 +1655,8 @@ fast2d_rotation_bounds(const SubmapDesc* __restrict__ submaps, const PairDesc* _
     RotateZDev(q.x, q.y, x, y, &x, &y);
     const float px = __fadd_rn(pd.tx, x);
     const float py = __fadd_rn(pd.ty, y);
-    const double cx = CellCoord(sm.max_y, py, sm.resolution);
-    const double cy = CellCoord(sm.max_x, px, sm.resolution);
+    const double cx = CellCoordFast(sm.max_y, py, sm.resolution, inv_res);
+    const double cy = CellCoordFast(sm.max_x, px, sm.resolution, inv_res);
     const int ix = fabs(cx) > kIndexLimit ? 0 : static_cast<int>(cx);
     const int iy = fabs(cy) > kIndexLimit ? 0 : static_cast<int>(cy);
     mnx = min(mnx, ix); mxx = max(mxx, ix);
