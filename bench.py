@@ -28,6 +28,7 @@ import json
 import math
 import os
 import sys
+import threading
 import time
 
 import numpy as np
@@ -74,6 +75,9 @@ def parse():
     p.add_argument("--c3-chunk", type=int, default=0,
                    help="submaps per claimed chunk (0: 4 on one GPU, 2 on several, so the "
                         "ranks' last claims end closer together)")
+    p.add_argument("--c3-workers", type=int, default=1,
+                   help="host threads per rank, each with its own context (stream): a chunk's "
+                        "host work (tie resolution, records) overlaps the next chunk's search")
     p.add_argument("--cpu-pairs", type=int, default=0,
                    help="CPU baseline sample size (0: 2000 for C3, sized to --cpu-seconds for C2)")
     return p.parse_args()
@@ -299,6 +303,15 @@ def traffic_fields(traffic, kernel_ms_avg, peak):
     gbps = traffic["traffic_bytes_per_launch"] / (kernel_ms_avg * 1e-3) / 1e9
     return {"traffic": traffic["traffic_bytes_per_launch"], "traffic_source": traffic["source"],
             "traffic_GBps": gbps, "traffic_frac": gbps / peak}
+
+
+def sum_timing(csm, tms):
+    """Adds the timing records of several contexts (the high-water mark: max)."""
+    out = csm.Timing()
+    for name, _ in csm.Timing._fields_:
+        vals = [getattr(t, name) for t in tms]
+        setattr(out, name, max(vals) if name == "stack_high_water" else sum(vals))
+    return out
 
 
 def committed_traffic(args, world_size, workload="c2"):
@@ -916,7 +929,9 @@ def c3_run(csm, ctx, args, rank, world_size, dist, coll_dev, comm, gather, trans
                                  seed=args.seed)
     gen_s = time.time() - t0
     opts = csm.FastCorrelativeScanMatcherOptions2D(7.0, math.radians(30.0), 7, args.search_depth)
-    scans = csm.ScanSet(None, ctx, packed=(world.points, world.offsets))
+    # One context (stream + scratch) and scan set per host worker.
+    ctxs = [ctx] + [csm.Context(ctx.device) for _ in range(max(args.c3_workers, 1) - 1)]
+    scan_sets = [csm.ScanSet(None, c, packed=(world.points, world.offsets)) for c in ctxs]
     slice_ = args.c3_slice
     # The timed queue: steps x slice submaps, in queue order (wrapping after S).
     queue = (np.arange(args.steps * slice_) % S).astype(np.int64)
@@ -926,7 +941,8 @@ def c3_run(csm, ctx, args, rank, world_size, dist, coll_dev, comm, gather, trans
     phase = {"pyramids": 0.0, "search": 0.0, "close": 0.0, "records": 0.0}
     profile = bool(os.environ.get("C3_PROFILE"))
 
-    def run_chunk(subs, base):
+    def run_chunk(subs, base, w=0):
+        ctx, scans = ctxs[w], scan_sets[w]
         t0 = time.perf_counter()
         mats = [csm.FastCorrelativeScanMatcher2D(world.grid(int(s)), opts, ctx) for s in subs]
         sub_local = np.repeat(np.arange(len(subs), dtype=np.int32), N)
@@ -948,40 +964,61 @@ def c3_run(csm, ctx, args, rank, world_size, dist, coll_dev, comm, gather, trans
             phase["records"] += time.perf_counter() - t3
         return res, rec
 
+    claim_lock = threading.Lock()  # one claim in flight per rank (the comm's socket)
+
     def claim(key):
-        if comm is None:
-            claim.local[key] = claim.local.get(key, 0) + 1
-            return claim.local[key] - 1
-        return comm.fetch_add(key, 1)
+        with claim_lock:
+            if comm is None:
+                claim.local[key] = claim.local.get(key, 0) + 1
+                return claim.local[key] - 1
+            return comm.fetch_add(key, 1)
     claim.local = {}
 
     for w in range(args.warmup):  # one chunk each: module load, staging buffers
-        run_chunk(chunks[(rank + w) % n_chunks], 0)
-    ctx.reset_timing()
-    ctx.enable_timing(True)
+        for i in range(len(ctxs)):
+            run_chunk(chunks[(rank + w) % n_chunks], 0, i)
+    for c in ctxs:
+        c.reset_timing()
+        c.enable_timing(True)
     barrier_sync()
     t_start = time.perf_counter()
-    errors, mine, recs = 0, 0, []
-    while True:
-        c = claim(1)  # key 1: the timed queue's head
-        if c >= n_chunks:
-            break
-        res, rec = run_chunk(chunks[c], np.int64(c) * K * N)
-        errors += int((res["status"] < 0).sum())
-        recs.append(rec)
-        mine += 1
-        if rank == 0 and (c % 10 == 0 or world_size == 1):
-            print(f"c3: chunk {c + 1}/{n_chunks} {time.perf_counter() - t_start:.1f} s",
-                  file=sys.stderr, flush=True)
+    done = {"errors": 0, "mine": 0, "recs": []}
+
+    def worker(w):
+        while True:
+            c = claim(1)  # key 1: the timed queue's head
+            if c >= n_chunks:
+                return
+            res, rec = run_chunk(chunks[c], np.int64(c) * K * N, w)
+            with claim_lock:
+                done["errors"] += int((res["status"] < 0).sum())
+                done["recs"].append(rec)
+                done["mine"] += 1
+            if rank == 0 and (c % 10 == 0 or world_size == 1):
+                print(f"c3: chunk {c + 1}/{n_chunks} {time.perf_counter() - t_start:.1f} s",
+                      file=sys.stderr, flush=True)
+
+    if len(ctxs) == 1:
+        worker(0)
+    else:
+        threads = [threading.Thread(target=worker, args=(w,)) for w in range(len(ctxs))]
+        for t in threads:
+            t.start()
+        for t in threads:
+            t.join()
+    errors, mine, recs = done["errors"], done["mine"], done["recs"]
+    tms = [c.timing() for c in ctxs]
     if profile:
         print("c3 host phases (s): " + ", ".join(f"{k} {v:.2f}" for k, v in phase.items())
-              + f"; kernel {ctx.timing().search_kernel_ms * 1e-3:.2f}", file=sys.stderr, flush=True)
+              + f"; kernel {sum(t.search_kernel_ms for t in tms) * 1e-3:.2f}",
+              file=sys.stderr, flush=True)
     allrec = gather(np.concatenate(recs) if recs else np.zeros((0, cdist.RECORD_WIDTH)))
     barrier_sync()
     elapsed = time.perf_counter() - t_start
-    ctx.enable_timing(False)
-    tm = ctx.timing()
-    lv_cands, lv_batches = ctx.level_stats()
+    for c in ctxs:
+        c.enable_timing(False)
+    tm = sum_timing(csm, [c.timing() for c in ctxs])
+    lv_cands, lv_batches = (list(map(sum, zip(*v))) for v in zip(*[c.level_stats() for c in ctxs]))
     accepted = len(allrec) if rank == 0 else 0
     elapsed = cdist.max_over_ranks(elapsed, dist, coll_dev)
     errors = int(cdist.sum_over_ranks(errors, dist, coll_dev))
@@ -1034,7 +1071,10 @@ def c3_run(csm, ctx, args, rank, world_size, dist, coll_dev, comm, gather, trans
         out["cpu_baseline"] = cpu_pairs_2d(world, ps, pn, args_c,
                                            "uniformly sampled (submap, node) pairs of the C3 queue")
         out["speedup_vs_cpu"] = out["value"] / out["cpu_baseline"]["value"]
-    scans.close()
+    for sc, c in zip(scan_sets, ctxs):
+        sc.close()
+        if c is not ctx:
+            c.close()
     return out, errors
 
 

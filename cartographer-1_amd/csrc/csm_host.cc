@@ -30,6 +30,7 @@
 #include "csm_device.h"
 #include "csm_internal.h"
 #include "csm_launch.h"
+#include "parallel_sort.h"
 #include "search_window.h"
 
 namespace csm {
@@ -543,7 +544,11 @@ int ResolveTies(csm_context* ctx, csm_fast2d* const* submaps, csm_scan_set* scan
     tp4 = now();
     // ScoreCandidates: score = ToScore(sum / n), then
     // std::sort(greater<Candidate2D>) — the same algorithm and the same
-    // comparisons give the same permutation for any element type.
+    // comparisons give the same permutation for any element type; IntroSort
+    // (parallel_sort.h) is that algorithm with independent partitions on
+    // threads. Up to 8 lists at once, 8 threads between them.
+    const size_t nthreads = std::min<size_t>(perm.size(), 8);
+    const int sort_threads = static_cast<int>(8 / std::max<size_t>(nthreads, 1));
     auto sort_one = [&](size_t pi) {
       const Tie& w = work[perm[pi]];
       Cand& c = cand[perm[pi]];
@@ -556,14 +561,14 @@ int ResolveTies(csm_context* ctx, csm_fast2d* const* submaps, csm_scan_set* scan
       for (int64_t i = 0; i < n; ++i)
         lst[i] = {SumToScore(ts[base[pi] + i], d.num_points, m->min_s, m->max_s),
                   static_cast<int32_t>(i)};
-      std::sort(lst.begin(), lst.end(),
+      IntroSort(lst.data(), lst.data() + n,
                 [](const std::pair<float, int32_t>& a, const std::pair<float, int32_t>& b) {
                   return a.first > b.first;
-                });
+                },
+                sort_threads);
       c.pos.resize(n);
       for (int64_t i = 0; i < n; ++i) c.pos[lst[i].second] = i;
     };
-    const size_t nthreads = std::min<size_t>(perm.size(), 8);
     if (nthreads <= 1) {
       for (size_t pi = 0; pi < perm.size(); ++pi) sort_one(pi);
     } else {
