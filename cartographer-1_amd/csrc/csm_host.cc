@@ -558,16 +558,20 @@ int ResolveTies(csm_context* ctx, csm_fast2d* const* submaps, csm_scan_set* scan
       // 8-byte elements (the comparisons, and so the permutation, are the
       // same whatever the element carries).
       std::vector<std::pair<float, int32_t>> lst(n);
-      for (int64_t i = 0; i < n; ++i)
-        lst[i] = {SumToScore(ts[base[pi] + i], d.num_points, m->min_s, m->max_s),
-                  static_cast<int32_t>(i)};
+      ParallelRanges(n, sort_threads, [&](std::ptrdiff_t lo, std::ptrdiff_t hi) {
+        for (std::ptrdiff_t i = lo; i < hi; ++i)
+          lst[i] = {SumToScore(ts[base[pi] + i], d.num_points, m->min_s, m->max_s),
+                    static_cast<int32_t>(i)};
+      });
       IntroSort(lst.data(), lst.data() + n,
                 [](const std::pair<float, int32_t>& a, const std::pair<float, int32_t>& b) {
                   return a.first > b.first;
                 },
                 sort_threads);
       c.pos.resize(n);
-      for (int64_t i = 0; i < n; ++i) c.pos[lst[i].second] = i;
+      ParallelRanges(n, sort_threads, [&](std::ptrdiff_t lo, std::ptrdiff_t hi) {
+        for (std::ptrdiff_t i = lo; i < hi; ++i) c.pos[lst[i].second] = i;
+      });
     };
     if (nthreads <= 1) {
       for (size_t pi = 0; pi < perm.size(); ++pi) sort_one(pi);

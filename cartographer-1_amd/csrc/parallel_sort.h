@@ -154,6 +154,21 @@ void InsertionSort(T* first, T* last, Comp& comp) {
 
 }  // namespace sort_detail
 
+// fn(lo, hi) over [0, n) in up to `threads` contiguous pieces, one thread each.
+template <typename Fn>
+void ParallelRanges(std::ptrdiff_t n, int threads, Fn fn) {
+  const std::ptrdiff_t pieces =
+      std::max<std::ptrdiff_t>(1, std::min<std::ptrdiff_t>(threads, n / sort_detail::kParallelGrain));
+  if (pieces <= 1) {
+    fn(std::ptrdiff_t{0}, n);
+    return;
+  }
+  std::vector<std::thread> pool;
+  for (std::ptrdiff_t p = 1; p < pieces; ++p) pool.emplace_back(fn, n * p / pieces, n * (p + 1) / pieces);
+  fn(std::ptrdiff_t{0}, n / pieces);
+  for (auto& t : pool) t.join();
+}
+
 // Sorts [first, last) into exactly the order std::sort(first, last, comp)
 // gives, using up to `threads` threads.
 template <typename T, typename Comp>
