@@ -719,9 +719,11 @@ int RunBatch(csm_context* ctx, csm_fast2d* const* submaps, int32_t num_submaps,
   const char* forced_env = std::getenv("CSM_SEARCH_KERNEL");
   const int forced = forced_env ? std::atoi(forced_env) : 0;
   SearchPlan plan;
-  // The v4/v5 kernel keeps rot_chunk discretized scans (4 B/point) in LDS;
-  // above ~8k points per scan the v1 kernel (lanes = points) is used.
-  plan.use_v2 = forced == 2 || (forced != 1 && max_npad <= 8192);
+  // The v4/v5 kernel keeps rot_chunk discretized scans (4 B/point) and their
+  // cluster lists in LDS: up to kMaxPoints (16448 points, one rotation per
+  // workgroup, ~128 KB) it fits, so it takes every batch; the v1 kernel
+  // (lanes = points) runs only when forced (CSM_SEARCH_KERNEL=1).
+  plan.use_v2 = forced != 1;
   plan.hex = hex;
   plan.max_npad = max_npad;
   const char* rc_env = std::getenv("CSM_ROT_CHUNK");

@@ -41,7 +41,7 @@ def assert_fast_parity(oracle, om, limits, cells, gpu, ref, full, init, cloud, t
     """Same match decision, bit-identical score and the reference's pose. The
     v4/v5 kernels restore the reference's pick among exactly tied leaves
     (csm_host.cc ResolveTies), so the pose must be identical; only the v1
-    kernel (clouds past 8192 points) keeps the smallest tied leaf
+    kernel (CSM_SEARCH_KERNEL=1, never chosen by default) keeps the smallest tied leaf
     (ties_ok=True), which is then checked to score exactly the maximum."""
     g_ok, g_score, g_pose = gpu
     o_ok, o_score, o_pose = ref[:3]
@@ -167,7 +167,7 @@ def search_kernel(request, monkeypatch):
     top level and the one two below, quad planes elsewhere, FIFO node order),
     v5 with every even level hex, hex levels mixed into quad ones under the
     depth-first LIFO order, v4 (quad planes only) in both orders, and v1
-    (lanes = points, row-major pyramid; used above ~8k points). The plane
+    (lanes = points, row-major pyramid; only when forced). The plane
     layout is fixed when a matcher is created, so the variables are set
     before."""
     for var in ("CSM_SEARCH_KERNEL", "CSM_HEX_LEVELS", "CSM_SEARCH_ORDER"):
@@ -313,3 +313,57 @@ def test_run_lists_parity(csm, oracle, world, search_kernel):
                                         full_submap_center(limits, g.cells), c,
                                         ties_ok=search_kernel == "v1"))
     assert kinds.count("nomatch") < len(kinds)
+
+
+def _large_cloud(world, n_points, seed):
+    """n_points points: node clouds repeated with a few centimetres of jitter
+    (every copy after the first), so cells hold many points and runs split."""
+    rng = np.random.default_rng(seed)
+    base = world.cloud(int(world.submap_nodes[0]))
+    reps = -(-n_points // len(base))
+    c = np.concatenate([base] * reps)[:n_points].astype(np.float64)
+    jitter = rng.uniform(-0.03, 0.03, c.shape)
+    jitter[:len(base)] = 0.0
+    c[:, :2] += jitter[:, :2]
+    return np.ascontiguousarray(c, np.float32)
+
+
+@pytest.mark.parametrize("kernel", ["v5", "v4", "v1"])
+def test_large_clouds_match_oracle(csm, oracle, world, kernel, monkeypatch):
+    """Clouds past 8192 points, up to the boundary's limit kMaxPoints = 16448
+    (csm_device.h): Match() with a local window, in one batch with a small
+    cloud. v5 (the default for every size) runs one rotation per workgroup
+    here, its 16448-point scan and lists in ~128 KB of LDS; v4 and the forced
+    v1 kernel too."""
+    for var in ("CSM_SEARCH_KERNEL", "CSM_HEX_LEVELS", "CSM_SEARCH_ORDER"):
+        monkeypatch.delenv(var, raising=False)
+    if kernel != "v5":
+        monkeypatch.setenv("CSM_SEARCH_KERNEL", kernel[1:])
+    opts = csm.FastCorrelativeScanMatcherOptions2D(1.0, 0.15, 5)
+    s = 0
+    g = world.grid(s)
+    limits = (g.resolution, g.max_x, g.max_y)
+    m = csm.FastCorrelativeScanMatcher2D(g, opts)
+    om = oracle.fast2d(limits, g.cells, 1.0, 0.15, 5)
+    n = int(world.submap_nodes[s])
+    truth = world.node_poses[n]
+    init = (truth[0] + 0.3, truth[1] - 0.2, truth[2] + 0.05)
+    clouds = [_large_cloud(world, 9000, 1), _large_cloud(world, 16448, 2), world.cloud(n)]
+    scans = csm.ScanSet(clouds)
+    pairs = csm.make_pairs(np.zeros(3, np.int32), np.arange(3, dtype=np.int32), 0.3,
+                           full_submap=False, initial=[init] * 3)
+    res = csm.match_batch([m], scans, pairs)
+    assert_search_ok(csm, res["status"])
+    matched = 0
+    for k, c in enumerate(clouds):
+        gpu = (int(res[k]["status"]) == csm.CSM_OK, float(res[k]["score"]),
+               (float(res[k]["x"]), float(res[k]["y"]), float(res[k]["theta"])))
+        ref = om.match(init, c, 0.3)
+        assert_fast_parity(oracle, om, limits, g.cells, gpu, ref, False, init, c,
+                           ties_ok=kernel == "v1")
+        matched += int(gpu[0])
+    assert matched == 3
+    # One point past the limit is refused, not searched.
+    big = csm.ScanSet([_large_cloud(world, 16449, 3)])
+    r = csm.match_batch([m], big, csm.make_pairs([0], [0], 0.3, full_submap=False, initial=[init]))
+    assert int(r[0]["status"]) == csm.CSM_ERANGE
