@@ -220,6 +220,9 @@ _SIGNATURES = {
     "csm_scan_set_create": (C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_int64),
                                       C.c_int32, C.POINTER(C.c_void_p)]),
     "csm_scan_set_destroy": (None, [C.c_void_p]),
+    "csm_scan_set_append": (C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_int64),
+                                      C.c_int32, C.POINTER(C.c_int32)]),
+    "csm_scan_set_size": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int64)]),
     "csm_fast2d_match_batch": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.c_int32,
                                          C.c_void_p, C.POINTER(Pair2D), C.c_int64,
                                          C.POINTER(Result2D)]),
@@ -937,6 +940,29 @@ class ScanSet:
 
     def __len__(self):
         return len(self.offsets) - 1
+
+    def append(self, clouds: Sequence) -> int:
+        """Adds clouds to the resident set (csm_scan_set_append); earlier
+        scans keep their indices. Returns the first new scan's index."""
+        arrs = [_f32_points(c) for c in clouds]
+        offsets = np.zeros(len(arrs) + 1, np.int64)
+        offsets[1:] = np.cumsum([len(a) for a in arrs])
+        pts = np.ascontiguousarray(np.concatenate(arrs) if arrs else np.zeros((0, 3), np.float32))
+        first = C.c_int32()
+        _check(self._lib.csm_scan_set_append(self.handle, _ptr(pts, C.c_float),
+                                             _ptr(offsets, C.c_int64), len(arrs),
+                                             C.byref(first)), "csm_scan_set_append")
+        # `points` stays the creation-time clouds (the device set and its C
+        # host copy hold the rest); `offsets` covers every scan.
+        self.offsets = np.concatenate([self.offsets, self.offsets[-1] + offsets[1:]])
+        return int(first.value)
+
+    def device_size(self) -> Tuple[int, int]:
+        """(scans, points) the device set holds (csm_scan_set_size)."""
+        n, p = C.c_int32(), C.c_int64()
+        _check(self._lib.csm_scan_set_size(self.handle, C.byref(n), C.byref(p)),
+               "csm_scan_set_size")
+        return int(n.value), int(p.value)
 
     def close(self):
         if getattr(self, "handle", None):

@@ -94,6 +94,9 @@ class ConstraintBuilderOptions:
     fast_correlative_scan_matcher_options_3d: FastCorrelativeScanMatcherOptions3D = field(
         default_factory=FastCorrelativeScanMatcherOptions3D)
     flush_pairs: int = 0  # 0: search each node's pairs when the node ends
+    # Node clouds stay on the device across flushes; past this many resident
+    # points the builder starts a new set (as the C++ header's option).
+    scan_cache_points: int = 1 << 25
     # ceres_scan_matcher (pose_graph.lua:30-39): every accepted 2D match is
     # refined with CeresScanMatcher2D (constraint_builder_2d.cc:245-249).
     ceres_scan_matcher_options: CeresOptions2D = field(default_factory=CeresOptions2D.make)
@@ -133,6 +136,8 @@ class ConstraintBuilder2D:
         self._samplers: Dict[Tuple[int, int], FixedRatioSampler] = {}
         self._constraints: List[Optional[Constraint]] = []
         self._pending: List[_Pending] = []
+        self._scans: Optional[ScanSet] = None  # node clouds resident across flushes
+        self._scan_cache: Dict[Tuple[int, int], tuple] = {}  # node -> (cloud, index, points)
         self._started_nodes = 0
         self._finished_nodes = 0
         # Metrics (constraint_builder_2d.cc:46-53).
@@ -186,6 +191,49 @@ class ConstraintBuilder2D:
         return len(self._matchers)
 
     # -- internals ----------------------------------------------------------
+    def _resident_scans(self) -> ScanSet:
+        """The node clouds' device set, kept across flushes (TrajectoryNode
+        clouds are immutable, so each node's cloud is uploaded once); a new
+        set is started past options.scan_cache_points resident points."""
+        if self._scans is not None and \
+                int(self._scans.offsets[-1]) > self.options.scan_cache_points:
+            self._drop_scans()
+        if self._scans is None:
+            self._scans = ScanSet([], self.context)
+        return self._scans
+
+    def _drop_scans(self):
+        if self._scans is not None:
+            self._scans.close()
+        self._scans, self._scan_cache = None, {}
+
+    def _scan_indices(self, pending, scans: ScanSet) -> List[int]:
+        """Scan index of each pending pair's cloud; a node's cloud is reused
+        when it is the same points (compared, so callers may pass a fresh
+        array each time), appended otherwise."""
+        fresh, fresh_keys, index, seen = [], [], [], {}
+        for p in pending:
+            c = self._scan_cache.get(p.node_id)
+            if c is None or (c[0] is not p.cloud and (p.node_id, id(p.cloud)) not in seen):
+                pts = _f32_points(p.cloud)
+                seen[(p.node_id, id(p.cloud))] = True
+                if c is None or not np.array_equal(c[2], pts):
+                    c = (p.cloud, -1 - len(fresh), pts)
+                    fresh.append(pts)
+                    fresh_keys.append(p.node_id)
+                else:
+                    c = (p.cloud, c[1], c[2])
+                self._scan_cache[p.node_id] = c
+            index.append(c[1])
+        if fresh:
+            first = scans.append(fresh)
+            index = [first - 1 - k if k < 0 else k for k in index]
+            for key in fresh_keys:
+                cloud, k, pts = self._scan_cache[key]
+                if k < 0:
+                    self._scan_cache[key] = (cloud, first - 1 - k, pts)
+        return index
+
     def _enqueue(self, submap_id, submap, node_id, cloud, full, initial):
         key = tuple(submap_id)
         if key not in self._matchers:
@@ -198,24 +246,21 @@ class ConstraintBuilder2D:
     def _flush(self):
         pending, self._pending = self._pending, []
         if pending:
-            matchers, slot_of, clouds, scan_of = [], {}, [], {}
-            submap_idx, scan_idx = [], []
+            matchers, slot_of = [], {}
+            submap_idx = []
             for p in pending:
                 if p.submap_id not in slot_of:
                     slot_of[p.submap_id] = len(matchers)
                     matchers.append(self._matchers[p.submap_id])
-                if id(p.cloud) not in scan_of:  # a node's cloud uploads once
-                    scan_of[id(p.cloud)] = len(clouds)
-                    clouds.append(_f32_points(p.cloud))
                 submap_idx.append(slot_of[p.submap_id])
-                scan_idx.append(scan_of[id(p.cloud)])
+            scans = self._resident_scans()
+            scan_idx = self._scan_indices(pending, scans)
             pairs = make_pairs(submap_idx, scan_idx, 0.0, full_submap=True)
             for i, p in enumerate(pending):
                 pairs[i]["full_submap"] = 1 if p.full else 0
                 pairs[i]["min_score"] = (self.options.global_localization_min_score if p.full
                                          else self.options.min_score)
                 pairs[i]["x"], pairs[i]["y"], pairs[i]["theta"] = p.initial
-            scans = ScanSet(clouds, self.context)
             try:
                 results = match_batch(matchers, scans, pairs, self.context)
                 refined = {}
@@ -229,8 +274,9 @@ class ConstraintBuilder2D:
                         init, [q[:2] for q in init], self.options.ceres_scan_matcher_options,
                         self.context)
                     refined = {i: tuple(float(v) for v in poses[k]) for k, i in enumerate(ok)}
-            finally:
-                scans.close()
+            except BaseException:
+                self._drop_scans()
+                raise
             failed = 0
             for i, (p, r) in enumerate(zip(pending, results)):
                 if int(r["status"]) < 0:

@@ -1161,6 +1161,47 @@ void csm_scan_set_destroy(csm_scan_set* s) {
   delete s;
 }
 
+int csm_scan_set_append(csm_scan_set* s, const float* points_xyz, const int64_t* offsets,
+                        int32_t num_scans, int32_t* first_index) {
+  if (!s || !offsets || !first_index || num_scans < 0 || offsets[0] != 0) return CSM_EINVAL;
+  const int64_t added = offsets[num_scans];
+  if (added < 0 || (added > 0 && !points_xyz)) return CSM_EINVAL;
+  for (int32_t i = 0; i < num_scans; ++i)
+    if (offsets[i + 1] < offsets[i]) return CSM_EINVAL;
+  csm_context* ctx = s->ctx;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  if (EnsureDevice(ctx)) return CSM_EHIP;
+  const int64_t old_total = s->offsets.back();
+  if (static_cast<int64_t>(s->offsets.size()) - 1 + num_scans > INT32_MAX) return CSM_ERANGE;
+  const size_t need = sizeof(float) * 3 * static_cast<size_t>(old_total + added);
+  if (need > s->points.bytes) {
+    // Grow by half again, keeping the resident clouds (device-to-device).
+    csm::DevBuf grown;
+    if (grown.Reserve(std::max(need, s->points.bytes + s->points.bytes / 2))) return CSM_ENOMEM;
+    if (old_total > 0)
+      CSM_HIP(hipMemcpyAsync(grown.ptr, s->points.ptr, sizeof(float) * 3 * old_total,
+                             hipMemcpyDeviceToDevice, ctx->stream));
+    CSM_HIP(hipStreamSynchronize(ctx->stream));
+    std::swap(grown.ptr, s->points.ptr);
+    std::swap(grown.bytes, s->points.bytes);
+  }
+  if (added > 0)
+    CSM_HIP(hipMemcpyAsync(s->points.as<float>() + 3 * old_total, points_xyz,
+                           sizeof(float) * 3 * added, hipMemcpyHostToDevice, ctx->stream));
+  CSM_HIP(hipStreamSynchronize(ctx->stream));
+  *first_index = static_cast<int32_t>(s->offsets.size() - 1);
+  s->host_points.insert(s->host_points.end(), points_xyz, points_xyz + 3 * added);
+  for (int32_t i = 0; i < num_scans; ++i) s->offsets.push_back(old_total + offsets[i + 1]);
+  return CSM_OK;
+}
+
+int csm_scan_set_size(const csm_scan_set* s, int32_t* num_scans, int64_t* num_points) {
+  if (!s || !num_scans || !num_points) return CSM_EINVAL;
+  *num_scans = static_cast<int32_t>(s->offsets.size() - 1);
+  *num_points = s->offsets.back();
+  return CSM_OK;
+}
+
 int csm_fast2d_match_batch(csm_context* ctx, csm_fast2d* const* submaps, int32_t num_submaps,
                            const csm_scan_set* scans, const csm_pair2d* pairs,
                            int64_t num_pairs, csm_result2d* results) {

@@ -247,16 +247,65 @@ class ConstraintBuilder2D {
   }
 
   // Searches (and refines) pending_[which] as one batch.
-  void Search(const std::vector<size_t>& which_pending) {
+  // Device index of every pending_[which_pending[k]]'s cloud in scans_, which
+  // keeps node clouds resident across flushes: clouds not seen before (or a
+  // node whose cloud changed) are appended in one upload.
+  std::vector<int32_t> ResidentScans(const std::vector<size_t>& which_pending) {
+    int64_t fresh_points = 0;
+    for (size_t i : which_pending) {
+      auto c = scan_cache_.find(pending_[i].node_id);
+      if (c == scan_cache_.end() || c->second.cloud != pending_[i].cloud ||
+          c->second.size != pending_[i].cloud->size())
+        fresh_points += static_cast<int64_t>(pending_[i].cloud->size());
+    }
+    if (scans_ && cached_points_ + fresh_points > options_.scan_cache_points) {
+      csm_scan_set_destroy(scans_);
+      scans_ = nullptr;
+      scan_cache_.clear();
+      cached_points_ = 0;
+    }
+    if (!scans_) {
+      const int64_t zero = 0;
+      CheckOk(csm_scan_set_create(context_, nullptr, &zero, 0, &scans_), "csm_scan_set_create");
+    }
     std::vector<float> xyz;
     std::vector<int64_t> offsets{0};
-    std::vector<csm_fast2d*> handles;
-    std::map<SubmapId, int> slot_of;
-    std::map<const PointCloud*, int32_t> scan_of;  // a node's cloud uploads once
-    std::vector<csm_pair2d> pairs;
-    std::vector<std::shared_ptr<FastCorrelativeScanMatcher2D>> keep;
+    std::vector<int32_t> index;  // >= 0: resident; < 0: -1 - (k-th cloud of this upload)
+    std::vector<CachedScan*> fresh;
     for (size_t i : which_pending) {
       const Pending& p = pending_[i];
+      CachedScan& c = scan_cache_[p.node_id];
+      if (c.cloud != p.cloud || c.size != p.cloud->size() || c.index == kUnset) {
+        c.cloud = p.cloud;
+        c.size = p.cloud->size();
+        c.index = -static_cast<int32_t>(offsets.size());
+        fresh.push_back(&c);
+        xyz.insert(xyz.end(), p.cloud->xyz.begin(), p.cloud->xyz.end());
+        offsets.push_back(offsets.back() + static_cast<int64_t>(p.cloud->size()));
+      }
+      index.push_back(c.index);
+    }
+    if (offsets.size() > 1) {
+      int32_t first = 0;
+      CheckOk(csm_scan_set_append(scans_, xyz.data(), offsets.data(),
+                                  static_cast<int32_t>(offsets.size() - 1), &first),
+              "csm_scan_set_append");
+      cached_points_ += offsets.back();
+      for (int32_t& k : index)
+        if (k < 0) k = first - 1 - k;
+      for (CachedScan* c : fresh) c->index = first - 1 - c->index;
+    }
+    return index;
+  }
+
+  void Search(const std::vector<size_t>& which_pending) {
+    const std::vector<int32_t> scan_index = ResidentScans(which_pending);
+    std::vector<csm_fast2d*> handles;
+    std::map<SubmapId, int> slot_of;
+    std::vector<csm_pair2d> pairs;
+    std::vector<std::shared_ptr<FastCorrelativeScanMatcher2D>> keep;
+    for (size_t k = 0; k < which_pending.size(); ++k) {
+      const Pending& p = pending_[which_pending[k]];
       EnsureMatcher(p.submap_id, p.submap);
       auto m = matchers_.at(p.submap_id);
       auto s = slot_of.find(p.submap_id);
@@ -265,25 +314,14 @@ class ConstraintBuilder2D {
         handles.push_back(m->handle());
         keep.push_back(m);
       }
-      auto c = scan_of.find(p.cloud);
-      if (c == scan_of.end()) {
-        c = scan_of.emplace(p.cloud, static_cast<int32_t>(offsets.size() - 1)).first;
-        xyz.insert(xyz.end(), p.cloud->xyz.begin(), p.cloud->xyz.end());
-        offsets.push_back(offsets.back() + static_cast<int64_t>(p.cloud->size()));
-      }
       csm_pair2d q{};
       q.submap = s->second;
-      q.scan = c->second;
+      q.scan = scan_index[k];
       q.full_submap = p.full ? 1 : 0;
       q.min_score = p.full ? options_.global_localization_min_score : options_.min_score;
       q.initial = csm_pose2d{p.initial.x, p.initial.y, p.initial.theta};
       pairs.push_back(q);
     }
-    if (scans_) csm_scan_set_destroy(scans_);
-    scans_ = nullptr;
-    CheckOk(csm_scan_set_create(context_, xyz.data(), offsets.data(),
-                                static_cast<int32_t>(offsets.size() - 1), &scans_),
-            "csm_scan_set_create");
     std::vector<csm_result2d> results(pairs.size());
     CheckOk(csm_fast2d_match_batch(context_, handles.data(), static_cast<int32_t>(handles.size()),
                                    scans_, pairs.data(), static_cast<int64_t>(pairs.size()),
@@ -347,7 +385,15 @@ class ConstraintBuilder2D {
   std::map<SubmapId, FixedRatioSampler> samplers_;
   std::vector<std::unique_ptr<Constraint>> constraints_;
   std::vector<Pending> pending_;
-  csm_scan_set* scans_ = nullptr;
+  struct CachedScan {
+    const PointCloud* cloud = nullptr;
+    size_t size = 0;
+    int32_t index = kUnset;
+  };
+  static constexpr int32_t kUnset = INT32_MIN;
+  csm_scan_set* scans_ = nullptr;         // node clouds resident across flushes
+  std::map<NodeId, CachedScan> scan_cache_;
+  int64_t cached_points_ = 0;
   int num_started_nodes_ = 0, num_finished_nodes_ = 0;
   csm_comm* comm_ = nullptr;
   Sharding sharding_ = Sharding::kStatic;

@@ -21,6 +21,10 @@ struct SubmapId {
 };
 struct NodeId {
   int trajectory_id = 0, node_index = 0;
+  bool operator<(const NodeId& o) const {
+    return trajectory_id != o.trajectory_id ? trajectory_id < o.trajectory_id
+                                            : node_index < o.node_index;
+  }
 };
 
 // proto::ConstraintBuilderOptions (constraint_builder_options.proto:24-59),
@@ -41,6 +45,9 @@ struct ConstraintBuilderOptions {
   // ceres_scan_matcher_3d (pose_graph.lua:49-60), ConstraintBuilder3D (:264-275).
   csm_ceres3d_options ceres_scan_matcher_options_3d{5., 30., 10., 1., 10, /*nonmonotonic=*/0};
   bool refine_with_ceres = true;
+  // Node clouds stay on the device across flushes (a node's cloud is uploaded
+  // once); past this many resident points the 2D builder starts a new set.
+  int64_t scan_cache_points = int64_t{1} << 25;
 };
 
 // common/fixed_ratio_sampler.cc:32-39

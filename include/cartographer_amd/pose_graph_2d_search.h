@@ -35,11 +35,6 @@
 
 namespace cartographer_amd {
 
-inline bool operator<(const NodeId& a, const NodeId& b) {
-  return a.trajectory_id != b.trajectory_id ? a.trajectory_id < b.trajectory_id
-                                            : a.node_index < b.node_index;
-}
-
 // proto::PoseGraphOptions fields read here (pose_graph.lua:79-80).
 struct PoseGraphSearchOptions {
   double global_sampling_ratio = 0.003;

@@ -160,6 +160,16 @@ int csm_scan_set_create(csm_context* ctx, const float* points_xyz,
                         const int64_t* offsets, int32_t num_scans,
                         csm_scan_set** out);
 void csm_scan_set_destroy(csm_scan_set* s);
+/* Appends num_scans clouds (offsets[0] == 0, as for create) to a live set:
+ * the earlier scans keep their indices, device copies and cached rotation
+ * tables, and the first new scan gets index *first_index. Lets a builder keep
+ * one set across flushes (TrajectoryNode::Data clouds are immutable, so a
+ * node's cloud is uploaded once, not once per flush). */
+int csm_scan_set_append(csm_scan_set* s, const float* points_xyz,
+                        const int64_t* offsets, int32_t num_scans,
+                        int32_t* first_index);
+/* Scans and points currently held (for a caller's cache limit). */
+int csm_scan_set_size(const csm_scan_set* s, int32_t* num_scans, int64_t* num_points);
 
 typedef struct csm_pair2d {
   int32_t submap;      /* index into the submaps[] array */

@@ -14,7 +14,7 @@ import subprocess
 import numpy as np
 import pytest
 
-from conftest import ROOT
+from conftest import ROOT, assert_search_ok
 
 CPP_TEST = os.path.join(ROOT, "tests", "cpp", "constraint_builder_2d_test.cc")
 CPP_BIN = os.path.join(ROOT, "tests", "cpp", "_build", "constraint_builder_2d_test")
@@ -267,3 +267,71 @@ def test_builder_refines_accepted_matches(csm, cb, oracle):
                                       match[:2], match, world.cloud(a.node_id[1]))
         got_pose = cb.rigid2d_compose(local[s], b.relative_pose)
         assert np.allclose(got_pose, ref, atol=1e-6), (got_pose, ref)
+
+
+@pytest.mark.gpu
+def test_scan_set_append_matches_fresh_set(csm):
+    """csm_scan_set_append: scans appended in steps (the device buffer grows
+    and keeps the resident clouds) give the same batch results as one set
+    made from all clouds at once, and earlier indices stay valid."""
+    world = csm.SyntheticWorld2D(num_nodes=40, num_submaps=3, decimate_to=300, seed=11)
+    opts = csm.FastCorrelativeScanMatcherOptions2D(7.0, math.radians(30), 7)
+    mats = [csm.FastCorrelativeScanMatcher2D(world.grid(s), opts) for s in range(3)]
+    clouds = [world.cloud(n) for n in range(world.num_nodes)]
+    fresh = csm.ScanSet(clouds)
+    grown = csm.ScanSet(clouds[:2])
+    assert grown.append(clouds[2:5]) == 2
+    assert grown.append([]) == 5
+    assert grown.append(clouds[5:]) == 5  # past the initial capacity: device-to-device growth
+    assert grown.device_size() == (len(clouds), sum(len(c) for c in clouds))
+    assert len(grown) == len(clouds)
+    sub = [n % 3 for n in range(world.num_nodes)] + [int(s) for s in range(3)]
+    nodes = list(range(world.num_nodes)) + [int(world.submap_nodes[s]) for s in range(3)]
+    pairs = csm.make_pairs(sub, nodes, 0.5)
+    a = csm.match_batch(mats, fresh, pairs)
+    b = csm.match_batch(mats, grown, pairs)
+    assert_search_ok(csm, a["status"])
+    assert (a == b).all()
+    assert (a["status"] == 0).sum() >= 3
+
+
+@pytest.mark.gpu
+def test_builder_keeps_node_clouds_resident(csm, cb):
+    """The 2D builder uploads a node's cloud once across flushes (the pattern
+    of a finished submap matched against earlier nodes,
+    pose_graph_2d.cc:379-392), also when the caller hands a fresh array with
+    the same points; a node whose points change is uploaded again; results
+    equal a builder that starts a new set every flush (cache limit 0)."""
+    world = csm.SyntheticWorld2D(num_nodes=24, num_submaps=3, decimate_to=200, seed=5)
+    fopts = csm.FastCorrelativeScanMatcherOptions2D()
+
+    def run(cache_points):
+        opts = cb.ConstraintBuilderOptions(sampling_ratio=1.0, min_score=0.4,
+                                           global_localization_min_score=0.45,
+                                           max_constraint_distance=1e9,
+                                           fast_correlative_scan_matcher_options=fopts,
+                                           refine_with_ceres=False,
+                                           scan_cache_points=cache_points)
+        b = cb.ConstraintBuilder2D(opts)
+        submaps = {s: cb.Submap2D(world.grid(s), (0.0, 0.0, 0.0)) for s in range(3)}
+        for s in range(3):  # each "finished submap" against every node so far
+            for node in range(8 * (s + 1)):
+                cloud = world.cloud(node)
+                if s == 2 and node == 1:
+                    cloud = cloud.copy()
+                    cloud[0, 0] += 0.05  # changed points: uploaded again
+                b.MaybeAddGlobalConstraint((0, s), submaps[s], (0, node), cloud)
+            b.NotifyEndOfNode()
+        got = []
+        b.WhenDone(got.append)
+        return b, got[0]
+
+    b, got = run(1 << 25)
+    # 8 + 8 + 8 new nodes, plus node 1's changed cloud.
+    assert b._scans.device_size()[0] == 25
+    ref_b, ref = run(0)
+    assert len(got) == len(ref) > 3
+    for c, r in zip(got, ref):
+        assert (c.submap_id, c.node_id, c.score, c.relative_pose) == \
+            (r.submap_id, r.node_id, r.score, r.relative_pose)
+    assert b.global_constraints_searched == ref_b.global_constraints_searched == 48
