@@ -101,10 +101,66 @@ static void SkipsUnsearchablePairs() {
   EXPECT(builder.global_constraints_searched == 1 && builder.global_constraints_found == 1);
 }
 
+// Node clouds stay resident across flushes (csm_scan_set_append). A node
+// whose cloud changes between flushes is searched with the new points: the
+// second flush of a long-lived builder equals a fresh builder's result.
+static void ReusesResidentCloudsAcrossFlushes() {
+  std::vector<uint16_t> cells(100 * 110, 0);
+  // An L of occupied cells (correspondence cost value 1: probability 0.9).
+  for (int x = 10; x <= 14; ++x) cells[20 * 100 + x] = 1;
+  for (int y = 21; y <= 23; ++y) cells[y * 100 + 10] = 1;
+  Submap2DView submap;
+  submap.grid.resolution = 1.;
+  submap.grid.max_x = 2.;
+  submap.grid.max_y = 3.;
+  submap.grid.num_x_cells = 100;
+  submap.grid.num_y_cells = 110;
+  submap.grid.cells = cells.data();
+  submap.local_pose = Rigid2d{0., 0., 0.};
+  // The L's cell centres in the submap frame (x from the cell row, y from
+  // the column), then the same points shifted 3 m.
+  PointCloud first, shifted;
+  for (int x = 10; x <= 14; ++x) first.push_back(2.f - 20.5f, 3.f - (x + 0.5f), 0.f);
+  for (int y = 21; y <= 23; ++y) first.push_back(2.f - (y + 0.5f), 3.f - 10.5f, 0.f);
+  for (size_t i = 0; i < first.size(); ++i)
+    shifted.push_back(first.xyz[3 * i] + 3.f, first.xyz[3 * i + 1], 0.f);
+  const SubmapId submap_id{0, 0};
+  ConstraintBuilder2D kept(TestOptions());
+  ConstraintBuilder2D::Result r1, r2, fresh;
+  kept.MaybeAddGlobalConstraint(submap_id, &submap, NodeId{0, 7}, &first);
+  kept.NotifyEndOfNode();
+  kept.WhenDone([&](const ConstraintBuilder2D::Result& r) { r1 = r; });
+  kept.MaybeAddGlobalConstraint(submap_id, &submap, NodeId{0, 7}, &shifted);  // changed cloud
+  kept.MaybeAddGlobalConstraint(submap_id, &submap, NodeId{0, 8}, &first);    // new node
+  kept.NotifyEndOfNode();
+  kept.WhenDone([&](const ConstraintBuilder2D::Result& r) { r2 = r; });
+  ConstraintBuilder2D once(TestOptions());
+  once.MaybeAddGlobalConstraint(submap_id, &submap, NodeId{0, 7}, &shifted);
+  once.MaybeAddGlobalConstraint(submap_id, &submap, NodeId{0, 8}, &first);
+  once.NotifyEndOfNode();
+  once.WhenDone([&](const ConstraintBuilder2D::Result& r) { fresh = r; });
+  EXPECT(r1.size() == 1 && r2.size() == 2 && fresh.size() == 2);
+  if (r1.size() != 1 || r2.size() != 2 || fresh.size() != 2) return;
+  for (int k = 0; k < 2; ++k) {
+    EXPECT(r2[k].score == fresh[k].score);
+    EXPECT(r2[k].relative_pose.x == fresh[k].relative_pose.x &&
+           r2[k].relative_pose.y == fresh[k].relative_pose.y &&
+           r2[k].relative_pose.theta == fresh[k].relative_pose.theta);
+  }
+  // The shifted cloud matched elsewhere than the first (not a stale copy),
+  // and node 8's copy of the first cloud matched where node 7's first did.
+  EXPECT(r2[0].relative_pose.x != r1[0].relative_pose.x ||
+         r2[0].relative_pose.y != r1[0].relative_pose.y ||
+         r2[0].relative_pose.theta != r1[0].relative_pose.theta);
+  EXPECT(r2[1].score == r1[0].score && r2[1].relative_pose.x == r1[0].relative_pose.x &&
+         r2[1].relative_pose.y == r1[0].relative_pose.y);
+}
+
 int main() {
   CallsBack();
   FindsConstraints();
   SkipsUnsearchablePairs();
+  ReusesResidentCloudsAcrossFlushes();
   if (failures) return 1;
   std::printf("constraint_builder_2d_test: OK\n");
   return 0;

@@ -293,6 +293,18 @@ def test_scan_set_append_matches_fresh_set(csm):
     assert_search_ok(csm, a["status"])
     assert (a == b).all()
     assert (a["status"] == 0).sum() >= 3
+    # Malformed appends are refused and leave the set as it was.
+    import ctypes as C
+    lib, first = grown._lib, C.c_int32(-7)
+    pts = np.zeros((4, 3), np.float32)
+    bad_start = np.array([1, 4], np.int64)    # offsets[0] must be 0
+    decreasing = np.array([0, 3, 2], np.int64)
+    for offs in (bad_start, decreasing):
+        rc = lib.csm_scan_set_append(grown.handle, pts.ctypes.data_as(C.POINTER(C.c_float)),
+                                     offs.ctypes.data_as(C.POINTER(C.c_int64)), len(offs) - 1,
+                                     C.byref(first))
+        assert rc == csm.CSM_EINVAL and first.value == -7
+    assert grown.device_size() == (len(clouds), sum(len(c) for c in clouds))
 
 
 @pytest.mark.gpu
