@@ -78,6 +78,9 @@ def parse():
     p.add_argument("--c3-workers", type=int, default=1,
                    help="host threads per rank, each with its own context (stream): a chunk's "
                         "host work (tie resolution, records) overlaps the next chunk's search")
+    p.add_argument("--c3-tie-log", default="",
+                   help="write the C3 queue's exactly tied pairs (submap, node, branch) to "
+                        "<path>.rank<r>.json (input of tools/c3_tie_fixture.py)")
     p.add_argument("--cpu-pairs", type=int, default=0,
                    help="CPU baseline sample size (0: 2000 for C3, sized to --cpu-seconds for C2)")
     return p.parse_args()
@@ -456,12 +459,28 @@ def dropin_bench(csm, ctx, matchers, scans, world, args):
         a = time.perf_counter()
         m.MatchFullSubmap(cloud, args.min_score)
         single_ms.append((time.perf_counter() - a) * 1e3)
+    # Option A as the reference runs it: T pool threads calling MatchFullSubmap
+    # on shared matchers concurrently (constraint_builder_2d.cc:100-111), each
+    # call on its own call context (stream + scratch).
+    from concurrent.futures import ThreadPoolExecutor
+    threaded = {}
+    calls = 400
+    for T in (1, 4, 8, 16):
+        def one(j):
+            return matchers[j % k].MatchFullSubmap(world.cloud(j % args.nodes), args.min_score)
+        with ThreadPoolExecutor(max_workers=T) as ex:
+            list(ex.map(one, range(2 * T)))  # warm-up: one call context per thread
+            a = time.perf_counter()
+            list(ex.map(one, range(calls)))
+            wall = time.perf_counter() - a
+        threaded[str(T)] = {"calls": calls, "pairs_per_s": calls / wall}
     return {"per_node_flush": {"pairs_per_flush": k, "flushes": nodes,
                                "ms_per_flush_median": float(np.median(flush_ms)),
                                "pairs_per_s": k / (float(np.median(flush_ms)) * 1e-3)},
             "single_call": {"calls": len(single_ms),
                             "ms_per_match_full_submap_median": float(np.median(single_ms)),
                             "pairs_per_s": 1e3 / float(np.median(single_ms))},
+            "single_call_threads": threaded,
             "note": "through the Python ctypes mirror; a batch uploads its pair descriptors, the "
                     "scan set's rotation tables are built once and kept on the device"}
 
@@ -982,7 +1001,7 @@ def c3_run(csm, ctx, args, rank, world_size, dist, coll_dev, comm, gather, trans
         c.enable_timing(True)
     barrier_sync()
     t_start = time.perf_counter()
-    done = {"errors": 0, "mine": 0, "recs": []}
+    done = {"errors": 0, "mine": 0, "recs": [], "ties": []}
 
     def worker(w):
         while True:
@@ -990,10 +1009,13 @@ def c3_run(csm, ctx, args, rank, world_size, dist, coll_dev, comm, gather, trans
             if c >= n_chunks:
                 return
             res, rec = run_chunk(chunks[c], np.int64(c) * K * N, w)
+            tied = np.nonzero((res["status"] == 0) & (res["tie"] != 0))[0]
             with claim_lock:
                 done["errors"] += int((res["status"] < 0).sum())
                 done["recs"].append(rec)
                 done["mine"] += 1
+                for k in tied:  # (submap, node, csm_result2d.tie) of exactly tied pairs
+                    done["ties"].append((int(chunks[c][k // N]), int(k % N), int(res["tie"][k])))
             if rank == 0 and (c % 10 == 0 or world_size == 1):
                 print(f"c3: chunk {c + 1}/{n_chunks} {time.perf_counter() - t_start:.1f} s",
                       file=sys.stderr, flush=True)
@@ -1056,11 +1078,21 @@ def c3_run(csm, ctx, args, rank, world_size, dist, coll_dev, comm, gather, trans
         # Pairs with exactly tied maxima (resolved to the reference's pick,
         # csm_host.cc ResolveTies) and any left at the smallest-key leaf.
         "tied_pairs_rank0": int(tm.tied_pairs), "ties_unresolved_rank0": int(tm.ties_unresolved),
+        # Per resolution branch (csm_result2d.tie): under one top-level
+        # candidate, through the whole top-level list's introsort, unresolved.
+        "ties_by_branch_rank0": {name: sum(1 for t in done["ties"] if t[2] == code)
+                                 for name, code in (("ancestors", csm.TIE_ANCESTORS),
+                                                    ("toplist", csm.TIE_TOPLIST),
+                                                    ("unresolved", csm.TIE_UNRESOLVED))},
         "kernel_s_rank0": tm.search_kernel_ms * 1e-3, "search_launches_rank0": int(tm.search_launches),
         "search_levels": {"candidates_per_pair": [c / max(mine * K * N, 1) for c in lv_cands],
                           "mean_lanes_per_batch": [c / b if b else 0 for c, b in zip(lv_cands, lv_batches)]},
         "setup_s": {"world": gen_s},
     }
+    if args.c3_tie_log:  # the tied pairs, for tools/c3_tie_fixture.py
+        with open(f"{args.c3_tie_log}.rank{rank}.json", "w") as f:
+            json.dump({"seed": args.seed, "nodes": N, "submaps": S, "min_score": args.min_score,
+                       "ties": sorted(done["ties"])}, f)
     if rank == 0 and world_size == 1 and not args.no_cpu:
         rng = np.random.RandomState(12345)
         k = args.cpu_pairs or 2000

@@ -73,7 +73,12 @@ class Pair2D(C.Structure):
 
 
 class Result2D(C.Structure):
-    _fields_ = [("status", C.c_int32), ("score", C.c_float), ("pose", Pose2D)]
+    _fields_ = [("status", C.c_int32), ("score", C.c_float), ("pose", Pose2D),
+                ("tie", C.c_int32), ("reserved", C.c_int32)]
+
+
+# csm_result2d.tie: how a result was picked among exactly tied maxima.
+TIE_NONE, TIE_ANCESTORS, TIE_TOPLIST, TIE_UNRESOLVED = 0, 1, 2, 3
 
 
 class Timing(C.Structure):
@@ -83,7 +88,9 @@ class Timing(C.Structure):
                 ("rt3d_lookups", C.c_double), ("fast3d_kernel_ms", C.c_double),
                 ("fast3d_launches", C.c_int64), ("fast3d_lookups", C.c_double),
                 ("search_errors", C.c_int64), ("stack_high_water", C.c_int64),
-                ("tied_pairs", C.c_int64), ("ties_unresolved", C.c_int64)]
+                ("tied_pairs", C.c_int64), ("ties_unresolved", C.c_int64),
+                ("ties_toplist", C.c_int64), ("tied_pairs_3d", C.c_int64),
+                ("ties_unresolved_3d", C.c_int64)]
 
 
 class Pose3D(C.Structure):
@@ -980,7 +987,8 @@ PAIR_DTYPE = np.dtype([("submap", np.int32), ("scan", np.int32), ("full_submap",
                        ("min_score", np.float32), ("x", np.float64), ("y", np.float64),
                        ("theta", np.float64)])
 RESULT_DTYPE = np.dtype([("status", np.int32), ("score", np.float32), ("x", np.float64),
-                         ("y", np.float64), ("theta", np.float64)])
+                         ("y", np.float64), ("theta", np.float64), ("tie", np.int32),
+                         ("reserved", np.int32)])
 assert PAIR_DTYPE.itemsize == C.sizeof(Pair2D)
 assert RESULT_DTYPE.itemsize == C.sizeof(Result2D)
 

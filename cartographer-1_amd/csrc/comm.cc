@@ -14,6 +14,7 @@
 
 #include <arpa/inet.h>
 #include <dlfcn.h>
+#include <errno.h>
 #include <hip/hip_runtime.h>
 #include <netdb.h>
 #include <netinet/in.h>
@@ -69,7 +70,13 @@ RcclApi* Rccl() {
   static bool tried = false;
   if (tried) return api.lib ? &api : nullptr;
   tried = true;
-  void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+  // CSM_RCCL_LIB names another library with the same entry points (tests:
+  // tests/comm_standin/, a TCP stand-in that lets several ranks share one GPU
+  // box and run this file's RCCL code paths with N > 1).
+  const char* over = std::getenv("CSM_RCCL_LIB");
+  void* h = over && *over ? dlopen(over, RTLD_NOW | RTLD_LOCAL) : nullptr;
+  if (over && *over && !h) return nullptr;  // asked for, not loadable: fail, no silent swap
+  if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
   if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
   if (!h) return nullptr;
   auto sym = [&](const char* n) { return dlsym(h, n); };
@@ -92,10 +99,14 @@ RcclApi* Rccl() {
 }
 
 // ---- TCP helpers ----------------------------------------------------------------
+// A signal delivered to this thread interrupts poll / send / recv (EINTR;
+// Linux never restarts poll after a handler): retried, never read as a peer
+// failure. A bounded wait keeps its deadline across the retries.
 bool SendAll(int fd, const void* p, size_t n) {
   const char* c = static_cast<const char*>(p);
   while (n) {
     const ssize_t k = ::send(fd, c, n, MSG_NOSIGNAL);
+    if (k < 0 && errno == EINTR) continue;
     if (k <= 0) return false;
     c += k;
     n -= static_cast<size_t>(k);
@@ -105,10 +116,21 @@ bool SendAll(int fd, const void* p, size_t n) {
 
 bool RecvAll(int fd, void* p, size_t n, int timeout_ms) {
   char* c = static_cast<char*>(p);
+  const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(
+                                                                  std::max(timeout_ms, 0));
   while (n) {
+    int wait = -1;
+    if (timeout_ms >= 0) {
+      const auto left = std::chrono::duration_cast<std::chrono::milliseconds>(
+          deadline - std::chrono::steady_clock::now()).count();
+      wait = static_cast<int>(std::max<long long>(left, 0));
+    }
     pollfd pf{fd, POLLIN, 0};
-    if (::poll(&pf, 1, timeout_ms) <= 0) return false;
+    const int pr = ::poll(&pf, 1, wait);
+    if (pr < 0 && errno == EINTR) continue;
+    if (pr <= 0) return false;
     const ssize_t k = ::recv(fd, c, n, 0);
+    if (k < 0 && errno == EINTR) continue;
     if (k <= 0) return false;
     c += k;
     n -= static_cast<size_t>(k);
@@ -474,6 +496,10 @@ int csm_comm_get_unique_id(uint8_t* id) {
 int csm_comm_create_rccl(csm_context* ctx, int32_t rank, int32_t world_size, const uint8_t* id,
                          csm_comm** out) {
   if (!ctx || !id || !out || world_size < 1 || rank < 0 || rank >= world_size) return CSM_EINVAL;
+  // The gather's count exchange uses a fixed buffer of kCountWords words
+  // (world_size counts + 2 agreement words): refuse larger worlds here rather
+  // than at the first gather.
+  if (world_size > kCountWords - 2) return CSM_ERANGE;
   RcclApi* R = Rccl();
   if (!R) return CSM_EHIP;
   if (hipSetDevice(ctx->device) != hipSuccess) return CSM_EHIP;

@@ -85,30 +85,82 @@ int EnsureDevice(csm_context* ctx) {
 
 // The context's pool of device buffers from destroyed matchers: the smallest
 // one holding n bytes (and at most twice that) is reused, else a new one is
-// allocated. Callers hold ctx->mu.
+// allocated; if that allocation fails, the idle pooled buffers are released
+// and it is tried once more. Callers hold ctx->mu.
+void PoolRelease(csm_context* ctx) {
+  for (auto& b : ctx->buf_pool) (void)hipFree(b.first);
+  ctx->buf_pool.clear();
+}
 int PoolTake(csm_context* ctx, size_t n, DevBuf* out) {
   int best = -1;
   for (int i = 0; i < static_cast<int>(ctx->buf_pool.size()); ++i) {
     const size_t b = ctx->buf_pool[i].second;
     if (b >= n && b <= 2 * n + 4096 && (best < 0 || b < ctx->buf_pool[best].second)) best = i;
   }
-  if (best < 0) return out->Reserve(n);
+  if (best < 0) {
+    if (out->Reserve(n) == CSM_OK) return CSM_OK;
+    PoolRelease(ctx);
+    return out->Reserve(n);
+  }
   out->ptr = ctx->buf_pool[best].first;
   out->bytes = ctx->buf_pool[best].second;
   ctx->buf_pool.erase(ctx->buf_pool.begin() + best);
   return CSM_OK;
 }
+// At most 32 buffers and 1 GiB stay pooled (oldest freed first): enough for
+// a sweep's create / destroy churn of ~40 submaps, without holding memory a
+// later 3D or scratch allocation needs.
 void PoolGive(csm_context* ctx, DevBuf* b) {
   constexpr size_t kMaxPooled = 32;
+  constexpr size_t kMaxPooledBytes = size_t{1} << 30;
   if (!b->ptr) return;
-  if (ctx->buf_pool.size() >= kMaxPooled) {
-    (void)hipFree(ctx->buf_pool.front().first);
-    ctx->buf_pool.erase(ctx->buf_pool.begin());
-  }
   ctx->buf_pool.emplace_back(b->ptr, b->bytes);
   b->ptr = nullptr;
   b->bytes = 0;
+  size_t held = 0;
+  for (const auto& e : ctx->buf_pool) held += e.second;
+  while (!ctx->buf_pool.empty() &&
+         (ctx->buf_pool.size() > kMaxPooled || held > kMaxPooledBytes)) {
+    held -= ctx->buf_pool.front().second;
+    (void)hipFree(ctx->buf_pool.front().first);
+    ctx->buf_pool.erase(ctx->buf_pool.begin());
+  }
 }
+
+}  // namespace
+
+namespace csm {
+
+csm_context* AcquireCallContext(csm_context* owner) {
+  {
+    std::lock_guard<std::mutex> g(owner->call_mu);
+    if (!owner->call_free.empty()) {
+      csm_context* c = owner->call_free.back();
+      owner->call_free.pop_back();
+      c->timing = owner->timing.load();
+      return c;
+    }
+  }
+  csm_context* c = nullptr;
+  if (csm_context_create(owner->device, &c) != CSM_OK) return nullptr;
+  c->call_owner = owner;
+  c->timing = owner->timing.load();
+  std::lock_guard<std::mutex> g(owner->call_mu);
+  owner->call_all.push_back(c);
+  return c;
+}
+
+void ReleaseCallContext(csm_context* owner, csm_context* c) {
+  if (!c) return;
+  std::lock_guard<std::mutex> g(owner->call_mu);
+  AddTiming(&owner->call_t, c->t);
+  c->t = csm_timing{};
+  owner->call_free.push_back(c);
+}
+
+}  // namespace csm
+
+namespace {
 
 const std::pair<SearchWindow2D, std::vector<ZRot>>& WindowFor(
     csm_scan_set* s, int scan, double lin, double ang, double res) {
@@ -334,7 +386,8 @@ void RotationBounds(const csm_scan_set* scans, const PairDesc& d, const SubmapDe
 int ResolveTies(csm_context* ctx, csm_fast2d* const* submaps, csm_scan_set* scans,
                 const std::vector<PairDesc>& pdesc, const std::vector<float2>& rot_host,
                 const SearchPlan& plan, const std::vector<int32_t>& stat,
-                const std::vector<uint64_t>& keys_hi, std::vector<uint64_t>* keys) {
+                const std::vector<uint64_t>& keys_hi, std::vector<uint64_t>* keys,
+                std::vector<int8_t>* tie_code) {
   std::vector<int> tied;
   for (int k = 0; k < static_cast<int>(pdesc.size()); ++k) {
     const uint64_t key = (*keys)[k];
@@ -389,6 +442,7 @@ int ResolveTies(csm_context* ctx, csm_fast2d* const* submaps, csm_scan_set* scan
     const int cnt = counts[t];
     if ((st2[t] & kStatusRange) || cnt > kTieCap || cnt < 2) {
       ctx->t.ties_unresolved += 1;
+      (*tie_code)[k] = CSM_TIE_UNRESOLVED;
       continue;
     }
     const PairDesc& d = pdesc[k];
@@ -496,8 +550,11 @@ int ResolveTies(csm_context* ctx, csm_fast2d* const* submaps, csm_scan_set* scan
   // top-level permutation: bounds of all its rotations on the device, every
   // lattice node scored in one launch, each list sorted on its own thread.
   std::vector<int> perm;
-  for (size_t wi = 0; wi < work.size(); ++wi)
+  for (size_t wi = 0; wi < work.size(); ++wi) {
+    (*tie_code)[work[wi].k] = cand[wi].need_perm ? CSM_TIE_TOPLIST : CSM_TIE_ANCESTORS;
     if (cand[wi].need_perm) perm.push_back(static_cast<int>(wi));
+  }
+  ctx->t.ties_toplist += static_cast<int64_t>(perm.size());
   if (!perm.empty()) {
     std::vector<int2> bjobs;
     for (int wi : perm)
@@ -660,6 +717,8 @@ int RunBatch(csm_context* ctx, csm_fast2d* const* submaps, int32_t num_submaps,
     results[i].status = CSM_NO_MATCH;
     results[i].score = 0.f;
     results[i].pose = csm_pose2d{0., 0., 0.};
+    results[i].tie = CSM_TIE_NONE;
+    results[i].reserved = 0;
     if (p.submap < 0 || p.submap >= num_submaps || p.scan < 0 ||
         p.scan >= static_cast<int32_t>(scans->offsets.size()) - 1) {
       results[i].status = CSM_EINVAL;
@@ -799,8 +858,9 @@ int RunBatch(csm_context* ctx, csm_fast2d* const* submaps, int32_t num_submaps,
   const double search_ms = ms_since(t_search);
   const auto t_ties = std::chrono::steady_clock::now();
   const int64_t tied_before = ctx->t.tied_pairs;
+  std::vector<int8_t> tie_code(np, CSM_TIE_NONE);
   if (plan.use_v2 && (rcode = ResolveTies(ctx, submaps, scans, pdesc, rot_host, plan, stat, keys_hi,
-                                           &keys)))
+                                           &keys, &tie_code)))
     return rcode;
   const double ties_ms = ms_since(t_ties);
   const auto t_decode = std::chrono::steady_clock::now();
@@ -841,6 +901,7 @@ int RunBatch(csm_context* ctx, csm_fast2d* const* submaps, int32_t num_submaps,
     const double cx = -yo * res, cy = -xo * res;
     const double co = (rot - w.num_angular_perturbations) * w.angular_perturbation_step_size;
     results[i].status = CSM_OK;
+    results[i].tie = tie_code[k];
     results[i].score = SumToScore(sum, d.num_points, m->min_s, m->max_s);
     results[i].pose.x = init.x + cx;
     results[i].pose.y = init.y + cy;
@@ -907,11 +968,18 @@ void csm_context_enable_timing(csm_context* ctx, int32_t enable) {
   if (ctx) ctx->timing = enable != 0;
 }
 void csm_context_get_timing(csm_context* ctx, csm_timing* out) {
-  if (ctx && out) *out = ctx->t;
+  if (!ctx || !out) return;
+  *out = ctx->t;
+  std::lock_guard<std::mutex> g(ctx->call_mu);  // single calls' share
+  AddTiming(out, ctx->call_t);
 }
 void csm_context_reset_timing(csm_context* ctx) {
   if (!ctx) return;
   ctx->t = csm_timing{};
+  {
+    std::lock_guard<std::mutex> g(ctx->call_mu);
+    ctx->call_t = csm_timing{};
+  }
   for (int l = 0; l < kMaxLevels; ++l) ctx->level_cands[l] = ctx->level_batches[l] = 0.;
 }
 
@@ -1219,18 +1287,31 @@ static int SingleMatch(const csm_fast2d* m, const csm_pose2d* initial, int full,
                        const float* xyz, int32_t n, float min_score, float* score,
                        csm_pose2d* pose) {
   if (!m || !score || !pose || (n > 0 && !xyz) || n < 0 || (!full && !initial)) return CSM_EINVAL;
-  csm_context* ctx = m->ctx;
+  // A call context of the matcher's context (csm_internal.h): this call's
+  // stream and scratch; the pyramid is read-only and shared.
+  csm::CallContext cc(m->ctx);
+  csm_context* ctx = cc.get();
+  if (!ctx) return CSM_EHIP;
   std::lock_guard<std::mutex> lock(ctx->mu);
   if (EnsureDevice(ctx)) return CSM_EHIP;
-  csm_scan_set s;
+  // The call context's one-scan set, reset for this cloud (scan index 0
+  // names a different cloud on every call, so no window is kept).
+  csm_scan_set& s = ctx->single;
   s.ctx = ctx;
   s.offsets = {0, n};
   s.host_points.assign(xyz, xyz + 3 * static_cast<size_t>(n));
+  s.windows.clear();
+  s.rot_all.clear();
+  s.rot_offsets.clear();
+  s.rot_uploaded = 0;
   int rc;
   if ((rc = s.points.Reserve(sizeof(float) * 3 * std::max(n, 1)))) return rc;
-  if (n > 0)
-    CSM_HIP(hipMemcpyAsync(s.points.ptr, xyz, sizeof(float) * 3 * n, hipMemcpyHostToDevice,
-                           ctx->stream));
+  if (n > 0) {
+    if ((rc = ctx->single_stage.Reserve(sizeof(float) * 3 * n))) return rc;
+    std::memcpy(ctx->single_stage.ptr, xyz, sizeof(float) * 3 * n);
+    CSM_HIP(hipMemcpyAsync(s.points.ptr, ctx->single_stage.ptr, sizeof(float) * 3 * n,
+                           hipMemcpyHostToDevice, ctx->stream));
+  }
   csm_pair2d p{};
   p.submap = 0;
   p.scan = 0;

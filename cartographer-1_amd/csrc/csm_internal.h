@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <map>
 #include <mutex>
 #include <tuple>
@@ -81,15 +82,67 @@ struct Rt2dCache {
 
 }  // namespace csm
 
+struct csm_scan_set {
+  csm_context* ctx = nullptr;
+  std::vector<float> host_points;
+  std::vector<int64_t> offsets;
+  csm::DevBuf points;
+  // Rotation tables per (scan, angular window, linear window, resolution).
+  std::map<std::tuple<int, double, double, double>,
+           std::pair<csm::SearchWindow2D, std::vector<csm::ZRot>>>
+      windows;
+  // Their device copy, appended as batches meet new windows: (w, s) per
+  // rotation, the offset of each window's table, and how much is uploaded.
+  std::vector<float2> rot_all;
+  std::map<const void*, int32_t> rot_offsets;
+  csm::DevBuf rot_dev;
+  size_t rot_uploaded = 0;
+};
+
+// Timing records add up field by field (the stack high-water mark: max).
+inline void AddTiming(csm_timing* a, const csm_timing& b) {
+  a->search_kernel_ms += b.search_kernel_ms;
+  a->search_launches += b.search_launches;
+  a->search_lookups += b.search_lookups;
+  a->search_candidates += b.search_candidates;
+  a->other_kernel_ms += b.other_kernel_ms;
+  a->rt3d_kernel_ms += b.rt3d_kernel_ms;
+  a->rt3d_lookups += b.rt3d_lookups;
+  a->fast3d_kernel_ms += b.fast3d_kernel_ms;
+  a->fast3d_launches += b.fast3d_launches;
+  a->fast3d_lookups += b.fast3d_lookups;
+  a->search_errors += b.search_errors;
+  a->stack_high_water = std::max(a->stack_high_water, b.stack_high_water);
+  a->tied_pairs += b.tied_pairs;
+  a->ties_unresolved += b.ties_unresolved;
+  a->ties_toplist += b.ties_toplist;
+  a->tied_pairs_3d += b.tied_pairs_3d;
+  a->ties_unresolved_3d += b.ties_unresolved_3d;
+}
+
 struct csm_context {
   int device = 0;
   hipStream_t stream = nullptr;
   std::mutex mu;
+  // Single Match / MatchFullSubmap calls (csm_fast2d_match*, csm_fast3d_match*)
+  // run on a call context taken from the matcher's context for the duration
+  // of the call: its own stream and scratch, the matcher's device pyramid
+  // shared read-only. The reference calls these const methods concurrently
+  // from ThreadPool workers (constraint_builder_2d.cc:100-111); concurrent
+  // callers get distinct call contexts, so their searches overlap on the GPU
+  // instead of queuing on the creator's stream. The pool grows to the largest
+  // number of concurrent callers and is destroyed with the context.
+  std::mutex call_mu;
+  std::vector<csm_context*> call_free, call_all;
+  csm_context* call_owner = nullptr;  // set on call contexts
+  csm_timing call_t{};                // finished single calls' timing (call_mu)
+  csm_scan_set single;                // the cloud of the current single 2D call
+  csm::PinnedBuf single_stage;
   csm::DevBuf submap_desc, pair_desc, best, status, counters, pair_order,
       chunk_prefix, blocks, stats, spill, single_points, best_hi, ties, tie_count, sq_jobs,
       sq_queries, sq_sums;
   csm::Rt2dCache rt2d;
-  bool timing = false;
+  std::atomic<bool> timing{false};
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   csm_timing t{};
   double level_cands[csm::kMaxLevels] = {0};
@@ -114,6 +167,7 @@ struct csm_context {
   csm::DevBuf f2_cells, f2_widen, f2_qtab, f2_ctab;
   float f2_tab_key[2] = {-1.f, -1.f};
   ~csm_context() {
+    for (csm_context* c : call_all) csm_context_destroy(c);
     for (auto& b : buf_pool) (void)hipFree(b.first);
   }
 };
@@ -129,22 +183,24 @@ struct csm_fast2d {
   csm::DevBuf cost;  // float correspondence costs, x fastest (CeresScanMatcher2D refinement)
 };
 
-struct csm_scan_set {
-  csm_context* ctx = nullptr;
-  std::vector<float> host_points;
-  std::vector<int64_t> offsets;
-  csm::DevBuf points;
-  // Rotation tables per (scan, angular window, linear window, resolution).
-  std::map<std::tuple<int, double, double, double>,
-           std::pair<csm::SearchWindow2D, std::vector<csm::ZRot>>>
-      windows;
-  // Their device copy, appended as batches meet new windows: (w, s) per
-  // rotation, the offset of each window's table, and how much is uploaded.
-  std::vector<float2> rot_all;
-  std::map<const void*, int32_t> rot_offsets;
-  csm::DevBuf rot_dev;
-  size_t rot_uploaded = 0;
+namespace csm {
+// Call contexts (csm_context::call_free): taken for one single Match call,
+// returned with its timing added to the owner's.
+csm_context* AcquireCallContext(csm_context* owner);
+void ReleaseCallContext(csm_context* owner, csm_context* c);
+class CallContext {
+ public:
+  explicit CallContext(csm_context* owner) : owner_(owner), c_(AcquireCallContext(owner)) {}
+  ~CallContext() { ReleaseCallContext(owner_, c_); }
+  CallContext(const CallContext&) = delete;
+  CallContext& operator=(const CallContext&) = delete;
+  csm_context* get() const { return c_; }
+
+ private:
+  csm_context* owner_;
+  csm_context* c_;
 };
+}  // namespace csm
 
 // A HybridGrid on the device (host3d.cc builds it).
 struct csm_hybrid_grid {

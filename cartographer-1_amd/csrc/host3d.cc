@@ -1023,8 +1023,10 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
                            int64_t num_pairs, csm_result3d* results) {
   if (!ctx || num_pairs < 0 || (num_pairs > 0 && (!pairs || !results || !submaps || !nodes)))
     return CSM_EINVAL;
+  // Matchers from any context on ctx's device (e.g. a single call's call
+  // context searching its creator's matcher): their pyramids are read-only.
   for (int i = 0; i < num_submaps; ++i)
-    if (!submaps[i] || submaps[i]->ctx != ctx) return CSM_EINVAL;
+    if (!submaps[i] || submaps[i]->ctx->device != ctx->device) return CSM_EINVAL;
   using Clock = std::chrono::steady_clock;
   const bool prof3 = std::getenv("CSM_PROFILE3D") != nullptr;
   auto ht = Clock::now();
@@ -1452,7 +1454,9 @@ int csm_fast3d_match(const csm_fast3d* m, const csm_pose3d* node_pose,
   p.node_pose = *node_pose;
   p.submap_pose = *submap_pose;
   csm_fast3d* h = const_cast<csm_fast3d*>(m);
-  const int rc = csm_fast3d_match_batch(m->ctx, &h, 1, node, 1, &p, 1, result);
+  csm::CallContext cc(m->ctx);  // this call's stream and scratch (csm_internal.h)
+  if (!cc.get()) return CSM_EHIP;
+  const int rc = csm_fast3d_match_batch(cc.get(), &h, 1, node, 1, &p, 1, result);
   if (rc < 0) return rc;
   return result->status;
 }
@@ -1469,7 +1473,9 @@ int csm_fast3d_match_full_submap(const csm_fast3d* m, const double* node_rotatio
     p.submap_pose.q[k] = submap_rotation[k];
   }
   csm_fast3d* h = const_cast<csm_fast3d*>(m);
-  const int rc = csm_fast3d_match_batch(m->ctx, &h, 1, node, 1, &p, 1, result);
+  csm::CallContext cc(m->ctx);  // this call's stream and scratch (csm_internal.h)
+  if (!cc.get()) return CSM_EHIP;
+  const int rc = csm_fast3d_match_batch(cc.get(), &h, 1, node, 1, &p, 1, result);
   if (rc < 0) return rc;
   return result->status;
 }

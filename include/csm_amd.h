@@ -107,6 +107,13 @@ typedef struct csm_timing {
    * tied (counted whether or not timing is enabled). */
   int64_t tied_pairs;
   int64_t ties_unresolved;
+  /* Of tied_pairs: those whose pick needed the whole lowest-resolution list
+   * ordered (CSM_TIE_TOPLIST); the rest are CSM_TIE_ANCESTORS. 3D: pairs
+   * whose best sum was reached by more than one leaf, and those resolved
+   * past the device's first pick (csm_result3d.tie). */
+  int64_t ties_toplist;
+  int64_t tied_pairs_3d;
+  int64_t ties_unresolved_3d;
 } csm_timing;
 void csm_context_enable_timing(csm_context* ctx, int32_t enable);
 void csm_context_get_timing(csm_context* ctx, csm_timing* out);
@@ -179,10 +186,29 @@ typedef struct csm_pair2d {
   csm_pose2d initial;  /* used when full_submap == 0 */
 } csm_pair2d;
 
+/* How a result was picked among exactly tied maxima (csm_result2d.tie;
+ * DESIGN.md §2 "Exactly tied maxima"). The reference returns the first
+ * maximal leaf its depth-first search visits
+ * (fast_correlative_scan_matcher_2d.cc:276-312, :331-332, :344-376):
+ *   NONE       one leaf reaches the maximum;
+ *   ANCESTORS  several do, all under one highest-scoring lowest-resolution
+ *              candidate: the pick follows the children's visiting order;
+ *   TOPLIST    two distinct lowest-resolution candidates share the highest
+ *              score: the pair's whole lowest-resolution list was scored and
+ *              ordered with std::sort's introsort to find the first;
+ *   UNRESOLVED more than 4096 tied leaves: the smallest (rotation, x, y) leaf
+ *              is returned (same score; never seen in any test or bench). */
+#define CSM_TIE_NONE 0
+#define CSM_TIE_ANCESTORS 1
+#define CSM_TIE_TOPLIST 2
+#define CSM_TIE_UNRESOLVED 3
+
 typedef struct csm_result2d {
   int32_t status;      /* CSM_OK, CSM_NO_MATCH or a negative error */
   float score;
   csm_pose2d pose;
+  int32_t tie;         /* CSM_TIE_* (CSM_OK results only) */
+  int32_t reserved;
 } csm_result2d;
 
 /* The submap handles may come from any context on ctx's device (e.g. one
