@@ -222,6 +222,9 @@ _SIGNATURES = {
     "csm_fast2d_match_full_submap": (C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.c_int32,
                                                C.c_float, C.POINTER(C.c_float),
                                                C.POINTER(Pose2D)]),
+    "csm_fast2d_device_bytes": (C.c_int64, [C.c_void_p]),
+    "csm_fast3d_device_bytes": (C.c_int64, [C.c_void_p]),
+    "csm_hybrid_grid_device_bytes": (C.c_int64, [C.c_void_p]),
     "csm_fast2d_read_level": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_uint8), C.c_int64,
                                         C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "csm_scan_set_create": (C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_int64),
@@ -738,6 +741,10 @@ class FastCorrelativeScanMatcher2D:
             self.handle, _ptr(pts, C.c_float), len(pts), min_score, C.byref(score),
             C.byref(pose)), "csm_fast2d_match_full_submap")
         return rc == CSM_OK, float(score.value), pose.as_tuple()
+
+    def device_bytes(self) -> int:
+        """Device memory the matcher holds (csm_fast2d_device_bytes)."""
+        return int(self._lib.csm_fast2d_device_bytes(self.handle))
 
     def read_level(self, level: int) -> np.ndarray:
         """PrecomputationGrid2D level as (wide_ny, wide_nx) uint8."""

@@ -1185,6 +1185,10 @@ void csm_fast2d_destroy(csm_fast2d* m) {
   delete m;
 }
 
+int64_t csm_fast2d_device_bytes(const csm_fast2d* m) {
+  return m ? static_cast<int64_t>(m->pyramid.bytes + m->cost.bytes) : 0;
+}
+
 int csm_fast2d_read_level(const csm_fast2d* m, int32_t level, uint8_t* out,
                           int64_t capacity, int32_t* wide_nx, int32_t* wide_ny) {
   if (!m || level < 0 || level >= m->desc.levels || !wide_nx || !wide_ny) return CSM_EINVAL;

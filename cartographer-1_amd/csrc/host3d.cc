@@ -749,6 +749,16 @@ int csm_fast3d_create(csm_context* ctx, const csm_hybrid_grid* high, const csm_h
   return CSM_OK;
 }
 
+int64_t csm_fast3d_device_bytes(const csm_fast3d* m) {
+  return m ? static_cast<int64_t>(m->levels.bytes + m->octs.bytes) : 0;
+}
+
+int64_t csm_hybrid_grid_device_bytes(const csm_hybrid_grid* g) {
+  return g ? static_cast<int64_t>(g->values.bytes + g->prob.bytes + g->prob_pad.bytes +
+                                  g->prob_wide.bytes + g->prob_col.bytes)
+           : 0;
+}
+
 void csm_fast3d_destroy(csm_fast3d* m) {
   if (!m) return;
   (void)hipSetDevice(m->ctx->device);

@@ -44,6 +44,10 @@ class HybridGrid:
                "csm_hybrid_grid_create")
         self.handle = h
 
+    def device_bytes(self) -> int:
+        """Device memory of the grid's bricks (csm_hybrid_grid_device_bytes)."""
+        return int(self._lib.csm_hybrid_grid_device_bytes(self.handle))
+
     def info(self):
         o, d, g = (C.c_int32 * 3)(), (C.c_int32 * 3)(), C.c_int32()
         _check(self._lib.csm_hybrid_grid_info(self.handle, o, d, C.byref(g)), "csm_hybrid_grid_info")
@@ -247,6 +251,10 @@ class FastCorrelativeScanMatcher3D:
             self.close()
         except Exception:
             pass
+
+    def device_bytes(self) -> int:
+        """Device memory of the pyramid (csm_fast3d_device_bytes)."""
+        return int(self._lib.csm_fast3d_device_bytes(self.handle))
 
     def read_level(self, level: int):
         o, d = (C.c_int32 * 3)(), (C.c_int32 * 3)()

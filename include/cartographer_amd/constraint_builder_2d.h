@@ -14,6 +14,14 @@
 // csm_ceres2d_refine_batch, parity with Ceres unpinned) unless
 // options.refine_with_ceres is off.
 //
+// Lifetimes: the Submap2DView and PointCloud passed to MaybeAdd* must stay
+// valid (and unchanged) until the flush that searches the pair — the next
+// NotifyEndOfNode that flushes, or WhenDone — as the reference's tasks read
+// them until they run. Matchers are built from the view when the pair is
+// enqueued (kStatic) or searched (kClaim, or after the budgeted matcher cache
+// dropped the submap's matcher: options.matcher_cache_bytes, MatcherCache).
+// DeleteScanMatcher drops the submap's pending pairs.
+//
 // Multi-GPU (set_communicator): every rank makes the same calls; a rank
 // searches only the pairs of the submaps it owns (ShardOwner, Sharding::kStatic)
 // or the chunks of each flush it claims (Sharding::kClaim) on its own device,
@@ -24,6 +32,7 @@
 #ifndef CARTOGRAPHER_AMD_CONSTRAINT_BUILDER_2D_H_
 #define CARTOGRAPHER_AMD_CONSTRAINT_BUILDER_2D_H_
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <functional>
@@ -70,7 +79,9 @@ class ConstraintBuilder2D {
 
   explicit ConstraintBuilder2D(const ConstraintBuilderOptions& options,
                                csm_context* context = nullptr)
-      : options_(options), context_(context ? context : ThreadContext()) {}
+      : options_(options),
+        context_(context ? context : ThreadContext()),
+        matchers_(options.matcher_cache_bytes) {}
 
   ~ConstraintBuilder2D() {
     if (scans_) csm_scan_set_destroy(scans_);
@@ -125,10 +136,31 @@ class ConstraintBuilder2D {
 
   int GetNumFinishedNodes() const { return num_finished_nodes_; }
 
+  // Also drops the submap's pairs still pending (they yield no constraint):
+  // the reference's tasks would read the deleted matcher, and a pending pair
+  // must not make the builder rebuild it from a submap the caller is trimming.
   void DeleteScanMatcher(const SubmapId& submap_id) {
-    matchers_.erase(submap_id);
+    matchers_.Erase(submap_id);
     samplers_.erase(submap_id);
+    const size_t before = pending_.size();
+    pending_.erase(std::remove_if(pending_.begin(), pending_.end(),
+                                  [&](const Pending& p) {
+                                    return !(p.submap_id < submap_id) &&
+                                           !(submap_id < p.submap_id);
+                                  }),
+                   pending_.end());
+    if (pending_.size() != before)
+      std::fprintf(stderr,
+                   "ConstraintBuilder2D: DeleteScanMatcher dropped %zu pending pairs of a "
+                   "deleted submap\n",
+                   before - pending_.size());
   }
+
+  // kNumSubmapScanMatchersMetric, and the cache's device bytes and churn.
+  int num_submap_scan_matchers() const { return static_cast<int>(matchers_.size()); }
+  int64_t matcher_cache_bytes() const { return matchers_.bytes(); }
+  int64_t matcher_builds() const { return matchers_.builds; }
+  int64_t matcher_evictions() const { return matchers_.evictions; }
 
   // Metrics (constraint_builder_2d.cc:46-53).
   int64_t constraints_searched = 0, constraints_found = 0;
@@ -160,12 +192,17 @@ class ConstraintBuilder2D {
                csm_comm_rank(comm_);
   }
 
-  // DispatchScanMatcherConstruction (constraint_builder_2d.cc:165-186).
-  void EnsureMatcher(const SubmapId& submap_id, const Submap2DView* submap) {
-    if (!matchers_.count(submap_id))
-      matchers_.emplace(submap_id, std::make_shared<FastCorrelativeScanMatcher2D>(
-                                       submap->grid, options_.fast_correlative_scan_matcher_options,
-                                       context_));
+  // DispatchScanMatcherConstruction (constraint_builder_2d.cc:165-186), through
+  // the budgeted cache (a dropped matcher is rebuilt from the submap's grid).
+  std::shared_ptr<FastCorrelativeScanMatcher2D> EnsureMatcher(const SubmapId& submap_id,
+                                                              const Submap2DView* submap) {
+    return matchers_.Get(
+        submap_id,
+        [&] {
+          return std::make_shared<FastCorrelativeScanMatcher2D>(
+              submap->grid, options_.fast_correlative_scan_matcher_options, context_);
+        },
+        [](const FastCorrelativeScanMatcher2D& m) { return m.device_bytes(); });
   }
 
   // Rank 0 receives every rank's accepted constraints in slot order; the
@@ -246,16 +283,33 @@ class ConstraintBuilder2D {
     num_finished_nodes_ = num_started_nodes_;
   }
 
-  // Searches (and refines) pending_[which] as one batch.
   // Device index of every pending_[which_pending[k]]'s cloud in scans_, which
   // keeps node clouds resident across flushes: clouds not seen before (or a
   // node whose cloud changed) are appended in one upload.
+  // A cached cloud is reused only if it is the same PointCloud with the same
+  // size and content hash, so a caller refilling one PointCloud object for a
+  // node is uploaded again (the Python mirror compares the points).
+  static uint64_t CloudHash(const PointCloud& c) {
+    uint64_t h = 1469598103934665603ull;  // FNV-1a over the float bytes
+    const unsigned char* b = reinterpret_cast<const unsigned char*>(c.xyz.data());
+    for (size_t i = 0, n = c.xyz.size() * sizeof(float); i < n; ++i) h = (h ^ b[i]) * 1099511628211ull;
+    return h;
+  }
   std::vector<int32_t> ResidentScans(const std::vector<size_t>& which_pending) {
+    std::map<const PointCloud*, uint64_t> hashes;
+    auto hash_of = [&](const PointCloud* c) {
+      auto it = hashes.find(c);
+      if (it == hashes.end()) it = hashes.emplace(c, CloudHash(*c)).first;
+      return it->second;
+    };
+    auto stale = [&](const CachedScan& c, const PointCloud* cloud) {
+      return c.index == kUnset || c.cloud != cloud || c.size != cloud->size() ||
+             c.hash != hash_of(cloud);
+    };
     int64_t fresh_points = 0;
     for (size_t i : which_pending) {
       auto c = scan_cache_.find(pending_[i].node_id);
-      if (c == scan_cache_.end() || c->second.cloud != pending_[i].cloud ||
-          c->second.size != pending_[i].cloud->size())
+      if (c == scan_cache_.end() || stale(c->second, pending_[i].cloud))
         fresh_points += static_cast<int64_t>(pending_[i].cloud->size());
     }
     if (scans_ && cached_points_ + fresh_points > options_.scan_cache_points) {
@@ -275,9 +329,10 @@ class ConstraintBuilder2D {
     for (size_t i : which_pending) {
       const Pending& p = pending_[i];
       CachedScan& c = scan_cache_[p.node_id];
-      if (c.cloud != p.cloud || c.size != p.cloud->size() || c.index == kUnset) {
+      if (stale(c, p.cloud)) {
         c.cloud = p.cloud;
         c.size = p.cloud->size();
+        c.hash = hash_of(p.cloud);
         c.index = -static_cast<int32_t>(offsets.size());
         fresh.push_back(&c);
         xyz.insert(xyz.end(), p.cloud->xyz.begin(), p.cloud->xyz.end());
@@ -298,21 +353,54 @@ class ConstraintBuilder2D {
     return index;
   }
 
+  // Cuts pending_[which] into sub-batches whose matchers fit the matcher
+  // cache's budget together (one batch when unbounded or when they fit),
+  // whole submaps per sub-batch, and searches each.
   void Search(const std::vector<size_t>& which_pending) {
+    std::vector<size_t> order(which_pending);
+    if (matchers_.bounded())
+      std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) {
+        return pending_[a].submap_id < pending_[b].submap_id;
+      });
+    std::vector<size_t> part;
+    Held held;
+    int64_t held_bytes = 0;
+    for (size_t i : order) {
+      const Pending& p = pending_[i];
+      if (!held.count(p.submap_id)) {
+        auto m = EnsureMatcher(p.submap_id, p.submap);
+        const int64_t b = m->device_bytes();
+        if (!part.empty() && matchers_.bounded() && held_bytes + b > matchers_.budget()) {
+          SearchBatch(part, held);
+          part.clear();
+          held.clear();
+          held_bytes = 0;
+          matchers_.Trim();  // the searched part's matchers are no longer held
+        }
+        held.emplace(p.submap_id, std::move(m));
+        held_bytes += b;
+      }
+      part.push_back(i);
+    }
+    if (!part.empty()) SearchBatch(part, held);
+    held.clear();
+    matchers_.Trim();
+  }
+
+  using Held = std::map<SubmapId, std::shared_ptr<FastCorrelativeScanMatcher2D>>;
+
+  // Searches (and refines) pending_[which] as one batch over `held`'s matchers.
+  void SearchBatch(const std::vector<size_t>& which_pending, const Held& held) {
     const std::vector<int32_t> scan_index = ResidentScans(which_pending);
     std::vector<csm_fast2d*> handles;
     std::map<SubmapId, int> slot_of;
     std::vector<csm_pair2d> pairs;
-    std::vector<std::shared_ptr<FastCorrelativeScanMatcher2D>> keep;
     for (size_t k = 0; k < which_pending.size(); ++k) {
       const Pending& p = pending_[which_pending[k]];
-      EnsureMatcher(p.submap_id, p.submap);
-      auto m = matchers_.at(p.submap_id);
       auto s = slot_of.find(p.submap_id);
       if (s == slot_of.end()) {
         s = slot_of.emplace(p.submap_id, static_cast<int>(handles.size())).first;
-        handles.push_back(m->handle());
-        keep.push_back(m);
+        handles.push_back(held.at(p.submap_id)->handle());
       }
       csm_pair2d q{};
       q.submap = s->second;
@@ -381,13 +469,14 @@ class ConstraintBuilder2D {
 
   ConstraintBuilderOptions options_;
   csm_context* context_;
-  std::map<SubmapId, std::shared_ptr<FastCorrelativeScanMatcher2D>> matchers_;
+  MatcherCache<FastCorrelativeScanMatcher2D> matchers_;
   std::map<SubmapId, FixedRatioSampler> samplers_;
   std::vector<std::unique_ptr<Constraint>> constraints_;
   std::vector<Pending> pending_;
   struct CachedScan {
     const PointCloud* cloud = nullptr;
     size_t size = 0;
+    uint64_t hash = 0;
     int32_t index = kUnset;
   };
   static constexpr int32_t kUnset = INT32_MIN;

@@ -16,6 +16,10 @@
 // csm_ceres3d_refine_batch, parity with Ceres unpinned) unless
 // options.refine_with_ceres is off.
 //
+// Lifetimes as ConstraintBuilder2D: a Submap3DView and a node's data must stay
+// valid until the flush that searches the pair (matchers may be built, or
+// rebuilt after the budgeted cache dropped them, at that flush).
+//
 // Multi-GPU (set_communicator), as ConstraintBuilder2D: every rank makes the
 // same calls; a rank builds matchers for and searches only the submaps it
 // owns (ShardOwner, Sharding::kStatic) or the chunks of each flush it claims
@@ -28,6 +32,7 @@
 #ifndef CARTOGRAPHER_AMD_CONSTRAINT_BUILDER_3D_H_
 #define CARTOGRAPHER_AMD_CONSTRAINT_BUILDER_3D_H_
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <functional>
@@ -66,7 +71,9 @@ class ConstraintBuilder3D {
 
   explicit ConstraintBuilder3D(const ConstraintBuilderOptions& options,
                                csm_context* context = nullptr)
-      : options_(options), context_(context ? context : ThreadContext()) {}
+      : options_(options),
+        context_(context ? context : ThreadContext()),
+        matchers_(options.matcher_cache_bytes) {}
 
   // Shards the search over the ranks of `comm` (not owned; outlives the
   // builder). Call before the first MaybeAdd*. kClaim needs
@@ -127,9 +134,23 @@ class ConstraintBuilder3D {
 
   int GetNumFinishedNodes() const { return num_finished_nodes_; }
 
+  // Also drops the submap's pairs still pending (no constraint; see
+  // ConstraintBuilder2D::DeleteScanMatcher).
   void DeleteScanMatcher(const SubmapId& submap_id) {
-    matchers_.erase(submap_id);
+    matchers_.Erase(submap_id);
     samplers_.erase(submap_id);
+    const size_t before = pending_.size();
+    pending_.erase(std::remove_if(pending_.begin(), pending_.end(),
+                                  [&](const Pending& p) {
+                                    return !(p.submap_id < submap_id) &&
+                                           !(submap_id < p.submap_id);
+                                  }),
+                   pending_.end());
+    if (pending_.size() != before)
+      std::fprintf(stderr,
+                   "ConstraintBuilder3D: DeleteScanMatcher dropped %zu pending pairs of a "
+                   "deleted submap\n",
+                   before - pending_.size());
   }
 
   // Metrics (constraint_builder_3d.cc:46-59).
@@ -144,6 +165,9 @@ class ConstraintBuilder3D {
   std::vector<float> constraint_scores, global_constraint_scores;
   std::vector<float> rotational_scores, low_resolution_scores;
   int num_submap_scan_matchers() const { return static_cast<int>(matchers_.size()); }
+  int64_t matcher_cache_bytes() const { return matchers_.bytes(); }
+  int64_t matcher_builds() const { return matchers_.builds; }
+  int64_t matcher_evictions() const { return matchers_.evictions; }
 
  private:
   // SubmapScanMatcher (constraint_builder_3d.h:117-123): device grids and the
@@ -151,6 +175,9 @@ class ConstraintBuilder3D {
   struct SubmapScanMatcher {
     std::unique_ptr<HybridGrid3D> high, low;
     std::unique_ptr<FastCorrelativeScanMatcher3D> matcher;
+    int64_t device_bytes() const {
+      return high->device_bytes() + low->device_bytes() + matcher->device_bytes();
+    }
   };
 
   struct Pending {
@@ -242,15 +269,22 @@ class ConstraintBuilder3D {
   }
 
   // DispatchScanMatcherConstruction (constraint_builder_3d.cc:170-198).
-  void EnsureMatcher(const SubmapId& submap_id, const Submap3DView* submap) {
-    if (matchers_.count(submap_id)) return;
-    auto m = std::make_shared<SubmapScanMatcher>();
-    m->high.reset(new HybridGrid3D(submap->high_resolution_hybrid_grid, context_));
-    m->low.reset(new HybridGrid3D(submap->low_resolution_hybrid_grid, context_));
-    m->matcher.reset(new FastCorrelativeScanMatcher3D(
-        *m->high, m->low.get(), &submap->rotational_scan_matcher_histogram,
-        options_.fast_correlative_scan_matcher_options_3d, context_));
-    matchers_.emplace(submap_id, std::move(m));
+  // Through the budgeted cache (MatcherCache): a dropped matcher is rebuilt
+  // from the submap's grids and histogram on its next use.
+  std::shared_ptr<SubmapScanMatcher> EnsureMatcher(const SubmapId& submap_id,
+                                                   const Submap3DView* submap) {
+    return matchers_.Get(
+        submap_id,
+        [&] {
+          auto m = std::make_shared<SubmapScanMatcher>();
+          m->high.reset(new HybridGrid3D(submap->high_resolution_hybrid_grid, context_));
+          m->low.reset(new HybridGrid3D(submap->low_resolution_hybrid_grid, context_));
+          m->matcher.reset(new FastCorrelativeScanMatcher3D(
+              *m->high, m->low.get(), &submap->rotational_scan_matcher_histogram,
+              options_.fast_correlative_scan_matcher_options_3d, context_));
+          return m;
+        },
+        [](const SubmapScanMatcher& m) { return m.device_bytes(); });
   }
 
   void Flush() {
@@ -273,10 +307,44 @@ class ConstraintBuilder3D {
     num_finished_nodes_ = num_started_nodes_;
   }
 
-  // Searches (and refines) pending_[which] as one batch.
+  // Sub-batches whose matchers fit the cache budget together (as
+  // ConstraintBuilder2D::Search), each searched and refined as one batch.
   void Search(const std::vector<size_t>& which_pending) {
+    std::vector<size_t> order(which_pending);
+    if (matchers_.bounded())
+      std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) {
+        return pending_[a].submap_id < pending_[b].submap_id;
+      });
+    std::vector<size_t> part;
+    std::map<SubmapId, std::shared_ptr<SubmapScanMatcher>> held;
+    int64_t held_bytes = 0;
+    for (size_t i : order) {
+      const Pending& p = pending_[i];
+      if (!held.count(p.submap_id)) {
+        auto m = EnsureMatcher(p.submap_id, p.submap);
+        const int64_t b = m->device_bytes();
+        if (!part.empty() && matchers_.bounded() && held_bytes + b > matchers_.budget()) {
+          SearchBatch(part, held);
+          part.clear();
+          held.clear();
+          held_bytes = 0;
+          matchers_.Trim();  // the searched part's matchers are no longer held
+        }
+        held.emplace(p.submap_id, std::move(m));
+        held_bytes += b;
+      }
+      part.push_back(i);
+    }
+    if (!part.empty()) SearchBatch(part, held);
+    held.clear();
+    matchers_.Trim();
+  }
+
+  // Searches (and refines) pending_[which] as one batch over `held`'s matchers.
+  void SearchBatch(const std::vector<size_t>& which_pending,
+                   const std::map<SubmapId, std::shared_ptr<SubmapScanMatcher>>& held) {
     std::vector<csm_fast3d*> handles;
-    std::vector<std::shared_ptr<SubmapScanMatcher>> keep;
+    std::vector<const SubmapScanMatcher*> keep;
     std::map<SubmapId, int> slot_of;
     std::map<const TrajectoryNodeData3D*, int32_t> node_of;  // a node's data uploads once
     std::vector<csm_node3d> nodes;
@@ -286,8 +354,7 @@ class ConstraintBuilder3D {
       auto s = slot_of.find(p.submap_id);
       if (s == slot_of.end()) {
         s = slot_of.emplace(p.submap_id, static_cast<int>(handles.size())).first;
-        EnsureMatcher(p.submap_id, p.submap);
-        auto m = matchers_.at(p.submap_id);
+        const SubmapScanMatcher* m = held.at(p.submap_id).get();
         handles.push_back(m->matcher->handle());
         keep.push_back(m);
       }
@@ -376,7 +443,7 @@ class ConstraintBuilder3D {
 
   ConstraintBuilderOptions options_;
   csm_context* context_;
-  std::map<SubmapId, std::shared_ptr<SubmapScanMatcher>> matchers_;
+  MatcherCache<SubmapScanMatcher> matchers_;
   std::map<SubmapId, FixedRatioSampler> samplers_;
   std::vector<std::unique_ptr<Constraint3D>> constraints_;
   std::vector<Pending> pending_;

@@ -6,6 +6,9 @@
 #define CARTOGRAPHER_AMD_CONSTRAINT_BUILDER_COMMON_H_
 
 #include <cstdint>
+#include <list>
+#include <map>
+#include <memory>
 
 #include "scan_matching.h"
 #include "scan_matching_3d.h"
@@ -48,6 +51,85 @@ struct ConstraintBuilderOptions {
   // Node clouds stay on the device across flushes (a node's cloud is uploaded
   // once); past this many resident points the 2D builder starts a new set.
   int64_t scan_cache_points = int64_t{1} << 25;
+  // Device memory the per-submap matcher cache may hold (MatcherCache below;
+  // 0 = unbounded, the reference's behaviour: it keeps every matcher until
+  // DeleteScanMatcher, constraint_builder_2d.cc:165-186, :307-316). A 400x400
+  // 2D submap's matcher holds ~25 MB, so the default keeps ~1300 of them.
+  int64_t matcher_cache_bytes = int64_t{32} << 30;
+};
+
+// The per-submap matcher cache (DispatchScanMatcherConstruction,
+// constraint_builder_2d.cc:165-186) under a device-memory budget: least
+// recently used matchers are dropped once the cached ones hold more than
+// `budget` bytes, and rebuilt from the submap on their next use (a 2D build is
+// ~0.1 ms of device time). A matcher some batch still holds (a shared_ptr
+// besides the cache's) is never dropped, so a batch's matchers stay valid;
+// the builders cut a flush into sub-batches whose matchers fit the budget.
+template <typename M>
+class MatcherCache {
+ public:
+  explicit MatcherCache(int64_t budget) : budget_(budget) {}
+
+  bool Contains(const SubmapId& id) const { return map_.count(id) != 0; }
+  size_t size() const { return map_.size(); }
+  int64_t bytes() const { return bytes_; }
+  int64_t budget() const { return budget_; }
+  bool bounded() const { return budget_ > 0; }
+
+  // The cached matcher (now the most recent), or make() -> shared_ptr<M>
+  // inserted with its device bytes (bytes_of(const M&)).
+  template <typename Make, typename Bytes>
+  std::shared_ptr<M> Get(const SubmapId& id, Make&& make, Bytes&& bytes_of) {
+    auto it = map_.find(id);
+    if (it != map_.end()) {
+      lru_.splice(lru_.begin(), lru_, it->second.pos);
+      return it->second.m;
+    }
+    std::shared_ptr<M> m = make();
+    ++builds;
+    const int64_t b = bytes_of(*m);
+    lru_.push_front(id);
+    map_.emplace(id, Entry{m, b, lru_.begin()});
+    bytes_ += b;
+    Trim();
+    return m;
+  }
+
+  void Erase(const SubmapId& id) {
+    auto it = map_.find(id);
+    if (it == map_.end()) return;
+    bytes_ -= it->second.bytes;
+    lru_.erase(it->second.pos);
+    map_.erase(it);
+  }
+
+  int64_t builds = 0, evictions = 0;
+
+  // Drops least recently used matchers no batch holds until the cache is
+  // within its budget (Get does this after every build).
+  void Trim() {
+    if (budget_ <= 0) return;
+    for (auto p = lru_.end(); bytes_ > budget_ && p != lru_.begin();) {
+      --p;
+      auto it = map_.find(*p);
+      if (it->second.m.use_count() > 1) continue;  // held by a batch
+      bytes_ -= it->second.bytes;
+      map_.erase(it);
+      p = lru_.erase(p);
+      ++evictions;
+    }
+  }
+
+ private:
+  struct Entry {
+    std::shared_ptr<M> m;
+    int64_t bytes;
+    std::list<SubmapId>::iterator pos;
+  };
+  std::map<SubmapId, Entry> map_;
+  std::list<SubmapId> lru_;  // most recent first
+  int64_t bytes_ = 0;
+  int64_t budget_;
 };
 
 // common/fixed_ratio_sampler.cc:32-39

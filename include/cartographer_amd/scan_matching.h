@@ -135,6 +135,7 @@ class FastCorrelativeScanMatcher2D {
   }
 
   csm_fast2d* handle() const { return handle_; }
+  int64_t device_bytes() const { return csm_fast2d_device_bytes(handle_); }
 
  private:
   csm_fast2d* handle_ = nullptr;

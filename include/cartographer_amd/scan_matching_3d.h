@@ -74,6 +74,7 @@ class HybridGrid3D {
   HybridGrid3D(const HybridGrid3D&) = delete;
   HybridGrid3D& operator=(const HybridGrid3D&) = delete;
   const csm_hybrid_grid* handle() const { return handle_; }
+  int64_t device_bytes() const { return csm_hybrid_grid_device_bytes(handle_); }
 
  private:
   csm_hybrid_grid* handle_ = nullptr;
@@ -177,6 +178,7 @@ class FastCorrelativeScanMatcher3D {
   }
 
   csm_fast3d* handle() const { return handle_; }
+  int64_t device_bytes() const { return csm_fast3d_device_bytes(handle_); }
 
   static std::unique_ptr<Result> Convert(int rc, const csm_result3d& r) {
     if (rc != CSM_OK || r.status != CSM_OK) return nullptr;

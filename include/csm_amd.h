@@ -12,10 +12,16 @@
  * violations; the C++ shim (include/cartographer_amd/scan_matching.h) turns
  * negative codes into aborts to keep those semantics.
  *
- * Threading: handles are re-entrant for concurrent match calls (the reference
- * calls const Match methods concurrently from ThreadPool workers,
- * constraint_builder_2d.cc:100-111); each call serialises on its context's
- * stream. Use one context per calling thread for concurrency.
+ * Threading: matcher handles are re-entrant for concurrent match calls (the
+ * reference calls const Match methods concurrently from ThreadPool workers,
+ * constraint_builder_2d.cc:100-111). A single Match / MatchFullSubmap call
+ * (csm_fast2d_match*, csm_fast3d_match*) takes a call context from a pool on
+ * the matcher's context for its duration: its own HIP stream and scratch,
+ * the matcher's device pyramid shared read-only, so concurrent callers'
+ * searches overlap on the GPU. Calls that name a context (batches, RTCSM,
+ * filters, refinement) serialise on that context's stream; use one context
+ * per calling thread to run those concurrently. Destroying a handle while a
+ * call uses it is the caller's error, as in the reference.
  */
 #ifndef CSM_AMD_H_
 #define CSM_AMD_H_
@@ -152,6 +158,12 @@ int csm_fast2d_match(const csm_fast2d* m, const csm_pose2d* initial,
 int csm_fast2d_match_full_submap(const csm_fast2d* m, const float* points_xyz,
                                  int32_t n, float min_score, float* score,
                                  csm_pose2d* pose);
+
+/* Device bytes a matcher holds (its pyramid planes and cost grid), for a
+ * caller's cache budget (the drop-in builders' matcher_cache_bytes; the
+ * reference keeps every matcher until DeleteScanMatcher,
+ * constraint_builder_2d.cc:165-186, :307-316). */
+int64_t csm_fast2d_device_bytes(const csm_fast2d* m);
 
 /* Test-visible: copies PrecomputationGrid2D level `level` (uint8 wide grid,
  * fast_correlative_scan_matcher_2d.h:49-93) to host. */
@@ -403,6 +415,10 @@ int csm_fast3d_create(csm_context* ctx, const csm_hybrid_grid* high_resolution,
                       int32_t histogram_size, const csm_fast3d_options* options,
                       csm_fast3d** out);
 void csm_fast3d_destroy(csm_fast3d* m);
+/* Device bytes of the matcher's pyramid (levels and octet planes), and of a
+ * HybridGrid's bricks (as csm_fast2d_device_bytes). */
+int64_t csm_fast3d_device_bytes(const csm_fast3d* m);
+int64_t csm_hybrid_grid_device_bytes(const csm_hybrid_grid* g);
 /* Test-visible: copies pyramid level `level` (dense brick, x fastest). */
 int csm_fast3d_read_level(const csm_fast3d* m, int32_t level, uint8_t* out, int64_t capacity,
                           int32_t* origin3, int32_t* dims3);

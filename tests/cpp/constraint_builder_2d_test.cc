@@ -156,11 +156,117 @@ static void ReusesResidentCloudsAcrossFlushes() {
          r2[1].relative_pose.y == r1[0].relative_pose.y);
 }
 
+// Submaps with an L of occupied cells at a per-submap offset, and the L's
+// points (submap 0's cell centres) as a cloud.
+struct LWorld {
+  std::vector<std::vector<uint16_t>> cells;
+  std::vector<Submap2DView> submaps;
+  PointCloud cloud;
+  explicit LWorld(int n) : cells(n), submaps(n) {
+    for (int s = 0; s < n; ++s) {
+      cells[s].assign(100 * 110, 0);
+      const int ox = s % 7, oy = (s / 7) % 5;
+      for (int x = 10; x <= 14 + s % 3; ++x) cells[s][(20 + oy) * 100 + x + ox] = 1;
+      for (int y = 21; y <= 23 + s % 4; ++y) cells[s][(y + oy) * 100 + 10 + ox] = 1;
+      Submap2DView& v = submaps[s];
+      v.grid.resolution = 1.;
+      v.grid.max_x = 2.;
+      v.grid.max_y = 3.;
+      v.grid.num_x_cells = 100;
+      v.grid.num_y_cells = 110;
+      v.grid.cells = cells[s].data();
+      v.local_pose = Rigid2d{0.5 * s, -0.25 * s, 0.01 * s};
+    }
+    for (int x = 10; x <= 14; ++x) cloud.push_back(2.f - 20.5f, 3.f - (x + 0.5f), 0.f);
+    for (int y = 21; y <= 23; ++y) cloud.push_back(2.f - (y + 0.5f), 3.f - 10.5f, 0.f);
+  }
+};
+
+static ConstraintBuilder2D::Result Sweep(ConstraintBuilder2D* b, LWorld* w, int nodes) {
+  ConstraintBuilder2D::Result all;
+  for (int n = 0; n < nodes; ++n) {
+    for (size_t s = 0; s < w->submaps.size(); ++s)
+      b->MaybeAddGlobalConstraint(SubmapId{0, static_cast<int>(s)}, &w->submaps[s], NodeId{0, n},
+                                  &w->cloud);
+    b->NotifyEndOfNode();
+  }
+  b->WhenDone([&](const ConstraintBuilder2D::Result& r) { all = r; });
+  return all;
+}
+
+// The matcher cache under a device budget of 5 matchers: LRU matchers are
+// dropped and rebuilt, each flush is cut into sub-batches that fit, and the
+// constraints are the unbounded builder's, in the same order.
+static void BudgetedMatcherCache() {
+  LWorld w(40);
+  ConstraintBuilderOptions unbounded = TestOptions();
+  unbounded.matcher_cache_bytes = 0;
+  ConstraintBuilder2D ref(unbounded);
+  const ConstraintBuilder2D::Result expected = Sweep(&ref, &w, 3);
+  EXPECT(ref.num_submap_scan_matchers() == 40 && ref.matcher_evictions() == 0);
+  const int64_t one = ref.matcher_cache_bytes() / 40;
+  ConstraintBuilderOptions small = TestOptions();
+  small.matcher_cache_bytes = 5 * one;
+  ConstraintBuilder2D b(small);
+  const ConstraintBuilder2D::Result got = Sweep(&b, &w, 3);
+  EXPECT(b.matcher_evictions() > 0 && b.matcher_builds() > 40);
+  EXPECT(b.matcher_cache_bytes() <= 5 * one && b.num_submap_scan_matchers() <= 5);
+  EXPECT(got.size() == expected.size() && !got.empty());
+  for (size_t k = 0; k < got.size() && k < expected.size(); ++k) {
+    EXPECT(got[k].submap_id.submap_index == expected[k].submap_id.submap_index &&
+           got[k].node_id.node_index == expected[k].node_id.node_index);
+    EXPECT(got[k].score == expected[k].score);
+    EXPECT(got[k].relative_pose.x == expected[k].relative_pose.x &&
+           got[k].relative_pose.y == expected[k].relative_pose.y &&
+           got[k].relative_pose.theta == expected[k].relative_pose.theta);
+  }
+}
+
+// One PointCloud object refilled for the same node with other points of the
+// same count: the resident copy is stale and the new points are searched.
+static void RefilledCloudIsUploadedAgain() {
+  LWorld w(1);
+  PointCloud cloud = w.cloud;
+  ConstraintBuilder2D b(TestOptions());
+  ConstraintBuilder2D::Result r1, r2;
+  b.MaybeAddGlobalConstraint(SubmapId{0, 0}, &w.submaps[0], NodeId{0, 3}, &cloud);
+  b.NotifyEndOfNode();
+  b.WhenDone([&](const ConstraintBuilder2D::Result& r) { r1 = r; });
+  for (size_t i = 0; i < cloud.size(); ++i) cloud.xyz[3 * i] += 3.f;  // same object, same size
+  b.MaybeAddGlobalConstraint(SubmapId{0, 0}, &w.submaps[0], NodeId{0, 3}, &cloud);
+  b.NotifyEndOfNode();
+  b.WhenDone([&](const ConstraintBuilder2D::Result& r) { r2 = r; });
+  EXPECT(r1.size() == 1 && r2.size() == 1);
+  if (r1.size() == 1 && r2.size() == 1)
+    EXPECT(r1[0].relative_pose.x != r2[0].relative_pose.x ||
+           r1[0].relative_pose.y != r2[0].relative_pose.y);
+}
+
+// DeleteScanMatcher drops the submap's pending pairs: no constraint, no
+// rebuild from a view the caller is trimming.
+static void DeleteDropsPendingPairs() {
+  LWorld w(2);
+  ConstraintBuilderOptions o = TestOptions();
+  o.flush_pairs = 1000;  // nothing is searched before WhenDone
+  ConstraintBuilder2D b(o);
+  for (int s = 0; s < 2; ++s)
+    b.MaybeAddGlobalConstraint(SubmapId{0, s}, &w.submaps[s], NodeId{0, 0}, &w.cloud);
+  b.NotifyEndOfNode();
+  b.DeleteScanMatcher(SubmapId{0, 1});
+  ConstraintBuilder2D::Result r;
+  b.WhenDone([&](const ConstraintBuilder2D::Result& res) { r = res; });
+  EXPECT(r.size() == 1 && r[0].submap_id.submap_index == 0);
+  EXPECT(b.global_constraints_searched == 1);
+}
+
 int main() {
   CallsBack();
   FindsConstraints();
   SkipsUnsearchablePairs();
   ReusesResidentCloudsAcrossFlushes();
+  BudgetedMatcherCache();
+  RefilledCloudIsUploadedAgain();
+  DeleteDropsPendingPairs();
   if (failures) return 1;
   std::printf("constraint_builder_2d_test: OK\n");
   return 0;

@@ -372,11 +372,50 @@ static World MakeWorld() {
   return w;
 }
 
-// Connects rank `rank` of `world` (none for a world of 1); with `claim`, also
-// opens the claim service on port + 1.
+// The RCCL transport for a world of several processes on one GPU box: rank 0
+// makes the unique id (with CSM_RCCL_LIB naming the test stand-in,
+// tests/comm_standin/) and hands it over through the file CSM_TEST_RCCL_ID.
+static csm_comm* ConnectRccl(int rank, int world) {
+  const char* path = std::getenv("CSM_TEST_RCCL_ID");
+  if (!path) return nullptr;
+  uint8_t id[CSM_COMM_ID_BYTES];
+  const std::string tmp = std::string(path) + ".tmp";
+  if (rank == 0) {
+    if (csm_comm_get_unique_id(id) != CSM_OK) return nullptr;
+    FILE* f = std::fopen(tmp.c_str(), "wb");
+    if (!f || std::fwrite(id, 1, sizeof(id), f) != sizeof(id) || std::fclose(f) != 0) return nullptr;
+    if (std::rename(tmp.c_str(), path) != 0) return nullptr;
+  } else {
+    bool ok = false;
+    for (int t = 0; t < 6000 && !ok; ++t) {  // up to 120 s
+      if (FILE* f = std::fopen(path, "rb")) {
+        ok = std::fread(id, 1, sizeof(id), f) == sizeof(id);
+        std::fclose(f);
+      }
+      if (!ok) usleep(20000);
+    }
+    if (!ok) return nullptr;
+  }
+  csm_comm* comm = nullptr;
+  if (csm_comm_create_rccl(ThreadContext(), rank, world, id, &comm) != CSM_OK) return nullptr;
+  return comm;
+}
+
+// Connects rank `rank` of `world` (none for a world of 1) over TCP, or over
+// RCCL when CSM_TEST_COMM=rccl; with `claim`, also opens the claim service on
+// port + 1.
 static csm_comm* Connect(int rank, int world, int port, bool claim) {
   csm_comm* comm = nullptr;
-  if (world > 1 && csm_comm_create_tcp(rank, world, "127.0.0.1", port, &comm) != CSM_OK) {
+  const char* mode = std::getenv("CSM_TEST_COMM");
+  const bool rccl = mode && std::string(mode) == "rccl";
+  if (world > 1 && rccl) {
+    comm = ConnectRccl(rank, world);
+    if (!comm) {
+      std::fprintf(stderr, "rccl comm create failed\n");
+      std::exit(2);
+    }
+    std::fprintf(stderr, "transport rccl\n");
+  } else if (world > 1 && csm_comm_create_tcp(rank, world, "127.0.0.1", port, &comm) != CSM_OK) {
     std::fprintf(stderr, "comm create failed\n");
     std::exit(2);
   }

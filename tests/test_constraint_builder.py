@@ -347,3 +347,40 @@ def test_builder_keeps_node_clouds_resident(csm, cb):
         assert (c.submap_id, c.node_id, c.score, c.relative_pose) == \
             (r.submap_id, r.node_id, r.score, r.relative_pose)
     assert b.global_constraints_searched == ref_b.global_constraints_searched == 48
+
+
+@pytest.mark.gpu
+def test_matcher_budget_2000_submap_sweep(csm, cb):
+    """A 2000-submap sweep under a 4 GB matcher budget (about 160 of the
+    ~25 MB 400x400 matchers; the unbounded run holds all 2000, ~50 GB): the
+    cache drops and rebuilds matchers and cuts every flush into sub-batches
+    that fit, and delivers the unbounded run's constraints in the same order
+    (the reference keeps every matcher, constraint_builder_2d.cc:165-186)."""
+    world = csm.SyntheticWorld2D(num_nodes=2000, num_submaps=2000, submap_cells=400, beams=1080,
+                                 seed=20250127)
+    submaps = [cb.Submap2D(world.grid(s), (0.0, 0.0, 0.0)) for s in range(world.num_submaps)]
+    nodes = [int(world.submap_nodes[s]) for s in (3, 700, 1400)] + [1999]
+
+    def run(budget):
+        opts = cb.ConstraintBuilderOptions(max_constraint_distance=1e9, matcher_cache_bytes=budget)
+        b = cb.ConstraintBuilder2D(opts, csm.Context(0))
+        for n in nodes:
+            for s in range(world.num_submaps):
+                b.MaybeAddGlobalConstraint((0, s), submaps[s], (0, n), world.cloud(n))
+            b.NotifyEndOfNode()
+        got = []
+        b.WhenDone(got.append)
+        return b, got[0]
+
+    ref_b, ref = run(0)
+    assert ref_b.matcher_cache.evictions == 0 and len(ref_b.matcher_cache) == 2000
+    budget = 4 << 30
+    b, got = run(budget)
+    cache = b.matcher_cache
+    assert cache.evictions > 0 and cache.builds > 2000
+    assert cache.bytes <= budget
+    assert len(got) == len(ref) >= 3
+    for c, r in zip(got, ref):
+        assert (c.submap_id, c.node_id, c.score, c.relative_pose) == \
+            (r.submap_id, r.node_id, r.score, r.relative_pose)
+    assert b.global_constraints_searched == ref_b.global_constraints_searched == 4 * 2000

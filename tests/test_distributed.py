@@ -217,14 +217,33 @@ def test_cpp_diverging_submissions_abort(csm):
     assert out.stderr.count("ranks submitted different pair sequences") == 3, out.stderr
 
 
-def _run_ranks(mode, world):
+STANDIN = os.path.join(ROOT, "tests", "comm_standin", "librccl_standin.so")
+
+
+def _build_standin():
+    import subprocess
+    subprocess.check_call(["make", "-s", "-C", os.path.dirname(STANDIN)])
+
+
+def _run_ranks(mode, world, transport="tcp", tmp_path=None):
+    """Runs <world> ranks of the C++ test. transport "rccl": the library's
+    RCCL code path (csm_comm_create_rccl, RcclGather / RcclAllreduce) over the
+    test stand-in library (tests/comm_standin), since one GPU box cannot make
+    a multi-rank RCCL world."""
     import subprocess
     port = str(_free_port())
+    env = dict(os.environ)
+    if transport == "rccl":
+        _build_standin()
+        env.update(CSM_TEST_COMM="rccl", CSM_RCCL_LIB=STANDIN,
+                   CSM_TEST_RCCL_ID=str(tmp_path / "rccl_id"))
     procs = [subprocess.Popen([DIST_BIN, mode, str(r), str(world), port], stdout=subprocess.PIPE,
-                              stderr=subprocess.PIPE, text=True) for r in range(world)]
+                              stderr=subprocess.PIPE, text=True, env=env) for r in range(world)]
     outs = [p.communicate(timeout=180) for p in procs]
     for p, (o, e) in zip(procs, outs):
         assert p.returncode == 0, e
+        if transport == "rccl":
+            assert "transport rccl" in e, e
     if mode.endswith("-claim"):
         claimed = [int(l.split()[1]) for _, e in outs for l in e.splitlines() if l.startswith("claimed ")]
         assert len(claimed) == world and sum(claimed) > 0, [e for _, e in outs]
@@ -232,8 +251,10 @@ def _run_ranks(mode, world):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode,world", [("builder3d", 2), ("builder3d-claim", 2)])
-def test_cpp_sharded_builder_3d_matches_single_rank(csm, mode, world):
+@pytest.mark.parametrize("mode,world,transport", [("builder3d", 2, "tcp"),
+                                                  ("builder3d-claim", 2, "tcp"),
+                                                  ("builder3d", 3, "rccl")])
+def test_cpp_sharded_builder_3d_matches_single_rank(csm, mode, world, transport, tmp_path):
     """The C++ ConstraintBuilder3D sharded over 2 ranks (two processes on the
     one GPU, TCP transport; by submap owner, or by chunks claimed through
     csm_comm_fetch_add) delivers on rank 0 what the single-rank builder
@@ -244,7 +265,7 @@ def test_cpp_sharded_builder_3d_matches_single_rank(csm, mode, world):
     single = subprocess.run([DIST_BIN, "builder3d", "0", "1", "0"], capture_output=True, text=True,
                             timeout=120)
     assert single.returncode == 0, single.stderr
-    outs = _run_ranks(mode, world)
+    outs = _run_ranks(mode, world, transport, tmp_path)
     lines = single.stdout.strip().splitlines()
     assert sum(1 for l in lines if l.startswith("c ")) >= 4, single.stdout
     assert any(l.startswith("c ") and l.endswith(" 1") for l in lines), single.stdout  # a global one
@@ -253,8 +274,11 @@ def test_cpp_sharded_builder_3d_matches_single_rank(csm, mode, world):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode,world", [("builder", 2), ("builder-claim", 2), ("builder-claim", 3)])
-def test_cpp_sharded_builder_matches_single_rank(csm, mode, world):
+@pytest.mark.parametrize("mode,world,transport", [("builder", 2, "tcp"), ("builder-claim", 2, "tcp"),
+                                                  ("builder-claim", 3, "tcp"),
+                                                  ("builder", 2, "rccl"),
+                                                  ("builder-claim", 3, "rccl")])
+def test_cpp_sharded_builder_matches_single_rank(csm, mode, world, transport, tmp_path):
     """The C++ ConstraintBuilder2D sharded over 2-3 ranks (processes on the
     one GPU, TCP transport; Sharding::kStatic by submap owner, or
     Sharding::kClaim with one-submap chunks claimed dynamically) delivers on
@@ -265,7 +289,7 @@ def test_cpp_sharded_builder_matches_single_rank(csm, mode, world):
     single = subprocess.run([DIST_BIN, "builder", "0", "1", "0"], capture_output=True, text=True,
                             timeout=120)
     assert single.returncode == 0, single.stderr
-    outs = _run_ranks(mode, world)
+    outs = _run_ranks(mode, world, transport, tmp_path)
     lines = single.stdout.strip().splitlines()
     assert sum(1 for l in lines if l.startswith("c ")) >= 5, single.stdout
     assert outs[0][0].strip().splitlines() == lines
