@@ -659,11 +659,24 @@ def fast3d_bench(csm, ctx, args, rank=0, world_size=1, dist=None, coll_dev=None,
                              submap_range=(b0, b1 - b0), seed=args.seed + 5)
     gen = time.time() - t0
     o = csm.FastCorrelativeScanMatcherOptions3D()
-    grids = [(csm.HybridGrid(w.high_resolution, *w.high_cells[s], context=ctx),
+
+    def build():
+        """The submaps' HybridGrids and PrecomputationGridStack3D pyramids
+        (DispatchScanMatcherConstruction, constraint_builder_3d.cc:170-198)."""
+        g = [(csm.HybridGrid(w.high_resolution, *w.high_cells[s], context=ctx),
               csm.HybridGrid(w.low_resolution, *w.low_cells[s], context=ctx))
              for s in range(w.num_submaps)]
-    mats = [csm.FastCorrelativeScanMatcher3D(g[0], g[1], w.submap_hist[s], o, ctx)
-            for s, g in enumerate(grids)]
+        m = [csm.FastCorrelativeScanMatcher3D(gg[0], gg[1], w.submap_hist[s], o, ctx)
+             for s, gg in enumerate(g)]
+        return g, m
+
+    def close(g, m):
+        for x in m:
+            x.close()
+        for pair in g:
+            for x in pair:
+                x.close()
+
     # Node clouds converted to csm_node3d once, like inputs resident before the timed region.
     nodes = csm.NodeSet3D([w.node(i) for i in range(w.num_nodes)])
     sub = np.repeat(np.arange(w.num_submaps), w.num_nodes)
@@ -673,26 +686,48 @@ def fast3d_bench(csm, ctx, args, rank=0, world_size=1, dist=None, coll_dev=None,
     sub_global = w.submap_ids[sub].astype(np.int64)
     submission = sub_global * w.num_nodes + nod  # queue order: submap-major
 
+    # A step is the whole C5 queue as a sweep runs it: every submap's grids and
+    # pyramid are built (once per sweep, as the builder's matcher cache does),
+    # then all its pairs are searched; the builds are inside the timed region
+    # like C3's pyramids, and also reported on their own. Releasing the
+    # matchers afterwards (to the context's pool, where the next step's builds
+    # find them) is outside it, reported as release_ms_per_step.
+    phase = {"build": 0.0, "search": 0.0, "release": 0.0}
+
     def step():
-        res = csm.match_batch_3d(mats, nodes, pairs, ctx)
+        a = time.perf_counter()
+        g, m = build()
+        b = time.perf_counter()
+        res = csm.match_batch_3d(m, nodes, pairs, ctx)
         rec = cdist.make_records_3d(res, submission, sub_global, nod) if cdist else None
         if cdist is not None:
             rec = gather(rec) if gather is not None else \
                 cdist.gather_records(rec, dist, rank, world_size, coll_dev)
-        return res, rec
+        c = time.perf_counter()
+        phase["build"] += b - a
+        phase["search"] += c - b
+        return res, rec, (g, m)
 
-    step()  # warm-up at full size (staging buffers)
+    _, _, kept = step()  # warm-up at full size (staging buffers, the pool)
+    close(*kept)
+    phase["build"] = phase["search"] = 0.0
     ctx.reset_timing()
     ctx.enable_timing(True)
-    barrier_sync()
-    t0 = time.perf_counter()
     reps = max(1, args.steps3d)
     errors3 = 0
-    for _ in range(reps):
-        res3, rec = step()
+    wall = 0.0
+    for k in range(reps):
+        barrier_sync()
+        t0 = time.perf_counter()
+        res3, rec, kept = step()
+        barrier_sync()
+        wall += time.perf_counter() - t0
         errors3 += int((res3["status"] < 0).sum())
-    barrier_sync()
-    wall = time.perf_counter() - t0
+        if k + 1 < reps:
+            t0 = time.perf_counter()
+            close(*kept)
+            phase["release"] += time.perf_counter() - t0
+    grids, mats = kept
     tm = ctx.timing()
     ctx.enable_timing(False)
     if cdist is not None:
@@ -700,12 +735,25 @@ def fast3d_bench(csm, ctx, args, rank=0, world_size=1, dist=None, coll_dev=None,
     total = w.num_nodes * S3 * reps
     out = {"config": f"C5: MatchFullSubmap, {w.num_nodes} nodes x {S3} submaps split over "
                      f"{world_size} GPU(s) (0.10/0.45 m grids, ~200-point clouds, "
-                     "120-bucket histograms), branch_and_bound_depth 8, full_resolution_depth 3",
+                     "120-bucket histograms), branch_and_bound_depth 8, full_resolution_depth 3; a step "
+                     "builds every submap's HybridGrids and pyramid, then searches all pairs",
            "pairs_per_step": w.num_nodes * S3, "steps": reps, "value": total / wall,
            "unit": "pairs/s", "n_gpus": world_size, "scaling": "strong",
            "accepted_per_step": int(len(rec)) if rec is not None else int((res3["status"] == 0).sum()),
            "ms_per_step": wall / reps * 1e3,
            "errors_per_step": errors3 / reps, "stack_high_water": int(tm.stack_high_water),
+           # Pairs whose maximum more than one passing leaf reached (resolved to
+           # the reference's pick, host3d.cc ResolveTies3d), per step.
+           "tied_pairs_per_step": tm.tied_pairs_3d / reps,
+           "ties_unresolved_per_step": tm.ties_unresolved_3d / reps,
+           "ties_by_branch_last_step": {name: int(((res3["status"] == 0) & (res3["tie"] == code)).sum())
+                                        for name, code in (("ancestors", csm.TIE_ANCESTORS),
+                                                           ("toplist", csm.TIE_TOPLIST),
+                                                           ("unresolved", csm.TIE_UNRESOLVED))},
+           "build_ms_per_step": phase["build"] / reps * 1e3,
+           "release_ms_per_step": phase["release"] / max(reps - 1, 1) * 1e3,
+           "search_ms_per_step": phase["search"] / reps * 1e3,
+           "value_search_only": total / phase["search"] if phase["search"] else 0.0,
            "kernel_ms_per_step": tm.fast3d_kernel_ms / reps, "lookups_per_step": tm.fast3d_lookups / reps,
            "algorithmic_GBps": tm.fast3d_lookups / (tm.fast3d_kernel_ms * 1e-3) / 1e9
            if tm.fast3d_kernel_ms else 0.0, "setup_s": gen}

@@ -125,7 +125,8 @@ class Node3D(C.Structure):
 
 class Result3D(C.Structure):
     _fields_ = [("status", C.c_int32), ("score", C.c_float), ("pose", Pose3D),
-                ("rotational_score", C.c_float), ("low_resolution_score", C.c_float)]
+                ("rotational_score", C.c_float), ("low_resolution_score", C.c_float),
+                ("tie", C.c_int32), ("reserved", C.c_int32)]
 
 
 class CeresOptions2D(C.Structure):

@@ -19,6 +19,7 @@ constexpr int kRootScore3d = 256;         // roots scored at a time (one per lan
 constexpr int kTopCells3d = 512;          // distinct top-level cells of a cloud (LDS list)
 constexpr int kBatch3d = 16;              // DFS nodes scored per step (16 lanes each)
 constexpr int kMax3dTop = 1 << 20;        // top-level candidates per yaw
+constexpr int kTieCap3d = 4096;           // tied leaves recorded per pair (collect search)
 constexpr int kStack3d = 1024;            // DFS stack entries per workgroup in LDS
 constexpr int kSpill3d = 3072;            // further entries per workgroup in global memory
 constexpr int kStat3dHighWater = 14;      // stats word: DFS stack high-water (max over workgroups)
@@ -84,6 +85,9 @@ struct Pair3Desc {
   int32_t min_sum;          // smallest sum whose score exceeds min_score
   float min_low_resolution_score;
   int32_t key_shift, bits_xy, bits_z;  // leaf key layout
+  // Tie resolution (host3d.cc ResolveTies3d): a collect search records every
+  // leaf that passes the low-resolution check with sum == collect_sum.
+  int32_t collect, collect_sum;
 };
 
 // One discrete scan (yaw) of a pair: the pose the cloud is discretized with,

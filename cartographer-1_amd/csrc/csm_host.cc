@@ -83,53 +83,82 @@ int EnsureDevice(csm_context* ctx) {
   return hipSetDevice(ctx->device) == hipSuccess ? CSM_OK : CSM_EHIP;
 }
 
-// The context's pool of device buffers from destroyed matchers: the smallest
-// one holding n bytes (and at most twice that) is reused, else a new one is
-// allocated; if that allocation fails, the idle pooled buffers are released
-// and it is tried once more. Callers hold ctx->mu.
-void PoolRelease(csm_context* ctx) {
-  for (auto& b : ctx->buf_pool) (void)hipFree(b.first);
-  ctx->buf_pool.clear();
-}
-int PoolTake(csm_context* ctx, size_t n, DevBuf* out) {
-  int best = -1;
-  for (int i = 0; i < static_cast<int>(ctx->buf_pool.size()); ++i) {
-    const size_t b = ctx->buf_pool[i].second;
-    if (b >= n && b <= 2 * n + 4096 && (best < 0 || b < ctx->buf_pool[best].second)) best = i;
-  }
-  if (best < 0) {
-    if (out->Reserve(n) == CSM_OK) return CSM_OK;
-    PoolRelease(ctx);
-    return out->Reserve(n);
-  }
-  out->ptr = ctx->buf_pool[best].first;
-  out->bytes = ctx->buf_pool[best].second;
-  ctx->buf_pool.erase(ctx->buf_pool.begin() + best);
-  return CSM_OK;
-}
-// At most 32 buffers and 1 GiB stay pooled (oldest freed first): enough for
-// a sweep's create / destroy churn of ~40 submaps, without holding memory a
-// later 3D or scratch allocation needs.
-void PoolGive(csm_context* ctx, DevBuf* b) {
-  constexpr size_t kMaxPooled = 32;
-  constexpr size_t kMaxPooledBytes = size_t{1} << 30;
-  if (!b->ptr) return;
-  ctx->buf_pool.emplace_back(b->ptr, b->bytes);
-  b->ptr = nullptr;
-  b->bytes = 0;
-  size_t held = 0;
-  for (const auto& e : ctx->buf_pool) held += e.second;
-  while (!ctx->buf_pool.empty() &&
-         (ctx->buf_pool.size() > kMaxPooled || held > kMaxPooledBytes)) {
-    held -= ctx->buf_pool.front().second;
-    (void)hipFree(ctx->buf_pool.front().first);
-    ctx->buf_pool.erase(ctx->buf_pool.begin());
-  }
-}
-
 }  // namespace
 
 namespace csm {
+
+namespace {
+std::mutex& PoolRegistryMutex() {
+  static std::mutex m;
+  return m;
+}
+std::vector<BufPool*>& PoolRegistry() {
+  static std::vector<BufPool*> r;
+  return r;
+}
+}  // namespace
+
+BufPool::BufPool() {
+  std::lock_guard<std::mutex> g(PoolRegistryMutex());
+  PoolRegistry().push_back(this);
+}
+
+BufPool::~BufPool() {
+  {
+    std::lock_guard<std::mutex> g(PoolRegistryMutex());
+    auto& r = PoolRegistry();
+    r.erase(std::remove(r.begin(), r.end(), this), r.end());
+  }
+  Release();
+}
+
+void BufPool::Release() {
+  std::lock_guard<std::mutex> g(mu_);
+  for (auto& b : bufs_) (void)hipFree(b.first);
+  bufs_.clear();
+  held_ = 0;
+}
+
+int BufPool::Take(size_t n, DevBuf* out) {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    int best = -1;
+    for (int i = 0; i < static_cast<int>(bufs_.size()); ++i) {
+      const size_t b = bufs_[i].second;
+      if (b >= n && b <= 2 * n + 4096 && (best < 0 || b < bufs_[best].second)) best = i;
+    }
+    if (best >= 0) {
+      out->ptr = bufs_[best].first;
+      out->bytes = bufs_[best].second;
+      held_ -= bufs_[best].second;
+      bufs_.erase(bufs_.begin() + best);
+      return CSM_OK;
+    }
+  }
+  return out->Reserve(n);  // releases every pool and retries if the device is full
+}
+
+void BufPool::Give(DevBuf* b) {
+  constexpr size_t kMaxPooled = 8192;
+  if (!b->ptr) return;
+  std::lock_guard<std::mutex> g(mu_);
+  bufs_.emplace_back(b->ptr, b->bytes);
+  held_ += b->bytes;
+  b->ptr = nullptr;
+  b->bytes = 0;
+  size_t drop = 0;
+  while (drop < bufs_.size() && (bufs_.size() - drop > kMaxPooled || held_ > cap_bytes_)) {
+    held_ -= bufs_[drop].second;
+    (void)hipFree(bufs_[drop].first);
+    ++drop;
+  }
+  bufs_.erase(bufs_.begin(), bufs_.begin() + static_cast<std::ptrdiff_t>(drop));
+}
+
+void ReleaseIdlePools() {
+  std::lock_guard<std::mutex> g(PoolRegistryMutex());
+  for (BufPool* p : PoolRegistry()) p->Release();
+}
 
 csm_context* AcquireCallContext(csm_context* owner) {
   {
@@ -945,6 +974,9 @@ int csm_context_create(int32_t device, csm_context** out) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
     ctx->num_cus = prop.multiProcessorCount;
+  size_t free_b = 0, total_b = 0;
+  if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && total_b > 0)
+    ctx->pool.SetCapBytes(total_b / 4);  // idle pooled buffers: at most a quarter of the device
   *out = ctx.release();
   return CSM_OK;
 }
@@ -1130,7 +1162,7 @@ int csm_fast2d_create(csm_context* ctx, const csm_map_limits* limits,
     hex_mask = 0;
   }
   d.hex_mask = static_cast<int32_t>(hex_mask);
-  if ((rc = PoolTake(ctx, total, &m->pyramid))) return rc;
+  if ((rc = ctx->pool.Take(total, &m->pyramid))) return rc;
   d.pyramid_base = m->pyramid.as<uint8_t>();
   d.pyramid_bytes = static_cast<int32_t>(total);
   for (int l = 0; l < depth; ++l) {
@@ -1166,7 +1198,7 @@ int csm_fast2d_create(csm_context* ctx, const csm_map_limits* limits,
   }
   // Correspondence costs (Grid2D::GetCorrespondenceCost, grid_2d.cc) for the
   // CeresScanMatcher2D refinement: the value table with unknown -> max_cc.
-  if ((rc = PoolTake(ctx, sizeof(float) * n0, &m->cost))) return rc;
+  if ((rc = ctx->pool.Take(sizeof(float) * n0, &m->cost))) return rc;
   CSM_HIP(LaunchCellsToProbability(dcells.as<uint16_t>(), ctx->f2_ctab.as<float>(),
                                    m->cost.as<float>(), n0, st));
   // The cells are read from the caller's memory and the context's scratch
@@ -1178,10 +1210,9 @@ int csm_fast2d_create(csm_context* ctx, const csm_map_limits* limits,
 
 void csm_fast2d_destroy(csm_fast2d* m) {
   if (!m) return;
-  std::lock_guard<std::mutex> lock(m->ctx->mu);
   (void)hipSetDevice(m->ctx->device);
-  PoolGive(m->ctx, &m->pyramid);  // reused by the next csm_fast2d_create
-  PoolGive(m->ctx, &m->cost);
+  m->ctx->pool.Give(&m->pyramid);  // reused by the next create
+  m->ctx->pool.Give(&m->cost);
   delete m;
 }
 

@@ -24,6 +24,10 @@ namespace csm {
     if ((call) != hipSuccess) return CSM_EHIP;      \
   } while (0)
 
+// Frees every context's idle pooled buffers (BufPool below); a device
+// allocation that fails calls it and tries once more.
+void ReleaseIdlePools();
+
 // Grow-only device buffer.
 struct DevBuf {
   void* ptr = nullptr;
@@ -37,12 +41,46 @@ struct DevBuf {
     ptr = nullptr;
     bytes = 0;
     const size_t want = std::max<size_t>(n, 256);
-    if (hipMalloc(&ptr, want) != hipSuccess) return CSM_ENOMEM;
+    if (hipMalloc(&ptr, want) != hipSuccess) {
+      ReleaseIdlePools();
+      if (hipMalloc(&ptr, want) != hipSuccess) {
+        ptr = nullptr;
+        return CSM_ENOMEM;
+      }
+    }
     bytes = want;
     return CSM_OK;
   }
   template <typename T>
   T* as() const { return static_cast<T*>(ptr); }
+};
+
+// Device buffers of destroyed matchers and grids (2D pyramids and cost
+// grids, 3D bricks, levels and octets), kept for reuse by the next create: a
+// sweep builds and drops thousands of submaps, and hipMalloc / hipFree of
+// tens to hundreds of MB dominate a build otherwise (C5: 1.75 ms per submap).
+// Take: the smallest idle buffer holding n bytes and at most twice that, else
+// a new allocation. Give: keeps the buffer, freeing the oldest ones past the
+// caps (bytes: a quarter of the device's memory by default; count). Every
+// pool is registered process-wide so that any failed device allocation in the
+// library first releases all idle pooled memory (ReleaseIdlePools).
+class BufPool {
+ public:
+  BufPool();
+  ~BufPool();
+  BufPool(const BufPool&) = delete;
+  BufPool& operator=(const BufPool&) = delete;
+  int Take(size_t n, DevBuf* out);
+  void Give(DevBuf* b);
+  void Release();
+  void SetCapBytes(size_t cap) { cap_bytes_ = cap; }
+  size_t held() const { return held_; }
+
+ private:
+  std::mutex mu_;
+  std::vector<std::pair<void*, size_t>> bufs_;
+  size_t held_ = 0;
+  size_t cap_bytes_ = size_t{1} << 30;
 };
 
 // Page-locked host staging (H2D copies at full PCIe rate).
@@ -150,7 +188,8 @@ struct csm_context {
   int num_cus = 256;
   // 3D path scratch (host3d.cc).
   csm::DevBuf rt3_rot, rt3_rot4, rt3_cols, rt3_trans, rt3_points, rt3_best, f3_pairs, f3_yaws, f3_points,
-      f3_low_points, f3_best, f3_status, f3_counter, f3_items, f3_scores, f3_spill;
+      f3_low_points, f3_best, f3_status, f3_counter, f3_items, f3_scores, f3_spill, f3_best_hi,
+      f3_ties, f3_tie_count, f3_tie_yaws, f3_sq_jobs, f3_sq_queries, f3_sq_sums;
   csm::PinnedBuf f3_host_yaws, f3_host_points;
   // Side stream for the 3D batch's cloud upload (overlaps the rotational
   // scores on `stream`); the search waits on f3_points_ready.
@@ -160,15 +199,18 @@ struct csm_context {
   csm::DevBuf vf_points, vf_offsets, vf_keep, vf_counts;
   // CeresScanMatcher2D refinement scratch (ceres2d.hip).
   csm::DevBuf cr_items, cr_out, cr3_items, cr3_points, cr3_out;
-  // csm_fast2d_create: device buffers of destroyed matchers kept for reuse
-  // (pyramids, cost grids: a sweep creates and destroys thousands), scratch,
-  // and the quantization / cost tables of the last (min_cc, max_cc).
-  std::vector<std::pair<void*, size_t>> buf_pool;
+  // Device buffers of destroyed matchers and grids kept for reuse (BufPool),
+  // csm_fast2d_create's scratch and the quantization / cost tables of the
+  // last (min_cc, max_cc); the 3D value tables and the pinned staging of
+  // csm_hybrid_grid_create.
+  csm::BufPool pool;
   csm::DevBuf f2_cells, f2_widen, f2_qtab, f2_ctab;
   float f2_tab_key[2] = {-1.f, -1.f};
+  csm::DevBuf f3_ptab, f3_qtab, f3_grid_cells;
+  bool f3_tables = false;
+  csm::PinnedBuf f3_grid_stage;
   ~csm_context() {
     for (csm_context* c : call_all) csm_context_destroy(c);
-    for (auto& b : buf_pool) (void)hipFree(b.first);
   }
 };
 

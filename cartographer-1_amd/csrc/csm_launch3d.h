@@ -13,6 +13,8 @@ constexpr int kRt3dThreads = 384;  // translations per RTCSM3D launch
 hipError_t LaunchBrickFromValues(const uint16_t* values, int64_t n, const float* ptab,
                                  const uint8_t* qtab, float* prob, uint8_t* level0,
                                  hipStream_t st);
+hipError_t LaunchBrickScatter(const int32_t* ijk, const uint16_t* values, int64_t count,
+                              const Brick3& b, uint16_t* out, hipStream_t st);
 hipError_t LaunchLevelGather(const uint8_t* prev, const Brick3& pb, uint8_t* out, const Brick3& ob,
                              int shift, int half, hipStream_t st);
 hipError_t LaunchOctetBuild(const uint8_t* level, const Brick3& lb, int h, uint64_t* out,
@@ -70,7 +72,18 @@ hipError_t LaunchFast3dSearch(bool large, int grid, hipStream_t st, const Submap
                               const Pair3Desc* pairs, const Yaw3Desc* yaws, int item_begin,
                               int num_items, const float* points, const float* low_points,
                               unsigned* counter, unsigned long long* best, int32_t* status,
-                              unsigned long long* stats, int4* spill);
+                              unsigned long long* stats, int4* spill, unsigned long long* best_hi,
+                              uint4* ties, int32_t* tie_count);
+// Tie resolution: the reference's ScoreCandidates sum (fast_correlative_scan_
+// matcher_3d.cc:332-352) of (depth, x, y, z offset) queries; one workgroup per
+// job = (yaw item, queries[first, first + count)).
+struct Score3Job {
+  int32_t item, first, count, pad;
+};
+hipError_t LaunchFast3dScoreQueries(int num_jobs, hipStream_t st, const Submap3Desc* submaps,
+                                    const Pair3Desc* pairs, const Yaw3Desc* yaws,
+                                    const float* points, const Score3Job* jobs,
+                                    const int4* queries, int32_t* sums);
 hipError_t LaunchFast3dFinalize(int num_pairs, hipStream_t st, const Submap3Desc* submaps,
                                 const Pair3Desc* pairs, const Yaw3Desc* yaws,
                                 const float* low_points, const unsigned long long* best,

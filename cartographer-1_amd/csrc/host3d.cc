@@ -11,6 +11,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
+#include <limits>
+#include <tuple>
 #include <atomic>
 #include <chrono>
 #include <cmath>
@@ -28,6 +31,7 @@
 #include "csm_device3d.h"
 #include "csm_internal.h"
 #include "csm_launch3d.h"
+#include "parallel_sort.h"
 
 using namespace csm;
 
@@ -161,6 +165,21 @@ int EnsureDevice3(csm_context* ctx) {
   return hipSetDevice(ctx->device) == hipSuccess ? CSM_OK : CSM_EHIP;
 }
 
+// The value tables on the device, made once per context (caller holds ctx->mu).
+int EnsureValueTables(csm_context* ctx) {
+  if (ctx->f3_tables) return CSM_OK;
+  std::vector<float> ptab;
+  std::vector<uint8_t> qtab;
+  ValueTables(&ptab, &qtab);
+  int rc;
+  if ((rc = ctx->f3_ptab.Reserve(sizeof(float) * 32768)) || (rc = ctx->f3_qtab.Reserve(32768)))
+    return rc;
+  CSM_HIP(hipMemcpy(ctx->f3_ptab.ptr, ptab.data(), sizeof(float) * 32768, hipMemcpyHostToDevice));
+  CSM_HIP(hipMemcpy(ctx->f3_qtab.ptr, qtab.data(), 32768, hipMemcpyHostToDevice));
+  ctx->f3_tables = true;
+  return CSM_OK;
+}
+
 }  // namespace
 
 // ----------------------------------------------------------- HybridGrid --
@@ -200,28 +219,27 @@ int csm_hybrid_grid_create(csm_context* ctx, float resolution, const int32_t* ij
   const int64_t n = static_cast<int64_t>(b.nx) * b.ny * b.nz;
   if (n > (int64_t{1} << 31)) return CSM_ERANGE;
   if (n > 0) {
-    std::vector<uint16_t> dense(static_cast<size_t>(n), 0);
-    for (int64_t i = 0; i < count; ++i) {
-      const int64_t k = (static_cast<int64_t>(ijk[3 * i + 2] - b.oz) * b.ny + (ijk[3 * i + 1] - b.oy)) *
-                            b.nx +
-                        (ijk[3 * i] - b.ox);
-      dense[k] = values[i];
-    }
-    std::vector<float> ptab;
-    std::vector<uint8_t> qtab;
-    ValueTables(&ptab, &qtab);
-    DevBuf dptab;
-    if ((rc = g->values.Reserve(sizeof(uint16_t) * n))) return rc;
-    if ((rc = g->prob.Reserve(sizeof(float) * n))) return rc;
-    if ((rc = dptab.Reserve(sizeof(float) * 32768))) return rc;
+    // The cell list goes up through pinned staging and is scattered into the
+    // zeroed brick on the device (no dense host copy); bricks come from the
+    // context's pool (BufPool).
+    if ((rc = EnsureValueTables(ctx))) return rc;
+    const size_t list_bytes = static_cast<size_t>(count) * (3 * sizeof(int32_t) + sizeof(uint16_t));
+    if ((rc = ctx->f3_grid_stage.Reserve(list_bytes))) return rc;
+    if ((rc = ctx->f3_grid_cells.Reserve(list_bytes))) return rc;
+    if ((rc = ctx->pool.Take(sizeof(uint16_t) * n, &g->values))) return rc;
+    if ((rc = ctx->pool.Take(sizeof(float) * n, &g->prob))) return rc;
+    char* h = ctx->f3_grid_stage.as<char>();
+    std::memcpy(h, ijk, sizeof(int32_t) * 3 * count);
+    std::memcpy(h + sizeof(int32_t) * 3 * count, values, sizeof(uint16_t) * count);
     hipStream_t st = ctx->stream;
-    CSM_HIP(hipMemcpyAsync(g->values.ptr, dense.data(), sizeof(uint16_t) * n,
-                           hipMemcpyHostToDevice, st));
-    CSM_HIP(hipMemcpyAsync(dptab.ptr, ptab.data(), sizeof(float) * 32768, hipMemcpyHostToDevice,
-                           st));
-    CSM_HIP(LaunchBrickFromValues(g->values.as<uint16_t>(), n, dptab.as<float>(), nullptr,
+    CSM_HIP(hipMemcpyAsync(ctx->f3_grid_cells.ptr, h, list_bytes, hipMemcpyHostToDevice, st));
+    CSM_HIP(hipMemsetAsync(g->values.ptr, 0, sizeof(uint16_t) * n, st));
+    const int32_t* dijk = ctx->f3_grid_cells.as<int32_t>();
+    const uint16_t* dval = reinterpret_cast<const uint16_t*>(dijk + 3 * count);
+    CSM_HIP(LaunchBrickScatter(dijk, dval, count, b, g->values.as<uint16_t>(), st));
+    CSM_HIP(LaunchBrickFromValues(g->values.as<uint16_t>(), n, ctx->f3_ptab.as<float>(), nullptr,
                                   g->prob.as<float>(), nullptr, st));
-    CSM_HIP(hipStreamSynchronize(st));
+    CSM_HIP(hipStreamSynchronize(st));  // the staging is reused by the next create
   }
   *out = g.release();
   return CSM_OK;
@@ -230,6 +248,8 @@ int csm_hybrid_grid_create(csm_context* ctx, float resolution, const int32_t* ij
 void csm_hybrid_grid_destroy(csm_hybrid_grid* g) {
   if (!g) return;
   (void)hipSetDevice(g->ctx->device);
+  g->ctx->pool.Give(&g->values);  // reused by the next create
+  g->ctx->pool.Give(&g->prob);
   delete g;
 }
 
@@ -695,7 +715,7 @@ int csm_fast3d_create(csm_context* ctx, const csm_hybrid_grid* high, const csm_h
     total += (bytes + 255) & ~int64_t{255};
   }
   if (total > 0x7fffff00) return CSM_ERANGE;
-  if ((rc = m->levels.Reserve(std::max<int64_t>(total, 256)))) return rc;
+  if ((rc = ctx->pool.Take(std::max<int64_t>(total, 256), &m->levels))) return rc;
   d.levels = m->levels.as<uint8_t>();
   d.levels_bytes = static_cast<int32_t>(std::max<int64_t>(total, 256));
   // Octet bricks of the DFS child levels 0..search_levels-2.
@@ -718,7 +738,7 @@ int csm_fast3d_create(csm_context* ctx, const csm_hybrid_grid* high, const csm_h
     otot += static_cast<int64_t>(ob.nx) * ob.ny * ob.nz * 8;
   }
   if (otot > 0x7fffff00) return CSM_ERANGE;
-  if ((rc = m->octs.Reserve(std::max<int64_t>(otot, 256)))) return rc;
+  if ((rc = ctx->pool.Take(std::max<int64_t>(otot, 256), &m->octs))) return rc;
   d.octs = m->octs.as<uint8_t>();
   d.octs_bytes = static_cast<int32_t>(std::max<int64_t>(otot, 256));
   d.low_prob = low->prob.as<float>();
@@ -726,14 +746,9 @@ int csm_fast3d_create(csm_context* ctx, const csm_hybrid_grid* high, const csm_h
   d.low_resolution = low->resolution;
   hipStream_t st = ctx->stream;
   if (!empty) {
-    std::vector<float> ptab;
-    std::vector<uint8_t> qtab;
-    ValueTables(&ptab, &qtab);
-    DevBuf dq;
-    if ((rc = dq.Reserve(32768))) return rc;
-    CSM_HIP(hipMemcpyAsync(dq.ptr, qtab.data(), 32768, hipMemcpyHostToDevice, st));
+    if ((rc = EnsureValueTables(ctx))) return rc;
     const int64_t n0 = static_cast<int64_t>(d.level[0].nx) * d.level[0].ny * d.level[0].nz;
-    CSM_HIP(LaunchBrickFromValues(high->values.as<uint16_t>(), n0, nullptr, dq.as<uint8_t>(),
+    CSM_HIP(LaunchBrickFromValues(high->values.as<uint16_t>(), n0, nullptr, ctx->f3_qtab.as<uint8_t>(),
                                   nullptr, m->levels.as<uint8_t>() + d.level[0].offset, st));
     for (int l = 1; l < depth; ++l)
       CSM_HIP(LaunchLevelGather(m->levels.as<uint8_t>() + d.level[l - 1].offset, d.level[l - 1],
@@ -762,6 +777,8 @@ int64_t csm_hybrid_grid_device_bytes(const csm_hybrid_grid* g) {
 void csm_fast3d_destroy(csm_fast3d* m) {
   if (!m) return;
   (void)hipSetDevice(m->ctx->device);
+  m->ctx->pool.Give(&m->levels);  // reused by the next create
+  m->ctx->pool.Give(&m->octs);
   delete m;
 }
 
@@ -1026,6 +1043,303 @@ void ParallelPairs(int64_t num, F&& f) {
   HostPool::Get().Run(num, fn);
 }
 
+uint64_t LeafId3(const Pair3Desc& d, int yaw, int x, int y, int z) {  // kernels3d.hip LeafId
+  uint64_t id = static_cast<uint64_t>(yaw);
+  id = (id << d.bits_xy) | static_cast<uint64_t>(x + d.wxy);
+  id = (id << d.bits_xy) | static_cast<uint64_t>(y + d.wxy);
+  id = (id << d.bits_z) | static_cast<uint64_t>(z + d.wz);
+  return id;
+}
+
+// Exactly tied maxima in 3D. The search keeps, among the
+// leaves that pass the low-resolution check at the best sum, the smallest
+// (yaw, x, y, z) key and, next to it, the largest (best_hi). The reference
+// returns the first such leaf its depth-first search reaches
+// (fast_correlative_scan_matcher_3d.cc:377-440): the lowest-resolution
+// candidates in the order std::sort(greater<Candidate3D>) leaves their
+// generation order (scan_index, z, y, x; :297-330, :353-354) in, each node's
+// children (<= 8, generated z, y, x with x fastest, :412-430) by descending
+// score with ties in generation order (insertion sort: stable), and at depth 0
+// the first child that passes the low-resolution check (:384-401), the
+// incumbent kept on equal scores (:433-437). For a tied pair: (1) a collect
+// search with the maximum as its starting best records every passing leaf at
+// it; (2) their ancestors' exact scores at every reference depth are computed
+// on the device (fast3d_score_queries); (3) when two distinct
+// lowest-resolution ancestors share the highest score, the pair's whole
+// lowest-resolution list is scored and ordered with the same introsort
+// (parallel_sort.h). No oracle and no CPU scoring is involved. `code` gets
+// CSM_TIE_* per device pair.
+int ResolveTies3d(csm_context* ctx, csm_fast3d* const* submaps, const std::vector<Pair3Desc>& pdesc,
+                  const std::vector<int32_t>& stat, const std::vector<unsigned long long>& keys_hi,
+                  std::vector<unsigned long long>* keys, std::vector<int8_t>* code) {
+  const int np = static_cast<int>(pdesc.size());
+  std::vector<int> tied;
+  for (int dp = 0; dp < np; ++dp) {
+    const unsigned long long key = (*keys)[dp];
+    if (stat[dp] < 0 || key == 0) continue;
+    const Pair3Desc& d = pdesc[dp];
+    const unsigned long long mask = (1ull << d.key_shift) - 1;
+    const unsigned long long hi = keys_hi[dp];
+    if ((hi >> d.key_shift) == (key >> d.key_shift) && (hi & mask) != (~key & mask))
+      tied.push_back(dp);
+  }
+  if (tied.empty()) return CSM_OK;
+  ctx->t.tied_pairs_3d += static_cast<int64_t>(tied.size());
+  hipStream_t st = ctx->stream;
+  Pair3Desc* dpairs = ctx->f3_pairs.as<Pair3Desc>();
+  const Submap3Desc* dsub = reinterpret_cast<const Submap3Desc*>(dpairs + np);
+  const Yaw3Desc* dyaws = ctx->f3_yaws.as<Yaw3Desc>();
+  const int nt = static_cast<int>(tied.size());
+  int rc;
+  // (1) Collect search over the tied pairs' yaws (small clouds, then large).
+  std::vector<Pair3Desc> mod(nt);
+  std::vector<unsigned long long> init(nt);
+  int items_small = 0, items = 0;
+  for (int pass = 0; pass < 2; ++pass)
+    for (int t = 0; t < nt; ++t) {
+      const Pair3Desc& d = pdesc[tied[t]];
+      if ((d.num_points > kSmall3dPoints) != (pass == 1)) continue;
+      items += d.num_yaws;
+      if (pass == 0) items_small = items;
+    }
+  if ((rc = ctx->f3_tie_yaws.Reserve(sizeof(Yaw3Desc) * std::max(items, 1)))) return rc;
+  if ((rc = ctx->f3_tie_count.Reserve(sizeof(int32_t) * nt))) return rc;
+  if ((rc = ctx->f3_ties.Reserve(sizeof(uint4) * kTieCap3d * static_cast<size_t>(nt)))) return rc;
+  Yaw3Desc* tyaws = ctx->f3_tie_yaws.as<Yaw3Desc>();
+  int at = 0;
+  for (int pass = 0; pass < 2; ++pass)
+    for (int t = 0; t < nt; ++t) {
+      const int dp = tied[t];
+      const Pair3Desc& d = pdesc[dp];
+      if ((d.num_points > kSmall3dPoints) != (pass == 1)) continue;
+      CSM_HIP(hipMemcpyAsync(tyaws + at, dyaws + d.yaw_begin, sizeof(Yaw3Desc) * d.num_yaws,
+                             hipMemcpyDeviceToDevice, st));
+      at += d.num_yaws;
+    }
+  for (int t = 0; t < nt; ++t) {
+    const int dp = tied[t];
+    mod[t] = pdesc[dp];
+    mod[t].collect = t + 1;
+    mod[t].collect_sum = static_cast<int32_t>((*keys)[dp] >> pdesc[dp].key_shift);
+    init[t] = static_cast<unsigned long long>(mod[t].collect_sum) << pdesc[dp].key_shift;
+    CSM_HIP(hipMemcpyAsync(dpairs + dp, &mod[t], sizeof(Pair3Desc), hipMemcpyHostToDevice, st));
+    CSM_HIP(hipMemcpyAsync(ctx->f3_best.as<unsigned long long>() + dp, &init[t],
+                           sizeof(unsigned long long), hipMemcpyHostToDevice, st));
+  }
+  CSM_HIP(hipMemsetAsync(ctx->f3_tie_count.ptr, 0, sizeof(int32_t) * nt, st));
+  CSM_HIP(hipMemsetAsync(ctx->f3_counter.ptr, 0, 8, st));
+  unsigned* dcounter = ctx->f3_counter.as<unsigned>();
+  if (items_small > 0)
+    CSM_HIP(LaunchFast3dSearch(false, std::max(1, std::min(items_small, ctx->num_cus * kSearch3dBlocksPerCu)),
+                               st, dsub, dpairs, tyaws, 0, items_small, ctx->f3_points.as<float>(),
+                               ctx->f3_low_points.as<float>(), dcounter,
+                               ctx->f3_best.as<unsigned long long>(), ctx->f3_status.as<int32_t>(),
+                               nullptr, ctx->f3_spill.as<int4>(),
+                               ctx->f3_best_hi.as<unsigned long long>(), ctx->f3_ties.as<uint4>(),
+                               ctx->f3_tie_count.as<int32_t>()));
+  if (items > items_small)
+    CSM_HIP(LaunchFast3dSearch(true, std::max(1, std::min(items - items_small,
+                                                          ctx->num_cus * kSearch3dBlocksPerCuLarge)),
+                               st, dsub, dpairs, tyaws, items_small, items - items_small,
+                               ctx->f3_points.as<float>(), ctx->f3_low_points.as<float>(),
+                               dcounter + 1, ctx->f3_best.as<unsigned long long>(),
+                               ctx->f3_status.as<int32_t>(), nullptr, ctx->f3_spill.as<int4>(),
+                               ctx->f3_best_hi.as<unsigned long long>(), ctx->f3_ties.as<uint4>(),
+                               ctx->f3_tie_count.as<int32_t>()));
+  std::vector<int32_t> counts(nt), stat2(np);
+  std::vector<uint4> leaves_all(static_cast<size_t>(kTieCap3d) * nt);
+  CSM_HIP(hipMemcpyAsync(counts.data(), ctx->f3_tie_count.ptr, sizeof(int32_t) * nt,
+                         hipMemcpyDeviceToHost, st));
+  CSM_HIP(hipMemcpyAsync(leaves_all.data(), ctx->f3_ties.ptr, sizeof(uint4) * leaves_all.size(),
+                         hipMemcpyDeviceToHost, st));
+  CSM_HIP(hipMemcpyAsync(stat2.data(), ctx->f3_status.ptr, sizeof(int32_t) * np,
+                         hipMemcpyDeviceToHost, st));
+  // The pair descriptors back as the finalize kernel reads them.
+  for (int t = 0; t < nt; ++t)
+    CSM_HIP(hipMemcpyAsync(dpairs + tied[t], &pdesc[tied[t]], sizeof(Pair3Desc),
+                           hipMemcpyHostToDevice, st));
+  CSM_HIP(hipStreamSynchronize(st));
+
+  // (2) Ancestor scores at every reference depth 1..D (D = max_depth).
+  struct Work {
+    int dp, t, D, first, count;
+  };
+  std::vector<Work> work;
+  std::vector<int4> lv;  // per leaf: (yaw, x, y, z)
+  std::vector<Score3Job> jobs;
+  std::vector<int4> queries;
+  std::vector<int> leaf_query;  // per leaf: index of its depth-1 ancestor query
+  for (int t = 0; t < nt; ++t) {
+    const int dp = tied[t];
+    const Pair3Desc& d = pdesc[dp];
+    const int cnt = counts[t];
+    if (stat2[dp] < 0 || cnt < 2 || cnt > kTieCap3d) {
+      ctx->t.ties_unresolved_3d += 1;
+      (*code)[dp] = CSM_TIE_UNRESOLVED;
+      continue;
+    }
+    const int D = submaps[d.submap]->desc.num_levels - 1;
+    Work w{dp, t, D, static_cast<int>(lv.size()), cnt};
+    std::vector<std::vector<int>> by_yaw(d.num_yaws);
+    for (int i = 0; i < cnt; ++i) {
+      const uint4 e = leaves_all[static_cast<size_t>(t) * kTieCap3d + i];
+      lv.push_back(make_int4(static_cast<int>(e.x), static_cast<int>(e.y), static_cast<int>(e.z),
+                             static_cast<int>(e.w)));
+      if (static_cast<int>(e.x) < d.num_yaws) by_yaw[e.x].push_back(w.first + i);
+    }
+    leaf_query.resize(lv.size(), -1);
+    for (int j = 0; j < d.num_yaws; ++j) {
+      if (by_yaw[j].empty() || D < 1) continue;
+      Score3Job job{d.yaw_begin + j, static_cast<int32_t>(queries.size()), 0, 0};
+      for (int li : by_yaw[j]) {
+        leaf_query[li] = static_cast<int>(queries.size());
+        for (int l = 1; l <= D; ++l)
+          queries.push_back(make_int4(l, -d.wxy + (((lv[li].y + d.wxy) >> l) << l),
+                                      -d.wxy + (((lv[li].z + d.wxy) >> l) << l),
+                                      -d.wz + (((lv[li].w + d.wz) >> l) << l)));
+      }
+      job.count = static_cast<int32_t>(queries.size()) - job.first;
+      jobs.push_back(job);
+    }
+    work.push_back(w);
+  }
+  auto score = [&](const std::vector<Score3Job>& js, const std::vector<int4>& qs,
+                   std::vector<int32_t>* sums) -> int {
+    sums->assign(qs.size(), 0);
+    if (js.empty()) return CSM_OK;
+    int r2;
+    if ((r2 = ctx->f3_sq_jobs.Reserve(sizeof(Score3Job) * js.size()))) return r2;
+    if ((r2 = ctx->f3_sq_queries.Reserve(sizeof(int4) * qs.size()))) return r2;
+    if ((r2 = ctx->f3_sq_sums.Reserve(sizeof(int32_t) * qs.size()))) return r2;
+    CSM_HIP(hipMemcpyAsync(ctx->f3_sq_jobs.ptr, js.data(), sizeof(Score3Job) * js.size(),
+                           hipMemcpyHostToDevice, st));
+    CSM_HIP(hipMemcpyAsync(ctx->f3_sq_queries.ptr, qs.data(), sizeof(int4) * qs.size(),
+                           hipMemcpyHostToDevice, st));
+    CSM_HIP(LaunchFast3dScoreQueries(static_cast<int>(js.size()), st, dsub, dpairs, dyaws,
+                                     ctx->f3_points.as<float>(), ctx->f3_sq_jobs.as<Score3Job>(),
+                                     ctx->f3_sq_queries.as<int4>(), ctx->f3_sq_sums.as<int32_t>()));
+    CSM_HIP(hipMemcpyAsync(sums->data(), ctx->f3_sq_sums.ptr, sizeof(int32_t) * qs.size(),
+                           hipMemcpyDeviceToHost, st));
+    CSM_HIP(hipStreamSynchronize(st));
+    return CSM_OK;
+  };
+  std::vector<int32_t> sums;
+  if ((rc = score(jobs, queries, &sums))) return rc;
+  // Ancestor of leaf li at depth l: (yaw, x, y, z, score).
+  struct Anc {
+    int yaw, x, y, z;
+    float score;
+  };
+  auto anc = [&](const Work& w, int li, int l) {
+    const Pair3Desc& d = pdesc[w.dp];
+    if (l == 0) return Anc{lv[li].x, lv[li].y, lv[li].z, lv[li].w, 0.f};
+    const int4 q = queries[leaf_query[li] + l - 1];
+    return Anc{lv[li].x, q.y, q.z, q.w, SumToProbability(sums[leaf_query[li] + l - 1], d.num_points)};
+  };
+  // (3) Leaves under a highest-scoring lowest-resolution ancestor; the whole
+  // top list of pairs where two distinct such ancestors tie.
+  struct Cand {
+    std::vector<int> live;
+    bool need_perm = false;
+    int nx = 0, ny = 0, nz = 0;
+    std::vector<int64_t> pos;  // generation index -> sorted position
+  };
+  std::vector<Cand> cand(work.size());
+  std::vector<int> perm;
+  for (size_t wi = 0; wi < work.size(); ++wi) {
+    const Work& w = work[wi];
+    Cand& c = cand[wi];
+    float top = -std::numeric_limits<float>::infinity();
+    for (int i = 0; i < w.count; ++i) top = std::max(top, anc(w, w.first + i, w.D).score);
+    std::vector<std::array<int, 4>> nodes;
+    for (int i = 0; i < w.count; ++i) {
+      const Anc a = anc(w, w.first + i, w.D);
+      if (w.D > 0 && a.score != top) continue;
+      c.live.push_back(w.first + i);
+      const std::array<int, 4> key{a.yaw, a.x, a.y, a.z};
+      if (std::find(nodes.begin(), nodes.end(), key) == nodes.end()) nodes.push_back(key);
+    }
+    c.need_perm = nodes.size() > 1;
+    (*code)[w.dp] = c.need_perm ? CSM_TIE_TOPLIST : CSM_TIE_ANCESTORS;
+    if (c.need_perm) perm.push_back(static_cast<int>(wi));
+  }
+  ctx->t.ties_toplist += static_cast<int64_t>(perm.size());
+  if (!perm.empty()) {
+    std::vector<Score3Job> tj;
+    std::vector<int4> tq;
+    std::vector<int64_t> base(perm.size());
+    for (size_t k = 0; k < perm.size(); ++k) {
+      const Work& w = work[perm[k]];
+      Cand& c = cand[perm[k]];
+      const Pair3Desc& d = pdesc[w.dp];
+      const int step = 1 << w.D;
+      c.nx = c.ny = (2 * d.wxy + step) / step;  // GenerateLowestResolutionCandidates (:301-310)
+      c.nz = (2 * d.wz + step) / step;
+      base[k] = static_cast<int64_t>(tq.size());
+      for (int j = 0; j < d.num_yaws; ++j) {
+        Score3Job job{d.yaw_begin + j, static_cast<int32_t>(tq.size()), 0, 0};
+        for (int z = -d.wz; z <= d.wz; z += step)
+          for (int y = -d.wxy; y <= d.wxy; y += step)
+            for (int x = -d.wxy; x <= d.wxy; x += step) tq.push_back(make_int4(w.D, x, y, z));
+        job.count = static_cast<int32_t>(tq.size()) - job.first;
+        tj.push_back(job);
+      }
+    }
+    std::vector<int32_t> ts;
+    if ((rc = score(tj, tq, &ts))) return rc;
+    for (size_t k = 0; k < perm.size(); ++k) {
+      const Work& w = work[perm[k]];
+      Cand& c = cand[perm[k]];
+      const int64_t n = static_cast<int64_t>(pdesc[w.dp].num_yaws) * c.nx * c.ny * c.nz;
+      // ScoreCandidates' std::sort(greater<Candidate3D>) on the generation
+      // order: the same comparisons give the same permutation for any element.
+      std::vector<std::pair<float, int32_t>> lst(n);
+      for (int64_t i = 0; i < n; ++i)
+        lst[i] = {SumToProbability(ts[base[k] + i], pdesc[w.dp].num_points), static_cast<int32_t>(i)};
+      IntroSort(lst.data(), lst.data() + n,
+                [](const std::pair<float, int32_t>& a, const std::pair<float, int32_t>& b) {
+                  return a.first > b.first;
+                },
+                8);
+      c.pos.resize(n);
+      for (int64_t i = 0; i < n; ++i) c.pos[lst[i].second] = i;
+    }
+  }
+  // (4) The reference's first leaf among the live ones.
+  for (size_t wi = 0; wi < work.size(); ++wi) {
+    const Work& w = work[wi];
+    const Cand& c = cand[wi];
+    const Pair3Desc& d = pdesc[w.dp];
+    const int step = 1 << w.D;
+    auto top_pos = [&](const Anc& a) {
+      const int ix = (a.x + d.wxy) / step, iy = (a.y + d.wxy) / step, iz = (a.z + d.wz) / step;
+      return c.pos[((static_cast<int64_t>(a.yaw) * c.nz + iz) * c.ny + iy) * c.nx + ix];
+    };
+    auto first = [&](int a, int b) {
+      for (int l = w.D; l >= 0; --l) {
+        const Anc x = anc(w, a, l), y = anc(w, b, l);
+        if (x.yaw == y.yaw && x.x == y.x && x.y == y.y && x.z == y.z) continue;
+        if (l == w.D) {  // lowest-resolution candidates: score, then the sorted order
+          if (l > 0 && x.score != y.score) return x.score > y.score;
+          return top_pos(x) < top_pos(y);
+        }
+        if (l > 0 && x.score != y.score) return x.score > y.score;
+        // Siblings of one parent: generation order (z, then y, then x).
+        return std::make_tuple(x.z, x.y, x.x) < std::make_tuple(y.z, y.y, y.x);
+      }
+      return false;
+    };
+    int best = c.live[0];
+    for (size_t i = 1; i < c.live.size(); ++i)
+      if (first(c.live[i], best)) best = c.live[i];
+    const unsigned long long mask = (1ull << d.key_shift) - 1;
+    const unsigned long long sum = (*keys)[w.dp] >> d.key_shift;
+    (*keys)[w.dp] = (sum << d.key_shift) |
+                    (~LeafId3(d, lv[best].x, lv[best].y, lv[best].z, lv[best].w) & mask);
+  }
+  return CSM_OK;
+}
+
 }  // namespace
 
 int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t num_submaps,
@@ -1261,6 +1575,9 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
     return rc;
   if ((rc = ctx->f3_yaws.Reserve(sizeof(Yaw3Desc) * std::max(ny, 1)))) return rc;
   if ((rc = ctx->f3_best.Reserve(sizeof(unsigned long long) * np + sizeof(float) * np))) return rc;
+  if ((rc = ctx->f3_best_hi.Reserve(sizeof(unsigned long long) * np))) return rc;
+  if ((rc = ctx->f3_tie_count.Reserve(sizeof(int32_t)))) return rc;
+  if ((rc = ctx->f3_ties.Reserve(sizeof(uint4)))) return rc;
   if ((rc = ctx->f3_status.Reserve(sizeof(int32_t) * np))) return rc;
   if ((rc = ctx->f3_counter.Reserve(8 + 16 * sizeof(unsigned long long)))) return rc;
   Pair3Desc* dpairs = ctx->f3_pairs.as<Pair3Desc>();
@@ -1351,6 +1668,7 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
   }
   CSM_HIP(hipStreamWaitEvent(st, ctx->f3_points_ready, 0));
   CSM_HIP(hipMemsetAsync(dbest, 0, sizeof(unsigned long long) * np, st));
+  CSM_HIP(hipMemsetAsync(ctx->f3_best_hi.ptr, 0, sizeof(unsigned long long) * np, st));
   CSM_HIP(hipMemsetAsync(ctx->f3_status.ptr, 0, sizeof(int32_t) * np, st));
   CSM_HIP(hipMemsetAsync(ctx->f3_counter.ptr, 0, 8 + 16 * sizeof(unsigned long long), st));
   lap(4);
@@ -1365,25 +1683,28 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
     CSM_HIP(LaunchFast3dSearch(false, grid, st, dsub, dpairs, ctx->f3_yaws.as<Yaw3Desc>(), 0,
                                ny_small, ctx->f3_points.as<float>(),
                                ctx->f3_low_points.as<float>(), dcounter, dbest,
-                               ctx->f3_status.as<int32_t>(), dstats, ctx->f3_spill.as<int4>()));
+                               ctx->f3_status.as<int32_t>(), dstats, ctx->f3_spill.as<int4>(),
+                               ctx->f3_best_hi.as<unsigned long long>(), ctx->f3_ties.as<uint4>(),
+                               ctx->f3_tie_count.as<int32_t>()));
   }
   if (ny > ny_small) {
     const int grid = std::max(1, std::min(ny - ny_small, ctx->num_cus * kSearch3dBlocksPerCuLarge));
     CSM_HIP(LaunchFast3dSearch(true, grid, st, dsub, dpairs, ctx->f3_yaws.as<Yaw3Desc>(), ny_small,
                                ny - ny_small, ctx->f3_points.as<float>(),
                                ctx->f3_low_points.as<float>(), dcounter + 1, dbest,
-                               ctx->f3_status.as<int32_t>(), dstats, ctx->f3_spill.as<int4>()));
+                               ctx->f3_status.as<int32_t>(), dstats, ctx->f3_spill.as<int4>(),
+                               ctx->f3_best_hi.as<unsigned long long>(), ctx->f3_ties.as<uint4>(),
+                               ctx->f3_tie_count.as<int32_t>()));
   }
   if (ctx->timing) CSM_HIP(hipEventRecord(ctx->ev1, st));
-  CSM_HIP(LaunchFast3dFinalize(np, st, dsub, dpairs, ctx->f3_yaws.as<Yaw3Desc>(),
-                               ctx->f3_low_points.as<float>(), dbest, dlow));
-  std::vector<unsigned long long> keys(np);
+  std::vector<unsigned long long> keys(np), keys_hi(np);
   std::vector<float> lows(np);
   std::vector<int32_t> stat(np);
   unsigned long long lookups = 0, prof[16] = {0};
   CSM_HIP(hipMemcpyAsync(keys.data(), dbest, sizeof(unsigned long long) * np,
                          hipMemcpyDeviceToHost, st));
-  CSM_HIP(hipMemcpyAsync(lows.data(), dlow, sizeof(float) * np, hipMemcpyDeviceToHost, st));
+  CSM_HIP(hipMemcpyAsync(keys_hi.data(), ctx->f3_best_hi.ptr, sizeof(unsigned long long) * np,
+                         hipMemcpyDeviceToHost, st));
   CSM_HIP(hipMemcpyAsync(stat.data(), ctx->f3_status.ptr, sizeof(int32_t) * np,
                          hipMemcpyDeviceToHost, st));
   CSM_HIP(hipMemcpyAsync(prof, dstats, sizeof(prof), hipMemcpyDeviceToHost, st));
@@ -1394,6 +1715,20 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
     CSM_HIP(hipMemcpyAsync(ys.data(), dev_s, sizeof(float) * kept, hipMemcpyDeviceToHost, st));
   }
   CSM_HIP(hipStreamSynchronize(st));
+  // Exactly tied maxima: the reference's pick (ResolveTies3d), then the
+  // winning leaves' low-resolution scores (the Result field).
+  std::vector<int8_t> tie_code(np, CSM_TIE_NONE);
+  {
+    const std::vector<unsigned long long> before = keys;
+    if ((rc = ResolveTies3d(ctx, submaps, pdesc, stat, keys_hi, &keys, &tie_code))) return rc;
+    if (keys != before)
+      CSM_HIP(hipMemcpyAsync(dbest, keys.data(), sizeof(unsigned long long) * np,
+                             hipMemcpyHostToDevice, st));
+    CSM_HIP(LaunchFast3dFinalize(np, st, dsub, dpairs, ctx->f3_yaws.as<Yaw3Desc>(),
+                                 ctx->f3_low_points.as<float>(), dbest, dlow));
+    CSM_HIP(hipMemcpyAsync(lows.data(), dlow, sizeof(float) * np, hipMemcpyDeviceToHost, st));
+    CSM_HIP(hipStreamSynchronize(st));
+  }
   if (ctx->timing) {
     float ms = 0.f;
     CSM_HIP(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
@@ -1448,6 +1783,7 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
     results[i].pose = ToPose(t, Q4{y.nw, y.nx, y.ny, y.nz});
     results[i].rotational_score = y.rotational_score;
     results[i].low_resolution_score = lows[dp];
+    results[i].tie = tie_code[dp];
   }
   return CSM_OK;
 }

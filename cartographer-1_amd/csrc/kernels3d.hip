@@ -72,6 +72,18 @@ __global__ void brick_from_values(const uint16_t* __restrict__ values, int64_t n
   if (level0) level0[i] = qtab[v];
 }
 
+// A HybridGrid's known cells (the list its iterator yields) into the zeroed
+// dense brick: cell i at its offset in the brick (the list holds each cell
+// once, as HybridGrid's iteration / ToProto does).
+__global__ void brick_scatter(const int32_t* __restrict__ ijk, const uint16_t* __restrict__ values,
+                              int64_t count, Brick3 b, uint16_t* __restrict__ out) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  const int64_t k = (static_cast<int64_t>(ijk[3 * i + 2] - b.oz) * b.ny + (ijk[3 * i + 1] - b.oy)) * b.nx +
+                    (ijk[3 * i] - b.ox);
+  out[k] = values[i];
+}
+
 // PrecomputeGrid (precomputation_grid_3d.cc:63-81) in gather form:
 // out[j] = max over octants o of prev[j + shift*o], or, at half resolution,
 // max over o and e in {0,1}^3 of prev[2j + e + shift*o].
@@ -793,7 +805,7 @@ struct F3SharedT {
   int tcell[kTopCells3d];
   uint16_t tcount[kTopCells3d];
   int ntcell;
-  int nbatch, nleaf, sp, item, error, accepted, cached_submap, high_water;
+  int nbatch, nleaf, sp, item, error, skip, cached_submap, high_water;
   unsigned long long best;
   unsigned long long best_seen;  // last read of the pair's global best
 };
@@ -881,7 +893,9 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
               const float* __restrict__ points,
               const float* __restrict__ low_points, unsigned* __restrict__ counter,
               unsigned long long* __restrict__ best, int32_t* __restrict__ status,
-              unsigned long long* __restrict__ stats, int4* __restrict__ spill_base) {
+              unsigned long long* __restrict__ stats, int4* __restrict__ spill_base,
+              unsigned long long* __restrict__ best_hi, uint4* __restrict__ ties,
+              int32_t* __restrict__ tie_count) {
   __shared__ F3SharedT<kPts> sh;
   const int tid = threadIdx.x;
   unsigned long long lookups = 0, root_lookups = 0;
@@ -1448,7 +1462,9 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
           const unsigned long long id = LeafId(pd, yw.yaw_id, cxk, cyk, czk);
           const unsigned long long key = (static_cast<unsigned long long>(my) << pd.key_shift) |
                                          (~id & ((1ull << pd.key_shift) - 1));
-          if (key > sh.best) {
+          // Leaves at the best sum too (not only above the best key): a
+          // second leaf at the maximum is the tie witness.
+          if (my >= best_sum) {
             const int at = atomicAdd(&sh.nleaf, 1);
             sh.leaf_keys[at] = key;
             sh.leaf_x[at] = cxk;
@@ -1467,7 +1483,12 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
       const int nl = sh.nleaf;
       if (nl == 0) continue;
       // Leaves: descending key order; the first that passes the
-      // low-resolution check (:384-401) beats every later one.
+      // low-resolution check (:384-401) beats every later one. Leaves at the
+      // best sum that do not beat its key are still checked (witness path):
+      // one that passes is a second leaf at the maximum, recorded in best_hi
+      // (sum << shift | leaf id, the largest id) so the host can tell an
+      // exact tie (host3d.cc ResolveTies3d); once best_hi shows a tie at the
+      // current best sum, further witnesses are skipped unless collecting.
       if (tid == 0) {
         for (int a = 1; a < nl; ++a) {
           const unsigned long long kk = sh.leaf_keys[a];
@@ -1485,27 +1506,48 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
           sh.leaf_y[b2 + 1] = y;
           sh.leaf_z[b2 + 1] = z;
         }
-        sh.accepted = 0;
         sh.best = max(sh.best, *reinterpret_cast<volatile unsigned long long*>(best + yw.pair));
       }
       __syncthreads();
+      const unsigned long long id_mask = (1ull << pd.key_shift) - 1;
       for (int a = 0; a < nl; ++a) {
-        if (sh.leaf_keys[a] <= sh.best) break;  // uniform: sh.best is shared
+        const unsigned long long lkey = sh.leaf_keys[a], cur = sh.best;  // uniform: shared
+        const int lsum = static_cast<int>(lkey >> pd.key_shift);
+        if (lsum < static_cast<int>(cur >> pd.key_shift)) break;
+        const bool witness = lkey <= cur;
+        if (witness && !pd.collect) {
+          if (tid == 0) {
+            const unsigned long long hi =
+                *reinterpret_cast<volatile unsigned long long*>(best_hi + yw.pair);
+            sh.skip = static_cast<int>(hi >> pd.key_shift) == lsum &&
+                      (hi & id_mask) != (~cur & id_mask);
+          }
+          __syncthreads();
+          if (sh.skip) continue;
+        }
         const float rf = res;
         const float tx = __fadd_rn(yw.tx, __fmul_rn(rf, static_cast<float>(sh.leaf_x[a])));
         const float ty = __fadd_rn(yw.ty, __fmul_rn(rf, static_cast<float>(sh.leaf_y[a])));
         const float tz = __fadd_rn(yw.tz, __fmul_rn(rf, static_cast<float>(sh.leaf_z[a])));
         const float lrs = LowResScore(sh, sm, low_points + 3 * pd.low_offset, pd.num_low, yw.nw,
                                       yw.nx, yw.ny, yw.nz, tx, ty, tz);
-        if (tid == 0) {
-          if (static_cast<double>(lrs) >= static_cast<double>(pd.min_low_resolution_score)) {
-            atomicMax(best + yw.pair, sh.leaf_keys[a]);
-            sh.best = max(sh.best, sh.leaf_keys[a]);
-            sh.accepted = 1;
+        if (tid == 0 && static_cast<double>(lrs) >= static_cast<double>(pd.min_low_resolution_score)) {
+          const unsigned long long lid = ~lkey & id_mask;
+          if (!witness) {
+            atomicMax(best + yw.pair, lkey);
+            sh.best = max(sh.best, lkey);
+          }
+          atomicMax(best_hi + yw.pair, (static_cast<unsigned long long>(lsum) << pd.key_shift) | lid);
+          if (pd.collect && lsum == pd.collect_sum) {  // collect = tie slot + 1
+            const int slot = pd.collect - 1;
+            const int at = atomicAdd(tie_count + slot, 1);
+            if (at < kTieCap3d)
+              ties[static_cast<int64_t>(slot) * kTieCap3d + at] =
+                  make_uint4(static_cast<unsigned>(yw.yaw_id), static_cast<unsigned>(sh.leaf_x[a]),
+                             static_cast<unsigned>(sh.leaf_y[a]), static_cast<unsigned>(sh.leaf_z[a]));
           }
         }
         __syncthreads();
-        if (sh.accepted) break;
       }
       __syncthreads();
       F3_COUNT(6, nl);
@@ -1520,6 +1562,66 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
   if ((tid & 63) == 0 && stats && lookups) atomicAdd(stats, lookups);
   if (tid == 0 && stats) atomicMax(stats + kStat3dHighWater, static_cast<unsigned long long>(sh.high_water));
   F3_FLUSH(stats);
+}
+
+// The reference's ScoreCandidates sum (:332-352) for tie resolution
+// (host3d.cc ResolveTies3d): per job, one yaw item's cloud discretized as the
+// search does (DiscretizeScan :201-244), then for each (depth, x, y, z) query
+// the sum over points of level `depth` at the point's cell at that depth plus
+// the offset >> the depth's reduction exponent; cells outside the level's
+// brick read 0 (PrecomputationGrid3D::value of an unknown cell).
+__global__ void __launch_bounds__(kSearch3dThreads)
+fast3d_score_queries(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restrict__ pairs,
+                     const Yaw3Desc* __restrict__ yaws, const float* __restrict__ points,
+                     const Score3Job* __restrict__ jobs, const int4* __restrict__ queries,
+                     int32_t* __restrict__ sums) {
+  __shared__ int16_t cx[kMax3dPoints], cy[kMax3dPoints], cz[kMax3dPoints];
+  __shared__ int part[kSearch3dThreads / 64];
+  const int tid = threadIdx.x;
+  const Score3Job job = jobs[blockIdx.x];
+  const Yaw3Desc yw = yaws[job.item];
+  const Pair3Desc pd = pairs[yw.pair];
+  const Submap3Desc& sm = submaps[pd.submap];
+  const int n = min(pd.num_points, kMax3dPoints);
+  const float res = sm.resolution, inv = 1.f / sm.resolution;
+  for (int i = tid; i < n; i += kSearch3dThreads) {
+    const float* p = points + 3 * (pd.point_offset + i);
+    float ox, oy, oz;
+    Rotate3(yw.qw, yw.qx, yw.qy, yw.qz, p[0], p[1], p[2], &ox, &oy, &oz);
+    cx[i] = static_cast<int16_t>(RoundDiv(__fadd_rn(ox, yw.tx), res, inv));
+    cy[i] = static_cast<int16_t>(RoundDiv(__fadd_rn(oy, yw.ty), res, inv));
+    cz[i] = static_cast<int16_t>(RoundDiv(__fadd_rn(oz, yw.tz), res, inv));
+  }
+  __syncthreads();
+  for (int q = 0; q < job.count; ++q) {
+    const int4 qq = queries[job.first + q];
+    const int d = qq.x;
+    const int e = max(0, d - sm.full_resolution_depth + 1);
+    const bool reduced = d >= sm.full_resolution_depth;
+    const int lx = (-pd.wxy) >> e, ly = (-pd.wxy) >> e, lz = (-pd.wz) >> e;
+    const Brick3 b = sm.level[d];
+    const uint8_t* lv = sm.levels + b.offset;
+    int sum = 0;
+    for (int i = tid; i < n; i += kSearch3dThreads) {
+      int x = cx[i], y = cy[i], z = cz[i];
+      if (reduced) {
+        x = ((x - pd.wxy) >> e) - lx;
+        y = ((y - pd.wxy) >> e) - ly;
+        z = ((z - pd.wz) >> e) - lz;
+      }
+      int64_t idx;
+      if (InBrick(b, x + (qq.y >> e), y + (qq.z >> e), z + (qq.w >> e), &idx)) sum += lv[idx];
+    }
+    for (int m = 32; m > 0; m >>= 1) sum += __shfl_xor(sum, m, 64);
+    if ((tid & 63) == 0) part[tid >> 6] = sum;
+    __syncthreads();
+    if (tid == 0) {
+      int t = 0;
+      for (int w = 0; w < kSearch3dThreads / 64; ++w) t += part[w];
+      sums[job.first + q] = t;
+    }
+    __syncthreads();
+  }
 }
 
 // Low-resolution score of each pair's winning leaf (the Result field), with
@@ -1982,15 +2084,36 @@ hipError_t LaunchFast3dSearch(bool large, int grid, hipStream_t st, const Submap
                               const Pair3Desc* pairs, const Yaw3Desc* yaws, int item_begin,
                               int num_items, const float* points, const float* low_points,
                               unsigned* counter, unsigned long long* best, int32_t* status,
-                              unsigned long long* stats, int4* spill) {
+                              unsigned long long* stats, int4* spill, unsigned long long* best_hi,
+                              uint4* ties, int32_t* tie_count) {
   if (large)
     hipLaunchKernelGGL((fast3d_search<kMax3dPoints, kSearch3dBlocksPerCuLarge>), dim3(grid),
                        dim3(kSearch3dThreads), 0, st, submaps, pairs, yaws, item_begin, num_items,
-                       points, low_points, counter, best, status, stats, spill);
+                       points, low_points, counter, best, status, stats, spill, best_hi, ties,
+                       tie_count);
   else
     hipLaunchKernelGGL((fast3d_search<kSmall3dPoints, kSearch3dBlocksPerCu>), dim3(grid),
                        dim3(kSearch3dThreads), 0, st, submaps, pairs, yaws, item_begin, num_items,
-                       points, low_points, counter, best, status, stats, spill);
+                       points, low_points, counter, best, status, stats, spill, best_hi, ties,
+                       tie_count);
+  return hipGetLastError();
+}
+
+hipError_t LaunchBrickScatter(const int32_t* ijk, const uint16_t* values, int64_t count,
+                              const Brick3& b, uint16_t* out, hipStream_t st) {
+  if (count <= 0) return hipSuccess;
+  hipLaunchKernelGGL(brick_scatter, dim3(static_cast<unsigned>((count + 255) / 256)), dim3(256), 0, st,
+                     ijk, values, count, b, out);
+  return hipGetLastError();
+}
+
+hipError_t LaunchFast3dScoreQueries(int num_jobs, hipStream_t st, const Submap3Desc* submaps,
+                                    const Pair3Desc* pairs, const Yaw3Desc* yaws,
+                                    const float* points, const Score3Job* jobs,
+                                    const int4* queries, int32_t* sums) {
+  if (num_jobs <= 0) return hipSuccess;
+  hipLaunchKernelGGL(fast3d_score_queries, dim3(num_jobs), dim3(kSearch3dThreads), 0, st, submaps,
+                     pairs, yaws, points, jobs, queries, sums);
   return hipGetLastError();
 }
 

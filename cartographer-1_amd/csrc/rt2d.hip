@@ -135,11 +135,27 @@ __device__ __forceinline__ unsigned long long PenalizedKey(float sum, double res
          static_cast<unsigned long long>(0xffffffffu - idx);
 }
 
-template <bool kTsdf, int kDepth>
+// The fused path's per-call inputs (rt2d_score<..., kFused = true>): the
+// discretization of rt2d_discretize done by each workgroup for its own
+// rotation into LDS, so Match is one launch.
+struct Rt2dDisc {
+  const float* points;
+  const float2* rot;
+  float pre_w, pre_s, tx, ty;
+  double max_x, max_y, res;
+  int nx, ny, P;
+  const uint32_t* warm;
+  int warm_words;
+  uint32_t* sink;
+  unsigned* done;                        // workgroups finished (0 between calls)
+  unsigned long long* result;            // the winning key, in mapped host memory
+};
+
+template <bool kTsdf, int kDepth, bool kFused>
 __global__ void __launch_bounds__(64)
 rt2d_score(Rt2dGridDev grid, int grid_bytes, const int* __restrict__ bases, int n, int npad,
            int side, int parts_x, int L, int num_angular, double step, double res,
-           double wt, double wr, unsigned long long* __restrict__ best) {
+           double wt, double wr, unsigned long long* __restrict__ best, Rt2dDisc disc) {
   // Workgroup = (rotation, y offset, chunk of x offsets); lane = x offset.
   // Lanes then read one grid row (x is the fastest index), so a gather
   // touches one or two cache lines.
@@ -153,9 +169,41 @@ rt2d_score(Rt2dGridDev grid, int grid_bytes, const int* __restrict__ bases, int 
   // Candidate order of GenerateExhaustiveSearchCandidates: (scan, x, y).
   const int t = (valid ? xi : 0) * side + yi;
   const int off = yo * grid.W + xo;
+  extern __shared__ int4 lds_bases[];
+  if constexpr (kFused) {
+    // Warm this XCD's L2 with the padded grid (as rt2d_discretize does),
+    // then discretize the rotation's points into LDS with rt2d_discretize's
+    // arithmetic; the padding slots point inside the padded grid.
+    {
+      const int xcd_blocks = (gridDim.x + kNumXcd - 1 - blockIdx.x % kNumXcd) / kNumXcd;
+      const int slot = blockIdx.x / kNumXcd;
+      uint32_t acc = 0;
+      for (int i = (slot * 64 + lane) * 32; i < disc.warm_words; i += xcd_blocks * 64 * 32)
+        acc ^= disc.warm[i];
+      if (acc == 0x9e3779b9u) disc.sink[0] = acc;
+    }
+    int* sb = reinterpret_cast<int*>(lds_bases);
+    const int W = disc.nx + 2 * disc.P;
+    const float2 q = disc.rot[r];
+    for (int i = lane; i < npad; i += 64) {
+      if (i >= n) {
+        sb[i] = disc.P * W + disc.P;
+        continue;
+      }
+      float x, y;
+      RotateZDev(disc.pre_w, disc.pre_s, disc.points[3 * i], disc.points[3 * i + 1], &x, &y);
+      RotateZDev(q.x, q.y, x, y, &x, &y);
+      const float px = __fadd_rn(disc.tx, x), py = __fadd_rn(disc.ty, y);
+      const double cx = fmin(fmax(CellCoord(disc.max_y, py, disc.res), -(L + 1.)), disc.nx + static_cast<double>(L));
+      const double cy = fmin(fmax(CellCoord(disc.max_x, px, disc.res), -(L + 1.)), disc.ny + static_cast<double>(L));
+      sb[i] = (static_cast<int>(cy) + disc.P) * W + static_cast<int>(cx) + disc.P;
+    }
+    __syncthreads();
+  }
   // The rotation's point indices: wave-uniform, 16-byte aligned (npad is a
-  // multiple of kDepth), read with scalar loads.
-  const int4* __restrict__ B = reinterpret_cast<const int4*>(bases + static_cast<int64_t>(r) * npad);
+  // multiple of kDepth), read with scalar loads (LDS broadcasts when fused).
+  const int4* __restrict__ B = kFused ? lds_bases
+                                      : reinterpret_cast<const int4*>(bases + static_cast<int64_t>(r) * npad);
   const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
       kTsdf ? static_cast<void*>(const_cast<float2*>(grid.tsdf))
             : static_cast<void*>(const_cast<float*>(grid.prob)),
@@ -247,6 +295,23 @@ rt2d_score(Rt2dGridDev grid, int grid_bytes, const int* __restrict__ bases, int 
     key = o > key ? o : key;
   }
   if (lane == 0 && key != 0) atomicMax(best, key);
+  if constexpr (kFused) {
+    // The last workgroup to finish hands the winner to the host (mapped
+    // memory) and resets the key and the counter for the next call, so a
+    // Match is one upload, one launch and one synchronize.
+    if (lane == 0) {
+      __threadfence();
+      const unsigned done = atomicAdd(disc.done, 1u);
+      if (done == gridDim.x - 1) {
+        __threadfence();
+        const unsigned long long k = atomicOr(best, 0ull);
+        disc.result[0] = k;
+        __threadfence_system();
+        *best = 0ull;
+        *disc.done = 0u;
+      }
+    }
+  }
 }
 
 struct CandDev {

@@ -214,6 +214,7 @@ class Result:
     pose_estimate: tuple
     rotational_score: float
     low_resolution_score: float
+    tie: int = 0  # csm_result3d.tie (TIE_*): how the pick among exactly tied leaves was made
 
 
 def _result(r: Result3D) -> Optional[Result]:
@@ -221,7 +222,7 @@ def _result(r: Result3D) -> Optional[Result]:
     if r.status != CSM_OK:
         return None
     return Result(float(r.score), r.pose.as_tuple(), float(r.rotational_score),
-                  float(r.low_resolution_score))
+                  float(r.low_resolution_score), int(r.tie))
 
 
 class FastCorrelativeScanMatcher3D:
@@ -290,7 +291,8 @@ PAIR3_DTYPE = np.dtype([("submap", np.int32), ("node", np.int32), ("full_submap"
                         ("submap_q", np.float64, 4)])
 RESULT3_DTYPE = np.dtype([("status", np.int32), ("score", np.float32), ("t", np.float64, 3),
                           ("q", np.float64, 4), ("rotational_score", np.float32),
-                          ("low_resolution_score", np.float32)])
+                          ("low_resolution_score", np.float32), ("tie", np.int32),
+                          ("reserved", np.int32)])
 
 
 def make_pairs_3d(submap, node, min_score, full_submap=True, node_q=None, node_t=None,

@@ -113,10 +113,10 @@ typedef struct csm_timing {
    * tied (counted whether or not timing is enabled). */
   int64_t tied_pairs;
   int64_t ties_unresolved;
-  /* Of tied_pairs: those whose pick needed the whole lowest-resolution list
-   * ordered (CSM_TIE_TOPLIST); the rest are CSM_TIE_ANCESTORS. 3D: pairs
-   * whose best sum was reached by more than one leaf, and those resolved
-   * past the device's first pick (csm_result3d.tie). */
+  /* Pairs (2D and 3D) whose pick needed the whole lowest-resolution list
+   * ordered (CSM_TIE_TOPLIST). 3D: pairs whose best sum was reached by more
+   * than one leaf passing the low-resolution check, and those left at the
+   * smallest (yaw, x, y, z) leaf (more than 4096 such leaves). */
   int64_t ties_toplist;
   int64_t tied_pairs_3d;
   int64_t ties_unresolved_3d;
@@ -443,6 +443,8 @@ typedef struct csm_result3d {
   csm_pose3d pose;
   float rotational_score;
   float low_resolution_score;
+  int32_t tie;    /* CSM_TIE_*: how the pick among exactly tied leaves was made */
+  int32_t reserved;
 } csm_result3d;
 
 /* std::unique_ptr<Result> Match(const Rigid3d& global_node_pose,

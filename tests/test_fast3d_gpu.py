@@ -2,8 +2,8 @@
 on the MI355X vs the oracle.
 
 Bar: pyramid levels byte-identical; FastCSM3D score, rotational score and
-low-resolution score identical floats, pose identical (or an exactly tied
-leaf); RTCSM3D score within 1e-6 relative (the double exp() penalty may
+low-resolution score identical floats, pose identical (including the
+reference's pick among exactly tied leaves); RTCSM3D score within 1e-6 relative (the double exp() penalty may
 differ from glibc in the last ulps) and the same winning candidate.
 
 Scenarios restate fast_correlative_scan_matcher_3d_test.cc:36-204 and
@@ -43,28 +43,23 @@ def gpu_grid(csm, og):
 
 def assert_same_result(gpu, ref, om=None, full=False, node_pose=None, submap_pose=None,
                        node=None, min_low=0.15):
-    """Identical result, or — when the GPU's leaf differs — an exactly tied leaf:
-    same score, passing the low-resolution check (the reference's pick among
-    equal scores follows its unstable std::sort, :353-354)."""
+    """Identical result: match decision, score, pose, rotational and
+    low-resolution scores. Among leaves that tie at the maximum and pass the
+    low-resolution check the reference returns the first its depth-first
+    search reaches (fast_correlative_scan_matcher_3d.cc:332-355, :377-440);
+    the GPU restores that pick (host3d.cc ResolveTies3d), so the pose must be
+    the oracle's in every case. Returns "tie" when the GPU reported resolving
+    a tie (csm_result3d.tie), else "exact"."""
     assert (gpu is not None) == ref["matched"], (gpu, ref)
     if gpu is None:
         return "nomatch"
     assert np.float32(gpu.score) == np.float32(ref["score"])
     (gt, gq), (rt, rq) = gpu.pose_estimate, ref["pose"]
-    if tuple(gt) == tuple(rt) and tuple(gq) == tuple(rq):
-        assert np.float32(gpu.rotational_score) == np.float32(ref["rotational_score"])
-        assert np.float32(gpu.low_resolution_score) == np.float32(ref["low_resolution_score"])
-        return "exact"
-    assert om is not None, ("leaf differs", gpu, ref)
-    if full:
-        node_pose, submap_pose = ((0, 0, 0), node_pose), ((0, 0, 0), submap_pose)
-    leaf = om.evaluate_leaf(full, node_pose, submap_pose, node, gpu.pose_estimate)
-    assert leaf is not None, ("GPU pose is not a leaf of the search", gpu)
-    assert np.float32(leaf["score"]) == np.float32(gpu.score)
-    assert np.float32(leaf["rotational_score"]) == np.float32(gpu.rotational_score)
-    assert np.float32(leaf["low_resolution_score"]) == np.float32(gpu.low_resolution_score)
-    assert leaf["low_resolution_score"] >= min_low
-    return "tie"
+    assert tuple(gt) == tuple(rt) and tuple(gq) == tuple(rq), \
+        ("pose differs from the reference's pick", gpu, ref)
+    assert np.float32(gpu.rotational_score) == np.float32(ref["rotational_score"])
+    assert np.float32(gpu.low_resolution_score) == np.float32(ref["low_resolution_score"])
+    return "tie" if getattr(gpu, "tie", 0) else "exact"
 
 
 def options(csm, depth, full_depth, **kw):
@@ -510,3 +505,77 @@ def test_rt3d_c4_full_window(csm, oracle):
         assert math.isclose(float(scores[k, tt]), ref, rel_tol=1e-6), (k, tt, scores[k, tt], ref)
         exact += float(scores[k, tt]) == ref
     assert exact >= 0.95 * len(sample)
+
+
+# ----------------------------------------------------------- exact ties ------
+def _tied_world(oracle, csm, shifts, depth):
+    """A sparse pattern of voxels copied at each shift (cells never collide):
+    the pattern's own points then reach the same sum at every copy, an exact
+    tie between leaves that all pass the low-resolution check."""
+    rng = np.random.RandomState(3)
+    base = np.unique(rng.randint(-4, 4, (40, 3)) * 3, axis=0)
+    vals = rng.randint(20000, 32768, len(base)).astype(np.uint16)
+    ijk = np.concatenate([base + np.array(s) for s in shifts])
+    og = oracle.hybrid_grid(0.05)
+    og.set_values(ijk, np.concatenate([vals] * len(shifts)))
+    o = options(csm, depth, 3)
+    hist = np.zeros(10, np.float32)
+    om = oracle.fast3d(og, og, hist, opt_tuple(o))
+    g = gpu_grid(csm, og)
+    gm = csm.FastCorrelativeScanMatcher3D(g, g, hist, o)
+    cloud = (base * 0.05).astype(np.float32)
+    return om, gm, g, csm.NodeData3D(cloud, cloud, hist)
+
+
+TIE_SHIFTS = [[(1, 0, 0), (0, 0, 1)], [(1, 1, 0), (0, 0, 1)], [(-9, 0, 0), (9, 0, 0)],
+              [(-7, 2, 1), (7, -2, -1)], [(2, 0, 0), (0, 0, 1)], [(0, 1, 0), (0, 0, 1)],
+              [(-1, 0, 1), (1, 0, 0)], [(0, 0, 0), (3, 0, 0), (0, 0, 3)]]
+
+
+@pytest.mark.parametrize("depth", [4, 6])
+def test_exact_ties_take_the_reference_pick(csm, oracle, depth):
+    """Leaves that tie at the maximum and all pass the low-resolution check:
+    the reference returns the first one its DFS reaches (sorted children,
+    generation order z, y, x among equal scores, the lowest-resolution list in
+    std::sort's order), which is often not the smallest (yaw, x, y, z) key
+    (e.g. (1, 0, 0) before (0, 0, 1) under one parent; +9 before -9 when the
+    two top-level candidates tie at depth 6). The GPU must return exactly the
+    oracle's pose, through Match and MatchFullSubmap, and report the tie."""
+    ident = ((0, 0, 0), (1, 0, 0, 0))
+    ties = 0
+    for shifts in TIE_SHIFTS:
+        om, gm, g, node = _tied_world(oracle, csm, shifts, depth)
+        for init in [(0.0, 0.0, 0.0), (0.01, -0.02, 0.0)]:
+            ref = om.match((init, (1, 0, 0, 0)), ident, node, 0.1)
+            gpu = gm.Match((init, (1, 0, 0, 0)), ident, node, 0.1)
+            ties += assert_same_result(gpu, ref) == "tie"
+        ref = om.match_full_submap((1, 0, 0, 0), (1, 0, 0, 0), node, 0.1)
+        gpu = gm.MatchFullSubmap((1, 0, 0, 0), (1, 0, 0, 0), node, 0.1)
+        ties += assert_same_result(gpu, ref) == "tie"
+    assert ties >= len(TIE_SHIFTS), ties
+
+
+def test_exact_ties_in_batches(csm, oracle):
+    """The same tied pairs inside one batch next to untied ones (the collect
+    search and the score queries index pairs and yaws of a whole batch)."""
+    ident = ((0, 0, 0), (1, 0, 0, 0))
+    mats, nodes, refs, keep = [], [], [], []
+    for shifts in TIE_SHIFTS[:4]:
+        om, gm, g, node = _tied_world(oracle, csm, shifts, 6)
+        keep.append((g, om))
+        mats.append(gm)
+        nodes.append(node)
+    pairs = []
+    for s in range(len(mats)):
+        for n in range(len(nodes)):
+            pairs.append((s, n, False, 0.1, ((0.0, 0.0, 0.0), (1, 0, 0, 0)), ident))
+            refs.append(keep[s][1].match(((0.0, 0.0, 0.0), (1, 0, 0, 0)), ident, nodes[n], 0.1))
+    res = csm.match_batch_3d(mats, nodes, pairs)
+    assert_search_ok(csm, [r.status for r in res])
+    tied = 0
+    for (s, n, *_), r, ref in zip(pairs, res, refs):
+        gpu = None if r.status != csm.CSM_OK else type("R", (), {
+            "score": r.score, "pose_estimate": r.pose.as_tuple(), "rotational_score": r.rotational_score,
+            "low_resolution_score": r.low_resolution_score, "tie": r.tie})()
+        tied += assert_same_result(gpu, ref) == "tie"
+    assert tied >= 4
