@@ -324,8 +324,12 @@ int LaunchSearch(csm_context* ctx, csm_scan_set* scans, const std::vector<PairDe
     if (std::getenv("CSM_PROFILE2D") && !init_best)
       std::fprintf(stderr, "fast2d launch: %s %s, %d rotations per item, %zu B dynamic LDS (capc %d), %d workgroups per CU\n",
                    plan.hex ? "v5" : "v4", plan.fifo ? "fifo" : "lifo", rc, dyn_lds, capc, per_cu);
-    const int grid = static_cast<int>(std::min<int64_t>(static_cast<int64_t>(ctx->num_cus) * per_cu,
-                                                        std::max<int64_t>(total_chunks, 1)));
+    // Concurrent single calls (call contexts, csm_internal.h) each take a
+    // share of the chip, so their persistent grids tile it instead of
+    // queueing behind one another (at least one workgroup per CU each).
+    const int64_t full = static_cast<int64_t>(ctx->num_cus) * per_cu;
+    const int64_t share = std::max<int64_t>(ctx->num_cus, full / std::max(1, ctx->grid_share));
+    const int grid = static_cast<int>(std::min<int64_t>(share, std::max<int64_t>(total_chunks, 1)));
     // DFS stack spill: kSpill2 entries per persistent workgroup.
     if ((rcode = ctx->spill.Reserve(sizeof(uint2) * kSpill2 * static_cast<size_t>(grid))))
       return rcode;
@@ -1329,6 +1333,12 @@ static int SingleMatch(const csm_fast2d* m, const csm_pose2d* initial, int full,
   if (!ctx) return CSM_EHIP;
   std::lock_guard<std::mutex> lock(ctx->mu);
   if (EnsureDevice(ctx)) return CSM_EHIP;
+  struct InFlight {  // this call counted among the owner's concurrent single calls
+    std::atomic<int>& n;
+    explicit InFlight(std::atomic<int>& c) : n(c) { ++n; }
+    ~InFlight() { --n; }
+  } in_flight(m->ctx->calls_in_flight);
+  ctx->grid_share = std::max(1, m->ctx->calls_in_flight.load());
   // The call context's one-scan set, reset for this cloud (scan index 0
   // names a different cloud on every call, so no window is kept).
   csm_scan_set& s = ctx->single;

@@ -114,8 +114,9 @@ struct Rt2dCache {
   float truncation = 0.f, max_weight = 0.f;
   float ttab_key[2] = {0.f, 0.f};
   std::vector<uint16_t> cells, wcells;
-  DevBuf grid, dcells, ptab, ttab, bases, best, dstage, sink;
+  DevBuf grid, dcells, ptab, ttab, bases, best, dstage, sink, done;
   PinnedBuf stage, stage_cells, host_key;
+  bool done_zeroed = false;  // the hand-off counter (rt2d_score) starts at 0
 };
 
 }  // namespace csm
@@ -173,6 +174,8 @@ struct csm_context {
   std::mutex call_mu;
   std::vector<csm_context*> call_free, call_all;
   csm_context* call_owner = nullptr;  // set on call contexts
+  std::atomic<int> calls_in_flight{0};  // single calls running on this owner's call contexts
+  int grid_share = 1;  // a call context's search launch takes 1/grid_share of the GPU
   csm_timing call_t{};                // finished single calls' timing (call_mu)
   csm_scan_set single;                // the cloud of the current single 2D call
   csm::PinnedBuf single_stage;

@@ -37,7 +37,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
+#include <cstdio>
+#include <mutex>
 #include <cstdlib>
 #include <cstring>
 #include <vector>
@@ -135,27 +138,19 @@ __device__ __forceinline__ unsigned long long PenalizedKey(float sum, double res
          static_cast<unsigned long long>(0xffffffffu - idx);
 }
 
-// The fused path's per-call inputs (rt2d_score<..., kFused = true>): the
-// discretization of rt2d_discretize done by each workgroup for its own
-// rotation into LDS, so Match is one launch.
-struct Rt2dDisc {
-  const float* points;
-  const float2* rot;
-  float pre_w, pre_s, tx, ty;
-  double max_x, max_y, res;
-  int nx, ny, P;
-  const uint32_t* warm;
-  int warm_words;
-  uint32_t* sink;
-  unsigned* done;                        // workgroups finished (0 between calls)
-  unsigned long long* result;            // the winning key, in mapped host memory
+// The hand-off path's per-call state (rt2d_score<..., kHandoff = true>): the
+// last workgroup to finish writes the winning key to mapped host memory, so
+// the host reads it without a device-to-host copy (and may poll it).
+struct Rt2dHandoff {
+  unsigned* done;                 // workgroups finished (0 between calls)
+  unsigned long long* result;     // the winning key, in mapped host memory
 };
 
-template <bool kTsdf, int kDepth, bool kFused>
+template <bool kTsdf, int kDepth, bool kHandoff>
 __global__ void __launch_bounds__(64)
 rt2d_score(Rt2dGridDev grid, int grid_bytes, const int* __restrict__ bases, int n, int npad,
            int side, int parts_x, int L, int num_angular, double step, double res,
-           double wt, double wr, unsigned long long* __restrict__ best, Rt2dDisc disc) {
+           double wt, double wr, unsigned long long* __restrict__ best, Rt2dHandoff ho) {
   // Workgroup = (rotation, y offset, chunk of x offsets); lane = x offset.
   // Lanes then read one grid row (x is the fastest index), so a gather
   // touches one or two cache lines.
@@ -169,41 +164,9 @@ rt2d_score(Rt2dGridDev grid, int grid_bytes, const int* __restrict__ bases, int 
   // Candidate order of GenerateExhaustiveSearchCandidates: (scan, x, y).
   const int t = (valid ? xi : 0) * side + yi;
   const int off = yo * grid.W + xo;
-  extern __shared__ int4 lds_bases[];
-  if constexpr (kFused) {
-    // Warm this XCD's L2 with the padded grid (as rt2d_discretize does),
-    // then discretize the rotation's points into LDS with rt2d_discretize's
-    // arithmetic; the padding slots point inside the padded grid.
-    {
-      const int xcd_blocks = (gridDim.x + kNumXcd - 1 - blockIdx.x % kNumXcd) / kNumXcd;
-      const int slot = blockIdx.x / kNumXcd;
-      uint32_t acc = 0;
-      for (int i = (slot * 64 + lane) * 32; i < disc.warm_words; i += xcd_blocks * 64 * 32)
-        acc ^= disc.warm[i];
-      if (acc == 0x9e3779b9u) disc.sink[0] = acc;
-    }
-    int* sb = reinterpret_cast<int*>(lds_bases);
-    const int W = disc.nx + 2 * disc.P;
-    const float2 q = disc.rot[r];
-    for (int i = lane; i < npad; i += 64) {
-      if (i >= n) {
-        sb[i] = disc.P * W + disc.P;
-        continue;
-      }
-      float x, y;
-      RotateZDev(disc.pre_w, disc.pre_s, disc.points[3 * i], disc.points[3 * i + 1], &x, &y);
-      RotateZDev(q.x, q.y, x, y, &x, &y);
-      const float px = __fadd_rn(disc.tx, x), py = __fadd_rn(disc.ty, y);
-      const double cx = fmin(fmax(CellCoord(disc.max_y, py, disc.res), -(L + 1.)), disc.nx + static_cast<double>(L));
-      const double cy = fmin(fmax(CellCoord(disc.max_x, px, disc.res), -(L + 1.)), disc.ny + static_cast<double>(L));
-      sb[i] = (static_cast<int>(cy) + disc.P) * W + static_cast<int>(cx) + disc.P;
-    }
-    __syncthreads();
-  }
   // The rotation's point indices: wave-uniform, 16-byte aligned (npad is a
-  // multiple of kDepth), read with scalar loads (LDS broadcasts when fused).
-  const int4* __restrict__ B = kFused ? lds_bases
-                                      : reinterpret_cast<const int4*>(bases + static_cast<int64_t>(r) * npad);
+  // multiple of kDepth), read with scalar loads.
+  const int4* __restrict__ B = reinterpret_cast<const int4*>(bases + static_cast<int64_t>(r) * npad);
   const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
       kTsdf ? static_cast<void*>(const_cast<float2*>(grid.tsdf))
             : static_cast<void*>(const_cast<float*>(grid.prob)),
@@ -295,20 +258,17 @@ rt2d_score(Rt2dGridDev grid, int grid_bytes, const int* __restrict__ bases, int 
     key = o > key ? o : key;
   }
   if (lane == 0 && key != 0) atomicMax(best, key);
-  if constexpr (kFused) {
+  if constexpr (kHandoff) {
     // The last workgroup to finish hands the winner to the host (mapped
-    // memory) and resets the key and the counter for the next call, so a
-    // Match is one upload, one launch and one synchronize.
+    // memory) and resets the counter; rt2d_discretize zeroes the key.
     if (lane == 0) {
       __threadfence();
-      const unsigned done = atomicAdd(disc.done, 1u);
+      const unsigned done = atomicAdd(ho.done, 1u);
       if (done == gridDim.x - 1) {
         __threadfence();
-        const unsigned long long k = atomicOr(best, 0ull);
-        disc.result[0] = k;
+        ho.result[0] = atomicOr(best, 0ull);
         __threadfence_system();
-        *best = 0ull;
-        *disc.done = 0u;
+        *ho.done = 0u;
       }
     }
   }
@@ -441,12 +401,38 @@ int EnsureGrid(csm_context* ctx, const GridArgs& g, int P, Rt2dGridDev* out) {
   return CSM_OK;
 }
 
+using Rt2dClock = std::chrono::steady_clock;
+
+// CSM_PROFILE_RT2D=1: mean host time per Match phase (window + rotation
+// table, grid check, staging + uploads, launches, wait), printed to stderr
+// every 200 calls.
+void Rt2dProfile(Rt2dClock::time_point a, Rt2dClock::time_point b, Rt2dClock::time_point c,
+                 Rt2dClock::time_point d, Rt2dClock::time_point e, Rt2dClock::time_point f) {
+  static const bool on = std::getenv("CSM_PROFILE_RT2D") != nullptr;
+  if (!on) return;
+  static std::mutex mu;
+  static double acc[5] = {0, 0, 0, 0, 0};
+  static int calls = 0;
+  const Rt2dClock::time_point t[6] = {a, b, c, d, e, f};
+  std::lock_guard<std::mutex> lock(mu);
+  for (int k = 0; k < 5; ++k) acc[k] += std::chrono::duration<double, std::micro>(t[k + 1] - t[k]).count();
+  if (++calls == 200) {
+    std::fprintf(stderr,
+                 "rt2d host (us/call): window %.2f, grid check %.2f, staging %.2f, launches %.2f, "
+                 "wait %.2f\n",
+                 acc[0] / calls, acc[1] / calls, acc[2] / calls, acc[3] / calls, acc[4] / calls);
+    for (double& v : acc) v = 0;
+    calls = 0;
+  }
+}
+
 // RealTimeCorrelativeScanMatcher2D::Match (:117-149).
 int Rt2dMatch(csm_context* ctx, const csm_rt_options* o, const GridArgs& g,
               const csm_pose2d* initial, const float* xyz, int32_t n, double* score,
               csm_pose2d* pose) {
   if (!ctx || !o || !initial || !score || !pose || n <= 0 || !xyz || !ValidGrid(g))
     return CSM_EINVAL;
+  const auto t_entry = Rt2dClock::now();
   const csm_map_limits* l = g.limits;
   // :123-130: the window is built on the cloud rotated by the initial angle.
   const ZRot pre = MakeZRot(static_cast<float>(initial->theta));
@@ -463,11 +449,13 @@ int Rt2dMatch(csm_context* ctx, const csm_rt_options* o, const GridArgs& g,
     return CSM_ERANGE;
   std::vector<ZRot> table;
   RotationTable(w, &table);
+  const auto t_window = Rt2dClock::now();
   std::lock_guard<std::mutex> lock(ctx->mu);
   if (hipSetDevice(ctx->device) != hipSuccess) return CSM_EHIP;
   int rc;
   Rt2dGridDev grid;
   if ((rc = EnsureGrid(ctx, g, P, &grid))) return rc;
+  const auto t_grid = Rt2dClock::now();
   csm::Rt2dCache& c = ctx->rt2d;
   hipStream_t st = ctx->stream;
   // One pinned staging block: points, then the rotation table.
@@ -492,6 +480,35 @@ int Rt2dMatch(csm_context* ctx, const csm_rt_options* o, const GridArgs& g,
       (static_cast<int64_t>(l->num_x_cells) + 2 * P) * (l->num_y_cells + 2 * P) *
       (g.wcells ? sizeof(float2) : sizeof(float)));
   if ((rc = c.sink.Reserve(sizeof(uint32_t)))) return rc;
+  // Hand-off (default; CSM_RT2D_HANDOFF=0 for the copy path): the score
+  // kernel's last workgroup writes the winner to mapped host memory, so no
+  // device-to-host copy is queued. The host then waits on the stream
+  // (CSM_RT2D_WAIT=sync, default) or polls the mapped word (=poll; a
+  // stream query every 256 polls ends the wait if the kernel finished
+  // without writing it).
+  static const bool handoff = [] {
+    const char* e = std::getenv("CSM_RT2D_HANDOFF");
+    return !(e && std::atoi(e) == 0);
+  }();
+  static const bool poll = [] {
+    const char* e = std::getenv("CSM_RT2D_WAIT");
+    return e && std::strcmp(e, "poll") == 0;
+  }();
+  unsigned long long* hk = c.host_key.as<unsigned long long>();
+  Rt2dHandoff ho{nullptr, nullptr};
+  if (handoff) {
+    if ((rc = c.done.Reserve(sizeof(unsigned)))) return rc;
+    if (!c.done_zeroed) {
+      CSM_HIP(hipMemsetAsync(c.done.ptr, 0, sizeof(unsigned), st));
+      c.done_zeroed = true;
+    }
+    void* dk = nullptr;
+    CSM_HIP(hipHostGetDevicePointer(&dk, hk, 0));
+    ho.done = c.done.as<unsigned>();
+    ho.result = static_cast<unsigned long long*>(dk);
+  }
+  *hk = 0ull;
+  const auto t_prep = Rt2dClock::now();
   if (ctx->timing) CSM_HIP(hipEventRecord(ctx->ev0, st));
   const int64_t nthreads = static_cast<int64_t>(w.num_scans) * npad;
   hipLaunchKernelGGL(rt2d_discretize, dim3(static_cast<unsigned>((nthreads + 255) / 256)), dim3(256),
@@ -511,32 +528,52 @@ int Rt2dMatch(csm_context* ctx, const csm_rt_options* o, const GridArgs& g,
     const int d = e ? std::atoi(e) : 32;
     return (d == 8 || d == 16) ? d : 32;
   }();
-#define CSM_RT2D_LAUNCH(TSDF, D)                                                                 \
-  hipLaunchKernelGGL((rt2d_score<TSDF, D>), blocks, dim3(64), 0, st, grid, grid_bytes,           \
+#define CSM_RT2D_LAUNCH(TSDF, D, H)                                                               \
+  hipLaunchKernelGGL((rt2d_score<TSDF, D, H>), blocks, dim3(64), 0, st, grid, grid_bytes,         \
                      c.bases.as<int>(), n, npad, side, parts_x, L, w.num_angular_perturbations, \
                      w.angular_perturbation_step_size, l->resolution,                           \
                      o->translation_delta_cost_weight, o->rotation_delta_cost_weight,           \
-                     c.best.as<unsigned long long>())
+                     c.best.as<unsigned long long>(), ho)
+#define CSM_RT2D_DEPTHS(TSDF, H)                 \
+  do {                                           \
+    if (depth == 8) CSM_RT2D_LAUNCH(TSDF, 8, H); \
+    else if (depth == 32) CSM_RT2D_LAUNCH(TSDF, 32, H); \
+    else CSM_RT2D_LAUNCH(TSDF, 16, H);           \
+  } while (0)
   if (g.wcells) {
-    if (depth == 8) CSM_RT2D_LAUNCH(true, 8);
-    else if (depth == 32) CSM_RT2D_LAUNCH(true, 32);
-    else CSM_RT2D_LAUNCH(true, 16);
+    if (handoff) CSM_RT2D_DEPTHS(true, true);
+    else CSM_RT2D_DEPTHS(true, false);
   } else {
-    if (depth == 8) CSM_RT2D_LAUNCH(false, 8);
-    else if (depth == 32) CSM_RT2D_LAUNCH(false, 32);
-    else CSM_RT2D_LAUNCH(false, 16);
+    if (handoff) CSM_RT2D_DEPTHS(false, true);
+    else CSM_RT2D_DEPTHS(false, false);
   }
+#undef CSM_RT2D_DEPTHS
 #undef CSM_RT2D_LAUNCH
   CSM_HIP(hipGetLastError());
   if (ctx->timing) CSM_HIP(hipEventRecord(ctx->ev1, st));
-  unsigned long long* hk = c.host_key.as<unsigned long long>();
-  CSM_HIP(hipMemcpyAsync(hk, c.best.ptr, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
-  CSM_HIP(hipStreamSynchronize(st));
+  if (!handoff)
+    CSM_HIP(hipMemcpyAsync(hk, c.best.ptr, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+  const auto t_launch = Rt2dClock::now();
+  if (handoff && poll) {
+    // The key is never 0 once written (a valid lane always scores).
+    volatile unsigned long long* vk = hk;
+    for (unsigned spin = 1; *vk == 0ull; ++spin) {
+      if ((spin & 255u) == 0u) {
+        const hipError_t q = hipStreamQuery(st);
+        if (q == hipSuccess) break;
+        if (q != hipErrorNotReady) return CSM_EHIP;
+      }
+    }
+    if (ctx->timing) CSM_HIP(hipEventSynchronize(ctx->ev1));
+  } else {
+    CSM_HIP(hipStreamSynchronize(st));
+  }
   if (ctx->timing) {
     float ms = 0.f;
     CSM_HIP(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
     ctx->t.other_kernel_ms += ms;
   }
+  Rt2dProfile(t_entry, t_window, t_grid, t_prep, t_launch, Rt2dClock::now());
   const unsigned long long key = *hk;
   if (key == 0) return CSM_EINVAL;
   const uint32_t bits = static_cast<uint32_t>(key >> 32);
