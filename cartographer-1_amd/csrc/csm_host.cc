@@ -245,47 +245,18 @@ int LaunchSearch(csm_context* ctx, csm_scan_set* scans, const std::vector<PairDe
   wq.queue_begin[kNumXcd] = static_cast<int32_t>(order.size());
   prefix.push_back(running);
 
-  int rcode;
-  if ((rcode = ctx->pair_desc.Reserve(sizeof(PairDesc) * np))) return rcode;
-  if ((rcode = ctx->best.Reserve(sizeof(uint64_t) * np))) return rcode;
-  if ((rcode = ctx->best_hi.Reserve(sizeof(uint64_t) * np))) return rcode;
-  if ((rcode = ctx->status.Reserve(sizeof(int32_t) * np))) return rcode;
-  if ((rcode = ctx->counters.Reserve(sizeof(unsigned long long) * kNumXcd))) return rcode;
-  if ((rcode = ctx->pair_order.Reserve(sizeof(int32_t) * order.size()))) return rcode;
-  if ((rcode = ctx->chunk_prefix.Reserve(sizeof(int64_t) * prefix.size()))) return rcode;
-  if ((rcode = ctx->stats.Reserve(sizeof(unsigned long long) * kStatsWords))) return rcode;
-  if ((rcode = ctx->tie_count.Reserve(sizeof(int32_t) * np))) return rcode;
-  if (ties && (rcode = ctx->ties.Reserve(sizeof(uint2) * kTieCap * static_cast<size_t>(np))))
-    return rcode;
-  hipStream_t st = ctx->stream;
-  CSM_HIP(hipMemcpyAsync(ctx->pair_desc.ptr, pdesc.data(), sizeof(PairDesc) * np,
-                         hipMemcpyHostToDevice, st));
-  CSM_HIP(hipMemcpyAsync(ctx->pair_order.ptr, order.data(), sizeof(int32_t) * order.size(),
-                         hipMemcpyHostToDevice, st));
-  CSM_HIP(hipMemcpyAsync(ctx->chunk_prefix.ptr, prefix.data(), sizeof(int64_t) * prefix.size(),
-                         hipMemcpyHostToDevice, st));
-  if (init_best)
-    CSM_HIP(hipMemcpyAsync(ctx->best.ptr, init_best->data(), sizeof(uint64_t) * np,
-                           hipMemcpyHostToDevice, st));
-  else
-    CSM_HIP(hipMemsetAsync(ctx->best.ptr, 0, sizeof(uint64_t) * np, st));
-  CSM_HIP(hipMemsetAsync(ctx->best_hi.ptr, 0, sizeof(uint64_t) * np, st));
-  CSM_HIP(hipMemsetAsync(ctx->status.ptr, 0, sizeof(int32_t) * np, st));
-  CSM_HIP(hipMemsetAsync(ctx->tie_count.ptr, 0, sizeof(int32_t) * np, st));
-  CSM_HIP(hipMemsetAsync(ctx->counters.ptr, 0, sizeof(unsigned long long) * kNumXcd, st));
-  CSM_HIP(hipMemsetAsync(ctx->stats.ptr, 0, sizeof(unsigned long long) * kStatsWords, st));
-  wq.pair_order = ctx->pair_order.as<int32_t>();
-  wq.chunk_prefix = ctx->chunk_prefix.as<int64_t>();
-
-  // ---- launch: persistent workgroups ----------------------------------------
-  const int64_t total_chunks = running;
-  const int max_npad = plan.max_npad;
-  if (timed) CSM_HIP(hipEventRecord(ctx->ev0, st));
+  // Block table (v2 kernel): for every 64 chunks of a queue, the first
+  // pair_order entry.
+  std::vector<int32_t> blocks;
+  WorkQueues2 wq2{};
   if (plan.use_v2) {
-    // Block table: for every 64 chunks of a queue, the first pair_order entry.
-    std::vector<int32_t> blocks;
-    WorkQueues2 wq2{};
     wq2.rot_chunk = rc;
+    // CSM_SORT_BATCH=1: batch nodes in (rotation, level, y, x) order (A/B).
+    static const int sort_batch = [] {
+      const char* e = std::getenv("CSM_SORT_BATCH");
+      return e ? std::atoi(e) : 0;
+    }();
+    wq2.sort_batch = sort_batch;
     for (int x = 0; x < kNumXcd; ++x) {
       wq2.queue_begin[x] = wq.queue_begin[x];
       wq2.queue_chunks[x] = wq.queue_chunks[x];
@@ -298,14 +269,66 @@ int LaunchSearch(csm_context* ctx, csm_scan_set* scans, const std::vector<PairDe
       }
     }
     wq2.queue_begin[kNumXcd] = wq.queue_begin[kNumXcd];
-    if ((rcode = ctx->blocks.Reserve(sizeof(int32_t) * std::max<size_t>(blocks.size(), 1))))
-      return rcode;
-    if (!blocks.empty())
-      CSM_HIP(hipMemcpyAsync(ctx->blocks.ptr, blocks.data(), sizeof(int32_t) * blocks.size(),
-                             hipMemcpyHostToDevice, st));
+  }
+
+  // One device arena per launch (csm_context::arena): the inputs, uploaded
+  // with one copy from pinned staging, then the outputs, zeroed with one
+  // memset and read back with one copy into pinned memory:
+  //   pair_desc | pair_order | chunk_prefix | blocks || best | best_hi |
+  //   status | tie_count | counters | stats
+  // (init_best, when given, is uploaded into `best` with the inputs.)
+  auto align = [](size_t v) { return (v + 255) & ~size_t{255}; };
+  size_t at = 0;
+  auto region = [&](size_t bytes) {
+    const size_t o = at;
+    at = align(at + std::max<size_t>(bytes, 1));
+    return o;
+  };
+  const size_t o_pd = region(sizeof(PairDesc) * np), o_order = region(sizeof(int32_t) * order.size()),
+               o_prefix = region(sizeof(int64_t) * prefix.size()),
+               o_blocks = region(sizeof(int32_t) * blocks.size());
+  const size_t o_best = region(sizeof(uint64_t) * np), o_hi = region(sizeof(uint64_t) * np),
+               o_status = region(sizeof(int32_t) * np), o_tcount = region(sizeof(int32_t) * np),
+               o_counters = region(sizeof(unsigned long long) * kNumXcd);
+  const size_t o_stats = region(sizeof(unsigned long long) * kStatsWords);
+  const size_t arena_bytes = at;
+  const size_t in_end = init_best ? o_hi : o_best;  // uploaded bytes
+  const size_t zero_begin = in_end;
+  int rcode;
+  if ((rcode = ctx->arena.Reserve(arena_bytes))) return rcode;
+  if ((rcode = ctx->arena_in.Reserve(in_end))) return rcode;
+  if ((rcode = ctx->arena_out.Reserve(arena_bytes - o_best))) return rcode;
+  if (ties && (rcode = ctx->ties.Reserve(sizeof(uint2) * kTieCap * static_cast<size_t>(np))))
+    return rcode;
+  char* hin = ctx->arena_in.as<char>();
+  std::memcpy(hin + o_pd, pdesc.data(), sizeof(PairDesc) * np);
+  std::memcpy(hin + o_order, order.data(), sizeof(int32_t) * order.size());
+  std::memcpy(hin + o_prefix, prefix.data(), sizeof(int64_t) * prefix.size());
+  if (!blocks.empty()) std::memcpy(hin + o_blocks, blocks.data(), sizeof(int32_t) * blocks.size());
+  if (init_best) std::memcpy(hin + o_best, init_best->data(), sizeof(uint64_t) * np);
+  char* dev = ctx->arena.as<char>();
+  hipStream_t st = ctx->stream;
+  CSM_HIP(hipMemcpyAsync(dev, hin, in_end, hipMemcpyHostToDevice, st));
+  CSM_HIP(hipMemsetAsync(dev + zero_begin, 0, arena_bytes - zero_begin, st));
+  ctx->pair_desc_dev = dev + o_pd;
+  PairDesc* d_pairs = reinterpret_cast<PairDesc*>(dev + o_pd);
+  uint64_t* d_best = reinterpret_cast<uint64_t*>(dev + o_best);
+  uint64_t* d_hi = reinterpret_cast<uint64_t*>(dev + o_hi);
+  int32_t* d_status = reinterpret_cast<int32_t*>(dev + o_status);
+  int32_t* d_tcount = reinterpret_cast<int32_t*>(dev + o_tcount);
+  unsigned long long* d_counters = reinterpret_cast<unsigned long long*>(dev + o_counters);
+  unsigned long long* d_stats = reinterpret_cast<unsigned long long*>(dev + o_stats);
+  wq.pair_order = reinterpret_cast<int32_t*>(dev + o_order);
+  wq.chunk_prefix = reinterpret_cast<int64_t*>(dev + o_prefix);
+
+  // ---- launch: persistent workgroups ----------------------------------------
+  const int64_t total_chunks = running;
+  const int max_npad = plan.max_npad;
+  if (timed) CSM_HIP(hipEventRecord(ctx->ev0, st));
+  if (plan.use_v2) {
     wq2.pair_order = wq.pair_order;
     wq2.chunk_prefix = wq.chunk_prefix;
-    wq2.block_first = ctx->blocks.as<int32_t>();
+    wq2.block_first = reinterpret_cast<int32_t*>(dev + o_blocks);
     // Per rotation: npad raw cells and capc cluster-list entries. capc =
     // 3/4 npad holds the three cluster lists of a typical scan (0.55 npad on
     // C2); a list that does not fit falls back to a finer one in the kernel.
@@ -333,43 +356,36 @@ int LaunchSearch(csm_context* ctx, csm_scan_set* scans, const std::vector<PairDe
     // DFS stack spill: kSpill2 entries per persistent workgroup.
     if ((rcode = ctx->spill.Reserve(sizeof(uint2) * kSpill2 * static_cast<size_t>(grid))))
       return rcode;
-    CSM_HIP(LaunchFast2dSearchV2(grid, dyn_lds, st, ctx->submap_desc.as<SubmapDesc>(),
-                                 ctx->pair_desc.as<PairDesc>(), scans->points.as<float>(),
-                                 scans->rot_dev.as<float2>(), wq2,
-                                 ctx->counters.as<unsigned long long>(), ctx->best.as<uint64_t>(),
-                                 ctx->status.as<int32_t>(), ctx->stats.as<unsigned long long>(),
-                                 ctx->spill.as<uint2>(), max_npad, capc, plan.hex, plan.fifo,
-                                 ctx->best_hi.as<uint64_t>(), ties ? ctx->ties.as<uint2>() : nullptr,
-                                 ctx->tie_count.as<int32_t>(), ties != nullptr));
+    CSM_HIP(LaunchFast2dSearchV2(grid, dyn_lds, st, ctx->submap_desc.as<SubmapDesc>(), d_pairs,
+                                 scans->points.as<float>(), scans->rot_dev.as<float2>(), wq2,
+                                 d_counters, d_best, d_status, d_stats, ctx->spill.as<uint2>(),
+                                 max_npad, capc, plan.hex, plan.fifo, d_hi,
+                                 ties ? ctx->ties.as<uint2>() : nullptr, d_tcount, ties != nullptr));
   } else {
     const size_t dyn_lds = static_cast<size_t>(rc) * max_npad * sizeof(uint32_t);
     const int grid = static_cast<int>(std::min<int64_t>(static_cast<int64_t>(ctx->num_cus) * 4,
                                                         std::max<int64_t>(total_chunks, 1)));
-    CSM_HIP(LaunchFast2dSearch(grid, dyn_lds, st, ctx->submap_desc.as<SubmapDesc>(),
-                               ctx->pair_desc.as<PairDesc>(), scans->points.as<float>(),
-                               scans->rot_dev.as<float2>(), wq,
-                               ctx->counters.as<unsigned long long>(), ctx->best.as<uint64_t>(),
-                               ctx->status.as<int32_t>(), ctx->stats.as<unsigned long long>()));
+    CSM_HIP(LaunchFast2dSearch(grid, dyn_lds, st, ctx->submap_desc.as<SubmapDesc>(), d_pairs,
+                               scans->points.as<float>(), scans->rot_dev.as<float2>(), wq,
+                               d_counters, d_best, d_status, d_stats));
   }
   if (timed) CSM_HIP(hipEventRecord(ctx->ev1, st));
-  keys->resize(np);
-  keys_hi->resize(np);
-  stat->resize(np);
-  CSM_HIP(hipMemcpyAsync(keys->data(), ctx->best.ptr, sizeof(uint64_t) * np, hipMemcpyDeviceToHost, st));
-  CSM_HIP(hipMemcpyAsync(keys_hi->data(), ctx->best_hi.ptr, sizeof(uint64_t) * np,
-                         hipMemcpyDeviceToHost, st));
-  CSM_HIP(hipMemcpyAsync(stat->data(), ctx->status.ptr, sizeof(int32_t) * np, hipMemcpyDeviceToHost, st));
-  CSM_HIP(hipMemcpyAsync(stats_host, ctx->stats.ptr, sizeof(unsigned long long) * kStatsWords,
-                         hipMemcpyDeviceToHost, st));
+  char* hout = ctx->arena_out.as<char>();
+  CSM_HIP(hipMemcpyAsync(hout, dev + o_best, arena_bytes - o_best, hipMemcpyDeviceToHost, st));
   if (ties) {
     ties->resize(static_cast<size_t>(kTieCap) * np);
-    tie_counts->resize(np);
     CSM_HIP(hipMemcpyAsync(ties->data(), ctx->ties.ptr, sizeof(uint2) * ties->size(),
-                           hipMemcpyDeviceToHost, st));
-    CSM_HIP(hipMemcpyAsync(tie_counts->data(), ctx->tie_count.ptr, sizeof(int32_t) * np,
                            hipMemcpyDeviceToHost, st));
   }
   CSM_HIP(hipStreamSynchronize(st));
+  auto out = [&](size_t o) { return hout + (o - o_best); };
+  keys->assign(reinterpret_cast<uint64_t*>(out(o_best)), reinterpret_cast<uint64_t*>(out(o_best)) + np);
+  keys_hi->assign(reinterpret_cast<uint64_t*>(out(o_hi)), reinterpret_cast<uint64_t*>(out(o_hi)) + np);
+  stat->assign(reinterpret_cast<int32_t*>(out(o_status)), reinterpret_cast<int32_t*>(out(o_status)) + np);
+  std::memcpy(stats_host, out(o_stats), sizeof(unsigned long long) * kStatsWords);
+  if (ties)
+    tie_counts->assign(reinterpret_cast<int32_t*>(out(o_tcount)),
+                       reinterpret_cast<int32_t*>(out(o_tcount)) + np);
   return CSM_OK;
 }
 
@@ -524,7 +540,7 @@ int ResolveTies(csm_context* ctx, csm_fast2d* const* submaps, csm_scan_set* scan
     CSM_HIP(hipMemcpyAsync(ctx->sq_queries.ptr, qs.data(), sizeof(int4) * qs.size(),
                            hipMemcpyHostToDevice, st));
     CSM_HIP(LaunchFast2dScoreQueries(static_cast<int>(js.size()), plan.max_npad, st,
-                                     ctx->submap_desc.as<SubmapDesc>(), ctx->pair_desc.as<PairDesc>(),
+                                     ctx->submap_desc.as<SubmapDesc>(), static_cast<const PairDesc*>(ctx->pair_desc_dev),
                                      scans->points.as<float>(), scans->rot_dev.as<float2>(),
                                      ctx->sq_jobs.as<ScoreJob>(), ctx->sq_queries.as<int4>(),
                                      ctx->sq_sums.as<int32_t>()));
@@ -534,7 +550,7 @@ int ResolveTies(csm_context* ctx, csm_fast2d* const* submaps, csm_scan_set* scan
     return CSM_OK;
   };
   const auto tp1 = now();
-  // The jobs index pd2 (ctx->pair_desc holds it after the second search).
+  // The jobs index pd2 (ctx->pair_desc_dev holds it after the second search).
   std::vector<int32_t> sums;
   if ((rc = score(jobs, queries, &sums))) return rc;
   // Per tie: the leaves that can come first. The reference visits the
@@ -599,7 +615,7 @@ int ResolveTies(csm_context* ctx, csm_fast2d* const* submaps, csm_scan_set* scan
     CSM_HIP(hipMemcpyAsync(ctx->sq_jobs.ptr, bjobs.data(), sizeof(int2) * bjobs.size(),
                            hipMemcpyHostToDevice, st));
     CSM_HIP(LaunchFast2dRotationBounds(static_cast<int>(bjobs.size()), st, ctx->submap_desc.as<SubmapDesc>(),
-                                       ctx->pair_desc.as<PairDesc>(), scans->points.as<float>(),
+                                       static_cast<const PairDesc*>(ctx->pair_desc_dev), scans->points.as<float>(),
                                        scans->rot_dev.as<float2>(), ctx->sq_jobs.as<int2>(),
                                        ctx->sq_sums.as<int4>()));
     CSM_HIP(hipMemcpyAsync(bounds.data(), ctx->sq_sums.ptr, sizeof(int4) * bjobs.size(),
@@ -834,15 +850,29 @@ int RunBatch(csm_context* ctx, csm_fast2d* const* submaps, int32_t num_submaps,
   if ((rcode = ctx->submap_desc.Reserve(sizeof(SubmapDesc) * num_submaps))) return rcode;
   if (rot_host.size() > scans->rot_uploaded) {  // new windows since the last batch
     const size_t want = sizeof(float2) * rot_host.size();
-    if (want > scans->rot_dev.bytes && (rcode = scans->rot_dev.Reserve(want + want / 2))) return rcode;
+    if (want > scans->rot_dev.bytes) {  // a new buffer: upload the whole table below
+      if ((rcode = scans->rot_dev.Reserve(want + want / 2))) return rcode;
+      scans->rot_uploaded = 0;
+    }
   }
   hipStream_t st = ctx->stream;
-  CSM_HIP(hipMemcpyAsync(ctx->submap_desc.ptr, sdesc.data(), sizeof(SubmapDesc) * num_submaps,
-                         hipMemcpyHostToDevice, st));
-  if (rot_host.size() > scans->rot_uploaded) {
-    CSM_HIP(hipMemcpyAsync(scans->rot_dev.ptr, rot_host.data(), sizeof(float2) * rot_host.size(),
-                           hipMemcpyHostToDevice, st));
-    scans->rot_uploaded = rot_host.size();
+  // Staged through pinned memory (async copies; the stage is rewritten only
+  // by the next batch on this context, after this one's synchronize).
+  {
+    const size_t sd_bytes = sizeof(SubmapDesc) * num_submaps;
+    const size_t rot_new = rot_host.size() - std::min(rot_host.size(), scans->rot_uploaded);
+    const size_t rot_at = (sd_bytes + 255) & ~size_t{255};
+    if ((rcode = ctx->upload_stage.Reserve(rot_at + sizeof(float2) * rot_new))) return rcode;
+    char* h = ctx->upload_stage.as<char>();
+    std::memcpy(h, sdesc.data(), sd_bytes);
+    CSM_HIP(hipMemcpyAsync(ctx->submap_desc.ptr, h, sd_bytes, hipMemcpyHostToDevice, st));
+    if (rot_new > 0) {
+      const size_t first = rot_host.size() - rot_new;
+      std::memcpy(h + rot_at, rot_host.data() + first, sizeof(float2) * rot_new);
+      CSM_HIP(hipMemcpyAsync(scans->rot_dev.as<float2>() + first, h + rot_at, sizeof(float2) * rot_new,
+                             hipMemcpyHostToDevice, st));
+      scans->rot_uploaded = rot_host.size();
+    }
   }
   std::vector<uint64_t> keys, keys_hi;
   std::vector<int32_t> stat;
@@ -993,6 +1023,7 @@ void csm_context_destroy(csm_context* ctx) {
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
   if (ctx->f3_copy_stream) (void)hipStreamSynchronize(ctx->f3_copy_stream);
   if (ctx->f3_points_ready) (void)hipEventDestroy(ctx->f3_points_ready);
+  if (ctx->f3_stage_copied) (void)hipEventDestroy(ctx->f3_stage_copied);
   if (ctx->f3_copy_stream) (void)hipStreamDestroy(ctx->f3_copy_stream);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;

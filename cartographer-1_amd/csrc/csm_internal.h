@@ -114,9 +114,8 @@ struct Rt2dCache {
   float truncation = 0.f, max_weight = 0.f;
   float ttab_key[2] = {0.f, 0.f};
   std::vector<uint16_t> cells, wcells;
-  DevBuf grid, dcells, ptab, ttab, bases, best, dstage, sink, done;
+  DevBuf grid, dcells, ptab, ttab, bases, best, dstage, sink;
   PinnedBuf stage, stage_cells, host_key;
-  bool done_zeroed = false;  // the hand-off counter (rt2d_score) starts at 0
 };
 
 }  // namespace csm
@@ -179,9 +178,12 @@ struct csm_context {
   csm_timing call_t{};                // finished single calls' timing (call_mu)
   csm_scan_set single;                // the cloud of the current single 2D call
   csm::PinnedBuf single_stage;
-  csm::DevBuf submap_desc, pair_desc, best, status, counters, pair_order,
-      chunk_prefix, blocks, stats, spill, single_points, best_hi, ties, tie_count, sq_jobs,
-      sq_queries, sq_sums;
+  csm::DevBuf submap_desc, spill, single_points, ties, sq_jobs, sq_queries, sq_sums;
+  // One 2D search launch's descriptors and outputs (csm_host.cc LaunchSearch),
+  // with pinned staging for its one upload and one readback.
+  csm::DevBuf arena;
+  csm::PinnedBuf arena_in, arena_out, upload_stage;
+  const void* pair_desc_dev = nullptr;  // the last launch's PairDesc array (in arena)
   csm::Rt2dCache rt2d;
   std::atomic<bool> timing{false};
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -198,6 +200,7 @@ struct csm_context {
   // scores on `stream`); the search waits on f3_points_ready.
   hipStream_t f3_copy_stream = nullptr;
   hipEvent_t f3_points_ready = nullptr;
+  hipEvent_t f3_stage_copied = nullptr;  // f3_grid_stage's last upload done
   // Voxel filter scratch (voxel_filter.hip).
   csm::DevBuf vf_points, vf_offsets, vf_keep, vf_counts;
   // CeresScanMatcher2D refinement scratch (ceres2d.hip).
@@ -250,6 +253,9 @@ class CallContext {
 // A HybridGrid on the device (host3d.cc builds it).
 struct csm_hybrid_grid {
   csm_context* ctx = nullptr;
+  // Recorded on ctx->stream after the build's kernels (creates return
+  // without waiting): consumers on other streams wait on it (WaitBuilt).
+  hipEvent_t ready = nullptr;
   float resolution = 0.f;
   int32_t grid_size = 0;
   csm::Brick3 brick{};
@@ -262,5 +268,16 @@ struct csm_hybrid_grid {
   csm::DevBuf prob_col;   // padded by prob_col_pad cells, z fastest (rt3d_score5)
   int prob_col_pad = 0;
 };
+
+namespace csm {
+// Grids and matchers are built asynchronously on their context's stream and
+// marked by a `ready` event. Work on the same stream is ordered after the
+// build already; another stream (a call context, another context of the
+// device) waits for the event on the device, host reads synchronize on it.
+inline int WaitBuilt(hipEvent_t ready, hipStream_t producer, hipStream_t consumer) {
+  if (!ready || producer == consumer) return CSM_OK;
+  return hipStreamWaitEvent(consumer, ready, 0) == hipSuccess ? CSM_OK : CSM_EHIP;
+}
+}  // namespace csm
 
 #endif  // CSM_INTERNAL_H_

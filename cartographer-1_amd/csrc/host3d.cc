@@ -228,18 +228,24 @@ int csm_hybrid_grid_create(csm_context* ctx, float resolution, const int32_t* ij
     if ((rc = ctx->f3_grid_cells.Reserve(list_bytes))) return rc;
     if ((rc = ctx->pool.Take(sizeof(uint16_t) * n, &g->values))) return rc;
     if ((rc = ctx->pool.Take(sizeof(float) * n, &g->prob))) return rc;
+    // The staging buffer is rewritten only once the previous create's copy
+    // out of it has finished (the kernels are not waited for).
+    if (ctx->f3_stage_copied) CSM_HIP(hipEventSynchronize(ctx->f3_stage_copied));
+    else CSM_HIP(hipEventCreateWithFlags(&ctx->f3_stage_copied, hipEventDisableTiming));
     char* h = ctx->f3_grid_stage.as<char>();
     std::memcpy(h, ijk, sizeof(int32_t) * 3 * count);
     std::memcpy(h + sizeof(int32_t) * 3 * count, values, sizeof(uint16_t) * count);
     hipStream_t st = ctx->stream;
     CSM_HIP(hipMemcpyAsync(ctx->f3_grid_cells.ptr, h, list_bytes, hipMemcpyHostToDevice, st));
+    CSM_HIP(hipEventRecord(ctx->f3_stage_copied, st));
     CSM_HIP(hipMemsetAsync(g->values.ptr, 0, sizeof(uint16_t) * n, st));
     const int32_t* dijk = ctx->f3_grid_cells.as<int32_t>();
     const uint16_t* dval = reinterpret_cast<const uint16_t*>(dijk + 3 * count);
     CSM_HIP(LaunchBrickScatter(dijk, dval, count, b, g->values.as<uint16_t>(), st));
     CSM_HIP(LaunchBrickFromValues(g->values.as<uint16_t>(), n, ctx->f3_ptab.as<float>(), nullptr,
                                   g->prob.as<float>(), nullptr, st));
-    CSM_HIP(hipStreamSynchronize(st));  // the staging is reused by the next create
+    CSM_HIP(hipEventCreateWithFlags(&g->ready, hipEventDisableTiming));
+    CSM_HIP(hipEventRecord(g->ready, st));
   }
   *out = g.release();
   return CSM_OK;
@@ -250,6 +256,7 @@ void csm_hybrid_grid_destroy(csm_hybrid_grid* g) {
   (void)hipSetDevice(g->ctx->device);
   g->ctx->pool.Give(&g->values);  // reused by the next create
   g->ctx->pool.Give(&g->prob);
+  if (g->ready) (void)hipEventDestroy(g->ready);
   delete g;
 }
 
@@ -646,6 +653,7 @@ struct csm_fast3d {
   std::vector<float> histogram;
   DevBuf levels, octs;
   Submap3Desc desc{};
+  hipEvent_t ready = nullptr;  // after the build's kernels on ctx->stream (WaitBuilt)
 };
 
 int csm_fast3d_create(csm_context* ctx, const csm_hybrid_grid* high, const csm_hybrid_grid* low,
@@ -758,7 +766,8 @@ int csm_fast3d_create(csm_context* ctx, const csm_hybrid_grid* high, const csm_h
       CSM_HIP(LaunchOctetBuild(m->levels.as<uint8_t>() + d.level[l].offset, d.level[l], d.oct_h[l],
                                reinterpret_cast<uint64_t*>(m->octs.as<uint8_t>() + d.oct[l].offset),
                                d.oct[l], st));
-    CSM_HIP(hipStreamSynchronize(st));
+    CSM_HIP(hipEventCreateWithFlags(&m->ready, hipEventDisableTiming));
+    CSM_HIP(hipEventRecord(m->ready, st));
   }
   *out = m.release();
   return CSM_OK;
@@ -779,6 +788,7 @@ void csm_fast3d_destroy(csm_fast3d* m) {
   (void)hipSetDevice(m->ctx->device);
   m->ctx->pool.Give(&m->levels);  // reused by the next create
   m->ctx->pool.Give(&m->octs);
+  if (m->ready) (void)hipEventDestroy(m->ready);
   delete m;
 }
 
@@ -803,6 +813,7 @@ int csm_fast3d_read_level(const csm_fast3d* m, int32_t level, uint8_t* out, int6
   int rc;
   if ((rc = EnsureDevice3(m->ctx))) return rc;
   if (n > 0) {
+    if (m->ready) CSM_HIP(hipEventSynchronize(m->ready));
     CSM_HIP(hipMemcpy(out, m->levels.as<uint8_t>() + b.offset, n, hipMemcpyDeviceToHost));
   }
   return CSM_OK;
@@ -1392,6 +1403,9 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
   {
     int rc;
     if ((rc = EnsureDevice3(ctx))) return rc;
+    // Matchers built on another stream: their builds finish first.
+    for (int i = 0; i < num_submaps; ++i)
+      if ((rc = WaitBuilt(submaps[i]->ready, submaps[i]->ctx->stream, ctx->stream))) return rc;
     if (!ctx->f3_copy_stream) {
       CSM_HIP(hipStreamCreateWithFlags(&ctx->f3_copy_stream, hipStreamNonBlocking));
       CSM_HIP(hipEventCreateWithFlags(&ctx->f3_points_ready, hipEventDisableTiming));

@@ -123,3 +123,43 @@ def test_tsdf_c1_shaped_synthetic(csm, oracle):
             assert pose == ref_pose
             checked += 1
     assert checked >= 2
+
+
+@pytest.mark.parametrize("lin,ang_deg", [(0.5, 10.0), (3.5, 2.0)])
+def test_wide_windows(csm, oracle, lin, ang_deg):
+    """Windows whose candidates' gathered values do not fit one LDS stage
+    (+-0.5 m: 21 x offsets x 1080 points, staged in segments) or span several
+    64-offset chunks (+-3.5 m: 141 x offsets)."""
+    world = csm.SyntheticWorld2D(num_nodes=6, num_submaps=6, submap_cells=200, seed=13)
+    opts = (lin, math.radians(ang_deg), 0.1, 0.1)
+    m = csm.RealTimeCorrelativeScanMatcher2D(csm.RealTimeCorrelativeScanMatcherOptions(*opts))
+    rng = np.random.RandomState(3)
+    for s in range(2):
+        g = world.grid(s)
+        n = int(world.submap_nodes[s])
+        t = world.node_poses[n]
+        init = (t[0] + rng.uniform(-0.3, 0.3), t[1] + rng.uniform(-0.3, 0.3),
+                t[2] + math.radians(rng.uniform(-1, 1)))
+        cloud = world.cloud(n)
+        score, pose = m.Match(init, cloud, g)
+        ref_score, ref_pose, _ = oracle.rt2d_match((g.resolution, g.max_x, g.max_y), g.cells,
+                                                   opts, init, cloud)
+        assert abs(score - ref_score) <= 1e-6 * abs(ref_score)
+        assert pose == ref_pose
+
+
+def test_tsdf_wide_window(csm, oracle):
+    """TSDF2D with a window past one LDS stage (+-0.6 m: 25 x offsets of
+    8-byte terms) and a cloud past the staged point indices."""
+    limits, tsd, wgt = _seven_point_tsdf(oracle)
+    g = csm.TSDF2D(*limits, tsd, wgt, 0.3, 1.0)
+    # 5005 points: the point indices are read from global memory (> 4096).
+    cloud = np.repeat(SEVEN, 715, axis=0) + np.float32(1e-5) * np.arange(5005, dtype=np.float32)[:, None]
+    cloud[:, 2] = 0
+    opts = (0.6, 0.05, 0.1, 0.1)
+    m = csm.RealTimeCorrelativeScanMatcher2D(csm.RealTimeCorrelativeScanMatcherOptions(*opts))
+    init = (0.02, -0.03, 0.01)
+    score, pose = m.Match(init, cloud, g)
+    ref_score, ref_pose, _ = oracle.rt2d_match_tsdf(limits, tsd, wgt, 0.3, 1.0, opts, init, cloud)
+    assert abs(score - ref_score) <= 1e-6 * abs(ref_score)
+    assert pose == ref_pose

@@ -19,3 +19,5 @@ done
 timeout -k 10 400 python -u bench.py --workload c2 --no-cpu --no-3d --steps 5 > $O/bench_c2.json 2> $O/bench_c2.err \
   || { tail -20 $O/bench_c2.err; exit 1; }
 python3 -c "import json; d=json.loads(open('$O/bench_c2.json').read().strip().splitlines()[-1]); print(json.dumps(d['dropin']))"
+timeout -k 10 120 ./tools/gather_pattern_bench > $O/gather_pattern.txt 2>&1 || { cat $O/gather_pattern.txt; exit 1; }
+cat $O/gather_pattern.txt
