@@ -418,7 +418,29 @@ def rt2d_bench(csm, ctx, args):
         a = time.perf_counter()
         m.Match(init, cloud, g2 if k % 2 == 0 else g)
         times_changed.append(time.perf_counter() - a)
+    # The same call through the C-ABI with its arguments built once: what a
+    # C++ caller (the reference's LocalTrajectoryBuilder2D) pays per Match.
+    import ctypes as C
+    lib = ctx._lib
+    opts_c = csm.RtOptions(opts.linear_search_window, opts.angular_search_window,
+                           opts.translation_delta_cost_weight, opts.rotation_delta_cost_weight)
+    lim = g.limits()
+    cells = np.ascontiguousarray(g.cells, dtype=np.uint16)
+    pts = np.ascontiguousarray(np.asarray(cloud, np.float32)[:, :3])
+    init_c = csm.Pose2D(*init)
+    score_c, pose_c = C.c_double(0.0), csm.Pose2D()
+    args_c = (ctx.handle, C.byref(opts_c), C.byref(lim), cells.ctypes.data_as(C.POINTER(C.c_uint16)),
+              g.min_correspondence_cost, g.max_correspondence_cost, C.byref(init_c),
+              pts.ctypes.data_as(C.POINTER(C.c_float)), len(pts), C.byref(score_c), C.byref(pose_c))
+    times_c = []
+    for _ in range(100):
+        a = time.perf_counter()
+        rc = lib.csm_rt2d_match(*args_c)
+        times_c.append(time.perf_counter() - a)
+        if rc < 0:
+            raise RuntimeError(f"csm_rt2d_match: {rc}")
     res = {"gpu_ms_per_scan_match_median": 1e3 * float(np.median(times)),
+           "cabi_ms_per_scan_match_median": 1e3 * float(np.median(times_c)),
            "gpu_ms_per_scan_match_median_grid_changed": 1e3 * float(np.median(times_changed)),
            "kernel_ms_per_scan_match": kernel_ms,
            "points": len(cloud)}

@@ -765,15 +765,16 @@ class RealTimeCorrelativeScanMatcher2D:
         self.context = context or default_context()
         self._lib = self.context._lib
         self.options = options
+        o = options
+        self._opts = RtOptions(o.linear_search_window, o.angular_search_window,
+                               o.translation_delta_cost_weight, o.rotation_delta_cost_weight)
 
     def Match(self, initial_pose_estimate, point_cloud, grid):
         """real_time_correlative_scan_matcher_2d.h:66-68 -> (score, pose). ``grid`` is a
         ProbabilityGrid or a TSDF2D (ScoreCandidates switches on the grid type,
         .cc:155-168)."""
         pts = _f32_points(point_cloud)
-        o = self.options
-        opts = RtOptions(o.linear_search_window, o.angular_search_window,
-                         o.translation_delta_cost_weight, o.rotation_delta_cost_weight)
+        opts = self._opts
         lim = grid.limits()
         init = Pose2D(*initial_pose_estimate)
         score = C.c_double(0.0)

@@ -113,7 +113,6 @@ struct WorkQueues2 {
   int32_t queue_begin[kNumXcd + 1];
   int64_t queue_chunks[kNumXcd];
   int32_t rot_chunk;
-  int32_t sort_batch;  // fast2d_search_v4: batch nodes sorted by (rotation, level, y, x)
 };
 
 constexpr int kStack2 = 1024;   // v4 per-workgroup DFS stack entries in LDS

@@ -251,12 +251,6 @@ int LaunchSearch(csm_context* ctx, csm_scan_set* scans, const std::vector<PairDe
   WorkQueues2 wq2{};
   if (plan.use_v2) {
     wq2.rot_chunk = rc;
-    // CSM_SORT_BATCH=1: batch nodes in (rotation, level, y, x) order (A/B).
-    static const int sort_batch = [] {
-      const char* e = std::getenv("CSM_SORT_BATCH");
-      return e ? std::atoi(e) : 0;
-    }();
-    wq2.sort_batch = sort_batch;
     for (int x = 0; x < kNumXcd; ++x) {
       wq2.queue_begin[x] = wq.queue_begin[x];
       wq2.queue_chunks[x] = wq.queue_chunks[x];

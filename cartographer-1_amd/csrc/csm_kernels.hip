@@ -1496,43 +1496,16 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
                 __ballot(expandable && rank == nodes - 1))));
             int len = 0;
             const bool took = expandable && lane < take;
-            // Node slot: the rank among the taken entries, or (sort_batch) the
-            // position in (rotation, level, y, x) order, so that lanes on one
-            // row of one plane are adjacent and share cache lines in groups.
-            uint32_t ex = ent.x, ey = ent.y;
-            int slot = rank;
-            bool writes = took;
-            if (queues.sort_batch) {
-              const uint32_t ux = (ent.x & 0xffffu) ^ 0x8000u, uy = (ent.x >> 16) ^ 0x8000u;
-              uint64_t key = took ? (static_cast<uint64_t>((ent.y >> 22) & 0x3ffu) << 48) |
-                                        (static_cast<uint64_t>(uy) << 32) | (ux << 16) |
-                                        static_cast<uint64_t>(lane)
-                                  : ~0ull;
-              // Bitonic sort over the wave: ascending, lane i ends with the
-              // i-th smallest key (rotation and level in the top bits).
-              for (int k = 2; k <= 64; k <<= 1) {
-                for (int j = k >> 1; j > 0; j >>= 1) {
-                  const uint64_t o = __shfl_xor(key, j, 64);
-                  const bool keep_min = ((lane & j) == 0) == ((lane & k) == 0);
-                  key = keep_min ? (o < key ? o : key) : (o > key ? o : key);
-                }
-              }
-              const int src = static_cast<int>(key & 63u);
-              ex = static_cast<uint32_t>(__shfl(static_cast<int>(ent.x), src, 64));
-              ey = static_cast<uint32_t>(__shfl(static_cast<int>(ent.y), src, 64));
-              slot = lane;
-              writes = lane < nodes;
-            }
-            if (writes) {
-              const int r = (ey >> 22) & 0x1f, lvl = static_cast<int>(ey >> 27);
+            if (took) {
+              const int r = (ent.y >> 22) & 0x1f, lvl = static_cast<int>(ent.y >> 27);
               const int sl = sh.lv[lvl - (hexb ? 2 : 1)][6];
               len = sh.list_len[r][sl];
-              sh.node_xo[slot] = static_cast<int16_t>(ex & 0xffff);
-              sh.node_yo[slot] = static_cast<int>(ex) >> 16;
-              sh.node_rot[slot] = r;
-              sh.node_level[slot] = lvl;
-              sh.node_off[slot] = sh.list_off[r][sl];
-              sh.node_len[slot] = len;
+              sh.node_xo[rank] = static_cast<int16_t>(ent.x & 0xffff);
+              sh.node_yo[rank] = static_cast<int>(ent.x) >> 16;
+              sh.node_rot[rank] = r;
+              sh.node_level[rank] = lvl;
+              sh.node_off[rank] = sh.list_off[r][sl];
+              sh.node_len[rank] = len;
             }
             blen = DppMax(len);
             bent = DppSum(len);

@@ -84,50 +84,132 @@ __global__ void brick_scatter(const int32_t* __restrict__ ijk, const uint16_t* _
   out[k] = values[i];
 }
 
+// Cell (x, y, z) of brick b as a 32-bit offset (bricks are < 2^31 cells), or
+// -1 outside.
+__device__ __forceinline__ int BrickIndex32(const Brick3& b, int x, int y, int z) {
+  const int lx = x - b.ox, ly = y - b.oy, lz = z - b.oz;
+  if (static_cast<unsigned>(lx) >= static_cast<unsigned>(b.nx) ||
+      static_cast<unsigned>(ly) >= static_cast<unsigned>(b.ny) ||
+      static_cast<unsigned>(lz) >= static_cast<unsigned>(b.nz))
+    return -1;
+  return (lz * b.ny + ly) * b.nx + lx;
+}
+
 // PrecomputeGrid (precomputation_grid_3d.cc:63-81) in gather form:
 // out[j] = max over octants o of prev[j + shift*o], or, at half resolution,
-// max over o and e in {0,1}^3 of prev[2j + e + shift*o].
-__global__ void level_gather(const uint8_t* __restrict__ prev, Brick3 pb, uint8_t* __restrict__ out,
-                             Brick3 ob, int shift, int half) {
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  const int64_t total = static_cast<int64_t>(ob.nx) * ob.ny * ob.nz;
-  if (i >= total) return;
-  const int lx = static_cast<int>(i % ob.nx);
-  const int ly = static_cast<int>((i / ob.nx) % ob.ny);
-  const int lz = static_cast<int>(i / (static_cast<int64_t>(ob.nx) * ob.ny));
-  const int x = lx + ob.ox, y = ly + ob.oy, z = lz + ob.oz;
-  unsigned v = 0;
+// max over o and e in {0,1}^3 of prev[2j + e + shift*o]. Grid: (x blocks of
+// 256, y, z; strided past 65535), so a thread's cell needs no division.
+__global__ void __launch_bounds__(256)
+level_gather(const uint8_t* __restrict__ prev, Brick3 pb, uint8_t* __restrict__ out, Brick3 ob,
+             int shift, int half) {
+  const int lx = blockIdx.x * 256 + threadIdx.x;
+  if (lx >= ob.nx) return;
+  const int x = lx + ob.ox;
   const int reps = half ? 8 : 1;
-  for (int e = 0; e < reps; ++e) {
-    const int bx = half ? 2 * x + (e & 1) : x;
-    const int by = half ? 2 * y + ((e >> 1) & 1) : y;
-    const int bz = half ? 2 * z + ((e >> 2) & 1) : z;
-    for (int o = 0; o < 8; ++o) {
-      int64_t k;
-      if (InBrick(pb, bx + shift * (o & 1), by + shift * ((o >> 1) & 1),
-                  bz + shift * ((o >> 2) & 1), &k))
-        v = max(v, static_cast<unsigned>(prev[k]));
+  for (int lz = blockIdx.z; lz < ob.nz; lz += gridDim.z) {
+    for (int ly = blockIdx.y; ly < ob.ny; ly += gridDim.y) {
+      const int y = ly + ob.oy, z = lz + ob.oz;
+      unsigned v = 0;
+      for (int e = 0; e < reps; ++e) {
+        const int bx = half ? 2 * x + (e & 1) : x;
+        const int by = half ? 2 * y + ((e >> 1) & 1) : y;
+        const int bz = half ? 2 * z + ((e >> 2) & 1) : z;
+#pragma unroll
+        for (int o = 0; o < 8; ++o) {
+          const int k = BrickIndex32(pb, bx + shift * (o & 1), by + shift * ((o >> 1) & 1),
+                                     bz + shift * ((o >> 2) & 1));
+          if (k >= 0) v = max(v, static_cast<unsigned>(prev[k]));
+        }
+      }
+      out[(lz * ob.ny + ly) * ob.nx + lx] = static_cast<uint8_t>(v);
     }
   }
-  out[i] = static_cast<uint8_t>(v);
 }
 
 // Octet layout (Submap3Desc::octs): out[c] packs level[c + H*(x, y, z)].
-__global__ void octet_build(const uint8_t* __restrict__ level, Brick3 lb, int h,
-                            uint64_t* __restrict__ out, Brick3 ob) {
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  const int64_t total = static_cast<int64_t>(ob.nx) * ob.ny * ob.nz;
-  if (i >= total) return;
-  const int x = static_cast<int>(i % ob.nx) + ob.ox;
-  const int y = static_cast<int>((i / ob.nx) % ob.ny) + ob.oy;
-  const int z = static_cast<int>(i / (static_cast<int64_t>(ob.nx) * ob.ny)) + ob.oz;
-  uint64_t v = 0;
-  for (int k = 0; k < 8; ++k) {
-    int64_t idx;
-    if (InBrick(lb, x + h * (k & 1), y + h * ((k >> 1) & 1), z + h * ((k >> 2) & 1), &idx))
-      v |= static_cast<uint64_t>(level[idx]) << (8 * k);
+// Grid as level_gather's.
+__global__ void __launch_bounds__(256)
+octet_build(const uint8_t* __restrict__ level, Brick3 lb, int h, uint64_t* __restrict__ out,
+            Brick3 ob) {
+  const int lx = blockIdx.x * 256 + threadIdx.x;
+  if (lx >= ob.nx) return;
+  const int x = lx + ob.ox;
+  for (int lz = blockIdx.z; lz < ob.nz; lz += gridDim.z) {
+    for (int ly = blockIdx.y; ly < ob.ny; ly += gridDim.y) {
+      const int y = ly + ob.oy, z = lz + ob.oz;
+      uint64_t v = 0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int idx =
+            BrickIndex32(lb, x + h * (k & 1), y + h * ((k >> 1) & 1), z + h * ((k >> 2) & 1));
+        if (idx >= 0) v |= static_cast<uint64_t>(level[idx]) << (8 * k);
+      }
+      out[(lz * ob.ny + ly) * ob.nx + lx] = v;
+    }
   }
-  out[i] = v;
+}
+
+// Row form of octet_build and of the full-resolution level_gather: a
+// workgroup makes whole output rows (y, z) from the 4 source rows
+// (y + h ky, z + h kz), ky, kz in {0, 1}, staged in LDS with dword loads (the
+// per-cell kernels issue 8 byte loads per cell, which binds them on the
+// texture path, ~1 TB/s written). Cells outside the source brick read 0, as
+// InBrick does. kOctet: out[c] packs byte k = level[c + h (k&1, k>>1&1, k>>2)]
+// (octet_build); else out[c] = the max of those 8 bytes (level_gather with
+// shift h, half = 0).
+template <bool kOctet>
+__global__ void __launch_bounds__(256)
+brick_rows(const uint8_t* __restrict__ src, Brick3 sb, int h, void* __restrict__ out, Brick3 ob) {
+  extern __shared__ uint8_t rows[];  // 4 rows x pitch
+  const int W = ob.nx + h, pitch = (W + 3) & ~3;
+  const int src_bytes = sb.nx * sb.ny * sb.nz;
+  // Up to 3 bytes past the brick are read (levels are 256-byte aligned in
+  // their buffer) and masked below.
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint8_t*>(src), 0, (src_bytes + 3) & ~3, 0x00020000);
+  const int xs = ob.ox - sb.ox;  // source x (brick-relative) of LDS position 0
+  for (int lz = blockIdx.y; lz < ob.nz; lz += gridDim.y) {
+    for (int ly = blockIdx.x; ly < ob.ny; ly += gridDim.x) {
+      const int y = ly + ob.oy, z = lz + ob.oz;
+      __syncthreads();  // the previous row's reads are done
+      for (int r = 0; r < 4; ++r) {
+        const int yy = y + h * (r & 1) - sb.oy, zz = z + h * (r >> 1) - sb.oz;
+        const bool row_ok = static_cast<unsigned>(yy) < static_cast<unsigned>(sb.ny) &&
+                            static_cast<unsigned>(zz) < static_cast<unsigned>(sb.nz);
+        const int b0 = (row_ok ? (zz * sb.ny + yy) * sb.nx : 0) + xs;  // byte of position 0
+        const int a0 = b0 & ~3;
+        const int nwords = (W + (b0 - a0) + 3) >> 2;
+        for (int i = threadIdx.x; i < nwords; i += 256) {
+          const int a = a0 + 4 * i;
+          const uint32_t w = row_ok ? __builtin_amdgcn_raw_buffer_load_b32(rs, a, 0, 0) : 0u;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int pos = a + j - b0;
+            if (pos >= 0 && pos < W) {
+              const bool in = row_ok && static_cast<unsigned>(xs + pos) < static_cast<unsigned>(sb.nx);
+              rows[r * pitch + pos] = in ? static_cast<uint8_t>(w >> (8 * j)) : 0;
+            }
+          }
+        }
+      }
+      __syncthreads();
+      const int base = (lz * ob.ny + ly) * ob.nx;
+      for (int lx = threadIdx.x; lx < ob.nx; lx += 256) {
+        if constexpr (kOctet) {
+          uint64_t v = 0;
+#pragma unroll
+          for (int k = 0; k < 8; ++k)
+            v |= static_cast<uint64_t>(rows[(k >> 1) * pitch + lx + h * (k & 1)]) << (8 * k);
+          static_cast<uint64_t*>(out)[base + lx] = v;
+        } else {
+          unsigned v = 0;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) v = max(v, static_cast<unsigned>(rows[(k >> 1) * pitch + lx + h * (k & 1)]));
+          static_cast<uint8_t*>(out)[base + lx] = static_cast<uint8_t>(v);
+        }
+      }
+    }
+  }
 }
 
 // ------------------------------------------------------------- RTCSM3D ----
@@ -1964,19 +2046,33 @@ hipError_t LaunchBrickFromValues(const uint16_t* values, int64_t n, const float*
 
 hipError_t LaunchLevelGather(const uint8_t* prev, const Brick3& pb, uint8_t* out, const Brick3& ob,
                              int shift, int half, hipStream_t st) {
-  const int64_t total = static_cast<int64_t>(ob.nx) * ob.ny * ob.nz;
-  if (total <= 0) return hipSuccess;
-  hipLaunchKernelGGL(level_gather, dim3(static_cast<unsigned>((total + 255) / 256)), dim3(256), 0,
-                     st, prev, pb, out, ob, shift, half);
+  if (ob.nx <= 0 || ob.ny <= 0 || ob.nz <= 0) return hipSuccess;
+  const size_t row_lds = 4 * static_cast<size_t>((ob.nx + shift + 3) & ~3);
+  if (!half && row_lds <= 65536) {
+    hipLaunchKernelGGL(brick_rows<false>, dim3(std::min(ob.ny, 65535), std::min(ob.nz, 65535)),
+                       dim3(256), row_lds, st, prev, pb, shift, static_cast<void*>(out), ob);
+    return hipGetLastError();
+  }
+  hipLaunchKernelGGL(level_gather,
+                     dim3(static_cast<unsigned>((ob.nx + 255) / 256), std::min(ob.ny, 65535),
+                          std::min(ob.nz, 65535)),
+                     dim3(256), 0, st, prev, pb, out, ob, shift, half);
   return hipGetLastError();
 }
 
 hipError_t LaunchOctetBuild(const uint8_t* level, const Brick3& lb, int h, uint64_t* out,
                             const Brick3& ob, hipStream_t st) {
-  const int64_t total = static_cast<int64_t>(ob.nx) * ob.ny * ob.nz;
-  if (total <= 0) return hipSuccess;
-  hipLaunchKernelGGL(octet_build, dim3(static_cast<unsigned>((total + 255) / 256)), dim3(256), 0,
-                     st, level, lb, h, out, ob);
+  if (ob.nx <= 0 || ob.ny <= 0 || ob.nz <= 0) return hipSuccess;
+  const size_t row_lds = 4 * static_cast<size_t>((ob.nx + h + 3) & ~3);
+  if (row_lds <= 65536) {
+    hipLaunchKernelGGL(brick_rows<true>, dim3(std::min(ob.ny, 65535), std::min(ob.nz, 65535)),
+                       dim3(256), row_lds, st, level, lb, h, static_cast<void*>(out), ob);
+    return hipGetLastError();
+  }
+  hipLaunchKernelGGL(octet_build,
+                     dim3(static_cast<unsigned>((ob.nx + 255) / 256), std::min(ob.ny, 65535),
+                          std::min(ob.nz, 65535)),
+                     dim3(256), 0, st, level, lb, h, out, ob);
   return hipGetLastError();
 }
 

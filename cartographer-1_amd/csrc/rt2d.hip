@@ -32,9 +32,6 @@
 //                    spread the work over the CUs' texture units. The exp penalty is applied in double, and
 //                    the first maximum in (scan, x, y) order wins
 //                    (std::max_element, :142-143) through a 64-bit atomicMax.
-//   rt2d_score_staged  the default scorer (round 4): same workgroups, 4
-//                    waves; three gather segments of points x offsets into
-//                    LDS (all lanes busy), one adds them in point order.
 //   rt2d_score_list  ScoreCandidates for an arbitrary candidate list and
 //                    caller-given discrete scans (bounds-checked lookups).
 #include <hip/hip_runtime.h>
@@ -44,7 +41,6 @@
 #include <cmath>
 #include <cstdio>
 #include <mutex>
-#include <type_traits>
 #include <cstdlib>
 #include <cstring>
 #include <vector>
@@ -249,146 +245,6 @@ rt2d_score(Rt2dGridDev grid, int grid_bytes, const int* __restrict__ bases, int 
   if (valid)
     key = PenalizedKey(score, res, xo, yo, r, num_angular, step, wt, wr,
                        static_cast<uint32_t>(r * side * side + t));
-  for (int m = 32; m >= 1; m >>= 1) {
-    const unsigned long long o = __shfl_xor(key, m, 64);
-    key = o > key ? o : key;
-  }
-  if (lane == 0 && key != 0) atomicMax(best, key);
-}
-
-// Staged scoring (round 4): the same workgroup decomposition (rotation, y
-// offset, chunk of 64 x offsets), 4 waves, with the gathers taken off the
-// candidates' sequential float sums. Gathers fill an LDS stage densely with
-// (point, x offset) pairs over all lanes (a C1 window of 9 x offsets still
-// fills every lane), then wave 0 adds the stage in point order, one lane per
-// candidate. When the whole rotation fits the stage (`seg` >= n) all 4 waves
-// gather it at once and one barrier separates the phases; otherwise waves
-// 1-3 gather segment k + 1 while wave 0 adds segment k (two stages
-// alternate). The sums are the reference's sequential float sums,
-// bit-identical to rt2d_score's.
-template <bool kTsdf>
-__global__ void __launch_bounds__(256)
-rt2d_score_staged(Rt2dGridDev grid, int grid_bytes, const int* __restrict__ bases, int n, int npad,
-                  int side, int parts_x, int L, int num_angular, double step, double res,
-                  double wt, double wr, unsigned long long* __restrict__ best, int seg) {
-  using Value = typename std::conditional<kTsdf, float2, float>::type;
-  constexpr int kBasesLds = 4096;  // rotation's point indices staged in LDS up to this many
-  extern __shared__ __align__(16) unsigned char stage_raw[];
-  __shared__ int sb[kBasesLds];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int blk = blockIdx.x;
-  const int r = blk / (side * parts_x);
-  const int rem = blk - r * side * parts_x;
-  const int yi = rem / parts_x, x0 = (rem - yi * parts_x) * 64;
-  const int nxv = min(64, side - x0);  // x offsets of this chunk
-  const int yo = -L + yi;
-  const int* __restrict__ B = bases + static_cast<int64_t>(r) * npad;
-  const bool lds_bases = n <= kBasesLds;
-  if (lds_bases)
-    for (int i = tid; i < n; i += 256) sb[i] = B[i];
-  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-      kTsdf ? static_cast<void*>(const_cast<float2*>(grid.tsdf))
-            : static_cast<void*>(const_cast<float*>(grid.prob)),
-      0, grid_bytes, 0x00020000);
-  constexpr int kShift = kTsdf ? 3 : 2;
-  const int row_off = yo * grid.W + x0 - L;  // + x: the candidate's offset
-  const bool single = seg >= n;
-  const int nseg = single ? 1 : (n + seg - 1) / seg;
-  Value* const st0 = reinterpret_cast<Value*>(stage_raw);
-  Value* const st1 = st0 + static_cast<size_t>(seg) * min(64, side);
-  // Gathers of segment k into `buf` by threads t0 = 0.. nthr - 1: pair
-  // f = t0 + j * nthr is (point f / nxv, x offset f % nxv), stored at buf[f].
-  auto gather = [&](int k, Value* buf, int t0, int nthr) {
-    const int p0 = k * seg, cnt = min(seg, n - p0), total = cnt * nxv;
-    const int dq = nthr / nxv, dr = nthr - dq * nxv;
-    int pt = t0 / nxv, xx = t0 - pt * nxv;
-    constexpr int kG = 16;  // loads in flight per thread
-    for (int f0 = t0; f0 < total; f0 += nthr * kG) {
-      Value v[kG];
-      int slot[kG];
-#pragma unroll
-      for (int u = 0; u < kG; ++u) {
-        const int f = f0 + u * nthr;
-        const bool in = f < total;
-        const int q = in ? p0 + pt : 0;
-        const int idx = lds_bases ? sb[q] : B[q];
-        const int byte = (idx + row_off + xx) << kShift;
-        if constexpr (kTsdf) {
-          const auto w = __builtin_amdgcn_raw_buffer_load_b64(rsrc, byte, 0, 0);
-          v[u] = make_float2(__uint_as_float(w[0]), __uint_as_float(w[1]));
-        } else {
-          v[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, byte, 0, 0));
-        }
-        slot[u] = in ? f : -1;
-        pt += dq;
-        xx += dr;
-        if (xx >= nxv) {
-          xx -= nxv;
-          ++pt;
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < kG; ++u)
-        if (slot[u] >= 0) buf[slot[u]] = v[u];
-    }
-  };
-  float s = 0.f, sw = 0.f;
-  const int my = min(lane, nxv - 1);
-  auto add = [&](const Value* buf, int cnt) {
-    const Value* col = buf + my;
-    int p = 0;
-    for (; p + 32 <= cnt; p += 32) {
-      Value v[32];
-#pragma unroll
-      for (int u = 0; u < 32; ++u) v[u] = col[(p + u) * nxv];
-#pragma unroll
-      for (int u = 0; u < 32; ++u) {
-        if constexpr (kTsdf) {
-          s = __fadd_rn(s, v[u].x);
-          sw = __fadd_rn(sw, v[u].y);
-        } else {
-          s = __fadd_rn(s, v[u]);
-        }
-      }
-    }
-    for (; p < cnt; ++p) {
-      const Value v = col[p * nxv];
-      if constexpr (kTsdf) {
-        s = __fadd_rn(s, v.x);
-        sw = __fadd_rn(sw, v.y);
-      } else {
-        s = __fadd_rn(s, v);
-      }
-    }
-  };
-  __syncthreads();  // sb
-  if (single) {
-    gather(0, st0, tid, 256);
-    __syncthreads();
-    if (wave == 0) add(st0, n);
-  } else {
-    if (wave > 0) gather(0, st0, tid - 64, 192);
-    __syncthreads();
-    for (int k = 0; k < nseg; ++k) {
-      if (wave > 0) {
-        if (k + 1 < nseg) gather(k + 1, (k + 1) & 1 ? st1 : st0, tid - 64, 192);
-      } else {
-        add(k & 1 ? st1 : st0, min(seg, n - k * seg));
-      }
-      __syncthreads();
-    }
-  }
-  if (wave != 0) return;
-  const bool valid = lane < nxv;
-  const int xi = x0 + (valid ? lane : 0);
-  const int xo = -L + xi;
-  float score;
-  if constexpr (kTsdf) score = sw == 0.f ? 0.f : __fdiv_rn(s, sw);
-  else score = __fdiv_rn(s, static_cast<float>(n));
-  unsigned long long key = 0;
-  if (valid)
-    key = PenalizedKey(score, res, xo, yo, r, num_angular, step, wt, wr,
-                       static_cast<uint32_t>(r * side * side + xi * side + yi));
   for (int m = 32; m >= 1; m >>= 1) {
     const unsigned long long o = __shfl_xor(key, m, 64);
     key = o > key ? o : key;
@@ -615,48 +471,30 @@ int Rt2dMatch(csm_context* ctx, const csm_rt_options* o, const GridArgs& g,
   CSM_HIP(hipGetLastError());
   const int parts_x = (side + 63) / 64;
   const dim3 blocks(static_cast<unsigned>(static_cast<int64_t>(w.num_scans) * side * parts_x));
-  // Scoring kernel: staged (default) or the one-wave pipelined rt2d_score
-  // (CSM_RT2D_KERNEL=1, A/B). rt2d_score's pipeline batch: 32 gathers (x2 in
-  // flight) by default, measured fastest (C1: 20.5 us against 22.8 at 16 and
-  // 29.4 at 8, profiles/r2/rt2d_depth); CSM_RT2D_DEPTH selects 8 or 16.
-  static const bool staged = [] {
-    const char* e = std::getenv("CSM_RT2D_KERNEL");
-    return !(e && std::atoi(e) == 1);
-  }();
+  // Pipeline batch: 32 gathers (x2 in flight) by default, measured fastest
+  // (C1: 20.5 us against 22.8 at 16 and 29.4 at 8, profiles/r2/rt2d_depth);
+  // CSM_RT2D_DEPTH selects 8 or 16 for experiments.
   static const int depth = [] {
     const char* e = std::getenv("CSM_RT2D_DEPTH");
     const int d = e ? std::atoi(e) : 32;
     return (d == 8 || d == 16) ? d : 32;
   }();
-#define CSM_RT2D_ARGS                                                                  \
-  grid, grid_bytes, c.bases.as<int>(), n, npad, side, parts_x, L,                     \
-      w.num_angular_perturbations, w.angular_perturbation_step_size, l->resolution,   \
-      o->translation_delta_cost_weight, o->rotation_delta_cost_weight,                \
-      c.best.as<unsigned long long>()
-#define CSM_RT2D_DEPTHS(TSDF)                                                                         \
-  do {                                                                                                \
-    if (depth == 8) hipLaunchKernelGGL((rt2d_score<TSDF, 8>), blocks, dim3(64), 0, st, CSM_RT2D_ARGS); \
-    else if (depth == 32) hipLaunchKernelGGL((rt2d_score<TSDF, 32>), blocks, dim3(64), 0, st, CSM_RT2D_ARGS); \
-    else hipLaunchKernelGGL((rt2d_score<TSDF, 16>), blocks, dim3(64), 0, st, CSM_RT2D_ARGS);          \
+#define CSM_RT2D_LAUNCH(TSDF, D)                                                                \
+  hipLaunchKernelGGL((rt2d_score<TSDF, D>), blocks, dim3(64), 0, st, grid, grid_bytes,          \
+                     c.bases.as<int>(), n, npad, side, parts_x, L, w.num_angular_perturbations, \
+                     w.angular_perturbation_step_size, l->resolution,                           \
+                     o->translation_delta_cost_weight, o->rotation_delta_cost_weight,           \
+                     c.best.as<unsigned long long>())
+#define CSM_RT2D_DEPTHS(TSDF)                 \
+  do {                                        \
+    if (depth == 8) CSM_RT2D_LAUNCH(TSDF, 8); \
+    else if (depth == 32) CSM_RT2D_LAUNCH(TSDF, 32); \
+    else CSM_RT2D_LAUNCH(TSDF, 16);           \
   } while (0)
-  if (staged) {
-    // Stage: the whole rotation when it fits 64 KB, else two 32 KB segments.
-    const size_t per_point = static_cast<size_t>(std::min(64, side)) * (g.wcells ? 8 : 4);
-    const int seg = static_cast<size_t>(n) * per_point <= 65536
-                        ? n
-                        : static_cast<int>(32768 / per_point);
-    const size_t lds = seg >= n ? static_cast<size_t>(n) * per_point : 2 * seg * per_point;
-    if (g.wcells)
-      hipLaunchKernelGGL((rt2d_score_staged<true>), blocks, dim3(256), lds, st, CSM_RT2D_ARGS, seg);
-    else
-      hipLaunchKernelGGL((rt2d_score_staged<false>), blocks, dim3(256), lds, st, CSM_RT2D_ARGS, seg);
-  } else if (g.wcells) {
-    CSM_RT2D_DEPTHS(true);
-  } else {
-    CSM_RT2D_DEPTHS(false);
-  }
+  if (g.wcells) CSM_RT2D_DEPTHS(true);
+  else CSM_RT2D_DEPTHS(false);
 #undef CSM_RT2D_DEPTHS
-#undef CSM_RT2D_ARGS
+#undef CSM_RT2D_LAUNCH
   CSM_HIP(hipGetLastError());
   if (ctx->timing) CSM_HIP(hipEventRecord(ctx->ev1, st));
   CSM_HIP(hipMemcpyAsync(hk, c.best.ptr, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
