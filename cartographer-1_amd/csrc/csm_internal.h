@@ -115,7 +115,7 @@ struct Rt2dCache {
   float ttab_key[2] = {0.f, 0.f};
   std::vector<uint16_t> cells, wcells;
   DevBuf grid, dcells, ptab, ttab, bases, best, dstage, sink;
-  PinnedBuf stage, stage_cells, host_key;
+  PinnedBuf stage, stage_cells, host_key, wg_keys;  // wg_keys: per-workgroup keys (zero-copy path)
 };
 
 }  // namespace csm

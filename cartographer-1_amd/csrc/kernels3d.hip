@@ -149,31 +149,46 @@ octet_build(const uint8_t* __restrict__ level, Brick3 lb, int h, uint64_t* __res
   }
 }
 
-// Row form of octet_build and of the full-resolution level_gather: a
-// workgroup makes whole output rows (y, z) from the 4 source rows
-// (y + h ky, z + h kz), ky, kz in {0, 1}, staged in LDS with dword loads (the
-// per-cell kernels issue 8 byte loads per cell, which binds them on the
-// texture path, ~1 TB/s written). Cells outside the source brick read 0, as
-// InBrick does. kOctet: out[c] packs byte k = level[c + h (k&1, k>>1&1, k>>2)]
-// (octet_build); else out[c] = the max of those 8 bytes (level_gather with
-// shift h, half = 0).
-template <bool kOctet>
+// Row form of octet_build and level_gather: a workgroup makes whole output
+// rows (y, z) from the source rows they read, staged in LDS with dword loads
+// (the per-cell kernels issue 8 or 64 byte loads per cell, which binds them
+// on the texture path). Cells outside the source brick read 0, as InBrick
+// does.
+//   kOctet: out[c] packs byte k = level[c + h (k&1, k>>1&1, k>>2)] (octet_build;
+//     4 source rows (y + h ky, z + h kz)).
+//   else, full resolution: out[c] = the max of those 8 bytes (level_gather
+//     with shift h, half = 0; 4 source rows).
+//   kHalf: out[c] = max over e, o in {0,1}^3 of prev[2c + e + h o]
+//     (level_gather with half = 1): 16 source rows (2y + {0, 1, h, h + 1}) x
+//     (2z + {0, 1, h, h + 1}), 4 x positions each.
+template <bool kOctet, bool kHalf>
 __global__ void __launch_bounds__(256)
 brick_rows(const uint8_t* __restrict__ src, Brick3 sb, int h, void* __restrict__ out, Brick3 ob) {
-  extern __shared__ uint8_t rows[];  // 4 rows x pitch
-  const int W = ob.nx + h, pitch = (W + 3) & ~3;
+  static_assert(!(kOctet && kHalf), "octets are built at the level's own resolution");
+  constexpr int kRows = kHalf ? 16 : 4;
+  extern __shared__ uint8_t rows[];  // kRows rows x pitch
+  const int W = kHalf ? 2 * ob.nx + h : ob.nx + h, pitch = (W + 3) & ~3;
   const int src_bytes = sb.nx * sb.ny * sb.nz;
   // Up to 3 bytes past the brick are read (levels are 256-byte aligned in
   // their buffer) and masked below.
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<uint8_t*>(src), 0, (src_bytes + 3) & ~3, 0x00020000);
-  const int xs = ob.ox - sb.ox;  // source x (brick-relative) of LDS position 0
+  const int xs = (kHalf ? 2 * ob.ox : ob.ox) - sb.ox;  // source x (brick-relative) of position 0
   for (int lz = blockIdx.y; lz < ob.nz; lz += gridDim.y) {
     for (int ly = blockIdx.x; ly < ob.ny; ly += gridDim.x) {
       const int y = ly + ob.oy, z = lz + ob.oz;
       __syncthreads();  // the previous row's reads are done
-      for (int r = 0; r < 4; ++r) {
-        const int yy = y + h * (r & 1) - sb.oy, zz = z + h * (r >> 1) - sb.oz;
+      for (int r = 0; r < kRows; ++r) {
+        int yy, zz;
+        if constexpr (kHalf) {
+          yy = 2 * y + (r & 1) + h * ((r >> 1) & 1);
+          zz = 2 * z + ((r >> 2) & 1) + h * (r >> 3);
+        } else {
+          yy = y + h * (r & 1);
+          zz = z + h * (r >> 1);
+        }
+        yy -= sb.oy;
+        zz -= sb.oz;
         const bool row_ok = static_cast<unsigned>(yy) < static_cast<unsigned>(sb.ny) &&
                             static_cast<unsigned>(zz) < static_cast<unsigned>(sb.nz);
         const int b0 = (row_ok ? (zz * sb.ny + yy) * sb.nx : 0) + xs;  // byte of position 0
@@ -201,10 +216,21 @@ brick_rows(const uint8_t* __restrict__ src, Brick3 sb, int h, void* __restrict__
           for (int k = 0; k < 8; ++k)
             v |= static_cast<uint64_t>(rows[(k >> 1) * pitch + lx + h * (k & 1)]) << (8 * k);
           static_cast<uint64_t*>(out)[base + lx] = v;
+        } else if constexpr (kHalf) {
+          unsigned v = 0;
+          const int p = 2 * lx;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const uint8_t* row = rows + r * pitch + p;
+            v = max(v, max(max(static_cast<unsigned>(row[0]), static_cast<unsigned>(row[1])),
+                           max(static_cast<unsigned>(row[h]), static_cast<unsigned>(row[h + 1]))));
+          }
+          static_cast<uint8_t*>(out)[base + lx] = static_cast<uint8_t>(v);
         } else {
           unsigned v = 0;
 #pragma unroll
-          for (int k = 0; k < 8; ++k) v = max(v, static_cast<unsigned>(rows[(k >> 1) * pitch + lx + h * (k & 1)]));
+          for (int k = 0; k < 8; ++k)
+            v = max(v, static_cast<unsigned>(rows[(k >> 1) * pitch + lx + h * (k & 1)]));
           static_cast<uint8_t*>(out)[base + lx] = static_cast<uint8_t>(v);
         }
       }
@@ -2047,10 +2073,16 @@ hipError_t LaunchBrickFromValues(const uint16_t* values, int64_t n, const float*
 hipError_t LaunchLevelGather(const uint8_t* prev, const Brick3& pb, uint8_t* out, const Brick3& ob,
                              int shift, int half, hipStream_t st) {
   if (ob.nx <= 0 || ob.ny <= 0 || ob.nz <= 0) return hipSuccess;
-  const size_t row_lds = 4 * static_cast<size_t>((ob.nx + shift + 3) & ~3);
-  if (!half && row_lds <= 65536) {
-    hipLaunchKernelGGL(brick_rows<false>, dim3(std::min(ob.ny, 65535), std::min(ob.nz, 65535)),
-                       dim3(256), row_lds, st, prev, pb, shift, static_cast<void*>(out), ob);
+  const size_t row_lds = half ? 16 * static_cast<size_t>((2 * ob.nx + shift + 3) & ~3)
+                              : 4 * static_cast<size_t>((ob.nx + shift + 3) & ~3);
+  if (row_lds <= 65536) {
+    const dim3 grid(std::min(ob.ny, 65535), std::min(ob.nz, 65535));
+    if (half)
+      hipLaunchKernelGGL((brick_rows<false, true>), grid, dim3(256), row_lds, st, prev, pb, shift,
+                         static_cast<void*>(out), ob);
+    else
+      hipLaunchKernelGGL((brick_rows<false, false>), grid, dim3(256), row_lds, st, prev, pb, shift,
+                         static_cast<void*>(out), ob);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(level_gather,
@@ -2065,7 +2097,7 @@ hipError_t LaunchOctetBuild(const uint8_t* level, const Brick3& lb, int h, uint6
   if (ob.nx <= 0 || ob.ny <= 0 || ob.nz <= 0) return hipSuccess;
   const size_t row_lds = 4 * static_cast<size_t>((ob.nx + h + 3) & ~3);
   if (row_lds <= 65536) {
-    hipLaunchKernelGGL(brick_rows<true>, dim3(std::min(ob.ny, 65535), std::min(ob.nz, 65535)),
+    hipLaunchKernelGGL((brick_rows<true, false>), dim3(std::min(ob.ny, 65535), std::min(ob.nz, 65535)),
                        dim3(256), row_lds, st, level, lb, h, static_cast<void*>(out), ob);
     return hipGetLastError();
   }

@@ -142,8 +142,11 @@ template <bool kTsdf, int kDepth>
 __global__ void __launch_bounds__(64)
 rt2d_score(Rt2dGridDev grid, int grid_bytes, const int* __restrict__ bases, int n, int npad,
            int side, int parts_x, int L, int num_angular, double step, double res,
-           double wt, double wr, unsigned long long* __restrict__ best) {
+           double wt, double wr, unsigned long long* __restrict__ best,
+           unsigned long long* __restrict__ wg_keys) {
   // Workgroup = (rotation, y offset, chunk of x offsets); lane = x offset.
+  // wg_keys (mapped host memory): each workgroup stores its best key there
+  // instead of the device atomicMax, and the host takes the max.
   // Lanes then read one grid row (x is the fastest index), so a gather
   // touches one or two cache lines.
   const int blk = blockIdx.x;
@@ -249,7 +252,11 @@ rt2d_score(Rt2dGridDev grid, int grid_bytes, const int* __restrict__ bases, int 
     const unsigned long long o = __shfl_xor(key, m, 64);
     key = o > key ? o : key;
   }
-  if (lane == 0 && key != 0) atomicMax(best, key);
+  if (wg_keys) {
+    if (lane == 0) wg_keys[blk] = key;
+  } else if (lane == 0 && key != 0) {
+    atomicMax(best, key);
+  }
 }
 
 struct CandDev {
@@ -447,6 +454,23 @@ int Rt2dMatch(csm_context* ctx, const csm_rt_options* o, const GridArgs& g,
   if ((rc = c.bases.Reserve(sizeof(int) * static_cast<size_t>(w.num_scans) * npad))) return rc;
   if ((rc = c.best.Reserve(sizeof(unsigned long long)))) return rc;
   if ((rc = c.host_key.Reserve(sizeof(unsigned long long)))) return rc;
+  const int parts_x = (side + 63) / 64;
+  const int64_t num_blocks = static_cast<int64_t>(w.num_scans) * side * parts_x;
+  // Keys to host memory (default; CSM_RT2D_HOSTKEYS=0 for the copy path):
+  // each scoring workgroup writes its best key to mapped pinned memory,
+  // reduced here after the synchronize, so no device-to-host copy is queued
+  // and the workgroups do not contend on one atomic.
+  static const bool hostkeys = [] {
+    const char* e = std::getenv("CSM_RT2D_HOSTKEYS");
+    return !(e && std::atoi(e) == 0);
+  }();
+  if ((rc = c.wg_keys.Reserve(sizeof(unsigned long long) * (hostkeys ? num_blocks : 1)))) return rc;
+  unsigned long long* dkeys = nullptr;
+  if (hostkeys) {
+    void* dk = nullptr;
+    CSM_HIP(hipHostGetDevicePointer(&dk, c.wg_keys.ptr, 0));
+    dkeys = static_cast<unsigned long long*>(dk);
+  }
   char* h = c.stage.as<char>();
   std::memcpy(h, xyz, pts_bytes);
   float2* hr = reinterpret_cast<float2*>(h + rot_off);
@@ -466,11 +490,10 @@ int Rt2dMatch(csm_context* ctx, const csm_rt_options* o, const GridArgs& g,
                      0, st, dpts, n, npad, drot, w.num_scans, pre.w, pre.s,
                      static_cast<float>(initial->x), static_cast<float>(initial->y), l->max_x,
                      l->max_y, l->resolution, l->num_x_cells, l->num_y_cells, L, P,
-                     c.bases.as<int>(), c.best.as<unsigned long long>(),
+                     c.bases.as<int>(), hostkeys ? nullptr : c.best.as<unsigned long long>(),
                      c.grid.as<uint32_t>(), grid_bytes / 4, c.sink.as<uint32_t>());
   CSM_HIP(hipGetLastError());
-  const int parts_x = (side + 63) / 64;
-  const dim3 blocks(static_cast<unsigned>(static_cast<int64_t>(w.num_scans) * side * parts_x));
+  const dim3 blocks(static_cast<unsigned>(num_blocks));
   // Pipeline batch: 32 gathers (x2 in flight) by default, measured fastest
   // (C1: 20.5 us against 22.8 at 16 and 29.4 at 8, profiles/r2/rt2d_depth);
   // CSM_RT2D_DEPTH selects 8 or 16 for experiments.
@@ -484,7 +507,7 @@ int Rt2dMatch(csm_context* ctx, const csm_rt_options* o, const GridArgs& g,
                      c.bases.as<int>(), n, npad, side, parts_x, L, w.num_angular_perturbations, \
                      w.angular_perturbation_step_size, l->resolution,                           \
                      o->translation_delta_cost_weight, o->rotation_delta_cost_weight,           \
-                     c.best.as<unsigned long long>())
+                     c.best.as<unsigned long long>(), dkeys)
 #define CSM_RT2D_DEPTHS(TSDF)                 \
   do {                                        \
     if (depth == 8) CSM_RT2D_LAUNCH(TSDF, 8); \
@@ -497,9 +520,19 @@ int Rt2dMatch(csm_context* ctx, const csm_rt_options* o, const GridArgs& g,
 #undef CSM_RT2D_LAUNCH
   CSM_HIP(hipGetLastError());
   if (ctx->timing) CSM_HIP(hipEventRecord(ctx->ev1, st));
-  CSM_HIP(hipMemcpyAsync(hk, c.best.ptr, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+  if (!hostkeys)
+    CSM_HIP(hipMemcpyAsync(hk, c.best.ptr, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
   const auto t_launch = Rt2dClock::now();
   CSM_HIP(hipStreamSynchronize(st));
+  if (hostkeys) {  // the workgroups' keys: the first maximum in (scan, x, y) order wins
+    const volatile unsigned long long* keys = c.wg_keys.as<unsigned long long>();
+    unsigned long long k = 0;
+    for (int64_t b = 0; b < num_blocks; ++b) {
+      const unsigned long long v = keys[b];
+      k = v > k ? v : k;
+    }
+    *hk = k;
+  }
   if (ctx->timing) {
     float ms = 0.f;
     CSM_HIP(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));

@@ -17,7 +17,7 @@ for st in "$@"; do
   echo "== $st $(date +%T)"
   case $st in
     tests)
-      timeout -k 10 400 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
+      timeout -k 10 700 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
         > $OUT/gpu_tests.log 2>&1 || { tail -30 $OUT/gpu_tests.log; exit 1; } ;;
     bench)
       t0=$(date +%s)
