@@ -496,6 +496,18 @@ def dropin_bench(csm, ctx, matchers, scans, world, args):
             list(ex.map(one, range(calls)))
             wall = time.perf_counter() - a
         threaded[str(T)] = {"calls": calls, "pairs_per_s": calls / wall}
+    # The same pattern from C++ threads (tools/dropin_threads.cc, no GIL):
+    # what the reference's ThreadPool sees through the C-ABI.
+    threaded_cpp = None
+    exe = os.path.join(ROOT, "tools", "dropin_threads")
+    if os.path.exists(exe):
+        import subprocess
+        try:
+            out = subprocess.run([exe, "2000", str(args.min_score)], capture_output=True, text=True,
+                                 timeout=300, check=True).stdout
+            threaded_cpp = json.loads(out.strip().splitlines()[-1])
+        except (subprocess.SubprocessError, ValueError) as e:
+            threaded_cpp = {"error": str(e)[:200]}
     return {"per_node_flush": {"pairs_per_flush": k, "flushes": nodes,
                                "ms_per_flush_median": float(np.median(flush_ms)),
                                "pairs_per_s": k / (float(np.median(flush_ms)) * 1e-3)},
@@ -503,6 +515,7 @@ def dropin_bench(csm, ctx, matchers, scans, world, args):
                             "ms_per_match_full_submap_median": float(np.median(single_ms)),
                             "pairs_per_s": 1e3 / float(np.median(single_ms))},
             "single_call_threads": threaded,
+            "single_call_threads_cpp": threaded_cpp,
             "note": "through the Python ctypes mirror; a batch uploads its pair descriptors, the "
                     "scan set's rotation tables are built once and kept on the device"}
 

@@ -194,13 +194,33 @@ int csm_hybrid_grid_create(csm_context* ctx, float resolution, const int32_t* ij
   auto g = std::make_unique<csm_hybrid_grid>();
   g->ctx = ctx;
   g->resolution = resolution;
+  // The cell list goes up through pinned staging and is scattered into the
+  // zeroed brick on the device (no dense host copy); bricks come from the
+  // context's pool (BufPool). One pass copies the indices into the staging
+  // and takes their bounds (the brick box). The staging is rewritten only
+  // once the previous create's copy out of it has finished (the kernels are
+  // not waited for).
+  const size_t list_bytes = static_cast<size_t>(count) * (3 * sizeof(int32_t) + sizeof(uint16_t));
   int lo[3] = {0, 0, 0}, hi[3] = {-1, -1, -1};
-  for (int64_t i = 0; i < count; ++i)
-    for (int a = 0; a < 3; ++a) {
-      const int v = ijk[3 * i + a];
-      if (i == 0 || v < lo[a]) lo[a] = v;
-      if (i == 0 || v > hi[a]) hi[a] = v;
+  if (count > 0) {
+    if (ctx->f3_stage_copied) CSM_HIP(hipEventSynchronize(ctx->f3_stage_copied));
+    else CSM_HIP(hipEventCreateWithFlags(&ctx->f3_stage_copied, hipEventDisableTiming));
+    if ((rc = ctx->f3_grid_stage.Reserve(list_bytes))) return rc;
+    int32_t* hs = ctx->f3_grid_stage.as<int32_t>();
+    int lx = ijk[0], ly = ijk[1], lz = ijk[2], ux = lx, uy = ly, uz = lz;
+    for (int64_t i = 0; i < count; ++i) {
+      const int x = ijk[3 * i], y = ijk[3 * i + 1], z = ijk[3 * i + 2];
+      hs[3 * i] = x;
+      hs[3 * i + 1] = y;
+      hs[3 * i + 2] = z;
+      lx = std::min(lx, x); ux = std::max(ux, x);
+      ly = std::min(ly, y); uy = std::max(uy, y);
+      lz = std::min(lz, z); uz = std::max(uz, z);
     }
+    std::memcpy(hs + 3 * count, values, sizeof(uint16_t) * count);
+    lo[0] = lx; lo[1] = ly; lo[2] = lz;
+    hi[0] = ux; hi[1] = uy; hi[2] = uz;
+  }
   if (grid_size <= 0) {  // DynamicGrid growth (hybrid_grid.h:283-296, :384-399)
     int gs = 128;
     for (int a = 0; a < 3 && count > 0; ++a)
@@ -219,24 +239,13 @@ int csm_hybrid_grid_create(csm_context* ctx, float resolution, const int32_t* ij
   const int64_t n = static_cast<int64_t>(b.nx) * b.ny * b.nz;
   if (n > (int64_t{1} << 31)) return CSM_ERANGE;
   if (n > 0) {
-    // The cell list goes up through pinned staging and is scattered into the
-    // zeroed brick on the device (no dense host copy); bricks come from the
-    // context's pool (BufPool).
     if ((rc = EnsureValueTables(ctx))) return rc;
-    const size_t list_bytes = static_cast<size_t>(count) * (3 * sizeof(int32_t) + sizeof(uint16_t));
-    if ((rc = ctx->f3_grid_stage.Reserve(list_bytes))) return rc;
     if ((rc = ctx->f3_grid_cells.Reserve(list_bytes))) return rc;
     if ((rc = ctx->pool.Take(sizeof(uint16_t) * n, &g->values))) return rc;
     if ((rc = ctx->pool.Take(sizeof(float) * n, &g->prob))) return rc;
-    // The staging buffer is rewritten only once the previous create's copy
-    // out of it has finished (the kernels are not waited for).
-    if (ctx->f3_stage_copied) CSM_HIP(hipEventSynchronize(ctx->f3_stage_copied));
-    else CSM_HIP(hipEventCreateWithFlags(&ctx->f3_stage_copied, hipEventDisableTiming));
-    char* h = ctx->f3_grid_stage.as<char>();
-    std::memcpy(h, ijk, sizeof(int32_t) * 3 * count);
-    std::memcpy(h + sizeof(int32_t) * 3 * count, values, sizeof(uint16_t) * count);
     hipStream_t st = ctx->stream;
-    CSM_HIP(hipMemcpyAsync(ctx->f3_grid_cells.ptr, h, list_bytes, hipMemcpyHostToDevice, st));
+    CSM_HIP(hipMemcpyAsync(ctx->f3_grid_cells.ptr, ctx->f3_grid_stage.ptr, list_bytes,
+                           hipMemcpyHostToDevice, st));
     CSM_HIP(hipEventRecord(ctx->f3_stage_copied, st));
     CSM_HIP(hipMemsetAsync(g->values.ptr, 0, sizeof(uint16_t) * n, st));
     const int32_t* dijk = ctx->f3_grid_cells.as<int32_t>();

@@ -8,6 +8,7 @@
 #   c3      bench.py --workload c3 (2000 x 1000 queue, 1 GPU) + CPU baseline
 #   c3trace rocprofv3 --kernel-trace --stats of two 16-submap slices of the C3 queue (8 chunk launches)
 #   c3pmc   FETCH_SIZE pass on one 16-submap slice of the C3 queue (4 chunk launches)
+#   c5      C5 probe (builds inside the step), its kernel trace and PMC passes of fast3d_search
 set -u
 OUT=$1; shift
 R=${GRAFT_REPO_ROOT:-$PWD}
@@ -59,6 +60,21 @@ for st in "$@"; do
         > $R/$OUT/c3pmc/p0.json 2> $R/$OUT/c3pmc/p0.log) || { echo "c3 pmc pass failed"; tail -5 $OUT/c3pmc/p0.log; exit 1; }
       ms=$(python3 -c "import json,sys; print(json.loads([l for l in open('$OUT/c3pmc/p0.json') if l.startswith('{')][-1])['roofline']['kernel_ms_avg'])" 2>/dev/null || echo 0)
       python3 tools/traffic_json.py $OUT/c3pmc $OUT/traffic_c3.json $(python3 -c "import sys; sys.path.insert(0,'.'); import bench; print(bench.KERNEL_TAG)") $ms c3 2000 4 16 ;;
+    c5)
+      mkdir -p $OUT/pmc3d
+      timeout -k 10 300 python -u tools/probe_c5.py > $OUT/c5.json 2> $OUT/c5.err || { tail -20 $OUT/c5.err; exit 1; }
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/$OUT/c5trace \
+        -o c5 --output-format csv -- python3 $R/tools/probe_c5.py > $R/$OUT/c5trace.json 2> $R/$OUT/c5trace.err) \
+        || { tail -20 $OUT/c5trace.err; exit 1; }
+      i=0
+      for g in "FETCH_SIZE" "TCC_HIT_sum TCC_MISS_sum TCC_REQ_sum" "TA_TA_BUSY_sum TA_BUFFER_READ_WAVEFRONTS_sum GRBM_GUI_ACTIVE" \
+               "TD_TD_BUSY_sum GRBM_COUNT"; do
+        (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 240 rocprofv3 --pmc $g -d $R/$OUT/pmc3d/p$i -o run \
+          --output-format csv -- python3 $R/tools/probe_c5.py > $R/$OUT/pmc3d/p$i.json 2> $R/$OUT/pmc3d/p$i.log) \
+          || { echo "c5 pmc pass $i failed"; tail -5 $OUT/pmc3d/p$i.log; exit 1; }
+        i=$((i+1))
+      done
+      python3 tools/pmc_sum.py $OUT/pmc3d fast3d_search > $OUT/pmc3d/pmc_c5_summary.txt ;;
   esac
 done
 echo "== done $(date +%T)"

@@ -19,3 +19,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/tra
 for f in c1 c5; do python3 -c "
 import csv
 for r in csv.DictReader(open('$O/trace/${f}_kernel_stats.csv')): print(r['Name'][:60], r['Calls'], r['TotalDurationNs'], r['AverageNs'])"; done
+timeout -k 10 300 ./tools/dropin_threads 2000 > $O/dropin_cpp.json 2> $O/dropin_cpp.err || { tail -20 $O/dropin_cpp.err; exit 1; }
+cat $O/dropin_cpp.json
