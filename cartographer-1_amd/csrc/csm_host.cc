@@ -222,9 +222,25 @@ int LaunchSearch(csm_context* ctx, csm_scan_set* scans, const std::vector<PairDe
   const int np = static_cast<int>(pdesc.size());
   const int rc = plan.rc;
   // Per-XCD queues: submap s -> queue s % 8 so a submap's pyramid stays in
-  // one XCD's L2; pairs within a queue in submap order.
+  // one XCD's L2; pairs within a queue in submap order. A batch of fewer
+  // than 8 submaps (the C3 chunks hold 4) spreads each submap's pairs over
+  // 8 / S queues (CSM_QUEUE_SPREAD, A/B), so every XCD starts on a submap of
+  // its own instead of the empty queues' workgroups all stealing from the
+  // first one.
+  static const bool spread_on = [] {
+    const char* e = std::getenv("CSM_QUEUE_SPREAD");
+    return e && std::atoi(e) != 0;
+  }();
+  int nsub = 0;
+  for (int i = 0; i < np; ++i) nsub = std::max(nsub, pdesc[i].submap + 1);
+  const int reps = spread_on && nsub > 0 && nsub < kNumXcd ? kNumXcd / nsub : 1;
+  std::vector<int32_t> seen(reps > 1 ? nsub : 0, 0);
   std::vector<std::vector<int32_t>> q(kNumXcd);
-  for (int i = 0; i < np; ++i) q[pdesc[i].submap % kNumXcd].push_back(i);
+  for (int i = 0; i < np; ++i) {
+    const int sm = pdesc[i].submap;
+    const int qi = reps > 1 ? sm + nsub * (seen[sm]++ % reps) : sm % kNumXcd;
+    q[qi].push_back(i);
+  }
   std::vector<int32_t> order;
   std::vector<int64_t> prefix;
   WorkQueues wq{};
