@@ -161,8 +161,12 @@ octet_build(const uint8_t* __restrict__ level, Brick3 lb, int h, uint64_t* __res
 //   kHalf: out[c] = max over e, o in {0,1}^3 of prev[2c + e + h o]
 //     (level_gather with half = 1): 16 source rows (2y + {0, 1, h, h + 1}) x
 //     (2z + {0, 1, h, h + 1}), 4 x positions each.
+// One wave per output row: a row's loads and stores are a few instructions,
+// so the kernel is bound by how many rows are in flight (latency), and
+// single-wave workgroups keep 4x as many rows resident as 256-thread ones.
+constexpr int kRowThreads = 64;
 template <bool kOctet, bool kHalf>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(kRowThreads)
 brick_rows(const uint8_t* __restrict__ src, Brick3 sb, int h, void* __restrict__ out, Brick3 ob) {
   static_assert(!(kOctet && kHalf), "octets are built at the level's own resolution");
   constexpr int kRows = kHalf ? 16 : 4;
@@ -194,7 +198,7 @@ brick_rows(const uint8_t* __restrict__ src, Brick3 sb, int h, void* __restrict__
         const int b0 = (row_ok ? (zz * sb.ny + yy) * sb.nx : 0) + xs;  // byte of position 0
         const int a0 = b0 & ~3;
         const int nwords = (W + (b0 - a0) + 3) >> 2;
-        for (int i = threadIdx.x; i < nwords; i += 256) {
+        for (int i = threadIdx.x; i < nwords; i += kRowThreads) {
           const int a = a0 + 4 * i;
           const uint32_t w = row_ok ? __builtin_amdgcn_raw_buffer_load_b32(rs, a, 0, 0) : 0u;
 #pragma unroll
@@ -209,7 +213,7 @@ brick_rows(const uint8_t* __restrict__ src, Brick3 sb, int h, void* __restrict__
       }
       __syncthreads();
       const int base = (lz * ob.ny + ly) * ob.nx;
-      for (int lx = threadIdx.x; lx < ob.nx; lx += 256) {
+      for (int lx = threadIdx.x; lx < ob.nx; lx += kRowThreads) {
         if constexpr (kOctet) {
           uint64_t v = 0;
 #pragma unroll
@@ -2078,10 +2082,10 @@ hipError_t LaunchLevelGather(const uint8_t* prev, const Brick3& pb, uint8_t* out
   if (row_lds <= 65536) {
     const dim3 grid(std::min(ob.ny, 65535), std::min(ob.nz, 65535));
     if (half)
-      hipLaunchKernelGGL((brick_rows<false, true>), grid, dim3(256), row_lds, st, prev, pb, shift,
+      hipLaunchKernelGGL((brick_rows<false, true>), grid, dim3(kRowThreads), row_lds, st, prev, pb, shift,
                          static_cast<void*>(out), ob);
     else
-      hipLaunchKernelGGL((brick_rows<false, false>), grid, dim3(256), row_lds, st, prev, pb, shift,
+      hipLaunchKernelGGL((brick_rows<false, false>), grid, dim3(kRowThreads), row_lds, st, prev, pb, shift,
                          static_cast<void*>(out), ob);
     return hipGetLastError();
   }
@@ -2098,7 +2102,7 @@ hipError_t LaunchOctetBuild(const uint8_t* level, const Brick3& lb, int h, uint6
   const size_t row_lds = 4 * static_cast<size_t>((ob.nx + h + 3) & ~3);
   if (row_lds <= 65536) {
     hipLaunchKernelGGL((brick_rows<true, false>), dim3(std::min(ob.ny, 65535), std::min(ob.nz, 65535)),
-                       dim3(256), row_lds, st, level, lb, h, static_cast<void*>(out), ob);
+                       dim3(kRowThreads), row_lds, st, level, lb, h, static_cast<void*>(out), ob);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(octet_build,
