@@ -293,8 +293,8 @@ def roofline_fields(tm, achieved, peak, traffic, kernel_ms_avg, bytes_per_launch
             "candidate_equivalent_bytes_per_launch": candidate_bytes}
 
 
-TRAFFIC_FILES = {"c2": os.path.join("profiles", "r3bi", "traffic_c2.json"),
-                 "c3": os.path.join("profiles", "r3bi", "traffic_c3.json")}
+TRAFFIC_FILES = {"c2": os.path.join("profiles", "r4z", "traffic_c2.json"),
+                 "c3": os.path.join("profiles", "r4z", "traffic_c3.json")}
 
 
 def traffic_fields(traffic, kernel_ms_avg, peak):

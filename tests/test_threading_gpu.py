@@ -176,3 +176,19 @@ def test_threads_3d_single_calls(csm):
             assert np.float32(g.score) == np.float32(r.score)
             assert g.pose_estimate == r.pose.as_tuple()
     assert matched >= 2
+
+
+def test_cpp_threads_match_single_thread_results():
+    """The threading contract from C++ threads (no GIL): 16 threads call
+    csm_fast2d_match_full_submap on shared matchers at once; every result
+    equals the single-threaded one (tools/dropin_threads.cc --check)."""
+    import json
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools",
+                       "dropin_threads")
+    assert os.path.exists(exe), "build() makes tools/dropin_threads"
+    out = subprocess.run([exe, "0", "0.55", "--check"], capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, (out.stdout, out.stderr)
+    r = json.loads(out.stdout.strip().splitlines()[-1])
+    assert r["mismatches"] == 0 and r["matched"] > 0, r

@@ -6,12 +6,17 @@
 // once. Prints one JSON line: pairs/s per thread count, without the Python
 // GIL that bounds bench.py's threaded leg.
 //   built by cartographer-1_amd/csrc/Makefile (tools target)
-//   usage: dropin_threads [calls] [min_score]
+//   usage: dropin_threads [calls] [min_score] [--check]
+// --check: the threading contract test (tests/test_threading_gpu.py): 200
+// pairs matched on one thread, then the same pairs from 16 threads at once
+// (each pair twice); every concurrent result must equal the single-threaded
+// one bit for bit. Exit status 1 on any difference.
 #include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -63,6 +68,45 @@ int main(int argc, char** argv) {
     const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     return std::make_pair(n / s, errors.load());
   };
+  if (argc > 3 && std::string(argv[3]) == "--check") {
+    struct R {
+      int rc;
+      float score;
+      csm_pose2d pose;
+    };
+    const int n = 200;
+    auto one = [&](int j) {
+      const int node = (7 * j) % nodes;
+      R r{0, 0.f, {0., 0., 0.}};
+      r.rc = csm_fast2d_match_full_submap(m[j % submaps], pts + 3 * off[node],
+                                          static_cast<int32_t>(off[node + 1] - off[node]), min_score,
+                                          &r.score, &r.pose);
+      return r;
+    };
+    std::vector<R> ref(n);
+    for (int j = 0; j < n; ++j) ref[j] = one(j);
+    std::atomic<int> next{0}, bad{0}, matched{0};
+    std::vector<std::thread> pool;
+    for (int t = 0; t < 16; ++t)
+      pool.emplace_back([&] {
+        for (int k; (k = next.fetch_add(1)) < 2 * n;) {
+          const int j = k % n;
+          const R r = one(j);
+          if (r.rc == CSM_OK) matched.fetch_add(1);
+          if (r.rc != ref[j].rc || (r.rc == CSM_OK && (r.score != ref[j].score || r.pose.x != ref[j].pose.x ||
+                                                      r.pose.y != ref[j].pose.y ||
+                                                      r.pose.theta != ref[j].pose.theta)))
+            bad.fetch_add(1);
+        }
+      });
+    for (auto& th : pool) th.join();
+    std::printf("{\"check_pairs\": %d, \"concurrent_calls\": %d, \"matched\": %d, \"mismatches\": %d}\n", n,
+                2 * n, matched.load(), bad.load());
+    for (csm_fast2d* x : m) csm_fast2d_destroy(x);
+    csm_context_destroy(ctx);
+    csm_synth2d_destroy(w);
+    return bad.load() == 0 && matched.load() > 0 ? 0 : 1;
+  }
   std::printf("{\"calls\": %d, \"pairs_per_s\": {", calls);
   bool first = true;
   for (int threads : {1, 2, 4, 8, 16}) {
