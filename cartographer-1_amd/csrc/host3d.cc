@@ -10,6 +10,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <smmintrin.h>
+
 #include <algorithm>
 #include <array>
 #include <limits>
@@ -183,6 +185,58 @@ int EnsureValueTables(csm_context* ctx) {
 }  // namespace
 
 // ----------------------------------------------------------- HybridGrid --
+// Copies a HybridGrid cell list (count x (x, y, z)) into the pinned staging
+// and returns its bounds in one pass: 4 cells (12 ints) per step in three
+// 4-lane vectors whose lanes hold the components (x y z x), (y z x y),
+// (z x y z), folded per component after the loop. count > 0.
+static __attribute__((target("sse4.1"))) void StageCells(const int32_t* ijk, int64_t count, int32_t* hs,
+                                                          int lo[3], int hi[3]) {
+  int lx = ijk[0], ly = ijk[1], lz = ijk[2], ux = lx, uy = ly, uz = lz;
+  int64_t i = 0;
+  {
+    const __m128i* src = reinterpret_cast<const __m128i*>(ijk);
+    __m128i* dst = reinterpret_cast<__m128i*>(hs);
+    __m128i lo0 = _mm_set1_epi32(INT32_MAX), lo1 = lo0, lo2 = lo0;
+    __m128i hi0 = _mm_set1_epi32(INT32_MIN), hi1 = hi0, hi2 = hi0;
+    for (; i + 4 <= count; i += 4, src += 3, dst += 3) {
+      const __m128i a = _mm_loadu_si128(src), b = _mm_loadu_si128(src + 1),
+                    c = _mm_loadu_si128(src + 2);
+      _mm_storeu_si128(dst, a);
+      _mm_storeu_si128(dst + 1, b);
+      _mm_storeu_si128(dst + 2, c);
+      lo0 = _mm_min_epi32(lo0, a); hi0 = _mm_max_epi32(hi0, a);
+      lo1 = _mm_min_epi32(lo1, b); hi1 = _mm_max_epi32(hi1, b);
+      lo2 = _mm_min_epi32(lo2, c); hi2 = _mm_max_epi32(hi2, c);
+    }
+    alignas(16) int32_t l[12], h[12];
+    _mm_store_si128(reinterpret_cast<__m128i*>(l), lo0);
+    _mm_store_si128(reinterpret_cast<__m128i*>(l + 4), lo1);
+    _mm_store_si128(reinterpret_cast<__m128i*>(l + 8), lo2);
+    _mm_store_si128(reinterpret_cast<__m128i*>(h), hi0);
+    _mm_store_si128(reinterpret_cast<__m128i*>(h + 4), hi1);
+    _mm_store_si128(reinterpret_cast<__m128i*>(h + 8), hi2);
+    for (int k = 0; k < 12; ++k) {  // lane k holds component k % 3
+      int* lo_c = k % 3 == 0 ? &lx : (k % 3 == 1 ? &ly : &lz);
+      int* hi_c = k % 3 == 0 ? &ux : (k % 3 == 1 ? &uy : &uz);
+      if (i > 0) {
+        *lo_c = std::min(*lo_c, l[k]);
+        *hi_c = std::max(*hi_c, h[k]);
+      }
+    }
+  }
+  for (; i < count; ++i) {
+    const int x = ijk[3 * i], y = ijk[3 * i + 1], z = ijk[3 * i + 2];
+    hs[3 * i] = x;
+    hs[3 * i + 1] = y;
+    hs[3 * i + 2] = z;
+    lx = std::min(lx, x); ux = std::max(ux, x);
+    ly = std::min(ly, y); uy = std::max(uy, y);
+    lz = std::min(lz, z); uz = std::max(uz, z);
+  }
+  lo[0] = lx; lo[1] = ly; lo[2] = lz;
+  hi[0] = ux; hi[1] = uy; hi[2] = uz;
+}
+
 int csm_hybrid_grid_create(csm_context* ctx, float resolution, const int32_t* ijk,
                            const uint16_t* values, int64_t count, int32_t grid_size,
                            csm_hybrid_grid** out) {
@@ -207,19 +261,8 @@ int csm_hybrid_grid_create(csm_context* ctx, float resolution, const int32_t* ij
     else CSM_HIP(hipEventCreateWithFlags(&ctx->f3_stage_copied, hipEventDisableTiming));
     if ((rc = ctx->f3_grid_stage.Reserve(list_bytes))) return rc;
     int32_t* hs = ctx->f3_grid_stage.as<int32_t>();
-    int lx = ijk[0], ly = ijk[1], lz = ijk[2], ux = lx, uy = ly, uz = lz;
-    for (int64_t i = 0; i < count; ++i) {
-      const int x = ijk[3 * i], y = ijk[3 * i + 1], z = ijk[3 * i + 2];
-      hs[3 * i] = x;
-      hs[3 * i + 1] = y;
-      hs[3 * i + 2] = z;
-      lx = std::min(lx, x); ux = std::max(ux, x);
-      ly = std::min(ly, y); uy = std::max(uy, y);
-      lz = std::min(lz, z); uz = std::max(uz, z);
-    }
+    StageCells(ijk, count, hs, lo, hi);
     std::memcpy(hs + 3 * count, values, sizeof(uint16_t) * count);
-    lo[0] = lx; lo[1] = ly; lo[2] = lz;
-    hi[0] = ux; hi[1] = uy; hi[2] = uz;
   }
   if (grid_size <= 0) {  // DynamicGrid growth (hybrid_grid.h:283-296, :384-399)
     int gs = 128;
