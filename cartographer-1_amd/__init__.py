@@ -290,6 +290,10 @@ _SIGNATURES = {
                                  C.POINTER(Pose3D)]),
     "csm_fast3d_create": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(C.c_float),
                                     C.c_int32, C.POINTER(Fast3DOptions), C.POINTER(C.c_void_p)]),
+    "csm_fast3d_create_batch": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_void_p),
+                                          C.POINTER(C.c_void_p), C.POINTER(C.POINTER(C.c_float)),
+                                          C.POINTER(C.c_int32), C.POINTER(Fast3DOptions),
+                                          C.POINTER(C.c_void_p)]),
     "csm_fast3d_destroy": (None, [C.c_void_p]),
     "csm_fast3d_read_level": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_uint8), C.c_int64,
                                         C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),

@@ -42,6 +42,23 @@ struct Brick3 {
   int64_t offset;  // byte offset of this brick in its allocation
 };
 
+// One output brick of a batched pyramid build (csm_fast3d_create_batch):
+// source brick -> output brick, as level_gather (shift h, half) or
+// octet_build (h) do it. `lds`: the job's staged-rows bytes.
+struct RowJob3 {
+  const uint8_t* src;
+  void* out;
+  Brick3 sb, ob;
+  int32_t h, lds;
+};
+
+// One level-0 conversion of a batched build (brick_from_values' qtab path).
+struct ValueJob3 {
+  const uint16_t* values;
+  uint8_t* level0;
+  int64_t n;
+};
+
 // One FastCSM3D submap (csm_fast3d): pyramid levels (uint8 bricks in one
 // allocation) and the low-resolution HybridGrid (float probability brick).
 struct Submap3Desc {

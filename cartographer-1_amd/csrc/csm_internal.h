@@ -201,6 +201,10 @@ struct csm_context {
   hipStream_t f3_copy_stream = nullptr;
   hipEvent_t f3_points_ready = nullptr;
   hipEvent_t f3_stage_copied = nullptr;  // f3_grid_stage's last upload done
+  // Batched pyramid builds (csm_fast3d_create_batch): job lists, staged.
+  csm::PinnedBuf f3_job_stage;
+  csm::DevBuf f3_jobs;
+  hipEvent_t f3_jobs_copied = nullptr;
   // Voxel filter scratch (voxel_filter.hip).
   csm::DevBuf vf_points, vf_offsets, vf_keep, vf_counts;
   // CeresScanMatcher2D refinement scratch (ceres2d.hip).

@@ -19,6 +19,12 @@ hipError_t LaunchLevelGather(const uint8_t* prev, const Brick3& pb, uint8_t* out
                              int shift, int half, hipStream_t st);
 hipError_t LaunchOctetBuild(const uint8_t* level, const Brick3& lb, int h, uint64_t* out,
                             const Brick3& ob, hipStream_t st);
+// Batched builds (csm_fast3d_create_batch): one launch per level for all
+// jobs (device arrays); max_rows / max_lds over the jobs (lds <= 64 KiB).
+hipError_t LaunchBrickRowsBatch(const RowJob3* jobs, int num_jobs, int max_rows, int max_lds,
+                                bool octet, bool half, hipStream_t st);
+hipError_t LaunchValuesToLevel0Batch(const ValueJob3* jobs, int num_jobs, int64_t max_n,
+                                     const uint8_t* qtab, hipStream_t st);
 hipError_t LaunchRt3dScore(int num_rot, hipStream_t st, const float* prob, const Brick3& gb,
                            float res, const float* points, int n, const float4* rot,
                            const float* rot_angle, const float4* trans, int num_trans, int t_base,

@@ -261,7 +261,35 @@ int csm_hybrid_grid_create(csm_context* ctx, float resolution, const int32_t* ij
     else CSM_HIP(hipEventCreateWithFlags(&ctx->f3_stage_copied, hipEventDisableTiming));
     if ((rc = ctx->f3_grid_stage.Reserve(list_bytes))) return rc;
     int32_t* hs = ctx->f3_grid_stage.as<int32_t>();
-    StageCells(ijk, count, hs, lo, hi);
+    // Large lists (a submap's high-resolution grid holds ~200k cells, 2.4 MB)
+    // are staged by several threads: the copy is bound by one core's memory
+    // bandwidth otherwise.
+    const int parts = count >= (int64_t{1} << 16)
+                          ? static_cast<int>(std::min<int64_t>(8, count >> 15))
+                          : 1;
+    if (parts == 1) {
+      StageCells(ijk, count, hs, lo, hi);
+    } else {
+      std::vector<std::array<int, 6>> part_bounds(parts);
+      std::vector<std::thread> pool;
+      const int64_t chunk = (count + parts - 1) / parts;
+      for (int t = 0; t < parts; ++t)
+        pool.emplace_back([&, t] {
+          const int64_t b = t * chunk, e = std::min(count, b + chunk);
+          int l3[3], h3[3];
+          StageCells(ijk + 3 * b, e - b, hs + 3 * b, l3, h3);
+          part_bounds[t] = {l3[0], l3[1], l3[2], h3[0], h3[1], h3[2]};
+        });
+      for (auto& th : pool) th.join();
+      for (int a = 0; a < 3; ++a) {
+        lo[a] = part_bounds[0][a];
+        hi[a] = part_bounds[0][3 + a];
+        for (int t = 1; t < parts; ++t) {
+          lo[a] = std::min(lo[a], part_bounds[t][a]);
+          hi[a] = std::max(hi[a], part_bounds[t][3 + a]);
+        }
+      }
+    }
     std::memcpy(hs + 3 * count, values, sizeof(uint16_t) * count);
   }
   if (grid_size <= 0) {  // DynamicGrid growth (hybrid_grid.h:283-296, :384-399)
@@ -708,19 +736,25 @@ struct csm_fast3d {
   hipEvent_t ready = nullptr;  // after the build's kernels on ctx->stream (WaitBuilt)
 };
 
-int csm_fast3d_create(csm_context* ctx, const csm_hybrid_grid* high, const csm_hybrid_grid* low,
-                      const float* histogram, int32_t histogram_size,
-                      const csm_fast3d_options* options, csm_fast3d** out) {
-  if (!ctx || !high || !low || !options || !out || histogram_size < 0 ||
-      (histogram_size > 0 && !histogram))
-    return CSM_EINVAL;
+namespace {
+
+// A matcher's level boxes and buffers (PrecomputationGridStack3D,
+// fast_correlative_scan_matcher_3d.cc:57-77); the build kernels are queued by
+// BuildFast3d. Caller holds ctx->mu.
+struct Fast3dPlan {
+  int depth = 0;
+  bool empty = true;
+  int shifts[kMaxLevels3d] = {0};
+  int halves[kMaxLevels3d] = {0};
+  const csm_hybrid_grid* high = nullptr;
+};
+
+int PlanFast3d(csm_context* ctx, const csm_hybrid_grid* high, const csm_hybrid_grid* low,
+               const float* histogram, int32_t histogram_size, const csm_fast3d_options* options,
+               std::unique_ptr<csm_fast3d>* out, Fast3dPlan* plan) {
+  if (!high || !low || histogram_size < 0 || (histogram_size > 0 && !histogram)) return CSM_EINVAL;
   if (high->ctx != ctx || low->ctx != ctx) return CSM_EINVAL;
-  // fast_correlative_scan_matcher_3d.cc:60-61
-  if (options->branch_and_bound_depth < 1 || options->full_resolution_depth < 1) return CSM_EINVAL;
-  if (options->branch_and_bound_depth > kMaxLevels3d) return CSM_ERANGE;
-  std::lock_guard<std::mutex> lock(ctx->mu);
   int rc;
-  if ((rc = EnsureDevice3(ctx))) return rc;
   auto m = std::make_unique<csm_fast3d>();
   m->ctx = ctx;
   m->options = *options;
@@ -728,17 +762,19 @@ int csm_fast3d_create(csm_context* ctx, const csm_hybrid_grid* high, const csm_h
   m->width_in_voxels = high->grid_size;
   m->low = low;
   m->histogram.assign(histogram, histogram + histogram_size);
-  // Level boxes (PrecomputationGridStack3D, .cc:57-77): level d covers the
-  // cells its scatter-max can reach from level d-1.
+  // Level boxes: level d covers the cells its scatter-max can reach from
+  // level d-1.
   const int depth = std::min(options->branch_and_bound_depth + kExtraLevels3d, kMaxLevels3d);
+  plan->depth = depth;
+  plan->high = high;
   Submap3Desc& d = m->desc;
   d.num_levels = options->branch_and_bound_depth;
   d.search_levels = depth;
   d.full_resolution_depth = options->full_resolution_depth;
   d.resolution = high->resolution;
   int64_t total = 0;
-  std::vector<int> shifts(depth, 0), halves(depth, 0);
   const bool empty = high->brick.nx == 0;
+  plan->empty = empty;
   d.level[0] = high->brick;
   int last_width = 1;
   for (int l = 0; l < depth; ++l) {
@@ -747,8 +783,8 @@ int csm_fast3d_create(csm_context* ctx, const csm_hybrid_grid* high, const csm_h
       const int next_width = 1 << l;
       const int f = 1 << std::max(0, l - options->full_resolution_depth);
       const int s = (next_width - last_width + (f - 1)) / f;
-      shifts[l] = s;
-      halves[l] = half ? 1 : 0;
+      plan->shifts[l] = s;
+      plan->halves[l] = half ? 1 : 0;
       const Brick3& p = d.level[l - 1];
       Brick3 b{};
       if (!empty) {
@@ -804,24 +840,132 @@ int csm_fast3d_create(csm_context* ctx, const csm_hybrid_grid* high, const csm_h
   d.low_prob = low->prob.as<float>();
   d.low = low->brick;
   d.low_resolution = low->resolution;
-  hipStream_t st = ctx->stream;
-  if (!empty) {
-    if ((rc = EnsureValueTables(ctx))) return rc;
+  *out = std::move(m);
+  return CSM_OK;
+}
+
+// Queues the pyramid builds of `count` planned matchers on ctx->stream: the
+// level-0 conversion, then level by level the gathers, then the octets, each
+// one launch for every matcher of the batch (blockIdx.y = matcher), and
+// records each matcher's ready event. The job lists go up through pinned
+// staging, rewritten only after the previous batch's copy has finished.
+int BuildFast3d(csm_context* ctx, csm_fast3d* const* ms, const Fast3dPlan* plans, int count) {
+  int rc;
+  if ((rc = EnsureValueTables(ctx))) return rc;
+  std::vector<ValueJob3> vjobs;
+  int depth = 0;
+  for (int i = 0; i < count; ++i) depth = std::max(depth, plans[i].depth);
+  std::vector<std::vector<RowJob3>> level_jobs(depth), oct_jobs(depth);
+  auto row_lds = [](const Brick3& ob, int h, bool half) {
+    return (half ? 16 : 4) * ((half ? 2 * ob.nx + h : ob.nx + h) + 3 & ~3);
+  };
+  for (int i = 0; i < count; ++i) {
+    const Fast3dPlan& pl = plans[i];
+    if (pl.empty) continue;
+    const Submap3Desc& d = ms[i]->desc;
+    uint8_t* lv = ms[i]->levels.as<uint8_t>();
     const int64_t n0 = static_cast<int64_t>(d.level[0].nx) * d.level[0].ny * d.level[0].nz;
-    CSM_HIP(LaunchBrickFromValues(high->values.as<uint16_t>(), n0, nullptr, ctx->f3_qtab.as<uint8_t>(),
-                                  nullptr, m->levels.as<uint8_t>() + d.level[0].offset, st));
-    for (int l = 1; l < depth; ++l)
-      CSM_HIP(LaunchLevelGather(m->levels.as<uint8_t>() + d.level[l - 1].offset, d.level[l - 1],
-                                m->levels.as<uint8_t>() + d.level[l].offset, d.level[l], shifts[l],
-                                halves[l], st));
-    for (int l = 0; l + 1 < depth; ++l)
-      CSM_HIP(LaunchOctetBuild(m->levels.as<uint8_t>() + d.level[l].offset, d.level[l], d.oct_h[l],
-                               reinterpret_cast<uint64_t*>(m->octs.as<uint8_t>() + d.oct[l].offset),
-                               d.oct[l], st));
-    CSM_HIP(hipEventCreateWithFlags(&m->ready, hipEventDisableTiming));
-    CSM_HIP(hipEventRecord(m->ready, st));
+    vjobs.push_back(ValueJob3{pl.high->values.as<uint16_t>(), lv + d.level[0].offset, n0});
+    for (int l = 1; l < pl.depth; ++l)
+      level_jobs[l].push_back(RowJob3{lv + d.level[l - 1].offset, lv + d.level[l].offset,
+                                      d.level[l - 1], d.level[l], pl.shifts[l],
+                                      row_lds(d.level[l], pl.shifts[l], pl.halves[l] != 0)});
+    for (int l = 0; l + 1 < pl.depth; ++l)
+      oct_jobs[l].push_back(RowJob3{lv + d.level[l].offset, ms[i]->octs.as<uint8_t>() + d.oct[l].offset,
+                                    d.level[l], d.oct[l], d.oct_h[l], row_lds(d.oct[l], d.oct_h[l], false)});
   }
-  *out = m.release();
+  // One job array: values jobs, then each level's, then each octet level's.
+  size_t nrow = 0;
+  for (int l = 0; l < depth; ++l) nrow += level_jobs[l].size() + oct_jobs[l].size();
+  const size_t vbytes = (sizeof(ValueJob3) * vjobs.size() + 255) & ~size_t{255};
+  const size_t bytes = vbytes + sizeof(RowJob3) * nrow;
+  hipStream_t st = ctx->stream;
+  if (bytes > 0) {
+    if (ctx->f3_jobs_copied) CSM_HIP(hipEventSynchronize(ctx->f3_jobs_copied));
+    else CSM_HIP(hipEventCreateWithFlags(&ctx->f3_jobs_copied, hipEventDisableTiming));
+    if ((rc = ctx->f3_job_stage.Reserve(bytes))) return rc;
+    if ((rc = ctx->f3_jobs.Reserve(bytes))) return rc;
+    char* h = ctx->f3_job_stage.as<char>();
+    std::memcpy(h, vjobs.data(), sizeof(ValueJob3) * vjobs.size());
+    RowJob3* rj = reinterpret_cast<RowJob3*>(h + vbytes);
+    for (int l = 0; l < depth; ++l) {
+      for (const RowJob3& j : level_jobs[l]) *rj++ = j;
+      for (const RowJob3& j : oct_jobs[l]) *rj++ = j;
+    }
+    CSM_HIP(hipMemcpyAsync(ctx->f3_jobs.ptr, h, bytes, hipMemcpyHostToDevice, st));
+    CSM_HIP(hipEventRecord(ctx->f3_jobs_copied, st));
+    const char* dev = ctx->f3_jobs.as<char>();
+    int64_t max_n = 0;
+    for (const ValueJob3& v : vjobs) max_n = std::max(max_n, v.n);
+    CSM_HIP(LaunchValuesToLevel0Batch(reinterpret_cast<const ValueJob3*>(dev), static_cast<int>(vjobs.size()),
+                                      max_n, ctx->f3_qtab.as<uint8_t>(), st));
+    const RowJob3* drow = reinterpret_cast<const RowJob3*>(dev + vbytes);
+    auto launch = [&](const std::vector<RowJob3>& jobs, bool octet, bool half) -> int {
+      if (jobs.empty()) return CSM_OK;
+      int max_rows = 0, max_lds = 0;
+      for (const RowJob3& j : jobs) {
+        max_rows = std::max(max_rows, j.ob.ny * j.ob.nz);
+        max_lds = std::max(max_lds, j.lds);
+      }
+      if (max_lds > 65536) {  // rows past 16k cells: the per-cell kernels, one job at a time
+        for (const RowJob3& j : jobs)
+          CSM_HIP(octet ? LaunchOctetBuild(j.src, j.sb, j.h, static_cast<uint64_t*>(j.out), j.ob, st)
+                        : LaunchLevelGather(j.src, j.sb, static_cast<uint8_t*>(j.out), j.ob, j.h,
+                                            half ? 1 : 0, st));
+      } else {
+        CSM_HIP(LaunchBrickRowsBatch(drow, static_cast<int>(jobs.size()), max_rows, max_lds, octet,
+                                     half, st));
+      }
+      drow += jobs.size();
+      return CSM_OK;
+    };
+    const int frd = ms[0]->options.full_resolution_depth;
+    for (int l = 0; l < depth; ++l) {
+      if ((rc = launch(level_jobs[l], false, l >= frd && l > 0))) return rc;
+      if ((rc = launch(oct_jobs[l], true, false))) return rc;
+    }
+  }
+  for (int i = 0; i < count; ++i) {
+    if (plans[i].empty) continue;
+    CSM_HIP(hipEventCreateWithFlags(&ms[i]->ready, hipEventDisableTiming));
+    CSM_HIP(hipEventRecord(ms[i]->ready, st));
+  }
+  return CSM_OK;
+}
+
+}  // namespace
+
+int csm_fast3d_create(csm_context* ctx, const csm_hybrid_grid* high, const csm_hybrid_grid* low,
+                      const float* histogram, int32_t histogram_size,
+                      const csm_fast3d_options* options, csm_fast3d** out) {
+  return csm_fast3d_create_batch(ctx, 1, &high, &low, &histogram, &histogram_size, options, out);
+}
+
+int csm_fast3d_create_batch(csm_context* ctx, int32_t count, const csm_hybrid_grid* const* high,
+                            const csm_hybrid_grid* const* low, const float* const* histograms,
+                            const int32_t* histogram_sizes, const csm_fast3d_options* options,
+                            csm_fast3d** out) {
+  if (!ctx || !options || count < 0 || (count > 0 && (!high || !low || !histograms ||
+                                                      !histogram_sizes || !out)))
+    return CSM_EINVAL;
+  // fast_correlative_scan_matcher_3d.cc:60-61
+  if (options->branch_and_bound_depth < 1 || options->full_resolution_depth < 1) return CSM_EINVAL;
+  if (options->branch_and_bound_depth > kMaxLevels3d) return CSM_ERANGE;
+  if (count > 65535) return CSM_ERANGE;  // one launch's grid.y
+  if (count == 0) return CSM_OK;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  int rc;
+  if ((rc = EnsureDevice3(ctx))) return rc;
+  std::vector<std::unique_ptr<csm_fast3d>> made(count);
+  std::vector<Fast3dPlan> plans(count);
+  for (int i = 0; i < count; ++i)
+    if ((rc = PlanFast3d(ctx, high[i], low[i], histograms[i], histogram_sizes[i], options, &made[i],
+                         &plans[i])))
+      return rc;  // made[] frees what was planned
+  std::vector<csm_fast3d*> ms(count);
+  for (int i = 0; i < count; ++i) ms[i] = made[i].get();
+  if ((rc = BuildFast3d(ctx, ms.data(), plans.data(), count))) return rc;
+  for (int i = 0; i < count; ++i) out[i] = made[i].release();
   return CSM_OK;
 }
 

@@ -166,11 +166,11 @@ octet_build(const uint8_t* __restrict__ level, Brick3 lb, int h, uint64_t* __res
 // single-wave workgroups keep 4x as many rows resident as 256-thread ones.
 constexpr int kRowThreads = 64;
 template <bool kOctet, bool kHalf>
-__global__ void __launch_bounds__(kRowThreads)
-brick_rows(const uint8_t* __restrict__ src, Brick3 sb, int h, void* __restrict__ out, Brick3 ob) {
+__device__ __forceinline__ void BrickRows(const uint8_t* __restrict__ src, Brick3 sb, int h,
+                                          void* __restrict__ out, Brick3 ob, int block, int blocks,
+                                          uint8_t* rows) {
   static_assert(!(kOctet && kHalf), "octets are built at the level's own resolution");
   constexpr int kRows = kHalf ? 16 : 4;
-  extern __shared__ uint8_t rows[];  // kRows rows x pitch
   const int W = kHalf ? 2 * ob.nx + h : ob.nx + h, pitch = (W + 3) & ~3;
   const int src_bytes = sb.nx * sb.ny * sb.nz;
   // Up to 3 bytes past the brick are read (levels are 256-byte aligned in
@@ -178,8 +178,10 @@ brick_rows(const uint8_t* __restrict__ src, Brick3 sb, int h, void* __restrict__
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<uint8_t*>(src), 0, (src_bytes + 3) & ~3, 0x00020000);
   const int xs = (kHalf ? 2 * ob.ox : ob.ox) - sb.ox;  // source x (brick-relative) of position 0
-  for (int lz = blockIdx.y; lz < ob.nz; lz += gridDim.y) {
-    for (int ly = blockIdx.x; ly < ob.ny; ly += gridDim.x) {
+  const int nrows = ob.ny * ob.nz;
+  for (int row = block; row < nrows; row += blocks) {
+    {
+      const int ly = row % ob.ny, lz = row / ob.ny;
       const int y = ly + ob.oy, z = lz + ob.oz;
       __syncthreads();  // the previous row's reads are done
       for (int r = 0; r < kRows; ++r) {
@@ -240,6 +242,34 @@ brick_rows(const uint8_t* __restrict__ src, Brick3 sb, int h, void* __restrict__
       }
     }
   }
+}
+
+template <bool kOctet, bool kHalf>
+__global__ void __launch_bounds__(kRowThreads)
+brick_rows(const uint8_t* __restrict__ src, Brick3 sb, int h, void* __restrict__ out, Brick3 ob) {
+  extern __shared__ uint8_t rows[];  // kRows rows x pitch
+  BrickRows<kOctet, kHalf>(src, sb, h, out, ob, blockIdx.x, gridDim.x, rows);
+}
+
+// Batched form (csm_fast3d_create_batch): blockIdx.y picks the job, so one
+// launch builds a level (or its octets) for every submap of the batch.
+template <bool kOctet, bool kHalf>
+__global__ void __launch_bounds__(kRowThreads)
+brick_rows_batch(const RowJob3* __restrict__ jobs) {
+  extern __shared__ uint8_t rows[];
+  const RowJob3 jb = jobs[blockIdx.y];
+  if (jb.ob.nx <= 0 || jb.ob.ny <= 0 || jb.ob.nz <= 0) return;
+  BrickRows<kOctet, kHalf>(jb.src, jb.sb, jb.h, jb.out, jb.ob, blockIdx.x, gridDim.x, rows);
+}
+
+// Batched level-0 conversion (ConvertToPrecomputationGrid, the qtab path of
+// brick_from_values): blockIdx.y picks the submap.
+__global__ void __launch_bounds__(256)
+values_to_level0_batch(const ValueJob3* __restrict__ jobs, const uint8_t* __restrict__ qtab) {
+  const ValueJob3 jb = jobs[blockIdx.y];
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < jb.n;
+       i += static_cast<int64_t>(gridDim.x) * 256)
+    jb.level0[i] = qtab[jb.values[i] & 0x7fff];
 }
 
 // ------------------------------------------------------------- RTCSM3D ----
@@ -2080,7 +2110,7 @@ hipError_t LaunchLevelGather(const uint8_t* prev, const Brick3& pb, uint8_t* out
   const size_t row_lds = half ? 16 * static_cast<size_t>((2 * ob.nx + shift + 3) & ~3)
                               : 4 * static_cast<size_t>((ob.nx + shift + 3) & ~3);
   if (row_lds <= 65536) {
-    const dim3 grid(std::min(ob.ny, 65535), std::min(ob.nz, 65535));
+    const dim3 grid(static_cast<unsigned>(std::min<int64_t>(static_cast<int64_t>(ob.ny) * ob.nz, 1 << 20)));
     if (half)
       hipLaunchKernelGGL((brick_rows<false, true>), grid, dim3(kRowThreads), row_lds, st, prev, pb, shift,
                          static_cast<void*>(out), ob);
@@ -2101,7 +2131,8 @@ hipError_t LaunchOctetBuild(const uint8_t* level, const Brick3& lb, int h, uint6
   if (ob.nx <= 0 || ob.ny <= 0 || ob.nz <= 0) return hipSuccess;
   const size_t row_lds = 4 * static_cast<size_t>((ob.nx + h + 3) & ~3);
   if (row_lds <= 65536) {
-    hipLaunchKernelGGL((brick_rows<true, false>), dim3(std::min(ob.ny, 65535), std::min(ob.nz, 65535)),
+    hipLaunchKernelGGL((brick_rows<true, false>),
+                       dim3(static_cast<unsigned>(std::min<int64_t>(static_cast<int64_t>(ob.ny) * ob.nz, 1 << 20))),
                        dim3(kRowThreads), row_lds, st, level, lb, h, static_cast<void*>(out), ob);
     return hipGetLastError();
   }
@@ -2109,6 +2140,30 @@ hipError_t LaunchOctetBuild(const uint8_t* level, const Brick3& lb, int h, uint6
                      dim3(static_cast<unsigned>((ob.nx + 255) / 256), std::min(ob.ny, 65535),
                           std::min(ob.nz, 65535)),
                      dim3(256), 0, st, level, lb, h, out, ob);
+  return hipGetLastError();
+}
+
+hipError_t LaunchBrickRowsBatch(const RowJob3* jobs, int num_jobs, int max_rows, int max_lds,
+                                bool octet, bool half, hipStream_t st) {
+  if (num_jobs <= 0 || max_rows <= 0) return hipSuccess;
+  if (num_jobs > 65535 || max_lds > 65536 || (octet && half)) return hipErrorInvalidValue;
+  const dim3 grid(static_cast<unsigned>(std::min(max_rows, 1 << 16)), static_cast<unsigned>(num_jobs));
+  if (octet)
+    hipLaunchKernelGGL((brick_rows_batch<true, false>), grid, dim3(kRowThreads), max_lds, st, jobs);
+  else if (half)
+    hipLaunchKernelGGL((brick_rows_batch<false, true>), grid, dim3(kRowThreads), max_lds, st, jobs);
+  else
+    hipLaunchKernelGGL((brick_rows_batch<false, false>), grid, dim3(kRowThreads), max_lds, st, jobs);
+  return hipGetLastError();
+}
+
+hipError_t LaunchValuesToLevel0Batch(const ValueJob3* jobs, int num_jobs, int64_t max_n,
+                                     const uint8_t* qtab, hipStream_t st) {
+  if (num_jobs <= 0 || max_n <= 0) return hipSuccess;
+  if (num_jobs > 65535) return hipErrorInvalidValue;
+  const dim3 grid(static_cast<unsigned>(std::min<int64_t>((max_n + 255) / 256, 1 << 14)),
+                  static_cast<unsigned>(num_jobs));
+  hipLaunchKernelGGL(values_to_level0_batch, grid, dim3(256), 0, st, jobs, qtab);
   return hipGetLastError();
 }
 

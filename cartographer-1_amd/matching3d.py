@@ -242,6 +242,35 @@ class FastCorrelativeScanMatcher3D:
                "csm_fast3d_create")
         self.handle = h
 
+    @classmethod
+    def create_batch(cls, grids, histograms, options: FastCorrelativeScanMatcherOptions3D,
+                     context: Optional[Context] = None):
+        """Many matchers in one call (csm_fast3d_create_batch): ``grids`` is a
+        list of (high_resolution, low_resolution) HybridGrid pairs; returns
+        the matchers in the same order, each what the constructor returns."""
+        context = context or default_context()
+        lib = context._lib
+        n = len(grids)
+        if n != len(histograms):
+            raise ValueError("one histogram per grid pair")
+        hists = [np.ascontiguousarray(np.asarray(h, np.float32)) for h in histograms]
+        highs = (C.c_void_p * max(n, 1))(*[g[0].handle for g in grids])
+        lows = (C.c_void_p * max(n, 1))(*[g[1].handle for g in grids])
+        hptr = (C.POINTER(C.c_float) * max(n, 1))(*[_ptr(h, C.c_float) for h in hists])
+        hsize = (C.c_int32 * max(n, 1))(*[len(h) for h in hists])
+        out = (C.c_void_p * max(n, 1))()
+        opts = options.to_c()
+        _check(lib.csm_fast3d_create_batch(context.handle, n, highs, lows, hptr, hsize,
+                                           C.byref(opts), out), "csm_fast3d_create_batch")
+        made = []
+        for i in range(n):
+            m = cls.__new__(cls)
+            m.context, m._lib, m.options = context, lib, options
+            m.low_resolution_grid = grids[i][1]  # must outlive the matcher
+            m.handle = C.c_void_p(out[i])
+            made.append(m)
+        return made
+
     def close(self):
         if getattr(self, "handle", None):
             self._lib.csm_fast3d_destroy(self.handle)

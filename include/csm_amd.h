@@ -414,6 +414,18 @@ int csm_fast3d_create(csm_context* ctx, const csm_hybrid_grid* high_resolution,
                       const csm_hybrid_grid* low_resolution, const float* histogram,
                       int32_t histogram_size, const csm_fast3d_options* options,
                       csm_fast3d** out);
+/* `count` FastCorrelativeScanMatcher3D constructions in one call (a sweep
+ * that builds many submaps' matchers at once, e.g. ConstraintBuilder3D's
+ * DispatchScanMatcherConstruction for every submap of a loaded map,
+ * constraint_builder_3d.cc:170-198): out[i] is what csm_fast3d_create(ctx,
+ * high[i], low[i], histograms[i], histogram_sizes[i], options) returns, with
+ * each pyramid level built for all of them in one launch. On error no
+ * matcher is returned. count <= 65535. */
+int csm_fast3d_create_batch(csm_context* ctx, int32_t count,
+                            const csm_hybrid_grid* const* high_resolution,
+                            const csm_hybrid_grid* const* low_resolution,
+                            const float* const* histograms, const int32_t* histogram_sizes,
+                            const csm_fast3d_options* options, csm_fast3d** out);
 void csm_fast3d_destroy(csm_fast3d* m);
 /* Device bytes of the matcher's pyramid (levels and octet planes), and of a
  * HybridGrid's bricks (as csm_fast2d_device_bytes). */

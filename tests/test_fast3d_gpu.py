@@ -369,6 +369,47 @@ def test_synthetic_pairs_match_oracle(csm, oracle, world3d):
     assert stats["exact"] + stats["tie"] >= 3, stats
 
 
+def test_create_batch_equals_single_creates(csm, oracle, world3d):
+    """csm_fast3d_create_batch builds every level of every matcher in one
+    launch per level: the levels are byte-identical to the oracle's
+    (PrecomputationGridStack3D) and to single creates', and a batch search
+    over the batch-built matchers returns what the single-built ones do."""
+    w = world3d
+    o = csm.FastCorrelativeScanMatcherOptions3D()
+    grids = [(csm.HybridGrid(w.high_resolution, *w.high_cells[s]),
+              csm.HybridGrid(w.low_resolution, *w.low_cells[s])) for s in range(w.num_submaps)]
+    batch = csm.FastCorrelativeScanMatcher3D.create_batch(grids, list(w.submap_hist[:w.num_submaps]), o)
+    single = [csm.FastCorrelativeScanMatcher3D(g[0], g[1], w.submap_hist[s], o)
+              for s, g in enumerate(grids)]
+    for s in range(w.num_submaps):
+        oh, ol = oracle.hybrid_grid(w.high_resolution), oracle.hybrid_grid(w.low_resolution)
+        oh.set_values(*w.high_cells[s])
+        ol.set_values(*w.low_cells[s])
+        om = oracle.fast3d(oh, ol, w.submap_hist[s], opt_tuple(o))
+        for lvl in range(o.branch_and_bound_depth):
+            ob, vb = batch[s].read_level(lvl)
+            os_, vs = single[s].read_level(lvl)
+            assert ob == os_ and np.array_equal(vb, vs), (s, lvl)
+            ijk, v = om.level(lvl)
+            assert np.count_nonzero(vb) == np.count_nonzero(v), (s, lvl)
+            loc = ijk - np.asarray(ob)
+            assert np.all(vb[loc[:, 2], loc[:, 1], loc[:, 0]] == v), (s, lvl)
+    nodes = csm.NodeSet3D([w.node(i) for i in range(w.num_nodes)])
+    sub = np.repeat(np.arange(w.num_submaps), w.num_nodes)
+    nod = np.tile(np.arange(w.num_nodes), w.num_submaps)
+    rot = np.array([w.node_rotation(n) for n in range(w.num_nodes)])
+    pairs = csm.make_pairs_3d(sub, nod, 0.6, True, node_q=rot[nod])
+    rb = csm.match_batch_3d(batch, nodes, pairs)
+    rs = csm.match_batch_3d(single, nodes, pairs)
+    assert (rb["status"] == rs["status"]).all()
+    ok = rb["status"] == csm.CSM_OK
+    assert ok.sum() >= 3
+    for f in ("score", "rotational_score", "low_resolution_score", "t", "q"):
+        assert np.array_equal(rb[f][ok], rs[f][ok]), f
+    for m in batch + single:
+        m.close()
+
+
 def test_large_clouds_match_oracle(csm, oracle, world3d):
     """Clouds past the small build's LDS capacity (2048 points) take the
     large-cloud build (up to 8192); a batch mixing both is split over the
