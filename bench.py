@@ -701,10 +701,12 @@ def fast3d_bench(csm, ctx, args, rank=0, world_size=1, dist=None, coll_dev=None,
         g = [(csm.HybridGrid(w.high_resolution, *w.high_cells[s], context=ctx),
               csm.HybridGrid(w.low_resolution, *w.low_cells[s], context=ctx))
              for s in range(w.num_submaps)]
-        # All the sweep's matchers in one csm_fast3d_create_batch call: each
-        # pyramid level is built for every submap in one launch.
-        m = csm.FastCorrelativeScanMatcher3D.create_batch(
-            g, [w.submap_hist[s] for s in range(len(g))], o, ctx)
+        # One create per submap, as the builder makes them: each submap's
+        # pyramid builds on the device while the host prepares the next
+        # (csm_fast3d_create_batch, one launch per level for all submaps,
+        # measured slower here: its builds start only after the last grid).
+        m = [csm.FastCorrelativeScanMatcher3D(gg[0], gg[1], w.submap_hist[s], o, ctx)
+             for s, gg in enumerate(g)]
         return g, m
 
     def close(g, m):

@@ -261,35 +261,7 @@ int csm_hybrid_grid_create(csm_context* ctx, float resolution, const int32_t* ij
     else CSM_HIP(hipEventCreateWithFlags(&ctx->f3_stage_copied, hipEventDisableTiming));
     if ((rc = ctx->f3_grid_stage.Reserve(list_bytes))) return rc;
     int32_t* hs = ctx->f3_grid_stage.as<int32_t>();
-    // Large lists (a submap's high-resolution grid holds ~200k cells, 2.4 MB)
-    // are staged by several threads: the copy is bound by one core's memory
-    // bandwidth otherwise.
-    const int parts = count >= (int64_t{1} << 16)
-                          ? static_cast<int>(std::min<int64_t>(8, count >> 15))
-                          : 1;
-    if (parts == 1) {
-      StageCells(ijk, count, hs, lo, hi);
-    } else {
-      std::vector<std::array<int, 6>> part_bounds(parts);
-      std::vector<std::thread> pool;
-      const int64_t chunk = (count + parts - 1) / parts;
-      for (int t = 0; t < parts; ++t)
-        pool.emplace_back([&, t] {
-          const int64_t b = t * chunk, e = std::min(count, b + chunk);
-          int l3[3], h3[3];
-          StageCells(ijk + 3 * b, e - b, hs + 3 * b, l3, h3);
-          part_bounds[t] = {l3[0], l3[1], l3[2], h3[0], h3[1], h3[2]};
-        });
-      for (auto& th : pool) th.join();
-      for (int a = 0; a < 3; ++a) {
-        lo[a] = part_bounds[0][a];
-        hi[a] = part_bounds[0][3 + a];
-        for (int t = 1; t < parts; ++t) {
-          lo[a] = std::min(lo[a], part_bounds[t][a]);
-          hi[a] = std::max(hi[a], part_bounds[t][3 + a]);
-        }
-      }
-    }
+    StageCells(ijk, count, hs, lo, hi);
     std::memcpy(hs + 3 * count, values, sizeof(uint16_t) * count);
   }
   if (grid_size <= 0) {  // DynamicGrid growth (hybrid_grid.h:283-296, :384-399)
@@ -846,12 +818,33 @@ int PlanFast3d(csm_context* ctx, const csm_hybrid_grid* high, const csm_hybrid_g
 
 // Queues the pyramid builds of `count` planned matchers on ctx->stream: the
 // level-0 conversion, then level by level the gathers, then the octets, each
-// one launch for every matcher of the batch (blockIdx.y = matcher), and
-// records each matcher's ready event. The job lists go up through pinned
+// one launch for every matcher of the batch (blockIdx.y = matcher; a single
+// matcher takes its own launches), and records each matcher's ready event. The job lists go up through pinned
 // staging, rewritten only after the previous batch's copy has finished.
 int BuildFast3d(csm_context* ctx, csm_fast3d* const* ms, const Fast3dPlan* plans, int count) {
   int rc;
   if ((rc = EnsureValueTables(ctx))) return rc;
+  hipStream_t st = ctx->stream;
+  if (count == 1) {  // one matcher: its own launches, no job list to stage
+    csm_fast3d* m = ms[0];
+    const Fast3dPlan& pl = plans[0];
+    if (pl.empty) return CSM_OK;
+    const Submap3Desc& d = m->desc;
+    uint8_t* lv = m->levels.as<uint8_t>();
+    const int64_t n0 = static_cast<int64_t>(d.level[0].nx) * d.level[0].ny * d.level[0].nz;
+    CSM_HIP(LaunchBrickFromValues(pl.high->values.as<uint16_t>(), n0, nullptr,
+                                  ctx->f3_qtab.as<uint8_t>(), nullptr, lv + d.level[0].offset, st));
+    for (int l = 1; l < pl.depth; ++l)
+      CSM_HIP(LaunchLevelGather(lv + d.level[l - 1].offset, d.level[l - 1], lv + d.level[l].offset,
+                                d.level[l], pl.shifts[l], pl.halves[l], st));
+    for (int l = 0; l + 1 < pl.depth; ++l)
+      CSM_HIP(LaunchOctetBuild(lv + d.level[l].offset, d.level[l], d.oct_h[l],
+                               reinterpret_cast<uint64_t*>(m->octs.as<uint8_t>() + d.oct[l].offset),
+                               d.oct[l], st));
+    CSM_HIP(hipEventCreateWithFlags(&m->ready, hipEventDisableTiming));
+    CSM_HIP(hipEventRecord(m->ready, st));
+    return CSM_OK;
+  }
   std::vector<ValueJob3> vjobs;
   int depth = 0;
   for (int i = 0; i < count; ++i) depth = std::max(depth, plans[i].depth);
@@ -879,7 +872,6 @@ int BuildFast3d(csm_context* ctx, csm_fast3d* const* ms, const Fast3dPlan* plans
   for (int l = 0; l < depth; ++l) nrow += level_jobs[l].size() + oct_jobs[l].size();
   const size_t vbytes = (sizeof(ValueJob3) * vjobs.size() + 255) & ~size_t{255};
   const size_t bytes = vbytes + sizeof(RowJob3) * nrow;
-  hipStream_t st = ctx->stream;
   if (bytes > 0) {
     if (ctx->f3_jobs_copied) CSM_HIP(hipEventSynchronize(ctx->f3_jobs_copied));
     else CSM_HIP(hipEventCreateWithFlags(&ctx->f3_jobs_copied, hipEventDisableTiming));
