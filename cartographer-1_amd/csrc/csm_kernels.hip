@@ -740,6 +740,14 @@ __device__ void CountLines(Shared& sh, int level, int ad, int oob) {
 // g, g + groups, ... of the node's list (cells, counts). A child's sum is
 // sum_k cnt[k] * value over the list: the reference's per-point sum
 // regrouped at level 0, an upper bound of it at coarser levels.
+#ifndef CSM_CPOL_QUAD
+// Cache-policy bits of the quad and hex gathers (buffer-load aux operand:
+// 1 sc0, 2 nt, 16 sc1); 0 = default policy (experiments: profiles/r4ae).
+#define CSM_CPOL_QUAD 0
+#endif
+#ifndef CSM_CPOL_HEX
+#define CSM_CPOL_HEX 0
+#endif
 template <typename Shared>
 __device__ __forceinline__ void V4Score(Shared& sh, const uint32_t* cells, const uint8_t* cnts,
                                         int raw_end, const SubmapDesc& sm) {
@@ -809,7 +817,7 @@ __device__ __forceinline__ void V4Score(Shared& sh, const uint32_t* cells, const
       for (int u = 0; u < U; ++u) CSM_COUNT_LINES(level, ad[u], kOOB);
       uint32_t v[U];
   #pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, ad[u], 0, 0);
+      for (int u = 0; u < U; ++u) v[u] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, ad[u], 0, CSM_CPOL_QUAD);
   #pragma unroll
       for (int u = 0; u < U; ++u) accumulate(v[u], c[u]);
     }
@@ -817,7 +825,7 @@ __device__ __forceinline__ void V4Score(Shared& sh, const uint32_t* cells, const
       const int idx = i + g;
       const bool in = idx < e && idx < len;
       const int j = in ? idx : 0;
-      const uint32_t vv = __builtin_amdgcn_raw_buffer_load_b32(rsrc, address(P[j], in), 0, 0);
+      const uint32_t vv = __builtin_amdgcn_raw_buffer_load_b32(rsrc, address(P[j], in), 0, CSM_CPOL_QUAD);
       accumulate(vv, in ? (raw ? 1u : Cn[j]) : 0u);
     }
   }
@@ -907,7 +915,7 @@ __device__ __forceinline__ void V4ScoreHex(Shared& sh, const uint32_t* cells, co
       for (int u = 0; u < U; ++u) CSM_COUNT_LINES(level, ad[u], kOOB);
       decltype(__builtin_amdgcn_raw_buffer_load_b128(rsrc, 0, 0, 0)) v[U];
   #pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, ad[u], 0, 0);
+      for (int u = 0; u < U; ++u) v[u] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, ad[u], 0, CSM_CPOL_HEX);
   #pragma unroll
       for (int u = 0; u < U; ++u) accumulate(v[u], c[u]);
     }
@@ -915,7 +923,7 @@ __device__ __forceinline__ void V4ScoreHex(Shared& sh, const uint32_t* cells, co
       const int idx = i + g;
       const bool in = idx < e && idx < len;
       const int j = in ? idx : 0;
-      const auto vv = __builtin_amdgcn_raw_buffer_load_b128(rsrc, address(P[j], in), 0, 0);
+      const auto vv = __builtin_amdgcn_raw_buffer_load_b128(rsrc, address(P[j], in), 0, CSM_CPOL_HEX);
       accumulate(vv, in ? (raw ? 1u : Cn[j]) : 0u);
     }
   }
