@@ -1172,7 +1172,7 @@ int csm_fast2d_create(csm_context* ctx, const csm_map_limits* limits,
     kind[depth - 1] = 4;
     for (int L = depth - 1; L >= 1;) {
       if (L >= 2 && ((mask >> L) & 1u)) {
-        kind[L - 2] = 16;
+        kind[L - 2] = kHexEntryBytes;
         L -= 2;
       } else {
         kind[L - 1] = 4;
@@ -1184,7 +1184,7 @@ int csm_fast2d_create(csm_context* ctx, const csm_map_limits* limits,
     for (int l = 0; l < depth; ++l) {
       const int h = 1 << l;
       const int km1 = (1 << d.cshift[l]) - 1;
-      const bool hexl = kind[l] == 16;
+      const bool hexl = kind[l] == kHexEntryBytes;
       const int reach = hexl ? 3 * h : h, period = hexl ? 4 * h : 2 * h;
       d.quad_es[l] = kind[l];
       d.quad_bias[l] = (h - 1) + km1 + reach;
@@ -1203,6 +1203,7 @@ int csm_fast2d_create(csm_context* ctx, const csm_map_limits* limits,
     }
     return total <= 0x7fffff00u;
   };
+  if (CSM_HEX8) hex_mask &= ~4u;  // no quantized plane at level 0
   if (!layout(hex_mask)) {
     if (!hex_mask || !layout(0)) return CSM_ERANGE;
     hex_mask = 0;
@@ -1237,10 +1238,10 @@ int csm_fast2d_create(csm_context* ctx, const csm_map_limits* limits,
       CSM_HIP(LaunchPyramidQuad(d.level[l], d.wide_nx[l], d.wide_ny[l], l, km1,
                                 const_cast<uint32_t*>(d.quad[l]), d.quad_w[l], d.quad_h[l],
                                 d.quad_pws[l], d.quad_pph[l], d.quad_bytes[l] / 4, st));
-    else if (d.quad_es[l] == 16)
+    else if (d.quad_es[l] == kHexEntryBytes)
       CSM_HIP(LaunchPyramidHex(d.level[l], d.wide_nx[l], d.wide_ny[l], l, km1, dwiden.as<uint8_t>(),
                                const_cast<uint32_t*>(d.quad[l]), d.quad_w[l], d.quad_h[l],
-                               d.quad_pws[l], d.quad_pph[l], d.quad_bytes[l] / 16, st));
+                               d.quad_pws[l], d.quad_pph[l], d.quad_bytes[l] / kHexEntryBytes, st));
   }
   // Correspondence costs (Grid2D::GetCorrespondenceCost, grid_2d.cc) for the
   // CeresScanMatcher2D refinement: the value table with unknown -> max_cc.

@@ -600,8 +600,10 @@ __global__ void pyramid_widen(const uint8_t* __restrict__ level, int wnx, int wn
 // Polyphase with period P = 4h: plane (X' mod P, Y' mod P), entry
 // (X' / P, Y' / P), so sibling nodes' lookups of one point are adjacent
 // entries.
+// CSM_HEX8: the 8-byte form, nibbles q = ceil(M / 17): dword d, byte b holds
+// q(2d, b) in its low and q(2d + 1, b) in its high nibble.
 __global__ void pyramid_hex(const uint8_t* __restrict__ mlev, int mw, int mh, int log_h,
-                            uint4* __restrict__ out, int qw, int qh, int pws, int pph, int total) {
+                            void* __restrict__ out, int qw, int qh, int pws, int pph, int total) {
   const int o = blockIdx.x * blockDim.x + threadIdx.x;
   if (o >= total) return;
   const int h = 1 << log_h;
@@ -611,21 +613,29 @@ __global__ void pyramid_hex(const uint8_t* __restrict__ mlev, int mw, int mh, in
   const int fx = pi & (p - 1), fy = pi >> s;
   const int ky = k / pws, kx = k - ky * pws;
   const int xq = (kx << s) + fx, yq = (ky << s) + fy;
-  uint4 v = make_uint4(0u, 0u, 0u, 0u);
+  uint32_t w[4] = {0u, 0u, 0u, 0u};
   if (xq < qw && yq < qh) {
     const int X = xq - 3 * h, Y = yq - 3 * h;
     auto m = [&](int a, int b) -> uint32_t {
       return (a >= 0 && b >= 0 && a < mw && b < mh) ? mlev[static_cast<size_t>(b) * mw + a] : 0u;
     };
-    uint32_t w[4];
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
       const int xa = X + a * h;
       w[a] = m(xa, Y) | (m(xa, Y + h) << 8) | (m(xa, Y + 2 * h) << 16) | (m(xa, Y + 3 * h) << 24);
     }
-    v = make_uint4(w[0], w[1], w[2], w[3]);
   }
-  out[o] = v;
+  if (CSM_HEX8) {
+    // Per byte: ceil(v / 17) = (v + 16) / 17 <= 15, as (x * 241) >> 12 for x <= 271.
+    auto q = [](uint32_t x) {
+      uint32_t r = 0;
+      for (int b = 0; b < 4; ++b) r |= ((((x >> (8 * b)) & 0xffu) + 16u) * 241u >> 12) << (8 * b);
+      return r;
+    };
+    static_cast<uint2*>(out)[o] = make_uint2(q(w[0]) | (q(w[1]) << 4), q(w[2]) | (q(w[3]) << 4));
+  } else {
+    static_cast<uint4*>(out)[o] = make_uint4(w[0], w[1], w[2], w[3]);
+  }
 }
 
 // ---------------------------------------------------------------- K2-K4 v4 -
@@ -887,11 +897,29 @@ __device__ __forceinline__ void V4ScoreHex(Shared& sh, const uint32_t* cells, co
                        static_cast<unsigned>(Y) < static_cast<unsigned>(qh);
     const int a = __umul24((((Y & pmask) << sft) | (X & pmask)), ps16) + qoff;
     const int b = __umul24(Y >> sft, pws16) + a;
-    return valid ? ((X >> sft) << 4) + b : kOOB;
+    return valid ? ((X >> sft) << (CSM_HEX8 ? 3 : 4)) + b : kOOB;
   };
+#if CSM_HEX8
+  using HexVec = decltype(__builtin_amdgcn_raw_buffer_load_b64(rsrc, 0, 0, 0));
+  auto hload = [&](int ad) { return __builtin_amdgcn_raw_buffer_load_b64(rsrc, ad, 0, CSM_CPOL_HEX); };
+  // Children (2d, b) and (2d + 1, b) accumulate the low and high nibble of
+  // byte b of dword d times the entry's count (sums in units of 17).
+  auto accumulate = [&](const HexVec& v, uint32_t c) {
+#pragma unroll
+    for (int d = 0; d < 2; ++d) {
+      const uint32_t lo = v[d] & 0x0f0f0f0fu, hi = (v[d] >> 4) & 0x0f0f0f0fu;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        acc[8 * d + b] = __builtin_amdgcn_udot4(lo, c << (8 * b), acc[8 * d + b], false);
+        acc[8 * d + 4 + b] = __builtin_amdgcn_udot4(hi, c << (8 * b), acc[8 * d + 4 + b], false);
+      }
+    }
+  };
+#else
+  using HexVec = decltype(__builtin_amdgcn_raw_buffer_load_b128(rsrc, 0, 0, 0));
+  auto hload = [&](int ad) { return __builtin_amdgcn_raw_buffer_load_b128(rsrc, ad, 0, CSM_CPOL_HEX); };
   // Child (a, b) accumulates byte b of dword a times the entry's count.
-  auto accumulate = [&](const decltype(__builtin_amdgcn_raw_buffer_load_b128(rsrc, 0, 0, 0))& v,
-                        uint32_t c) {
+  auto accumulate = [&](const HexVec& v, uint32_t c) {
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
 #pragma unroll
@@ -899,6 +927,7 @@ __device__ __forceinline__ void V4ScoreHex(Shared& sh, const uint32_t* cells, co
         acc[4 * a + b] = __builtin_amdgcn_udot4(v[a], c << (8 * b), acc[4 * a + b], false);
     }
   };
+#endif
   if (active) {  // the missing nodes' lanes issue no loads
     int i = s;
     for (; i + U * groups <= e; i += U * groups) {
@@ -913,9 +942,9 @@ __device__ __forceinline__ void V4ScoreHex(Shared& sh, const uint32_t* cells, co
         c[u] = in ? (raw ? 1u : Cn[j]) : 0u;
       }
       for (int u = 0; u < U; ++u) CSM_COUNT_LINES(level, ad[u], kOOB);
-      decltype(__builtin_amdgcn_raw_buffer_load_b128(rsrc, 0, 0, 0)) v[U];
+      HexVec v[U];
   #pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, ad[u], 0, CSM_CPOL_HEX);
+      for (int u = 0; u < U; ++u) v[u] = hload(ad[u]);
   #pragma unroll
       for (int u = 0; u < U; ++u) accumulate(v[u], c[u]);
     }
@@ -923,7 +952,7 @@ __device__ __forceinline__ void V4ScoreHex(Shared& sh, const uint32_t* cells, co
       const int idx = i + g;
       const bool in = idx < e && idx < len;
       const int j = in ? idx : 0;
-      const auto vv = __builtin_amdgcn_raw_buffer_load_b128(rsrc, address(P[j], in), 0, CSM_CPOL_HEX);
+      const HexVec vv = hload(address(P[j], in));
       accumulate(vv, in ? (raw ? 1u : Cn[j]) : 0u);
     }
   }
@@ -1321,7 +1350,7 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
           if (nd < pn) {
             clvl = sh.node_level[nd] - (hexb ? 2 : 1);
             const int h = 1 << clvl;
-            sum = sh.part[nd][c];
+            sum = sh.part[nd][c] * (hexb ? kHexScale : 1);
             sh.part[nd][c] = 0;
             r = sh.node_rot[nd];
             xo = sh.node_xo[nd] + (c >> (lk >> 1)) * h;
@@ -1555,7 +1584,7 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
       const int done = Uniform(sh.done);
       if (done) break;
       if (nodes > 0) {
-        // Algorithmic bytes: 4 per quad-dword gather, 16 per hex gather.
+        // Algorithmic bytes: 4 per quad-dword gather, 16 (CSM_HEX8: 8) per hex gather.
         const bool hexb = kHex && Uniform(sh.batch_hex);
         if (hexb)
           V4ScoreHex(sh, cells, cnts, raw_end, sm);
@@ -1563,7 +1592,7 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
           V4Score(sh, cells, cnts, raw_end, sm);
         const int kids = hexb ? 16 : 4;
         local_cands += kids * nodes;
-        local_lookups += static_cast<unsigned long long>(kids) *
+        local_lookups += static_cast<unsigned long long>(hexb ? kHexEntryBytes : 4) *
                          static_cast<unsigned>(Uniform(sh.batch_entries));
       }
       __syncthreads();
@@ -1791,7 +1820,7 @@ hipError_t LaunchPyramidHex(const uint8_t* level, int wnx, int wny, int log_h, i
   hipLaunchKernelGGL(pyramid_widen, dim3((mw + 255) / 256, mh), dim3(256), 0, st, level, wnx, wny, km1,
                      scratch, mw, mh);
   hipLaunchKernelGGL(pyramid_hex, dim3((total + 255) / 256), dim3(256), 0, st, scratch, mw, mh, log_h,
-                     reinterpret_cast<uint4*>(out), qw, qh, pws, pph, total);
+                     static_cast<void*>(out), qw, qh, pws, pph, total);
   return hipGetLastError();
 }
 
