@@ -258,7 +258,7 @@ def c2_run(csm, ctx, args, rank, world_size, dist, coll_dev, gather, transport, 
         "accepted_constraints_per_step": accepted,
         "errors_per_step": errors / steps,
         "stack_high_water": int(tm.stack_high_water),
-        "tied_pairs": int(tm.tied_pairs), "ties_unresolved": int(tm.ties_unresolved),
+        "tied_pairs": int(tm.tied_pairs), "ties_walked": int(tm.ties_walked),
         "search_levels": {"candidates_per_pair": [c / max(n_pairs * steps, 1) for c in lv_cands],
                           "mean_lanes_per_batch": [c / b if b else 0 for c, b in zip(lv_cands, lv_batches)]},
         "setup_s": {"world": gen_s, "pyramids_and_upload": build_s},
@@ -784,11 +784,11 @@ def fast3d_bench(csm, ctx, args, rank=0, world_size=1, dist=None, coll_dev=None,
            # Pairs whose maximum more than one passing leaf reached (resolved to
            # the reference's pick, host3d.cc ResolveTies3d), per step.
            "tied_pairs_per_step": tm.tied_pairs_3d / reps,
-           "ties_unresolved_per_step": tm.ties_unresolved_3d / reps,
+           "ties_walked_per_step": tm.ties_walked_3d / reps,
            "ties_by_branch_last_step": {name: int(((res3["status"] == 0) & (res3["tie"] == code)).sum())
                                         for name, code in (("ancestors", csm.TIE_ANCESTORS),
                                                            ("toplist", csm.TIE_TOPLIST),
-                                                           ("unresolved", csm.TIE_UNRESOLVED))},
+                                                           ("walk", csm.TIE_WALK))},
            "build_ms_per_step": phase["build"] / reps * 1e3,
            "release_ms_per_step": phase["release"] / max(reps - 1, 1) * 1e3,
            "search_ms_per_step": phase["search"] / reps * 1e3,
@@ -1164,13 +1164,13 @@ def c3_run(csm, ctx, args, rank, world_size, dist, coll_dev, comm, gather, trans
         "chunks": n_chunks, "chunks_claimed": int(claimed), "chunks_max_rank": int(chunks_max),
         # Pairs with exactly tied maxima (resolved to the reference's pick,
         # csm_host.cc ResolveTies) and any left at the smallest-key leaf.
-        "tied_pairs_rank0": int(tm.tied_pairs), "ties_unresolved_rank0": int(tm.ties_unresolved),
+        "tied_pairs_rank0": int(tm.tied_pairs), "ties_walked_rank0": int(tm.ties_walked),
         # Per resolution branch (csm_result2d.tie): under one top-level
         # candidate, through the whole top-level list's introsort, unresolved.
         "ties_by_branch_rank0": {name: sum(1 for t in done["ties"] if t[2] == code)
                                  for name, code in (("ancestors", csm.TIE_ANCESTORS),
                                                     ("toplist", csm.TIE_TOPLIST),
-                                                    ("unresolved", csm.TIE_UNRESOLVED))},
+                                                    ("walk", csm.TIE_WALK))},
         "kernel_s_rank0": tm.search_kernel_ms * 1e-3, "search_launches_rank0": int(tm.search_launches),
         "search_levels": {"candidates_per_pair": [c / max(mine * K * N, 1) for c in lv_cands],
                           "mean_lanes_per_batch": [c / b if b else 0 for c, b in zip(lv_cands, lv_batches)]},

@@ -78,7 +78,7 @@ class Result2D(C.Structure):
 
 
 # csm_result2d.tie: how a result was picked among exactly tied maxima.
-TIE_NONE, TIE_ANCESTORS, TIE_TOPLIST, TIE_UNRESOLVED = 0, 1, 2, 3
+TIE_NONE, TIE_ANCESTORS, TIE_TOPLIST, TIE_WALK = 0, 1, 2, 3
 
 
 class Timing(C.Structure):
@@ -88,9 +88,9 @@ class Timing(C.Structure):
                 ("rt3d_lookups", C.c_double), ("fast3d_kernel_ms", C.c_double),
                 ("fast3d_launches", C.c_int64), ("fast3d_lookups", C.c_double),
                 ("search_errors", C.c_int64), ("stack_high_water", C.c_int64),
-                ("tied_pairs", C.c_int64), ("ties_unresolved", C.c_int64),
+                ("tied_pairs", C.c_int64), ("ties_walked", C.c_int64),
                 ("ties_toplist", C.c_int64), ("tied_pairs_3d", C.c_int64),
-                ("ties_unresolved_3d", C.c_int64)]
+                ("ties_walked_3d", C.c_int64)]
 
 
 class Pose3D(C.Structure):

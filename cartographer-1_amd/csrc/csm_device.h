@@ -104,6 +104,21 @@ struct ScoreJob {
 };
 constexpr int kTieCap = 4096;  // tied leaves recorded per pair
 
+// Ordered walk (csm_host.cc ResolveTies, pairs with more tied leaves than the
+// collect pass records): one workgroup per job follows the reference's
+// visiting order from the sorted lowest-resolution list down to the first
+// leaf at the maximum (fast_correlative_scan_matcher_2d.cc:335-378).
+struct WalkJob2 {
+  int32_t pair;          // into the collect launch's pair descriptors
+  int32_t target_sum;    // the pair's maximum leaf sum
+  int32_t top_level;     // branch_and_bound_depth - 1
+  int32_t top_first;     // sorted lowest-resolution entries (rot, x, y, sum), sum >= target
+  int32_t top_count;
+  int32_t bounds_first;  // ShrinkToFit bounds of rotation r at bounds_first + r
+  float min_s, max_s;    // the submap's score range (SumToScore)
+};
+constexpr int kWalkStack = 64;  // 1 + 3 x depth entries at most
+
 // Per-XCD work queues over rotation chunks of pairs.
 struct WorkQueues {
   const int32_t* pair_order;      // pairs, grouped by queue

@@ -444,13 +444,13 @@ void RotationBounds(const csm_scan_set* scans, const PairDesc& d, const SubmapDe
 // CPU scoring is involved.
 int ResolveTies(csm_context* ctx, csm_fast2d* const* submaps, csm_scan_set* scans,
                 const std::vector<PairDesc>& pdesc, const std::vector<float2>& rot_host,
-                const SearchPlan& plan, const std::vector<int32_t>& stat,
+                const SearchPlan& plan, std::vector<int32_t>* stat,
                 const std::vector<uint64_t>& keys_hi, std::vector<uint64_t>* keys,
                 std::vector<int8_t>* tie_code) {
   std::vector<int> tied;
   for (int k = 0; k < static_cast<int>(pdesc.size()); ++k) {
     const uint64_t key = (*keys)[k];
-    if ((stat[k] & kStatusRange) || key == 0) continue;
+    if (((*stat)[k] & kStatusRange) || key == 0) continue;
     const int64_t sum = static_cast<int64_t>(key >> kSumShift);
     if (sum <= pdesc[k].max_rejected_sum) continue;
     if ((keys_hi[k] >> kSumShift) == (key >> kSumShift) && keys_hi[k] != HighLeafKey(key))
@@ -496,12 +496,16 @@ int ResolveTies(csm_context* ctx, csm_fast2d* const* submaps, csm_scan_set* scan
   std::vector<ScoreJob> jobs;
   std::vector<int4> queries;
   std::vector<int> leaf_query;       // per leaf: first of its D - 1 ancestor queries
+  std::vector<int> walk;             // tied pairs (pd2 index) whose leaves overflow the record
   for (size_t t = 0; t < tied.size(); ++t) {
     const int k = tied[t];
     const int cnt = counts[t];
     if ((st2[t] & kStatusRange) || cnt > kTieCap || cnt < 2) {
-      ctx->t.ties_unresolved += 1;
-      (*tie_code)[k] = CSM_TIE_UNRESOLVED;
+      // More tied leaves than the collect pass records (or its frontier
+      // overflowed): walk the reference's order on the device instead (4).
+      ctx->t.ties_walked += 1;
+      (*tie_code)[k] = CSM_TIE_WALK;
+      walk.push_back(static_cast<int>(t));
       continue;
     }
     const PairDesc& d = pdesc[k];
@@ -614,12 +618,26 @@ int ResolveTies(csm_context* ctx, csm_fast2d* const* submaps, csm_scan_set* scan
     if (cand[wi].need_perm) perm.push_back(static_cast<int>(wi));
   }
   ctx->t.ties_toplist += static_cast<int64_t>(perm.size());
-  if (!perm.empty()) {
+  // The whole lowest-resolution list of tied pairs `ts` (pd2 indices) in the
+  // reference's order: ShrinkToFit bounds of every rotation on the device,
+  // every lattice node of the reference's top level scored in one launch
+  // (GenerateLowestResolutionCandidates, :276-312), each list sorted on its
+  // own threads.
+  struct TopList {
+    std::vector<std::array<int, 4>> rb;  // per rotation bounds
+    std::vector<int64_t> rot_first;      // per rotation first lattice index
+    std::vector<int32_t> sums;           // lattice index -> sum
+    std::vector<int32_t> order;          // sorted position -> lattice index
+  };
+  auto top_lists = [&](const std::vector<int>& ts, std::vector<TopList>* out) -> int {
+    out->assign(ts.size(), TopList{});
+    if (ts.empty()) return CSM_OK;
     std::vector<int2> bjobs;
-    for (int wi : perm)
-      for (int r = 0; r < pdesc[work[wi].k].num_scans; ++r) bjobs.push_back(make_int2(work[wi].t, r));
-    if ((rc = ctx->sq_jobs.Reserve(sizeof(int2) * bjobs.size()))) return rc;
-    if ((rc = ctx->sq_sums.Reserve(sizeof(int4) * bjobs.size()))) return rc;
+    for (int t : ts)
+      for (int r = 0; r < pd2[t].num_scans; ++r) bjobs.push_back(make_int2(t, r));
+    int r2;
+    if ((r2 = ctx->sq_jobs.Reserve(sizeof(int2) * bjobs.size()))) return r2;
+    if ((r2 = ctx->sq_sums.Reserve(sizeof(int4) * bjobs.size()))) return r2;
     hipStream_t st = ctx->stream;
     std::vector<int4> bounds(bjobs.size());
     CSM_HIP(hipMemcpyAsync(ctx->sq_jobs.ptr, bjobs.data(), sizeof(int2) * bjobs.size(),
@@ -633,20 +651,20 @@ int ResolveTies(csm_context* ctx, csm_fast2d* const* submaps, csm_scan_set* scan
     CSM_HIP(hipStreamSynchronize(st));
     std::vector<ScoreJob> tj;
     std::vector<int4> tq;
-    std::vector<int64_t> base(perm.size());
+    std::vector<int64_t> base(ts.size());
     size_t bi = 0;
-    for (size_t pi = 0; pi < perm.size(); ++pi) {
-      const Tie& w = work[perm[pi]];
-      Cand& c = cand[perm[pi]];
-      const int n = pdesc[w.k].num_scans;
-      const int T = w.depth - 1, step = 1 << T;
+    for (size_t pi = 0; pi < ts.size(); ++pi) {
+      const PairDesc& d = pd2[ts[pi]];
+      TopList& c = (*out)[pi];
+      const int n = d.num_scans;
+      const int T = submaps[d.submap]->options.branch_and_bound_depth - 1, step = 1 << T;
       base[pi] = static_cast<int64_t>(tq.size());
       c.rb.resize(n);
       c.rot_first.assign(n + 1, 0);
       for (int r = 0; r < n; ++r, ++bi) {
         const int4 b = bounds[bi];
         c.rb[r] = {b.x, b.y, b.z, b.w};
-        ScoreJob job{w.t, r, static_cast<int32_t>(tq.size()), 0};
+        ScoreJob job{ts[pi], r, static_cast<int32_t>(tq.size()), 0};
         for (int x = b.x; x <= b.y; x += step)
           for (int y = b.z; y <= b.w; y += step) tq.push_back(make_int4(T, x, y, 0));
         job.count = static_cast<int32_t>(tq.size()) - job.first;
@@ -655,50 +673,132 @@ int ResolveTies(csm_context* ctx, csm_fast2d* const* submaps, csm_scan_set* scan
       }
     }
     tp3 = now();
-    std::vector<int32_t> ts;
-    if ((rc = score(tj, tq, &ts))) return rc;
+    std::vector<int32_t> sc;
+    if ((r2 = score(tj, tq, &sc))) return r2;
     tp4 = now();
     // ScoreCandidates: score = ToScore(sum / n), then
     // std::sort(greater<Candidate2D>) — the same algorithm and the same
     // comparisons give the same permutation for any element type; IntroSort
     // (parallel_sort.h) is that algorithm with independent partitions on
     // threads. Up to 8 lists at once, 8 threads between them.
-    const size_t nthreads = std::min<size_t>(perm.size(), 8);
+    const size_t nthreads = std::min<size_t>(ts.size(), 8);
     const int sort_threads = static_cast<int>(8 / std::max<size_t>(nthreads, 1));
     auto sort_one = [&](size_t pi) {
-      const Tie& w = work[perm[pi]];
-      Cand& c = cand[perm[pi]];
-      const PairDesc& d = pdesc[w.k];
+      TopList& c = (*out)[pi];
+      const PairDesc& d = pd2[ts[pi]];
       const csm_fast2d* m = submaps[d.submap];
       const int64_t n = c.rot_first.back();
+      c.sums.assign(sc.begin() + base[pi], sc.begin() + base[pi] + n);
       // 8-byte elements (the comparisons, and so the permutation, are the
       // same whatever the element carries).
       std::vector<std::pair<float, int32_t>> lst(n);
       ParallelRanges(n, sort_threads, [&](std::ptrdiff_t lo, std::ptrdiff_t hi) {
         for (std::ptrdiff_t i = lo; i < hi; ++i)
-          lst[i] = {SumToScore(ts[base[pi] + i], d.num_points, m->min_s, m->max_s),
-                    static_cast<int32_t>(i)};
+          lst[i] = {SumToScore(c.sums[i], d.num_points, m->min_s, m->max_s), static_cast<int32_t>(i)};
       });
       IntroSort(lst.data(), lst.data() + n,
                 [](const std::pair<float, int32_t>& a, const std::pair<float, int32_t>& b) {
                   return a.first > b.first;
                 },
                 sort_threads);
-      c.pos.resize(n);
+      c.order.resize(n);
       ParallelRanges(n, sort_threads, [&](std::ptrdiff_t lo, std::ptrdiff_t hi) {
-        for (std::ptrdiff_t i = lo; i < hi; ++i) c.pos[lst[i].second] = i;
+        for (std::ptrdiff_t i = lo; i < hi; ++i) c.order[i] = lst[i].second;
       });
     };
     if (nthreads <= 1) {
-      for (size_t pi = 0; pi < perm.size(); ++pi) sort_one(pi);
+      for (size_t pi = 0; pi < ts.size(); ++pi) sort_one(pi);
     } else {
       std::vector<std::thread> pool;
       std::atomic<size_t> next{0};
       for (size_t i = 0; i < nthreads; ++i)
         pool.emplace_back([&] {
-          for (size_t pi; (pi = next.fetch_add(1)) < perm.size();) sort_one(pi);
+          for (size_t pi; (pi = next.fetch_add(1)) < ts.size();) sort_one(pi);
         });
       for (auto& th : pool) th.join();
+    }
+    return CSM_OK;
+  };
+  if (!perm.empty()) {
+    std::vector<int> ts;
+    for (int wi : perm) ts.push_back(work[wi].t);
+    std::vector<TopList> tl;
+    if ((rc = top_lists(ts, &tl))) return rc;
+    for (size_t pi = 0; pi < perm.size(); ++pi) {
+      Cand& c = cand[perm[pi]];
+      c.rb = std::move(tl[pi].rb);
+      c.rot_first = std::move(tl[pi].rot_first);
+      const std::vector<int32_t>& order = tl[pi].order;
+      c.pos.resize(order.size());
+      ParallelRanges(static_cast<std::ptrdiff_t>(order.size()), 8,
+                     [&](std::ptrdiff_t lo, std::ptrdiff_t hi) {
+                       for (std::ptrdiff_t i = lo; i < hi; ++i) c.pos[order[i]] = i;
+                     });
+    }
+  }
+  // (4) Pairs whose tied leaves overflow the record: the device walks the
+  // reference's visiting order (fast2d_walk) from the sorted top list, of
+  // which only the entries whose sum reaches the maximum can lead to it.
+  if (!walk.empty()) {
+    std::vector<TopList> tl;
+    if ((rc = top_lists(walk, &tl))) return rc;
+    std::vector<WalkJob2> wj;
+    std::vector<int4> wtop, wb;
+    for (size_t wi = 0; wi < walk.size(); ++wi) {
+      const int t = walk[wi];
+      const PairDesc& d = pd2[t];
+      const csm_fast2d* m = submaps[d.submap];
+      const TopList& c = tl[wi];
+      const int T = m->options.branch_and_bound_depth - 1, step = 1 << T;
+      WalkJob2 j{t, d.collect_sum, T, static_cast<int32_t>(wtop.size()), 0,
+                 static_cast<int32_t>(wb.size()), m->min_s, m->max_s};
+      for (const auto& b : c.rb) wb.push_back(make_int4(b[0], b[1], b[2], b[3]));
+      for (const int32_t li : c.order) {
+        if (c.sums[li] < d.collect_sum) continue;
+        const int r = static_cast<int>(std::upper_bound(c.rot_first.begin(), c.rot_first.end(), li) -
+                                       c.rot_first.begin()) - 1;
+        const int ny = (c.rb[r][3] - c.rb[r][2] + step) / step;
+        const int64_t loc = li - c.rot_first[r];
+        wtop.push_back(make_int4(r, c.rb[r][0] + static_cast<int>(loc / ny) * step,
+                                 c.rb[r][2] + static_cast<int>(loc % ny) * step, c.sums[li]));
+      }
+      j.top_count = static_cast<int32_t>(wtop.size()) - j.top_first;
+      wj.push_back(j);
+    }
+    // One buffer: jobs | top entries | bounds | results.
+    const size_t o_top = (sizeof(WalkJob2) * wj.size() + 15) & ~size_t{15};
+    const size_t o_b = o_top + sizeof(int4) * std::max<size_t>(wtop.size(), 1);
+    const size_t o_out = o_b + sizeof(int4) * wb.size();
+    const size_t bytes = o_out + sizeof(int4) * wj.size();
+    if ((rc = ctx->walk_buf.Reserve(bytes))) return rc;
+    char* dw = ctx->walk_buf.as<char>();
+    std::vector<char> hw(o_out);
+    std::memcpy(hw.data(), wj.data(), sizeof(WalkJob2) * wj.size());
+    if (!wtop.empty()) std::memcpy(hw.data() + o_top, wtop.data(), sizeof(int4) * wtop.size());
+    std::memcpy(hw.data() + o_b, wb.data(), sizeof(int4) * wb.size());
+    hipStream_t st = ctx->stream;
+    CSM_HIP(hipMemcpyAsync(dw, hw.data(), o_out, hipMemcpyHostToDevice, st));
+    CSM_HIP(LaunchFast2dWalk(static_cast<int>(wj.size()), plan.max_npad, st,
+                             ctx->submap_desc.as<SubmapDesc>(),
+                             static_cast<const PairDesc*>(ctx->pair_desc_dev), scans->points.as<float>(),
+                             scans->rot_dev.as<float2>(), reinterpret_cast<const WalkJob2*>(dw),
+                             reinterpret_cast<const int4*>(dw + o_top),
+                             reinterpret_cast<const int4*>(dw + o_b), reinterpret_cast<int4*>(dw + o_out)));
+    std::vector<int4> found(wj.size());
+    CSM_HIP(hipMemcpyAsync(found.data(), dw + o_out, sizeof(int4) * wj.size(), hipMemcpyDeviceToHost, st));
+    CSM_HIP(hipStreamSynchronize(st));
+    for (size_t wi = 0; wi < walk.size(); ++wi) {
+      const int k = tied[walk[wi]];
+      if (!found[wi].w) {
+        // Unreachable: the maximum is some leaf's sum, and the walk visits
+        // every node whose sum reaches it. Never return a leaf that is not
+        // the reference's: the pair's result is void.
+        (*keys)[k] = 0;
+        (*stat)[k] |= kStatusRange;
+        continue;
+      }
+      (*keys)[k] = PackLeafKey(static_cast<uint32_t>(pd2[walk[wi]].collect_sum), found[wi].x,
+                               found[wi].y, found[wi].z);
     }
   }
   const auto tp5 = now();
@@ -932,7 +1032,7 @@ int RunBatch(csm_context* ctx, csm_fast2d* const* submaps, int32_t num_submaps,
   const auto t_ties = std::chrono::steady_clock::now();
   const int64_t tied_before = ctx->t.tied_pairs;
   std::vector<int8_t> tie_code(np, CSM_TIE_NONE);
-  if (plan.use_v2 && (rcode = ResolveTies(ctx, submaps, scans, pdesc, rot_host, plan, stat, keys_hi,
+  if (plan.use_v2 && (rcode = ResolveTies(ctx, submaps, scans, pdesc, rot_host, plan, &stat, keys_hi,
                                            &keys, &tie_code)))
     return rcode;
   const double ties_ms = ms_since(t_ties);

@@ -152,10 +152,10 @@ inline void AddTiming(csm_timing* a, const csm_timing& b) {
   a->search_errors += b.search_errors;
   a->stack_high_water = std::max(a->stack_high_water, b.stack_high_water);
   a->tied_pairs += b.tied_pairs;
-  a->ties_unresolved += b.ties_unresolved;
+  a->ties_walked += b.ties_walked;
   a->ties_toplist += b.ties_toplist;
   a->tied_pairs_3d += b.tied_pairs_3d;
-  a->ties_unresolved_3d += b.ties_unresolved_3d;
+  a->ties_walked_3d += b.ties_walked_3d;
 }
 
 struct csm_context {
@@ -178,7 +178,7 @@ struct csm_context {
   csm_timing call_t{};                // finished single calls' timing (call_mu)
   csm_scan_set single;                // the cloud of the current single 2D call
   csm::PinnedBuf single_stage;
-  csm::DevBuf submap_desc, spill, single_points, ties, sq_jobs, sq_queries, sq_sums;
+  csm::DevBuf submap_desc, spill, single_points, ties, sq_jobs, sq_queries, sq_sums, walk_buf;
   // One 2D search launch's descriptors and outputs (csm_host.cc LaunchSearch),
   // with pinned staging for its one upload and one readback.
   csm::DevBuf arena;
@@ -194,7 +194,7 @@ struct csm_context {
   // 3D path scratch (host3d.cc).
   csm::DevBuf rt3_rot, rt3_rot4, rt3_cols, rt3_trans, rt3_points, rt3_best, f3_pairs, f3_yaws, f3_points,
       f3_low_points, f3_best, f3_status, f3_counter, f3_items, f3_scores, f3_spill, f3_best_hi,
-      f3_ties, f3_tie_count, f3_tie_yaws, f3_sq_jobs, f3_sq_queries, f3_sq_sums;
+      f3_ties, f3_tie_count, f3_tie_yaws, f3_sq_jobs, f3_sq_queries, f3_sq_sums, f3_walk_buf;
   csm::PinnedBuf f3_host_yaws, f3_host_points;
   // Side stream for the 3D batch's cloud upload (overlaps the rotational
   // scores on `stream`); the search waits on f3_points_ready.

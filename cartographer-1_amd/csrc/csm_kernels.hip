@@ -1625,22 +1625,12 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
 #endif
 }
 
-// Tie resolution (csm_host.cc ResolveTies): exact level-d sums of listed
-// candidates, ScoreCandidates' integer sums (fast_correlative_scan_matcher_2d.cc
-// :314-333) over the row-major levels. One workgroup per (pair, rotation)
-// job: the rotation's scan is discretized into LDS exactly as the search
-// discretizes it (padding cells lie off every level), then each wave sums its
-// queries (level, x_off, y_off) over the points.
-__global__ void __launch_bounds__(256)
-fast2d_score_queries(const SubmapDesc* __restrict__ submaps, const PairDesc* __restrict__ pairs,
-                     const float* __restrict__ points, const float2* __restrict__ rot_table,
-                     const ScoreJob* __restrict__ jobs, const int4* __restrict__ queries,
-                     int32_t* __restrict__ sums, int npad) {
-  extern __shared__ __align__(16) uint32_t cells[];
-  const ScoreJob job = jobs[blockIdx.x];
-  const PairDesc pd = pairs[job.pair];
-  const SubmapDesc& sm = submaps[pd.submap];
-  const float2 q = rot_table[pd.rot_offset + job.rot];
+// One rotation of a pair's scan discretized into LDS exactly as the search
+// discretizes it (padding cells lie off every level). The caller
+// synchronizes before reading `cells`.
+__device__ void DiscretizeRotation(uint32_t* __restrict__ cells, int npad, const PairDesc& pd,
+                                   const SubmapDesc& sm, float2 q,
+                                   const float* __restrict__ points) {
   const double inv_res = 1.0 / sm.resolution;  // CellCoordFast
   for (int i = threadIdx.x; i < npad; i += blockDim.x) {
     uint32_t c = 0x80008000u;  // (-32768, -32768): outside every level
@@ -1659,12 +1649,148 @@ fast2d_score_queries(const SubmapDesc* __restrict__ submaps, const PairDesc* __r
     }
     cells[i] = c;
   }
+}
+
+// Tie resolution (csm_host.cc ResolveTies): exact level-d sums of listed
+// candidates, ScoreCandidates' integer sums (fast_correlative_scan_matcher_2d.cc
+// :314-333) over the row-major levels. One workgroup per (pair, rotation)
+// job: the rotation's scan is discretized into LDS, then each wave sums its
+// queries (level, x_off, y_off) over the points.
+__global__ void __launch_bounds__(256)
+fast2d_score_queries(const SubmapDesc* __restrict__ submaps, const PairDesc* __restrict__ pairs,
+                     const float* __restrict__ points, const float2* __restrict__ rot_table,
+                     const ScoreJob* __restrict__ jobs, const int4* __restrict__ queries,
+                     int32_t* __restrict__ sums, int npad) {
+  extern __shared__ __align__(16) uint32_t cells[];
+  const ScoreJob job = jobs[blockIdx.x];
+  const PairDesc pd = pairs[job.pair];
+  const SubmapDesc& sm = submaps[pd.submap];
+  DiscretizeRotation(cells, npad, pd, sm, rot_table[pd.rot_offset + job.rot], points);
   __syncthreads();
   for (int k = threadIdx.x >> 6; k < job.count; k += blockDim.x >> 6) {
     const int4 qu = queries[job.first + k];
     const int s = ScoreOne(cells, npad, MakeView(sm, qu.x), qu.y, qu.z);
     if ((threadIdx.x & 63) == 0) sums[job.first + k] = s;
   }
+}
+
+// ScoreCandidates' score (fast_correlative_scan_matcher_2d.cc:330-332,
+// PrecomputationGrid2D::ToScore) with the host's float operations
+// (search_window.cc SumToScore): the children's visiting order compares it.
+__device__ __forceinline__ float SumToScoreDev(int sum, int n, float min_s, float max_s) {
+  const float mean = __fdiv_rn(static_cast<float>(sum), static_cast<float>(n));
+  return __fadd_rn(min_s, __fmul_rn(mean, __fdiv_rn(__fsub_rn(max_s, min_s), 255.f)));
+}
+
+// Ordered walk to the reference's pick among exactly tied maxima, for pairs
+// whose tied leaves overflow the collect pass (csm_host.cc ResolveTies). The
+// reference's BranchAndBound (fast_correlative_scan_matcher_2d.cc:335-378)
+// visits the sorted lowest-resolution list in order, each node's <= 4
+// children (x, then y; a child past the rotation's ShrinkToFit bound ends
+// its loop) by descending score with equal scores in generation order, and
+// keeps the first leaf at the maximum: before it is reached the incumbent is
+// below the maximum, so every node whose sum reaches the maximum is visited,
+// and nodes below it cannot hold that leaf. One workgroup per job walks that
+// order depth-first over nodes whose exact sum is >= target, one child per
+// wave, and stops at the first leaf whose sum is the target.
+__global__ void __launch_bounds__(256)
+fast2d_walk(const SubmapDesc* __restrict__ submaps, const PairDesc* __restrict__ pairs,
+            const float* __restrict__ points, const float2* __restrict__ rot_table,
+            const WalkJob2* __restrict__ jobs, const int4* __restrict__ top,
+            const int4* __restrict__ bounds, int4* __restrict__ out, int npad) {
+  extern __shared__ __align__(16) uint32_t cells[];
+  __shared__ int4 stk[kWalkStack];
+  __shared__ int sp;
+  __shared__ int csum[4];
+  __shared__ int4 res;
+  const int tid = threadIdx.x, wave = tid >> 6;
+  const WalkJob2 job = jobs[blockIdx.x];
+  const PairDesc pd = pairs[job.pair];
+  const SubmapDesc& sm = submaps[pd.submap];
+  const int target = job.target_sum;
+  if (tid == 0) res = make_int4(0, 0, 0, 0);
+  __syncthreads();
+  int cur_rot = -1;
+  for (int ti = 0; ti < job.top_count; ++ti) {
+    const int4 te = top[job.top_first + ti];  // (rot, x, y, sum), uniform
+    if (job.top_level == 0) {                 // the list holds the leaves
+      if (te.w == target) {
+        if (tid == 0) res = make_int4(te.x, te.y, te.z, 1);
+        break;
+      }
+      continue;
+    }
+    if (te.x != cur_rot) {
+      __syncthreads();  // the previous rotation's readers are done
+      DiscretizeRotation(cells, npad, pd, sm, rot_table[pd.rot_offset + te.x], points);
+      cur_rot = te.x;
+    }
+    const int4 b = bounds[job.bounds_first + te.x];
+    __syncthreads();  // every wave has read the previous walk's empty stack
+    if (tid == 0) {
+      stk[0] = make_int4(job.top_level, te.y, te.z, 0);
+      sp = 1;
+    }
+    for (;;) {
+      __syncthreads();  // cells, the stack and res are visible
+      const int s = sp;
+      if (s == 0 || res.w) break;
+      const int4 nd = stk[s - 1];
+      const int d = nd.x, hw = 1 << (d - 1);
+      // Children in generation order (:353-366).
+      int cxs[4], cys[4], nc = 0;
+      for (int a = 0; a < 2; ++a) {
+        const int xo = nd.y + a * hw;
+        if (xo > b.y) break;
+        for (int c = 0; c < 2; ++c) {
+          const int yo = nd.z + c * hw;
+          if (yo > b.w) break;
+          cxs[nc] = xo;
+          cys[nc] = yo;
+          ++nc;
+        }
+      }
+      int mx = 0, my = 0;
+      for (int c = 0; c < 4; ++c)
+        if (c == wave && c < nc) { mx = cxs[c]; my = cys[c]; }
+      if (wave < nc) {
+        const int sum = ScoreOne(cells, npad, MakeView(sm, d - 1), mx, my);
+        if ((tid & 63) == 0) csum[wave] = sum;
+      }
+      __syncthreads();
+      if (tid == 0) {
+        // Stable descending order by score (std::sort on <= 16 elements is
+        // libstdc++'s insertion sort).
+        int ord[4];
+        float sc[4];
+        for (int c = 0; c < nc; ++c) {
+          ord[c] = c;
+          sc[c] = SumToScoreDev(csum[c], pd.num_points, job.min_s, job.max_s);
+        }
+        for (int i = 1; i < nc; ++i) {
+          const int k = ord[i];
+          int j = i - 1;
+          while (j >= 0 && sc[k] > sc[ord[j]]) {
+            ord[j + 1] = ord[j];
+            --j;
+          }
+          ord[j + 1] = k;
+        }
+        int top_sp = s - 1;
+        if (d == 1) {  // leaves: BranchAndBound(depth 0) returns the first (:339-341)
+          if (nc > 0 && csum[ord[0]] == target) res = make_int4(te.x, cxs[ord[0]], cys[ord[0]], 1);
+        } else {
+          for (int i = nc - 1; i >= 0; --i)
+            if (csum[ord[i]] >= target && top_sp < kWalkStack)
+              stk[top_sp++] = make_int4(d - 1, cxs[ord[i]], cys[ord[i]], 0);
+        }
+        sp = top_sp;
+      }
+    }
+    if (res.w) break;
+  }
+  __syncthreads();
+  if (tid == 0) out[blockIdx.x] = res;
 }
 
 // ShrinkToFit bounds (correlative_scan_matcher_2d.cc:73-91) of one (pair,
@@ -1788,6 +1914,14 @@ hipError_t LaunchFast2dScoreQueries(int num_jobs, int npad, hipStream_t st, cons
                                     const int4* queries, int32_t* sums) {
   hipLaunchKernelGGL(fast2d_score_queries, dim3(num_jobs), dim3(256), sizeof(uint32_t) * npad, st,
                      submaps, pairs, points, rot_table, jobs, queries, sums, npad);
+  return hipGetLastError();
+}
+
+hipError_t LaunchFast2dWalk(int num_jobs, int npad, hipStream_t st, const SubmapDesc* submaps,
+                            const PairDesc* pairs, const float* points, const float2* rot_table,
+                            const WalkJob2* jobs, const int4* top, const int4* bounds, int4* out) {
+  hipLaunchKernelGGL(fast2d_walk, dim3(num_jobs), dim3(256), sizeof(uint32_t) * npad, st, submaps,
+                     pairs, points, rot_table, jobs, top, bounds, out, npad);
   return hipGetLastError();
 }
 

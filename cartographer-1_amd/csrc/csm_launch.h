@@ -29,6 +29,11 @@ hipError_t LaunchFast2dScoreQueries(int num_jobs, int npad, hipStream_t st, cons
                                     const PairDesc* pairs, const float* points,
                                     const float2* rot_table, const ScoreJob* jobs,
                                     const int4* queries, int32_t* sums);
+// Ordered walks to the reference's pick among tied maxima (ResolveTies):
+// out[j] = (rot, x, y, found).
+hipError_t LaunchFast2dWalk(int num_jobs, int npad, hipStream_t st, const SubmapDesc* submaps,
+                            const PairDesc* pairs, const float* points, const float2* rot_table,
+                            const WalkJob2* jobs, const int4* top, const int4* bounds, int4* out);
 // ShrinkToFit bounds of (pair, rotation) jobs (ResolveTies).
 hipError_t LaunchFast2dRotationBounds(int num_jobs, hipStream_t st, const SubmapDesc* submaps,
                                       const PairDesc* pairs, const float* points,

@@ -1373,8 +1373,8 @@ int ResolveTies3d(csm_context* ctx, csm_fast3d* const* submaps, const std::vecto
     const Pair3Desc& d = pdesc[dp];
     const int cnt = counts[t];
     if (stat2[dp] < 0 || cnt < 2 || cnt > kTieCap3d) {
-      ctx->t.ties_unresolved_3d += 1;
-      (*code)[dp] = CSM_TIE_UNRESOLVED;
+      ctx->t.ties_walked_3d += 1;
+      (*code)[dp] = CSM_TIE_WALK;
       continue;
     }
     const int D = submaps[d.submap]->desc.num_levels - 1;

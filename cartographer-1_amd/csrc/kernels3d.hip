@@ -1665,7 +1665,11 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
                       (hi & id_mask) != (~cur & id_mask);
           }
           __syncthreads();
-          if (sh.skip) continue;
+          // Every wave takes its copy before thread 0 may rewrite the flag
+          // for the next leaf.
+          const int skip = sh.skip;
+          __syncthreads();
+          if (skip) continue;
         }
         const float rf = res;
         const float tx = __fadd_rn(yw.tx, __fmul_rn(rf, static_cast<float>(sh.leaf_x[a])));

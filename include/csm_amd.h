@@ -109,17 +109,18 @@ typedef struct csm_timing {
   int64_t stack_high_water;
   /* 2D searches whose maximum was reached by more than one leaf (the
    * reference's pick among them is restored, DESIGN.md §2 "Ties"), and those
-   * left at the smallest (rotation, x, y) leaf because more than 4096 leaves
-   * tied (counted whether or not timing is enabled). */
+   * of them picked by walking the reference's order on the device because
+   * more than 4096 leaves tied (CSM_TIE_WALK; counted whether or not timing
+   * is enabled). */
   int64_t tied_pairs;
-  int64_t ties_unresolved;
+  int64_t ties_walked;
   /* Pairs (2D and 3D) whose pick needed the whole lowest-resolution list
    * ordered (CSM_TIE_TOPLIST). 3D: pairs whose best sum was reached by more
-   * than one leaf passing the low-resolution check, and those left at the
-   * smallest (yaw, x, y, z) leaf (more than 4096 such leaves). */
+   * than one leaf passing the low-resolution check, and those of them picked
+   * by the ordered walk (more than 4096 such leaves). */
   int64_t ties_toplist;
   int64_t tied_pairs_3d;
-  int64_t ties_unresolved_3d;
+  int64_t ties_walked_3d;
 } csm_timing;
 void csm_context_enable_timing(csm_context* ctx, int32_t enable);
 void csm_context_get_timing(csm_context* ctx, csm_timing* out);
@@ -208,12 +209,15 @@ typedef struct csm_pair2d {
  *   TOPLIST    two distinct lowest-resolution candidates share the highest
  *              score: the pair's whole lowest-resolution list was scored and
  *              ordered with std::sort's introsort to find the first;
- *   UNRESOLVED more than 4096 tied leaves: the smallest (rotation, x, y) leaf
- *              is returned (same score; never seen in any test or bench). */
+ *   WALK       more tied leaves than the collect pass records (4096): the
+ *              device walks the reference's visiting order itself, from the
+ *              sorted lowest-resolution list down to the first leaf at the
+ *              maximum (any number of tied leaves).
+ * Every branch returns the reference's leaf; none falls back to another. */
 #define CSM_TIE_NONE 0
 #define CSM_TIE_ANCESTORS 1
 #define CSM_TIE_TOPLIST 2
-#define CSM_TIE_UNRESOLVED 3
+#define CSM_TIE_WALK 3
 
 typedef struct csm_result2d {
   int32_t status;      /* CSM_OK, CSM_NO_MATCH or a negative error */
