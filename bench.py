@@ -45,6 +45,10 @@ def load_pkg():
     return ge._load_package()
 
 
+# Rank 0's gathered constraint records per workload (--dump-records).
+DUMP = {}
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -61,7 +65,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=20.0)
     p.add_argument("--cpu-threads", type=int, default=0)
     p.add_argument("--no-cpu", action="store_true")
-    p.add_argument("--no-rt", action="store_true", help="skip the secondary 2D legs")
+    p.add_argument("--no-rt", action="store_true",
+                   help="skip the secondary legs (C2, C2 strict, C1, C4); C5 runs unless --no-3d")
     p.add_argument("--seed", type=int, default=20250127)
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
     p.add_argument("--no-3d", action="store_true")
@@ -81,6 +86,12 @@ def parse():
     p.add_argument("--c3-tie-log", default="",
                    help="write the C3 queue's exactly tied pairs (submap, node, branch) to "
                         "<path>.rank<r>.json (input of tools/c3_tie_fixture.py)")
+    p.add_argument("--comm-backend", default="auto", choices=["auto", "rccl", "tcp"],
+                   help="csm_comm transport at N > 1 (auto: RCCL with --dist-backend nccl, TCP "
+                        "with gloo); rccl with gloo rehearses the RCCL branch on one GPU against "
+                        "a library named by CSM_RCCL_LIB (tests/test_bench_multirank_gpu.py)")
+    p.add_argument("--dump-records", default="",
+                   help="rank 0 writes the gathered C3 and C5 constraint records to this .npz")
     p.add_argument("--cpu-pairs", type=int, default=0,
                    help="CPU baseline sample size (0: 2000 for C3, sized to --cpu-seconds for C2)")
     return p.parse_args()
@@ -145,7 +156,7 @@ def main():
                                                     "errors_per_step")}
             out["c2_strict"]["kernel_ms"] = c2s["roofline"]["kernel_ms_avg"]
         out["rt2d"] = rt2d_bench(csm, ctx, args)
-    if rank == 0 and world_size == 1 and not args.no_3d:
+    if rank == 0 and world_size == 1 and not args.no_3d and not args.no_rt:
         out["rt3d"] = rt3d_bench(csm, ctx, args)
     if not args.no_3d:  # collective over ranks: the C5 sweep, submap-sharded
         f3 = fast3d_bench(csm, ctx, args, rank, world_size, dist, coll_dev, barrier_sync, cdist,
@@ -154,15 +165,19 @@ def main():
             out["fast3d"] = f3
     if rank == 0:
         print(json.dumps(out), flush=True)
+        if args.dump_records:
+            np.savez(args.dump_records, **DUMP)
     if dist is not None:
         dist.barrier()
     if comm is not None:
         comm.close()
     if dist is not None:
         dist.destroy_process_group()
-    failed = errors + (out.get("fast3d", {}).get("errors_per_step", 0) if rank == 0 else 0)
+    f3 = out.get("fast3d", {}) if rank == 0 else {}
+    failed = errors + f3.get("errors_per_step", 0) + f3.get("parity_failures", 0)
     if failed:
-        print(f"bench: {failed} pair searches returned an error status", file=sys.stderr)
+        print(f"bench: {failed} pair searches returned an error status or differ from the oracle "
+              "in a parity sample", file=sys.stderr)
         sys.exit(3)
 
 
@@ -355,7 +370,8 @@ def make_comm_checked(csm, ctx, args, rank, world_size, dist, coll_dev):
     import torch
     from torch.distributed import distributed_c10d
     store = distributed_c10d._get_default_store()
-    backend = "rccl" if args.dist_backend == "nccl" else "tcp"
+    backend = args.comm_backend if args.comm_backend != "auto" else \
+        ("rccl" if args.dist_backend == "nccl" else "tcp")
     base = int(os.environ.get("MASTER_PORT", "29500"))
     comm, err = None, None
     try:
@@ -444,16 +460,13 @@ def rt2d_bench(csm, ctx, args):
            "gpu_ms_per_scan_match_median_grid_changed": 1e3 * float(np.median(times_changed)),
            "kernel_ms_per_scan_match": kernel_ms,
            "points": len(cloud)}
-    try:
-        sys.path.insert(0, os.path.join(ROOT, "tests"))
-        import oracle_lib
-        o = oracle_lib.Oracle()
-        cpu_s = o.rt2d_time((g.resolution, g.max_x, g.max_y), g.cells,
-                            (0.2, math.radians(10.0), 0.1, 0.1), init, cloud, 20)
-        res["cpu_ms_per_scan_match"] = cpu_s * 1e3
-        res["cpu_threads"] = 1
-    except OSError:
-        pass
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib
+    o = oracle_lib.Oracle()
+    cpu_s = o.rt2d_time((g.resolution, g.max_x, g.max_y), g.cells,
+                        (0.2, math.radians(10.0), 0.1, 0.1), init, cloud, 20)
+    res["cpu_ms_per_scan_match"] = cpu_s * 1e3
+    res["cpu_threads"] = 1
     return res
 
 
@@ -566,8 +579,8 @@ def voxel_filter_bench(csm, ctx, world, args):
         res["cpu_clouds_per_s"] = len(clouds) / cpu_s
         res["cpu_threads"] = 1
         res["matches_oracle"] = bool((ref == keep).all())
-    except OSError:
-        pass
+    except OSError as e:  # the checker must be there: fail loudly
+        raise RuntimeError(f"oracle (CPU baseline) unavailable: {e}") from e
     return res
 
 
@@ -604,8 +617,8 @@ def ceres_bench(csm, ctx, world, matchers, scans, pairs, res, my_submaps, node_i
         out["cpu_baseline"] = {"value": 1.0 / cpu_s, "unit": "refinements/s", "cores": 1,
                                "kind": "port", "sample": f"{k} of the accepted matches (oracle "
                                                          "restatement, includes grid copy-in)"}
-    except OSError:
-        pass
+    except OSError as e:  # the checker must be there: fail loudly
+        raise RuntimeError(f"oracle (CPU baseline) unavailable: {e}") from e
     return out
 
 
@@ -673,8 +686,8 @@ def rt3d_bench(csm, ctx, args):
                 "kind": "port",
                 "sample": f"{sample} candidates spread over the {total} of one match, "
                           f"{sec:.2f} s, extrapolated to all candidates (oracle, -O3)"}
-        except OSError:
-            pass
+        except OSError as e:  # the checker must be there: fail loudly
+            raise RuntimeError(f"oracle (CPU baseline) unavailable: {e}") from e
     return res
 
 
@@ -767,6 +780,8 @@ def fast3d_bench(csm, ctx, args, rank=0, world_size=1, dist=None, coll_dev=None,
             close(*kept)
             phase["release"] += time.perf_counter() - t0
     grids, mats = kept
+    if rank == 0 and rec is not None:
+        DUMP["c5"] = np.asarray(rec)
     tm = ctx.timing()
     ctx.enable_timing(False)
     if cdist is not None:
@@ -813,61 +828,64 @@ def fast3d_bench(csm, ctx, args, rank=0, world_size=1, dist=None, coll_dev=None,
                           "workload": "CeresScanMatcher3D::Match on one C5 step's accepted "
                                       "matches (pose_graph.lua options)"}
     if not args.no_cpu:
-        try:
-            sys.path.insert(0, os.path.join(ROOT, "tests"))
-            import ctypes as C
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import ctypes as C
 
-            import oracle_lib
-            orc = oracle_lib.Oracle()
-            opt = (o.branch_and_bound_depth, o.full_resolution_depth, o.min_rotational_score,
-                   o.min_low_resolution_score, o.linear_xy_search_window,
-                   o.linear_z_search_window, o.angular_search_window)
-            keep = []
-            handles = []
-            for s in range(w.num_submaps):
-                oh, ol = orc.hybrid_grid(w.high_resolution), orc.hybrid_grid(w.low_resolution)
-                oh.set_values(*w.high_cells[s])
-                ol.set_values(*w.low_cells[s])
-                om = orc.fast3d(oh, ol, w.submap_hist[s], opt)
-                keep.append((oh, ol, om))
-                handles.append(om.h)
-            hoff = np.zeros(w.num_nodes + 1, np.int64)
-            hoff[1:] = np.cumsum([len(x) for x in w.high])
-            loff = np.zeros(w.num_nodes + 1, np.int64)
-            loff[1:] = np.cumsum([len(x) for x in w.low])
-            high = np.ascontiguousarray(np.concatenate(w.high), np.float32)
-            low = np.ascontiguousarray(np.concatenate(w.low), np.float32)
-            hists = np.ascontiguousarray(np.stack(w.node_hist), np.float32)
-            nq = np.ascontiguousarray([w.node_rotation(i) for i in range(w.num_nodes)], np.float64)
-            cpu = host_cpu()
-            threads = args.cpu_threads or cpu["usable_cpus"]
-            rng = np.random.RandomState(777)
-            P = C.POINTER
-            hv = (C.c_void_p * len(handles))(*handles)
+        import oracle_lib
+        orc = oracle_lib.Oracle()
+        opt = (o.branch_and_bound_depth, o.full_resolution_depth, o.min_rotational_score,
+               o.min_low_resolution_score, o.linear_xy_search_window,
+               o.linear_z_search_window, o.angular_search_window)
+        keep = []
+        handles = []
+        for s in range(w.num_submaps):
+            oh, ol = orc.hybrid_grid(w.high_resolution), orc.hybrid_grid(w.low_resolution)
+            oh.set_values(*w.high_cells[s])
+            ol.set_values(*w.low_cells[s])
+            om = orc.fast3d(oh, ol, w.submap_hist[s], opt)
+            keep.append((oh, ol, om))
+            handles.append(om.h)
+        hoff = np.zeros(w.num_nodes + 1, np.int64)
+        hoff[1:] = np.cumsum([len(x) for x in w.high])
+        loff = np.zeros(w.num_nodes + 1, np.int64)
+        loff[1:] = np.cumsum([len(x) for x in w.low])
+        high = np.ascontiguousarray(np.concatenate(w.high), np.float32)
+        low = np.ascontiguousarray(np.concatenate(w.low), np.float32)
+        hists = np.ascontiguousarray(np.stack(w.node_hist), np.float32)
+        nq = np.ascontiguousarray([w.node_rotation(i) for i in range(w.num_nodes)], np.float64)
+        cpu = host_cpu()
+        threads = args.cpu_threads or cpu["usable_cpus"]
+        rng = np.random.RandomState(777)
+        P = C.POINTER
+        hv = (C.c_void_p * len(handles))(*handles)
 
-            def run(k):
-                ps = rng.randint(0, w.num_submaps, k).astype(np.int32)
-                pn = rng.randint(0, w.num_nodes, k).astype(np.int32)
-                matched = np.zeros(k, np.int32)
-                task = np.zeros(k)
-                wall = orc.lib.oracle_fast3d_match_pairs(
-                    hv, high.ctypes.data_as(P(C.c_float)), hoff.ctypes.data_as(P(C.c_int64)),
-                    low.ctypes.data_as(P(C.c_float)), loff.ctypes.data_as(P(C.c_int64)),
-                    hists.ctypes.data_as(P(C.c_float)), hists.shape[1],
-                    nq.ctypes.data_as(P(C.c_double)), ps.ctypes.data_as(P(C.c_int32)),
-                    pn.ctypes.data_as(P(C.c_int32)), k, threads, 0.6,
-                    matched.ctypes.data_as(P(C.c_int32)), task.ctypes.data_as(P(C.c_double)))
-                return wall, task
+        def run(k):
+            ps = rng.randint(0, w.num_submaps, k).astype(np.int32)
+            pn = rng.randint(0, w.num_nodes, k).astype(np.int32)
+            matched = np.zeros(k, np.int32)
+            results = np.zeros((k, 14))
+            task = np.zeros(k)
+            wall = orc.lib.oracle_fast3d_match_pairs(
+                hv, high.ctypes.data_as(P(C.c_float)), hoff.ctypes.data_as(P(C.c_int64)),
+                low.ctypes.data_as(P(C.c_float)), loff.ctypes.data_as(P(C.c_int64)),
+                hists.ctypes.data_as(P(C.c_float)), hists.shape[1],
+                nq.ctypes.data_as(P(C.c_double)), ps.ctypes.data_as(P(C.c_int32)),
+                pn.ctypes.data_as(P(C.c_int32)), k, threads, 0.6,
+                matched.ctypes.data_as(P(C.c_int32)), results.ctypes.data_as(P(C.c_double)),
+                task.ctypes.data_as(P(C.c_double)))
+            return wall, task, (ps, pn, results)
 
-            probe, _ = run(threads)
-            k = min(20000, max(threads, int(threads * 10.0 / max(probe, 1e-3))))
-            sec, task = run(k)
-            cb = summarize_cpu(k, sec, task, threads, cpu, [], "uniformly sampled pairs of the same queue")
-            cb["sample"] = (f"{k} uniformly sampled pairs of the same queue, {sec:.1f} s on "
-                            f"{threads} threads (oracle, -O3)")
-            out["cpu_baseline"] = cb
-        except OSError:
-            pass
+        probe, _, _ = run(threads)
+        k = min(20000, max(threads, int(threads * 10.0 / max(probe, 1e-3))))
+        sec, task, sampled = run(k)
+        cb = summarize_cpu(k, sec, task, threads, cpu, [], "uniformly sampled pairs of the same queue")
+        cb["sample"] = (f"{k} uniformly sampled pairs of the same queue, {sec:.1f} s on "
+                        f"{threads} threads (oracle, -O3)")
+        out["cpu_baseline"] = cb
+        # The same pairs' GPU results from the last timed step, against
+        # the oracle's (fast_correlative_scan_matcher_3d.cc:148-199).
+        out["parity_sample"] = parity_3d(res3, sampled, w.num_nodes)
+        out["parity_failures"] = parity_failures(out["parity_sample"])
     return out
 
 
@@ -879,7 +897,7 @@ def cpu_baseline(world, my_submaps, args):
     k = 100000
     ps = np.asarray(my_submaps)[rng.randint(0, len(my_submaps), k)]
     pn = rng.randint(0, world.num_nodes, k)
-    return cpu_pairs_2d(world, ps, pn, args, "uniformly sampled (submap, scan) pairs of the same C2 queue")
+    return cpu_pairs_2d(world, ps, pn, args, "uniformly sampled (submap, scan) pairs of the same C2 queue")[0]
 
 
 def host_cpu():
@@ -892,8 +910,8 @@ def host_cpu():
             if line.startswith("model name"):
                 info["model"] = line.split(":", 1)[1].strip()
                 break
-    except OSError:
-        pass
+    except OSError as e:  # the checker must be there: fail loudly
+        raise RuntimeError(f"oracle (CPU baseline) unavailable: {e}") from e
     try:
         info["affinity_cpus"] = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
@@ -974,6 +992,11 @@ def cpu_pairs_2d(world, pair_sub, pair_node, args, what):
     offs = np.ascontiguousarray(world.offsets, np.int64)
     P = C.POINTER
     cursor = [0]
+    # The oracle's result for every sample index it ran (probes and the main
+    # run): the bench's parity check against the GPU's results of the same
+    # pairs (c3_run).
+    ores = {"done": np.zeros(len(inv), bool), "matched": np.zeros(len(inv), bool),
+            "score": np.zeros(len(inv), np.float32), "pose": np.zeros((len(inv), 3))}
 
     def run(k, threads):
         # Consecutive slices of the (shuffled) sample: probes and the main
@@ -996,6 +1019,10 @@ def cpu_pairs_2d(world, pair_sub, pair_node, args, what):
                 poses.ctypes.data_as(P(C.c_double)), matched.ctypes.data_as(P(C.c_int32)),
                 task.ctypes.data_as(P(C.c_double)))
             tasks.append(task)
+            ores["done"][idx] = True
+            ores["matched"][idx] = matched != 0
+            ores["score"][idx] = scores
+            ores["pose"][idx] = poses.reshape(-1, 3)
             done += kk
             if k > 64 * threads:
                 print(f"cpu baseline: {done}/{k} pairs, {time.time() - t0:.0f} s", file=sys.stderr,
@@ -1010,7 +1037,57 @@ def cpu_pairs_2d(world, pair_sub, pair_node, args, what):
     (threads, rate), probes = timed_pool(run, options)
     k = args.cpu_pairs or max(4 * threads, int(rate * args.cpu_seconds))
     wall, task = run(k, threads)
-    return summarize_cpu(k, wall, task, threads, cpu, probes, what)
+    return summarize_cpu(k, wall, task, threads, cpu, probes, what), ores
+
+
+def parity_2d(sample, ores):
+    """The GPU's results of the sampled pairs (from the timed run) against the
+    oracle's MatchFullSubmap of the same pairs: the match decision, the score
+    (bit-identical float) and the pose (identical doubles, the reference's pick
+    among exact ties included; fast_correlative_scan_matcher_2d.cc:210-262)."""
+    both = sample["have"] & ores["done"]
+    g = sample["gpu"][both]
+    gm = g["status"] == 0
+    om = ores["matched"][both]
+    dec = gm != om
+    ok = gm & om
+    gpose = np.stack([g["x"], g["y"], g["theta"]], 1)
+    score_bad = ok & (g["score"].astype(np.float32) != ores["score"][both])
+    pose_bad = ok & np.any(gpose != ores["pose"][both], axis=1)
+    return {"pairs": int(len(both)), "compared": int(both.sum()), "matched_oracle": int(om.sum()),
+            "mismatched_decision": int(dec.sum()), "mismatched_score": int(score_bad.sum()),
+            "mismatched_pose": int(pose_bad.sum()), "gpu_errors": int((g["status"] < 0).sum()),
+            "what": "the CPU baseline's sampled pairs: the GPU's results from the timed run vs the "
+                    "oracle's (decision, float score bit-exact, pose exact)"}
+
+
+def parity_3d(res3, sampled, num_nodes):
+    """C5's CPU sample: the GPU's MatchFullSubmap results of the sampled pairs
+    (pair index = submap x nodes + node, the last timed step) against the
+    oracle's: decision, score, rotational and low-resolution scores
+    (bit-identical floats) and pose (identical, ties included)."""
+    ps, pn, o = sampled
+    g = res3[ps.astype(np.int64) * num_nodes + pn]
+    gm = g["status"] == 0
+    om = o[:, 0] != 0
+    ok = gm & om
+    score_bad = ok & ((g["score"].astype(np.float32) != o[:, 1].astype(np.float32)) |
+                      (g["rotational_score"].astype(np.float32) != o[:, 2].astype(np.float32)) |
+                      (g["low_resolution_score"].astype(np.float32) != o[:, 3].astype(np.float32)))
+    gpose = np.concatenate([np.asarray(g["t"], np.float64), np.asarray(g["q"], np.float64)], 1)
+    pose_bad = ok & np.any(gpose != o[:, 4:11], axis=1)
+    return {"pairs": int(len(ps)), "compared": int(len(ps)), "matched_oracle": int(om.sum()),
+            "mismatched_decision": int((gm != om).sum()), "mismatched_score": int(score_bad.sum()),
+            "mismatched_pose": int(pose_bad.sum()), "gpu_errors": int((g["status"] < 0).sum()),
+            "what": "the CPU baseline's sampled pairs: the GPU's results from the last timed step vs "
+                    "the oracle's (decision, float scores bit-exact, pose exact)"}
+
+
+def parity_failures(p):
+    """Pairs of a parity sample that differ from the oracle, plus any sampled
+    pair the GPU did not return (the check must cover the whole sample)."""
+    return (p["mismatched_decision"] + p["mismatched_score"] + p["mismatched_pose"] +
+            p["gpu_errors"] + (p["pairs"] - p["compared"]))
 
 
 def c3_run(csm, ctx, args, rank, world_size, dist, coll_dev, comm, gather, transport,
@@ -1080,6 +1157,21 @@ def c3_run(csm, ctx, args, rank, world_size, dist, coll_dev, comm, gather, trans
             return comm.fetch_add(key, 1)
     claim.local = {}
 
+    # The CPU baseline's sample of the queue, drawn up front: the timed run
+    # keeps the GPU's result of each sampled pair, which is then compared with
+    # the oracle's result of the same pair (parity_sample; rank 0 at N = 1).
+    sample = None
+    if rank == 0 and world_size == 1 and not args.no_cpu:
+        rng = np.random.RandomState(12345)
+        k_s = args.cpu_pairs or 2000
+        # Submaps of the timed queue (all of them when it covers the queue).
+        s_sub = np.unique(queue)[rng.randint(0, len(np.unique(queue)), k_s)]
+        s_node = rng.randint(0, N, k_s)
+        want = {}
+        for i, (a, b) in enumerate(zip(s_sub, s_node)):
+            want.setdefault(int(a), []).append((i, int(b)))
+        sample = {"sub": s_sub, "node": s_node, "want": want,
+                  "gpu": np.zeros(k_s, csm.RESULT_DTYPE), "have": np.zeros(k_s, bool)}
     for w in range(args.warmup):  # one chunk each: module load, staging buffers
         for i in range(len(ctxs)):
             run_chunk(chunks[(rank + w) % n_chunks], 0, i)
@@ -1097,6 +1189,11 @@ def c3_run(csm, ctx, args, rank, world_size, dist, coll_dev, comm, gather, trans
                 return
             res, rec = run_chunk(chunks[c], np.int64(c) * K * N, w)
             tied = np.nonzero((res["status"] == 0) & (res["tie"] != 0))[0]
+            if sample is not None:
+                for j, sm in enumerate(chunks[c]):
+                    for i, n in sample["want"].get(int(sm), ()):
+                        sample["gpu"][i] = res[j * N + n]
+                        sample["have"][i] = True
             with claim_lock:
                 done["errors"] += int((res["status"] < 0).sum())
                 done["recs"].append(rec)
@@ -1129,6 +1226,8 @@ def c3_run(csm, ctx, args, rank, world_size, dist, coll_dev, comm, gather, trans
     tm = sum_timing(csm, [c.timing() for c in ctxs])
     lv_cands, lv_batches = (list(map(sum, zip(*v))) for v in zip(*[c.level_stats() for c in ctxs]))
     accepted = len(allrec) if rank == 0 else 0
+    if rank == 0:
+        DUMP["c3"] = np.asarray(allrec)
     elapsed = cdist.max_over_ranks(elapsed, dist, coll_dev)
     errors = int(cdist.sum_over_ranks(errors, dist, coll_dev))
     total_pairs = len(queue) * N
@@ -1180,16 +1279,18 @@ def c3_run(csm, ctx, args, rank, world_size, dist, coll_dev, comm, gather, trans
         with open(f"{args.c3_tie_log}.rank{rank}.json", "w") as f:
             json.dump({"seed": args.seed, "nodes": N, "submaps": S, "min_score": args.min_score,
                        "ties": sorted(done["ties"])}, f)
-    if rank == 0 and world_size == 1 and not args.no_cpu:
-        rng = np.random.RandomState(12345)
-        k = args.cpu_pairs or 2000
+    if sample is not None:
         args_c = argparse.Namespace(**vars(args))
-        args_c.cpu_pairs = k
-        ps = rng.randint(0, S, k)
-        pn = rng.randint(0, N, k)
-        out["cpu_baseline"] = cpu_pairs_2d(world, ps, pn, args_c,
-                                           "uniformly sampled (submap, node) pairs of the C3 queue")
+        args_c.cpu_pairs = len(sample["sub"])
+        out["cpu_baseline"], ores = cpu_pairs_2d(world, sample["sub"], sample["node"], args_c,
+                                                 "uniformly sampled (submap, node) pairs of the C3 queue")
         out["speedup_vs_cpu"] = out["value"] / out["cpu_baseline"]["value"]
+        out["parity_sample"] = parity_2d(sample, ores)
+        bad = parity_failures(out["parity_sample"])
+        if bad:
+            print(f"bench: C3 parity sample: {bad} of {out['parity_sample']['compared']} pairs differ "
+                  "from the oracle", file=sys.stderr, flush=True)
+            errors += bad
     for sc, c in zip(scan_sets, ctxs):
         sc.close()
         if c is not ctx:

@@ -20,6 +20,7 @@ constexpr int kTopCells3d = 512;          // distinct top-level cells of a cloud
 constexpr int kBatch3d = 16;              // DFS nodes scored per step (16 lanes each)
 constexpr int kMax3dTop = 1 << 20;        // top-level candidates per yaw
 constexpr int kTieCap3d = 4096;           // tied leaves recorded per pair (collect search)
+constexpr int kWalkStack3d = 128;         // ordered-walk stack: 1 + 7 x depth entries at most
 constexpr int kStack3d = 1024;            // DFS stack entries per workgroup in LDS
 constexpr int kSpill3d = 3072;            // further entries per workgroup in global memory
 constexpr int kStat3dHighWater = 14;      // stats word: DFS stack high-water (max over workgroups)
@@ -105,6 +106,17 @@ struct Pair3Desc {
   // Tie resolution (host3d.cc ResolveTies3d): a collect search records every
   // leaf that passes the low-resolution check with sum == collect_sum.
   int32_t collect, collect_sum;
+};
+
+// Ordered walk (host3d.cc ResolveTies3d, pairs whose passing tied leaves
+// overflow the collect record; kernels3d.hip fast3d_walk).
+struct Walk3Job {
+  int32_t pair;        // device pair index
+  int32_t target_sum;  // the pair's best passing leaf sum
+  int32_t top_level;   // max_depth
+  int32_t top_first;   // sorted lowest-resolution entries (yaw, x | y << 16, z, sum), sum >= target
+  int32_t top_count;
+  int32_t pad[3];
 };
 
 // One discrete scan (yaw) of a pair: the pose the cloud is discretized with,

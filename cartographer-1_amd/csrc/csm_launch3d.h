@@ -90,6 +90,12 @@ hipError_t LaunchFast3dScoreQueries(int num_jobs, hipStream_t st, const Submap3D
                                     const Pair3Desc* pairs, const Yaw3Desc* yaws,
                                     const float* points, const Score3Job* jobs,
                                     const int4* queries, int32_t* sums);
+// Ordered walks to the reference's pick among tied maxima (ResolveTies3d):
+// out[2 j] = (yaw, x, y, z), out[2 j + 1].x = found.
+hipError_t LaunchFast3dWalk(int num_jobs, hipStream_t st, const Submap3Desc* submaps,
+                            const Pair3Desc* pairs, const Yaw3Desc* yaws, const float* points,
+                            const float* low_points, const Walk3Job* jobs, const int4* top,
+                            int4* out);
 hipError_t LaunchFast3dFinalize(int num_pairs, hipStream_t st, const Submap3Desc* submaps,
                                 const Pair3Desc* pairs, const Yaw3Desc* yaws,
                                 const float* low_points, const unsigned long long* best,

@@ -1269,9 +1269,10 @@ uint64_t LeafId3(const Pair3Desc& d, int yaw, int x, int y, int z) {  // kernels
 // (parallel_sort.h). No oracle and no CPU scoring is involved. `code` gets
 // CSM_TIE_* per device pair.
 int ResolveTies3d(csm_context* ctx, csm_fast3d* const* submaps, const std::vector<Pair3Desc>& pdesc,
-                  const std::vector<int32_t>& stat, const std::vector<unsigned long long>& keys_hi,
+                  std::vector<int32_t>* stat_io, const std::vector<unsigned long long>& keys_hi,
                   std::vector<unsigned long long>* keys, std::vector<int8_t>* code) {
   const int np = static_cast<int>(pdesc.size());
+  const std::vector<int32_t>& stat = *stat_io;
   std::vector<int> tied;
   for (int dp = 0; dp < np; ++dp) {
     const unsigned long long key = (*keys)[dp];
@@ -1368,13 +1369,17 @@ int ResolveTies3d(csm_context* ctx, csm_fast3d* const* submaps, const std::vecto
   std::vector<Score3Job> jobs;
   std::vector<int4> queries;
   std::vector<int> leaf_query;  // per leaf: index of its depth-1 ancestor query
+  std::vector<int> walk;        // tied pairs (device index) whose leaves overflow the record
   for (int t = 0; t < nt; ++t) {
     const int dp = tied[t];
     const Pair3Desc& d = pdesc[dp];
     const int cnt = counts[t];
     if (stat2[dp] < 0 || cnt < 2 || cnt > kTieCap3d) {
+      // More passing tied leaves than the collect pass records (or its
+      // stack overflowed): the device walks the reference's order (5).
       ctx->t.ties_walked_3d += 1;
       (*code)[dp] = CSM_TIE_WALK;
+      walk.push_back(dp);
       continue;
     }
     const int D = submaps[d.submap]->desc.num_levels - 1;
@@ -1535,6 +1540,91 @@ int ResolveTies3d(csm_context* ctx, csm_fast3d* const* submaps, const std::vecto
     const unsigned long long sum = (*keys)[w.dp] >> d.key_shift;
     (*keys)[w.dp] = (sum << d.key_shift) |
                     (~LeafId3(d, lv[best].x, lv[best].y, lv[best].z, lv[best].w) & mask);
+  }
+  // (5) Pairs whose passing tied leaves overflow the record: the whole
+  // lowest-resolution list scored and sorted as in (3), and the device walks
+  // the reference's visiting order from it (fast3d_walk); only entries whose
+  // sum reaches the maximum can lead to the pick.
+  if (!walk.empty()) {
+    std::vector<Score3Job> tj;
+    std::vector<int4> tq;
+    std::vector<int64_t> base(walk.size());
+    std::vector<int> wD(walk.size());
+    for (size_t k = 0; k < walk.size(); ++k) {
+      const Pair3Desc& d = pdesc[walk[k]];
+      const int D = submaps[d.submap]->desc.num_levels - 1, step = 1 << D;
+      wD[k] = D;
+      base[k] = static_cast<int64_t>(tq.size());
+      for (int j = 0; j < d.num_yaws; ++j) {
+        Score3Job job{d.yaw_begin + j, static_cast<int32_t>(tq.size()), 0, 0};
+        for (int z = -d.wz; z <= d.wz; z += step)  // GenerateLowestResolutionCandidates (:297-330)
+          for (int y = -d.wxy; y <= d.wxy; y += step)
+            for (int x = -d.wxy; x <= d.wxy; x += step) tq.push_back(make_int4(D, x, y, z));
+        job.count = static_cast<int32_t>(tq.size()) - job.first;
+        tj.push_back(job);
+      }
+    }
+    std::vector<int32_t> ts;
+    if ((rc = score(tj, tq, &ts))) return rc;
+    std::vector<Walk3Job> wj;
+    std::vector<int4> wtop;
+    for (size_t k = 0; k < walk.size(); ++k) {
+      const Pair3Desc& d = pdesc[walk[k]];
+      const int64_t n = (k + 1 < walk.size() ? base[k + 1] : static_cast<int64_t>(tq.size())) - base[k];
+      std::vector<std::pair<float, int32_t>> lst(n);
+      for (int64_t i = 0; i < n; ++i)
+        lst[i] = {SumToProbability(ts[base[k] + i], d.num_points), static_cast<int32_t>(i)};
+      IntroSort(lst.data(), lst.data() + n,
+                [](const std::pair<float, int32_t>& a, const std::pair<float, int32_t>& b) {
+                  return a.first > b.first;
+                },
+                8);
+      const int32_t target = static_cast<int32_t>((*keys)[walk[k]] >> d.key_shift);
+      Walk3Job j{walk[k], target, wD[k], static_cast<int32_t>(wtop.size()), 0, {0, 0, 0}};
+      const int per_yaw = static_cast<int>(n / std::max(1, d.num_yaws));
+      for (const auto& e : lst) {
+        const int32_t sum = ts[base[k] + e.second];
+        if (sum < target) continue;
+        const int4 q = tq[base[k] + e.second];
+        const int yaw = e.second / per_yaw;
+        wtop.push_back(make_int4(yaw, (q.y & 0xffff) | (q.z << 16), q.w, sum));
+      }
+      j.top_count = static_cast<int32_t>(wtop.size()) - j.top_first;
+      wj.push_back(j);
+    }
+    const size_t o_top = sizeof(Walk3Job) * wj.size();
+    const size_t o_out = o_top + sizeof(int4) * std::max<size_t>(wtop.size(), 1);
+    const size_t bytes = o_out + 2 * sizeof(int4) * wj.size();
+    if ((rc = ctx->f3_walk_buf.Reserve(bytes))) return rc;
+    char* dw = ctx->f3_walk_buf.as<char>();
+    std::vector<char> hw(o_out);
+    std::memcpy(hw.data(), wj.data(), o_top);
+    if (!wtop.empty()) std::memcpy(hw.data() + o_top, wtop.data(), sizeof(int4) * wtop.size());
+    CSM_HIP(hipMemcpyAsync(dw, hw.data(), o_out, hipMemcpyHostToDevice, st));
+    CSM_HIP(LaunchFast3dWalk(static_cast<int>(wj.size()), st, dsub, dpairs, dyaws,
+                             ctx->f3_points.as<float>(), ctx->f3_low_points.as<float>(),
+                             reinterpret_cast<const Walk3Job*>(dw),
+                             reinterpret_cast<const int4*>(dw + o_top),
+                             reinterpret_cast<int4*>(dw + o_out)));
+    std::vector<int4> found(2 * wj.size());
+    CSM_HIP(hipMemcpyAsync(found.data(), dw + o_out, 2 * sizeof(int4) * wj.size(),
+                           hipMemcpyDeviceToHost, st));
+    CSM_HIP(hipStreamSynchronize(st));
+    for (size_t k = 0; k < walk.size(); ++k) {
+      const int dp = walk[k];
+      const Pair3Desc& d = pdesc[dp];
+      if (!found[2 * k + 1].x) {
+        // Unreachable (the maximum is a passing leaf's sum and the walk visits
+        // every node whose sum reaches it): never return a leaf that is not
+        // the reference's, the pair's result is void.
+        (*stat_io)[dp] = CSM_ERANGE;
+        continue;
+      }
+      const int4 f = found[2 * k];
+      const unsigned long long mask = (1ull << d.key_shift) - 1;
+      const unsigned long long sum = (*keys)[dp] >> d.key_shift;
+      (*keys)[dp] = (sum << d.key_shift) | (~LeafId3(d, f.x, f.y, f.z, f.w) & mask);
+    }
   }
   return CSM_OK;
 }
@@ -1922,7 +2012,7 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
   std::vector<int8_t> tie_code(np, CSM_TIE_NONE);
   {
     const std::vector<unsigned long long> before = keys;
-    if ((rc = ResolveTies3d(ctx, submaps, pdesc, stat, keys_hi, &keys, &tie_code))) return rc;
+    if ((rc = ResolveTies3d(ctx, submaps, pdesc, &stat, keys_hi, &keys, &tie_code))) return rc;
     if (keys != before)
       CSM_HIP(hipMemcpyAsync(dbest, keys.data(), sizeof(unsigned long long) * np,
                              hipMemcpyHostToDevice, st));

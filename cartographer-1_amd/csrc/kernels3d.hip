@@ -1770,6 +1770,211 @@ fast3d_score_queries(const Submap3Desc* __restrict__ submaps, const Pair3Desc* _
   }
 }
 
+// PrecomputationGrid3D::ToProbability(sum / n) (precomputation_grid_3d.h:32-35)
+// with the host's float operations (host3d.cc SumToProbability).
+__device__ __forceinline__ float SumToProbabilityDev(int sum, int n) {
+  const float kMinP = 0.1f, kMaxP = 1.f - kMinP;
+  return __fadd_rn(kMinP, __fmul_rn(__fdiv_rn(static_cast<float>(sum), static_cast<float>(n)),
+                                    __fdiv_rn(__fsub_rn(kMaxP, kMinP), 255.f)));
+}
+
+struct Walk3Shared {
+  int16_t cx[kMax3dPoints], cy[kMax3dPoints], cz[kMax3dPoints];
+  int4 stk[kWalkStack3d];  // (depth, x, y, z)
+  int sp;
+  int csum[8];
+  int4 res;                // (yaw, x, y, z) of the pick
+  int found, pass;
+  float lr[kSearch3dThreads];  // LowResScore's staging
+};
+
+// Ordered walk to the reference's pick among exactly tied maxima, for pairs
+// whose passing tied leaves overflow the collect pass (host3d.cc
+// ResolveTies3d). BranchAndBound (fast_correlative_scan_matcher_3d.cc:377-440)
+// visits the sorted lowest-resolution list in order, each node's <= 8
+// children (z, then y, then x, x fastest; a child past the window ends its
+// loop, :412-430) by descending score with equal scores in generation order
+// (insertion sort), and at depth 0 returns the first child that passes the
+// low-resolution check (:384-401). Until the first passing leaf at the
+// maximum is reached the incumbent is below the maximum, so every node whose
+// sum reaches it is visited; a passing leaf above the maximum does not exist.
+// One workgroup per job walks that order depth-first over nodes whose exact
+// sum is >= target (wave w scores children w and w + 4) and stops at the
+// first child, in order, that reaches the target and passes.
+__global__ void __launch_bounds__(kSearch3dThreads)
+fast3d_walk(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restrict__ pairs,
+            const Yaw3Desc* __restrict__ yaws, const float* __restrict__ points,
+            const float* __restrict__ low_points, const Walk3Job* __restrict__ jobs,
+            const int4* __restrict__ top, int4* __restrict__ out) {
+  // out[2 j] = (yaw, x, y, z) of job j's pick, out[2 j + 1].x = found.
+  __shared__ Walk3Shared sh;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const Walk3Job job = jobs[blockIdx.x];
+  const Pair3Desc pd = pairs[job.pair];
+  const Submap3Desc& sm = submaps[pd.submap];
+  const int n = min(pd.num_points, kMax3dPoints);
+  const int target = job.target_sum;
+  const float res = sm.resolution, inv = 1.f / sm.resolution;
+  if (tid == 0) {
+    sh.res = make_int4(0, 0, 0, 0);
+    sh.found = 0;
+    sh.pass = 0;
+  }
+  int cur_yaw = -1;
+  Yaw3Desc yw{};
+  // Low-resolution check of leaf (x, y, z) of the current yaw (uniform).
+  auto passes = [&](int x, int y, int z) {
+    const float tx = __fadd_rn(yw.tx, __fmul_rn(res, static_cast<float>(x)));
+    const float ty = __fadd_rn(yw.ty, __fmul_rn(res, static_cast<float>(y)));
+    const float tz = __fadd_rn(yw.tz, __fmul_rn(res, static_cast<float>(z)));
+    const float lrs = LowResScore(sh, sm, low_points + 3 * pd.low_offset, pd.num_low, yw.nw, yw.nx,
+                                  yw.ny, yw.nz, tx, ty, tz);
+    if (tid == 0)
+      sh.pass = static_cast<double>(lrs) >= static_cast<double>(pd.min_low_resolution_score);
+    __syncthreads();
+    const int p = sh.pass;
+    __syncthreads();
+    return p != 0;
+  };
+  __syncthreads();
+  for (int ti = 0; ti < job.top_count && !sh.found; ++ti) {
+    const int4 te = top[job.top_first + ti];  // (yaw, x | y << 16, z, sum), uniform
+    const int tx0 = static_cast<int16_t>(te.y & 0xffff), ty0 = te.y >> 16;
+    if (te.x != cur_yaw) {
+      __syncthreads();  // the previous yaw's readers are done
+      cur_yaw = te.x;
+      yw = yaws[pd.yaw_begin + cur_yaw];
+      for (int i = tid; i < n; i += kSearch3dThreads) {  // DiscretizeScan (:201-244)
+        const float* p = points + 3 * (pd.point_offset + i);
+        float ox, oy, oz;
+        Rotate3(yw.qw, yw.qx, yw.qy, yw.qz, p[0], p[1], p[2], &ox, &oy, &oz);
+        sh.cx[i] = static_cast<int16_t>(RoundDiv(__fadd_rn(ox, yw.tx), res, inv));
+        sh.cy[i] = static_cast<int16_t>(RoundDiv(__fadd_rn(oy, yw.ty), res, inv));
+        sh.cz[i] = static_cast<int16_t>(RoundDiv(__fadd_rn(oz, yw.tz), res, inv));
+      }
+      __syncthreads();
+    }
+    if (job.top_level == 0) {  // the list holds the leaves (depth-0 loop, :384-401)
+      const bool hit = te.w >= target && passes(tx0, ty0, te.z);
+      if (hit && tid == 0) {
+        sh.res = make_int4(te.x, tx0, ty0, te.z);
+        sh.found = 1;
+      }
+      __syncthreads();
+      continue;
+    }
+    __syncthreads();  // every wave has read the previous walk's empty stack
+    if (tid == 0) {
+      sh.stk[0] = make_int4(job.top_level, tx0, ty0, te.z);
+      sh.sp = 1;
+    }
+    for (;;) {
+      __syncthreads();
+      const int s = sh.sp;
+      if (s == 0 || sh.found) break;
+      const int4 nd = sh.stk[s - 1];
+      const int d = nd.x, hw = 1 << (d - 1);
+      // Children in generation order (:412-430).
+      int cxs[8], cys[8], czs[8], nc = 0;
+      for (int a = 0; a < 2; ++a) {
+        const int zo = nd.w + a * hw;
+        if (zo > pd.wz) break;
+        for (int b = 0; b < 2; ++b) {
+          const int yo = nd.z + b * hw;
+          if (yo > pd.wxy) break;
+          for (int c = 0; c < 2; ++c) {
+            const int xo = nd.y + c * hw;
+            if (xo > pd.wxy) break;
+            cxs[nc] = xo;
+            cys[nc] = yo;
+            czs[nc] = zo;
+            ++nc;
+          }
+        }
+      }
+      // ScoreCandidates at depth d - 1 (:332-352), as fast3d_score_queries.
+      const int cd = d - 1;
+      const int e = max(0, cd - sm.full_resolution_depth + 1);
+      const bool reduced = cd >= sm.full_resolution_depth;
+      const int lx = (-pd.wxy) >> e, ly = (-pd.wxy) >> e, lz = (-pd.wz) >> e;
+      const Brick3 bk = sm.level[cd];
+      const uint8_t* lv = sm.levels + bk.offset;
+      for (int c = wave; c < nc; c += kSearch3dThreads / 64) {
+        int qx = 0, qy = 0, qz = 0;
+        for (int k = 0; k < 8; ++k)
+          if (k == c) { qx = cxs[k]; qy = cys[k]; qz = czs[k]; }
+        int sum = 0;
+        for (int i = lane; i < n; i += 64) {
+          int x = sh.cx[i], y = sh.cy[i], z = sh.cz[i];
+          if (reduced) {
+            x = ((x - pd.wxy) >> e) - lx;
+            y = ((y - pd.wxy) >> e) - ly;
+            z = ((z - pd.wz) >> e) - lz;
+          }
+          int64_t idx;
+          if (InBrick(bk, x + (qx >> e), y + (qy >> e), z + (qz >> e), &idx)) sum += lv[idx];
+        }
+        for (int m = 32; m > 0; m >>= 1) sum += __shfl_xor(sum, m, 64);
+        if (lane == 0) sh.csum[c] = sum;
+      }
+      __syncthreads();
+      // Stable descending order by score (insertion sort, every thread alike).
+      int ord[8];
+      float sc[8];
+      for (int c = 0; c < nc; ++c) {
+        ord[c] = c;
+        sc[c] = SumToProbabilityDev(sh.csum[c], pd.num_points);
+      }
+      for (int i = 1; i < nc; ++i) {
+        const int k = ord[i];
+        int j = i - 1;
+        while (j >= 0 && sc[k] > sc[ord[j]]) {
+          ord[j + 1] = ord[j];
+          --j;
+        }
+        ord[j + 1] = k;
+      }
+      if (cd == 0) {
+        // Depth 0: the first child, in order, at or above the target that
+        // passes (none above it passes: the target is the passing maximum).
+        int hit = -1;
+        for (int i = 0; i < nc && hit < 0; ++i) {
+          const int c = ord[i];
+          if (sh.csum[c] < target) break;
+          int x = 0, y = 0, z = 0;
+          for (int k = 0; k < 8; ++k)
+            if (k == c) { x = cxs[k]; y = cys[k]; z = czs[k]; }
+          if (passes(x, y, z)) hit = c;
+        }
+        if (tid == 0) {
+          if (hit >= 0) {
+            int x = 0, y = 0, z = 0;
+            for (int k = 0; k < 8; ++k)
+              if (k == hit) { x = cxs[k]; y = cys[k]; z = czs[k]; }
+            sh.res = make_int4(cur_yaw, x, y, z);
+            sh.found = 1;
+          }
+          sh.sp = s - 1;
+        }
+      } else if (tid == 0) {
+        int top_sp = s - 1;
+        for (int i = nc - 1; i >= 0; --i) {
+          const int c = ord[i];
+          if (sh.csum[c] >= target && top_sp < kWalkStack3d)
+            sh.stk[top_sp++] = make_int4(cd, cxs[c], cys[c], czs[c]);
+        }
+        sh.sp = top_sp;
+      }
+    }
+    __syncthreads();
+  }
+  __syncthreads();
+  if (tid == 0) {
+    out[2 * blockIdx.x] = sh.res;
+    out[2 * blockIdx.x + 1] = make_int4(sh.found, 0, 0, 0);
+  }
+}
+
 // Low-resolution score of each pair's winning leaf (the Result field), with
 // the same arithmetic as the search: one workgroup per pair.
 __global__ void __launch_bounds__(kSearch3dThreads)
@@ -2315,6 +2520,16 @@ hipError_t LaunchFast3dFinalize(int num_pairs, hipStream_t st, const Submap3Desc
   if (num_pairs <= 0) return hipSuccess;
   hipLaunchKernelGGL(fast3d_finalize, dim3(num_pairs), dim3(kSearch3dThreads), 0, st, submaps,
                      pairs, yaws, low_points, best, low_score);
+  return hipGetLastError();
+}
+
+hipError_t LaunchFast3dWalk(int num_jobs, hipStream_t st, const Submap3Desc* submaps,
+                            const Pair3Desc* pairs, const Yaw3Desc* yaws, const float* points,
+                            const float* low_points, const Walk3Job* jobs, const int4* top,
+                            int4* out) {
+  if (num_jobs <= 0) return hipSuccess;
+  hipLaunchKernelGGL(fast3d_walk, dim3(num_jobs), dim3(kSearch3dThreads), 0, st, submaps, pairs,
+                     yaws, points, low_points, jobs, top, out);
   return hipGetLastError();
 }
 

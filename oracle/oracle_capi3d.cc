@@ -236,7 +236,8 @@ double oracle_fast3d_match_pairs(void** submaps, const float* high, const int64_
                                  const float* low, const int64_t* low_off, const float* hists,
                                  int hsize, const double* node_q, const int32_t* pair_submap,
                                  const int32_t* pair_node, int64_t num_pairs, int threads,
-                                 float min_score, int32_t* matched, double* task_seconds) {
+                                 float min_score, int32_t* matched, double* results,
+                                 double* task_seconds) {
   std::atomic<int64_t> next{0};
   const auto t0 = std::chrono::steady_clock::now();
   auto work = [&]() {
@@ -251,6 +252,7 @@ double oracle_fast3d_match_pairs(void** submaps, const float* high, const int64_
       const Fast3dResult r = static_cast<Fast3dHandle*>(submaps[pair_submap[i]])->m->MatchFullSubmap(
           Quatd{q[0], q[1], q[2], q[3]}, Quatd{1., 0., 0., 0.}, node, min_score);
       matched[i] = r.matched ? 1 : 0;
+      if (results) PutResult(r, results + 14 * i);  // score, poses: the bench's parity sample
       if (task_seconds)
         task_seconds[i] = std::chrono::duration<double>(std::chrono::steady_clock::now() - ts).count();
     }

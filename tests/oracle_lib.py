@@ -271,7 +271,7 @@ _SIG3D = {
     "oracle_rt3d_score": (F, [VP, P(D), P(D), P(F), I32, I64, P(D)]),
     "oracle_rt3d_window": (None, [P(D), F, P(F), I32, P(I32), P(F), P(I32)]),
     "oracle_fast3d_match_pairs": (D, [P(VP), P(F), P(I64), P(F), P(I64), P(F), I32, P(D),
-                                      P(I32), P(I32), I64, I32, F, P(I32), P(D)]),
+                                      P(I32), P(I32), I64, I32, F, P(I32), P(D), P(D)]),
     "oracle_rt3d_time": (D, [VP, P(D), P(D), P(F), I32, I64, I64]),
 }
 

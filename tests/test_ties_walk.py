@@ -88,8 +88,10 @@ def test_finds_constraints_inputs_match_oracle(csm, oracle, kernel):
     assert_search_ok(csm, res["status"])
     _assert_exact(res[0], om.match(init, cloud, 0.0))
     _assert_exact(res[1], om.match_full_submap(cloud, 0.0))
-    assert (res["tie"] == csm.TIE_WALK).all(), res["tie"]
-    assert tm.ties_walked == 2
+    # The local window (+-7 cells) ties fewer leaves than the collect record
+    # holds; the whole grid ties past it.
+    assert res[0]["tie"] != csm.TIE_NONE and res[1]["tie"] == csm.TIE_WALK, res["tie"]
+    assert tm.ties_walked == 1
     # The single-call drop-ins take the same path.
     assert m.Match(init, cloud, 0.0) == (True, float(res[0]["score"]),
                                          (res[0]["x"], res[0]["y"], res[0]["theta"]))
@@ -151,3 +153,172 @@ def test_plateau_ties_past_the_record(csm, oracle, kernel, seed):
     assert res[0]["tie"] == csm.TIE_WALK and tm.ties_walked == 1
     assert m.MatchFullSubmap(cloud, 0.5) == (True, float(res[0]["score"]),
                                              (res[0]["x"], res[0]["y"], res[0]["theta"]))
+
+
+# ---------------------------------------------------------------------- 3D --
+
+def _options3d(csm, depth, full_depth, min_low, lin_xy, lin_z, ang=0.3):
+    return csm.FastCorrelativeScanMatcherOptions3D(depth, full_depth, 0.1, min_low, lin_xy, lin_z,
+                                                   ang)
+
+
+def _same3d(gpu, ref):
+    from test_fast3d_gpu import assert_same_result
+    return assert_same_result(gpu, ref)
+
+
+def _matchers3d(csm, oracle, og_high, og_low, hist, o):
+    from test_fast3d_gpu import gpu_grid, opt_tuple
+    om = oracle.fast3d(og_high, og_low, hist, opt_tuple(o))
+    gh, gl = gpu_grid(csm, og_high), gpu_grid(csm, og_low)
+    return om, csm.FastCorrelativeScanMatcher3D(gh, gl, hist, o), (gh, gl)
+
+
+def test_finds_constraints_3d_inputs_match_oracle(csm, oracle):
+    """ConstraintBuilder3DTest.FindsConstraints (constraint_builder_3d_test.cc:
+    73-116): an empty Submap3D (every lookup unknown) and a one-point node,
+    min_score 0, rotational and low-resolution minimums 0, the default 3D
+    windows (xy 5 m, z 1 m, 15 deg; depth 8, full resolution depth 3): every
+    leaf ties. Match at identity and MatchFullSubmap take the oracle's pose."""
+    f = csm.FastCorrelativeScanMatcherOptions3D(min_rotational_score=0.0,
+                                                 min_low_resolution_score=0.0)
+    hist = np.zeros(3, np.float32)
+    og_h, og_l = oracle.hybrid_grid(0.1), oracle.hybrid_grid(0.1)
+    om, gm, keep = _matchers3d(csm, oracle, og_h, og_l, hist, f)
+    pt = np.array([[0.1, 0.2, 0.3]], np.float32)
+    node = csm.NodeData3D(pt, pt, hist)
+    ident = ((0.0, 0.0, 0.0), (1.0, 0.0, 0.0, 0.0))
+    ctx = csm.default_context(0)
+    ctx.reset_timing()
+    gpu = gm.Match(ident, ident, node, 0.0)
+    assert _same3d(gpu, om.match(ident, ident, node, 0.0)) == "tie"
+    assert gpu.tie == csm.TIE_WALK
+    gpu = gm.MatchFullSubmap((1, 0, 0, 0), (1, 0, 0, 0), node, 0.0)
+    assert _same3d(gpu, om.match_full_submap((1, 0, 0, 0), (1, 0, 0, 0), node, 0.0)) == "tie"
+    assert gpu.tie == csm.TIE_WALK
+    assert ctx.timing().ties_walked_3d == 2
+
+
+def _plateau3d(csm, oracle, seed, low_split):
+    """A block of equal high-resolution voxels (more placements of the cloud
+    on it than the collect record holds) in a field of random lower ones;
+    with low_split the low-resolution grid covers only part of the block, so
+    tied leaves at the maximum fail the low-resolution check there and the
+    walk must pass over them (the depth-0 loop, :384-401)."""
+    rng = np.random.default_rng(seed)
+    g = np.stack(np.meshgrid(np.arange(-24, 24), np.arange(-24, 24), np.arange(-10, 10),
+                             indexing="ij"), -1).reshape(-1, 3)
+    vals = rng.integers(4000, 20000, len(g)).astype(np.uint16)
+    block = (np.abs(g[:, 0]) < 16) & (np.abs(g[:, 1]) < 16) & (np.abs(g[:, 2]) < 7)
+    vals[block] = 30000
+    og_h = oracle.hybrid_grid(0.05)
+    og_h.set_values(g.astype(np.int32), vals)
+    og_l = oracle.hybrid_grid(0.05)
+    low = block & (g[:, 0] >= -2) if low_split else block
+    og_l.set_values(g[low].astype(np.int32), np.full(int(low.sum()), 30000, np.uint16))
+    cloud = rng.uniform(-0.12, 0.12, (14, 3)).astype(np.float32)
+    return og_h, og_l, cloud
+
+
+@pytest.mark.parametrize("low_split", [False, True])
+@pytest.mark.parametrize("depth,full_depth", [(6, 3), (4, 4)])
+def test_plateau_3d_ties_past_the_record(csm, oracle, low_split, depth, full_depth):
+    og_h, og_l, cloud = _plateau3d(csm, oracle, 11, low_split)
+    hist = np.zeros(10, np.float32)
+    o = _options3d(csm, depth, full_depth, 0.5, 0.6, 0.3, 0.2)
+    om, gm, keep = _matchers3d(csm, oracle, og_h, og_l, hist, o)
+    node = csm.NodeData3D(cloud, cloud, hist)
+    ctx = csm.default_context(0)
+    ident = ((0.0, 0.0, 0.0), (1.0, 0.0, 0.0, 0.0))
+    for init in [(0.0, 0.0, 0.0), (0.07, -0.04, 0.02)]:
+        ctx.reset_timing()
+        ref = om.match((init, (1, 0, 0, 0)), ident, node, 0.3)
+        gpu = gm.Match((init, (1, 0, 0, 0)), ident, node, 0.3)
+        assert ref["matched"]
+        assert _same3d(gpu, ref) == "tie"
+        assert gpu.tie == csm.TIE_WALK and ctx.timing().ties_walked_3d == 1
+
+
+# ----------------------------------------------------- through the builders --
+
+@pytest.fixture(scope="module")
+def cb(csm):
+    import importlib
+    return importlib.import_module("cartographer_amd.constraint_builder")
+
+
+@pytest.mark.parametrize("refine", [False, True])
+def test_finds_constraints_builder_poses_match_oracle(csm, cb, oracle, refine):
+    """ConstraintBuilder2DTest.FindsConstraints (constraint_builder_2d_test.cc:
+    70-112) through the drop-in, its constraints' poses compared with the
+    oracle: MaybeAddConstraint starts at submap pose * initial relative pose
+    (constraint_builder_2d.cc:195-197) and MaybeAddGlobalConstraint searches
+    the whole submap; each constraint is the oracle's match (every leaf tied)
+    expressed in the submap frame (:251-252), and with refine_with_ceres the
+    CeresScanMatcher2D refinement of it (oracle/ceres2d.cc, 1e-6)."""
+    limits, cells, grid = _unknown_grid(csm)
+    origin = (4.0, 5.0, 0.0)  # Submap2D origin (:80-81)
+    submap = cb.Submap2D(grid, origin)
+    opts = cb.ConstraintBuilderOptions(sampling_ratio=1.0, min_score=0.0,
+                                       global_localization_min_score=0.0,
+                                       refine_with_ceres=refine)
+    builder = cb.ConstraintBuilder2D(opts)
+    cloud = np.array([[0.1, 0.2, 0.3]], np.float32)
+    for _ in range(2):
+        builder.MaybeAddConstraint((0, 1), submap, (0, 0), cloud, (0.0, 0.0, 0.0))
+    builder.MaybeAddGlobalConstraint((0, 1), submap, (0, 0), cloud)
+    builder.NotifyEndOfNode()
+    got = []
+    builder.WhenDone(got.append)
+    got = got[0]
+    assert len(got) == 3 and all(c.tag == "INTER_SUBMAP" for c in got)
+    f = opts.fast_correlative_scan_matcher_options
+    om = oracle.fast2d(limits, cells, f.linear_search_window, f.angular_search_window,
+                       f.branch_and_bound_depth)
+    init = cb.rigid2d_compose(origin, (0.0, 0.0, 0.0))
+    refs = [om.match(init, cloud, 0.0)] * 2 + [om.match_full_submap(cloud, 0.0)]
+    o = opts.ceres_scan_matcher_options
+    copts = (o.occupied_space_weight, o.translation_weight, o.rotation_weight, o.max_num_iterations)
+    for c, ref in zip(got, refs):
+        assert ref[0] and np.float32(c.score) == np.float32(ref[1])
+        pose = cb.rigid2d_compose(origin, c.relative_pose)
+        if not refine:
+            assert np.allclose(pose, ref[2], rtol=0, atol=1e-12), (pose, ref[2])
+        else:
+            want, _ = oracle.ceres2d_match(limits, cells, copts, ref[2][:2], ref[2], cloud)
+            assert np.allclose(pose, want, atol=1e-6), (pose, want)
+
+
+def test_finds_constraints_3d_builder_poses_match_oracle(csm, cb, oracle):
+    """ConstraintBuilder3DTest.FindsConstraints (constraint_builder_3d_test.cc:
+    73-116) through the drop-in: an empty Submap3D, every leaf tied; each
+    constraint's pose is the oracle's Match / MatchFullSubmap pick."""
+    from test_fast3d_gpu import opt_tuple
+    f = csm.FastCorrelativeScanMatcherOptions3D(min_rotational_score=0.0,
+                                                 min_low_resolution_score=0.0)
+    opts = cb.ConstraintBuilderOptions(sampling_ratio=1.0, min_score=0.0,
+                                       global_localization_min_score=0.0,
+                                       fast_correlative_scan_matcher_options_3d=f,
+                                       refine_with_ceres=False)
+    empty = (np.zeros((0, 3), np.int32), np.zeros(0, np.uint16))
+    submap = cb.Submap3D(0.1, empty, 0.1, empty, np.zeros(3, np.float32))
+    pt = np.array([[0.1, 0.2, 0.3]], np.float32)
+    node = csm.NodeData3D(pt, pt, np.zeros(3, np.float32))
+    ident = ((0.0, 0.0, 0.0), (1.0, 0.0, 0.0, 0.0))
+    builder = cb.ConstraintBuilder3D(opts)
+    for _ in range(2):
+        builder.MaybeAddConstraint((0, 1), submap, (0, 0), node, ident, ident)
+    builder.MaybeAddGlobalConstraint((0, 1), submap, (0, 0), node, (1, 0, 0, 0), (1, 0, 0, 0))
+    builder.NotifyEndOfNode()
+    got = []
+    builder.WhenDone(got.append)
+    got = got[0]
+    assert len(got) == 3
+    og_h, og_l = oracle.hybrid_grid(0.1), oracle.hybrid_grid(0.1)
+    om = oracle.fast3d(og_h, og_l, np.zeros(3, np.float32), opt_tuple(f))
+    refs = [om.match(ident, ident, node, 0.0)] * 2 + \
+        [om.match_full_submap((1, 0, 0, 0), (1, 0, 0, 0), node, 0.0)]
+    for c, ref in zip(got, refs):
+        assert ref["matched"] and np.float32(c.score) == np.float32(ref["score"])
+        (gt, gq), (rt, rq) = c.relative_pose, ref["pose"]
+        assert tuple(gt) == tuple(rt) and tuple(gq) == tuple(rq), (c.relative_pose, ref["pose"])
