@@ -27,6 +27,7 @@ Ceres unpinned) unless ``refine_with_ceres`` is off.
 
 from __future__ import annotations
 
+import logging
 import math
 import sys
 from dataclasses import dataclass, field
@@ -39,6 +40,78 @@ from . import (CSM_OK, strerror, CeresOptions2D, CeresOptions3D, Context, FastCo
                FastCorrelativeScanMatcherOptions2D, FastCorrelativeScanMatcherOptions3D,
                HybridGrid, NodeData3D, ProbabilityGrid, ScanSet, _f32_points, default_context,
                make_pairs, make_pairs_3d, match_batch, match_batch_3d)
+from . import metrics as _metrics
+
+_LOG = logging.getLogger("cartographer_amd.constraint_builder")
+
+
+def _normalize_angle_difference(a: float) -> float:
+    """common::NormalizeAngleDifference (common/math.h)."""
+    while a > math.pi:
+        a -= 2.0 * math.pi
+    while a < -math.pi:
+        a += 2.0 * math.pi
+    return a
+
+
+def _quat_mul(a, b):
+    aw, ax, ay, az = a
+    bw, bx, by, bz = b
+    return (aw * bw - ax * bx - ay * by - az * bz, aw * bx + ax * bw + ay * bz - az * by,
+            aw * by + ay * bw + az * bx - ax * bz, aw * bz + az * bw + ax * by - ay * bx)
+
+
+def _quat_rotate(q, v):
+    n = sum(c * c for c in q)
+    r = _quat_mul(_quat_mul(q, (0.0,) + tuple(v)), (q[0], -q[1], -q[2], -q[3]))
+    return tuple(c / n for c in r[1:])
+
+
+def rigid3d_compose(a, b):
+    """transform::Rigid3d operator* on ((t), (w, x, y, z))."""
+    t = _quat_rotate(a[1], b[0])
+    return (tuple(t[k] + a[0][k] for k in range(3)), _quat_mul(a[1], b[1]))
+
+
+def rigid3d_inverse(a):
+    q = a[1]
+    n = sum(c * c for c in q)
+    qi = (q[0] / n, -q[1] / n, -q[2] / n, -q[3] / n)
+    t = _quat_rotate(qi, a[0])
+    return (tuple(-c for c in t), qi)
+
+
+class _BuilderMetrics:
+    """The process-wide metrics of one builder kind (the reference's static
+    k*Metric pointers, constraint_builder_2d.cc:46-53 / _3d.cc:46-59): Null
+    until RegisterMetrics."""
+
+    def __init__(self, three_d: bool):
+        C, G, H = _metrics.Counter.Null(), _metrics.Gauge.Null(), _metrics.Histogram.Null()
+        self.searched = self.found = self.global_searched = self.global_found = C
+        self.queue_length = self.num_submap_scan_matchers = G
+        # [local, global] x [score] (2D) or [score, rotational, low resolution] (3D)
+        self.scores = [[H] * (3 if three_d else 1) for _ in range(2)]
+
+    def register(self, factory, dim: str):
+        base = f"mapping_constraints_constraint_builder_{dim}"
+        counts = factory.NewCounterFamily(f"{base}_constraints", "Constraints computed")
+        self.searched = counts.Add({"search_region": "local", "matcher": "searched"})
+        self.found = counts.Add({"search_region": "local", "matcher": "found"})
+        self.global_searched = counts.Add({"search_region": "global", "matcher": "searched"})
+        self.global_found = counts.Add({"search_region": "global", "matcher": "found"})
+        self.queue_length = factory.NewGaugeFamily(f"{base}_queue_length", "Queue length").Add({})
+        scores = factory.NewHistogramFamily(f"{base}_scores", "Constraint scores built",
+                                            _metrics.Histogram.FixedWidth(0.05, 20))
+        for g, region in enumerate(("local", "global")):
+            if dim == "2d":
+                self.scores[g] = [scores.Add({"search_region": region})]
+            else:
+                self.scores[g] = [scores.Add({"search_region": region, "kind": k})
+                                  for k in ("score", "rotational_score", "low_resolution_score")]
+        self.num_submap_scan_matchers = factory.NewGaugeFamily(
+            f"{base}_num_submap_scan_matchers",
+            "Current number of constructed submap scan matchers").Add({})
 
 
 def rigid2d_compose(a, b):
@@ -145,24 +218,28 @@ def _budget_parts(pending, key_of, cache: _MatcherCache, make, bytes_of):
     if cache.budget > 0:
         order.sort(key=key_of)  # stable: submission order within a submap
     part, held, held_bytes = [], {}, 0
-    for p in order:
-        k = key_of(p)
-        if k not in held:
-            m = cache.get(k, lambda: make(p), bytes_of)
-            b = int(bytes_of(m))
-            if part and cache.budget > 0 and held_bytes + b > cache.budget:
-                yield part, held
-                cache.pinned = {k}
-                part, held, held_bytes = [], {}, 0
-                cache.trim()
-            cache.pinned.add(k)
-            held[k] = m
-            held_bytes += b
-        part.append(p)
-    if part:
-        yield part, held
-    cache.pinned = set()
-    cache.trim()
+    try:
+        for p in order:
+            k = key_of(p)
+            if k not in held:
+                m = cache.get(k, lambda: make(p), bytes_of)
+                b = int(bytes_of(m))
+                if part and cache.budget > 0 and held_bytes + b > cache.budget:
+                    yield part, held
+                    cache.pinned = {k}
+                    part, held, held_bytes = [], {}, 0
+                    cache.trim()
+                cache.pinned.add(k)
+                held[k] = m
+                held_bytes += b
+            part.append(p)
+        if part:
+            yield part, held
+    finally:
+        # Also when a part's search raises (the generator is then closed):
+        # no matcher stays pinned, so the budget keeps working.
+        cache.pinned = set()
+        cache.trim()
 
 
 @dataclass
@@ -201,6 +278,10 @@ class ConstraintBuilderOptions:
     # ceres_scan_matcher_3d (pose_graph.lua:49-60), ConstraintBuilder3D (:264-275).
     ceres_scan_matcher_options_3d: CeresOptions3D = field(default_factory=CeresOptions3D.make)
     refine_with_ceres: bool = True
+    # log_matches (pose_graph.lua:24): a line per accepted match and the score
+    # histogram at every WhenDone, to the builder's log_sink (default: the
+    # logging module at INFO, logger "cartographer_amd.constraint_builder").
+    log_matches: bool = True
 
 
 @dataclass
@@ -227,8 +308,18 @@ class _Pending:
 
 
 class ConstraintBuilder2D:
+    _metrics = _BuilderMetrics(False)
+
+    @classmethod
+    def RegisterMetrics(cls, factory):
+        """The metric families of constraint_builder_2d.cc:318-343 (same names
+        and labels), shared by every ConstraintBuilder2D of the process."""
+        cls._metrics.register(factory, "2d")
+
     def __init__(self, options: ConstraintBuilderOptions, context: Optional[Context] = None):
         self.options = options
+        self.score_histogram = _metrics.ScoreHistogram()  # score_histogram_ (:239)
+        self.log_sink = _LOG.info  # where the log_matches lines go (LOG(INFO))
         self.context = context or default_context()
         self._matchers = _MatcherCache(options.matcher_cache_bytes)
         self._samplers: Dict[Tuple[int, int], FixedRatioSampler] = {}
@@ -272,7 +363,12 @@ class ConstraintBuilder2D:
     def WhenDone(self, callback: Callable[[List[Constraint]], None]):
         self._flush()
         result = [c for c in self._constraints if c is not None]
+        if self.options.log_matches:  # RunWhenDoneCallback (:289-293)
+            self.log_sink(f"{len(self._constraints)} computations resulted in {len(result)} "
+                          "additional constraints.")
+            self.log_sink("Score histogram:\n" + self.score_histogram.ToString(10))
         self._constraints = []
+        self._metrics.queue_length.Set(len(self._constraints))
         callback(result)
 
     def GetNumFinishedNodes(self) -> int:
@@ -283,6 +379,7 @@ class ConstraintBuilder2D:
         header does."""
         key = tuple(submap_id)
         self._matchers.pop(key, lambda m: m.close())
+        self._metrics.num_submap_scan_matchers.Set(len(self._matchers))
         self._samplers.pop(key, None)
         before = len(self._pending)
         self._pending = [p for p in self._pending if p.submap_id != key]
@@ -350,12 +447,14 @@ class ConstraintBuilder2D:
     def _enqueue(self, submap_id, submap, node_id, cloud, full, initial):
         key = tuple(submap_id)
         self._constraints.append(None)
+        self._metrics.queue_length.Set(len(self._constraints))  # (:98, :123)
         p = _Pending(key, submap, tuple(node_id), cloud, full, tuple(initial),
                      len(self._constraints) - 1)
         # DispatchScanMatcherConstruction at enqueue (:165-186), via the cache.
         self._matchers.get(key, lambda: self._make_matcher(p), lambda m: m.device_bytes())
         self._matchers.pinned.discard(key)
         self._matchers.trim()
+        self._metrics.num_submap_scan_matchers.Set(len(self._matchers))
         self._pending.append(p)
 
     def _flush(self):
@@ -409,20 +508,29 @@ class ConstraintBuilder2D:
                     self.last_error = int(r["status"])
                     failed += 1
                     continue
+                m = self._metrics
                 if p.full:
                     self.global_constraints_searched += 1
+                    m.global_searched.Increment()
                 else:
                     self.constraints_searched += 1
+                    m.searched.Increment()
                 if int(r["status"]) != CSM_OK:
                     continue
                 score = float(r["score"])
                 if p.full:
                     self.global_constraints_found += 1
                     self.global_constraint_scores.append(score)
+                    m.global_found.Increment()
                 else:
                     self.constraints_found += 1
                     self.constraint_scores.append(score)
+                    m.found.Increment()
+                m.scores[p.full][0].Observe(score)
+                self.score_histogram.Add(score)
                 pose = refined.get(i, (float(r["x"]), float(r["y"]), float(r["theta"])))
+                if self.options.log_matches:
+                    self._log_match(p, pose, score)
                 self._constraints[p.slot] = Constraint(
                     submap_id=p.submap_id, node_id=p.node_id,
                     relative_pose=rigid2d_compose(rigid2d_inverse(p.submap.local_pose), pose),
@@ -432,6 +540,19 @@ class ConstraintBuilder2D:
             if failed:
                 print(f"ConstraintBuilder2D: {failed} of {len(pending)} pairs skipped "
                       f"({strerror(self.last_error)})", file=sys.stderr)
+
+    def _log_match(self, p, pose, score):
+        """ComputeConstraint's log_matches line (:260-276); `pose` is the
+        refined pose estimate (map <- node), p.initial the search start."""
+        info = (f"Node ({p.node_id[0]}, {p.node_id[1]}) with {len(p.cloud)} points on submap "
+                f"({p.submap_id[0]}, {p.submap_id[1]})")
+        if p.full:
+            info += " matches"
+        else:
+            d = rigid2d_compose(rigid2d_inverse(p.initial), pose)
+            info += " differs by translation %.2f rotation %.3f" % (
+                math.hypot(d[0], d[1]), abs(_normalize_angle_difference(d[2])))
+        self.log_sink(info + " with score %.1f%%." % (100.0 * score))
 
 
 # ---------------------------------------------------------------------------
@@ -492,8 +613,20 @@ class _Pending3D:
 
 
 class ConstraintBuilder3D:
+    _metrics = _BuilderMetrics(True)
+
+    @classmethod
+    def RegisterMetrics(cls, factory):
+        """The metric families of constraint_builder_3d.cc:351-386."""
+        cls._metrics.register(factory, "3d")
+
     def __init__(self, options: ConstraintBuilderOptions, context: Optional[Context] = None):
         self.options = options
+        # score_histogram_, rotational_score_histogram_, low_resolution_score_histogram_ (:257-259)
+        self.score_histogram = _metrics.ScoreHistogram()
+        self.rotational_score_histogram = _metrics.ScoreHistogram()
+        self.low_resolution_score_histogram = _metrics.ScoreHistogram()
+        self.log_sink = _LOG.info
         self.context = context or default_context()
         self._matchers = _MatcherCache(options.matcher_cache_bytes)  # key -> (high, low, m)
         self._submaps: Dict[Tuple[int, int], Submap3D] = {}  # for rebuilds of dropped matchers
@@ -542,7 +675,16 @@ class ConstraintBuilder3D:
     def WhenDone(self, callback: Callable[[List[Constraint3D]], None]):
         self._flush()
         result = [c for c in self._constraints if c is not None]
+        if self.options.log_matches:  # RunWhenDoneCallback (:317-326)
+            self.log_sink(f"{len(self._constraints)} computations resulted in {len(result)} "
+                          "additional constraints.\nScore histogram:\n"
+                          + self.score_histogram.ToString(10)
+                          + "\nRotational score histogram:\n"
+                          + self.rotational_score_histogram.ToString(10)
+                          + "\nLow resolution score histogram:\n"
+                          + self.low_resolution_score_histogram.ToString(10))
         self._constraints = []
+        self._metrics.queue_length.Set(len(self._constraints))
         callback(result)
 
     def GetNumFinishedNodes(self) -> int:
@@ -552,6 +694,7 @@ class ConstraintBuilder3D:
         """Also drops the submap's pending pairs (no constraint)."""
         key = tuple(submap_id)
         self._matchers.pop(key, _MatcherCache._close)  # matcher, then its grids
+        self._metrics.num_submap_scan_matchers.Set(len(self._matchers))
         self._samplers.pop(key, None)
         self._submaps.pop(key, None)
         before = len(self._pending)
@@ -585,11 +728,13 @@ class ConstraintBuilder3D:
         key = tuple(submap_id)
         self._submaps[key] = submap
         self._constraints.append(None)
+        self._metrics.queue_length.Set(len(self._constraints))  # (:101, :127)
         p = _Pending3D(key, tuple(node_id), data, full, node_pose, submap_pose,
                        len(self._constraints) - 1)
         self._matchers.get(key, lambda: self._make_matcher(p), self._bytes_of)
         self._matchers.pinned.discard(key)
         self._matchers.trim()
+        self._metrics.num_submap_scan_matchers.Set(len(self._matchers))
         self._pending.append(p)
 
     def _flush(self):
@@ -647,21 +792,32 @@ class ConstraintBuilder3D:
                     self.last_error = int(r["status"])
                     failed += 1
                     continue
+                m = self._metrics
                 if p.full:
                     self.global_constraints_searched += 1
+                    m.global_searched.Increment()
                 else:
                     self.constraints_searched += 1
+                    m.searched.Increment()
                 if int(r["status"]) != CSM_OK:
                     continue
                 score = float(r["score"])
+                rot, low = float(r["rotational_score"]), float(r["low_resolution_score"])
                 if p.full:
                     self.global_constraints_found += 1
                     self.global_constraint_scores.append(score)
+                    m.global_found.Increment()
                 else:
                     self.constraints_found += 1
                     self.constraint_scores.append(score)
-                self.rotational_scores.append(float(r["rotational_score"]))
-                self.low_resolution_scores.append(float(r["low_resolution_score"]))
+                    m.found.Increment()
+                for h, v in zip(m.scores[p.full], (score, rot, low)):
+                    h.Observe(v)
+                self.score_histogram.Add(score)
+                self.rotational_score_histogram.Add(rot)
+                self.low_resolution_score_histogram.Add(low)
+                self.rotational_scores.append(rot)
+                self.low_resolution_scores.append(low)
                 pose = refined.get(i, (tuple(float(v) for v in r["t"]),
                                        tuple(float(v) for v in r["q"])))
                 self._constraints[p.slot] = Constraint3D(
@@ -671,6 +827,26 @@ class ConstraintBuilder3D:
                     rotation_weight=self.options.loop_closure_rotation_weight,
                     score=score, rotational_score=float(r["rotational_score"]),
                     low_resolution_score=float(r["low_resolution_score"]))
+                if self.options.log_matches:
+                    self._log_match(p, self._constraints[p.slot].relative_pose, score)
             if failed:
                 print(f"ConstraintBuilder3D: {failed} of {len(pending)} pairs skipped "
                       f"({strerror(self.last_error)})", file=sys.stderr)
+
+    def _log_match(self, p, constraint, score):
+        """ComputeConstraint's log_matches line (:284-303): difference =
+        global_node_pose^-1 * global_submap_pose * constraint, its angle
+        transform::GetAngle."""
+        info = (f"Node ({p.node_id[0]}, {p.node_id[1]}) with "
+                f"{len(p.data.high_resolution_point_cloud)} points on submap "
+                f"({p.submap_id[0]}, {p.submap_id[1]})")
+        if p.full:
+            info += " matches"
+        else:
+            d = rigid3d_compose(rigid3d_compose(rigid3d_inverse(p.node_pose), p.submap_pose),
+                                constraint)
+            q = d[1]
+            angle = 2.0 * math.atan2(math.sqrt(q[1] ** 2 + q[2] ** 2 + q[3] ** 2), abs(q[0]))
+            info += " differs by translation %.2f rotation %.3f" % (
+                math.sqrt(sum(c * c for c in d[0])), angle)
+        self.log_sink(info + " with score %.1f%%." % (100.0 * score))

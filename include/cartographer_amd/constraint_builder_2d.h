@@ -6,8 +6,10 @@
 // NotifyEndOfNode (:139-151), WhenDone (:153-163) with results in submission
 // order and failures dropped (:279-300), GetNumFinishedNodes (:302-305),
 // DeleteScanMatcher (:307-316), the per-submap matcher cache
-// (DispatchScanMatcherConstruction :165-186) and the metric counters
-// (:46-53). Instead of one Task per pair on common::ThreadPool, pending pairs
+// (DispatchScanMatcherConstruction :165-186), the metrics (:46-53,
+// RegisterMetrics :318-343: constraint counters, queue-length and matcher
+// gauges, local and global score histograms), the score histogram and the
+// log_matches lines (:239, :260-276, :289-293). Instead of one Task per pair on common::ThreadPool, pending pairs
 // are searched as one GPU batch when a node ends (or when `flush_pairs` are
 // pending). Accepted matches are then refined as one batch by the
 // CeresScanMatcher2D restatement of ComputeConstraint (:245-249;
@@ -38,11 +40,13 @@
 #include <functional>
 #include <map>
 #include <memory>
+#include <string>
 #include <utility>
 #include <vector>
 
 #include "constraint_builder_common.h"
 #include "constraint_gather.h"
+#include "metrics.h"
 #include "scan_matching.h"
 
 namespace cartographer_amd {
@@ -130,7 +134,13 @@ class ConstraintBuilder2D {
       for (auto& c : constraints_)
         if (c) result.push_back(*c);
     }
+    if (options_.log_matches) {  // RunWhenDoneCallback (:289-293)
+      log_(std::to_string(constraints_.size()) + " computations resulted in " +
+           std::to_string(result.size()) + " additional constraints.");
+      log_("Score histogram:\n" + score_histogram_.ToString(10));
+    }
     constraints_.clear();
+    Metrics().queue_length->Set(constraints_.size());
     callback(result);
   }
 
@@ -142,6 +152,7 @@ class ConstraintBuilder2D {
   void DeleteScanMatcher(const SubmapId& submap_id) {
     matchers_.Erase(submap_id);
     samplers_.erase(submap_id);
+    Metrics().num_submap_scan_matchers->Set(matchers_.size());
     const size_t before = pending_.size();
     pending_.erase(std::remove_if(pending_.begin(), pending_.end(),
                                   [&](const Pending& p) {
@@ -162,7 +173,35 @@ class ConstraintBuilder2D {
   int64_t matcher_builds() const { return matchers_.builds; }
   int64_t matcher_evictions() const { return matchers_.evictions; }
 
-  // Metrics (constraint_builder_2d.cc:46-53).
+  // The metric families (constraint_builder_2d.cc:318-343): the same names
+  // and labels. Until called, the metrics are Null ones (:46-53). Shared by
+  // every ConstraintBuilder2D of the process, as the reference's statics.
+  static void RegisterMetrics(metrics::FamilyFactory* factory) {
+    MetricSet& m = Metrics();
+    auto* counts = factory->NewCounterFamily("mapping_constraints_constraint_builder_2d_constraints",
+                                             "Constraints computed");
+    m.searched = counts->Add({{"search_region", "local"}, {"matcher", "searched"}});
+    m.found = counts->Add({{"search_region", "local"}, {"matcher", "found"}});
+    m.global_searched = counts->Add({{"search_region", "global"}, {"matcher", "searched"}});
+    m.global_found = counts->Add({{"search_region", "global"}, {"matcher", "found"}});
+    m.queue_length = factory->NewGaugeFamily("mapping_constraints_constraint_builder_2d_queue_length",
+                                             "Queue length")->Add({});
+    auto* scores = factory->NewHistogramFamily("mapping_constraints_constraint_builder_2d_scores",
+                                               "Constraint scores built",
+                                               metrics::Histogram::FixedWidth(0.05, 20));
+    m.scores = scores->Add({{"search_region", "local"}});
+    m.global_scores = scores->Add({{"search_region", "global"}});
+    m.num_submap_scan_matchers =
+        factory->NewGaugeFamily("mapping_constraints_constraint_builder_2d_num_submap_scan_matchers",
+                                "Current number of constructed submap scan matchers")->Add({});
+  }
+
+  // score_histogram_ (:239): every accepted match's score, over the builder's life.
+  const ScoreHistogram& score_histogram() const { return score_histogram_; }
+  // Where the log_matches lines go (LOG(INFO) in the reference).
+  void set_log_sink(LogSink sink) { log_ = std::move(sink); }
+
+  // Counters of this builder (the metric counters above are process-wide).
   int64_t constraints_searched = 0, constraints_found = 0;
   int64_t global_constraints_searched = 0, global_constraints_found = 0;
   // Pairs skipped because the device search returned an error (not counted
@@ -196,13 +235,15 @@ class ConstraintBuilder2D {
   // the budgeted cache (a dropped matcher is rebuilt from the submap's grid).
   std::shared_ptr<FastCorrelativeScanMatcher2D> EnsureMatcher(const SubmapId& submap_id,
                                                               const Submap2DView* submap) {
-    return matchers_.Get(
+    auto m = matchers_.Get(
         submap_id,
         [&] {
           return std::make_shared<FastCorrelativeScanMatcher2D>(
               submap->grid, options_.fast_correlative_scan_matcher_options, context_);
         },
         [](const FastCorrelativeScanMatcher2D& m) { return m.device_bytes(); });
+    Metrics().num_submap_scan_matchers->Set(matchers_.size());
+    return m;
   }
 
   // Rank 0 receives every rank's accepted constraints in slot order; the
@@ -253,12 +294,10 @@ class ConstraintBuilder2D {
 
   void Enqueue(const SubmapId& submap_id, const Submap2DView* submap, const NodeId& node_id,
                const PointCloud* cloud, bool full, const Rigid2d& initial) {
-    if (!Owned(submap_id)) {  // another rank searches it; the slot keeps submission order
-      constraints_.emplace_back();
-      return;
-    }
-    if (!Claiming()) EnsureMatcher(submap_id, submap);  // claimed chunks build theirs
     constraints_.emplace_back();
+    Metrics().queue_length->Set(constraints_.size());  // (:98, :123)
+    if (!Owned(submap_id)) return;  // another rank searches it; the slot keeps submission order
+    if (!Claiming()) EnsureMatcher(submap_id, submap);  // claimed chunks build theirs
     pending_.push_back(Pending{submap_id, submap, node_id, cloud, full, initial,
                                constraints_.size() - 1});
   }
@@ -447,9 +486,14 @@ class ConstraintBuilder2D {
         last_error = results[i].status;
         continue;
       }
+      MetricSet& m = Metrics();
       (p.full ? global_constraints_searched : constraints_searched) += 1;
+      (p.full ? m.global_searched : m.searched)->Increment();
       if (results[i].status != CSM_OK) continue;
       (p.full ? global_constraints_found : constraints_found) += 1;
+      (p.full ? m.global_found : m.found)->Increment();
+      (p.full ? m.global_scores : m.scores)->Observe(results[i].score);
+      score_histogram_.Add(results[i].score);
       const Rigid2d pose{results[i].pose.x, results[i].pose.y, results[i].pose.theta};
       Constraint c;
       c.submap_id = p.submap_id;
@@ -460,6 +504,7 @@ class ConstraintBuilder2D {
       c.tag = Constraint::INTER_SUBMAP;
       c.score = results[i].score;
       constraints_[p.slot].reset(new Constraint(c));
+      if (options_.log_matches) LogMatch(p, pose, results[i].score);
     }
     if (failed_this_flush)
       std::fprintf(stderr, "ConstraintBuilder2D: %lld of %zu pairs skipped (%s)\n",
@@ -467,8 +512,50 @@ class ConstraintBuilder2D {
                    csm_strerror(last_error));
   }
 
+  // ComputeConstraint's log_matches line (:260-276); `pose` is the refined
+  // pose_estimate (map <- node), p.initial the search start.
+  void LogMatch(const Pending& p, const Rigid2d& pose, float score) {
+    char buf[160];
+    std::string info = "Node (" + std::to_string(p.node_id.trajectory_id) + ", " +
+                       std::to_string(p.node_id.node_index) + ") with " +
+                       std::to_string(p.cloud->size()) + " points on submap (" +
+                       std::to_string(p.submap_id.trajectory_id) + ", " +
+                       std::to_string(p.submap_id.submap_index) + ")";
+    if (p.full) {
+      info += " matches";
+    } else {
+      const Rigid2d d = Compose(Inverse(p.initial), pose);
+      double a = d.theta;  // common::NormalizeAngleDifference
+      while (a > M_PI) a -= 2. * M_PI;
+      while (a < -M_PI) a += 2. * M_PI;
+      std::snprintf(buf, sizeof(buf), " differs by translation %.2f rotation %.3f",
+                    std::hypot(d.x, d.y), std::abs(a));
+      info += buf;
+    }
+    std::snprintf(buf, sizeof(buf), " with score %.1f%%.", 100. * score);
+    log_(info + buf);
+  }
+
+  // The process-wide metrics (the reference's static k*Metric pointers).
+  struct MetricSet {
+    metrics::Counter* searched = metrics::Counter::Null();
+    metrics::Counter* found = metrics::Counter::Null();
+    metrics::Counter* global_searched = metrics::Counter::Null();
+    metrics::Counter* global_found = metrics::Counter::Null();
+    metrics::Gauge* queue_length = metrics::Gauge::Null();
+    metrics::Histogram* scores = metrics::Histogram::Null();
+    metrics::Histogram* global_scores = metrics::Histogram::Null();
+    metrics::Gauge* num_submap_scan_matchers = metrics::Gauge::Null();
+  };
+  static MetricSet& Metrics() {
+    static MetricSet m;
+    return m;
+  }
+
   ConstraintBuilderOptions options_;
   csm_context* context_;
+  ScoreHistogram score_histogram_;
+  LogSink log_ = DefaultLogSink("ConstraintBuilder2D");
   MatcherCache<FastCorrelativeScanMatcher2D> matchers_;
   std::map<SubmapId, FixedRatioSampler> samplers_;
   std::vector<std::unique_ptr<Constraint>> constraints_;

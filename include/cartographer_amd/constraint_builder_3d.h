@@ -38,11 +38,13 @@
 #include <functional>
 #include <map>
 #include <memory>
+#include <string>
 #include <utility>
 #include <vector>
 
 #include "constraint_builder_common.h"
 #include "constraint_gather.h"
+#include "metrics.h"
 #include "scan_matching_3d.h"
 
 namespace cartographer_amd {
@@ -122,8 +124,16 @@ class ConstraintBuilder3D {
       for (auto& c : constraints_)
         if (c) result.push_back(*c);
     }
+    if (options_.log_matches) {  // RunWhenDoneCallback (:317-326)
+      log_(std::to_string(constraints_.size()) + " computations resulted in " +
+           std::to_string(result.size()) + " additional constraints.\nScore histogram:\n" +
+           score_histogram_.ToString(10) + "\nRotational score histogram:\n" +
+           rotational_score_histogram_.ToString(10) + "\nLow resolution score histogram:\n" +
+           low_resolution_score_histogram_.ToString(10));
+    }
     constraints_.clear();
-    // The score metrics (constraint_builder_3d.cc:46-59), submission order.
+    Metrics().queue_length->Set(constraints_.size());
+    // The score lists (constraint_builder_3d.cc:46-59), submission order.
     for (const Constraint3D& c : result) {
       (c.global ? global_constraint_scores : constraint_scores).push_back(c.score);
       rotational_scores.push_back(c.rotational_score);
@@ -139,6 +149,7 @@ class ConstraintBuilder3D {
   void DeleteScanMatcher(const SubmapId& submap_id) {
     matchers_.Erase(submap_id);
     samplers_.erase(submap_id);
+    Metrics().num_submap_scan_matchers->Set(matchers_.size());
     const size_t before = pending_.size();
     pending_.erase(std::remove_if(pending_.begin(), pending_.end(),
                                   [&](const Pending& p) {
@@ -153,7 +164,42 @@ class ConstraintBuilder3D {
                    before - pending_.size());
   }
 
-  // Metrics (constraint_builder_3d.cc:46-59).
+  // The metric families (constraint_builder_3d.cc:351-386), same names and
+  // labels; Null metrics until called (:46-59); process-wide like the
+  // reference's statics.
+  static void RegisterMetrics(metrics::FamilyFactory* factory) {
+    MetricSet& m = Metrics();
+    auto* counts = factory->NewCounterFamily("mapping_constraints_constraint_builder_3d_constraints",
+                                             "Constraints computed");
+    m.searched = counts->Add({{"search_region", "local"}, {"matcher", "searched"}});
+    m.found = counts->Add({{"search_region", "local"}, {"matcher", "found"}});
+    m.global_searched = counts->Add({{"search_region", "global"}, {"matcher", "searched"}});
+    m.global_found = counts->Add({{"search_region", "global"}, {"matcher", "found"}});
+    m.queue_length = factory->NewGaugeFamily("mapping_constraints_constraint_builder_3d_queue_length",
+                                             "Queue length")->Add({});
+    auto* scores = factory->NewHistogramFamily("mapping_constraints_constraint_builder_3d_scores",
+                                               "Constraint scores built",
+                                               metrics::Histogram::FixedWidth(0.05, 20));
+    for (int g = 0; g < 2; ++g) {
+      const std::string region = g ? "global" : "local";
+      m.scores[g][0] = scores->Add({{"search_region", region}, {"kind", "score"}});
+      m.scores[g][1] = scores->Add({{"search_region", region}, {"kind", "rotational_score"}});
+      m.scores[g][2] = scores->Add({{"search_region", region}, {"kind", "low_resolution_score"}});
+    }
+    m.num_submap_scan_matchers =
+        factory->NewGaugeFamily("mapping_constraints_constraint_builder_3d_num_submap_scan_matchers",
+                                "Current number of constructed submap scan matchers")->Add({});
+  }
+
+  // score_histogram_, rotational_score_histogram_, low_resolution_score_histogram_ (:257-259).
+  const ScoreHistogram& score_histogram() const { return score_histogram_; }
+  const ScoreHistogram& rotational_score_histogram() const { return rotational_score_histogram_; }
+  const ScoreHistogram& low_resolution_score_histogram() const {
+    return low_resolution_score_histogram_;
+  }
+  void set_log_sink(LogSink sink) { log_ = std::move(sink); }
+
+  // Counters of this builder (the metric counters above are process-wide).
   int64_t constraints_searched = 0, constraints_found = 0;
   int64_t global_constraints_searched = 0, global_constraints_found = 0;
   // Pairs skipped because the device search returned an error (not counted
@@ -258,12 +304,10 @@ class ConstraintBuilder3D {
   void Enqueue(const SubmapId& submap_id, const Submap3DView* submap, const NodeId& node_id,
                const TrajectoryNodeData3D* data, bool full, const Rigid3d& node_pose,
                const Rigid3d& submap_pose) {
-    if (!Owned(submap_id)) {  // another rank searches it; the slot keeps submission order
-      constraints_.emplace_back();
-      return;
-    }
-    if (!Claiming()) EnsureMatcher(submap_id, submap);  // claimed chunks build theirs
     constraints_.emplace_back();
+    Metrics().queue_length->Set(constraints_.size());  // (:101, :127)
+    if (!Owned(submap_id)) return;  // another rank searches it; the slot keeps submission order
+    if (!Claiming()) EnsureMatcher(submap_id, submap);  // claimed chunks build theirs
     pending_.push_back(Pending{submap_id, submap, node_id, data, full, node_pose, submap_pose,
                                constraints_.size() - 1});
   }
@@ -273,7 +317,7 @@ class ConstraintBuilder3D {
   // from the submap's grids and histogram on its next use.
   std::shared_ptr<SubmapScanMatcher> EnsureMatcher(const SubmapId& submap_id,
                                                    const Submap3DView* submap) {
-    return matchers_.Get(
+    auto held = matchers_.Get(
         submap_id,
         [&] {
           auto m = std::make_shared<SubmapScanMatcher>();
@@ -285,6 +329,8 @@ class ConstraintBuilder3D {
           return m;
         },
         [](const SubmapScanMatcher& m) { return m.device_bytes(); });
+    Metrics().num_submap_scan_matchers->Set(matchers_.size());
+    return held;
   }
 
   void Flush() {
@@ -419,9 +465,18 @@ class ConstraintBuilder3D {
         last_error = results[i].status;
         continue;
       }
+      MetricSet& m = Metrics();
       (p.full ? global_constraints_searched : constraints_searched) += 1;
+      (p.full ? m.global_searched : m.searched)->Increment();
       if (results[i].status != CSM_OK) continue;
       (p.full ? global_constraints_found : constraints_found) += 1;
+      (p.full ? m.global_found : m.found)->Increment();
+      m.scores[p.full][0]->Observe(results[i].score);
+      m.scores[p.full][1]->Observe(results[i].rotational_score);
+      m.scores[p.full][2]->Observe(results[i].low_resolution_score);
+      score_histogram_.Add(results[i].score);
+      rotational_score_histogram_.Add(results[i].rotational_score);
+      low_resolution_score_histogram_.Add(results[i].low_resolution_score);
       Constraint3D c;
       c.submap_id = p.submap_id;
       c.node_id = p.node_id;
@@ -434,6 +489,7 @@ class ConstraintBuilder3D {
       c.low_resolution_score = results[i].low_resolution_score;
       c.global = p.full;
       constraints_[p.slot].reset(new Constraint3D(c));
+      if (options_.log_matches) LogMatch(p, c.relative_pose, results[i].score);
     }
     if (failed_this_flush)
       std::fprintf(stderr, "ConstraintBuilder3D: %lld of %zu pairs skipped (%s)\n",
@@ -441,8 +497,83 @@ class ConstraintBuilder3D {
                    csm_strerror(last_error));
   }
 
+  // ComputeConstraint's log_matches line (:284-303). difference =
+  // global_node_pose^-1 * global_submap_pose * constraint_transform; its
+  // angle is transform::GetAngle (2 atan2(|vec|, |w|)).
+  void LogMatch(const Pending& p, const Rigid3d& constraint, float score) {
+    char buf[160];
+    std::string info = "Node (" + std::to_string(p.node_id.trajectory_id) + ", " +
+                       std::to_string(p.node_id.node_index) + ") with " +
+                       std::to_string(p.data->high_resolution_point_cloud.size()) +
+                       " points on submap (" + std::to_string(p.submap_id.trajectory_id) + ", " +
+                       std::to_string(p.submap_id.submap_index) + ")";
+    if (p.full) {
+      info += " matches";
+    } else {
+      const Rigid3d d = Mul(Mul(Inv(p.node_pose), p.submap_pose), constraint);
+      const Quaterniond& q = d.rotation;
+      const double angle = 2. * std::atan2(std::sqrt(q.x * q.x + q.y * q.y + q.z * q.z),
+                                           std::abs(q.w));
+      std::snprintf(buf, sizeof(buf), " differs by translation %.2f rotation %.3f",
+                    std::sqrt(d.t[0] * d.t[0] + d.t[1] * d.t[1] + d.t[2] * d.t[2]), angle);
+      info += buf;
+    }
+    std::snprintf(buf, sizeof(buf), " with score %.1f%%.", 100. * score);
+    log_(info + buf);
+  }
+  // transform::Rigid3d operator* and inverse (rigid_transform.h:163-200) in double.
+  static Quaterniond QMul(const Quaterniond& a, const Quaterniond& b) {
+    return Quaterniond{a.w * b.w - a.x * b.x - a.y * b.y - a.z * b.z,
+                       a.w * b.x + a.x * b.w + a.y * b.z - a.z * b.y,
+                       a.w * b.y + a.y * b.w + a.z * b.x - a.x * b.z,
+                       a.w * b.z + a.z * b.w + a.x * b.y - a.y * b.x};
+  }
+  static void QRot(const Quaterniond& q, const double v[3], double out[3]) {
+    const Quaterniond p{0., v[0], v[1], v[2]};
+    const Quaterniond r = QMul(QMul(q, p), Quaterniond{q.w, -q.x, -q.y, -q.z});
+    const double n = q.w * q.w + q.x * q.x + q.y * q.y + q.z * q.z;
+    out[0] = r.x / n;
+    out[1] = r.y / n;
+    out[2] = r.z / n;
+  }
+  static Rigid3d Mul(const Rigid3d& a, const Rigid3d& b) {
+    Rigid3d r;
+    QRot(a.rotation, b.t, r.t);
+    for (int k = 0; k < 3; ++k) r.t[k] += a.t[k];
+    r.rotation = QMul(a.rotation, b.rotation);
+    return r;
+  }
+  static Rigid3d Inv(const Rigid3d& a) {
+    const Quaterniond& q = a.rotation;
+    const double n = q.w * q.w + q.x * q.x + q.y * q.y + q.z * q.z;
+    Rigid3d r;
+    r.rotation = Quaterniond{q.w / n, -q.x / n, -q.y / n, -q.z / n};
+    QRot(r.rotation, a.t, r.t);
+    for (int k = 0; k < 3; ++k) r.t[k] = -r.t[k];
+    return r;
+  }
+
+  struct MetricSet {  // the reference's static k*Metric pointers (:46-59)
+    metrics::Counter* searched = metrics::Counter::Null();
+    metrics::Counter* found = metrics::Counter::Null();
+    metrics::Counter* global_searched = metrics::Counter::Null();
+    metrics::Counter* global_found = metrics::Counter::Null();
+    metrics::Gauge* queue_length = metrics::Gauge::Null();
+    // [local, global][score, rotational_score, low_resolution_score]
+    metrics::Histogram* scores[2][3] = {
+        {metrics::Histogram::Null(), metrics::Histogram::Null(), metrics::Histogram::Null()},
+        {metrics::Histogram::Null(), metrics::Histogram::Null(), metrics::Histogram::Null()}};
+    metrics::Gauge* num_submap_scan_matchers = metrics::Gauge::Null();
+  };
+  static MetricSet& Metrics() {
+    static MetricSet m;
+    return m;
+  }
+
   ConstraintBuilderOptions options_;
   csm_context* context_;
+  ScoreHistogram score_histogram_, rotational_score_histogram_, low_resolution_score_histogram_;
+  LogSink log_ = DefaultLogSink("ConstraintBuilder3D");
   MatcherCache<SubmapScanMatcher> matchers_;
   std::map<SubmapId, FixedRatioSampler> samplers_;
   std::vector<std::unique_ptr<Constraint3D>> constraints_;

@@ -56,6 +56,9 @@ struct ConstraintBuilderOptions {
   // DeleteScanMatcher, constraint_builder_2d.cc:165-186, :307-316). A 400x400
   // 2D submap's matcher holds ~25 MB, so the default keeps ~1300 of them.
   int64_t matcher_cache_bytes = int64_t{32} << 30;
+  // log_matches (pose_graph.lua:24): one line per accepted match and the score
+  // histogram at every WhenDone, to the builder's log sink (metrics.h).
+  bool log_matches = true;
 };
 
 // The per-submap matcher cache (DispatchScanMatcherConstruction,

@@ -14,7 +14,7 @@ for f in 0 1; do
 done
 timeout -k 10 300 python -u tools/probe_c5.py > $O/c5.json 2> $O/c5.err || { tail -20 $O/c5.err; exit 1; }
 python3 -c "import json; d=json.load(open('$O/c5.json')); print({k: d[k] for k in ('value','value_search_only','ms_per_step','build_ms_per_step','release_ms_per_step','search_ms_per_step','kernel_ms_per_step','tied_pairs_per_step','ties_unresolved_per_step','ties_by_branch_last_step','accepted_per_step')})"
-timeout -k 10 120 ./tools/gather_lds_bench > $O/gather_lds.txt 2>&1 || { cat $O/gather_lds.txt; exit 1; }
+hipcc -O3 --offload-arch=gfx950 tools/gather_lds_bench.hip -o tools/gather_lds_bench && timeout -k 10 120 ./tools/gather_lds_bench > $O/gather_lds.txt 2>&1 || { cat $O/gather_lds.txt; exit 1; }
 cat $O/gather_lds.txt
 timeout -k 10 400 python -u bench.py --workload c2 --no-cpu --no-3d --steps 5 > $O/bench_c2.json 2> $O/bench_c2.err \
   || { tail -20 $O/bench_c2.err; exit 1; }
