@@ -332,6 +332,31 @@ def sum_timing(csm, tms):
     return out
 
 
+GATHER_FILE = os.path.join("profiles", "r5g", "gather_c3.json")
+
+
+def gather_roofline(kernel_ms):
+    """The C3 kernel against its texture-path ceiling: the
+    distinct 128-byte lines its gathers touch per launch (a CSM_KPROF pass)
+    at the gather microbenchmark's floor of TD cycles per line, spread over
+    every CU's TD at the engine clock, against this run's launch time; with
+    the measured TD cycles per line from a PMC pass of the same kernel tag
+    (tools/gather_roofline.py). None when no committed pass matches."""
+    try:
+        t = json.load(open(os.path.join(ROOT, GATHER_FILE)))
+    except (OSError, ValueError):
+        return None
+    if t.get("commit_kernel") != KERNEL_TAG or not kernel_ms:
+        return None
+    return {"bound": "texture data path: TD cycles per distinct 128-byte line a gather touches",
+            "line_touches_per_launch": t["line_touches_per_launch"],
+            "floor_td_cycles_per_line": t["floor_td_cycles_per_line"],
+            "floor_ms": t["floor_ms_per_launch"], "kernel_ms": kernel_ms,
+            "frac": t["floor_ms_per_launch"] / kernel_ms,
+            "td_cycles_per_line_measured": t["td_cycles_per_line_measured"],
+            "source": GATHER_FILE}
+
+
 def committed_traffic(args, world_size, workload="c2"):
     """HBM-side bytes per search launch from the committed PMC pass
     (profiles/*/traffic_*.json: rocprofv3 --pmc FETCH_SIZE, x2 gfx950
@@ -1257,6 +1282,7 @@ def c3_run(csm, ctx, args, rank, world_size, dist, coll_dev, comm, gather, trans
         "roofline": roofline_fields(tm, achieved, 8000.0, traffic, kernel_ms_avg, bytes_per_launch,
                                     tm.search_candidates / max(tm.search_launches, 1) *
                                     float(np.diff(world.offsets).mean())),
+        "gather_roofline": gather_roofline(kernel_ms_avg),
         "accepted_constraints": accepted,
         "errors_per_step": errors / args.steps,
         "stack_high_water": int(tm.stack_high_water),

@@ -243,7 +243,7 @@ def test_scripted_sweep_cpp_and_python(csm, cb, mt, bin_path):
         # 3D FindsConstraints inputs: 3 pairs a round, all found (score 0.1).
         assert got["queue_3d"] == 3 and got["queue_3d_after"] == 0
         assert got["counters_3d"] == [4, 4, 2, 2]
-        assert got["hist_3d_local_score"][_bucket(0.1, bounds)] == 4
+        assert got["hist_3d_local_score"][_bucket(float(np.float32(0.1)), bounds)] == 4
         assert sum(got["hist_3d_global_low_resolution_score"]) == 2
         log = got["log"]
         lines_2d = [x for x in log if x.startswith("2d Node")]
