@@ -37,6 +37,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 # Version tag of the search kernel the committed PMC traffic figures belong to
 # (a traffic file recorded on another kernel version is not reported).
 KERNEL_TAG = "v5-hybrid-refresh"
+# fast3d_search version whose PMC passes profiles/r5m/traffic_c5.json holds.
+KERNEL3D_TAG = "f3-octet-r5"
+TRAFFIC3D_FILE = os.path.join("profiles", "r5m", "traffic_c5.json")
 
 
 def load_pkg():
@@ -833,6 +836,7 @@ def fast3d_bench(csm, ctx, args, rank=0, world_size=1, dist=None, coll_dev=None,
            "release_ms_per_step": phase["release"] / max(reps - 1, 1) * 1e3,
            "search_ms_per_step": phase["search"] / reps * 1e3,
            "value_search_only": total / phase["search"] if phase["search"] else 0.0,
+           "roofline": roofline_3d(tm),
            "kernel_ms_per_step": tm.fast3d_kernel_ms / reps, "lookups_per_step": tm.fast3d_lookups / reps,
            "algorithmic_GBps": tm.fast3d_lookups / (tm.fast3d_kernel_ms * 1e-3) / 1e9
            if tm.fast3d_kernel_ms else 0.0, "setup_s": gen}
@@ -1084,6 +1088,32 @@ def parity_2d(sample, ores):
             "mismatched_pose": int(pose_bad.sum()), "gpu_errors": int((g["status"] < 0).sum()),
             "what": "the CPU baseline's sampled pairs: the GPU's results from the timed run vs the "
                     "oracle's (decision, float score bit-exact, pose exact)"}
+
+
+def roofline_3d(tm):
+    """C5's fast3d_search against the HBM roofline, as C3's: achieved =
+    algorithmic bytes per launch (1 B per precomputation-grid lookup, 8 per
+    octet gather; the kernel counts them) / the launch time from HIP events;
+    traffic = FETCH_SIZE x 1024 x 2 per dispatch from the committed PMC pass
+    of the same kernel tag (tools/traffic3d_json.py), with the rate it
+    implies at this run's launch time."""
+    launches = max(int(tm.fast3d_launches), 1)
+    kernel_ms = tm.fast3d_kernel_ms / launches
+    per_launch = tm.fast3d_lookups / launches
+    achieved = per_launch / (kernel_ms * 1e-3) / 1e9 if kernel_ms else 0.0
+    out = {"bound": "hbm", "achieved": achieved, "peak": 8000.0, "unit": "GB/s",
+           "frac": achieved / 8000.0, "bytes_per_launch": per_launch, "kernel_ms_avg": kernel_ms,
+           "launches": launches, "traffic": None, "traffic_frac": None}
+    try:
+        t = json.load(open(os.path.join(ROOT, TRAFFIC3D_FILE)))
+    except (OSError, ValueError):
+        return out
+    if t.get("commit_kernel") == KERNEL3D_TAG and t.get("traffic_bytes_per_launch") and kernel_ms:
+        out["traffic"] = t["traffic_bytes_per_launch"]
+        out["traffic_GBps"] = t["traffic_bytes_per_launch"] / (kernel_ms * 1e-3) / 1e9
+        out["traffic_frac"] = out["traffic_GBps"] / 8000.0
+        out["traffic_source"] = TRAFFIC3D_FILE
+    return out
 
 
 def parity_3d(res3, sampled, num_nodes):

@@ -1465,56 +1465,156 @@ int csm_fast2d_match_batch(csm_context* ctx, csm_fast2d* const* submaps, int32_t
                   results);
 }
 
-static int SingleMatch(const csm_fast2d* m, const csm_pose2d* initial, int full,
-                       const float* xyz, int32_t n, float min_score, float* score,
-                       csm_pose2d* pose) {
-  if (!m || !score || !pose || (n > 0 && !xyz) || n < 0 || (!full && !initial)) return CSM_EINVAL;
-  // A call context of the matcher's context (csm_internal.h): this call's
-  // stream and scratch; the pyramid is read-only and shared.
-  csm::CallContext cc(m->ctx);
+// One single Match / MatchFullSubmap call waiting in its owner's queue.
+struct SingleReq2 {
+  const csm_fast2d* m;
+  int full;
+  csm_pose2d initial;
+  const float* xyz;
+  int32_t n;
+  float min_score;
+  csm_result2d res;
+  int rc;
+  bool done;
+};
+
+constexpr int kCoalesceLeaders = 2;     // batches of queued single calls in flight
+constexpr int kCoalesceCap = 512;       // pairs per coalesced batch
+constexpr int kCoalesceWindowUs = 150;  // a leader's longest wait for more callers
+
+// Searches queued single calls as batches on one call context of `owner`: all
+// clouds in the call context's scan set, one pair per request (one batch per
+// plane kind, since a launch serves one kernel).
+static int RunSingleBatch(csm_context* owner, const std::vector<SingleReq2*>& reqs, int share) {
+  csm::CallContext cc(owner);
   csm_context* ctx = cc.get();
   if (!ctx) return CSM_EHIP;
   std::lock_guard<std::mutex> lock(ctx->mu);
   if (EnsureDevice(ctx)) return CSM_EHIP;
-  struct InFlight {  // this call counted among the owner's concurrent single calls
-    std::atomic<int>& n;
-    explicit InFlight(std::atomic<int>& c) : n(c) { ++n; }
-    ~InFlight() { --n; }
-  } in_flight(m->ctx->calls_in_flight);
-  ctx->grid_share = std::max(1, m->ctx->calls_in_flight.load());
-  // The call context's one-scan set, reset for this cloud (scan index 0
-  // names a different cloud on every call, so no window is kept).
+  ctx->grid_share = std::max(1, share);
   csm_scan_set& s = ctx->single;
   s.ctx = ctx;
-  s.offsets = {0, n};
-  s.host_points.assign(xyz, xyz + 3 * static_cast<size_t>(n));
+  s.offsets.assign(1, 0);
+  s.host_points.clear();
+  for (const SingleReq2* r : reqs) {
+    s.host_points.insert(s.host_points.end(), r->xyz, r->xyz + 3 * static_cast<size_t>(r->n));
+    s.offsets.push_back(s.offsets.back() + r->n);
+  }
+  // Scan indices name different clouds on every batch: no window is kept.
   s.windows.clear();
   s.rot_all.clear();
   s.rot_offsets.clear();
   s.rot_uploaded = 0;
+  const int64_t total = s.offsets.back();
   int rc;
-  if ((rc = s.points.Reserve(sizeof(float) * 3 * std::max(n, 1)))) return rc;
-  if (n > 0) {
-    if ((rc = ctx->single_stage.Reserve(sizeof(float) * 3 * n))) return rc;
-    std::memcpy(ctx->single_stage.ptr, xyz, sizeof(float) * 3 * n);
-    CSM_HIP(hipMemcpyAsync(s.points.ptr, ctx->single_stage.ptr, sizeof(float) * 3 * n,
+  if ((rc = s.points.Reserve(sizeof(float) * 3 * std::max<int64_t>(total, 1)))) return rc;
+  if (total > 0) {
+    if ((rc = ctx->single_stage.Reserve(sizeof(float) * 3 * total))) return rc;
+    std::memcpy(ctx->single_stage.ptr, s.host_points.data(), sizeof(float) * 3 * total);
+    CSM_HIP(hipMemcpyAsync(s.points.ptr, ctx->single_stage.ptr, sizeof(float) * 3 * total,
                            hipMemcpyHostToDevice, ctx->stream));
   }
-  csm_pair2d p{};
-  p.submap = 0;
-  p.scan = 0;
-  p.full_submap = full;
-  p.min_score = min_score;
-  if (!full) p.initial = *initial;
-  csm_fast2d* const handles[1] = {const_cast<csm_fast2d*>(m)};
-  csm_result2d r{};
-  rc = RunBatch(ctx, handles, 1, &s, &p, 1, &r);
-  if (rc < 0) return rc;
-  if (r.status == CSM_OK) {
-    *score = r.score;
-    *pose = r.pose;
+  for (int kind = 0; kind < 2; ++kind) {  // v4 (no hex planes), then v5
+    std::vector<csm_fast2d*> handles;
+    std::map<const csm_fast2d*, int> slot;
+    std::vector<csm_pair2d> pairs;
+    std::vector<size_t> which;
+    for (size_t k = 0; k < reqs.size(); ++k) {
+      const SingleReq2* r = reqs[k];
+      if ((r->m->desc.hex_mask != 0) != (kind == 1)) continue;
+      auto it = slot.find(r->m);
+      if (it == slot.end()) {
+        it = slot.emplace(r->m, static_cast<int>(handles.size())).first;
+        handles.push_back(const_cast<csm_fast2d*>(r->m));
+      }
+      csm_pair2d p{};
+      p.submap = it->second;
+      p.scan = static_cast<int32_t>(k);
+      p.full_submap = r->full;
+      p.min_score = r->min_score;
+      if (!r->full) p.initial = r->initial;
+      pairs.push_back(p);
+      which.push_back(k);
+    }
+    if (pairs.empty()) continue;
+    std::vector<csm_result2d> res(pairs.size());
+    if ((rc = RunBatch(ctx, handles.data(), static_cast<int32_t>(handles.size()), &s, pairs.data(),
+                       static_cast<int64_t>(pairs.size()), res.data())) < 0)
+      return rc;
+    for (size_t k = 0; k < which.size(); ++k) reqs[which[k]]->res = res[k];
   }
-  return r.status;
+  return CSM_OK;
+}
+
+// The reference's tasks call Match / MatchFullSubmap concurrently from
+// ThreadPool workers (constraint_builder_2d.cc:100-111, :188-215). One call
+// is one pair, far too little to fill the GPU, so concurrent callers of one
+// owner context are coalesced: each queues its pair; a caller that finds
+// fewer than kCoalesceLeaders batches running becomes a leader, waits up to
+// kCoalesceWindowUs for as many callers as the previous batch had, takes the
+// queue and searches it as one batch on a call context, then wakes the
+// callers it served. Results are the same as one call at a time (a pair's
+// result does not depend on its batch). CSM_SINGLE_COALESCE=0 runs each call
+// alone on its own call context.
+static int SingleMatch(const csm_fast2d* m, const csm_pose2d* initial, int full,
+                       const float* xyz, int32_t n, float min_score, float* score,
+                       csm_pose2d* pose) {
+  if (!m || !score || !pose || (n > 0 && !xyz) || n < 0 || (!full && !initial)) return CSM_EINVAL;
+  csm_context* owner = m->ctx;
+  struct InFlight {  // this call counted among the owner's concurrent single calls
+    std::atomic<int>& c;
+    explicit InFlight(std::atomic<int>& a) : c(a) { ++c; }
+    ~InFlight() { --c; }
+  } in_flight(owner->calls_in_flight);
+  SingleReq2 r{m, full, full ? csm_pose2d{0., 0., 0.} : *initial, xyz, n, min_score, {}, CSM_OK, false};
+  static const bool coalesce = [] {
+    const char* e = std::getenv("CSM_SINGLE_COALESCE");
+    return !(e && std::strcmp(e, "0") == 0);
+  }();
+  if (!coalesce) {
+    std::vector<SingleReq2*> one{&r};
+    r.rc = RunSingleBatch(owner, one, owner->calls_in_flight.load());
+  } else {
+    std::unique_lock<std::mutex> lk(owner->co_mu);
+    owner->co_queue.push_back(&r);
+    owner->co_cv.notify_all();
+    while (!r.done) {
+      const bool queued = std::find(owner->co_queue.begin(), owner->co_queue.end(), &r) !=
+                          owner->co_queue.end();
+      if (queued && owner->co_leaders < kCoalesceLeaders) {
+        ++owner->co_leaders;
+        const size_t want = static_cast<size_t>(std::max(1, owner->co_last_batch));
+        const auto deadline =
+            std::chrono::steady_clock::now() + std::chrono::microseconds(kCoalesceWindowUs);
+        while (owner->co_queue.size() < want &&
+               owner->co_cv.wait_until(lk, deadline) != std::cv_status::timeout) {
+        }
+        const size_t take_n = std::min<size_t>(owner->co_queue.size(), kCoalesceCap);
+        std::vector<SingleReq2*> take;
+        for (size_t i = 0; i < take_n; ++i) take.push_back(static_cast<SingleReq2*>(owner->co_queue[i]));
+        owner->co_queue.erase(owner->co_queue.begin(), owner->co_queue.begin() + take_n);
+        owner->co_last_batch = static_cast<int>(take_n);
+        const int share = owner->co_leaders;
+        lk.unlock();
+        const int rc = RunSingleBatch(owner, take, share);
+        lk.lock();
+        for (SingleReq2* q : take) {
+          q->rc = rc;
+          q->done = true;
+        }
+        --owner->co_leaders;
+        owner->co_cv.notify_all();
+      } else {
+        owner->co_cv.wait(lk);
+      }
+    }
+  }
+  if (r.rc < 0) return r.rc;
+  if (r.res.status == CSM_OK) {
+    *score = r.res.score;
+    *pose = r.res.pose;
+  }
+  return r.res.status;
 }
 
 int csm_fast2d_match(const csm_fast2d* m, const csm_pose2d* initial, const float* points_xyz,

@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <atomic>
 #include <map>
+#include <condition_variable>
 #include <mutex>
 #include <tuple>
 #include <vector>
@@ -175,6 +176,15 @@ struct csm_context {
   csm_context* call_owner = nullptr;  // set on call contexts
   std::atomic<int> calls_in_flight{0};  // single calls running on this owner's call contexts
   int grid_share = 1;  // a call context's search launch takes 1/grid_share of the GPU
+  // Coalesced single 2D calls (csm_host.cc SingleMatch): concurrent callers of
+  // this owner queue their pairs; a leader takes the queue after a short
+  // window and searches it as one batch on a call context, at most
+  // kCoalesceLeaders batches at a time.
+  std::mutex co_mu;
+  std::condition_variable co_cv;
+  std::vector<void*> co_queue;
+  int co_leaders = 0;
+  int co_last_batch = 1;  // the last batch's size: the next leader waits for as many
   csm_timing call_t{};                // finished single calls' timing (call_mu)
   csm_scan_set single;                // the cloud of the current single 2D call
   csm::PinnedBuf single_stage;
