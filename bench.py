@@ -77,6 +77,9 @@ def parse():
     p.add_argument("--submaps3d", type=int, default=200,
                    help="C5 submaps in total, split over the ranks")
     p.add_argument("--steps3d", type=int, default=3)
+    p.add_argument("--c5-groups", type=int, default=4,
+                   help="C5: submap groups per step; group g + 1 builds while group g is searched "
+                        "(1: build all, then search all)")
     p.add_argument("--c3-nodes", type=int, default=2000)
     p.add_argument("--c3-submaps", type=int, default=1000)
     p.add_argument("--c3-slice", type=int, default=50, help="submaps of the queue per step")
@@ -736,18 +739,30 @@ def fast3d_bench(csm, ctx, args, rank=0, world_size=1, dist=None, coll_dev=None,
     gen = time.time() - t0
     o = csm.FastCorrelativeScanMatcherOptions3D()
 
-    def build():
+    # Builds run on their own context (stream), issued by a helper thread: a
+    # step's submaps go in --c5-groups groups, and group g + 1's grids and
+    # pyramids are issued while group g is searched (the reference's matcher
+    # construction tasks run ahead of the constraint tasks that depend on
+    # them, constraint_builder_3d.cc:170-198). The search waits for each
+    # matcher's build (its ready event).
+    bctx = csm.Context(ctx.device) if args.c5_groups > 1 else ctx
+    from concurrent.futures import ThreadPoolExecutor
+    pool = ThreadPoolExecutor(max_workers=1) if args.c5_groups > 1 else None
+
+    def build(subs=None, bc=None):
         """The submaps' HybridGrids and PrecomputationGridStack3D pyramids
         (DispatchScanMatcherConstruction, constraint_builder_3d.cc:170-198)."""
-        g = [(csm.HybridGrid(w.high_resolution, *w.high_cells[s], context=ctx),
-              csm.HybridGrid(w.low_resolution, *w.low_cells[s], context=ctx))
-             for s in range(w.num_submaps)]
+        bc = bc or ctx
+        subs = range(w.num_submaps) if subs is None else subs
+        g = [(csm.HybridGrid(w.high_resolution, *w.high_cells[s], context=bc),
+              csm.HybridGrid(w.low_resolution, *w.low_cells[s], context=bc))
+             for s in subs]
         # One create per submap, as the builder makes them: each submap's
         # pyramid builds on the device while the host prepares the next
         # (csm_fast3d_create_batch, one launch per level for all submaps,
         # measured slower here: its builds start only after the last grid).
-        m = [csm.FastCorrelativeScanMatcher3D(gg[0], gg[1], w.submap_hist[s], o, ctx)
-             for s, gg in enumerate(g)]
+        m = [csm.FastCorrelativeScanMatcher3D(gg[0], gg[1], w.submap_hist[s], o, bc)
+             for s, gg in zip(subs, g)]
         return g, m
 
     def close(g, m):
@@ -774,11 +789,31 @@ def fast3d_bench(csm, ctx, args, rank=0, world_size=1, dist=None, coll_dev=None,
     # find them) is outside it, reported as release_ms_per_step.
     phase = {"build": 0.0, "search": 0.0, "release": 0.0}
 
+    groups = np.array_split(np.arange(w.num_submaps), max(1, args.c5_groups))
+
     def step():
         a = time.perf_counter()
-        g, m = build()
-        b = time.perf_counter()
-        res = csm.match_batch_3d(m, nodes, pairs, ctx)
+        if pool is None:
+            g, m = build()
+            b = time.perf_counter()
+            res = csm.match_batch_3d(m, nodes, pairs, ctx)
+        else:
+            g, m, parts, waited = [], [], [], 0.0
+            fut = pool.submit(build, groups[0], bctx)
+            for gi, grp in enumerate(groups):
+                t = time.perf_counter()
+                gg, mm = fut.result()
+                waited += time.perf_counter() - t
+                if gi + 1 < len(groups):
+                    fut = pool.submit(build, groups[gi + 1], bctx)
+                g += gg
+                m += mm
+                lo, hi = int(grp[0]) * w.num_nodes, (int(grp[-1]) + 1) * w.num_nodes
+                gp = pairs[lo:hi].copy()
+                gp["submap"] -= int(grp[0])
+                parts.append(csm.match_batch_3d(mm, nodes, gp, ctx))
+            res = np.concatenate(parts)
+            b = a + waited  # the builds' exposed time (the rest overlaps the searches)
         rec = cdist.make_records_3d(res, submission, sub_global, nod) if cdist else None
         if cdist is not None:
             rec = gather(rec) if gather is not None else \
@@ -808,6 +843,8 @@ def fast3d_bench(csm, ctx, args, rank=0, world_size=1, dist=None, coll_dev=None,
             close(*kept)
             phase["release"] += time.perf_counter() - t0
     grids, mats = kept
+    if pool is not None:
+        pool.shutdown()
     if rank == 0 and rec is not None:
         DUMP["c5"] = np.asarray(rec)
     tm = ctx.timing()
@@ -832,6 +869,9 @@ def fast3d_bench(csm, ctx, args, rank=0, world_size=1, dist=None, coll_dev=None,
                                         for name, code in (("ancestors", csm.TIE_ANCESTORS),
                                                            ("toplist", csm.TIE_TOPLIST),
                                                            ("walk", csm.TIE_WALK))},
+           "c5_groups": len(groups),
+           # Builds' exposed time: all of it with one group; with several, the
+           # first group's build and any wait for a later one.
            "build_ms_per_step": phase["build"] / reps * 1e3,
            "release_ms_per_step": phase["release"] / max(reps - 1, 1) * 1e3,
            "search_ms_per_step": phase["search"] / reps * 1e3,

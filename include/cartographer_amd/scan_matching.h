@@ -57,8 +57,11 @@ struct Grid2DView {
   double max_x = 0., max_y = 0.;
   int num_x_cells = 0, num_y_cells = 0;
   const uint16_t* cells = nullptr;       // correspondence_cost_cells() (TSD values for a TSDF)
-  float min_correspondence_cost = 0.1f;  // kMinCorrespondenceCost (-truncation for a TSDF)
-  float max_correspondence_cost = 0.9f;  // kMaxCorrespondenceCost (truncation for a TSDF)
+  // kMinCorrespondenceCost = 1.f - kMaxProbability and kMaxCorrespondenceCost =
+  // 1.f - kMinProbability, in float (probability_values.h:32-36): 0.100000024f
+  // and 0.9f (-truncation / truncation for a TSDF).
+  float min_correspondence_cost = 1.f - (1.f - 0.1f);
+  float max_correspondence_cost = 1.f - 0.1f;
   // TSDF2D only (tsdf_2d.h:55-60): weight_cells_ and TSDValueConverter's max weight.
   const uint16_t* weight_cells = nullptr;
   float max_weight = 0.f;

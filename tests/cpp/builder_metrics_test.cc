@@ -94,6 +94,7 @@ static void Sweep() {
     o.sampling_ratio = 1.;
     o.min_score = 0.3f;
     o.global_localization_min_score = 0.35f;
+    o.refine_with_ceres = std::getenv("CSM_TEST_NO_REFINE") == nullptr;
     ConstraintBuilder2D b(o);
     b.set_log_sink([&](const std::string& line) { log.push_back("2d " + line); });
     const std::vector<uint16_t> cells = SweepCells();

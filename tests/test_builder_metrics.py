@@ -256,10 +256,10 @@ def test_scripted_sweep_cpp_and_python(csm, cb, mt, bin_path):
     # The two implementations agree line for line.
     assert cpp["log"] == py["log"]
     assert cpp["tostring_2d"] == py["tostring_2d"]
-    # Same matches; the Ceres refinement's device reductions may round
-    # differently between two runs (the builders' refine test allows 1e-6).
+    # Same matches and the same refinement (the Ceres kernel's reductions are
+    # deterministic): only the Rigid2d algebra's last bits may differ.
     for a, b in zip(cpp["constraints_2d"], py["constraints_2d"]):
-        assert a[:3] == b[:3] and np.allclose(a[3:], b[3:], rtol=0, atol=1e-6), (a, b)
+        assert a[:3] == b[:3] and np.allclose(a[3:], b[3:], rtol=0, atol=1e-12), (a, b)
     for k in cpp:
         if k not in ("log", "constraints_2d"):
             assert cpp[k] == py[k], k
