@@ -434,7 +434,9 @@ int csm_ceres3d_refine_batch(csm_context* ctx, const csm_hybrid_grid* const* gri
     Refine3Desc& d = desc[i];
     const csm_hybrid_grid* g[2] = {grids[it.high_grid], grids[it.low_grid]};
     for (int k = 0; k < 2; ++k) {
-      if (g[k]->ctx != ctx) return CSM_EINVAL;
+      // Grids from any context on ctx's device (e.g. one whose stream built
+      // them while ctx searched); their builds are waited for below.
+      if (!g[k]->ctx || g[k]->ctx->device != ctx->device) return CSM_EINVAL;
       d.grid[k] = GridView3{g[k]->prob.as<float>(), g[k]->brick, g[k]->resolution};
       d.offset[k] = off[2 * it.node + k];
     }
@@ -453,6 +455,8 @@ int csm_ceres3d_refine_batch(csm_context* ctx, const csm_hybrid_grid* const* gri
   if ((rc = ctx->cr3_points.Reserve(sizeof(float) * std::max<size_t>(pts.size(), 3)))) return rc;
   if ((rc = ctx->cr3_out.Reserve(sizeof(double) * 7 * n + sizeof(int32_t) * n))) return rc;
   hipStream_t st = ctx->stream;
+  for (int32_t k = 0; k < num_grids; ++k)  // grids another context's stream built
+    if (grids[k] && (rc = WaitBuilt(grids[k]->ready, grids[k]->ctx->stream, st))) return rc;
   CSM_HIP(hipMemcpyAsync(ctx->cr3_items.ptr, desc.data(), sizeof(Refine3Desc) * n,
                          hipMemcpyHostToDevice, st));
   CSM_HIP(hipMemcpyAsync(ctx->cr3_points.ptr, pts.data(), sizeof(float) * pts.size(),

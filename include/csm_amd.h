@@ -550,6 +550,8 @@ typedef struct csm_refine3d {
   double target[3];
 } csm_refine3d;
 
+/* The grids may come from any context on ctx's device; the refinement waits
+ * on the device for their builds. */
 int csm_ceres3d_refine_batch(csm_context* ctx, const csm_hybrid_grid* const* grids,
                              int32_t num_grids, const csm_node3d* nodes, int32_t num_nodes,
                              const csm_refine3d* items, int64_t n,
