@@ -789,7 +789,7 @@ def fast3d_bench(csm, ctx, args, rank=0, world_size=1, dist=None, coll_dev=None,
     # find them) is outside it, reported as release_ms_per_step.
     phase = {"build": 0.0, "search": 0.0, "release": 0.0}
 
-    groups = np.array_split(np.arange(w.num_submaps), max(1, args.c5_groups))
+    groups = [g for g in np.array_split(np.arange(w.num_submaps), max(1, args.c5_groups)) if len(g)]
 
     def step():
         a = time.perf_counter()

@@ -1478,9 +1478,23 @@ struct SingleReq2 {
   bool done;
 };
 
-constexpr int kCoalesceLeaders = 2;     // batches of queued single calls in flight
-constexpr int kCoalesceCap = 512;       // pairs per coalesced batch
-constexpr int kCoalesceWindowUs = 150;  // a leader's longest wait for more callers
+constexpr int kCoalesceCap = 512;  // pairs per coalesced batch
+// Batches of queued single calls in flight, and a leader's longest wait for
+// more callers (A/B: CSM_COALESCE_LEADERS, CSM_COALESCE_WINDOW_US).
+static int CoalesceLeaders() {
+  static const int v = [] {
+    const char* e = std::getenv("CSM_COALESCE_LEADERS");
+    return e ? std::max(1, std::atoi(e)) : 2;
+  }();
+  return v;
+}
+static int CoalesceWindowUs() {
+  static const int v = [] {
+    const char* e = std::getenv("CSM_COALESCE_WINDOW_US");
+    return e ? std::max(0, std::atoi(e)) : 150;
+  }();
+  return v;
+}
 
 // Searches queued single calls as batches on one call context of `owner`: all
 // clouds in the call context's scan set, one pair per request (one batch per
@@ -1550,8 +1564,9 @@ static int RunSingleBatch(csm_context* owner, const std::vector<SingleReq2*>& re
 // ThreadPool workers (constraint_builder_2d.cc:100-111, :188-215). One call
 // is one pair, far too little to fill the GPU, so concurrent callers of one
 // owner context are coalesced: each queues its pair; a caller that finds
-// fewer than kCoalesceLeaders batches running becomes a leader, waits up to
-// kCoalesceWindowUs for as many callers as the previous batch had, takes the
+// fewer than CoalesceLeaders() (2) batches running becomes a leader, waits up
+// to CoalesceWindowUs() (150 us) for as many callers as the previous batch
+// had, takes the
 // queue and searches it as one batch on a call context, then wakes the
 // callers it served. Results are the same as one call at a time (a pair's
 // result does not depend on its batch). CSM_SINGLE_COALESCE=0 runs each call
@@ -1581,11 +1596,11 @@ static int SingleMatch(const csm_fast2d* m, const csm_pose2d* initial, int full,
     while (!r.done) {
       const bool queued = std::find(owner->co_queue.begin(), owner->co_queue.end(), &r) !=
                           owner->co_queue.end();
-      if (queued && owner->co_leaders < kCoalesceLeaders) {
+      if (queued && owner->co_leaders < CoalesceLeaders()) {
         ++owner->co_leaders;
         const size_t want = static_cast<size_t>(std::max(1, owner->co_last_batch));
         const auto deadline =
-            std::chrono::steady_clock::now() + std::chrono::microseconds(kCoalesceWindowUs);
+            std::chrono::steady_clock::now() + std::chrono::microseconds(CoalesceWindowUs());
         while (owner->co_queue.size() < want &&
                owner->co_cv.wait_until(lk, deadline) != std::cv_status::timeout) {
         }

@@ -99,7 +99,8 @@ def test_threads_on_one_handle(csm, world, cases):
 
 def test_threads_on_several_handles(csm, world, cases):
     """8 threads over every case, the matchers of one context, twice over
-    with timing enabled: single calls are counted in the owner's timing."""
+    with timing enabled: single calls are counted in the owner's timing, and
+    concurrent ones share launches."""
     cs, refs = cases
     ctx = csm.Context(0)
     mats = _mats(csm, world, ctx)
@@ -110,7 +111,9 @@ def test_threads_on_several_handles(csm, world, cases):
     ctx.enable_timing(False)
     _check(got, refs + refs, cs + cs)
     t = ctx.timing()
-    assert t.search_launches == 2 * len(cs), t.search_launches
+    # Concurrent calls are coalesced into batches (csm_host.cc SingleMatch):
+    # fewer launches than calls, every call counted once among them.
+    assert 1 <= t.search_launches < 2 * len(cs), t.search_launches
     assert t.search_errors == 0
 
 

@@ -23,8 +23,9 @@ run() {  # label, then env assignments
 import json; d=json.loads(open('$O/ab.json').read().strip().splitlines()[-1])
 print('$label', round(d['value'], 1), round(d['roofline']['kernel_ms_avg'], 1), d['accepted_constraints'], d['errors_per_step'])" | tee -a $O/ab_summary.txt
 }
-for c in 0,0,2,2,2,3,3,3,3,3,3,3 0,1,2,2,2,3,3,3,3,3,3,3 0,0,1,2,2,3,3,3,3,3,3,3 0,0,2,3,2,3,3,3,3,3,3,3 \
-         0,0,2,2,3,3,3,3,3,3,3,3 0,0,2,2,2,3,2,3,3,3,3,3 0,0,1,1,2,3,3,3,3,3,3,3 0,0,2,2,2,3,3,3,3,3,3,3; do
+for c in 0,0,2,2,2,3,3,3,3,3,3,3 0,1,2,2,2,3,3,3,3,3,3,3 0,0,1,2,2,3,3,3,3,3,3,3 0,1,1,2,2,3,3,3,3,3,3,3 \
+         0,0,1,1,2,3,3,3,3,3,3,3 0,0,2,3,2,3,3,3,3,3,3,3 0,0,2,2,3,3,3,3,3,3,3,3 0,0,2,2,2,3,2,3,3,3,3,3 \
+         0,0,2,2,2,3,3,3,3,3,3,3; do
   run cluster=$c CSM_CLUSTER=$c
 done
 date +%T
