@@ -66,6 +66,12 @@ static void FindsConstraints() {
     builder.WhenDone([&](const ConstraintBuilder2D::Result& r) { result = r; });
     EXPECT(result.size() == 3);
     for (const Constraint& c : result) EXPECT(c.tag == Constraint::INTER_SUBMAP);
+    // The constraints' poses, compared with the oracle by the Python runner
+    // (tests/test_constraint_builder.py): every leaf ties on this grid.
+    if (i == 0)
+      for (const Constraint& c : result)
+        std::printf("FINDS_CONSTRAINTS %.17g %.17g %.17g %.9g\n", c.relative_pose.x,
+                    c.relative_pose.y, c.relative_pose.theta, c.score);
     builder.DeleteScanMatcher(submap_id);
   }
   EXPECT(builder.constraints_searched == 4 && builder.constraints_found == 4);

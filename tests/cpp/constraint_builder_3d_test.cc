@@ -68,7 +68,16 @@ static void FindsConstraints() {  // :73-116
     size_t n = 0, inter = 0;
     builder.WhenDone([&](const ConstraintBuilder3D::Result& r) {
       n = r.size();
-      for (const Constraint3D& c : r) inter += c.tag == Constraint3D::INTER_SUBMAP;
+      for (const Constraint3D& c : r) {
+        inter += c.tag == Constraint3D::INTER_SUBMAP;
+        // Compared with the oracle by tests/test_constraint_builder_3d.py.
+        if (i == 0) {
+          const Rigid3d& p = c.relative_pose;
+          std::printf("FINDS_CONSTRAINTS %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.9g\n", p.t[0],
+                      p.t[1], p.t[2], p.rotation.w, p.rotation.x, p.rotation.y, p.rotation.z,
+                      c.score);
+        }
+      }
     });
     EXPECT(n == 3);
     EXPECT(inter == 3);

@@ -72,11 +72,35 @@ def test_cpp_headers_compile_and_link(csm):
 
 
 @pytest.mark.gpu
-def test_cpp_constraint_builder(csm):
+def test_cpp_constraint_builder(csm, oracle):
+    """The C++ restatement of ConstraintBuilder2DTest passes, and its
+    FindsConstraints constraints (all-unknown grid, every leaf tied) are the
+    oracle's picks refined by the CeresScanMatcher2D restatement
+    (oracle/ceres2d.cc; parity with Ceres itself unpinned), in the submap frame."""
+    import importlib
+    cb = importlib.import_module("cartographer_amd.constraint_builder")
     _build_cpp()
     out = subprocess.run([CPP_BIN], capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stderr
     assert "OK" in out.stdout
+    got = [tuple(float(v) for v in line.split()[1:]) for line in out.stdout.splitlines()
+           if line.startswith("FINDS_CONSTRAINTS")]
+    assert len(got) == 3
+    cells = np.zeros((110, 100), np.uint16)
+    limits = (1.0, 2.0, 3.0)
+    f = cb.ConstraintBuilderOptions().fast_correlative_scan_matcher_options
+    om = oracle.fast2d(limits, cells, f.linear_search_window, f.angular_search_window,
+                       f.branch_and_bound_depth)
+    cloud = np.array([[0.1, 0.2, 0.3]], np.float32)
+    origin = (4.0, 5.0, 0.0)
+    refs = [om.match(origin, cloud, 0.0)] * 2 + [om.match_full_submap(cloud, 0.0)]
+    o = cb.ConstraintBuilderOptions().ceres_scan_matcher_options
+    copts = (o.occupied_space_weight, o.translation_weight, o.rotation_weight, o.max_num_iterations)
+    for g, ref in zip(got, refs):
+        assert ref[0] and np.float32(g[3]) == np.float32(ref[1])
+        want, _ = oracle.ceres2d_match(limits, cells, copts, ref[2][:2], ref[2], cloud)
+        pose = cb.rigid2d_compose(origin, g[:3])
+        assert np.allclose(pose, want, atol=1e-6), (pose, want)
 
 
 def _unknown_submap(csm, cb):

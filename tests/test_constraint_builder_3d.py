@@ -48,11 +48,39 @@ def test_cpp_headers_compile_and_link_3d(csm):
 
 
 @pytest.mark.gpu
-def test_cpp_constraint_builder_3d(csm):
+def test_cpp_constraint_builder_3d(csm, oracle):
+    """The C++ restatement of ConstraintBuilder3DTest passes, and its
+    FindsConstraints constraints (an empty submap, every leaf tied) are the
+    oracle's Match / MatchFullSubmap picks refined by the CeresScanMatcher3D
+    restatement (oracle/ceres3d.cc; parity with Ceres itself unpinned)."""
+    import importlib
+    cb = importlib.import_module("cartographer_amd.constraint_builder")
+    from test_fast3d_gpu import opt_tuple
     _build_cpp()
     out = subprocess.run([CPP_BIN], capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stderr
     assert "OK" in out.stdout
+    got = [tuple(float(v) for v in line.split()[1:]) for line in out.stdout.splitlines()
+           if line.startswith("FINDS_CONSTRAINTS")]
+    assert len(got) == 3
+    f = csm.FastCorrelativeScanMatcherOptions3D(min_rotational_score=0.0,
+                                                 min_low_resolution_score=0.0)
+    og_h, og_l = oracle.hybrid_grid(0.1), oracle.hybrid_grid(0.1)
+    om = oracle.fast3d(og_h, og_l, np.zeros(3, np.float32), opt_tuple(f))
+    pt = np.array([[0.1, 0.2, 0.3]], np.float32)
+    node = csm.NodeData3D(pt, pt, np.zeros(3, np.float32))
+    ident = ((0.0, 0.0, 0.0), (1.0, 0.0, 0.0, 0.0))
+    refs = [om.match(ident, ident, node, 0.0)] * 2 + \
+        [om.match_full_submap((1, 0, 0, 0), (1, 0, 0, 0), node, 0.0)]
+    o3 = cb.ConstraintBuilderOptions().ceres_scan_matcher_options_3d
+    copts = (o3.occupied_space_weight_0, o3.occupied_space_weight_1, o3.translation_weight,
+             o3.rotation_weight, o3.max_num_iterations)
+    for g, ref in zip(got, refs):
+        assert ref["matched"] and np.float32(g[7]) == np.float32(ref["score"])
+        t, q = ref["pose"]
+        (rt, rq), _ = oracle.ceres3d_match(og_h, og_l, pt, pt, copts, t, t, q)
+        assert np.allclose(g[0:3], rt, atol=1e-6), (g, rt)
+        assert np.allclose(g[3:7], rq, atol=1e-6), (g, rq)
 
 
 def _test_options(cb, csm):
