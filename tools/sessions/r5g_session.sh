@@ -28,4 +28,6 @@ for c in 0,0,2,2,2,3,3,3,3,3,3,3 0,1,2,2,2,3,3,3,3,3,3,3 0,0,1,2,2,3,3,3,3,3,3,3
          0,0,2,2,2,3,3,3,3,3,3,3; do
   run cluster=$c CSM_CLUSTER=$c
 done
+# Hex-level sets not measured on C3 in round 4 (r4ad had {8,6} best of six).
+for v in 8 6 8,6,2 8,6; do run hex=$v CSM_HEX_LEVELS=$v; done
 date +%T
