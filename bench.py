@@ -80,6 +80,10 @@ def parse():
     p.add_argument("--c5-groups", type=int, default=4,
                    help="C5: submap groups per step; group g + 1 builds while group g is searched "
                         "(1: build all, then search all)")
+    p.add_argument("--c5-first-group", type=int, default=0,
+                   help="C5: submaps in the first group (its build is exposed; 0: an even split)")
+    p.add_argument("--c5-create", choices=("single", "batch"), default="single",
+                   help="C5: one csm_fast3d_create per submap, or one csm_fast3d_create_batch per group")
     p.add_argument("--c3-nodes", type=int, default=2000)
     p.add_argument("--c3-submaps", type=int, default=1000)
     p.add_argument("--c3-slice", type=int, default=50, help="submaps of the queue per step")
@@ -761,8 +765,11 @@ def fast3d_bench(csm, ctx, args, rank=0, world_size=1, dist=None, coll_dev=None,
         # pyramid builds on the device while the host prepares the next
         # (csm_fast3d_create_batch, one launch per level for all submaps,
         # measured slower here: its builds start only after the last grid).
-        m = [csm.FastCorrelativeScanMatcher3D(gg[0], gg[1], w.submap_hist[s], o, bc)
-             for s, gg in zip(subs, g)]
+        if args.c5_create == "batch":
+            m = csm.FastCorrelativeScanMatcher3D.create_batch(g, [w.submap_hist[s] for s in subs], o, bc)
+        else:
+            m = [csm.FastCorrelativeScanMatcher3D(gg[0], gg[1], w.submap_hist[s], o, bc)
+                 for s, gg in zip(subs, g)]
         return g, m
 
     def close(g, m):
@@ -789,7 +796,10 @@ def fast3d_bench(csm, ctx, args, rank=0, world_size=1, dist=None, coll_dev=None,
     # find them) is outside it, reported as release_ms_per_step.
     phase = {"build": 0.0, "search": 0.0, "release": 0.0}
 
-    groups = [g for g in np.array_split(np.arange(w.num_submaps), max(1, args.c5_groups)) if len(g)]
+    ids = np.arange(w.num_submaps)
+    f = min(args.c5_first_group, w.num_submaps) if args.c5_groups > 1 else 0
+    groups = [g for g in ([ids[:f]] if f else []) +
+              np.array_split(ids[f:], max(1, args.c5_groups - (1 if f else 0))) if len(g)]
 
     def step():
         a = time.perf_counter()
@@ -869,7 +879,8 @@ def fast3d_bench(csm, ctx, args, rank=0, world_size=1, dist=None, coll_dev=None,
                                         for name, code in (("ancestors", csm.TIE_ANCESTORS),
                                                            ("toplist", csm.TIE_TOPLIST),
                                                            ("walk", csm.TIE_WALK))},
-           "c5_groups": len(groups),
+           "c5_groups": len(groups), "c5_group_sizes": [len(g) for g in groups],
+           "c5_create": args.c5_create,
            # Builds' exposed time: all of it with one group; with several, the
            # first group's build and any wait for a later one.
            "build_ms_per_step": phase["build"] / reps * 1e3,

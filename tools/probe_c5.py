@@ -1,5 +1,5 @@
 """C5 leg alone (bench.fast3d_bench, no CPU baseline), for host/kernel
-phase profiling: CSM_PROFILE3D=1 python tools/probe_c5.py"""
+phase profiling: CSM_PROFILE3D=1 python tools/probe_c5.py [bench C5 flags]"""
 import json
 import os
 import sys
@@ -10,7 +10,7 @@ import bench  # noqa: E402
 
 
 def main():
-    sys.argv = [sys.argv[0], "--no-cpu"]
+    sys.argv = [sys.argv[0], "--no-cpu"] + sys.argv[1:]
     args = bench.parse()
     csm = bench.load_pkg()
     ctx = csm.Context(0)
