@@ -175,10 +175,11 @@ CSM_HD inline void UnpackLeafKey(uint64_t key, uint32_t* sum, int* rot, int* xo,
 // batches per level, 4 CSM_KPROF phase counters, the DFS stack high-water
 // mark (max over workgroups, entries).
 constexpr int kStatHighWater = 2 + 2 * kMaxLevels + 4;
-// CSM_KPROF builds: distinct 128-byte lines and gather instructions per child
-// level (the texture path's cost model).
+// CSM_KPROF builds: distinct 128-byte lines, gather instructions and quad
+// lines (distinct lines summed over the 4-lane groups) per child level (the
+// texture path's cost model).
 constexpr int kStatLines = kStatHighWater + 1;
-constexpr int kStatsWords = kStatLines + 2 * kMaxLevels;
+constexpr int kStatsWords = kStatLines + 3 * kMaxLevels;
 
 // Per-pair status written by the search kernel (0 = ok).
 constexpr int32_t kStatusRange = 1;

@@ -1024,6 +1024,11 @@ int RunBatch(csm_context* ctx, csm_fast2d* const* submaps, int32_t num_submaps,
                        static_cast<double>(kl[l]) / kl[kMaxLevels + l],
                        static_cast<double>(kl[kMaxLevels + l]));
       std::fprintf(stderr, "\n");
+      std::fprintf(stderr, "fast2d quad lines per gather by child level:");
+      for (int l = 0; l < kMaxLevels; ++l)
+        if (kl[kMaxLevels + l])
+          std::fprintf(stderr, " L%d %.1f", l, static_cast<double>(kl[2 * kMaxLevels + l]) / kl[kMaxLevels + l]);
+      std::fprintf(stderr, "\n");
     }
   }
 

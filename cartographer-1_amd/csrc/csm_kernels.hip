@@ -676,6 +676,13 @@ template <int kKids>
 struct V4Shared {
   // LDS part of the DFS stack (v5: a quarter, so 6 workgroups fit a CU's
   // LDS with their 16-child sums); the rest spills to global memory.
+#ifndef CSM_LANE_SORT
+// 1: the scoring lanes take the batch's nodes in (level, rotation, y, x)
+// order (wave 0 sorts the popped batch), so that nodes on one row of one
+// plane sit in the same 4-lane groups; the node slots, and so the push
+// order, stay as popped.
+#define CSM_LANE_SORT 0
+#endif
 #ifndef CSM_V4_RING
 #define CSM_V4_RING 0  // LDS stack entries (0: 1024 for v4, 256 for v5)
 #endif
@@ -705,7 +712,10 @@ struct V4Shared {
   // quad_off, 4 * quad_pws, plane bytes, quad_bias, cshift.
   int lv[kMaxLevels][8];
 #ifdef CSM_KPROF
-  unsigned long long kp_lines[kMaxLevels], kp_instr[kMaxLevels];
+  unsigned long long kp_lines[kMaxLevels], kp_instr[kMaxLevels], kp_qlines[kMaxLevels];
+#endif
+#if CSM_LANE_SORT
+  int lane_node[kBatchNodes];  // scoring lane slot -> node (CSM_LANE_SORT)
 #endif
 };
 
@@ -734,11 +744,19 @@ __device__ void CountLines(Shared& sh, int level, int ad, int oob) {
     const int o = __shfl(line, (lane + 64 - j) & 63, 64);
     if (lane >= j && o == line) first = false;
   }
+  // First lane of its line within its 4-lane group.
+  bool qfirst = valid;
+  for (int j = 1; j < 4; ++j) {
+    const int o = __shfl(line, (lane & ~3) | ((lane - j) & 3), 64);
+    if ((lane & 3) >= j && o == line) qfirst = false;
+  }
   const int n = __popcll(__ballot(first));
+  const int nq = __popcll(__ballot(qfirst));
   const int lv = __builtin_amdgcn_readfirstlane(level);
   if (__builtin_amdgcn_readfirstlane(lane) == lane) {
     atomicAdd(&sh.kp_lines[lv], static_cast<unsigned long long>(n));
     atomicAdd(&sh.kp_instr[lv], 1ull);
+    atomicAdd(&sh.kp_qlines[lv], static_cast<unsigned long long>(nq));
   }
 }
 #define CSM_COUNT_LINES(lvl, ad, oob) CountLines(sh, (lvl), (ad), (oob))
@@ -768,7 +786,11 @@ __device__ __forceinline__ void V4Score(Shared& sh, const uint32_t* cells, const
   const int pw = nodes <= 1 ? 1 : 1 << (32 - __clz(nodes - 1));
   const int groups = 64 / pw;
   const bool active = (lane & (pw - 1)) < nodes;
+#if CSM_LANE_SORT
+  const int node = active ? sh.lane_node[lane & (pw - 1)] : 0;
+#else
   const int node = active ? lane & (pw - 1) : 0;
+#endif
   const int g = lane / pw;
   // Each node scores its children at its own child level: one descriptor
   // spans the whole pyramid, the level is a per-lane byte offset.
@@ -846,10 +868,15 @@ __device__ __forceinline__ void V4Score(Shared& sh, const uint32_t* cells, const
     a3 += __shfl_xor(a3, m, 64);
   }
   if (lane < nodes) {
-    atomicAdd(&sh.part[lane][0], static_cast<int>(a0));  // (xo,     yo)
-    atomicAdd(&sh.part[lane][1], static_cast<int>(a1));  // (xo,     yo + h)
-    atomicAdd(&sh.part[lane][2], static_cast<int>(a2));  // (xo + h, yo)
-    atomicAdd(&sh.part[lane][3], static_cast<int>(a3));  // (xo + h, yo + h)
+#if CSM_LANE_SORT
+    const int nd = sh.lane_node[lane];
+#else
+    const int nd = lane;
+#endif
+    atomicAdd(&sh.part[nd][0], static_cast<int>(a0));  // (xo,     yo)
+    atomicAdd(&sh.part[nd][1], static_cast<int>(a1));  // (xo,     yo + h)
+    atomicAdd(&sh.part[nd][2], static_cast<int>(a2));  // (xo + h, yo)
+    atomicAdd(&sh.part[nd][3], static_cast<int>(a3));  // (xo + h, yo + h)
   }
 }
 
@@ -867,7 +894,11 @@ __device__ __forceinline__ void V4ScoreHex(Shared& sh, const uint32_t* cells, co
   const int pw = nodes <= 1 ? 1 : 1 << (32 - __clz(nodes - 1));  // as V4Score
   const int groups = 64 / pw;
   const bool active = (lane & (pw - 1)) < nodes;
+#if CSM_LANE_SORT
+  const int node = active ? sh.lane_node[lane & (pw - 1)] : 0;
+#else
   const int node = active ? lane & (pw - 1) : 0;
+#endif
   const int g = lane / pw;
   const int level = sh.node_level[node] - 2;
   const int* L = sh.lv[level];
@@ -961,8 +992,13 @@ __device__ __forceinline__ void V4ScoreHex(Shared& sh, const uint32_t* cells, co
     for (int j = 0; j < 16; ++j) acc[j] += __shfl_xor(acc[j], m, 64);
   }
   if (lane < nodes) {
+#if CSM_LANE_SORT
+    const int nd = sh.lane_node[lane];
+#else
+    const int nd = lane;
+#endif
 #pragma unroll
-    for (int j = 0; j < 16; ++j) atomicAdd(&sh.part[lane][j], static_cast<int>(acc[j]));
+    for (int j = 0; j < 16; ++j) atomicAdd(&sh.part[nd][j], static_cast<int>(acc[j]));
   }
 }
 
@@ -1108,7 +1144,7 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
   if (tid == 0) sh.queue = blockIdx.x % kNumXcd;
   unsigned long long lv_cands = 0, lv_batches = 0;  // wave 0, lane l: child level l
 #ifdef CSM_KPROF
-  if (tid < kMaxLevels) { sh.kp_lines[tid] = 0; sh.kp_instr[tid] = 0; }
+  if (tid < kMaxLevels) { sh.kp_lines[tid] = 0; sh.kp_instr[tid] = 0; sh.kp_qlines[tid] = 0; }
 #endif
   int tries = 0;
   __syncthreads();
@@ -1546,6 +1582,25 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
             }
             blen = DppMax(len);
             bent = DppSum(len);
+#if CSM_LANE_SORT
+            {
+              // Bitonic sort of (level, rotation, y, x, slot) over the wave;
+              // lane i ends with the i-th smallest key and records its slot.
+              const uint32_t ux = (ent.x & 0xffffu) ^ 0x8000u, uy = (ent.x >> 16) ^ 0x8000u;
+              uint64_t key = took ? (static_cast<uint64_t>(ent.y >> 22) << 38) |
+                                        (static_cast<uint64_t>(uy) << 22) |
+                                        (static_cast<uint64_t>(ux) << 6) | static_cast<uint64_t>(rank)
+                                  : ~0ull;
+              for (int k = 2; k <= 64; k <<= 1) {
+                for (int j = k >> 1; j > 0; j >>= 1) {
+                  const uint64_t o = __shfl_xor(key, j, 64);
+                  const bool keep_min = ((lane & j) == 0) == ((lane & k) == 0);
+                  key = keep_min ? (o < key ? o : key) : (o > key ? o : key);
+                }
+              }
+              if (lane < nodes) sh.lane_node[lane] = static_cast<int>(key & 63u);
+            }
+#endif
             // Per child level: candidates scored and batches (lane l counts
             // level l; one pass per distinct level, usually one).
             const int cl = static_cast<int>(ent.y >> 27) - (hexb ? 2 : 1);
@@ -1621,6 +1676,7 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
   if (stats && tid < kMaxLevels) {
     atomicAdd(&stats[kStatLines + tid], sh.kp_lines[tid]);
     atomicAdd(&stats[kStatLines + kMaxLevels + tid], sh.kp_instr[tid]);
+    atomicAdd(&stats[kStatLines + 2 * kMaxLevels + tid], sh.kp_qlines[tid]);
   }
 #endif
 }
