@@ -77,12 +77,15 @@ def parse():
     p.add_argument("--submaps3d", type=int, default=200,
                    help="C5 submaps in total, split over the ranks")
     p.add_argument("--steps3d", type=int, default=3)
-    p.add_argument("--c5-groups", type=int, default=4,
+    p.add_argument("--c5-groups", type=int, default=12,
                    help="C5: submap groups per step; group g + 1 builds while group g is searched "
                         "(1: build all, then search all)")
-    p.add_argument("--c5-first-group", type=int, default=0,
+    p.add_argument("--c5-search-streams", type=int, default=2,
+                   help="C5: contexts (streams) the groups' searches alternate over, one host "
+                        "thread each, so one group's host phases overlap another's kernel")
+    p.add_argument("--c5-first-group", type=int, default=6,
                    help="C5: submaps in the first group (its build is exposed; 0: an even split)")
-    p.add_argument("--c5-create", choices=("single", "batch"), default="single",
+    p.add_argument("--c5-create", choices=("single", "batch"), default="batch",
                    help="C5: one csm_fast3d_create per submap, or one csm_fast3d_create_batch per group")
     p.add_argument("--c3-nodes", type=int, default=2000)
     p.add_argument("--c3-submaps", type=int, default=1000)
@@ -752,6 +755,11 @@ def fast3d_bench(csm, ctx, args, rank=0, world_size=1, dist=None, coll_dev=None,
     bctx = csm.Context(ctx.device) if args.c5_groups > 1 else ctx
     from concurrent.futures import ThreadPoolExecutor
     pool = ThreadPoolExecutor(max_workers=1) if args.c5_groups > 1 else None
+    # Searches: group g on sctxs[g % K], from K host threads (the builder's
+    # constraint tasks run on a thread pool, constraint_builder_3d.cc:200-230).
+    nsearch = max(1, args.c5_search_streams) if pool is not None else 1
+    sctxs = [ctx] + [csm.Context(ctx.device) for _ in range(nsearch - 1)]
+    spool = ThreadPoolExecutor(max_workers=nsearch) if nsearch > 1 else None
 
     def build(subs=None, bc=None):
         """The submaps' HybridGrids and PrecomputationGridStack3D pyramids
@@ -761,10 +769,10 @@ def fast3d_bench(csm, ctx, args, rank=0, world_size=1, dist=None, coll_dev=None,
         g = [(csm.HybridGrid(w.high_resolution, *w.high_cells[s], context=bc),
               csm.HybridGrid(w.low_resolution, *w.low_cells[s], context=bc))
              for s in subs]
-        # One create per submap, as the builder makes them: each submap's
-        # pyramid builds on the device while the host prepares the next
-        # (csm_fast3d_create_batch, one launch per level for all submaps,
-        # measured slower here: its builds start only after the last grid).
+        # A group's matchers in one csm_fast3d_create_batch (one launch per
+        # level for the whole group), or one create per submap (--c5-create
+        # single). With the builds pipelined against the searches, the batch
+        # form's ~20 launches per group beat ~18 per submap (profiles/r5n/).
         if args.c5_create == "batch":
             m = csm.FastCorrelativeScanMatcher3D.create_batch(g, [w.submap_hist[s] for s in subs], o, bc)
         else:
@@ -807,7 +815,7 @@ def fast3d_bench(csm, ctx, args, rank=0, world_size=1, dist=None, coll_dev=None,
             g, m = build()
             b = time.perf_counter()
             res = csm.match_batch_3d(m, nodes, pairs, ctx)
-        else:
+        elif spool is None:
             g, m, parts, waited = [], [], [], 0.0
             fut = pool.submit(build, groups[0], bctx)
             for gi, grp in enumerate(groups):
@@ -824,6 +832,29 @@ def fast3d_bench(csm, ctx, args, rank=0, world_size=1, dist=None, coll_dev=None,
                 parts.append(csm.match_batch_3d(mm, nodes, gp, ctx))
             res = np.concatenate(parts)
             b = a + waited  # the builds' exposed time (the rest overlaps the searches)
+        else:
+            # Every group's build queued in order on the build thread; group
+            # g's search starts on its own thread once its build is issued.
+            bfuts = [pool.submit(build, grp, bctx) for grp in groups]
+
+            def search(gi):
+                grp = groups[gi]
+                _, mm = bfuts[gi].result()
+                lo, hi = int(grp[0]) * w.num_nodes, (int(grp[-1]) + 1) * w.num_nodes
+                gp = pairs[lo:hi].copy()
+                gp["submap"] -= int(grp[0])
+                return csm.match_batch_3d(mm, nodes, gp, sctxs[gi % nsearch])
+
+            sfuts = [spool.submit(search, gi) for gi in range(len(groups))]
+            bfuts[0].result()
+            b = time.perf_counter()  # the first group's build is exposed
+            parts = [f.result() for f in sfuts]
+            g, m = [], []
+            for f in bfuts:
+                gg, mm = f.result()
+                g += gg
+                m += mm
+            res = np.concatenate(parts)
         rec = cdist.make_records_3d(res, submission, sub_global, nod) if cdist else None
         if cdist is not None:
             rec = gather(rec) if gather is not None else \
@@ -836,8 +867,9 @@ def fast3d_bench(csm, ctx, args, rank=0, world_size=1, dist=None, coll_dev=None,
     _, _, kept = step()  # warm-up at full size (staging buffers, the pool)
     close(*kept)
     phase["build"] = phase["search"] = 0.0
-    ctx.reset_timing()
-    ctx.enable_timing(True)
+    for c in sctxs:
+        c.reset_timing()
+        c.enable_timing(True)
     reps = max(1, args.steps3d)
     errors3 = 0
     wall = 0.0
@@ -855,10 +887,13 @@ def fast3d_bench(csm, ctx, args, rank=0, world_size=1, dist=None, coll_dev=None,
     grids, mats = kept
     if pool is not None:
         pool.shutdown()
+    if spool is not None:
+        spool.shutdown()
     if rank == 0 and rec is not None:
         DUMP["c5"] = np.asarray(rec)
-    tm = ctx.timing()
-    ctx.enable_timing(False)
+    tm = merged_timing(sctxs)
+    for c in sctxs:
+        c.enable_timing(False)
     if cdist is not None:
         wall = cdist.max_over_ranks(wall, dist, coll_dev)
     total = w.num_nodes * S3 * reps
@@ -880,6 +915,7 @@ def fast3d_bench(csm, ctx, args, rank=0, world_size=1, dist=None, coll_dev=None,
                                                            ("toplist", csm.TIE_TOPLIST),
                                                            ("walk", csm.TIE_WALK))},
            "c5_groups": len(groups), "c5_group_sizes": [len(g) for g in groups],
+           "c5_search_streams": nsearch,
            "c5_create": args.c5_create,
            # Builds' exposed time: all of it with one group; with several, the
            # first group's build and any wait for a later one.
@@ -1139,6 +1175,17 @@ def parity_2d(sample, ores):
             "mismatched_pose": int(pose_bad.sum()), "gpu_errors": int((g["status"] < 0).sum()),
             "what": "the CPU baseline's sampled pairs: the GPU's results from the timed run vs the "
                     "oracle's (decision, float score bit-exact, pose exact)"}
+
+
+def merged_timing(contexts):
+    """The contexts' csm_timing summed field by field (the high-water mark
+    as a maximum)."""
+    ts = [c.timing() for c in contexts]
+    out = type(ts[0])()
+    for name, _ in out._fields_:
+        vals = [getattr(t, name) for t in ts]
+        setattr(out, name, max(vals) if name == "stack_high_water" else sum(vals))
+    return out
 
 
 def roofline_3d(tm):
