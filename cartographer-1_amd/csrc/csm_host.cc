@@ -1614,7 +1614,13 @@ static int SingleMatch(const csm_fast2d* m, const csm_pose2d* initial, int full,
         for (size_t i = 0; i < take_n; ++i) take.push_back(static_cast<SingleReq2*>(owner->co_queue[i]));
         owner->co_queue.erase(owner->co_queue.begin(), owner->co_queue.begin() + take_n);
         owner->co_last_batch = static_cast<int>(take_n);
-        const int share = owner->co_leaders;
+        // The batch's share of the persistent grid: the leaders running now
+        // (CSM_COALESCE_SHARE=n fixes it, A/B).
+        static const int fixed_share = [] {
+          const char* e = std::getenv("CSM_COALESCE_SHARE");
+          return e ? std::max(1, std::atoi(e)) : 0;
+        }();
+        const int share = fixed_share ? fixed_share : owner->co_leaders;
         lk.unlock();
         const int rc = RunSingleBatch(owner, take, share);
         lk.lock();
