@@ -179,7 +179,7 @@ constexpr int kStatHighWater = 2 + 2 * kMaxLevels + 4;
 // lines (distinct lines summed over the 4-lane groups) per child level (the
 // texture path's cost model).
 constexpr int kStatLines = kStatHighWater + 1;
-constexpr int kStatsWords = kStatLines + 3 * kMaxLevels;
+constexpr int kStatsWords = kStatLines + 5 * kMaxLevels;  // + active and out-of-range lanes
 
 // Per-pair status written by the search kernel (0 = ok).
 constexpr int32_t kStatusRange = 1;

@@ -1029,6 +1029,12 @@ int RunBatch(csm_context* ctx, csm_fast2d* const* submaps, int32_t num_submaps,
         if (kl[kMaxLevels + l])
           std::fprintf(stderr, " L%d %.1f", l, static_cast<double>(kl[2 * kMaxLevels + l]) / kl[kMaxLevels + l]);
       std::fprintf(stderr, "\n");
+      std::fprintf(stderr, "fast2d out-of-range / active lanes per gather by child level:");
+      for (int l = 0; l < kMaxLevels; ++l)
+        if (kl[kMaxLevels + l])
+          std::fprintf(stderr, " L%d %.1f/%.1f", l, static_cast<double>(kl[4 * kMaxLevels + l]) / kl[kMaxLevels + l],
+                       static_cast<double>(kl[3 * kMaxLevels + l]) / kl[kMaxLevels + l]);
+      std::fprintf(stderr, "\n");
     }
   }
 
@@ -1489,7 +1495,7 @@ constexpr int kCoalesceCap = 512;  // pairs per coalesced batch
 static int CoalesceLeaders() {
   static const int v = [] {
     const char* e = std::getenv("CSM_COALESCE_LEADERS");
-    return e ? std::max(1, std::atoi(e)) : 2;
+    return e ? std::max(1, std::atoi(e)) : 3;
   }();
   return v;
 }
@@ -1569,7 +1575,7 @@ static int RunSingleBatch(csm_context* owner, const std::vector<SingleReq2*>& re
 // ThreadPool workers (constraint_builder_2d.cc:100-111, :188-215). One call
 // is one pair, far too little to fill the GPU, so concurrent callers of one
 // owner context are coalesced: each queues its pair; a caller that finds
-// fewer than CoalesceLeaders() (2) batches running becomes a leader, waits up
+// fewer than CoalesceLeaders() (3) batches running becomes a leader, waits up
 // to CoalesceWindowUs() (150 us) for as many callers as the previous batch
 // had, takes the
 // queue and searches it as one batch on a call context, then wakes the
@@ -1614,11 +1620,14 @@ static int SingleMatch(const csm_fast2d* m, const csm_pose2d* initial, int full,
         for (size_t i = 0; i < take_n; ++i) take.push_back(static_cast<SingleReq2*>(owner->co_queue[i]));
         owner->co_queue.erase(owner->co_queue.begin(), owner->co_queue.begin() + take_n);
         owner->co_last_batch = static_cast<int>(take_n);
-        // The batch's share of the persistent grid: the leaders running now
-        // (CSM_COALESCE_SHARE=n fixes it, A/B).
+        // The batch's share of the persistent grid: the whole grid (a
+        // second batch's workgroups start as the first one's drain; measured
+        // 11.3k -> 12.7k pairs/s at 16 threads against a share per leader,
+        // profiles/r5r/). CSM_COALESCE_SHARE=n: 1/n of it; 0: one share per
+        // leader running.
         static const int fixed_share = [] {
           const char* e = std::getenv("CSM_COALESCE_SHARE");
-          return e ? std::max(1, std::atoi(e)) : 0;
+          return e ? std::max(0, std::atoi(e)) : 1;
         }();
         const int share = fixed_share ? fixed_share : owner->co_leaders;
         lk.unlock();

@@ -676,6 +676,11 @@ template <int kKids>
 struct V4Shared {
   // LDS part of the DFS stack (v5: a quarter, so 6 workgroups fit a CU's
   // LDS with their 16-child sums); the rest spills to global memory.
+#ifndef CSM_MASK_OOB
+// 1: lanes whose entry is out of range (off the plane, or past the node's
+// list) skip the gather instead of issuing it at the out-of-range offset.
+#define CSM_MASK_OOB 0
+#endif
 #ifndef CSM_LANE_SORT
 // 1: the scoring lanes take the batch's nodes in (level, rotation, y, x)
 // order (wave 0 sorts the popped batch), so that nodes on one row of one
@@ -713,6 +718,7 @@ struct V4Shared {
   int lv[kMaxLevels][8];
 #ifdef CSM_KPROF
   unsigned long long kp_lines[kMaxLevels], kp_instr[kMaxLevels], kp_qlines[kMaxLevels];
+  unsigned long long kp_active[kMaxLevels], kp_oob[kMaxLevels];
 #endif
 #if CSM_LANE_SORT
   int lane_node[kBatchNodes];  // scoring lane slot -> node (CSM_LANE_SORT)
@@ -752,11 +758,15 @@ __device__ void CountLines(Shared& sh, int level, int ad, int oob) {
   }
   const int n = __popcll(__ballot(first));
   const int nq = __popcll(__ballot(qfirst));
+  const int na = __popcll(__ballot(true));
+  const int no = __popcll(__ballot(!valid));
   const int lv = __builtin_amdgcn_readfirstlane(level);
   if (__builtin_amdgcn_readfirstlane(lane) == lane) {
     atomicAdd(&sh.kp_lines[lv], static_cast<unsigned long long>(n));
     atomicAdd(&sh.kp_instr[lv], 1ull);
     atomicAdd(&sh.kp_qlines[lv], static_cast<unsigned long long>(nq));
+    atomicAdd(&sh.kp_active[lv], static_cast<unsigned long long>(na));
+    atomicAdd(&sh.kp_oob[lv], static_cast<unsigned long long>(no));
   }
 }
 #define CSM_COUNT_LINES(lvl, ad, oob) CountLines(sh, (lvl), (ad), (oob))
@@ -849,7 +859,14 @@ __device__ __forceinline__ void V4Score(Shared& sh, const uint32_t* cells, const
       for (int u = 0; u < U; ++u) CSM_COUNT_LINES(level, ad[u], kOOB);
       uint32_t v[U];
   #pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, ad[u], 0, CSM_CPOL_QUAD);
+      for (int u = 0; u < U; ++u) {
+        if (CSM_MASK_OOB) {
+          v[u] = 0u;
+          if (ad[u] != kOOB) v[u] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, ad[u], 0, CSM_CPOL_QUAD);
+        } else {
+          v[u] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, ad[u], 0, CSM_CPOL_QUAD);
+        }
+      }
   #pragma unroll
       for (int u = 0; u < U; ++u) accumulate(v[u], c[u]);
     }
@@ -975,7 +992,14 @@ __device__ __forceinline__ void V4ScoreHex(Shared& sh, const uint32_t* cells, co
       for (int u = 0; u < U; ++u) CSM_COUNT_LINES(level, ad[u], kOOB);
       HexVec v[U];
   #pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = hload(ad[u]);
+      for (int u = 0; u < U; ++u) {
+        if (CSM_MASK_OOB) {
+          v[u] = HexVec{};
+          if (ad[u] != kOOB) v[u] = hload(ad[u]);
+        } else {
+          v[u] = hload(ad[u]);
+        }
+      }
   #pragma unroll
       for (int u = 0; u < U; ++u) accumulate(v[u], c[u]);
     }
@@ -1144,7 +1168,10 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
   if (tid == 0) sh.queue = blockIdx.x % kNumXcd;
   unsigned long long lv_cands = 0, lv_batches = 0;  // wave 0, lane l: child level l
 #ifdef CSM_KPROF
-  if (tid < kMaxLevels) { sh.kp_lines[tid] = 0; sh.kp_instr[tid] = 0; sh.kp_qlines[tid] = 0; }
+  if (tid < kMaxLevels) {
+    sh.kp_lines[tid] = 0; sh.kp_instr[tid] = 0; sh.kp_qlines[tid] = 0;
+    sh.kp_active[tid] = 0; sh.kp_oob[tid] = 0;
+  }
 #endif
   int tries = 0;
   __syncthreads();
@@ -1677,6 +1704,8 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
     atomicAdd(&stats[kStatLines + tid], sh.kp_lines[tid]);
     atomicAdd(&stats[kStatLines + kMaxLevels + tid], sh.kp_instr[tid]);
     atomicAdd(&stats[kStatLines + 2 * kMaxLevels + tid], sh.kp_qlines[tid]);
+    atomicAdd(&stats[kStatLines + 3 * kMaxLevels + tid], sh.kp_active[tid]);
+    atomicAdd(&stats[kStatLines + 4 * kMaxLevels + tid], sh.kp_oob[tid]);
   }
 #endif
 }
