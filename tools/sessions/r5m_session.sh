@@ -8,7 +8,7 @@ mkdir -p $O
 CSM_PROFILE3D=1 timeout -k 10 300 python -u tools/probe_c5.py > $O/c5prof.json 2> $O/c5prof.err || { tail -20 $O/c5prof.err; exit 1; }
 bash tools/gpu_measure.sh $O c5 || exit 1
 TAG3=$(python3 -c "import sys; sys.path.insert(0,'.'); import bench; print(bench.KERNEL3D_TAG)")
-python3 tools/traffic3d_json.py $O/pmc3d $O/traffic_c5.json $TAG3 || exit 1
+python3 tools/traffic3d_json.py $O/pmc3d $O/traffic_c5.json $TAG3 $O/c5.json || exit 1
 # C5 step shape A/B: first-group size and batched matcher creation.
 ab() {
   local label=$1; shift

@@ -4,7 +4,11 @@ tracing): HBM-side bytes per fast3d_search dispatch = FETCH_SIZE (KB) x 1024
 x 2 (the gfx950 correction, MI355X_MICROARCH.md), plus the texture-path and
 L2 counters per dispatch, tied to bench.py's KERNEL3D_TAG.
 
-    python tools/traffic3d_json.py PMC3D_DIR OUT_JSON KERNEL3D_TAG
+    python tools/traffic3d_json.py PMC3D_DIR OUT_JSON KERNEL3D_TAG [PROBE_JSON]
+
+PROBE_JSON (the probe's own output in the same session) adds the traffic
+per algorithmic byte, so bench.py can scale it to launches of another size
+(the C5 step's groups differ in size).
 """
 import collections
 import csv
@@ -15,6 +19,7 @@ import sys
 
 def main():
     pmc, out, tag = sys.argv[1:4]
+    probe = json.load(open(sys.argv[4])) if len(sys.argv) > 4 else None
     per = collections.defaultdict(lambda: collections.defaultdict(float))
     for f in glob.glob(f"{pmc}/p*/**/*counter_collection.csv", recursive=True):
         pass_id = f.split("/p", 1)[1].split("/", 1)[0] if "/p" in f else "0"
@@ -36,6 +41,11 @@ def main():
          "counters_per_dispatch": avg, "gfx950_fetch_correction": 2.0,
          "traffic_bytes_per_launch": kb * 1024 * 2.0 if kb else None,
          "source": f"rocprofv3 --pmc passes (own passes, no tracing); {pmc}"}
+    if probe and kb:
+        launches_per_step = probe["roofline"]["launches"] / max(probe["steps"], 1)
+        lookups_per_launch = probe["lookups_per_step"] / launches_per_step
+        t["algorithmic_bytes_per_launch"] = lookups_per_launch
+        t["traffic_bytes_per_algorithmic_byte"] = t["traffic_bytes_per_launch"] / lookups_per_launch
     json.dump(t, open(out, "w"), indent=1)
     print(json.dumps(t))
 
