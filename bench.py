@@ -83,6 +83,8 @@ def parse():
     p.add_argument("--c5-search-streams", type=int, default=2,
                    help="C5: contexts (streams) the groups' searches alternate over, one host "
                         "thread each, so one group's host phases overlap another's kernel")
+    p.add_argument("--c5-dropin-calls", type=int, default=4000,
+                   help="C5: single MatchFullSubmap calls from 16 threads (Option A), 0: skip")
     p.add_argument("--c5-first-group", type=int, default=6,
                    help="C5: submaps in the first group (its build is exposed; 0: an even split)")
     p.add_argument("--c5-create", choices=("single", "batch"), default="batch",
@@ -943,6 +945,8 @@ def fast3d_bench(csm, ctx, args, rank=0, world_size=1, dist=None, coll_dev=None,
                           "mean_iterations": float(np.mean(it3)),
                           "workload": "CeresScanMatcher3D::Match on one C5 step's accepted "
                                       "matches (pose_graph.lua options)"}
+    if args.c5_dropin_calls > 0:
+        out["dropin"] = dropin_3d(csm, w, mats, sub, nod, rot, res3, args.c5_dropin_calls)
     if not args.no_cpu:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import ctypes as C
@@ -1175,6 +1179,39 @@ def parity_2d(sample, ores):
             "mismatched_pose": int(pose_bad.sum()), "gpu_errors": int((g["status"] < 0).sum()),
             "what": "the CPU baseline's sampled pairs: the GPU's results from the timed run vs the "
                     "oracle's (decision, float score bit-exact, pose exact)"}
+
+
+def dropin_3d(csm, w, mats, sub, nod, rot, res3, calls, threads=16):
+    """Option A in 3D: single MatchFullSubmap calls on the last C5 step's
+    matchers from `threads` host threads, as the builder's thread pool issues
+    them (constraint_builder_3d.cc:200-230); the library coalesces concurrent
+    calls into batches (host3d.cc SingleMatch3). Each result must equal the
+    timed batch's result of the same pair."""
+    from concurrent.futures import ThreadPoolExecutor
+    pick = np.random.RandomState(7).randint(0, len(sub), calls)
+    node_objs = [w.node(i) for i in range(w.num_nodes)]
+    ident = (1.0, 0.0, 0.0, 0.0)
+
+    def one(i):
+        n = int(nod[i])
+        return mats[int(sub[i])].MatchFullSubmap(rot[n], ident, node_objs[n], 0.6)
+
+    with ThreadPoolExecutor(max_workers=threads) as ex:
+        list(ex.map(one, pick[:64]))  # warm-up: call contexts, staging
+        a = time.perf_counter()
+        got = list(ex.map(one, pick))
+        el = time.perf_counter() - a
+    mism = 0
+    for i, g in zip(pick, got):
+        ok = res3["status"][i] == csm.CSM_OK
+        if (g is not None) != ok or (ok and (np.float32(g.score) != np.float32(res3["score"][i]) or
+                                            g.pose_estimate != (tuple(res3["t"][i]), tuple(res3["q"][i])))):
+            mism += 1
+    if mism:
+        raise RuntimeError(f"C5 single calls: {mism} of {calls} differ from the batch's results")
+    return {"calls": int(calls), "threads": threads, "pairs_per_s": calls / el,
+            "matched": int(sum(g is not None for g in got)), "mismatches_vs_batch": mism,
+            "note": "single csm_fast3d_match_full_submap calls, coalesced by the library"}
 
 
 def merged_timing(contexts):

@@ -185,6 +185,10 @@ struct csm_context {
   std::vector<void*> co_queue;
   int co_leaders = 0;
   int co_last_batch = 1;  // the last batch's size: the next leader waits for as many
+  // The same for single 3D calls (host3d.cc SingleMatch3), under co_mu.
+  std::vector<void*> co3_queue;
+  int co3_leaders = 0;
+  int co3_last_batch = 1;
   csm_timing call_t{};                // finished single calls' timing (call_mu)
   csm_scan_set single;                // the cloud of the current single 2D call
   csm::PinnedBuf single_stage;

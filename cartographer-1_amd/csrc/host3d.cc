@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <array>
 #include <limits>
+#include <map>
 #include <tuple>
 #include <atomic>
 #include <chrono>
@@ -2080,6 +2081,116 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
   return CSM_OK;
 }
 
+namespace {
+
+// One single Match / MatchFullSubmap call waiting in its owner's queue.
+struct SingleReq3 {
+  const csm_fast3d* m;
+  csm_pair3d pair;
+  const csm_node3d* node;
+  csm_result3d res;
+  int rc;
+  bool done;
+};
+
+constexpr int kCoalesceCap3 = 512;  // pairs per coalesced batch
+
+// Searches queued single calls as one batch on a call context of `owner`:
+// the distinct matchers as the batch's submaps, one node per request.
+int RunSingleBatch3(csm_context* owner, const std::vector<SingleReq3*>& reqs) {
+  csm::CallContext cc(owner);
+  csm_context* ctx = cc.get();
+  if (!ctx) return CSM_EHIP;
+  std::vector<csm_fast3d*> subs;
+  std::map<const csm_fast3d*, int> slot;
+  std::vector<csm_node3d> nodes(reqs.size());
+  std::vector<csm_pair3d> pairs(reqs.size());
+  for (size_t k = 0; k < reqs.size(); ++k) {
+    auto it = slot.find(reqs[k]->m);
+    if (it == slot.end()) {
+      it = slot.emplace(reqs[k]->m, static_cast<int>(subs.size())).first;
+      subs.push_back(const_cast<csm_fast3d*>(reqs[k]->m));
+    }
+    nodes[k] = *reqs[k]->node;
+    pairs[k] = reqs[k]->pair;
+    pairs[k].submap = it->second;
+    pairs[k].node = static_cast<int32_t>(k);
+  }
+  std::vector<csm_result3d> res(reqs.size());
+  const int rc = csm_fast3d_match_batch(ctx, subs.data(), static_cast<int32_t>(subs.size()), nodes.data(),
+                                        static_cast<int32_t>(nodes.size()), pairs.data(),
+                                        static_cast<int64_t>(pairs.size()), res.data());
+  if (rc < 0) return rc;
+  for (size_t k = 0; k < reqs.size(); ++k) reqs[k]->res = res[k];
+  return CSM_OK;
+}
+
+// Concurrent single 3D calls on one owner context are coalesced as in 2D
+// (csm_host.cc SingleMatch): each queues its pair; a caller that finds fewer
+// than CSM_COALESCE_LEADERS (3) batches running becomes a leader, waits up
+// to CSM_COALESCE_WINDOW_US (150 us) for as many callers as the previous
+// batch had, searches the queue as one batch and wakes the callers it
+// served. A pair's result does not depend on its batch.
+// CSM_SINGLE_COALESCE=0: each call alone on its own call context.
+int SingleMatch3(const csm_fast3d* m, const csm_pair3d& pair, const csm_node3d* node,
+                 csm_result3d* result) {
+  csm_context* owner = m->ctx;
+  SingleReq3 r{m, pair, node, csm_result3d{}, CSM_OK, false};
+  static const bool coalesce = [] {
+    const char* e = std::getenv("CSM_SINGLE_COALESCE");
+    return !(e && std::strcmp(e, "0") == 0);
+  }();
+  static const int leaders = [] {
+    const char* e = std::getenv("CSM_COALESCE_LEADERS");
+    return e ? std::max(1, std::atoi(e)) : 3;
+  }();
+  static const int window_us = [] {
+    const char* e = std::getenv("CSM_COALESCE_WINDOW_US");
+    return e ? std::max(0, std::atoi(e)) : 150;
+  }();
+  if (!coalesce) {
+    std::vector<SingleReq3*> one{&r};
+    r.rc = RunSingleBatch3(owner, one);
+  } else {
+    std::unique_lock<std::mutex> lk(owner->co_mu);
+    owner->co3_queue.push_back(&r);
+    owner->co_cv.notify_all();
+    while (!r.done) {
+      const bool queued = std::find(owner->co3_queue.begin(), owner->co3_queue.end(), &r) !=
+                          owner->co3_queue.end();
+      if (queued && owner->co3_leaders < leaders) {
+        ++owner->co3_leaders;
+        const size_t want = static_cast<size_t>(std::max(1, owner->co3_last_batch));
+        const auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(window_us);
+        while (owner->co3_queue.size() < want &&
+               owner->co_cv.wait_until(lk, deadline) != std::cv_status::timeout) {
+        }
+        const size_t take_n = std::min<size_t>(owner->co3_queue.size(), kCoalesceCap3);
+        std::vector<SingleReq3*> take;
+        for (size_t i = 0; i < take_n; ++i) take.push_back(static_cast<SingleReq3*>(owner->co3_queue[i]));
+        owner->co3_queue.erase(owner->co3_queue.begin(), owner->co3_queue.begin() + take_n);
+        owner->co3_last_batch = static_cast<int>(take_n);
+        lk.unlock();
+        const int rc = RunSingleBatch3(owner, take);
+        lk.lock();
+        for (SingleReq3* q : take) {
+          q->rc = rc;
+          q->done = true;
+        }
+        --owner->co3_leaders;
+        owner->co_cv.notify_all();
+      } else {
+        owner->co_cv.wait(lk);
+      }
+    }
+  }
+  *result = r.res;
+  if (r.rc < 0) return r.rc;
+  return result->status;
+}
+
+}  // namespace
+
 int csm_fast3d_match(const csm_fast3d* m, const csm_pose3d* node_pose,
                      const csm_pose3d* submap_pose, const csm_node3d* node, float min_score,
                      csm_result3d* result) {
@@ -2091,12 +2202,7 @@ int csm_fast3d_match(const csm_fast3d* m, const csm_pose3d* node_pose,
   p.min_score = min_score;
   p.node_pose = *node_pose;
   p.submap_pose = *submap_pose;
-  csm_fast3d* h = const_cast<csm_fast3d*>(m);
-  csm::CallContext cc(m->ctx);  // this call's stream and scratch (csm_internal.h)
-  if (!cc.get()) return CSM_EHIP;
-  const int rc = csm_fast3d_match_batch(cc.get(), &h, 1, node, 1, &p, 1, result);
-  if (rc < 0) return rc;
-  return result->status;
+  return SingleMatch3(m, p, node, result);
 }
 
 int csm_fast3d_match_full_submap(const csm_fast3d* m, const double* node_rotation,
@@ -2110,10 +2216,5 @@ int csm_fast3d_match_full_submap(const csm_fast3d* m, const double* node_rotatio
     p.node_pose.q[k] = node_rotation[k];
     p.submap_pose.q[k] = submap_rotation[k];
   }
-  csm_fast3d* h = const_cast<csm_fast3d*>(m);
-  csm::CallContext cc(m->ctx);  // this call's stream and scratch (csm_internal.h)
-  if (!cc.get()) return CSM_EHIP;
-  const int rc = csm_fast3d_match_batch(cc.get(), &h, 1, node, 1, &p, 1, result);
-  if (rc < 0) return rc;
-  return result->status;
+  return SingleMatch3(m, p, node, result);
 }

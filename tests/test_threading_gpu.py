@@ -181,6 +181,39 @@ def test_threads_3d_single_calls(csm):
     assert matched >= 2
 
 
+def test_threads_3d_single_calls_several_matchers(csm):
+    """Concurrent single 3D calls on three matchers of one context are
+    coalesced into shared batches (host3d.cc SingleMatch3): 16 threads, each
+    result equal to the batch path's for the same pair."""
+    w = csm.SyntheticWorld3D(num_nodes=24, num_submaps=3, seed=7)
+    o = csm.FastCorrelativeScanMatcherOptions3D()
+    ctx = csm.Context(0)
+    ms = [csm.FastCorrelativeScanMatcher3D(csm.HybridGrid(w.high_resolution, *w.high_cells[s], context=ctx),
+                                           csm.HybridGrid(w.low_resolution, *w.low_cells[s], context=ctx),
+                                           w.submap_hist[s], o, ctx)
+          for s in range(w.num_submaps)]
+    ident = ((0, 0, 0), (1, 0, 0, 0))
+    nodes = [w.node(n) for n in range(w.num_nodes)]
+    pairs = [(s, n, True, 0.55, ((0, 0, 0), w.node_rotation(n)), ident)
+             for s in range(w.num_submaps) for n in range(w.num_nodes)]
+    batch = csm.match_batch_3d(ms, nodes, pairs, ctx)
+
+    def single(p):
+        s, n, _, ms_, npose, spose = p
+        return ms[s].MatchFullSubmap(npose[1], spose[1], nodes[n], ms_)
+
+    with ThreadPoolExecutor(max_workers=16) as ex:
+        got = list(ex.map(single, pairs * 2))
+    matched = 0
+    for p, g, r in zip(pairs * 2, got, batch * 2):
+        assert (g is not None) == (r.status == csm.CSM_OK), (p, g, r.status)
+        if g is not None:
+            matched += 1
+            assert np.float32(g.score) == np.float32(r.score)
+            assert g.pose_estimate == r.pose.as_tuple()
+    assert matched >= 4
+
+
 def test_cpp_threads_match_single_thread_results():
     """The threading contract from C++ threads (no GIL): 16 threads call
     csm_fast2d_match_full_submap on shared matchers at once; every result
