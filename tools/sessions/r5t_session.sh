@@ -9,7 +9,7 @@ date +%T
 timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_threading_gpu.py \
   > $O/threading.log 2>&1 || { tail -30 $O/threading.log; exit 1; }
 tail -1 $O/threading.log
-(cd /tmp && export TMPDIR=/tmp && timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $R/$O/trace -o bench \
+(cd /tmp && export TMPDIR=/tmp && timeout -k 10 780 rocprofv3 --kernel-trace --stats -d $R/$O/trace -o bench \
   --output-format csv -- python3 $R/bench.py > $R/$O/bench_full.json 2> $R/$O/bench_full.err) \
   || { tail -30 $O/bench_full.err; exit 1; }
 date +%T
