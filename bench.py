@@ -763,14 +763,29 @@ def fast3d_bench(csm, ctx, args, rank=0, world_size=1, dist=None, coll_dev=None,
     sctxs = [ctx] + [csm.Context(ctx.device) for _ in range(nsearch - 1)]
     spool = ThreadPoolExecutor(max_workers=nsearch) if nsearch > 1 else None
 
+    # CSM_C5_TRACE=1: host timestamps of each group's build and search
+    # (stderr), to see what the step waits on.
+    c5_trace = [] if os.environ.get("CSM_C5_TRACE") else None
+
     def build(subs=None, bc=None):
         """The submaps' HybridGrids and PrecomputationGridStack3D pyramids
         (DispatchScanMatcherConstruction, constraint_builder_3d.cc:170-198)."""
+        if c5_trace is not None:
+            c5_trace.append(("build+", len(c5_trace), time.perf_counter()))
+            try:
+                return build_(subs, bc)
+            finally:
+                c5_trace.append(("build-", len(c5_trace), time.perf_counter()))
+        return build_(subs, bc)
+
+    def build_(subs=None, bc=None):
         bc = bc or ctx
         subs = range(w.num_submaps) if subs is None else subs
         g = [(csm.HybridGrid(w.high_resolution, *w.high_cells[s], context=bc),
               csm.HybridGrid(w.low_resolution, *w.low_cells[s], context=bc))
              for s in subs]
+        if c5_trace is not None:
+            c5_trace.append(("grids", len(c5_trace), time.perf_counter()))
         # A group's matchers in one csm_fast3d_create_batch (one launch per
         # level for the whole group), or one create per submap (--c5-create
         # single). With the builds pipelined against the searches, the batch
@@ -845,7 +860,12 @@ def fast3d_bench(csm, ctx, args, rank=0, world_size=1, dist=None, coll_dev=None,
                 lo, hi = int(grp[0]) * w.num_nodes, (int(grp[-1]) + 1) * w.num_nodes
                 gp = pairs[lo:hi].copy()
                 gp["submap"] -= int(grp[0])
-                return csm.match_batch_3d(mm, nodes, gp, sctxs[gi % nsearch])
+                if c5_trace is not None:
+                    c5_trace.append(("search+", gi, time.perf_counter()))
+                r = csm.match_batch_3d(mm, nodes, gp, sctxs[gi % nsearch])
+                if c5_trace is not None:
+                    c5_trace.append(("search-", gi, time.perf_counter()))
+                return r
 
             sfuts = [spool.submit(search, gi) for gi in range(len(groups))]
             bfuts[0].result()
@@ -862,6 +882,10 @@ def fast3d_bench(csm, ctx, args, rank=0, world_size=1, dist=None, coll_dev=None,
             rec = gather(rec) if gather is not None else \
                 cdist.gather_records(rec, dist, rank, world_size, coll_dev)
         c = time.perf_counter()
+        if c5_trace is not None:
+            print("c5 trace:", " ".join(f"{k}{i}@{(t - a) * 1e3:.1f}" for k, i, t in c5_trace),
+                  file=sys.stderr)
+            c5_trace.clear()
         phase["build"] += b - a
         phase["search"] += c - b
         return res, rec, (g, m)

@@ -1144,8 +1144,6 @@ void csm_context_destroy(csm_context* ctx) {
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
   if (ctx->f3_copy_stream) (void)hipStreamSynchronize(ctx->f3_copy_stream);
   if (ctx->f3_points_ready) (void)hipEventDestroy(ctx->f3_points_ready);
-  if (ctx->f3_stage_copied) (void)hipEventDestroy(ctx->f3_stage_copied);
-  if (ctx->f3_jobs_copied) (void)hipEventDestroy(ctx->f3_jobs_copied);
   if (ctx->f3_copy_stream) (void)hipStreamDestroy(ctx->f3_copy_stream);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;

@@ -11,6 +11,7 @@
 #include <condition_variable>
 #include <mutex>
 #include <tuple>
+#include <deque>
 #include <vector>
 
 #include "../../include/csm_amd.h"
@@ -103,6 +104,44 @@ struct PinnedBuf {
   }
   template <typename T>
   T* as() const { return static_cast<T*>(ptr); }
+};
+
+// Pinned staging slots, each with the event of its last upload. Take(): a
+// slot whose upload has finished (round robin from the last one taken), else
+// a new slot (up to kMax), else the next one in turn once its upload is done.
+// A deque, so slots never move. The caller records `copied` after its copy.
+struct StageRing {
+  struct Slot {
+    PinnedBuf buf;
+    hipEvent_t copied = nullptr;
+  };
+  static constexpr size_t kMax = 128;
+  std::deque<Slot> slots;
+  size_t next = 0;
+  size_t largest = 0;  // every slot is sized for the largest upload seen: regrowing
+                       // (hipHostFree) would wait for the device
+  ~StageRing() {
+    for (Slot& s : slots)
+      if (s.copied) (void)hipEventDestroy(s.copied);
+  }
+  int Take(size_t bytes, Slot** out) {
+    size_t at = slots.size();
+    for (size_t k = 0; k < slots.size() && at == slots.size(); ++k) {
+      const size_t i = (next + k) % slots.size();
+      if (hipEventQuery(slots[i].copied) == hipSuccess) at = i;
+    }
+    if (at == slots.size() && slots.size() < kMax) {
+      slots.emplace_back();
+      if (hipEventCreateWithFlags(&slots.back().copied, hipEventDisableTiming) != hipSuccess) return CSM_EHIP;
+    } else if (at == slots.size()) {
+      at = next % slots.size();
+      if (hipEventSynchronize(slots[at].copied) != hipSuccess) return CSM_EHIP;
+    }
+    next = at + 1;
+    *out = &slots[at];
+    largest = std::max(largest, bytes);
+    return slots[at].buf.Reserve(largest);
+  }
 };
 
 // RealTimeCorrelativeScanMatcher2D state (rt2d.hip): the converted, padded
@@ -214,11 +253,14 @@ struct csm_context {
   // scores on `stream`); the search waits on f3_points_ready.
   hipStream_t f3_copy_stream = nullptr;
   hipEvent_t f3_points_ready = nullptr;
-  hipEvent_t f3_stage_copied = nullptr;  // f3_grid_stage's last upload done
-  // Batched pyramid builds (csm_fast3d_create_batch): job lists, staged.
-  csm::PinnedBuf f3_job_stage;
+  // Pinned staging of csm_hybrid_grid_create's cell lists and
+  // csm_fast3d_create_batch's job lists: one slot per upload in flight (a
+  // create takes a slot whose copy has finished, or a new one; TakeStageSlot),
+  // so a create never waits for an earlier create's upload, which may sit
+  // behind a search kernel holding every CU.
+  csm::StageRing f3_grid_stage, f3_job_stage;
+  // Batched pyramid builds (csm_fast3d_create_batch): job lists.
   csm::DevBuf f3_jobs;
-  hipEvent_t f3_jobs_copied = nullptr;
   // Voxel filter scratch (voxel_filter.hip).
   csm::DevBuf vf_points, vf_offsets, vf_keep, vf_counts;
   // CeresScanMatcher2D refinement scratch (ceres2d.hip).
@@ -232,7 +274,6 @@ struct csm_context {
   float f2_tab_key[2] = {-1.f, -1.f};
   csm::DevBuf f3_ptab, f3_qtab, f3_grid_cells;
   bool f3_tables = false;
-  csm::PinnedBuf f3_grid_stage;
   ~csm_context() {
     for (csm_context* c : call_all) csm_context_destroy(c);
   }

@@ -252,16 +252,15 @@ int csm_hybrid_grid_create(csm_context* ctx, float resolution, const int32_t* ij
   // The cell list goes up through pinned staging and is scattered into the
   // zeroed brick on the device (no dense host copy); bricks come from the
   // context's pool (BufPool). One pass copies the indices into the staging
-  // and takes their bounds (the brick box). The staging is rewritten only
-  // once the previous create's copy out of it has finished (the kernels are
-  // not waited for).
+  // and takes their bounds (the brick box). Each create stages into its own
+  // slot (StageRing), so creates queue up without waiting for the device,
+  // e.g. behind a running search.
   const size_t list_bytes = static_cast<size_t>(count) * (3 * sizeof(int32_t) + sizeof(uint16_t));
   int lo[3] = {0, 0, 0}, hi[3] = {-1, -1, -1};
+  csm::StageRing::Slot* slot = nullptr;
   if (count > 0) {
-    if (ctx->f3_stage_copied) CSM_HIP(hipEventSynchronize(ctx->f3_stage_copied));
-    else CSM_HIP(hipEventCreateWithFlags(&ctx->f3_stage_copied, hipEventDisableTiming));
-    if ((rc = ctx->f3_grid_stage.Reserve(list_bytes))) return rc;
-    int32_t* hs = ctx->f3_grid_stage.as<int32_t>();
+    if ((rc = ctx->f3_grid_stage.Take(list_bytes, &slot))) return rc;
+    int32_t* hs = slot->buf.as<int32_t>();
     StageCells(ijk, count, hs, lo, hi);
     std::memcpy(hs + 3 * count, values, sizeof(uint16_t) * count);
   }
@@ -288,9 +287,8 @@ int csm_hybrid_grid_create(csm_context* ctx, float resolution, const int32_t* ij
     if ((rc = ctx->pool.Take(sizeof(uint16_t) * n, &g->values))) return rc;
     if ((rc = ctx->pool.Take(sizeof(float) * n, &g->prob))) return rc;
     hipStream_t st = ctx->stream;
-    CSM_HIP(hipMemcpyAsync(ctx->f3_grid_cells.ptr, ctx->f3_grid_stage.ptr, list_bytes,
-                           hipMemcpyHostToDevice, st));
-    CSM_HIP(hipEventRecord(ctx->f3_stage_copied, st));
+    CSM_HIP(hipMemcpyAsync(ctx->f3_grid_cells.ptr, slot->buf.ptr, list_bytes, hipMemcpyHostToDevice, st));
+    CSM_HIP(hipEventRecord(slot->copied, st));
     CSM_HIP(hipMemsetAsync(g->values.ptr, 0, sizeof(uint16_t) * n, st));
     const int32_t* dijk = ctx->f3_grid_cells.as<int32_t>();
     const uint16_t* dval = reinterpret_cast<const uint16_t*>(dijk + 3 * count);
@@ -874,11 +872,10 @@ int BuildFast3d(csm_context* ctx, csm_fast3d* const* ms, const Fast3dPlan* plans
   const size_t vbytes = (sizeof(ValueJob3) * vjobs.size() + 255) & ~size_t{255};
   const size_t bytes = vbytes + sizeof(RowJob3) * nrow;
   if (bytes > 0) {
-    if (ctx->f3_jobs_copied) CSM_HIP(hipEventSynchronize(ctx->f3_jobs_copied));
-    else CSM_HIP(hipEventCreateWithFlags(&ctx->f3_jobs_copied, hipEventDisableTiming));
-    if ((rc = ctx->f3_job_stage.Reserve(bytes))) return rc;
+    csm::StageRing::Slot* slot = nullptr;
+    if ((rc = ctx->f3_job_stage.Take(bytes, &slot))) return rc;
     if ((rc = ctx->f3_jobs.Reserve(bytes))) return rc;
-    char* h = ctx->f3_job_stage.as<char>();
+    char* h = slot->buf.as<char>();
     std::memcpy(h, vjobs.data(), sizeof(ValueJob3) * vjobs.size());
     RowJob3* rj = reinterpret_cast<RowJob3*>(h + vbytes);
     for (int l = 0; l < depth; ++l) {
@@ -886,7 +883,7 @@ int BuildFast3d(csm_context* ctx, csm_fast3d* const* ms, const Fast3dPlan* plans
       for (const RowJob3& j : oct_jobs[l]) *rj++ = j;
     }
     CSM_HIP(hipMemcpyAsync(ctx->f3_jobs.ptr, h, bytes, hipMemcpyHostToDevice, st));
-    CSM_HIP(hipEventRecord(ctx->f3_jobs_copied, st));
+    CSM_HIP(hipEventRecord(slot->copied, st));
     const char* dev = ctx->f3_jobs.as<char>();
     int64_t max_n = 0;
     for (const ValueJob3& v : vjobs) max_n = std::max(max_n, v.n);
@@ -951,13 +948,21 @@ int csm_fast3d_create_batch(csm_context* ctx, int32_t count, const csm_hybrid_gr
   if ((rc = EnsureDevice3(ctx))) return rc;
   std::vector<std::unique_ptr<csm_fast3d>> made(count);
   std::vector<Fast3dPlan> plans(count);
+  const auto t0 = std::chrono::steady_clock::now();
   for (int i = 0; i < count; ++i)
     if ((rc = PlanFast3d(ctx, high[i], low[i], histograms[i], histogram_sizes[i], options, &made[i],
                          &plans[i])))
       return rc;  // made[] frees what was planned
   std::vector<csm_fast3d*> ms(count);
   for (int i = 0; i < count; ++i) ms[i] = made[i].get();
+  const auto t1 = std::chrono::steady_clock::now();
   if ((rc = BuildFast3d(ctx, ms.data(), plans.data(), count))) return rc;
+  if (std::getenv("CSM_PROFILE3D_BUILD")) {
+    const auto t2 = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "fast3d create_batch: %d matchers, plan %.2f ms, build issue %.2f ms\n", count,
+                 std::chrono::duration<double, std::milli>(t1 - t0).count(),
+                 std::chrono::duration<double, std::milli>(t2 - t1).count());
+  }
   for (int i = 0; i < count; ++i) out[i] = made[i].release();
   return CSM_OK;
 }
