@@ -1272,7 +1272,7 @@ def roofline_3d(tm):
         # its traffic per algorithmic byte times this run's bytes per launch.
         ratio = t.get("traffic_bytes_per_algorithmic_byte")
         out["traffic"] = ratio * per_launch if ratio else t["traffic_bytes_per_launch"]
-        out["traffic_GBps"] = t["traffic_bytes_per_launch"] / (kernel_ms * 1e-3) / 1e9
+        out["traffic_GBps"] = out["traffic"] / (kernel_ms * 1e-3) / 1e9
         out["traffic_frac"] = out["traffic_GBps"] / 8000.0
         out["traffic_source"] = TRAFFIC3D_FILE
     return out
