@@ -87,6 +87,9 @@ def parse():
                    help="C5: single MatchFullSubmap calls from 16 threads (Option A), 0: skip")
     p.add_argument("--c5-first-group", type=int, default=6,
                    help="C5: submaps in the first group (its build is exposed; 0: an even split)")
+    p.add_argument("--c5-grids", choices=("single", "batch"), default="batch",
+                   help="C5: one csm_hybrid_grid_create per grid, or one csm_hybrid_grid_create_batch "
+                        "per group and resolution")
     p.add_argument("--c5-create", choices=("single", "batch"), default="batch",
                    help="C5: one csm_fast3d_create per submap, or one csm_fast3d_create_batch per group")
     p.add_argument("--c3-nodes", type=int, default=2000)
@@ -781,9 +784,14 @@ def fast3d_bench(csm, ctx, args, rank=0, world_size=1, dist=None, coll_dev=None,
     def build_(subs=None, bc=None):
         bc = bc or ctx
         subs = range(w.num_submaps) if subs is None else subs
-        g = [(csm.HybridGrid(w.high_resolution, *w.high_cells[s], context=bc),
-              csm.HybridGrid(w.low_resolution, *w.low_cells[s], context=bc))
-             for s in subs]
+        if args.c5_grids == "batch":  # one csm_hybrid_grid_create_batch per resolution
+            hi = csm.HybridGrid.create_batch(w.high_resolution, [w.high_cells[s] for s in subs], context=bc)
+            lo = csm.HybridGrid.create_batch(w.low_resolution, [w.low_cells[s] for s in subs], context=bc)
+            g = list(zip(hi, lo))
+        else:
+            g = [(csm.HybridGrid(w.high_resolution, *w.high_cells[s], context=bc),
+                  csm.HybridGrid(w.low_resolution, *w.low_cells[s], context=bc))
+                 for s in subs]
         if c5_trace is not None:
             c5_trace.append(("grids", len(c5_trace), time.perf_counter()))
         # A group's matchers in one csm_fast3d_create_batch (one launch per

@@ -272,6 +272,11 @@ _SIGNATURES = {
     "csm_hybrid_grid_create": (C.c_int, [C.c_void_p, C.c_float, C.POINTER(C.c_int32),
                                          C.POINTER(C.c_uint16), C.c_int64, C.c_int32,
                                          C.POINTER(C.c_void_p)]),
+    "csm_hybrid_grid_create_batch": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_float),
+                                               C.POINTER(C.POINTER(C.c_int32)),
+                                               C.POINTER(C.POINTER(C.c_uint16)),
+                                               C.POINTER(C.c_int64), C.POINTER(C.c_int32),
+                                               C.POINTER(C.c_void_p)]),
     "csm_hybrid_grid_destroy": (None, [C.c_void_p]),
     "csm_hybrid_grid_get_probability": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32), C.c_int64,
                                                   C.POINTER(C.c_float)]),

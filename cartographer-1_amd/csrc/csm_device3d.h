@@ -43,6 +43,19 @@ struct Brick3 {
   int64_t offset;  // byte offset of this brick in its allocation
 };
 
+// One HybridGrid of a batched grid build (csm_hybrid_grid_create_batch): its
+// cell list (device), the dense value brick it is scattered into and the
+// float probability brick made from it (n cells each).
+struct GridJob3 {
+  const int32_t* ijk;
+  const uint16_t* vals;
+  int64_t count;
+  Brick3 b;
+  uint16_t* values;
+  float* prob;
+  int64_t n;
+};
+
 // One output brick of a batched pyramid build (csm_fast3d_create_batch):
 // source brick -> output brick, as level_gather (shift h, half) or
 // octet_build (h) do it. `lds`: the job's staged-rows bytes.

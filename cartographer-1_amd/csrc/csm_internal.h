@@ -272,7 +272,7 @@ struct csm_context {
   csm::BufPool pool;
   csm::DevBuf f2_cells, f2_widen, f2_qtab, f2_ctab;
   float f2_tab_key[2] = {-1.f, -1.f};
-  csm::DevBuf f3_ptab, f3_qtab, f3_grid_cells;
+  csm::DevBuf f3_ptab, f3_qtab, f3_grid_cells, f3_grid_batch;
   bool f3_tables = false;
   ~csm_context() {
     for (csm_context* c : call_all) csm_context_destroy(c);

@@ -15,6 +15,11 @@ hipError_t LaunchBrickFromValues(const uint16_t* values, int64_t n, const float*
                                  hipStream_t st);
 hipError_t LaunchBrickScatter(const int32_t* ijk, const uint16_t* values, int64_t count,
                               const Brick3& b, uint16_t* out, hipStream_t st);
+// Batched grid builds (csm_hybrid_grid_create_batch): every job's value
+// brick zeroed, its cells scattered, its probabilities made; blockIdx.y =
+// job, max_n / max_count over the jobs.
+hipError_t LaunchGridBuildBatch(const GridJob3* jobs, int num_jobs, int64_t max_n, int64_t max_count,
+                                const float* ptab, hipStream_t st);
 hipError_t LaunchLevelGather(const uint8_t* prev, const Brick3& pb, uint8_t* out, const Brick3& ob,
                              int shift, int half, hipStream_t st);
 hipError_t LaunchOctetBuild(const uint8_t* level, const Brick3& lb, int h, uint64_t* out,

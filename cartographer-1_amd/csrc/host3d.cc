@@ -302,6 +302,101 @@ int csm_hybrid_grid_create(csm_context* ctx, float resolution, const int32_t* ij
   return CSM_OK;
 }
 
+// csm_hybrid_grid_create for many grids: one staging upload (every cell
+// list and the job list), one zero / scatter / probability launch each for
+// all of them (LaunchGridBuildBatch) instead of four operations per grid.
+int csm_hybrid_grid_create_batch(csm_context* ctx, int32_t num, const float* resolutions,
+                                 const int32_t* const* ijk, const uint16_t* const* values,
+                                 const int64_t* counts, const int32_t* grid_sizes,
+                                 csm_hybrid_grid** out) {
+  if (!ctx || num < 0 || (num > 0 && (!resolutions || !ijk || !values || !counts || !out)))
+    return CSM_EINVAL;
+  if (num > 65535) return CSM_ERANGE;  // one launch's grid.y
+  for (int i = 0; i < num; ++i)
+    if (!(resolutions[i] > 0.f) || counts[i] < 0 || (counts[i] > 0 && (!ijk[i] || !values[i])))
+      return CSM_EINVAL;
+  if (num == 0) return CSM_OK;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  int rc;
+  if ((rc = EnsureDevice3(ctx))) return rc;
+  // Staging layout: each grid's cells (3 int32 per cell) then values (uint16),
+  // 16-byte aligned, then the job array.
+  std::vector<size_t> at(num);
+  size_t bytes = 0;
+  for (int i = 0; i < num; ++i) {
+    at[i] = bytes;
+    bytes += (static_cast<size_t>(counts[i]) * (3 * sizeof(int32_t) + sizeof(uint16_t)) + 15) & ~size_t{15};
+  }
+  const size_t jobs_at = bytes;
+  bytes += sizeof(GridJob3) * num;
+  csm::StageRing::Slot* slot = nullptr;
+  if ((rc = ctx->f3_grid_stage.Take(bytes, &slot))) return rc;
+  if ((rc = ctx->f3_grid_batch.Reserve(bytes))) return rc;
+  char* hs = slot->buf.as<char>();
+  char* dev = ctx->f3_grid_batch.as<char>();
+  GridJob3* jobs = reinterpret_cast<GridJob3*>(hs + jobs_at);
+  std::vector<std::unique_ptr<csm_hybrid_grid>> made(num);
+  int njobs = 0;
+  int64_t max_n = 0, max_count = 0;
+  for (int i = 0; i < num; ++i) {
+    auto g = std::make_unique<csm_hybrid_grid>();
+    g->ctx = ctx;
+    g->resolution = resolutions[i];
+    const int64_t count = counts[i];
+    int lo[3] = {0, 0, 0}, hi[3] = {-1, -1, -1};
+    int32_t* hc = reinterpret_cast<int32_t*>(hs + at[i]);
+    if (count > 0) {
+      StageCells(ijk[i], count, hc, lo, hi);
+      std::memcpy(hc + 3 * count, values[i], sizeof(uint16_t) * count);
+    }
+    int grid_size = grid_sizes ? grid_sizes[i] : 0;
+    if (grid_size <= 0) {  // DynamicGrid growth, as csm_hybrid_grid_create
+      int gs = 128;
+      for (int a = 0; a < 3 && count > 0; ++a)
+        while (lo[a] < -(gs / 2) || hi[a] >= gs / 2) gs *= 2;
+      grid_size = gs;
+    }
+    g->grid_size = grid_size;
+    Brick3& b = g->brick;
+    b.ox = lo[0];
+    b.oy = lo[1];
+    b.oz = lo[2];
+    b.nx = count > 0 ? hi[0] - lo[0] + 1 : 0;
+    b.ny = count > 0 ? hi[1] - lo[1] + 1 : 0;
+    b.nz = count > 0 ? hi[2] - lo[2] + 1 : 0;
+    b.offset = 0;
+    const int64_t n = static_cast<int64_t>(b.nx) * b.ny * b.nz;
+    if (n > (int64_t{1} << 31)) return CSM_ERANGE;  // made[] returns its buffers to the pool
+    if (n > 0) {
+      if ((rc = ctx->pool.Take(sizeof(uint16_t) * n, &g->values))) return rc;
+      if ((rc = ctx->pool.Take(sizeof(float) * n, &g->prob))) return rc;
+      const int32_t* dijk = reinterpret_cast<const int32_t*>(dev + at[i]);
+      jobs[njobs++] = GridJob3{dijk, reinterpret_cast<const uint16_t*>(dijk + 3 * count), count, b,
+                               g->values.as<uint16_t>(), g->prob.as<float>(), n};
+      max_n = std::max(max_n, n);
+      max_count = std::max(max_count, count);
+    }
+    made[i] = std::move(g);
+  }
+  if (njobs > 0) {
+    if ((rc = EnsureValueTables(ctx))) return rc;
+    hipStream_t st = ctx->stream;
+    // The job array sits at jobs_at whatever njobs is: copy through it.
+    const size_t copy = jobs_at + sizeof(GridJob3) * njobs;
+    CSM_HIP(hipMemcpyAsync(dev, hs, copy, hipMemcpyHostToDevice, st));
+    CSM_HIP(hipEventRecord(slot->copied, st));
+    CSM_HIP(LaunchGridBuildBatch(reinterpret_cast<const GridJob3*>(dev + jobs_at), njobs, max_n, max_count,
+                                 ctx->f3_ptab.as<float>(), st));
+    for (int i = 0; i < num; ++i) {
+      if (made[i]->values.ptr == nullptr) continue;
+      CSM_HIP(hipEventCreateWithFlags(&made[i]->ready, hipEventDisableTiming));
+      CSM_HIP(hipEventRecord(made[i]->ready, st));
+    }
+  }
+  for (int i = 0; i < num; ++i) out[i] = made[i].release();
+  return CSM_OK;
+}
+
 void csm_hybrid_grid_destroy(csm_hybrid_grid* g) {
   if (!g) return;
   (void)hipSetDevice(g->ctx->device);

@@ -84,6 +84,36 @@ __global__ void brick_scatter(const int32_t* __restrict__ ijk, const uint16_t* _
   out[k] = values[i];
 }
 
+// Batched grid builds (csm_hybrid_grid_create_batch), blockIdx.y = job:
+// zero the value bricks (16 bytes per thread and step), scatter the cell
+// lists into them, then the probabilities, as brick_scatter and
+// brick_from_values do for one grid.
+__global__ void __launch_bounds__(256) grid_zero_batch(const GridJob3* __restrict__ jobs) {
+  const GridJob3 j = jobs[blockIdx.y];
+  const int64_t n8 = j.n / 8;  // whole 16-byte pieces (value bricks are 256-byte aligned)
+  uint4* v = reinterpret_cast<uint4*>(j.values);
+  const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  for (int64_t i = t; i < n8; i += static_cast<int64_t>(gridDim.x) * blockDim.x)
+    v[i] = make_uint4(0u, 0u, 0u, 0u);
+  if (t < j.n - 8 * n8) j.values[8 * n8 + t] = 0;  // the last < 8 values
+}
+__global__ void __launch_bounds__(256) grid_scatter_batch(const GridJob3* __restrict__ jobs) {
+  const GridJob3 j = jobs[blockIdx.y];
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < j.count;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int64_t k = (static_cast<int64_t>(j.ijk[3 * i + 2] - j.b.oz) * j.b.ny + (j.ijk[3 * i + 1] - j.b.oy)) *
+                          j.b.nx + (j.ijk[3 * i] - j.b.ox);
+    j.values[k] = j.vals[i];
+  }
+}
+__global__ void __launch_bounds__(256) grid_prob_batch(const GridJob3* __restrict__ jobs,
+                                                       const float* __restrict__ ptab) {
+  const GridJob3 j = jobs[blockIdx.y];
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < j.n;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x)
+    j.prob[i] = ptab[j.values[i] & 0x7fff];
+}
+
 // Cell (x, y, z) of brick b as a 32-bit offset (bricks are < 2^31 cells), or
 // -1 outside.
 __device__ __forceinline__ int BrickIndex32(const Brick3& b, int x, int y, int z) {
@@ -2492,6 +2522,21 @@ hipError_t LaunchFast3dSearch(bool large, int grid, hipStream_t st, const Submap
                        dim3(kSearch3dThreads), 0, st, submaps, pairs, yaws, item_begin, num_items,
                        points, low_points, counter, best, status, stats, spill, best_hi, ties,
                        tie_count);
+  return hipGetLastError();
+}
+
+hipError_t LaunchGridBuildBatch(const GridJob3* jobs, int num_jobs, int64_t max_n, int64_t max_count,
+                                const float* ptab, hipStream_t st) {
+  if (num_jobs <= 0 || max_n <= 0) return hipSuccess;
+  // Grid-stride over each job: at most 2048 blocks per job in x.
+  auto blocks = [](int64_t work) {
+    const int64_t b = (work + 255) / 256;
+    return static_cast<unsigned>(b < 1 ? 1 : b > 2048 ? 2048 : b);
+  };
+  hipLaunchKernelGGL(grid_zero_batch, dim3(blocks(max_n / 8 + 8), num_jobs), dim3(256), 0, st, jobs);
+  if (max_count > 0)
+    hipLaunchKernelGGL(grid_scatter_batch, dim3(blocks(max_count), num_jobs), dim3(256), 0, st, jobs);
+  hipLaunchKernelGGL(grid_prob_batch, dim3(blocks(max_n), num_jobs), dim3(256), 0, st, jobs, ptab);
   return hipGetLastError();
 }
 

@@ -44,6 +44,35 @@ class HybridGrid:
                "csm_hybrid_grid_create")
         self.handle = h
 
+    @classmethod
+    def create_batch(cls, resolution, cells, grid_sizes=None, context: Optional[Context] = None):
+        """Many grids in one call (csm_hybrid_grid_create_batch): ``cells`` is a
+        list of (indices, values) pairs, ``resolution`` one value or one per
+        grid; returns the grids in order, each what the constructor returns."""
+        context = context or default_context()
+        lib = context._lib
+        n = len(cells)
+        res = np.broadcast_to(np.asarray(resolution, np.float32), (n,)).copy()
+        idx = [np.ascontiguousarray(np.asarray(c[0], np.int32).reshape(-1, 3)) for c in cells]
+        val = [np.ascontiguousarray(np.asarray(c[1], np.uint16).reshape(-1)) for c in cells]
+        if any(len(i) != len(v) for i, v in zip(idx, val)):
+            raise ValueError("indices and values differ in length")
+        k = max(n, 1)
+        iptr = (C.POINTER(C.c_int32) * k)(*[_ptr(i, C.c_int32) for i in idx])
+        vptr = (C.POINTER(C.c_uint16) * k)(*[_ptr(v, C.c_uint16) for v in val])
+        cnt = (C.c_int64 * k)(*[len(v) for v in val])
+        gs = (C.c_int32 * k)(*([int(g) for g in grid_sizes] if grid_sizes is not None else [0] * n))
+        out = (C.c_void_p * k)()
+        _check(lib.csm_hybrid_grid_create_batch(context.handle, n, _ptr(res, C.c_float), iptr, vptr, cnt,
+                                                gs, out), "csm_hybrid_grid_create_batch")
+        made = []
+        for i in range(n):
+            g = cls.__new__(cls)
+            g.context, g._lib, g.resolution = context, lib, float(res[i])
+            g.handle = C.c_void_p(out[i])
+            made.append(g)
+        return made
+
     def device_bytes(self) -> int:
         """Device memory of the grid's bricks (csm_hybrid_grid_device_bytes)."""
         return int(self._lib.csm_hybrid_grid_device_bytes(self.handle))

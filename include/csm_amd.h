@@ -350,6 +350,15 @@ typedef struct csm_hybrid_grid csm_hybrid_grid;
 int csm_hybrid_grid_create(csm_context* ctx, float resolution, const int32_t* xyz_indices,
                            const uint16_t* values, int64_t count, int32_t grid_size,
                            csm_hybrid_grid** out);
+/* `num` grids in one call, each as csm_hybrid_grid_create builds it (the
+ * same bricks and values), with one upload and one launch per build step for
+ * all of them: for a caller that builds many submaps' grids at once (the
+ * constraint builder's matcher construction, constraint_builder_3d.cc:
+ * 170-198). grid_sizes may be NULL (every grid derives its size). */
+int csm_hybrid_grid_create_batch(csm_context* ctx, int32_t num, const float* resolutions,
+                                 const int32_t* const* xyz_indices, const uint16_t* const* values,
+                                 const int64_t* counts, const int32_t* grid_sizes,
+                                 csm_hybrid_grid** out);
 void csm_hybrid_grid_destroy(csm_hybrid_grid* g);
 /* Bounding box origin / extent of the device brick and the grid size. */
 int csm_hybrid_grid_info(const csm_hybrid_grid* g, int32_t* origin3, int32_t* dims3,

@@ -369,6 +369,56 @@ def test_synthetic_pairs_match_oracle(csm, oracle, world3d):
     assert stats["exact"] + stats["tie"] >= 3, stats
 
 
+def test_grid_create_batch_equals_single_creates(csm, world3d):
+    """csm_hybrid_grid_create_batch (one upload and one launch per build step
+    for all grids) makes what csm_hybrid_grid_create makes grid by grid: the
+    same brick boxes and grid sizes, the same probabilities at every known
+    cell and at unknown ones, the same interpolation, and matchers built on
+    the batch grids search exactly like matchers on single-created grids. An
+    empty grid inside the batch stays empty."""
+    w = world3d
+    S = w.num_submaps
+    single = [(csm.HybridGrid(w.high_resolution, *w.high_cells[s]),
+               csm.HybridGrid(w.low_resolution, *w.low_cells[s])) for s in range(S)]
+    empty = (np.zeros((0, 3), np.int32), np.zeros(0, np.uint16))
+    hi = csm.HybridGrid.create_batch(w.high_resolution, [w.high_cells[s] for s in range(S)] + [empty])
+    lo = csm.HybridGrid.create_batch([w.low_resolution] * S, [w.low_cells[s] for s in range(S)])
+    assert hi[-1].info()[1] == (0, 0, 0)
+    rng = np.random.default_rng(7)
+    for s in range(S):
+        for b, g, cells in ((hi[s], single[s][0], w.high_cells[s]), (lo[s], single[s][1], w.low_cells[s])):
+            assert b.info() == g.info(), s
+            ijk = np.asarray(cells[0], np.int32).reshape(-1, 3)
+            probe = np.concatenate([ijk, ijk[rng.integers(0, len(ijk), 500)] + rng.integers(-3, 4, (500, 3))])
+            assert np.array_equal(b.get_probability(probe), g.get_probability(probe)), s
+            pts = (ijk[rng.integers(0, len(ijk), 200)] + rng.random((200, 3)) - 0.5) * b.resolution
+            assert np.array_equal(b.interpolate(pts), g.interpolate(pts)), s
+    o = csm.FastCorrelativeScanMatcherOptions3D()
+    mb = csm.FastCorrelativeScanMatcher3D.create_batch(list(zip(hi[:S], lo)), list(w.submap_hist[:S]), o)
+    ms = csm.FastCorrelativeScanMatcher3D.create_batch(single, list(w.submap_hist[:S]), o)
+    for s in range(S):
+        for lvl in range(o.branch_and_bound_depth):
+            ob, vb = mb[s].read_level(lvl)
+            os_, vs = ms[s].read_level(lvl)
+            assert ob == os_ and np.array_equal(vb, vs), (s, lvl)
+    nodes = csm.NodeSet3D([w.node(i) for i in range(w.num_nodes)])
+    sub = np.repeat(np.arange(S), w.num_nodes)
+    nod = np.tile(np.arange(w.num_nodes), S)
+    rot = np.array([w.node_rotation(n) for n in range(w.num_nodes)])
+    pairs = csm.make_pairs_3d(sub, nod, 0.6, True, node_q=rot[nod])
+    rb = csm.match_batch_3d(mb, nodes, pairs)
+    rs = csm.match_batch_3d(ms, nodes, pairs)
+    assert (rb["status"] == rs["status"]).all()
+    ok = rb["status"] == csm.CSM_OK
+    assert ok.sum() >= 3
+    for f in ("score", "rotational_score", "low_resolution_score", "t", "q"):
+        assert np.array_equal(rb[f][ok], rs[f][ok]), f
+    for m in mb + ms:
+        m.close()
+    for g in hi + lo + [x for pair in single for x in pair]:
+        g.close()
+
+
 def test_create_batch_equals_single_creates(csm, oracle, world3d):
     """csm_fast3d_create_batch builds every level of every matcher in one
     launch per level: the levels are byte-identical to the oracle's
