@@ -703,6 +703,7 @@ struct V4Shared {
   int node_xo[kBatchNodes], node_yo[kBatchNodes], node_rot[kBatchNodes], node_level[kBatchNodes];
   int node_off[kBatchNodes], node_len[kBatchNodes];  // the node's children-level list
   int nodes, done, batch_len, batch_entries;
+  int tie_sum;  // a sum the pair's witness keys already show two leaves at (-1: none)
   int item_pair, item_chunk, queue;
   int sp;
   uint64_t best;
@@ -1124,6 +1125,11 @@ __device__ __forceinline__ uint32_t ClusterMask(int sl) {
 // (DESIGN.md §5).
 #define CSM_XFAST 1
 #endif
+#ifndef CSM_TIE_PRUNE
+// 1: the main search stops expanding nodes bounded by a sum its witness keys
+// already show tied (FindsConstraints-like inputs: every leaf ties).
+#define CSM_TIE_PRUNE 1
+#endif
 #ifndef CSM_V4_WAVES
 // Waves per SIMD the register budget targets: 6 workgroups per CU (v5 with
 // its 256-entry LDS ring fits 6 in LDS too; measured best).
@@ -1376,6 +1382,7 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
       sh.ovf = 0;
       sh.head = 0;
       sh.best = LoadBest(pair_best);
+      sh.tie_sum = -1;
       sh.batch_no = 0;
       sh.nodes = 0;
       sh.done = 0;
@@ -1455,6 +1462,16 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
               atomicMax(reinterpret_cast<unsigned long long*>(pair_best), key);
               atomicMax(reinterpret_cast<unsigned long long*>(&sh.best), key);
             }
+            // Two leaves at the pass's largest sum, or one at the best sum
+            // other than the best's: the pair ties there, so nodes bounded by
+            // that sum need not be expanded (sh.tie_sum; tie resolution
+            // searches those leaves again, ResolveTies).
+            if (CSM_TIE_PRUNE && !kCollect && lane == 0) {
+              const uint32_t ks = static_cast<uint32_t>(key >> kSumShift);
+              if (ks >= cur_sum &&
+                  (hi != HighLeafKey(key) || (key != cur && static_cast<uint32_t>(cur >> kSumShift) == ks)))
+                atomicMax(&sh.tie_sum, static_cast<int>(ks));
+            }
             // The largest-index leaf at the running maximum: a second maximal
             // leaf shows as a different index at the final sum (ResolveTies).
             if (lane == 0 && static_cast<uint32_t>(hi >> kSumShift) >= cur_sum)
@@ -1524,7 +1541,17 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
         constexpr int kRing = decltype(sh)::kStackLds;
         int sp = min(sh.sp, kFifo ? kRing : sh.kStackCapacity);
         int ovf = kFifo ? min(sh.ovf, kSpill2) : 0;
-        if (sp == 0 && ovf == 0 && sh.vnext < vtotal) {
+        // The collect pass abandons a pair once its tied leaves overflow the
+        // record: the host resolves it with the ordered walk (fast2d_walk).
+        const bool abandon =
+            kCollect && Uniform(static_cast<int>(
+                            *reinterpret_cast<volatile int32_t*>(tie_count + pair_index) > kTieCap)) != 0;
+        if (abandon) {
+          sp = 0;
+          ovf = 0;
+          if (lane == 0) sh.vnext = vtotal;
+        }
+        if (!abandon && sp == 0 && ovf == 0 && sh.vnext < vtotal) {
           const int v0 = sh.vnext, vc = min(kRootChunk, vtotal - v0);
           if (kFifo && lane == 0) sh.head = 0;  // empty ring: restart at slot 0
           for (int k = lane; k < vc; k += 64) {
@@ -1549,10 +1576,15 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
         }
         // (c) Pop the next batch: up to 64 nodes, best first.
         if (lane == 0 && (sh.batch_no++ & (CSM_BEST_REFRESH - 1)) == 0) {
+          // Every 8th batch also reads the tie witness: once it shows two
+          // leaves at the best sum, the search only has to find a larger sum,
+          // so nodes bounded by that sum are pruned (tie resolution searches
+          // those leaves again, ResolveTies).
           const uint64_t fresh = LoadBest(pair_best);
           if (fresh > sh.best) sh.best = fresh;
         }
         const uint32_t cur_sum = static_cast<uint32_t>(sh.best >> kSumShift);
+        const int tie_sum = Uniform(sh.tie_sum);
         int nodes = 0, blen = 0, bent = 0;
         if (sp > 0 || ovf > 0) {
           // Up to 64 entries from the top (any level); expand a power of two
@@ -1584,7 +1616,11 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
             hexb = top_hx;
           }
           const unsigned long long inm = __ballot(in);
-          const bool expandable = in && (ent.y & 0x3fffff) >= cur_sum;
+          // A node bounded by a sum the witness keys already show tied
+          // (sh.tie_sum) is not expanded: only a larger sum can change the
+          // maximum.
+          const bool expandable = in && (ent.y & 0x3fffff) >= cur_sum &&
+                                  static_cast<int>(ent.y & 0x3fffff) > tie_sum;
           const unsigned long long em = __ballot(expandable);
           const int ne = __popcll(em);
           int take = __popcll(inm);

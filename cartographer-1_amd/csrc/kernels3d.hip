@@ -978,6 +978,8 @@ struct F3SharedT {
   uint16_t tcount[kTopCells3d];
   int ntcell;
   int nbatch, nleaf, sp, item, error, skip, cached_submap, high_water;
+  int tie_sum;   // a sum the witness keys already show two passing leaves at (-1: none)
+  int abandon;   // collect pass: the pair's tied leaves overflowed the record
   unsigned long long best;
   unsigned long long best_seen;  // last read of the pair's global best
 };
@@ -1119,6 +1121,8 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
       sh.sp = 0;
       sh.best = best[yw.pair];
       sh.best_seen = 0;
+      sh.tie_sum = -1;
+      sh.abandon = 0;
     }
     __syncthreads();
     // Lowest-resolution candidates (GenerateLowestResolutionCandidates
@@ -1272,6 +1276,7 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
     F3_MARK(9);
     const bool skip_empty = pd.min_sum > 0;
     for (int r0 = 0; r0 < T; r0 += kRootScore3d) {
+    if (sh.abandon) break;  // uniform: written before the last batch's barrier
     const int r1 = min(T, r0 + kRootScore3d);
     if (tid == 0) sh.nroot = 0;
     __syncthreads();
@@ -1400,7 +1405,16 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
       if (tid < 64) {
         const unsigned long long bk = max(sh.best, sh.best_seen);
         const int best_sum = static_cast<int>(bk >> pd.key_shift);
-        int sp = sh.sp, m = 0;
+        // Once this workgroup has seen two passing leaves at a sum (the leaf
+        // loop below sets sh.tie_sum), only a larger sum can change the
+        // maximum: nodes bounded by it are pruned (tie resolution searches
+        // those leaves again, ResolveTies3d). The collect pass instead
+        // abandons a pair whose record overflowed (the host then walks it,
+        // fast3d_walk).
+        const int tie_sum = sh.tie_sum;
+        const bool abandon =
+            pd.collect && *reinterpret_cast<volatile int32_t*>(tie_count + pd.collect - 1) > kTieCap3d;
+        int sp = abandon ? 0 : sh.sp, m = 0;
         while (sp > 0 && m < kBatch3d) {
           const int at = sp - 1 - tid;
           int s = 0;
@@ -1410,7 +1424,7 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
             e = at < kStack3d ? make_int4(sh.sx[at], sh.sy[at], (sh.sz[at] & 0xffff) | (sh.sd[at] << 16), sh.ssum[at])
                               : spill[at - kStack3d];
             s = e.w;
-            keep = s >= best_sum && s >= pd.min_sum;
+            keep = s >= best_sum && s >= pd.min_sum && s > tie_sum;
           }
           const unsigned long long mask = __ballot(keep);
           const int rank = m + __popcll(mask & ((1ull << tid) - 1ull));
@@ -1430,6 +1444,7 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
           sh.sp = sp;
           sh.nbatch = m;
           sh.nleaf = 0;
+          if (abandon) sh.abandon = 1;
         }
       }
       __syncthreads();
@@ -1597,6 +1612,7 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
         const int k = hl;
         if (k == 0) lookups += static_cast<unsigned long long>(__popc(nc)) * n;
         const int best_sum = static_cast<int>(sh.best >> pd.key_shift);
+        const int tie_sum = sh.tie_sum;
         int my = acc[0];
 #pragma unroll
         for (int j = 1; j < 8; ++j) my = k == j ? acc[j] : my;
@@ -1607,7 +1623,7 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
           int m = 0, rank = 0;
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
-            const bool kj = ((nc >> j) & 1) && acc[j] >= pd.min_sum && acc[j] >= best_sum;
+            const bool kj = ((nc >> j) & 1) && acc[j] >= pd.min_sum && acc[j] >= best_sum && acc[j] > tie_sum;
             m += kj;
             rank += kj && (acc[j] < my || (acc[j] == my && j < k));
           }
@@ -1619,7 +1635,7 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
           }
           base = __shfl(base, (tid & 63) & ~(kLanes - 1), 64);
           const int at = base + rank;
-          if (pres && my >= pd.min_sum && my >= best_sum && at < kStack3d + kSpill3d) {
+          if (pres && my >= pd.min_sum && my >= best_sum && my > tie_sum && at < kStack3d + kSpill3d) {
             if (at < kStack3d) {
               sh.sx[at] = static_cast<int16_t>(cxk);
               sh.sy[at] = static_cast<int16_t>(cyk);
@@ -1636,7 +1652,7 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
                                          (~id & ((1ull << pd.key_shift) - 1));
           // Leaves at the best sum too (not only above the best key): a
           // second leaf at the maximum is the tie witness.
-          if (my >= best_sum) {
+          if (my >= best_sum && my > tie_sum) {
             const int at = atomicAdd(&sh.nleaf, 1);
             sh.leaf_keys[at] = key;
             sh.leaf_x[at] = cxk;
@@ -1693,6 +1709,7 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
                 *reinterpret_cast<volatile unsigned long long*>(best_hi + yw.pair);
             sh.skip = static_cast<int>(hi >> pd.key_shift) == lsum &&
                       (hi & id_mask) != (~cur & id_mask);
+            if (sh.skip) sh.tie_sum = max(sh.tie_sum, lsum);  // the witness shows the tie
           }
           __syncthreads();
           // Every wave takes its copy before thread 0 may rewrite the flag
@@ -1712,6 +1729,8 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
           if (!witness) {
             atomicMax(best + yw.pair, lkey);
             sh.best = max(sh.best, lkey);
+          } else if (!pd.collect && lkey != cur) {
+            sh.tie_sum = max(sh.tie_sum, lsum);  // a second passing leaf at the best sum
           }
           atomicMax(best_hi + yw.pair, (static_cast<unsigned long long>(lsum) << pd.key_shift) | lid);
           if (pd.collect && lsum == pd.collect_sum) {  // collect = tie slot + 1
@@ -1728,7 +1747,7 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
       __syncthreads();
       F3_COUNT(6, nl);
     }
-      rb_end = k0;
+      rb_end = sh.abandon ? 0 : k0;
     }
     F3_MARK(3);
     }  // root chunks
