@@ -140,6 +140,13 @@ struct WorkQueues2 {
   int32_t rot_chunk;
 };
 
+// Rotations per v4/v5 search item at most (per-rotation LDS tables are sized
+// for it; the host clamps CSM_ROT_CHUNK to it).
+#ifndef CSM_MAX_ROT_CHUNK
+#define CSM_MAX_ROT_CHUNK 16
+#endif
+constexpr int kV4MaxRotChunk = CSM_MAX_ROT_CHUNK;
+
 constexpr int kStack2 = 1024;   // v4 per-workgroup DFS stack entries in LDS
 constexpr int kSpill2 = 7168;   // further entries per workgroup in global memory
 constexpr int kBatchNodes = 64; // nodes expanded per batch (256 children; hex: 1024)

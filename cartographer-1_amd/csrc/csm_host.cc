@@ -946,8 +946,8 @@ int RunBatch(csm_context* ctx, csm_fast2d* const* submaps, int32_t num_submaps,
   plan.max_npad = max_npad;
   const char* rc_env = std::getenv("CSM_ROT_CHUNK");
   const int v4_budget = 9 * 1024;  // C2 (1088 padded points): 2 rotations per chunk, the measured best
-  const int v4_rc = rc_env ? std::max(1, std::min(16, std::atoi(rc_env)))
-                           : std::max(1, std::min(8, v4_budget / (max_npad * 4)));
+  const int v4_rc = rc_env ? std::max(1, std::min(kV4MaxRotChunk, std::atoi(rc_env)))
+                           : std::max(1, std::min(std::min(8, kV4MaxRotChunk), v4_budget / (max_npad * 4)));
   const int lds_budget = 40 * 1024;
   plan.rc = plan.use_v2 ? v4_rc : std::max(1, std::min(16, lds_budget / (max_npad * 4)));
   // Node order: FIFO (level by level, the default) or LIFO (depth-first,

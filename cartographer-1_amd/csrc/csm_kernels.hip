@@ -667,7 +667,7 @@ __global__ void pyramid_hex(const uint8_t* __restrict__ mlev, int mw, int mh, in
 #ifndef CSM_U_HEX
 #define CSM_U_HEX 4   // hex gathers in flight per lane (V4ScoreHex)
 #endif
-constexpr int kMaxRotChunk = 16;
+constexpr int kMaxRotChunk = kV4MaxRotChunk;
 constexpr int kLists = kMaxClusterShift + 1;
 
 // kKids: children sums per node, 4 (quad batches only, v4) or 16 (v5: hex
