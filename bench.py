@@ -36,10 +36,10 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 # Version tag of the search kernel the committed PMC traffic figures belong to
 # (a traffic file recorded on another kernel version is not reported).
-KERNEL_TAG = "v5-hybrid-refresh"
-# fast3d_search version whose PMC passes profiles/r5m/traffic_c5.json holds.
-KERNEL3D_TAG = "f3-octet-r5"
-TRAFFIC3D_FILE = os.path.join("profiles", "r5m", "traffic_c5.json")
+KERNEL_TAG = "v5-tieprune"
+# fast3d_search version whose PMC passes profiles/r5ay/traffic_c5.json holds.
+KERNEL3D_TAG = "f3-octet-tieprune"
+TRAFFIC3D_FILE = os.path.join("profiles", "r5ay", "traffic_c5.json")
 
 
 def load_pkg():
@@ -326,8 +326,8 @@ def roofline_fields(tm, achieved, peak, traffic, kernel_ms_avg, bytes_per_launch
             "candidate_equivalent_bytes_per_launch": candidate_bytes}
 
 
-TRAFFIC_FILES = {"c2": os.path.join("profiles", "r4z", "traffic_c2.json"),
-                 "c3": os.path.join("profiles", "r4z", "traffic_c3.json")}
+TRAFFIC_FILES = {"c2": os.path.join("profiles", "r5ay", "traffic_c2.json"),
+                 "c3": os.path.join("profiles", "r5ay", "traffic_c3.json")}
 
 
 def traffic_fields(traffic, kernel_ms_avg, peak):
@@ -350,7 +350,7 @@ def sum_timing(csm, tms):
     return out
 
 
-GATHER_FILE = os.path.join("profiles", "r5g", "gather_c3.json")
+GATHER_FILE = os.path.join("profiles", "r5ay", "gather_c3.json")
 
 
 def gather_roofline(kernel_ms):
