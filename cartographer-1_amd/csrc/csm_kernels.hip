@@ -654,10 +654,10 @@ __global__ void pyramid_hex(const uint8_t* __restrict__ mlev, int mw, int mh, in
 // exactly: the result is unchanged.
 //
 // The DFS stack mixes the chunk's rotations; a batch pops up to 64 nodes
-// (deepest level first, best bound first): a lane takes one node and a
-// strided subset of that node's list, and per entry issues ONE dword load
-// from the quad layout that returns all four children's values. The 4 waves
-// split the entries and meet in LDS; all waves combine, prune and push
+// (deepest level first, best bound first): a thread takes one node and a
+// strided subset of that node's list (CSM_FLAT_LANES), and per entry issues
+// ONE dword load from the quad layout that returns all four children's
+// values. The threads' sums meet in LDS; all waves combine, prune and push
 // survivors sorted (best on top), wave 0 pops the next batch. Roots are
 // virtual nodes one level above the top lattice.
 
@@ -666,6 +666,16 @@ __global__ void pyramid_hex(const uint8_t* __restrict__ mlev, int mw, int mh, in
 #endif
 #ifndef CSM_U_HEX
 #define CSM_U_HEX 4   // hex gathers in flight per lane (V4ScoreHex)
+#endif
+#ifndef CSM_FLAT_LANES
+// 1: the scoring lanes of all 4 waves take (node, chunk) pairs, node = t mod
+// nodes, chunk = t / nodes over the workgroup's 256 threads, and chunk c of
+// C = 256 / nodes walks entries c, c + C, ... of the node's list (a batch of
+// 36 nodes issues 7 chunks' worth of lanes instead of 4 waves x 36 lanes);
+// sums meet through LDS atomics (C3 launch 571.4 -> 569.0 ms, profiles/r5ba).
+// 0: each wave takes a quarter of the entry range and its lanes the nodes
+// modulo the next power of two.
+#define CSM_FLAT_LANES 1
 #endif
 constexpr int kMaxRotChunk = kV4MaxRotChunk;
 constexpr int kLists = kMaxClusterShift + 1;
@@ -792,6 +802,14 @@ __device__ __forceinline__ void V4Score(Shared& sh, const uint32_t* cells, const
                                         int raw_end, const SubmapDesc& sm) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nodes = Uniform(sh.nodes);
+#if CSM_FLAT_LANES
+  static_assert(!CSM_LANE_SORT, "CSM_FLAT_LANES maps lanes to nodes itself");
+  // Thread -> (node, chunk); chunk g of `groups` walks entries g, g + groups, ...
+  const int groups = kSearchThreads / nodes;
+  const int g = static_cast<int>(threadIdx.x) / nodes;
+  const bool active = g < groups;
+  const int node = active ? static_cast<int>(threadIdx.x) - g * nodes : 0;
+#else
   // Lane -> (node, entry group): node = lane mod pw, pw = nodes rounded up to
   // a power of two; the lanes of the pw - nodes missing nodes sit out.
   const int pw = nodes <= 1 ? 1 : 1 << (32 - __clz(nodes - 1));
@@ -803,6 +821,7 @@ __device__ __forceinline__ void V4Score(Shared& sh, const uint32_t* cells, const
   const int node = active ? lane & (pw - 1) : 0;
 #endif
   const int g = lane / pw;
+#endif
   // Each node scores its children at its own child level: one descriptor
   // spans the whole pyramid, the level is a per-lane byte offset.
   const int level = sh.node_level[node] - 1;
@@ -819,8 +838,15 @@ __device__ __forceinline__ void V4Score(Shared& sh, const uint32_t* cells, const
   const int cx = sh.node_xo[node] + L[5];
   const int cy = sh.node_yo[node] + L[5];
   const int blen = Uniform(sh.batch_len);
+#if CSM_FLAT_LANES
+  // Entry indices i + g for i = 0, groups, ... up to the batch's longest list.
+  const int s = 0, e = Uniform((blen + groups - 1) / groups * groups);
+  (void)lane;
+  (void)wave;
+#else
   const int quarter = (blen + kWaves - 1) / kWaves;
   const int s = Uniform(min(blen, wave * quarter)), e = Uniform(min(blen, wave * quarter + quarter));
+#endif
   constexpr int kOOB = 0x7ffffff0;
   constexpr int U = CSM_U_QUAD;
   uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
@@ -879,6 +905,14 @@ __device__ __forceinline__ void V4Score(Shared& sh, const uint32_t* cells, const
       accumulate(vv, in ? (raw ? 1u : Cn[j]) : 0u);
     }
   }
+#if CSM_FLAT_LANES
+  if (active && (a0 | a1 | a2 | a3) != 0u) {
+    atomicAdd(&sh.part[node][0], static_cast<int>(a0));
+    atomicAdd(&sh.part[node][1], static_cast<int>(a1));
+    atomicAdd(&sh.part[node][2], static_cast<int>(a2));
+    atomicAdd(&sh.part[node][3], static_cast<int>(a3));
+  }
+#else
   for (int m = pw; m < 64; m <<= 1) {
     a0 += __shfl_xor(a0, m, 64);
     a1 += __shfl_xor(a1, m, 64);
@@ -896,6 +930,7 @@ __device__ __forceinline__ void V4Score(Shared& sh, const uint32_t* cells, const
     atomicAdd(&sh.part[nd][2], static_cast<int>(a2));  // (xo + h, yo)
     atomicAdd(&sh.part[nd][3], static_cast<int>(a3));  // (xo + h, yo + h)
   }
+#endif
 }
 
 // Hex batches (v5): a node at level L scores its 16 grandchildren at level
@@ -909,6 +944,12 @@ __device__ __forceinline__ void V4ScoreHex(Shared& sh, const uint32_t* cells, co
                                            int raw_end, const SubmapDesc& sm) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nodes = Uniform(sh.nodes);
+#if CSM_FLAT_LANES  // as V4Score
+  const int groups = kSearchThreads / nodes;
+  const int g = static_cast<int>(threadIdx.x) / nodes;
+  const bool active = g < groups;
+  const int node = active ? static_cast<int>(threadIdx.x) - g * nodes : 0;
+#else
   const int pw = nodes <= 1 ? 1 : 1 << (32 - __clz(nodes - 1));  // as V4Score
   const int groups = 64 / pw;
   const bool active = (lane & (pw - 1)) < nodes;
@@ -918,6 +959,7 @@ __device__ __forceinline__ void V4ScoreHex(Shared& sh, const uint32_t* cells, co
   const int node = active ? lane & (pw - 1) : 0;
 #endif
   const int g = lane / pw;
+#endif
   const int level = sh.node_level[node] - 2;
   const int* L = sh.lv[level];
   const int qw = L[0], qh = L[1], qoff = L[2], pws16 = L[3], ps16 = L[4];
@@ -932,8 +974,14 @@ __device__ __forceinline__ void V4ScoreHex(Shared& sh, const uint32_t* cells, co
   const int cx = sh.node_xo[node] + L[5];
   const int cy = sh.node_yo[node] + L[5];
   const int blen = Uniform(sh.batch_len);
+#if CSM_FLAT_LANES
+  const int s = 0, e = Uniform((blen + groups - 1) / groups * groups);
+  (void)lane;
+  (void)wave;
+#else
   const int quarter = (blen + kWaves - 1) / kWaves;
   const int s = Uniform(min(blen, wave * quarter)), e = Uniform(min(blen, wave * quarter + quarter));
+#endif
   constexpr int kOOB = 0x7ffffff0;
   constexpr int U = CSM_U_HEX;
   uint32_t acc[16];
@@ -1012,6 +1060,13 @@ __device__ __forceinline__ void V4ScoreHex(Shared& sh, const uint32_t* cells, co
       accumulate(vv, in ? (raw ? 1u : Cn[j]) : 0u);
     }
   }
+#if CSM_FLAT_LANES
+  if (active) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if (acc[j] != 0u) atomicAdd(&sh.part[node][j], static_cast<int>(acc[j]));
+  }
+#else
   for (int m = pw; m < 64; m <<= 1) {
 #pragma unroll
     for (int j = 0; j < 16; ++j) acc[j] += __shfl_xor(acc[j], m, 64);
@@ -1025,6 +1080,7 @@ __device__ __forceinline__ void V4ScoreHex(Shared& sh, const uint32_t* cells, co
 #pragma unroll
     for (int j = 0; j < 16; ++j) atomicAdd(&sh.part[nd][j], static_cast<int>(acc[j]));
   }
+#endif
 }
 
 // Cluster key of a packed cell (int16 x | int16 y << 16): both coordinates
