@@ -62,15 +62,17 @@ for st in "$@"; do
       python3 tools/traffic_json.py $OUT/c3pmc $OUT/traffic_c3.json $(python3 -c "import sys; sys.path.insert(0,'.'); import bench; print(bench.KERNEL_TAG)") $ms c3 2000 4 16 ;;
     c5)
       mkdir -p $OUT/pmc3d
-      timeout -k 10 300 python -u tools/probe_c5.py > $OUT/c5.json 2> $OUT/c5.err || { tail -20 $OUT/c5.err; exit 1; }
+      # --c5-dropin-calls 0: the single-call leg's small dispatches would
+      # otherwise dominate the per-dispatch averages of the PMC passes.
+      timeout -k 10 300 python -u tools/probe_c5.py --c5-dropin-calls 0 > $OUT/c5.json 2> $OUT/c5.err || { tail -20 $OUT/c5.err; exit 1; }
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/$OUT/c5trace \
-        -o c5 --output-format csv -- python3 $R/tools/probe_c5.py > $R/$OUT/c5trace.json 2> $R/$OUT/c5trace.err) \
+        -o c5 --output-format csv -- python3 $R/tools/probe_c5.py --c5-dropin-calls 0 > $R/$OUT/c5trace.json 2> $R/$OUT/c5trace.err) \
         || { tail -20 $OUT/c5trace.err; exit 1; }
       i=0
       for g in "FETCH_SIZE" "TCC_HIT_sum TCC_MISS_sum TCC_REQ_sum" "TA_TA_BUSY_sum TA_BUFFER_READ_WAVEFRONTS_sum GRBM_GUI_ACTIVE" \
                "TD_TD_BUSY_sum GRBM_COUNT"; do
         (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 240 rocprofv3 --pmc $g -d $R/$OUT/pmc3d/p$i -o run \
-          --output-format csv -- python3 $R/tools/probe_c5.py > $R/$OUT/pmc3d/p$i.json 2> $R/$OUT/pmc3d/p$i.log) \
+          --output-format csv -- python3 $R/tools/probe_c5.py --c5-dropin-calls 0 > $R/$OUT/pmc3d/p$i.json 2> $R/$OUT/pmc3d/p$i.log) \
           || { echo "c5 pmc pass $i failed"; tail -5 $OUT/pmc3d/p$i.log; exit 1; }
         i=$((i+1))
       done

@@ -4,7 +4,9 @@
 #     -> traffic_c3.json, traffic_c2.json;
 #  2. the C3 gather roofline: a CSM_KPROF pass (variants/kprof5, lines per
 #     gather) and a TD/TA pass on the same slice -> gather_c3.json;
-#  3. C5: probe, kernel trace, PMC passes of fast3d_search -> traffic_c5.json;
+#  3. C5: probe, kernel trace, PMC passes of fast3d_search -> traffic_c5.json
+#     (superseded by r5bd: these passes averaged over the single-call leg's
+#     small dispatches too);
 #  (the default bench.py run reading those files: r5az_session.sh).
 set -u
 O=gpurun_out/r5ay
