@@ -112,11 +112,44 @@ def parse():
                    help="rank 0 writes the gathered C3 and C5 constraint records to this .npz")
     p.add_argument("--cpu-pairs", type=int, default=0,
                    help="CPU baseline sample size (0: 2000 for C3, sized to --cpu-seconds for C2)")
+    p.add_argument("--parity-pairs", type=int, default=-1,
+                   help="C3 pairs of the timed run compared with the oracle afterwards (-1: the "
+                        "CPU baseline's 2000 at N = 1, 500 at N > 1; 0: none). At N > 1 the rank "
+                        "that claims a sampled pair keeps its result; rank 0 gathers and checks them")
     return p.parse_args()
+
+
+def launch_ranks(args):
+    """`bench.py --gpus N` (N > 1) run without a launcher: start N ranks under
+    torch.distributed.run as a child process, before this process touches the
+    GPU, and exit with its status. Under a launcher WORLD_SIZE must equal
+    --gpus, so a scaling line can never silently measure fewer GPUs."""
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is None:
+        if args.gpus <= 1:
+            return
+        import socket
+        import subprocess
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+               f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+               "--master-port", str(port), os.path.abspath(__file__), *sys.argv[1:]]
+        print(f"bench: --gpus {args.gpus} without a launcher: starting {args.gpus} ranks "
+              "(torch.distributed.run)", file=sys.stderr, flush=True)
+        sys.exit(subprocess.call(cmd, env=env))
+    if int(ws) != args.gpus:
+        print(f"bench: WORLD_SIZE={ws} but --gpus {args.gpus}: refusing to report a {ws}-rank "
+              f"run as {args.gpus} GPUs", file=sys.stderr, flush=True)
+        sys.exit(2)
 
 
 def main():
     args = parse()
+    launch_ranks(args)
     rank = int(os.environ.get("RANK", "0"))
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -136,7 +169,8 @@ def main():
 
     csm = load_pkg()
     ctx = csm.Context(device)
-    comm, transport = make_comm_checked(csm, ctx, args, rank, world_size, dist, coll_dev)
+    comm, transport, comm_ranks = make_comm_checked(csm, ctx, args, rank, world_size, dist,
+                                                    coll_dev)
     cdist = importlib.import_module("cartographer_amd.distributed")
     if comm is not None:
         def gather(rec):
@@ -154,6 +188,7 @@ def main():
     if args.workload == "c3":
         out, errors = c3_run(csm, ctx, args, rank, world_size, dist, coll_dev, comm, gather,
                              transport, barrier_sync)
+        out["comm_ranks"] = comm_ranks
     else:
         out, errors = c2_run(csm, ctx, args, rank, world_size, dist, coll_dev, gather, transport,
                              barrier_sync, headline=True)
@@ -407,9 +442,12 @@ def make_comm_checked(csm, ctx, args, rank, world_size, dist, coll_dev):
     (all_reduce MIN) before any of them uses it: if one failed, ALL exit
     non-zero. There is no fallback transport, so a scaling run either
     measures the product path or fails visibly.
-    Returns (comm or None at N = 1, transport name)."""
+    Once up, the communicator must report world_size ranks, and an
+    all-reduce over it (RCCL at N > 1 in production) must count every rank:
+    that count is the line's comm_ranks.
+    Returns (comm or None at N = 1, transport name, ranks the communicator spans)."""
     if dist is None:
-        return None, "local"
+        return None, "local", 1
     import torch
     from torch.distributed import distributed_c10d
     store = distributed_c10d._get_default_store()
@@ -443,7 +481,12 @@ def make_comm_checked(csm, ctx, args, rank, world_size, dist, coll_dev):
         print(f"bench: rank {rank}: csm_comm ({backend}) not available on every rank"
               + (f": {err}" if err else ""), file=sys.stderr, flush=True)
         sys.exit(4)
-    return comm, f"csm_comm_{backend}"
+    ranks = int(comm.allreduce(np.ones(1, np.int64))[0])
+    if comm.size() != world_size or comm.rank() != rank or ranks != world_size:
+        print(f"bench: rank {rank}: csm_comm spans {ranks} ranks (size {comm.size()}, rank "
+              f"{comm.rank()}), expected {world_size}", file=sys.stderr, flush=True)
+        sys.exit(4)
+    return comm, f"csm_comm_{backend}", ranks
 
 
 def rt2d_bench(csm, ctx, args):
@@ -1147,8 +1190,11 @@ def cpu_pairs_2d(world, pair_sub, pair_node, args, what):
     # The oracle's result for every sample index it ran (probes and the main
     # run): the bench's parity check against the GPU's results of the same
     # pairs (c3_run).
+    # Per pair also the oracle's work counters (lookups, candidates per
+    # level; oracle_fast2d_match_pairs_stats): work_ratio's reference side.
     ores = {"done": np.zeros(len(inv), bool), "matched": np.zeros(len(inv), bool),
-            "score": np.zeros(len(inv), np.float32), "pose": np.zeros((len(inv), 3))}
+            "score": np.zeros(len(inv), np.float32), "pose": np.zeros((len(inv), 3)),
+            "stats": np.zeros((len(inv), 16), np.int64)}
 
     def run(k, threads):
         # Consecutive slices of the (shuffled) sample: probes and the main
@@ -1164,12 +1210,14 @@ def cpu_pairs_2d(world, pair_sub, pair_node, args, what):
             pn = np.ascontiguousarray(pair_node[idx], np.int32)
             scores, poses = np.zeros(kk, np.float32), np.zeros(3 * kk)
             matched, task = np.zeros(kk, np.int32), np.zeros(kk)
-            wall += o.lib.oracle_fast2d_match_pairs(
+            st = np.zeros((kk, 16), np.int64)
+            wall += o.lib.oracle_fast2d_match_pairs_stats(
                 handles, pts.ctypes.data_as(P(C.c_float)), offs.ctypes.data_as(P(C.c_int64)),
                 ps.ctypes.data_as(P(C.c_int32)), pn.ctypes.data_as(P(C.c_int32)), kk, threads,
                 args.min_score, scores.ctypes.data_as(P(C.c_float)),
                 poses.ctypes.data_as(P(C.c_double)), matched.ctypes.data_as(P(C.c_int32)),
-                task.ctypes.data_as(P(C.c_double)))
+                task.ctypes.data_as(P(C.c_double)), st.ctypes.data_as(P(C.c_int64)))
+            ores["stats"][idx] = st
             tasks.append(task)
             ores["done"][idx] = True
             ores["matched"][idx] = matched != 0
@@ -1190,6 +1238,106 @@ def cpu_pairs_2d(world, pair_sub, pair_node, args, what):
     k = args.cpu_pairs or max(4 * threads, int(rate * args.cpu_seconds))
     wall, task = run(k, threads)
     return summarize_cpu(k, wall, task, threads, cpu, probes, what), ores
+
+
+def gather_sample(sample, comm, csm):
+    """The sampled pairs' GPU results held by every rank (each kept the
+    results of the chunks it claimed) to rank 0 over the C-ABI communicator
+    (csm_comm_gather): (sample index, csm_result2d) rows; rank 0 fills its
+    sample table with them. Every sampled pair must come back from some rank
+    (parity_failures counts the missing)."""
+    row = np.dtype([("i", "<i8"), ("r", csm.RESULT_DTYPE)])
+    have = np.nonzero(sample["have"])[0]
+    mine = np.zeros(len(have), row)
+    mine["i"] = have
+    mine["r"] = sample["gpu"][have]
+    blobs = comm.gather(mine.tobytes())
+    if blobs is None:  # not rank 0
+        return
+    for b in blobs:
+        rows = np.frombuffer(b, row)
+        sample["gpu"][rows["i"]] = rows["r"]
+        sample["have"][rows["i"]] = True
+
+
+def work_ratio(csm, ctx, world, opts, sample, ores, args, queue_levels):
+    """SURVEY §8(d)'s reference lookup count next to the GPU's work, on the
+    same sampled pairs. Reference side: the oracle's counters from the parity
+    run (GetValue calls, fast_correlative_scan_matcher_2d.cc:319-330, and
+    candidates scored per level, :335-378). GPU side: the sampled pairs
+    searched again after the timed region, grouped by submap, with the
+    kernel's counters (gpu_sample_work)."""
+    done = ores["done"]
+    g_lv, g_cand, g_vals = gpu_sample_work(csm, ctx, world, opts, sample["sub"][done],
+                                           sample["node"][done], args.min_score)
+    return work_ratio_fields(ores["stats"][done], g_lv, g_cand, g_vals, queue_levels)
+
+
+def gpu_sample_work(csm, ctx, world, opts, subs, nodes, min_score):
+    """The GPU search's work on the given (submap, node) pairs: candidates
+    scored per level (12), all candidates, and candidate values its gathers
+    fetch (1 B each: 4 per quad entry, 16 per hex entry, an entry being a
+    point or a weighted cluster; the kernel's issued bytes), summed over the
+    pairs. Searched in groups of up to 32 submaps on `ctx`, untimed."""
+    uniq = np.unique(subs)
+    g_lv = np.zeros(12)
+    g_cand = g_vals = 0.0
+    scans = csm.ScanSet(None, ctx, packed=(world.points, world.offsets))
+    ctx.enable_timing(True)
+    for a in range(0, len(uniq), 32):
+        grp = uniq[a:a + 32]
+        mats = [csm.FastCorrelativeScanMatcher2D(world.grid(int(s)), opts, ctx) for s in grp]
+        pos = {int(s): i for i, s in enumerate(grp)}
+        sel = np.nonzero(np.isin(subs, grp))[0]
+        sub_local = np.array([pos[int(s)] for s in subs[sel]], np.int32)
+        pairs = csm.make_pairs(sub_local, np.asarray(nodes)[sel].astype(np.int32), min_score,
+                               full_submap=True)
+        ctx.reset_timing()
+        csm.match_batch(mats, scans, pairs, ctx)
+        tm = ctx.timing()
+        lv, _ = ctx.level_stats()
+        g_lv[:len(lv)] += np.asarray(lv, np.float64)[:12]
+        g_cand += tm.search_candidates
+        g_vals += tm.search_lookups
+        for m in mats:
+            m.close()
+    ctx.enable_timing(False)
+    ctx.reset_timing()
+    scans.close()
+    return g_lv, g_cand, g_vals
+
+
+def work_ratio_fields(stats, gpu_levels, gpu_candidates, gpu_values, queue_levels):
+    """work_ratio's line fields from the oracle's per-pair counters (rows of
+    16: lookups, scans, lowest-resolution candidates, candidates per level
+    0..12) and the GPU's totals over the same pairs. Both count a candidate at
+    the level it is scored at; the GPU's pyramid is deeper (automatic depth),
+    its hex levels skip the level between, and its inner bounds are the
+    looser clustered ones, so levels differ and the totals are
+    what compare."""
+    stats = np.asarray(stats, np.int64).reshape(-1, 16)
+    k = max(len(stats), 1)
+    o_lv = stats[:, 3:16].sum(0) / k
+    o_cand = float(o_lv.sum())
+    o_look = float(stats[:, 0].sum()) / k
+    g_lv = np.asarray(gpu_levels, np.float64) / k
+    g_cand, g_vals = gpu_candidates / k, gpu_values / k
+    return {"pairs": len(stats),
+            "oracle": {"candidates_per_pair": o_cand, "candidates_per_pair_by_level": o_lv.tolist(),
+                       "lookups_per_pair": o_look,
+                       "what": "reference algorithm (oracle restatement): candidates scored at "
+                               "each level and GetValue calls (candidates x points)"},
+            "gpu_same_pairs": {"candidates_per_pair": g_cand,
+                               "candidates_per_pair_by_level": g_lv.tolist(),
+                               "candidate_values_per_pair": g_vals,
+                               "what": "the same pairs searched again after the timed region: "
+                                       "candidates scored per level, and candidate values the "
+                                       "gathers fetch (1 B each: 4 per quad entry, 16 per hex "
+                                       "entry, an entry being a point or a weighted cluster)"},
+            "gpu_queue_candidates_per_pair": float(np.sum(queue_levels)),
+            "candidates_ratio": g_cand / o_cand if o_cand else None,
+            "leaf_candidates_ratio": float(g_lv[0] / o_lv[0]) if o_lv[0] else None,
+            "lookups_ratio": g_vals / o_look if o_look else None}
 
 
 def parity_2d(sample, ores):
@@ -1382,13 +1530,19 @@ def c3_run(csm, ctx, args, rank, world_size, dist, coll_dev, comm, gather, trans
             return comm.fetch_add(key, 1)
     claim.local = {}
 
-    # The CPU baseline's sample of the queue, drawn up front: the timed run
-    # keeps the GPU's result of each sampled pair, which is then compared with
-    # the oracle's result of the same pair (parity_sample; rank 0 at N = 1).
+    # The parity sample of the queue, drawn up front (the same seed on every
+    # rank, so every rank holds rank 0's draw): the timed run keeps the GPU's
+    # result of each sampled pair on whichever rank claims it; afterwards the
+    # results are gathered to rank 0 and compared with the oracle's result of
+    # the same pair (parity_sample). At N = 1 the oracle's run on the sample is
+    # also the CPU baseline.
     sample = None
-    if rank == 0 and world_size == 1 and not args.no_cpu:
+    k_s = args.parity_pairs
+    if k_s < 0:
+        k_s = 0 if (world_size == 1 and args.no_cpu) else \
+            (args.cpu_pairs or 2000) if world_size == 1 else 500
+    if k_s > 0:
         rng = np.random.RandomState(12345)
-        k_s = args.cpu_pairs or 2000
         # Submaps of the timed queue (all of them when it covers the queue).
         s_sub = np.unique(queue)[rng.randint(0, len(np.unique(queue)), k_s)]
         s_node = rng.randint(0, N, k_s)
@@ -1446,6 +1600,9 @@ def c3_run(csm, ctx, args, rank, world_size, dist, coll_dev, comm, gather, trans
     allrec = gather(np.concatenate(recs) if recs else np.zeros((0, cdist.RECORD_WIDTH)))
     barrier_sync()
     elapsed = time.perf_counter() - t_start
+    if sample is not None and comm is not None:
+        # After the timed region: every rank's results of sampled pairs to rank 0.
+        gather_sample(sample, comm, csm)
     for c in ctxs:
         c.enable_timing(False)
     tm = sum_timing(csm, [c.timing() for c in ctxs])
@@ -1505,13 +1662,18 @@ def c3_run(csm, ctx, args, rank, world_size, dist, coll_dev, comm, gather, trans
         with open(f"{args.c3_tie_log}.rank{rank}.json", "w") as f:
             json.dump({"seed": args.seed, "nodes": N, "submaps": S, "min_score": args.min_score,
                        "ties": sorted(done["ties"])}, f)
-    if sample is not None:
+    if sample is not None and rank == 0:
         args_c = argparse.Namespace(**vars(args))
         args_c.cpu_pairs = len(sample["sub"])
-        out["cpu_baseline"], ores = cpu_pairs_2d(world, sample["sub"], sample["node"], args_c,
-                                                 "uniformly sampled (submap, node) pairs of the C3 queue")
-        out["speedup_vs_cpu"] = out["value"] / out["cpu_baseline"]["value"]
+        cb, ores = cpu_pairs_2d(world, sample["sub"], sample["node"], args_c,
+                                "uniformly sampled (submap, node) pairs of the C3 queue")
+        if world_size == 1 and not args.no_cpu:
+            out["cpu_baseline"] = cb
+            out["speedup_vs_cpu"] = out["value"] / out["cpu_baseline"]["value"]
         out["parity_sample"] = parity_2d(sample, ores)
+        out["parity_sample"]["ranks"] = world_size
+        out["work_ratio"] = work_ratio(csm, ctx, world, opts, sample, ores, args,
+                                       out["search_levels"]["candidates_per_pair"])
         bad = parity_failures(out["parity_sample"])
         if bad:
             print(f"bench: C3 parity sample: {bad} of {out['parity_sample']['compared']} pairs differ "

@@ -72,15 +72,7 @@ struct SubmapDesc {
 
 constexpr int kMaxClusterShift = 3;  // clusters of 1, 2, 4, 8 cells per side
 
-#ifndef CSM_HEX8
-#define CSM_HEX8 0
-#endif
-// CSM_HEX8 = 1: 8-byte hex entries, 16 nibbles q = ceil(M / 17), so a hex
-// batch's sums are 17 x sum(count x q) >= the 16-byte plane's sums: still
-// upper bounds, looser, at half the plane bytes. Never at level 0 (leaves
-// are exact): hex_mask drops bit 2 under it.
-constexpr int kHexEntryBytes = CSM_HEX8 ? 8 : 16;
-constexpr int kHexScale = CSM_HEX8 ? 17 : 1;
+constexpr int kHexEntryBytes = 16;  // one hex entry: 16 uint8 grandchild values
 
 // One (node, submap) search.
 struct PairDesc {

@@ -1312,7 +1312,6 @@ int csm_fast2d_create(csm_context* ctx, const csm_map_limits* limits,
     }
     return total <= 0x7fffff00u;
   };
-  if (CSM_HEX8) hex_mask &= ~4u;  // no quantized plane at level 0
   if (!layout(hex_mask)) {
     if (!hex_mask || !layout(0)) return CSM_ERANGE;
     hex_mask = 0;
@@ -1597,7 +1596,11 @@ static int SingleMatch(const csm_fast2d* m, const csm_pose2d* initial, int full,
   }();
   if (!coalesce) {
     std::vector<SingleReq2*> one{&r};
-    r.rc = RunSingleBatch(owner, one, owner->calls_in_flight.load());
+    try {
+      r.rc = RunSingleBatch(owner, one, owner->calls_in_flight.load());
+    } catch (...) {  // no exception crosses the C-ABI
+      r.rc = CSM_ENOMEM;
+    }
   } else {
     std::unique_lock<std::mutex> lk(owner->co_mu);
     owner->co_queue.push_back(&r);
@@ -1629,7 +1632,15 @@ static int SingleMatch(const csm_fast2d* m, const csm_pose2d* initial, int full,
         }();
         const int share = fixed_share ? fixed_share : owner->co_leaders;
         lk.unlock();
-        const int rc = RunSingleBatch(owner, take, share);
+        // Whatever happens in the batch (an allocation that throws), every
+        // request taken is answered and the leader slot given back below;
+        // otherwise their callers would wait on co_cv forever.
+        int rc;
+        try {
+          rc = RunSingleBatch(owner, take, share);
+        } catch (...) {
+          rc = CSM_ENOMEM;
+        }
         lk.lock();
         for (SingleReq2* q : take) {
           q->rc = rc;

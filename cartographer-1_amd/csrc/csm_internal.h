@@ -106,41 +106,58 @@ struct PinnedBuf {
   T* as() const { return static_cast<T*>(ptr); }
 };
 
-// Pinned staging slots, each with the event of its last upload. Take(): a
-// slot whose upload has finished (round robin from the last one taken), else
-// a new slot (up to kMax), else the next one in turn once its upload is done.
-// A deque, so slots never move. The caller records `copied` after its copy.
+// Pinned staging slots, each with the event of its last upload. Take(bytes):
+// the smallest slot whose upload has finished and that already holds `bytes`;
+// else a new slot sized for this request (while fewer than kMax slots and
+// kMaxPinned bytes are held); else a finished slot (or, when none is, the
+// next one in turn once its upload is done) regrown to the request. A slot is
+// never regrown while a fitting one is free, because freeing pinned memory
+// (hipHostFree) waits for the device, which may be busy with a search kernel
+// for tens of ms. Each slot is sized to the requests it served, not to the
+// largest upload ever staged, so one large batch upload does not inflate
+// every later small create's slot. A deque, so slots never move. The caller
+// records `copied` after its copy.
 struct StageRing {
   struct Slot {
     PinnedBuf buf;
     hipEvent_t copied = nullptr;
   };
   static constexpr size_t kMax = 128;
+  static constexpr size_t kMaxPinned = size_t{1} << 30;  // pinned bytes past which slots are reused
   std::deque<Slot> slots;
   size_t next = 0;
-  size_t largest = 0;  // every slot is sized for the largest upload seen: regrowing
-                       // (hipHostFree) would wait for the device
+  size_t pinned = 0;  // sum of the slots' buffer sizes
   ~StageRing() {
     for (Slot& s : slots)
       if (s.copied) (void)hipEventDestroy(s.copied);
   }
   int Take(size_t bytes, Slot** out) {
-    size_t at = slots.size();
-    for (size_t k = 0; k < slots.size() && at == slots.size(); ++k) {
-      const size_t i = (next + k) % slots.size();
-      if (hipEventQuery(slots[i].copied) == hipSuccess) at = i;
+    const size_t n = slots.size();
+    size_t fit = n, any = n;  // smallest finished slot that fits; some finished slot
+    for (size_t k = 0; k < n; ++k) {
+      const size_t i = (next + k) % n;
+      if (hipEventQuery(slots[i].copied) != hipSuccess) continue;
+      if (any == n) any = i;
+      if (slots[i].buf.bytes >= bytes && (fit == n || slots[i].buf.bytes < slots[fit].buf.bytes)) fit = i;
     }
-    if (at == slots.size() && slots.size() < kMax) {
+    size_t at = fit;
+    if (at == n && n < kMax && (n == 0 || pinned + bytes <= kMaxPinned)) {
       slots.emplace_back();
       if (hipEventCreateWithFlags(&slots.back().copied, hipEventDisableTiming) != hipSuccess) return CSM_EHIP;
-    } else if (at == slots.size()) {
-      at = next % slots.size();
+      at = n;
+    } else if (at == n && any != n) {
+      at = any;
+    } else if (at == n) {
+      at = next % n;
       if (hipEventSynchronize(slots[at].copied) != hipSuccess) return CSM_EHIP;
     }
     next = at + 1;
     *out = &slots[at];
-    largest = std::max(largest, bytes);
-    return slots[at].buf.Reserve(largest);
+    PinnedBuf& b = slots[at].buf;
+    pinned -= b.bytes;
+    const int rc = b.Reserve(bytes);
+    pinned += b.bytes;
+    return rc;
   }
 };
 
@@ -257,8 +274,10 @@ struct csm_context {
   // csm_fast3d_create_batch's job lists: one slot per upload in flight (a
   // create takes a slot whose copy has finished, or a new one; TakeStageSlot),
   // so a create never waits for an earlier create's upload, which may sit
-  // behind a search kernel holding every CU.
-  csm::StageRing f3_grid_stage, f3_job_stage;
+  // behind a search kernel holding every CU. Batched grid creates
+  // (csm_hybrid_grid_create_batch) stage whole groups and have a ring of
+  // their own, so single creates never take a slot sized for a batch.
+  csm::StageRing f3_grid_stage, f3_grid_batch_stage, f3_job_stage;
   // Batched pyramid builds (csm_fast3d_create_batch): job lists.
   csm::DevBuf f3_jobs;
   // Voxel filter scratch (voxel_filter.hip).

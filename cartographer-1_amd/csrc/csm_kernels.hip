@@ -600,8 +600,6 @@ __global__ void pyramid_widen(const uint8_t* __restrict__ level, int wnx, int wn
 // Polyphase with period P = 4h: plane (X' mod P, Y' mod P), entry
 // (X' / P, Y' / P), so sibling nodes' lookups of one point are adjacent
 // entries.
-// CSM_HEX8: the 8-byte form, nibbles q = ceil(M / 17): dword d, byte b holds
-// q(2d, b) in its low and q(2d + 1, b) in its high nibble.
 __global__ void pyramid_hex(const uint8_t* __restrict__ mlev, int mw, int mh, int log_h,
                             void* __restrict__ out, int qw, int qh, int pws, int pph, int total) {
   const int o = blockIdx.x * blockDim.x + threadIdx.x;
@@ -625,17 +623,7 @@ __global__ void pyramid_hex(const uint8_t* __restrict__ mlev, int mw, int mh, in
       w[a] = m(xa, Y) | (m(xa, Y + h) << 8) | (m(xa, Y + 2 * h) << 16) | (m(xa, Y + 3 * h) << 24);
     }
   }
-  if (CSM_HEX8) {
-    // Per byte: ceil(v / 17) = (v + 16) / 17 <= 15, as (x * 241) >> 12 for x <= 271.
-    auto q = [](uint32_t x) {
-      uint32_t r = 0;
-      for (int b = 0; b < 4; ++b) r |= ((((x >> (8 * b)) & 0xffu) + 16u) * 241u >> 12) << (8 * b);
-      return r;
-    };
-    static_cast<uint2*>(out)[o] = make_uint2(q(w[0]) | (q(w[1]) << 4), q(w[2]) | (q(w[3]) << 4));
-  } else {
-    static_cast<uint4*>(out)[o] = make_uint4(w[0], w[1], w[2], w[3]);
-  }
+  static_cast<uint4*>(out)[o] = make_uint4(w[0], w[1], w[2], w[3]);
 }
 
 // ---------------------------------------------------------------- K2-K4 v4 -
@@ -655,7 +643,7 @@ __global__ void pyramid_hex(const uint8_t* __restrict__ mlev, int mw, int mh, in
 //
 // The DFS stack mixes the chunk's rotations; a batch pops up to 64 nodes
 // (deepest level first, best bound first): a thread takes one node and a
-// strided subset of that node's list (CSM_FLAT_LANES), and per entry issues
+// strided subset of that node's list (flat lanes, below), and per entry issues
 // ONE dword load from the quad layout that returns all four children's
 // values. The threads' sums meet in LDS; all waves combine, prune and push
 // survivors sorted (best on top), wave 0 pops the next batch. Roots are
@@ -667,16 +655,11 @@ __global__ void pyramid_hex(const uint8_t* __restrict__ mlev, int mw, int mh, in
 #ifndef CSM_U_HEX
 #define CSM_U_HEX 4   // hex gathers in flight per lane (V4ScoreHex)
 #endif
-#ifndef CSM_FLAT_LANES
-// 1: the scoring lanes of all 4 waves take (node, chunk) pairs, node = t mod
-// nodes, chunk = t / nodes over the workgroup's 256 threads, and chunk c of
-// C = 256 / nodes walks entries c, c + C, ... of the node's list (a batch of
-// 36 nodes issues 7 chunks' worth of lanes instead of 4 waves x 36 lanes);
+// Scoring lanes (V4Score, V4ScoreHex): the 4 waves' 256 threads take (node,
+// chunk) pairs, node = t mod nodes, chunk = t / nodes, and chunk c of C =
+// 256 / nodes walks entries c, c + C, ... of the node's list (a batch of 36
+// nodes issues 7 chunks' worth of lanes instead of 4 waves x 36 lanes); the
 // sums meet through LDS atomics (C3 launch 571.4 -> 569.0 ms, profiles/r5ba).
-// 0: each wave takes a quarter of the entry range and its lanes the nodes
-// modulo the next power of two.
-#define CSM_FLAT_LANES 1
-#endif
 constexpr int kMaxRotChunk = kV4MaxRotChunk;
 constexpr int kLists = kMaxClusterShift + 1;
 
@@ -686,22 +669,7 @@ template <int kKids>
 struct V4Shared {
   // LDS part of the DFS stack (v5: a quarter, so 6 workgroups fit a CU's
   // LDS with their 16-child sums); the rest spills to global memory.
-#ifndef CSM_MASK_OOB
-// 1: lanes whose entry is out of range (off the plane, or past the node's
-// list) skip the gather instead of issuing it at the out-of-range offset.
-#define CSM_MASK_OOB 0
-#endif
-#ifndef CSM_LANE_SORT
-// 1: the scoring lanes take the batch's nodes in (level, rotation, y, x)
-// order (wave 0 sorts the popped batch), so that nodes on one row of one
-// plane sit in the same 4-lane groups; the node slots, and so the push
-// order, stay as popped.
-#define CSM_LANE_SORT 0
-#endif
-#ifndef CSM_V4_RING
-#define CSM_V4_RING 0  // LDS stack entries (0: 1024 for v4, 256 for v5)
-#endif
-  static constexpr int kStackLds = CSM_V4_RING ? CSM_V4_RING : (kKids == 16 ? kStack2 / 4 : kStack2);
+  static constexpr int kStackLds = kKids == 16 ? kStack2 / 4 : kStack2;
   static constexpr int kStackCapacity = kStackLds + kSpill2;
   uint2 stack[kStackLds];  // w0: xo | yo << 16; w1: sum | rot << 22 | level << 27
   int part[kBatchNodes][kKids];  // children sums, accumulated by the 4 waves (LDS atomics)
@@ -730,9 +698,6 @@ struct V4Shared {
 #ifdef CSM_KPROF
   unsigned long long kp_lines[kMaxLevels], kp_instr[kMaxLevels], kp_qlines[kMaxLevels];
   unsigned long long kp_active[kMaxLevels], kp_oob[kMaxLevels];
-#endif
-#if CSM_LANE_SORT
-  int lane_node[kBatchNodes];  // scoring lane slot -> node (CSM_LANE_SORT)
 #endif
 };
 
@@ -789,39 +754,15 @@ __device__ void CountLines(Shared& sh, int level, int ad, int oob) {
 // g, g + groups, ... of the node's list (cells, counts). A child's sum is
 // sum_k cnt[k] * value over the list: the reference's per-point sum
 // regrouped at level 0, an upper bound of it at coarser levels.
-#ifndef CSM_CPOL_QUAD
-// Cache-policy bits of the quad and hex gathers (buffer-load aux operand:
-// 1 sc0, 2 nt, 16 sc1); 0 = default policy (experiments: profiles/r4ae).
-#define CSM_CPOL_QUAD 0
-#endif
-#ifndef CSM_CPOL_HEX
-#define CSM_CPOL_HEX 0
-#endif
 template <typename Shared>
 __device__ __forceinline__ void V4Score(Shared& sh, const uint32_t* cells, const uint8_t* cnts,
                                         int raw_end, const SubmapDesc& sm) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nodes = Uniform(sh.nodes);
-#if CSM_FLAT_LANES
-  static_assert(!CSM_LANE_SORT, "CSM_FLAT_LANES maps lanes to nodes itself");
   // Thread -> (node, chunk); chunk g of `groups` walks entries g, g + groups, ...
   const int groups = kSearchThreads / nodes;
   const int g = static_cast<int>(threadIdx.x) / nodes;
   const bool active = g < groups;
   const int node = active ? static_cast<int>(threadIdx.x) - g * nodes : 0;
-#else
-  // Lane -> (node, entry group): node = lane mod pw, pw = nodes rounded up to
-  // a power of two; the lanes of the pw - nodes missing nodes sit out.
-  const int pw = nodes <= 1 ? 1 : 1 << (32 - __clz(nodes - 1));
-  const int groups = 64 / pw;
-  const bool active = (lane & (pw - 1)) < nodes;
-#if CSM_LANE_SORT
-  const int node = active ? sh.lane_node[lane & (pw - 1)] : 0;
-#else
-  const int node = active ? lane & (pw - 1) : 0;
-#endif
-  const int g = lane / pw;
-#endif
   // Each node scores its children at its own child level: one descriptor
   // spans the whole pyramid, the level is a per-lane byte offset.
   const int level = sh.node_level[node] - 1;
@@ -838,15 +779,8 @@ __device__ __forceinline__ void V4Score(Shared& sh, const uint32_t* cells, const
   const int cx = sh.node_xo[node] + L[5];
   const int cy = sh.node_yo[node] + L[5];
   const int blen = Uniform(sh.batch_len);
-#if CSM_FLAT_LANES
   // Entry indices i + g for i = 0, groups, ... up to the batch's longest list.
   const int s = 0, e = Uniform((blen + groups - 1) / groups * groups);
-  (void)lane;
-  (void)wave;
-#else
-  const int quarter = (blen + kWaves - 1) / kWaves;
-  const int s = Uniform(min(blen, wave * quarter)), e = Uniform(min(blen, wave * quarter + quarter));
-#endif
   constexpr int kOOB = 0x7ffffff0;
   constexpr int U = CSM_U_QUAD;
   uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
@@ -886,14 +820,7 @@ __device__ __forceinline__ void V4Score(Shared& sh, const uint32_t* cells, const
       for (int u = 0; u < U; ++u) CSM_COUNT_LINES(level, ad[u], kOOB);
       uint32_t v[U];
   #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if (CSM_MASK_OOB) {
-          v[u] = 0u;
-          if (ad[u] != kOOB) v[u] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, ad[u], 0, CSM_CPOL_QUAD);
-        } else {
-          v[u] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, ad[u], 0, CSM_CPOL_QUAD);
-        }
-      }
+      for (int u = 0; u < U; ++u) v[u] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, ad[u], 0, 0);
   #pragma unroll
       for (int u = 0; u < U; ++u) accumulate(v[u], c[u]);
     }
@@ -901,36 +828,16 @@ __device__ __forceinline__ void V4Score(Shared& sh, const uint32_t* cells, const
       const int idx = i + g;
       const bool in = idx < e && idx < len;
       const int j = in ? idx : 0;
-      const uint32_t vv = __builtin_amdgcn_raw_buffer_load_b32(rsrc, address(P[j], in), 0, CSM_CPOL_QUAD);
+      const uint32_t vv = __builtin_amdgcn_raw_buffer_load_b32(rsrc, address(P[j], in), 0, 0);
       accumulate(vv, in ? (raw ? 1u : Cn[j]) : 0u);
     }
   }
-#if CSM_FLAT_LANES
   if (active && (a0 | a1 | a2 | a3) != 0u) {
-    atomicAdd(&sh.part[node][0], static_cast<int>(a0));
-    atomicAdd(&sh.part[node][1], static_cast<int>(a1));
-    atomicAdd(&sh.part[node][2], static_cast<int>(a2));
-    atomicAdd(&sh.part[node][3], static_cast<int>(a3));
+    atomicAdd(&sh.part[node][0], static_cast<int>(a0));  // (xo,     yo)
+    atomicAdd(&sh.part[node][1], static_cast<int>(a1));  // (xo,     yo + h)
+    atomicAdd(&sh.part[node][2], static_cast<int>(a2));  // (xo + h, yo)
+    atomicAdd(&sh.part[node][3], static_cast<int>(a3));  // (xo + h, yo + h)
   }
-#else
-  for (int m = pw; m < 64; m <<= 1) {
-    a0 += __shfl_xor(a0, m, 64);
-    a1 += __shfl_xor(a1, m, 64);
-    a2 += __shfl_xor(a2, m, 64);
-    a3 += __shfl_xor(a3, m, 64);
-  }
-  if (lane < nodes) {
-#if CSM_LANE_SORT
-    const int nd = sh.lane_node[lane];
-#else
-    const int nd = lane;
-#endif
-    atomicAdd(&sh.part[nd][0], static_cast<int>(a0));  // (xo,     yo)
-    atomicAdd(&sh.part[nd][1], static_cast<int>(a1));  // (xo,     yo + h)
-    atomicAdd(&sh.part[nd][2], static_cast<int>(a2));  // (xo + h, yo)
-    atomicAdd(&sh.part[nd][3], static_cast<int>(a3));  // (xo + h, yo + h)
-  }
-#endif
 }
 
 // Hex batches (v5): a node at level L scores its 16 grandchildren at level
@@ -942,24 +849,11 @@ __device__ __forceinline__ void V4Score(Shared& sh, const uint32_t* cells, const
 template <typename Shared>
 __device__ __forceinline__ void V4ScoreHex(Shared& sh, const uint32_t* cells, const uint8_t* cnts,
                                            int raw_end, const SubmapDesc& sm) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nodes = Uniform(sh.nodes);
-#if CSM_FLAT_LANES  // as V4Score
-  const int groups = kSearchThreads / nodes;
+  const int groups = kSearchThreads / nodes;  // as V4Score
   const int g = static_cast<int>(threadIdx.x) / nodes;
   const bool active = g < groups;
   const int node = active ? static_cast<int>(threadIdx.x) - g * nodes : 0;
-#else
-  const int pw = nodes <= 1 ? 1 : 1 << (32 - __clz(nodes - 1));  // as V4Score
-  const int groups = 64 / pw;
-  const bool active = (lane & (pw - 1)) < nodes;
-#if CSM_LANE_SORT
-  const int node = active ? sh.lane_node[lane & (pw - 1)] : 0;
-#else
-  const int node = active ? lane & (pw - 1) : 0;
-#endif
-  const int g = lane / pw;
-#endif
   const int level = sh.node_level[node] - 2;
   const int* L = sh.lv[level];
   const int qw = L[0], qh = L[1], qoff = L[2], pws16 = L[3], ps16 = L[4];
@@ -974,14 +868,7 @@ __device__ __forceinline__ void V4ScoreHex(Shared& sh, const uint32_t* cells, co
   const int cx = sh.node_xo[node] + L[5];
   const int cy = sh.node_yo[node] + L[5];
   const int blen = Uniform(sh.batch_len);
-#if CSM_FLAT_LANES
   const int s = 0, e = Uniform((blen + groups - 1) / groups * groups);
-  (void)lane;
-  (void)wave;
-#else
-  const int quarter = (blen + kWaves - 1) / kWaves;
-  const int s = Uniform(min(blen, wave * quarter)), e = Uniform(min(blen, wave * quarter + quarter));
-#endif
   constexpr int kOOB = 0x7ffffff0;
   constexpr int U = CSM_U_HEX;
   uint32_t acc[16];
@@ -994,27 +881,10 @@ __device__ __forceinline__ void V4ScoreHex(Shared& sh, const uint32_t* cells, co
                        static_cast<unsigned>(Y) < static_cast<unsigned>(qh);
     const int a = __umul24((((Y & pmask) << sft) | (X & pmask)), ps16) + qoff;
     const int b = __umul24(Y >> sft, pws16) + a;
-    return valid ? ((X >> sft) << (CSM_HEX8 ? 3 : 4)) + b : kOOB;
+    return valid ? ((X >> sft) << 4) + b : kOOB;
   };
-#if CSM_HEX8
-  using HexVec = decltype(__builtin_amdgcn_raw_buffer_load_b64(rsrc, 0, 0, 0));
-  auto hload = [&](int ad) { return __builtin_amdgcn_raw_buffer_load_b64(rsrc, ad, 0, CSM_CPOL_HEX); };
-  // Children (2d, b) and (2d + 1, b) accumulate the low and high nibble of
-  // byte b of dword d times the entry's count (sums in units of 17).
-  auto accumulate = [&](const HexVec& v, uint32_t c) {
-#pragma unroll
-    for (int d = 0; d < 2; ++d) {
-      const uint32_t lo = v[d] & 0x0f0f0f0fu, hi = (v[d] >> 4) & 0x0f0f0f0fu;
-#pragma unroll
-      for (int b = 0; b < 4; ++b) {
-        acc[8 * d + b] = __builtin_amdgcn_udot4(lo, c << (8 * b), acc[8 * d + b], false);
-        acc[8 * d + 4 + b] = __builtin_amdgcn_udot4(hi, c << (8 * b), acc[8 * d + 4 + b], false);
-      }
-    }
-  };
-#else
   using HexVec = decltype(__builtin_amdgcn_raw_buffer_load_b128(rsrc, 0, 0, 0));
-  auto hload = [&](int ad) { return __builtin_amdgcn_raw_buffer_load_b128(rsrc, ad, 0, CSM_CPOL_HEX); };
+  auto hload = [&](int ad) { return __builtin_amdgcn_raw_buffer_load_b128(rsrc, ad, 0, 0); };
   // Child (a, b) accumulates byte b of dword a times the entry's count.
   auto accumulate = [&](const HexVec& v, uint32_t c) {
 #pragma unroll
@@ -1024,7 +894,6 @@ __device__ __forceinline__ void V4ScoreHex(Shared& sh, const uint32_t* cells, co
         acc[4 * a + b] = __builtin_amdgcn_udot4(v[a], c << (8 * b), acc[4 * a + b], false);
     }
   };
-#endif
   if (active) {  // the missing nodes' lanes issue no loads
     int i = s;
     for (; i + U * groups <= e; i += U * groups) {
@@ -1041,14 +910,7 @@ __device__ __forceinline__ void V4ScoreHex(Shared& sh, const uint32_t* cells, co
       for (int u = 0; u < U; ++u) CSM_COUNT_LINES(level, ad[u], kOOB);
       HexVec v[U];
   #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if (CSM_MASK_OOB) {
-          v[u] = HexVec{};
-          if (ad[u] != kOOB) v[u] = hload(ad[u]);
-        } else {
-          v[u] = hload(ad[u]);
-        }
-      }
+      for (int u = 0; u < U; ++u) v[u] = hload(ad[u]);
   #pragma unroll
       for (int u = 0; u < U; ++u) accumulate(v[u], c[u]);
     }
@@ -1060,27 +922,11 @@ __device__ __forceinline__ void V4ScoreHex(Shared& sh, const uint32_t* cells, co
       accumulate(vv, in ? (raw ? 1u : Cn[j]) : 0u);
     }
   }
-#if CSM_FLAT_LANES
   if (active) {
 #pragma unroll
     for (int j = 0; j < 16; ++j)
       if (acc[j] != 0u) atomicAdd(&sh.part[node][j], static_cast<int>(acc[j]));
   }
-#else
-  for (int m = pw; m < 64; m <<= 1) {
-#pragma unroll
-    for (int j = 0; j < 16; ++j) acc[j] += __shfl_xor(acc[j], m, 64);
-  }
-  if (lane < nodes) {
-#if CSM_LANE_SORT
-    const int nd = sh.lane_node[lane];
-#else
-    const int nd = lane;
-#endif
-#pragma unroll
-    for (int j = 0; j < 16; ++j) atomicAdd(&sh.part[nd][j], static_cast<int>(acc[j]));
-  }
-#endif
 }
 
 // Cluster key of a packed cell (int16 x | int16 y << 16): both coordinates
@@ -1163,12 +1009,6 @@ __device__ __forceinline__ uint32_t ClusterMask(int sl) {
 // kFifo = false: the stack is LIFO with the deepest level on top (depth-first,
 // early leaves). kFifo = true: a FIFO ring (level by level: batches fill up
 // with the whole frontier of a level; leaves come last).
-#ifndef CSM_POW2_BATCH
-// 1: a batch takes a power of two of the expandable entries (every lane
-// busy); 0: all of them, up to 64 (fewer, fuller batches; lanes of a
-// non-power-of-two count partly idle).
-#define CSM_POW2_BATCH 0
-#endif
 #ifndef CSM_BEST_REFRESH
 #define CSM_BEST_REFRESH 1  // batches between reads of the pair's global best (power of 2; profiles/r3ap)
 #endif
@@ -1476,7 +1316,7 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
           if (nd < pn) {
             clvl = sh.node_level[nd] - (hexb ? 2 : 1);
             const int h = 1 << clvl;
-            sum = sh.part[nd][c] * (hexb ? kHexScale : 1);
+            sum = sh.part[nd][c];
             sh.part[nd][c] = 0;
             r = sh.node_rot[nd];
             xo = sh.node_xo[nd] + (c >> (lk >> 1)) * h;
@@ -1522,10 +1362,14 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
             // other than the best's: the pair ties there, so nodes bounded by
             // that sum need not be expanded (sh.tie_sum; tie resolution
             // searches those leaves again, ResolveTies).
+            // Only a real incumbent (cur != 0) can be the second leaf: with
+            // none yet, cur_sum is 0 and a single leaf at sum 0 (reachable
+            // when min_score lets sum 0 pass) would look tied.
             if (CSM_TIE_PRUNE && !kCollect && lane == 0) {
               const uint32_t ks = static_cast<uint32_t>(key >> kSumShift);
               if (ks >= cur_sum &&
-                  (hi != HighLeafKey(key) || (key != cur && static_cast<uint32_t>(cur >> kSumShift) == ks)))
+                  (hi != HighLeafKey(key) ||
+                   (cur != 0 && key != cur && static_cast<uint32_t>(cur >> kSumShift) == ks)))
                 atomicMax(&sh.tie_sum, static_cast<int>(ks));
             }
             // The largest-index leaf at the running maximum: a second maximal
@@ -1681,7 +1525,7 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
           const int ne = __popcll(em);
           int take = __popcll(inm);
           if (ne > 0) {
-            nodes = CSM_POW2_BATCH ? 1 << (31 - __clz(ne)) : ne;
+            nodes = ne;  // every expandable entry among the next 64 (profiles/r3y)
             const int rank = __popcll(em & ((1ull << lane) - 1));
             // Entries up to the nodes-th expandable one are taken.
             take = static_cast<int>(__ffsll(static_cast<long long>(
@@ -1701,25 +1545,6 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
             }
             blen = DppMax(len);
             bent = DppSum(len);
-#if CSM_LANE_SORT
-            {
-              // Bitonic sort of (level, rotation, y, x, slot) over the wave;
-              // lane i ends with the i-th smallest key and records its slot.
-              const uint32_t ux = (ent.x & 0xffffu) ^ 0x8000u, uy = (ent.x >> 16) ^ 0x8000u;
-              uint64_t key = took ? (static_cast<uint64_t>(ent.y >> 22) << 38) |
-                                        (static_cast<uint64_t>(uy) << 22) |
-                                        (static_cast<uint64_t>(ux) << 6) | static_cast<uint64_t>(rank)
-                                  : ~0ull;
-              for (int k = 2; k <= 64; k <<= 1) {
-                for (int j = k >> 1; j > 0; j >>= 1) {
-                  const uint64_t o = __shfl_xor(key, j, 64);
-                  const bool keep_min = ((lane & j) == 0) == ((lane & k) == 0);
-                  key = keep_min ? (o < key ? o : key) : (o > key ? o : key);
-                }
-              }
-              if (lane < nodes) sh.lane_node[lane] = static_cast<int>(key & 63u);
-            }
-#endif
             // Per child level: candidates scored and batches (lane l counts
             // level l; one pass per distinct level, usually one).
             const int cl = static_cast<int>(ent.y >> 27) - (hexb ? 2 : 1);
@@ -1758,7 +1583,7 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
       const int done = Uniform(sh.done);
       if (done) break;
       if (nodes > 0) {
-        // Algorithmic bytes: 4 per quad-dword gather, 16 (CSM_HEX8: 8) per hex gather.
+        // Algorithmic bytes: 4 per quad-dword gather, 16 per hex gather.
         const bool hexb = kHex && Uniform(sh.batch_hex);
         if (hexb)
           V4ScoreHex(sh, cells, cnts, raw_end, sm);

@@ -330,7 +330,7 @@ int csm_hybrid_grid_create_batch(csm_context* ctx, int32_t num, const float* res
   const size_t jobs_at = bytes;
   bytes += sizeof(GridJob3) * num;
   csm::StageRing::Slot* slot = nullptr;
-  if ((rc = ctx->f3_grid_stage.Take(bytes, &slot))) return rc;
+  if ((rc = ctx->f3_grid_batch_stage.Take(bytes, &slot))) return rc;
   if ((rc = ctx->f3_grid_batch.Reserve(bytes))) return rc;
   char* hs = slot->buf.as<char>();
   char* dev = ctx->f3_grid_batch.as<char>();
@@ -2250,7 +2250,11 @@ int SingleMatch3(const csm_fast3d* m, const csm_pair3d& pair, const csm_node3d* 
   }();
   if (!coalesce) {
     std::vector<SingleReq3*> one{&r};
-    r.rc = RunSingleBatch3(owner, one);
+    try {
+      r.rc = RunSingleBatch3(owner, one);
+    } catch (...) {  // no exception crosses the C-ABI
+      r.rc = CSM_ENOMEM;
+    }
   } else {
     std::unique_lock<std::mutex> lk(owner->co_mu);
     owner->co3_queue.push_back(&r);
@@ -2271,7 +2275,12 @@ int SingleMatch3(const csm_fast3d* m, const csm_pair3d& pair, const csm_node3d* 
         owner->co3_queue.erase(owner->co3_queue.begin(), owner->co3_queue.begin() + take_n);
         owner->co3_last_batch = static_cast<int>(take_n);
         lk.unlock();
-        const int rc = RunSingleBatch3(owner, take);
+        int rc;  // as in 2D: every request taken is answered, whatever the batch throws
+        try {
+          rc = RunSingleBatch3(owner, take);
+        } catch (...) {
+          rc = CSM_ENOMEM;
+        }
         lk.lock();
         for (SingleReq3* q : take) {
           q->rc = rc;

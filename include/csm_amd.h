@@ -113,6 +113,7 @@ typedef struct csm_timing {
    * more than 4096 leaves tied (CSM_TIE_WALK; counted whether or not timing
    * is enabled). */
   int64_t tied_pairs;
+  /* Named ties_unresolved before round 5 (same slot, same layout). */
   int64_t ties_walked;
   /* Pairs (2D and 3D) whose pick needed the whole lowest-resolution list
    * ordered (CSM_TIE_TOPLIST). 3D: pairs whose best sum was reached by more
@@ -120,7 +121,7 @@ typedef struct csm_timing {
    * by the ordered walk (more than 4096 such leaves). */
   int64_t ties_toplist;
   int64_t tied_pairs_3d;
-  int64_t ties_walked_3d;
+  int64_t ties_walked_3d; /* named ties_unresolved_3d before round 5 */
 } csm_timing;
 void csm_context_enable_timing(csm_context* ctx, int32_t enable);
 void csm_context_get_timing(csm_context* ctx, csm_timing* out);
@@ -218,6 +219,9 @@ typedef struct csm_pair2d {
 #define CSM_TIE_ANCESTORS 1
 #define CSM_TIE_TOPLIST 2
 #define CSM_TIE_WALK 3
+/* Round-4 name of code 3 (before the walk resolved every such pair, it marked
+ * them unresolved); kept so that callers written against it still compile. */
+#define CSM_TIE_UNRESOLVED CSM_TIE_WALK
 
 typedef struct csm_result2d {
   int32_t status;      /* CSM_OK, CSM_NO_MATCH or a negative error */

@@ -176,12 +176,18 @@ int32_t oracle_fast2d_tie_leaves(void* h, int32_t full_submap, const double* ini
 // CPU baseline: pairs (submap index, node index) matched with
 // MatchFullSubmap on `threads` workers pulling pairs FIFO. Returns wall
 // seconds; matched[i] = 1 on success.
-double oracle_fast2d_match_pairs(void* const* submaps, const float* points,
-                                 const int64_t* point_offsets,
-                                 const int32_t* pair_submap,
-                                 const int32_t* pair_node, int64_t num_pairs,
-                                 int32_t threads, float min_score, float* scores,
-                                 double* poses, int32_t* matched, double* task_seconds) {
+// oracle_fast2d_match_pairs_stats: the same, and per pair (when stats is
+// not null) the 16 counters of oracle_fast2d_match_full_submap: lookups
+// (GetValue calls, fast_correlative_scan_matcher_2d.cc:319-330), scans,
+// lowest-resolution candidates, candidates scored per level 0..12 — the
+// reference's work per pair, next to the GPU search's (bench.py work_ratio).
+double oracle_fast2d_match_pairs_stats(void* const* submaps, const float* points,
+                                       const int64_t* point_offsets,
+                                       const int32_t* pair_submap,
+                                       const int32_t* pair_node, int64_t num_pairs,
+                                       int32_t threads, float min_score, float* scores,
+                                       double* poses, int32_t* matched, double* task_seconds,
+                                       int64_t* stats) {
   std::vector<PointCloud> clouds;
   // Clouds are materialised per task (TrajectoryNode::Data holds them
   // already in the reference; conversion is outside the timed region).
@@ -201,7 +207,10 @@ double oracle_fast2d_match_pairs(void* const* submaps, const float* points,
         Rigid2d pose;
         float score = 0.f;
         const auto ts = std::chrono::steady_clock::now();
-        const bool ok = m->MatchFullSubmap(clouds[pair_node[i]], min_score, &score, &pose);
+        MatchStats2D st;
+        const bool ok = m->MatchFullSubmap(clouds[pair_node[i]], min_score, &score, &pose,
+                                           stats ? &st : nullptr);
+        if (stats) FillStats(st, stats + 16 * i);
         if (task_seconds)  // per-task time, for the baseline's confidence interval
           task_seconds[i] =
               std::chrono::duration<double>(std::chrono::steady_clock::now() - ts).count();
@@ -214,6 +223,17 @@ double oracle_fast2d_match_pairs(void* const* submaps, const float* points,
     });
   for (auto& th : pool) th.join();
   return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
+double oracle_fast2d_match_pairs(void* const* submaps, const float* points,
+                                 const int64_t* point_offsets,
+                                 const int32_t* pair_submap,
+                                 const int32_t* pair_node, int64_t num_pairs,
+                                 int32_t threads, float min_score, float* scores,
+                                 double* poses, int32_t* matched, double* task_seconds) {
+  return oracle_fast2d_match_pairs_stats(submaps, points, point_offsets, pair_submap, pair_node,
+                                         num_pairs, threads, min_score, scores, poses, matched,
+                                         task_seconds, nullptr);
 }
 
 // RealTimeCorrelativeScanMatcher2D::Match over a probability grid.

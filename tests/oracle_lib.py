@@ -30,6 +30,8 @@ class Oracle:
             "oracle_fast2d_tie_leaves": (I32, [VP, I32, P(D), P(F), I32, F, I32, P(I32), P(I32)]),
             "oracle_fast2d_match_pairs": (D, [P(VP), P(F), P(I64), P(I32), P(I32), I64, I32, F,
                                               P(F), P(D), P(I32), P(D)]),
+            "oracle_fast2d_match_pairs_stats": (D, [P(VP), P(F), P(I64), P(I32), P(I32), I64, I32,
+                                                    F, P(F), P(D), P(I32), P(D), P(I64)]),
             "oracle_rt2d_match": (D, [D, D, D, I32, I32, P(C.c_uint16), D, D, D, D, P(D), P(F),
                                       I32, P(D), P(I64)]),
             "oracle_rt2d_time": (D, [D, D, D, I32, I32, P(C.c_uint16), D, D, D, D, P(D), P(F),

@@ -12,10 +12,16 @@ csm_comm_gather (C3 and C5), the max-over-ranks timing and the strong-scaling
 accounting. The gathered records must equal a single-rank run's, in
 submission order (ConstraintBuilder2D::WhenDone, constraint_builder_2d.cc:
 279-300).
+
+The two ranks are started the way a bare `bench.py --gpus 2` starts them
+(no launcher: bench.py runs torch.distributed.run itself), so a scaling
+command can never silently measure one rank; the line must report the
+communicator's rank count (comm_ranks) and a parity sample of the timed
+run, gathered from whichever rank claimed each sampled pair and compared
+with the oracle on rank 0 (VERDICT r5 Next 1).
 """
 import json
 import os
-import socket
 import subprocess
 import sys
 
@@ -29,15 +35,7 @@ pytestmark = pytest.mark.gpu
 STANDIN = os.path.join(ROOT, "tests", "comm_standin", "librccl_standin.so")
 SMALL = ["--workload", "c3", "--c3-nodes", "48", "--c3-submaps", "12", "--c3-slice", "4",
          "--steps", "3", "--warmup", "1", "--no-rt", "--no-cpu", "--nodes3d", "40",
-         "--submaps3d", "6", "--steps3d", "1"]
-
-
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
+         "--submaps3d", "6", "--steps3d", "1", "--parity-pairs", "24"]
 
 
 def _json_line(out):
@@ -54,16 +52,24 @@ def test_two_ranks_rccl_branch_equal_single_rank(tmp_path):
     j1 = _json_line(r1.stdout)
     two = tmp_path / "two.npz"
     env2 = dict(env, CSM_RCCL_LIB=STANDIN)
-    port = _free_port()
-    r2 = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
-                         "--nproc-per-node", "2", "--master-addr", "127.0.0.1", "--master-port",
-                         str(port), os.path.join(ROOT, "bench.py"), "--gpus", "2", *SMALL,
+    for var in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env2.pop(var, None)
+    r2 = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", *SMALL,
                          "--dist-backend", "gloo", "--comm-backend", "rccl",
                          "--dump-records", str(two)], capture_output=True, text=True,
                         timeout=300, cwd=ROOT, env=env2)
     assert r2.returncode == 0, r2.stderr[-3000:]
+    assert "starting 2 ranks" in r2.stderr
     j2 = _json_line(r2.stdout)
     assert j2["config"]["gather"] == "csm_comm_rccl" and j2["n_gpus"] == 2
+    assert j1["comm_ranks"] == 1 and j2["comm_ranks"] == 2
+    for j in (j1, j2):  # the timed run's sampled pairs, against the oracle
+        p = j["parity_sample"]
+        assert p["pairs"] == p["compared"] == 24, p
+        assert p["mismatched_decision"] == p["mismatched_score"] == p["mismatched_pose"] == 0, p
+        assert p["gpu_errors"] == 0
+        assert j["work_ratio"]["pairs"] == 24 and j["work_ratio"]["oracle"]["lookups_per_pair"] > 0
+    assert j2["parity_sample"]["ranks"] == 2
     a, b = np.load(one), np.load(two)
     for key in ("c3", "c5"):
         assert a[key].shape == b[key].shape and len(a[key]) > 0, key

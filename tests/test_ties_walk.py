@@ -155,6 +155,39 @@ def test_plateau_ties_past_the_record(csm, oracle, kernel, seed):
                                              (res[0]["x"], res[0]["y"], res[0]["theta"]))
 
 
+@pytest.mark.parametrize("depth", [1, 2, 4])
+def test_zero_sum_leaves_without_incumbent(csm, oracle, kernel, depth):
+    """min_score 0 lets a leaf of sum 0 pass (ToScore(0) = 0.1 > 0): a cloud
+    lying wholly in unknown cells next to a known corner, searched in small
+    local windows whose leaf passes often hold a single leaf. The first such
+    leaf must not count as a tie with the (absent) incumbent, or nodes bounded
+    by 0 stop being expanded and the reference's pick among the zero-sum
+    leaves is lost."""
+    cells = np.zeros((60, 60), np.uint16)
+    cells[:12, :12] = 20000  # known cells far from the clouds
+    limits = (1.0, 30.0, 30.0)
+    grid = csm.ProbabilityGrid(*limits, cells)
+    rng = np.random.default_rng(17 + depth)
+    clouds = [np.array([[0.3, -0.2, 0.0]], np.float32),
+              rng.uniform(-2, 2, (5, 3)).astype(np.float32)]
+    specs, refs = [], []
+    for lin in (1.0, 2.0, 3.0):
+        for ang in (0.0, math.radians(2.0)):
+            m = csm.FastCorrelativeScanMatcher2D(grid, csm.FastCorrelativeScanMatcherOptions2D(
+                lin, ang, depth))
+            om = oracle.fast2d(limits, cells, lin, ang, depth)
+            for i, c in enumerate(clouds):
+                init = (-10.0 + 0.3 * i, -12.0, 0.1)
+                specs.append((m, i, init))
+                refs.append(om.match(init, c, 0.0))
+    mats = [s[0] for s in specs]
+    res, _ = _run(csm, mats, clouds, [(k, s[1], False, 0.0, s[2]) for k, s in enumerate(specs)])
+    assert_search_ok(csm, res["status"])
+    for k, ref in enumerate(refs):
+        assert ref[0], ref  # every leaf sums to 0, and 0 passes min_score 0
+        _assert_exact(res[k], ref)
+
+
 # ---------------------------------------------------------------------- 3D --
 
 def _options3d(csm, depth, full_depth, min_low, lin_xy, lin_z, ang=0.3):
