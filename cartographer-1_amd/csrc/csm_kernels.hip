@@ -1021,6 +1021,21 @@ __device__ __forceinline__ uint32_t ClusterMask(int sl) {
 // (DESIGN.md §5).
 #define CSM_XFAST 1
 #endif
+#ifndef CSM_ORIGIN_ALIGN
+// The node lattice of a rotation starts at its ShrinkToFit corner (b0, b2)
+// rounded down to a multiple of this power of two (>= the largest cluster,
+// 2^kMaxClusterShift), and nodes wholly below the corner are dropped, so the
+// leaves are still exactly the reference's [b0, b1] x [b2, b3]. Every node's
+// offset is then a multiple of 8 at levels >= 3, and a cluster entry's cell
+// a multiple of its cluster size, so the plane entries a level's cluster
+// lists can address lie in one residue class: 1/16 of the level-2..4 planes
+// and 1/64 of the level-6 hex plane, the same class for every pair and
+// rotation, instead of all of them across a chunk's items. The planes'
+// touched footprint shrinks to what one XCD's L2 holds. 1: the reference's
+// corner (no alignment).
+#define CSM_ORIGIN_ALIGN 8
+#endif
+static_assert((CSM_ORIGIN_ALIGN & (CSM_ORIGIN_ALIGN - 1)) == 0, "CSM_ORIGIN_ALIGN: a power of two");
 #ifndef CSM_TIE_PRUNE
 // 1: the main search stops expanding nodes bounded by a sum its witness keys
 // already show tied (FindsConstraints-like inputs: every leaf ties).
@@ -1264,7 +1279,8 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
       const int b0 = max(-pd.num_linear, lo_x), b1 = min(pd.num_linear, hi_x);
       const int b2 = max(-pd.num_linear, lo_y), b3 = min(pd.num_linear, hi_y);
       sh.bounds[r][0] = b0; sh.bounds[r][1] = b1; sh.bounds[r][2] = b2; sh.bounds[r][3] = b3;
-      const int tnx = (b1 - b0 + step) / step, tny = (b3 - b2 + step) / step;
+      const int a0 = b0 & -CSM_ORIGIN_ALIGN, a2 = b2 & -CSM_ORIGIN_ALIGN;  // lattice origin
+      const int tnx = (b1 - a0 + step) / step, tny = (b3 - a2 + step) / step;
       sh.vny[r] = (tny + 1) >> 1;
       sh.root_prefix[r + 1] = ((tnx + 1) >> 1) * sh.vny[r];
     }
@@ -1321,7 +1337,10 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
             r = sh.node_rot[nd];
             xo = sh.node_xo[nd] + (c >> (lk >> 1)) * h;
             yo = sh.node_yo[nd] + (c & ((1 << (lk >> 1)) - 1)) * h;
-            exists = xo <= sh.bounds[r][1] && yo <= sh.bounds[r][3];
+            // Inside the window: not past (b1, b3), and not wholly below
+            // (b0, b2), which only the aligned origin's nodes can be.
+            exists = xo <= sh.bounds[r][1] && yo <= sh.bounds[r][3] &&
+                     xo + h > sh.bounds[r][0] && yo + h > sh.bounds[r][2];
           }
           const uint64_t cur = sh.best;
           const uint32_t cur_sum = static_cast<uint32_t>(cur >> kSumShift);
@@ -1465,8 +1484,8 @@ fast2d_search_v4(const SubmapDesc* __restrict__ submaps,
               xi = lv % vnx;
               yi = lv / vnx;
             }
-            const int xo = sh.bounds[r][0] + xi * 2 * step;
-            const int yo = sh.bounds[r][2] + yi * 2 * step;
+            const int xo = (sh.bounds[r][0] & -CSM_ORIGIN_ALIGN) + xi * 2 * step;
+            const int yo = (sh.bounds[r][2] & -CSM_ORIGIN_ALIGN) + yi * 2 * step;
             sh.stack[k] = make_uint2((static_cast<uint32_t>(xo) & 0xffff) | (static_cast<uint32_t>(yo) << 16),
                                      0x3fffffu | (static_cast<uint32_t>(r) << 22) |
                                          (static_cast<uint32_t>(top_level + 1) << 27));
