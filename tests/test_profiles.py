@@ -1,0 +1,36 @@
+"""Every committed profile summary is rebuilt from the committed per-dispatch
+reductions alone (tools/profiles.py, manifests under profiles/<round>/) and
+must equal the committed file; and the summaries bench.py reads name their
+committed inputs, not gpurun_out/ scratch (VERDICT r5 Next 6). CPU only."""
+import glob
+import json
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+import bench  # noqa: E402
+import profiles  # noqa: E402
+
+MANIFESTS = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "manifest.json")))
+
+
+@pytest.mark.parametrize("manifest", MANIFESTS, ids=[os.path.basename(os.path.dirname(m)) for m in MANIFESTS])
+def test_summary_rebuilds_from_committed_inputs(manifest):
+    assert profiles.check(manifest) == []
+
+
+def test_bench_summaries_come_from_manifests():
+    files = list(bench.TRAFFIC_FILES.values()) + [bench.GATHER_FILE, bench.TRAFFIC3D_FILE]
+    built = set()
+    for m in MANIFESTS:
+        base = os.path.relpath(os.path.dirname(m), ROOT)
+        built |= {os.path.join(base, name) for name in json.load(open(m))["outputs"]}
+    for rel in files:
+        assert rel in built, f"{rel} has no manifest"
+        src = json.load(open(os.path.join(ROOT, rel)))["source"]
+        assert "gpurun_out" not in src, (rel, src)
