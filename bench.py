@@ -482,9 +482,9 @@ def make_comm_checked(csm, ctx, args, rank, world_size, dist, coll_dev):
               + (f": {err}" if err else ""), file=sys.stderr, flush=True)
         sys.exit(4)
     ranks = int(comm.allreduce(np.ones(1, np.int64))[0])
-    if comm.size() != world_size or comm.rank() != rank or ranks != world_size:
-        print(f"bench: rank {rank}: csm_comm spans {ranks} ranks (size {comm.size()}, rank "
-              f"{comm.rank()}), expected {world_size}", file=sys.stderr, flush=True)
+    if comm.size != world_size or comm.rank != rank or ranks != world_size:
+        print(f"bench: rank {rank}: csm_comm spans {ranks} ranks (size {comm.size}, rank "
+              f"{comm.rank}), expected {world_size}", file=sys.stderr, flush=True)
         sys.exit(4)
     return comm, f"csm_comm_{backend}", ranks
 
