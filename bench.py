@@ -36,7 +36,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 # Version tag of the search kernel the committed PMC traffic figures belong to
 # (a traffic file recorded on another kernel version is not reported).
-KERNEL_TAG = "v5-flat"
+KERNEL_TAG = "v5-align8"
 # fast3d_search version whose PMC passes profiles/r5bd/traffic_c5.json holds.
 KERNEL3D_TAG = "f3-octet-tieprune"
 TRAFFIC3D_FILE = os.path.join("profiles", "r5bd", "traffic_c5.json")
@@ -361,8 +361,8 @@ def roofline_fields(tm, achieved, peak, traffic, kernel_ms_avg, bytes_per_launch
             "candidate_equivalent_bytes_per_launch": candidate_bytes}
 
 
-TRAFFIC_FILES = {"c2": os.path.join("profiles", "r5bb", "traffic_c2.json"),
-                 "c3": os.path.join("profiles", "r5bb", "traffic_c3.json")}
+TRAFFIC_FILES = {"c2": os.path.join("profiles", "r6f", "traffic_c2.json"),
+                 "c3": os.path.join("profiles", "r6f", "traffic_c3.json")}
 
 
 def traffic_fields(traffic, kernel_ms_avg, peak):
@@ -385,7 +385,7 @@ def sum_timing(csm, tms):
     return out
 
 
-GATHER_FILE = os.path.join("profiles", "r5bb", "gather_c3.json")
+GATHER_FILE = os.path.join("profiles", "r6f", "gather_c3.json")
 
 
 def gather_roofline(kernel_ms):
