@@ -65,7 +65,7 @@ hipError_t LaunchRt3dScore4(int num_blocks, hipStream_t st, const float* pad, co
                             int num_rot, double wt, double wr, unsigned long long* best,
                             float* scores, int scores_pitch);
 // rt3d_score5: v4's rotation blocks, one wave per (x, y) column of the
-// translation lattice (nl = 2L + 1 in {3, 5, 7} z steps), over the brick
+// translation lattice (nl = 2L + 1 in {3, 5, ..., 15} z steps), over the brick
 // padded by P and stored z fastest (LaunchPadProbBrickZ). col_t0[c] = the
 // scaled translation of step 0 of column c, col_thr[c] = per-axis rounding
 // thresholds of the column test.

@@ -610,9 +610,10 @@ int RunRt3d(csm_context* ctx, const csm_rt_options* o, const csm_hybrid_grid* gr
                            st));
     CSM_HIP(hipMemcpyAsync(didx, bidx.data(), sizeof(int32_t) * bidx.size(), hipMemcpyHostToDevice,
                            st));
-    // v5 (column gathers) for 3-, 5- and 7-step z columns.
+    // v5 (column gathers) for z columns of 3 to 15 steps (one wave per
+    // column, nl waves per workgroup; wider windows run v4).
     const int nl = static_cast<int>(w.nl);
-    const bool v5 = !std::getenv("CSM_RT3D_V4") && (nl == 3 || nl == 5 || nl == 7);
+    const bool v5 = !std::getenv("CSM_RT3D_V4") && nl >= 3 && nl <= 15 && (nl & 1);
     if (v5) {
       csm_hybrid_grid* g = const_cast<csm_hybrid_grid*>(grid);
       if (g->prob_col_pad != P) {

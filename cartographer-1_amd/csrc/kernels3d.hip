@@ -7,6 +7,7 @@
 
 #include <cstdint>
 #include <cstdlib>
+#include <type_traits>
 
 #include "csm_device3d.h"
 #include "csm_launch3d.h"
@@ -852,16 +853,17 @@ rt3d_score5(const float* __restrict__ col, int pnx, int pny, int pnz, float bx, 
                             fmaxf(__fsub_rn(fabsf(__fsub_rn(yz, rz)), th.z), __fsub_rn(a.w, 0.5f)));
       float v[NL];
       if (m < 0.f) {
+        // The column's NL cells: ceil(NL / 4) 16-byte loads (one or two up to
+        // 7 steps, three for 9 and 11, four for 13 and 15); the cells read
+        // past the column's last step are discarded.
         const float off = fmaf(rz, sz, fmaf(ry, sy, fmaf(rx, sx, base)));  // exact (< 2^24)
         const int o = static_cast<int>(off);
-        const auto lo4 = __builtin_amdgcn_raw_buffer_load_b128(rsrc, o, 0, 0);
+        constexpr int kLoads = (NL + 3) / 4;
+        decltype(__builtin_amdgcn_raw_buffer_load_b128(rsrc, 0, 0, 0)) q4[kLoads];
 #pragma unroll
-        for (int k = 0; k < NL && k < 4; ++k) v[k] = __uint_as_float(lo4[k]);
-        if constexpr (NL > 4) {
-          const auto hi4 = __builtin_amdgcn_raw_buffer_load_b128(rsrc, o + 16, 0, 0);
+        for (int j = 0; j < kLoads; ++j) q4[j] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, o + 16 * j, 0, 0);
 #pragma unroll
-          for (int k = 4; k < NL; ++k) v[k] = __uint_as_float(hi4[k - 4]);
-        }
+        for (int k = 0; k < NL; ++k) v[k] = __uint_as_float(q4[k >> 2][k & 3]);
       } else {  // rare: v3's per-step path
         const float* p = points + 3 * static_cast<int64_t>(tb + i);
         float ax, ay, az;
@@ -1512,9 +1514,35 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
           a6 = __builtin_amdgcn_udot4(hi, 0x00010000u, a6, false);
           a7 = __builtin_amdgcn_udot4(hi, 0x01000000u, a7, false);
         };
-        // All of a lane's points (up to kRound per round) in flight at once;
-        // past-the-end slots load from the out-of-range offset and add 0.
-        constexpr int kRound = 16;
+        // A lane's points in flight at once, 16 per round. A load past the
+        // cloud still costs texture-path cycles (it reads the out-of-range
+        // offset and adds 0), so the last round is cut to the 4, 8, 12 or 16
+        // loads that cover the cloud's nu = ceil(n / 16) points per lane
+        // (wave-uniform: every node of the item has the same cloud): a
+        // 186-point cloud issues 12 loads per lane, not 16.
+        const int nu = (n + kLanes - 1) / kLanes;
+        auto rounds = [&](auto&& ld) {
+          int u0 = 0;
+          auto issue = [&](auto kk) {
+            constexpr int K = decltype(kk)::value;
+            uint64_t v[K];
+#pragma unroll
+            for (int u = 0; u < K; ++u) v[u] = ld(hl + (u0 + u) * kLanes);
+#pragma unroll
+            for (int u = 0; u < K; ++u) accumulate(v[u]);
+            u0 += K;
+          };
+          while (nu - u0 >= 16) issue(std::integral_constant<int, 16>{});
+          const int left = nu - u0;
+          if (left > 12)
+            issue(std::integral_constant<int, 16>{});
+          else if (left > 8)
+            issue(std::integral_constant<int, 12>{});
+          else if (left > 4)
+            issue(std::integral_constant<int, 8>{});
+          else if (left > 0)
+            issue(std::integral_constant<int, 4>{});
+        };
         if (packed) {
           // c - o of a point as bitfields; at this level, with e <= E,
           // a = ((c - o) >> e) + Kx etc. (the window and box origin folded in).
@@ -1546,13 +1574,7 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
               const uint32_t hi = __builtin_amdgcn_raw_buffer_load_b32(rs, off + 4, 0, 0);
               return (static_cast<uint64_t>(hi) << 32) | lo;
             };
-            for (int i0 = hl; i0 < n; i0 += kRound * kLanes) {
-              uint64_t v[kRound];
-#pragma unroll
-              for (int u = 0; u < kRound; ++u) v[u] = load_in(i0 + u * kLanes);
-#pragma unroll
-              for (int u = 0; u < kRound; ++u) accumulate(v[u]);
-            }
+            rounds(load_in);
           } else {
             auto load_chk = [&](int i) -> uint64_t {
               const bool live = i < n;
@@ -1568,22 +1590,10 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
               const uint32_t hi = __builtin_amdgcn_raw_buffer_load_b32(rs, off + 4, 0, 0);
               return (static_cast<uint64_t>(hi) << 32) | lo;
             };
-            for (int i0 = hl; i0 < n; i0 += kRound * kLanes) {
-              uint64_t v[kRound];
-#pragma unroll
-              for (int u = 0; u < kRound; ++u) v[u] = load_chk(i0 + u * kLanes);
-#pragma unroll
-              for (int u = 0; u < kRound; ++u) accumulate(v[u]);
-            }
+            rounds(load_chk);
           }
         } else {
-          for (int i0 = hl; i0 < n; i0 += kRound * kLanes) {
-            uint64_t v[kRound];
-#pragma unroll
-            for (int u = 0; u < kRound; ++u) v[u] = load(i0 + u * kLanes);
-#pragma unroll
-            for (int u = 0; u < kRound; ++u) accumulate(v[u]);
-          }
+          rounds(load);
         }
         acc[0] = a0;
         acc[1] = a1;
@@ -2475,6 +2485,10 @@ hipError_t LaunchRt3dScore5(int nl, int num_blocks, hipStream_t st, const float*
     case 3: CSM_RT5(3); break;
     case 5: CSM_RT5(5); break;
     case 7: CSM_RT5(7); break;
+    case 9: CSM_RT5(9); break;
+    case 11: CSM_RT5(11); break;
+    case 13: CSM_RT5(13); break;
+    case 15: CSM_RT5(15); break;
     default: return hipErrorInvalidValue;
   }
 #undef CSM_RT5

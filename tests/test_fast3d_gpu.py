@@ -284,18 +284,21 @@ def test_rt3d_column_kernel_tilted_initial(csm, oracle, window, rt3d_kernel):
         assert pose == ref_pose
 
 
-def test_rt3d_nine_step_window(csm, oracle, rt3d_kernel):
-    """+-0.4 m at 0.1 m: 9-step z columns, which v5 does not take (the host
-    selects v4 unforced), under a tilted and a yawed initial pose."""
+@pytest.mark.parametrize("steps", [9, 11, 13])
+def test_rt3d_wide_z_windows(csm, oracle, rt3d_kernel, steps):
+    """+-0.4 / 0.5 / 0.6 m at 0.1 m: 9-, 11- and 13-step z columns, which v5
+    takes with three or four 16-byte loads per column (rt3d_score5<9..13>),
+    under a tilted and a yawed initial pose (real_time_correlative_scan_
+    matcher_3d.cc:55-113 generates the same lattice)."""
     rng = np.random.default_rng(19)
     cloud = rng.uniform(-4, 4, (300, 3)).astype(np.float32) * np.float32([1, 1, 0.4])
     og = oracle.hybrid_grid(0.1)
     og.insert((0, 0, 0), cloud, 0.7, 0.4, 5)
-    opts = (0.4, math.radians(1.0), 0.1, 0.1)
+    opts = (round((steps // 2) * 0.1, 10), math.radians(1.0), 0.1, 0.1)
     g = gpu_grid(csm, og)
     m = csm.RealTimeCorrelativeScanMatcher3D(csm.RealTimeCorrelativeScanMatcherOptions(*opts))
     nt, _ = m.window(cloud, 0.1)
-    assert nt == 9 ** 3
+    assert nt == steps ** 3
     roll = math.radians(6.0)
     for initial in [((0.05, -0.03, 0.02), (math.cos(roll / 2), math.sin(roll / 2), 0.0, 0.0)),
                     ((0.0, 0.0, 0.0), quat_z(0.1))]:

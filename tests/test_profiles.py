@@ -34,3 +34,18 @@ def test_bench_summaries_come_from_manifests():
         assert rel in built, f"{rel} has no manifest"
         src = json.load(open(os.path.join(ROOT, rel)))["source"]
         assert "gpurun_out" not in src, (rel, src)
+
+
+def test_cited_profile_paths_exist():
+    """Every profiles/ path the documents cite is committed (ADVICE r5:
+    evidence trails must not dangle)."""
+    import re
+    missing = []
+    for doc in ("DESIGN.md", "EXPERIMENTS.md", "INTEGRATION.md", "README.md"):
+        path = os.path.join(ROOT, doc)
+        if not os.path.exists(path):
+            continue
+        for cite in set(re.findall(r"profiles/r[0-9a-z]+(?:/[A-Za-z0-9_./-]*[A-Za-z0-9_])?", open(path).read())):
+            if not os.path.exists(os.path.join(ROOT, cite)):
+                missing.append((doc, cite))
+    assert not missing, missing
