@@ -1004,7 +1004,25 @@ def fast3d_bench(csm, ctx, args, rank=0, world_size=1, dist=None, coll_dev=None,
            "kernel_ms_per_step": tm.fast3d_kernel_ms / reps, "lookups_per_step": tm.fast3d_lookups / reps,
            "algorithmic_GBps": tm.fast3d_lookups / (tm.fast3d_kernel_ms * 1e-3) / 1e9
            if tm.fast3d_kernel_ms else 0.0, "setup_s": gen}
-    if rank != 0 or world_size != 1:
+    if world_size > 1:
+        # Parity at N > 1: every rank checks a uniform sample of its own share
+        # (its submaps x every node) of the last timed step against the
+        # oracle on its host, and the counts are summed over the ranks.
+        total_k = args.parity_pairs if args.parity_pairs > 0 else 512
+        if args.parity_pairs != 0:
+            k = max(1, -(-total_k // world_size))
+            _, _, sampled = oracle3d_runner(w, o, args.cpu_threads or host_cpu()["usable_cpus"])(k)
+            mine = parity_3d(res3, sampled, w.num_nodes)
+            summed = {key: int(cdist.sum_over_ranks(mine[key], dist, coll_dev))
+                      for key in ("pairs", "compared", "matched_oracle", "mismatched_decision",
+                                  "mismatched_score", "mismatched_pose", "gpu_errors")}
+            summed["ranks"] = world_size
+            summed["what"] = ("each rank's uniform sample of its own share of the last timed step, "
+                              "its GPU results vs the oracle's on that rank's host; counts summed")
+            out["parity_sample"] = summed
+            out["parity_failures"] = parity_failures(summed)
+        return out
+    if rank != 0:
         return out
     # CeresScanMatcher3D refinement of the last step's accepted matches
     # (constraint_builder_3d.cc:264-275), one device batch.
@@ -1023,53 +1041,9 @@ def fast3d_bench(csm, ctx, args, rank=0, world_size=1, dist=None, coll_dev=None,
     if args.c5_dropin_calls > 0:
         out["dropin"] = dropin_3d(csm, w, mats, sub, nod, rot, res3, args.c5_dropin_calls)
     if not args.no_cpu:
-        sys.path.insert(0, os.path.join(ROOT, "tests"))
-        import ctypes as C
-
-        import oracle_lib
-        orc = oracle_lib.Oracle()
-        opt = (o.branch_and_bound_depth, o.full_resolution_depth, o.min_rotational_score,
-               o.min_low_resolution_score, o.linear_xy_search_window,
-               o.linear_z_search_window, o.angular_search_window)
-        keep = []
-        handles = []
-        for s in range(w.num_submaps):
-            oh, ol = orc.hybrid_grid(w.high_resolution), orc.hybrid_grid(w.low_resolution)
-            oh.set_values(*w.high_cells[s])
-            ol.set_values(*w.low_cells[s])
-            om = orc.fast3d(oh, ol, w.submap_hist[s], opt)
-            keep.append((oh, ol, om))
-            handles.append(om.h)
-        hoff = np.zeros(w.num_nodes + 1, np.int64)
-        hoff[1:] = np.cumsum([len(x) for x in w.high])
-        loff = np.zeros(w.num_nodes + 1, np.int64)
-        loff[1:] = np.cumsum([len(x) for x in w.low])
-        high = np.ascontiguousarray(np.concatenate(w.high), np.float32)
-        low = np.ascontiguousarray(np.concatenate(w.low), np.float32)
-        hists = np.ascontiguousarray(np.stack(w.node_hist), np.float32)
-        nq = np.ascontiguousarray([w.node_rotation(i) for i in range(w.num_nodes)], np.float64)
         cpu = host_cpu()
         threads = args.cpu_threads or cpu["usable_cpus"]
-        rng = np.random.RandomState(777)
-        P = C.POINTER
-        hv = (C.c_void_p * len(handles))(*handles)
-
-        def run(k):
-            ps = rng.randint(0, w.num_submaps, k).astype(np.int32)
-            pn = rng.randint(0, w.num_nodes, k).astype(np.int32)
-            matched = np.zeros(k, np.int32)
-            results = np.zeros((k, 14))
-            task = np.zeros(k)
-            wall = orc.lib.oracle_fast3d_match_pairs(
-                hv, high.ctypes.data_as(P(C.c_float)), hoff.ctypes.data_as(P(C.c_int64)),
-                low.ctypes.data_as(P(C.c_float)), loff.ctypes.data_as(P(C.c_int64)),
-                hists.ctypes.data_as(P(C.c_float)), hists.shape[1],
-                nq.ctypes.data_as(P(C.c_double)), ps.ctypes.data_as(P(C.c_int32)),
-                pn.ctypes.data_as(P(C.c_int32)), k, threads, 0.6,
-                matched.ctypes.data_as(P(C.c_int32)), results.ctypes.data_as(P(C.c_double)),
-                task.ctypes.data_as(P(C.c_double)))
-            return wall, task, (ps, pn, results)
-
+        run = oracle3d_runner(w, o, threads)
         probe, _, _ = run(threads)
         k = min(20000, max(threads, int(threads * 10.0 / max(probe, 1e-3))))
         sec, task, sampled = run(k)
@@ -1082,6 +1056,58 @@ def fast3d_bench(csm, ctx, args, rank=0, world_size=1, dist=None, coll_dev=None,
         out["parity_sample"] = parity_3d(res3, sampled, w.num_nodes)
         out["parity_failures"] = parity_failures(out["parity_sample"])
     return out
+
+
+def oracle3d_runner(w, o, threads):
+    """run(k) -> (wall s, per-task s, (submaps, nodes, results)): the oracle's
+    MatchFullSubmap on k uniformly drawn (submap, node) pairs of world `w`
+    (this rank's submaps x every node), `threads` tasks at a time."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import ctypes as C
+
+    import oracle_lib
+    orc = oracle_lib.Oracle()
+    opt = (o.branch_and_bound_depth, o.full_resolution_depth, o.min_rotational_score,
+           o.min_low_resolution_score, o.linear_xy_search_window,
+           o.linear_z_search_window, o.angular_search_window)
+    keep = []
+    handles = []
+    for s in range(w.num_submaps):
+        oh, ol = orc.hybrid_grid(w.high_resolution), orc.hybrid_grid(w.low_resolution)
+        oh.set_values(*w.high_cells[s])
+        ol.set_values(*w.low_cells[s])
+        om = orc.fast3d(oh, ol, w.submap_hist[s], opt)
+        keep.append((oh, ol, om))
+        handles.append(om.h)
+    hoff = np.zeros(w.num_nodes + 1, np.int64)
+    hoff[1:] = np.cumsum([len(x) for x in w.high])
+    loff = np.zeros(w.num_nodes + 1, np.int64)
+    loff[1:] = np.cumsum([len(x) for x in w.low])
+    high = np.ascontiguousarray(np.concatenate(w.high), np.float32)
+    low = np.ascontiguousarray(np.concatenate(w.low), np.float32)
+    hists = np.ascontiguousarray(np.stack(w.node_hist), np.float32)
+    nq = np.ascontiguousarray([w.node_rotation(i) for i in range(w.num_nodes)], np.float64)
+    rng = np.random.RandomState(777)
+    P = C.POINTER
+    hv = (C.c_void_p * len(handles))(*handles)
+
+    def run(k):
+        ps = rng.randint(0, w.num_submaps, k).astype(np.int32)
+        pn = rng.randint(0, w.num_nodes, k).astype(np.int32)
+        matched = np.zeros(k, np.int32)
+        results = np.zeros((k, 14))
+        task = np.zeros(k)
+        wall = orc.lib.oracle_fast3d_match_pairs(
+            hv, high.ctypes.data_as(P(C.c_float)), hoff.ctypes.data_as(P(C.c_int64)),
+            low.ctypes.data_as(P(C.c_float)), loff.ctypes.data_as(P(C.c_int64)),
+            hists.ctypes.data_as(P(C.c_float)), hists.shape[1],
+            nq.ctypes.data_as(P(C.c_double)), ps.ctypes.data_as(P(C.c_int32)),
+            pn.ctypes.data_as(P(C.c_int32)), k, threads, 0.6,
+            matched.ctypes.data_as(P(C.c_int32)), results.ctypes.data_as(P(C.c_double)),
+            task.ctypes.data_as(P(C.c_double)))
+        _ = len(keep)  # the oracle's grids and matchers live as long as run()
+        return wall, task, (ps, pn, results)
+    return run
 
 
 def cpu_baseline(world, my_submaps, args):

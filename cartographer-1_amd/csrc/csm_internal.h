@@ -245,6 +245,8 @@ struct csm_context {
   std::vector<void*> co3_queue;
   int co3_leaders = 0;
   int co3_last_batch = 1;
+  int co3_in_flight = 0;  // single 3D calls between queueing and their return
+  int co3_callers = 0;    // recent high-water of co3_in_flight (one less per batch)
   csm_timing call_t{};                // finished single calls' timing (call_mu)
   csm_scan_set single;                // the cloud of the current single 2D call
   csm::PinnedBuf single_stage;
@@ -266,6 +268,10 @@ struct csm_context {
       f3_low_points, f3_best, f3_status, f3_counter, f3_items, f3_scores, f3_spill, f3_best_hi,
       f3_ties, f3_tie_count, f3_tie_yaws, f3_sq_jobs, f3_sq_queries, f3_sq_sums, f3_walk_buf;
   csm::PinnedBuf f3_host_yaws, f3_host_points;
+  // Pinned staging of a 3D batch's small uploads and readbacks (one copy
+  // each way per phase), and the device buffer the readbacks are packed in.
+  csm::PinnedBuf f3_up, f3_rb;
+  csm::DevBuf f3_pack;
   // Side stream for the 3D batch's cloud upload (overlaps the rotational
   // scores on `stream`); the search waits on f3_points_ready.
   hipStream_t f3_copy_stream = nullptr;

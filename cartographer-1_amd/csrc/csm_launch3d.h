@@ -101,6 +101,17 @@ hipError_t LaunchFast3dWalk(int num_jobs, hipStream_t st, const Submap3Desc* sub
                             const Pair3Desc* pairs, const Yaw3Desc* yaws, const float* points,
                             const float* low_points, const Walk3Job* jobs, const int4* top,
                             int4* out);
+// Up to kSegs3 device segments (4-byte multiples) in one launch: copied
+// back to back into `out` (PackSegments: one readback instead of one copy
+// per buffer) or zeroed (ZeroSegments, out null: one launch instead of one
+// memset per buffer).
+constexpr int kSegs3 = 8;
+struct Segs3 {
+  void* ptr[kSegs3];
+  int64_t bytes[kSegs3];
+  int n;
+};
+hipError_t LaunchSegments(const Segs3& segs, void* out, hipStream_t st);
 hipError_t LaunchFast3dFinalize(int num_pairs, hipStream_t st, const Submap3Desc* submaps,
                                 const Pair3Desc* pairs, const Yaw3Desc* yaws,
                                 const float* low_points, const unsigned long long* best,

@@ -1903,19 +1903,26 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
       unsigned* dcursor = reinterpret_cast<unsigned*>(drange + rp.size());
       RotPair3Host* drp = ctx->f3_items.as<RotPair3Host>();
       float* dh = reinterpret_cast<float*>(drp + rp.size());
-      CSM_HIP(hipMemcpyAsync(drp, rp.data(), sizeof(RotPair3Host) * rp.size(),
-                             hipMemcpyHostToDevice, st));
+      // Pinned staging both ways, one copy each: the pair records and
+      // histograms up (contiguous on the device), the ranges and the cursor
+      // (adjacent) back. Pageable copies cost ~25 us each, which dominated
+      // a single call's latency (profiles/r6h/).
+      const size_t up_bytes = sizeof(RotPair3Host) * rp.size() + sizeof(float) * hists.size();
+      const size_t rb_bytes = sizeof(int2) * rp.size() + sizeof(unsigned);
+      if ((rc = ctx->f3_up.Reserve(up_bytes)) || (rc = ctx->f3_rb.Reserve(rb_bytes))) return rc;
+      std::memcpy(ctx->f3_up.ptr, rp.data(), sizeof(RotPair3Host) * rp.size());
       if (!hists.empty())
-        CSM_HIP(hipMemcpyAsync(dh, hists.data(), sizeof(float) * hists.size(),
-                               hipMemcpyHostToDevice, st));
+        std::memcpy(ctx->f3_up.as<char>() + sizeof(RotPair3Host) * rp.size(), hists.data(),
+                    sizeof(float) * hists.size());
+      CSM_HIP(hipMemcpyAsync(drp, ctx->f3_up.ptr, up_bytes, hipMemcpyHostToDevice, st));
       CSM_HIP(hipMemsetAsync(dcursor, 0, sizeof(unsigned), st));
       CSM_HIP(LaunchRotScores(drp, static_cast<int>(rp.size()), max_yaws, dh, dscores, st));
       CSM_HIP(LaunchYawCompact(drp, static_cast<int>(rp.size()), dscores, dcursor, drange, dk, ds,
                                st));
-      CSM_HIP(hipMemcpyAsync(range.data(), drange, sizeof(int2) * rp.size(),
-                             hipMemcpyDeviceToHost, st));
-      CSM_HIP(hipMemcpyAsync(&kept, dcursor, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+      CSM_HIP(hipMemcpyAsync(ctx->f3_rb.ptr, drange, rb_bytes, hipMemcpyDeviceToHost, st));
       CSM_HIP(hipStreamSynchronize(st));
+      std::memcpy(range.data(), ctx->f3_rb.ptr, sizeof(int2) * rp.size());
+      std::memcpy(&kept, ctx->f3_rb.as<char>() + sizeof(int2) * rp.size(), sizeof(unsigned));
       // The passing (k, score) lists stay on the device (f3_scores) for the
       // yaw_build kernel; the host reads them back with the results.
       dev_k = dk;
@@ -1981,9 +1988,15 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
   unsigned* dcounter = ctx->f3_counter.as<unsigned>();
   unsigned long long* dstats = reinterpret_cast<unsigned long long*>(
       reinterpret_cast<char*>(ctx->f3_counter.ptr) + 8);
-  CSM_HIP(hipMemcpyAsync(dpairs, pdesc.data(), sizeof(Pair3Desc) * np, hipMemcpyHostToDevice, st));
-  CSM_HIP(hipMemcpyAsync(dsub, sdesc.data(), sizeof(Submap3Desc) * num_submaps,
-                         hipMemcpyHostToDevice, st));
+  // Pair and submap descriptors (adjacent on the device) in one pinned
+  // upload; the yaw-build records follow in the same staging buffer.
+  const size_t desc_bytes = sizeof(Pair3Desc) * np + sizeof(Submap3Desc) * num_submaps;
+  const size_t yb_at = (desc_bytes + 15) & ~size_t{15};
+  if ((rc = ctx->f3_up.Reserve(yb_at + sizeof(YawBuild3) * np))) return rc;
+  std::memcpy(ctx->f3_up.ptr, pdesc.data(), sizeof(Pair3Desc) * np);
+  std::memcpy(ctx->f3_up.as<char>() + sizeof(Pair3Desc) * np, sdesc.data(),
+              sizeof(Submap3Desc) * num_submaps);
+  CSM_HIP(hipMemcpyAsync(dpairs, ctx->f3_up.ptr, desc_bytes, hipMemcpyHostToDevice, st));
   if (ny > 0) {
     // Discrete-scan poses of the yaws that pass, built on the device from the
     // compacted (k, score) lists; the few yaws whose float sin / cos rounding
@@ -2010,20 +2023,27 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
       b.num = pdesc[dp].num_yaws;
     }
     // f3_items held the rotational-score inputs, which are consumed (synced).
-    if ((rc = ctx->f3_items.Reserve(sizeof(YawBuild3) * np + sizeof(YawFlag3) * kYawFlagCap + 16)))
+    // Layout [flag count (16 B) | flags | build records]: the count and the
+    // first 64 flags come back in one pinned copy.
+    if ((rc = ctx->f3_items.Reserve(16 + sizeof(YawFlag3) * kYawFlagCap + sizeof(YawBuild3) * np)))
       return rc;
-    YawBuild3* dyb = ctx->f3_items.as<YawBuild3>();
-    YawFlag3* dflags = reinterpret_cast<YawFlag3*>(dyb + np);
-    unsigned* dflag_count = reinterpret_cast<unsigned*>(dflags + kYawFlagCap);
-    CSM_HIP(hipMemcpyAsync(dyb, yb.data(), sizeof(YawBuild3) * np, hipMemcpyHostToDevice, st));
+    unsigned* dflag_count = ctx->f3_items.as<unsigned>();
+    YawFlag3* dflags = reinterpret_cast<YawFlag3*>(ctx->f3_items.as<char>() + 16);
+    YawBuild3* dyb = reinterpret_cast<YawBuild3*>(dflags + kYawFlagCap);
+    std::memcpy(ctx->f3_up.as<char>() + yb_at, yb.data(), sizeof(YawBuild3) * np);
+    CSM_HIP(hipMemcpyAsync(dyb, ctx->f3_up.as<char>() + yb_at, sizeof(YawBuild3) * np,
+                           hipMemcpyHostToDevice, st));
     CSM_HIP(hipMemsetAsync(dflag_count, 0, sizeof(unsigned), st));
     CSM_HIP(LaunchYawBuild(dyb, np, dev_k, dev_s, ctx->f3_yaws.as<Yaw3Desc>(), dflag_count, dflags,
                            st));
     unsigned nflag = 0;
     YawFlag3 flags[64];
-    CSM_HIP(hipMemcpyAsync(&nflag, dflag_count, sizeof(unsigned), hipMemcpyDeviceToHost, st));
-    CSM_HIP(hipMemcpyAsync(flags, dflags, sizeof(flags), hipMemcpyDeviceToHost, st));
+    const size_t flag_rb = 16 + sizeof(flags);
+    if ((rc = ctx->f3_rb.Reserve(flag_rb))) return rc;
+    CSM_HIP(hipMemcpyAsync(ctx->f3_rb.ptr, dflag_count, flag_rb, hipMemcpyDeviceToHost, st));
     CSM_HIP(hipStreamSynchronize(st));
+    std::memcpy(&nflag, ctx->f3_rb.ptr, sizeof(unsigned));
+    std::memcpy(flags, ctx->f3_rb.as<char>() + 16, sizeof(flags));
     // CSM_YAW_HOST_BUILD (tests): the host path for every yaw.
     if (nflag > static_cast<unsigned>(kYawFlagCap) || std::getenv("CSM_YAW_HOST_BUILD")) {
       // More undecided roundings than the flag list holds (~2^-15 per value,
@@ -2061,10 +2081,19 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
     }
   }
   CSM_HIP(hipStreamWaitEvent(st, ctx->f3_points_ready, 0));
-  CSM_HIP(hipMemsetAsync(dbest, 0, sizeof(unsigned long long) * np, st));
-  CSM_HIP(hipMemsetAsync(ctx->f3_best_hi.ptr, 0, sizeof(unsigned long long) * np, st));
-  CSM_HIP(hipMemsetAsync(ctx->f3_status.ptr, 0, sizeof(int32_t) * np, st));
-  CSM_HIP(hipMemsetAsync(ctx->f3_counter.ptr, 0, 8 + 16 * sizeof(unsigned long long), st));
+  {  // best keys, witnesses, statuses, claim counters and stats: one launch
+    Segs3 z{};
+    z.ptr[0] = dbest;
+    z.bytes[0] = sizeof(unsigned long long) * np;
+    z.ptr[1] = ctx->f3_best_hi.ptr;
+    z.bytes[1] = sizeof(unsigned long long) * np;
+    z.ptr[2] = ctx->f3_status.ptr;
+    z.bytes[2] = sizeof(int32_t) * np;
+    z.ptr[3] = ctx->f3_counter.ptr;
+    z.bytes[3] = 8 + 16 * sizeof(unsigned long long);
+    z.n = 4;
+    CSM_HIP(LaunchSegments(z, nullptr, st));
+  }
   lap(4);
   {
     const size_t wgs = static_cast<size_t>(ctx->num_cus) *
@@ -2095,20 +2124,36 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
   std::vector<float> lows(np);
   std::vector<int32_t> stat(np);
   unsigned long long lookups = 0, prof[16] = {0};
-  CSM_HIP(hipMemcpyAsync(keys.data(), dbest, sizeof(unsigned long long) * np,
-                         hipMemcpyDeviceToHost, st));
-  CSM_HIP(hipMemcpyAsync(keys_hi.data(), ctx->f3_best_hi.ptr, sizeof(unsigned long long) * np,
-                         hipMemcpyDeviceToHost, st));
-  CSM_HIP(hipMemcpyAsync(stat.data(), ctx->f3_status.ptr, sizeof(int32_t) * np,
-                         hipMemcpyDeviceToHost, st));
-  CSM_HIP(hipMemcpyAsync(prof, dstats, sizeof(prof), hipMemcpyDeviceToHost, st));
   yk.resize(std::max(kept, 1u));
   ys.resize(std::max(kept, 1u));
-  if (kept > 0) {
-    CSM_HIP(hipMemcpyAsync(yk.data(), dev_k, sizeof(int32_t) * kept, hipMemcpyDeviceToHost, st));
-    CSM_HIP(hipMemcpyAsync(ys.data(), dev_s, sizeof(float) * kept, hipMemcpyDeviceToHost, st));
+  {  // keys, witnesses, statuses, stats and the passing yaws: packed on the
+     // device, one pinned readback
+    Segs3 g{};
+    void* src[6] = {dbest, ctx->f3_best_hi.ptr, ctx->f3_status.ptr, dstats,
+                    const_cast<int32_t*>(dev_k), const_cast<float*>(dev_s)};
+    const int64_t by[6] = {static_cast<int64_t>(sizeof(unsigned long long)) * np,
+                           static_cast<int64_t>(sizeof(unsigned long long)) * np,
+                           static_cast<int64_t>(sizeof(int32_t)) * np, static_cast<int64_t>(sizeof(prof)),
+                           static_cast<int64_t>(sizeof(int32_t)) * kept,
+                           static_cast<int64_t>(sizeof(float)) * kept};
+    int64_t total = 0;
+    for (int k = 0; k < 6; ++k) {
+      g.ptr[k] = src[k];
+      g.bytes[k] = src[k] ? by[k] : 0;
+      total += g.bytes[k];
+    }
+    g.n = 6;
+    if ((rc = ctx->f3_pack.Reserve(total)) || (rc = ctx->f3_rb.Reserve(total))) return rc;
+    CSM_HIP(LaunchSegments(g, ctx->f3_pack.ptr, st));
+    CSM_HIP(hipMemcpyAsync(ctx->f3_rb.ptr, ctx->f3_pack.ptr, total, hipMemcpyDeviceToHost, st));
+    CSM_HIP(hipStreamSynchronize(st));
+    const char* h = ctx->f3_rb.as<char>();
+    void* dst[6] = {keys.data(), keys_hi.data(), stat.data(), prof, yk.data(), ys.data()};
+    for (int k = 0; k < 6; ++k) {
+      if (g.bytes[k]) std::memcpy(dst[k], h, g.bytes[k]);
+      h += g.bytes[k];
+    }
   }
-  CSM_HIP(hipStreamSynchronize(st));
   // Exactly tied maxima: the reference's pick (ResolveTies3d), then the
   // winning leaves' low-resolution scores (the Result field).
   std::vector<int8_t> tie_code(np, CSM_TIE_NONE);
@@ -2120,8 +2165,10 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
                              hipMemcpyHostToDevice, st));
     CSM_HIP(LaunchFast3dFinalize(np, st, dsub, dpairs, ctx->f3_yaws.as<Yaw3Desc>(),
                                  ctx->f3_low_points.as<float>(), dbest, dlow));
-    CSM_HIP(hipMemcpyAsync(lows.data(), dlow, sizeof(float) * np, hipMemcpyDeviceToHost, st));
+    if ((rc = ctx->f3_rb.Reserve(sizeof(float) * np))) return rc;
+    CSM_HIP(hipMemcpyAsync(ctx->f3_rb.ptr, dlow, sizeof(float) * np, hipMemcpyDeviceToHost, st));
     CSM_HIP(hipStreamSynchronize(st));
+    std::memcpy(lows.data(), ctx->f3_rb.ptr, sizeof(float) * np);
   }
   if (ctx->timing) {
     float ms = 0.f;
@@ -2226,13 +2273,21 @@ int RunSingleBatch3(csm_context* owner, const std::vector<SingleReq3*>& reqs) {
   return CSM_OK;
 }
 
-// Concurrent single 3D calls on one owner context are coalesced as in 2D
-// (csm_host.cc SingleMatch): each queues its pair; a caller that finds fewer
-// than CSM_COALESCE_LEADERS (3) batches running becomes a leader, waits up
-// to CSM_COALESCE_WINDOW_US (150 us) for as many callers as the previous
-// batch had, searches the queue as one batch and wakes the callers it
-// served. A pair's result does not depend on its batch.
-// CSM_SINGLE_COALESCE=0: each call alone on its own call context.
+// Concurrent single 3D calls on one owner context are coalesced (as in 2D,
+// csm_host.cc SingleMatch): each queues its pair; a caller that finds fewer
+// than CSM_COALESCE_LEADERS3 (2) batches running becomes a leader, waits up
+// to CSM_COALESCE_WINDOW_US3 (300 us) until the queue holds its share of the
+// callers, ceil(callers / leaders), searches the queue as one batch and
+// wakes the callers it served. `callers` is the owner's recent high-water
+// mark of calls in flight (decaying by one per batch), so with T threads
+// calling back to back two batches of about T / 2 alternate, one searching
+// while the other's callers return and queue again. A 3D pair costs a few
+// microseconds of device time against ~0.3 ms of fixed latency per batch
+// (the pipeline's launches, copies and synchronizations), so batch size,
+// not device time, sets the single-call rate: the previous rule (wait for
+// as many callers as the previous batch had, 3 leaders) settled at ~2
+// pairs per batch (profiles/r6h/). A pair's result does not depend on its
+// batch. CSM_SINGLE_COALESCE=0: each call alone on its own call context.
 int SingleMatch3(const csm_fast3d* m, const csm_pair3d& pair, const csm_node3d* node,
                  csm_result3d* result) {
   csm_context* owner = m->ctx;
@@ -2242,12 +2297,12 @@ int SingleMatch3(const csm_fast3d* m, const csm_pair3d& pair, const csm_node3d* 
     return !(e && std::strcmp(e, "0") == 0);
   }();
   static const int leaders = [] {
-    const char* e = std::getenv("CSM_COALESCE_LEADERS");
-    return e ? std::max(1, std::atoi(e)) : 3;
+    const char* e = std::getenv("CSM_COALESCE_LEADERS3");
+    return e ? std::max(1, std::atoi(e)) : 2;
   }();
   static const int window_us = [] {
-    const char* e = std::getenv("CSM_COALESCE_WINDOW_US");
-    return e ? std::max(0, std::atoi(e)) : 150;
+    const char* e = std::getenv("CSM_COALESCE_WINDOW_US3");
+    return e ? std::max(0, std::atoi(e)) : 300;
   }();
   if (!coalesce) {
     std::vector<SingleReq3*> one{&r};
@@ -2259,13 +2314,15 @@ int SingleMatch3(const csm_fast3d* m, const csm_pair3d& pair, const csm_node3d* 
   } else {
     std::unique_lock<std::mutex> lk(owner->co_mu);
     owner->co3_queue.push_back(&r);
+    owner->co3_callers = std::max(owner->co3_callers, ++owner->co3_in_flight);
     owner->co_cv.notify_all();
     while (!r.done) {
       const bool queued = std::find(owner->co3_queue.begin(), owner->co3_queue.end(), &r) !=
                           owner->co3_queue.end();
       if (queued && owner->co3_leaders < leaders) {
         ++owner->co3_leaders;
-        const size_t want = static_cast<size_t>(std::max(1, owner->co3_last_batch));
+        owner->co3_callers = std::max(owner->co3_in_flight, owner->co3_callers - 1);
+        const size_t want = static_cast<size_t>((owner->co3_callers + leaders - 1) / leaders);
         const auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(window_us);
         while (owner->co3_queue.size() < want &&
                owner->co_cv.wait_until(lk, deadline) != std::cv_status::timeout) {
@@ -2293,6 +2350,7 @@ int SingleMatch3(const csm_fast3d* m, const csm_pair3d& pair, const csm_node3d* 
         owner->co_cv.wait(lk);
       }
     }
+    --owner->co3_in_flight;
   }
   *result = r.res;
   if (r.rc < 0) return r.rc;

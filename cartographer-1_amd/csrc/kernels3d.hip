@@ -2591,6 +2591,31 @@ hipError_t LaunchFast3dScoreQueries(int num_jobs, hipStream_t st, const Submap3D
   return hipGetLastError();
 }
 
+// blockIdx.y = segment, 64 workgroups each: out == nullptr zeroes the
+// segments, else segment k is copied to out + (the bytes of segments 0..k-1).
+__global__ void __launch_bounds__(256) segments_kernel(Segs3 segs, uint32_t* __restrict__ out) {
+  const int k = blockIdx.y;
+  int64_t at = 0;
+  for (int j = 0; j < k; ++j) at += segs.bytes[j];
+  uint32_t* p = static_cast<uint32_t*>(segs.ptr[k]);
+  const int64_t words = segs.bytes[k] / 4;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < words; i += 256 * gridDim.x) {
+    if (out)
+      out[at / 4 + i] = p[i];
+    else
+      p[i] = 0u;
+  }
+}
+
+hipError_t LaunchSegments(const Segs3& segs, void* out, hipStream_t st) {
+  if (segs.n <= 0) return hipSuccess;
+  for (int k = 0; k < segs.n; ++k)
+    if (segs.bytes[k] % 4 != 0 || (segs.bytes[k] > 0 && !segs.ptr[k])) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(segments_kernel, dim3(64, segs.n), dim3(256), 0, st, segs,
+                     static_cast<uint32_t*>(out));
+  return hipGetLastError();
+}
+
 hipError_t LaunchFast3dFinalize(int num_pairs, hipStream_t st, const Submap3Desc* submaps,
                                 const Pair3Desc* pairs, const Yaw3Desc* yaws,
                                 const float* low_points, const unsigned long long* best,

@@ -70,6 +70,9 @@ def test_two_ranks_rccl_branch_equal_single_rank(tmp_path):
         assert p["gpu_errors"] == 0
         assert j["work_ratio"]["pairs"] == 24 and j["work_ratio"]["oracle"]["lookups_per_pair"] > 0
     assert j2["parity_sample"]["ranks"] == 2
+    p3 = j2["fast3d"]["parity_sample"]  # each rank's C5 share against the oracle, summed
+    assert p3["ranks"] == 2 and p3["pairs"] == p3["compared"] == 24, p3
+    assert p3["mismatched_decision"] == p3["mismatched_score"] == p3["mismatched_pose"] == 0, p3
     a, b = np.load(one), np.load(two)
     for key in ("c3", "c5"):
         assert a[key].shape == b[key].shape and len(a[key]) > 0, key
