@@ -38,8 +38,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 # (a traffic file recorded on another kernel version is not reported).
 KERNEL_TAG = "v5-align8"
 # fast3d_search version whose PMC passes profiles/r5bd/traffic_c5.json holds.
-KERNEL3D_TAG = "f3-octet-tieprune"
-TRAFFIC3D_FILE = os.path.join("profiles", "r5bd", "traffic_c5.json")
+KERNEL3D_TAG = "f3-octet-trim"
+TRAFFIC3D_FILE = os.path.join("profiles", "r6l", "traffic_c5.json")
 
 
 def load_pkg():
@@ -1415,9 +1415,25 @@ def dropin_3d(csm, w, mats, sub, nod, rot, res3, calls, threads=16):
             mism += 1
     if mism:
         raise RuntimeError(f"C5 single calls: {mism} of {calls} differ from the batch's results")
+    # The same call pattern from C++ threads (tools/dropin_threads3d.cc, no
+    # GIL) on a C5 slice: what ConstraintBuilder3D's ThreadPool sees through
+    # the C-ABI, with every result checked against the batch's.
+    threaded_cpp = None
+    exe = os.path.join(ROOT, "tools", "dropin_threads3d")
+    if os.path.exists(exe):
+        import subprocess
+        try:
+            res = subprocess.run([exe, "4000", "8", "200"], capture_output=True, text=True, timeout=300)
+            threaded_cpp = json.loads(res.stdout.strip().splitlines()[-1])
+            if res.returncode != 0:
+                raise RuntimeError(f"dropin_threads3d: exit {res.returncode}, {threaded_cpp}")
+        except (subprocess.SubprocessError, ValueError, IndexError) as e:
+            threaded_cpp = {"error": str(e)[:200]}
     return {"calls": int(calls), "threads": threads, "pairs_per_s": calls / el,
             "matched": int(sum(g is not None for g in got)), "mismatches_vs_batch": mism,
-            "note": "single csm_fast3d_match_full_submap calls, coalesced by the library"}
+            "single_call_threads_cpp": threaded_cpp,
+            "note": "single csm_fast3d_match_full_submap calls from Python threads (GIL-bound), "
+                    "coalesced by the library; single_call_threads_cpp: C++ threads on a C5 slice"}
 
 
 def merged_timing(contexts):
