@@ -71,3 +71,41 @@ def test_launch_ranks_rejects_mismatch(monkeypatch, bad):
     with pytest.raises(SystemExit) as e:
         bench.launch_ranks(argparse.Namespace(**bad))
     assert e.value.code == 2
+
+
+def test_gather_sample_merges_every_ranks_results():
+    """At N > 1 each rank keeps the sampled pairs of the chunks it claimed;
+    rank 0 receives every rank's (index, result) rows through csm_comm_gather
+    and fills its table (bench.gather_sample). A fake communicator stands in
+    for the 2-rank gather."""
+    ensure_built()
+    csm = load_package()
+    k = 10
+
+    def table(have):
+        t = {"gpu": np.zeros(k, csm.RESULT_DTYPE), "have": np.zeros(k, bool)}
+        for i in have:
+            t["gpu"][i]["status"] = 0
+            t["gpu"][i]["score"] = 0.5 + i / 100
+            t["have"][i] = True
+        return t
+
+    r0, r1 = table([0, 3, 4]), table([1, 2, 7, 9])
+
+    class FakeComm:
+        def __init__(self, blobs):
+            self.blobs = blobs
+
+        def gather(self, blob):
+            return None if self.blobs is None else [blob] + self.blobs
+
+    row = np.dtype([("i", "<i8"), ("r", csm.RESULT_DTYPE)])
+    have1 = np.nonzero(r1["have"])[0]
+    other = np.zeros(len(have1), row)
+    other["i"], other["r"] = have1, r1["gpu"][have1]
+    bench.gather_sample(r0, FakeComm([other.tobytes()]), csm)
+    assert r0["have"].tolist() == [i in (0, 1, 2, 3, 4, 7, 9) for i in range(k)]
+    for i in (1, 2, 7, 9):
+        assert r0["gpu"][i]["score"] == np.float32(0.5 + i / 100)
+    bench.gather_sample(r1, FakeComm(None), csm)  # a non-root rank: its table is untouched
+    assert r1["have"].sum() == 4
