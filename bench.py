@@ -38,8 +38,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 # (a traffic file recorded on another kernel version is not reported).
 KERNEL_TAG = "v5-align8"
 # fast3d_search version whose PMC passes profiles/r5bd/traffic_c5.json holds.
-KERNEL3D_TAG = "f3-octet-tieprune"
-TRAFFIC3D_FILE = os.path.join("profiles", "r5bd", "traffic_c5.json")
+KERNEL3D_TAG = "f3-octet-trim"
+TRAFFIC3D_FILE = os.path.join("profiles", "r6l", "traffic_c5.json")
 
 
 def load_pkg():
