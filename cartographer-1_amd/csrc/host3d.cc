@@ -1733,9 +1733,18 @@ int ResolveTies3d(csm_context* ctx, csm_fast3d* const* submaps, const std::vecto
 
 }  // namespace
 
-int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t num_submaps,
-                           const csm_node3d* nodes, int32_t num_nodes, const csm_pair3d* pairs,
-                           int64_t num_pairs, csm_result3d* results) {
+namespace {
+// MatchBatch3's answer when the device flagged a yaw whose float rounding it
+// could not decide after the flag check was deferred: the batch runs again
+// with the check before the search.
+constexpr int kRetryWithYawFlags = 0x7fff0001;
+
+// defer_flags: the yaw build's flag count is read back with the results
+// instead of synchronizing after the build (one synchronization less per
+// batch; a flag, ~2^-16 per yaw, makes the caller rerun with the check).
+int MatchBatch3(csm_context* ctx, csm_fast3d* const* submaps, int32_t num_submaps,
+                const csm_node3d* nodes, int32_t num_nodes, const csm_pair3d* pairs,
+                int64_t num_pairs, csm_result3d* results, bool defer_flags) {
   if (!ctx || num_pairs < 0 || (num_pairs > 0 && (!pairs || !results || !submaps || !nodes)))
     return CSM_EINVAL;
   // Matchers from any context on ctx's device (e.g. a single call's call
@@ -1993,6 +2002,8 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
   const size_t desc_bytes = sizeof(Pair3Desc) * np + sizeof(Submap3Desc) * num_submaps;
   const size_t yb_at = (desc_bytes + 15) & ~size_t{15};
   if ((rc = ctx->f3_up.Reserve(yb_at + sizeof(YawBuild3) * np))) return rc;
+  unsigned* dflag_count = nullptr;  // the yaw build's flag count (device)
+  if (std::getenv("CSM_YAW_HOST_BUILD")) defer_flags = false;
   std::memcpy(ctx->f3_up.ptr, pdesc.data(), sizeof(Pair3Desc) * np);
   std::memcpy(ctx->f3_up.as<char>() + sizeof(Pair3Desc) * np, sdesc.data(),
               sizeof(Submap3Desc) * num_submaps);
@@ -2027,7 +2038,7 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
     // first 64 flags come back in one pinned copy.
     if ((rc = ctx->f3_items.Reserve(16 + sizeof(YawFlag3) * kYawFlagCap + sizeof(YawBuild3) * np)))
       return rc;
-    unsigned* dflag_count = ctx->f3_items.as<unsigned>();
+    dflag_count = ctx->f3_items.as<unsigned>();
     YawFlag3* dflags = reinterpret_cast<YawFlag3*>(ctx->f3_items.as<char>() + 16);
     YawBuild3* dyb = reinterpret_cast<YawBuild3*>(dflags + kYawFlagCap);
     std::memcpy(ctx->f3_up.as<char>() + yb_at, yb.data(), sizeof(YawBuild3) * np);
@@ -2039,46 +2050,48 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
     unsigned nflag = 0;
     YawFlag3 flags[64];
     const size_t flag_rb = 16 + sizeof(flags);
-    if ((rc = ctx->f3_rb.Reserve(flag_rb))) return rc;
-    CSM_HIP(hipMemcpyAsync(ctx->f3_rb.ptr, dflag_count, flag_rb, hipMemcpyDeviceToHost, st));
-    CSM_HIP(hipStreamSynchronize(st));
-    std::memcpy(&nflag, ctx->f3_rb.ptr, sizeof(unsigned));
-    std::memcpy(flags, ctx->f3_rb.as<char>() + 16, sizeof(flags));
-    // CSM_YAW_HOST_BUILD (tests): the host path for every yaw.
-    if (nflag > static_cast<unsigned>(kYawFlagCap) || std::getenv("CSM_YAW_HOST_BUILD")) {
-      // More undecided roundings than the flag list holds (~2^-15 per value,
-      // so only in batches of ~10^8 yaws): rebuild every yaw on the host.
-      std::vector<int32_t> hk(std::max(kept, 1u));
-      std::vector<float> hs(std::max(kept, 1u));
-      CSM_HIP(hipMemcpyAsync(hk.data(), dev_k, sizeof(int32_t) * kept, hipMemcpyDeviceToHost, st));
-      CSM_HIP(hipMemcpyAsync(hs.data(), dev_s, sizeof(float) * kept, hipMemcpyDeviceToHost, st));
+    if (!defer_flags) {
+      if ((rc = ctx->f3_rb.Reserve(flag_rb))) return rc;
+      CSM_HIP(hipMemcpyAsync(ctx->f3_rb.ptr, dflag_count, flag_rb, hipMemcpyDeviceToHost, st));
       CSM_HIP(hipStreamSynchronize(st));
-      if ((rc = ctx->f3_host_yaws.Reserve(sizeof(Yaw3Desc) * ny))) return rc;
-      Yaw3Desc* hy = ctx->f3_host_yaws.as<Yaw3Desc>();
-      ParallelPairs(np, [&](int64_t dp) {
-        const int64_t i = pair_of[dp];
-        BuildYaws(hk.data() + yaw_src[i], hs.data() + yaw_src[i], prep[i].num_yaws,
-                  static_cast<int32_t>(dp), prep[i], hy + pdesc[dp].yaw_begin);
-      });
-      CSM_HIP(hipMemcpyAsync(ctx->f3_yaws.ptr, hy, sizeof(Yaw3Desc) * ny, hipMemcpyHostToDevice, st));
-      nflag = 0;
-    }
-    if (nflag > 0) {
-      std::vector<YawFlag3> all(flags, flags + std::min<unsigned>(nflag, 64));
-      if (nflag > 64) {
-        all.resize(nflag);
-        CSM_HIP(hipMemcpy(all.data(), dflags, sizeof(YawFlag3) * nflag, hipMemcpyDeviceToHost));
+      std::memcpy(&nflag, ctx->f3_rb.ptr, sizeof(unsigned));
+      std::memcpy(flags, ctx->f3_rb.as<char>() + 16, sizeof(flags));
+      // CSM_YAW_HOST_BUILD (tests): the host path for every yaw.
+      if (nflag > static_cast<unsigned>(kYawFlagCap) || std::getenv("CSM_YAW_HOST_BUILD")) {
+        // More undecided roundings than the flag list holds (~2^-15 per value,
+        // so only in batches of ~10^8 yaws): rebuild every yaw on the host.
+        std::vector<int32_t> hk(std::max(kept, 1u));
+        std::vector<float> hs(std::max(kept, 1u));
+        CSM_HIP(hipMemcpyAsync(hk.data(), dev_k, sizeof(int32_t) * kept, hipMemcpyDeviceToHost, st));
+        CSM_HIP(hipMemcpyAsync(hs.data(), dev_s, sizeof(float) * kept, hipMemcpyDeviceToHost, st));
+        CSM_HIP(hipStreamSynchronize(st));
+        if ((rc = ctx->f3_host_yaws.Reserve(sizeof(Yaw3Desc) * ny))) return rc;
+        Yaw3Desc* hy = ctx->f3_host_yaws.as<Yaw3Desc>();
+        ParallelPairs(np, [&](int64_t dp) {
+          const int64_t i = pair_of[dp];
+          BuildYaws(hk.data() + yaw_src[i], hs.data() + yaw_src[i], prep[i].num_yaws,
+                    static_cast<int32_t>(dp), prep[i], hy + pdesc[dp].yaw_begin);
+        });
+        CSM_HIP(hipMemcpyAsync(ctx->f3_yaws.ptr, hy, sizeof(Yaw3Desc) * ny, hipMemcpyHostToDevice, st));
+        nflag = 0;
       }
-      if ((rc = ctx->f3_host_yaws.Reserve(sizeof(Yaw3Desc) * all.size()))) return rc;
-      Yaw3Desc* hy = ctx->f3_host_yaws.as<Yaw3Desc>();
-      for (size_t f = 0; f < all.size(); ++f) {
-        const YawFlag3& fl = all[f];
-        BuildYaws(&fl.k, &fl.score, 1, fl.dp, prep[pair_of[fl.dp]], &hy[f]);
-        hy[f].yaw_id = fl.j;
-        CSM_HIP(hipMemcpyAsync(ctx->f3_yaws.as<Yaw3Desc>() + pdesc[fl.dp].yaw_begin + fl.j, &hy[f],
-                               sizeof(Yaw3Desc), hipMemcpyHostToDevice, st));
+      if (nflag > 0) {
+        std::vector<YawFlag3> all(flags, flags + std::min<unsigned>(nflag, 64));
+        if (nflag > 64) {
+          all.resize(nflag);
+          CSM_HIP(hipMemcpy(all.data(), dflags, sizeof(YawFlag3) * nflag, hipMemcpyDeviceToHost));
+        }
+        if ((rc = ctx->f3_host_yaws.Reserve(sizeof(Yaw3Desc) * all.size()))) return rc;
+        Yaw3Desc* hy = ctx->f3_host_yaws.as<Yaw3Desc>();
+        for (size_t f = 0; f < all.size(); ++f) {
+          const YawFlag3& fl = all[f];
+          BuildYaws(&fl.k, &fl.score, 1, fl.dp, prep[pair_of[fl.dp]], &hy[f]);
+          hy[f].yaw_id = fl.j;
+          CSM_HIP(hipMemcpyAsync(ctx->f3_yaws.as<Yaw3Desc>() + pdesc[fl.dp].yaw_begin + fl.j, &hy[f],
+                                 sizeof(Yaw3Desc), hipMemcpyHostToDevice, st));
+        }
       }
-    }
+    }  // !defer_flags
   }
   CSM_HIP(hipStreamWaitEvent(st, ctx->f3_points_ready, 0));
   {  // best keys, witnesses, statuses, claim counters and stats: one launch
@@ -2126,49 +2139,64 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
   unsigned long long lookups = 0, prof[16] = {0};
   yk.resize(std::max(kept, 1u));
   ys.resize(std::max(kept, 1u));
-  {  // keys, witnesses, statuses, stats and the passing yaws: packed on the
-     // device, one pinned readback
+  // The winners' low-resolution scores (the Result field) for the keys as
+  // the search left them; redone below only if tie resolution moves a key.
+  CSM_HIP(LaunchFast3dFinalize(np, st, dsub, dpairs, ctx->f3_yaws.as<Yaw3Desc>(),
+                               ctx->f3_low_points.as<float>(), dbest, dlow));
+  unsigned nflag = 0;
+  {  // keys, witnesses, statuses, stats, the passing yaws, the low-resolution
+     // scores and (deferred) the yaw flag count: packed on the device, one
+     // pinned readback
     Segs3 g{};
-    void* src[6] = {dbest, ctx->f3_best_hi.ptr, ctx->f3_status.ptr, dstats,
-                    const_cast<int32_t*>(dev_k), const_cast<float*>(dev_s)};
-    const int64_t by[6] = {static_cast<int64_t>(sizeof(unsigned long long)) * np,
+    const bool rb_flags = defer_flags && dflag_count;
+    void* src[8] = {dbest, ctx->f3_best_hi.ptr, ctx->f3_status.ptr, dstats,
+                    const_cast<int32_t*>(dev_k), const_cast<float*>(dev_s), dlow,
+                    rb_flags ? dflag_count : nullptr};
+    const int64_t by[8] = {static_cast<int64_t>(sizeof(unsigned long long)) * np,
                            static_cast<int64_t>(sizeof(unsigned long long)) * np,
                            static_cast<int64_t>(sizeof(int32_t)) * np, static_cast<int64_t>(sizeof(prof)),
                            static_cast<int64_t>(sizeof(int32_t)) * kept,
-                           static_cast<int64_t>(sizeof(float)) * kept};
+                           static_cast<int64_t>(sizeof(float)) * kept,
+                           static_cast<int64_t>(sizeof(float)) * np,
+                           static_cast<int64_t>(sizeof(unsigned))};
     int64_t total = 0;
-    for (int k = 0; k < 6; ++k) {
+    for (int k = 0; k < 8; ++k) {
       g.ptr[k] = src[k];
       g.bytes[k] = src[k] ? by[k] : 0;
       total += g.bytes[k];
     }
-    g.n = 6;
+    g.n = 8;
     if ((rc = ctx->f3_pack.Reserve(total)) || (rc = ctx->f3_rb.Reserve(total))) return rc;
     CSM_HIP(LaunchSegments(g, ctx->f3_pack.ptr, st));
     CSM_HIP(hipMemcpyAsync(ctx->f3_rb.ptr, ctx->f3_pack.ptr, total, hipMemcpyDeviceToHost, st));
     CSM_HIP(hipStreamSynchronize(st));
     const char* h = ctx->f3_rb.as<char>();
-    void* dst[6] = {keys.data(), keys_hi.data(), stat.data(), prof, yk.data(), ys.data()};
-    for (int k = 0; k < 6; ++k) {
+    void* dst[8] = {keys.data(), keys_hi.data(), stat.data(), prof, yk.data(), ys.data(),
+                    lows.data(), &nflag};
+    for (int k = 0; k < 8; ++k) {
       if (g.bytes[k]) std::memcpy(dst[k], h, g.bytes[k]);
       h += g.bytes[k];
     }
   }
+  // Only with deferred flags; CSM_YAW_FORCE_RETRY (tests) takes the retry
+  // path on every batch.
+  if (nflag != 0 || (defer_flags && std::getenv("CSM_YAW_FORCE_RETRY"))) return kRetryWithYawFlags;
   // Exactly tied maxima: the reference's pick (ResolveTies3d), then the
   // winning leaves' low-resolution scores (the Result field).
   std::vector<int8_t> tie_code(np, CSM_TIE_NONE);
   {
     const std::vector<unsigned long long> before = keys;
     if ((rc = ResolveTies3d(ctx, submaps, pdesc, &stat, keys_hi, &keys, &tie_code))) return rc;
-    if (keys != before)
+    if (keys != before) {
       CSM_HIP(hipMemcpyAsync(dbest, keys.data(), sizeof(unsigned long long) * np,
                              hipMemcpyHostToDevice, st));
-    CSM_HIP(LaunchFast3dFinalize(np, st, dsub, dpairs, ctx->f3_yaws.as<Yaw3Desc>(),
-                                 ctx->f3_low_points.as<float>(), dbest, dlow));
-    if ((rc = ctx->f3_rb.Reserve(sizeof(float) * np))) return rc;
-    CSM_HIP(hipMemcpyAsync(ctx->f3_rb.ptr, dlow, sizeof(float) * np, hipMemcpyDeviceToHost, st));
-    CSM_HIP(hipStreamSynchronize(st));
-    std::memcpy(lows.data(), ctx->f3_rb.ptr, sizeof(float) * np);
+      CSM_HIP(LaunchFast3dFinalize(np, st, dsub, dpairs, ctx->f3_yaws.as<Yaw3Desc>(),
+                                   ctx->f3_low_points.as<float>(), dbest, dlow));
+      if ((rc = ctx->f3_rb.Reserve(sizeof(float) * np))) return rc;
+      CSM_HIP(hipMemcpyAsync(ctx->f3_rb.ptr, dlow, sizeof(float) * np, hipMemcpyDeviceToHost, st));
+      CSM_HIP(hipStreamSynchronize(st));
+      std::memcpy(lows.data(), ctx->f3_rb.ptr, sizeof(float) * np);
+    }
   }
   if (ctx->timing) {
     float ms = 0.f;
@@ -2227,6 +2255,17 @@ int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t
     results[i].tie = tie_code[dp];
   }
   return CSM_OK;
+}
+
+}  // namespace
+
+int csm_fast3d_match_batch(csm_context* ctx, csm_fast3d* const* submaps, int32_t num_submaps,
+                           const csm_node3d* nodes, int32_t num_nodes, const csm_pair3d* pairs,
+                           int64_t num_pairs, csm_result3d* results) {
+  const int rc = MatchBatch3(ctx, submaps, num_submaps, nodes, num_nodes, pairs, num_pairs, results,
+                             /*defer_flags=*/true);
+  if (rc != kRetryWithYawFlags) return rc;
+  return MatchBatch3(ctx, submaps, num_submaps, nodes, num_nodes, pairs, num_pairs, results, false);
 }
 
 namespace {

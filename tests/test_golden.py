@@ -227,13 +227,17 @@ def test_oracle_reproduces_rt3d_golden(oracle):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("yaw_build", ["device", "host"])
+@pytest.mark.parametrize("yaw_build", ["device", "host", "retry"])
 def test_gpu_matches_fast3d_golden(csm, oracle, yaw_build, monkeypatch):
-    """Both discrete-scan pose paths: built on the device (yaw_build, libm
-    fix-ups for undecided roundings) and the host path that a flag-list
-    overflow falls back to (CSM_YAW_HOST_BUILD forces it)."""
+    """Every discrete-scan pose path: built on the device (yaw_build, flag
+    count read back with the results), the rerun with the flag check before
+    the search that a flagged yaw triggers (libm fix-ups; CSM_YAW_FORCE_RETRY
+    forces it) and the host path that a flag-list overflow falls back to
+    (CSM_YAW_HOST_BUILD forces it)."""
     if yaw_build == "host":
         monkeypatch.setenv("CSM_YAW_HOST_BUILD", "1")
+    if yaw_build == "retry":
+        monkeypatch.setenv("CSM_YAW_FORCE_RETRY", "1")
     from test_fast3d_gpu import assert_same_result
     d = _load("fast3d_c5.npz")
     o = csm.FastCorrelativeScanMatcherOptions3D(*[int(v) if i < 2 else float(v)
