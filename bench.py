@@ -37,9 +37,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 # Version tag of the search kernel the committed PMC traffic figures belong to
 # (a traffic file recorded on another kernel version is not reported).
 KERNEL_TAG = "v5-align8"
-# fast3d_search version whose PMC passes profiles/r5bd/traffic_c5.json holds.
-KERNEL3D_TAG = "f3-octet-trim"
-TRAFFIC3D_FILE = os.path.join("profiles", "r6l", "traffic_c5.json")
+# fast3d_search version whose PMC passes TRAFFIC3D_FILE holds.
+KERNEL3D_TAG = "f3-tiny5"
+TRAFFIC3D_FILE = os.path.join("profiles", "r6q", "traffic_c5.json")
 
 
 def load_pkg():

@@ -11,6 +11,7 @@ namespace csm {
 constexpr int kMaxLevels3d = 12;
 constexpr int kExtraLevels3d = 2;       // coarser levels above the reference's stack (roots only)
 constexpr int kRootTarget3d = 512;       // a pair's roots start at the lowest level with <= this many
+constexpr int kTiny3dPoints = 512;       // cloud capacity (LDS) of the tiny-cloud build (24 KiB, 5 per CU)
 constexpr int kSmall3dPoints = 2048;      // cloud capacity (LDS) of the 4-workgroups-per-CU build
 constexpr int kMax3dPoints = 8192;        // of the large-cloud build (2 per CU); more: CSM_ERANGE
 constexpr int kTopLds3d = 6 * 1024;       // top pyramid level cached in LDS when it fits
@@ -21,14 +22,26 @@ constexpr int kBatch3d = 16;              // DFS nodes scored per step (16 lanes
 constexpr int kMax3dTop = 1 << 20;        // top-level candidates per yaw
 constexpr int kTieCap3d = 4096;           // tied leaves recorded per pair (collect search)
 constexpr int kWalkStack3d = 128;         // ordered-walk stack: 1 + 7 x depth entries at most
-constexpr int kStack3d = 1024;            // DFS stack entries per workgroup in LDS
-constexpr int kSpill3d = 3072;            // further entries per workgroup in global memory
+constexpr int kStack3d = 1024;            // DFS stack entries per workgroup in LDS (small, large builds)
+constexpr int kTinyStack3d = 512;        // of the tiny-cloud build
+constexpr int kDfsCap3d = 4096;           // DFS stack entries per workgroup, LDS + global spill
 constexpr int kStat3dHighWater = 14;      // stats word: DFS stack high-water (max over workgroups)
 constexpr int kMax3dYaws = 1 << 16;
 constexpr int kMax3dWindow = 1 << 14;
 constexpr int kSearch3dThreads = 256;
-constexpr int kSearch3dBlocksPerCu = 4;       // resident workgroups per CU, small-cloud build
+constexpr int kSearch3dBlocksPerCuTiny = 5;   // resident workgroups per CU, tiny-cloud build
+constexpr int kSearch3dBlocksPerCu = 4;       // small-cloud build
 constexpr int kSearch3dBlocksPerCuLarge = 2;  // large-cloud build
+// Octet loads a lane of the tiny build keeps in flight: 8 fit its 96 VGPRs
+// (16 spill 13); the small and large builds keep 16.
+constexpr int kTinyInflight3d = 8;
+// Search builds by cloud size: 0 tiny, 1 small, 2 large.
+constexpr int kSearch3dTiers = 3;
+constexpr int Search3dTier(int num_points) {
+  return num_points <= kTiny3dPoints ? 0 : num_points <= kSmall3dPoints ? 1 : 2;
+}
+constexpr int kSearch3dBlocksPerCuMax = kSearch3dBlocksPerCuTiny > kSearch3dBlocksPerCu
+                                            ? kSearch3dBlocksPerCuTiny : kSearch3dBlocksPerCu;
 constexpr int kCellLimit3d = 16000;       // |cell index| kept in int16 in LDS
 // Per pair: key = sum << key_shift | ~leaf_id, leaf_id = ((yaw << bxy | x) << bxy
 // | y) << bz | z with x = ox + wxy etc.; the host sizes the fields so that

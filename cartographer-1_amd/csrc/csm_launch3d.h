@@ -77,9 +77,9 @@ hipError_t LaunchRt3dScore5(int nl, int num_blocks, hipStream_t st, const float*
                             const int* rot_index, const float* rot_angle, const float4* trans,
                             const float4* col_t0, const float4* col_thr, int num_rot, double wt,
                             double wr, unsigned long long* best, float* scores, int scores_pitch);
-// Items [item_begin, item_begin + num_items) of the yaw list; `large`
-// selects the build for clouds of more than kSmall3dPoints points.
-hipError_t LaunchFast3dSearch(bool large, int grid, hipStream_t st, const Submap3Desc* submaps,
+// Items [item_begin, item_begin + num_items) of the yaw list; `tier`
+// (Search3dTier of the items' cloud size) selects the build.
+hipError_t LaunchFast3dSearch(int tier, int grid, hipStream_t st, const Submap3Desc* submaps,
                               const Pair3Desc* pairs, const Yaw3Desc* yaws, int item_begin,
                               int num_items, const float* points, const float* low_points,
                               unsigned* counter, unsigned long long* best, int32_t* status,

@@ -1352,6 +1352,21 @@ uint64_t LeafId3(const Pair3Desc& d, int yaw, int x, int y, int z) {  // kernels
   return id;
 }
 
+// fast3d_search workgroups for `items` items of a build tier: the tier's
+// resident workgroups on every CU at most.
+int SearchGrid3(const csm_context* ctx, int tier, int items) {
+  static constexpr int kPerCu[kSearch3dTiers] = {kSearch3dBlocksPerCuTiny, kSearch3dBlocksPerCu,
+                                                  kSearch3dBlocksPerCuLarge};
+  return std::max(1, std::min(items, ctx->num_cus * kPerCu[tier]));
+}
+
+// DFS stack spill of every tier's grid: kDfsCap3d entries less the build's
+// LDS stack per workgroup (the tiers run one after another on one stream).
+size_t SpillBytes3(const csm_context* ctx) {
+  return sizeof(int4) * static_cast<size_t>(kDfsCap3d - std::min(kTinyStack3d, kStack3d)) *
+         static_cast<size_t>(ctx->num_cus) * kSearch3dBlocksPerCuMax;
+}
+
 // Exactly tied maxima in 3D. The search keeps, among the
 // leaves that pass the low-resolution check at the best sum, the smallest
 // (yaw, x, y, z) key and, next to it, the largest (best_hi). The reference
@@ -1393,27 +1408,28 @@ int ResolveTies3d(csm_context* ctx, csm_fast3d* const* submaps, const std::vecto
   const Yaw3Desc* dyaws = ctx->f3_yaws.as<Yaw3Desc>();
   const int nt = static_cast<int>(tied.size());
   int rc;
-  // (1) Collect search over the tied pairs' yaws (small clouds, then large).
+  // (1) Collect search over the tied pairs' yaws (by search build tier).
   std::vector<Pair3Desc> mod(nt);
   std::vector<unsigned long long> init(nt);
-  int items_small = 0, items = 0;
-  for (int pass = 0; pass < 2; ++pass)
+  int items = 0, tier_end[kSearch3dTiers] = {};
+  for (int pass = 0; pass < kSearch3dTiers; ++pass) {
     for (int t = 0; t < nt; ++t) {
       const Pair3Desc& d = pdesc[tied[t]];
-      if ((d.num_points > kSmall3dPoints) != (pass == 1)) continue;
+      if (Search3dTier(d.num_points) != pass) continue;
       items += d.num_yaws;
-      if (pass == 0) items_small = items;
     }
+    tier_end[pass] = items;
+  }
   if ((rc = ctx->f3_tie_yaws.Reserve(sizeof(Yaw3Desc) * std::max(items, 1)))) return rc;
   if ((rc = ctx->f3_tie_count.Reserve(sizeof(int32_t) * nt))) return rc;
   if ((rc = ctx->f3_ties.Reserve(sizeof(uint4) * kTieCap3d * static_cast<size_t>(nt)))) return rc;
   Yaw3Desc* tyaws = ctx->f3_tie_yaws.as<Yaw3Desc>();
   int at = 0;
-  for (int pass = 0; pass < 2; ++pass)
+  for (int pass = 0; pass < kSearch3dTiers; ++pass)
     for (int t = 0; t < nt; ++t) {
       const int dp = tied[t];
       const Pair3Desc& d = pdesc[dp];
-      if ((d.num_points > kSmall3dPoints) != (pass == 1)) continue;
+      if (Search3dTier(d.num_points) != pass) continue;
       CSM_HIP(hipMemcpyAsync(tyaws + at, dyaws + d.yaw_begin, sizeof(Yaw3Desc) * d.num_yaws,
                              hipMemcpyDeviceToDevice, st));
       at += d.num_yaws;
@@ -1429,25 +1445,17 @@ int ResolveTies3d(csm_context* ctx, csm_fast3d* const* submaps, const std::vecto
                            sizeof(unsigned long long), hipMemcpyHostToDevice, st));
   }
   CSM_HIP(hipMemsetAsync(ctx->f3_tie_count.ptr, 0, sizeof(int32_t) * nt, st));
-  CSM_HIP(hipMemsetAsync(ctx->f3_counter.ptr, 0, 8, st));
+  CSM_HIP(hipMemsetAsync(ctx->f3_counter.ptr, 0, 4 * kSearch3dTiers, st));
   unsigned* dcounter = ctx->f3_counter.as<unsigned>();
-  if (items_small > 0)
-    CSM_HIP(LaunchFast3dSearch(false, std::max(1, std::min(items_small, ctx->num_cus * kSearch3dBlocksPerCu)),
-                               st, dsub, dpairs, tyaws, 0, items_small, ctx->f3_points.as<float>(),
-                               ctx->f3_low_points.as<float>(), dcounter,
-                               ctx->f3_best.as<unsigned long long>(), ctx->f3_status.as<int32_t>(),
-                               nullptr, ctx->f3_spill.as<int4>(),
-                               ctx->f3_best_hi.as<unsigned long long>(), ctx->f3_ties.as<uint4>(),
-                               ctx->f3_tie_count.as<int32_t>()));
-  if (items > items_small)
-    CSM_HIP(LaunchFast3dSearch(true, std::max(1, std::min(items - items_small,
-                                                          ctx->num_cus * kSearch3dBlocksPerCuLarge)),
-                               st, dsub, dpairs, tyaws, items_small, items - items_small,
-                               ctx->f3_points.as<float>(), ctx->f3_low_points.as<float>(),
-                               dcounter + 1, ctx->f3_best.as<unsigned long long>(),
-                               ctx->f3_status.as<int32_t>(), nullptr, ctx->f3_spill.as<int4>(),
-                               ctx->f3_best_hi.as<unsigned long long>(), ctx->f3_ties.as<uint4>(),
-                               ctx->f3_tie_count.as<int32_t>()));
+  for (int tier = 0, b = 0; tier < kSearch3dTiers; b = tier_end[tier++])
+    if (tier_end[tier] > b)
+      CSM_HIP(LaunchFast3dSearch(tier, SearchGrid3(ctx, tier, tier_end[tier] - b), st, dsub, dpairs,
+                                 tyaws, b, tier_end[tier] - b, ctx->f3_points.as<float>(),
+                                 ctx->f3_low_points.as<float>(), dcounter + tier,
+                                 ctx->f3_best.as<unsigned long long>(), ctx->f3_status.as<int32_t>(),
+                                 nullptr, ctx->f3_spill.as<int4>(),
+                                 ctx->f3_best_hi.as<unsigned long long>(), ctx->f3_ties.as<uint4>(),
+                                 ctx->f3_tie_count.as<int32_t>()));
   std::vector<int32_t> counts(nt), stat2(np);
   std::vector<uint4> leaves_all(static_cast<size_t>(kTieCap3d) * nt);
   CSM_HIP(hipMemcpyAsync(counts.data(), ctx->f3_tie_count.ptr, sizeof(int32_t) * nt,
@@ -1953,8 +1961,8 @@ int MatchBatch3(csm_context* ctx, csm_fast3d* const* submaps, int32_t num_submap
   int ny = 0;
   // Pairs whose cloud fits the small-cloud build first, then the rest: two
   // launches over the two item ranges.
-  int ny_small = 0;
-  for (int pass = 0; pass < 2; ++pass)
+  int tier_end[kSearch3dTiers] = {};
+  for (int pass = 0; pass < kSearch3dTiers; ++pass) {
   for (int64_t i = 0; i < num_pairs; ++i) {
     if (results[i].status != CSM_NO_MATCH) continue;
     if (prep[i].status != CSM_OK) {
@@ -1962,7 +1970,7 @@ int MatchBatch3(csm_context* ctx, csm_fast3d* const* submaps, int32_t num_submap
       continue;
     }
     if (pairs[i].min_score >= 1.f || nodes[pairs[i].node].num_high_resolution == 0) continue;
-    if ((nodes[pairs[i].node].num_high_resolution > kSmall3dPoints) != (pass == 1)) continue;
+    if (Search3dTier(nodes[pairs[i].node].num_high_resolution) != pass) continue;
     Pair3Desc d = prep[i].desc;
     d.submap = pairs[i].submap;
     d.point_offset = hoff[pairs[i].node];
@@ -1972,7 +1980,8 @@ int MatchBatch3(csm_context* ctx, csm_fast3d* const* submaps, int32_t num_submap
     ny += d.num_yaws;
     pdesc.push_back(d);
     pair_of.push_back(i);
-    if (pass == 0) ny_small = ny;
+  }
+  tier_end[pass] = ny;
   }
   const int np = static_cast<int>(pdesc.size());
   hipStream_t st = ctx->stream;
@@ -1989,14 +1998,14 @@ int MatchBatch3(csm_context* ctx, csm_fast3d* const* submaps, int32_t num_submap
   if ((rc = ctx->f3_tie_count.Reserve(sizeof(int32_t)))) return rc;
   if ((rc = ctx->f3_ties.Reserve(sizeof(uint4)))) return rc;
   if ((rc = ctx->f3_status.Reserve(sizeof(int32_t) * np))) return rc;
-  if ((rc = ctx->f3_counter.Reserve(8 + 16 * sizeof(unsigned long long)))) return rc;
+  if ((rc = ctx->f3_counter.Reserve(16 + 16 * sizeof(unsigned long long)))) return rc;
   Pair3Desc* dpairs = ctx->f3_pairs.as<Pair3Desc>();
   Submap3Desc* dsub = reinterpret_cast<Submap3Desc*>(dpairs + np);
   unsigned long long* dbest = ctx->f3_best.as<unsigned long long>();
   float* dlow = reinterpret_cast<float*>(dbest + np);
   unsigned* dcounter = ctx->f3_counter.as<unsigned>();
   unsigned long long* dstats = reinterpret_cast<unsigned long long*>(
-      reinterpret_cast<char*>(ctx->f3_counter.ptr) + 8);
+      reinterpret_cast<char*>(ctx->f3_counter.ptr) + 16);
   // Pair and submap descriptors (adjacent on the device) in one pinned
   // upload; the yaw-build records follow in the same staging buffer.
   const size_t desc_bytes = sizeof(Pair3Desc) * np + sizeof(Submap3Desc) * num_submaps;
@@ -2103,35 +2112,21 @@ int MatchBatch3(csm_context* ctx, csm_fast3d* const* submaps, int32_t num_submap
     z.ptr[2] = ctx->f3_status.ptr;
     z.bytes[2] = sizeof(int32_t) * np;
     z.ptr[3] = ctx->f3_counter.ptr;
-    z.bytes[3] = 8 + 16 * sizeof(unsigned long long);
+    z.bytes[3] = 16 + 16 * sizeof(unsigned long long);
     z.n = 4;
     CSM_HIP(LaunchSegments(z, nullptr, st));
   }
   lap(4);
-  {
-    const size_t wgs = static_cast<size_t>(ctx->num_cus) *
-                       std::max(kSearch3dBlocksPerCu, kSearch3dBlocksPerCuLarge);
-    if ((rc = ctx->f3_spill.Reserve(sizeof(int4) * kSpill3d * wgs))) return rc;
-  }
+  if ((rc = ctx->f3_spill.Reserve(SpillBytes3(ctx)))) return rc;
   if (ctx->timing) CSM_HIP(hipEventRecord(ctx->ev0, st));
-  if (ny_small > 0) {
-    const int grid = std::max(1, std::min(ny_small, ctx->num_cus * kSearch3dBlocksPerCu));
-    CSM_HIP(LaunchFast3dSearch(false, grid, st, dsub, dpairs, ctx->f3_yaws.as<Yaw3Desc>(), 0,
-                               ny_small, ctx->f3_points.as<float>(),
-                               ctx->f3_low_points.as<float>(), dcounter, dbest,
-                               ctx->f3_status.as<int32_t>(), dstats, ctx->f3_spill.as<int4>(),
-                               ctx->f3_best_hi.as<unsigned long long>(), ctx->f3_ties.as<uint4>(),
-                               ctx->f3_tie_count.as<int32_t>()));
-  }
-  if (ny > ny_small) {
-    const int grid = std::max(1, std::min(ny - ny_small, ctx->num_cus * kSearch3dBlocksPerCuLarge));
-    CSM_HIP(LaunchFast3dSearch(true, grid, st, dsub, dpairs, ctx->f3_yaws.as<Yaw3Desc>(), ny_small,
-                               ny - ny_small, ctx->f3_points.as<float>(),
-                               ctx->f3_low_points.as<float>(), dcounter + 1, dbest,
-                               ctx->f3_status.as<int32_t>(), dstats, ctx->f3_spill.as<int4>(),
-                               ctx->f3_best_hi.as<unsigned long long>(), ctx->f3_ties.as<uint4>(),
-                               ctx->f3_tie_count.as<int32_t>()));
-  }
+  for (int tier = 0, b = 0; tier < kSearch3dTiers; b = tier_end[tier++])
+    if (tier_end[tier] > b)
+      CSM_HIP(LaunchFast3dSearch(tier, SearchGrid3(ctx, tier, tier_end[tier] - b), st, dsub, dpairs,
+                                 ctx->f3_yaws.as<Yaw3Desc>(), b, tier_end[tier] - b,
+                                 ctx->f3_points.as<float>(), ctx->f3_low_points.as<float>(),
+                                 dcounter + tier, dbest, ctx->f3_status.as<int32_t>(), dstats,
+                                 ctx->f3_spill.as<int4>(), ctx->f3_best_hi.as<unsigned long long>(),
+                                 ctx->f3_ties.as<uint4>(), ctx->f3_tie_count.as<int32_t>()));
   if (ctx->timing) CSM_HIP(hipEventRecord(ctx->ev1, st));
   std::vector<unsigned long long> keys(np), keys_hi(np);
   std::vector<float> lows(np);

@@ -947,7 +947,7 @@ __global__ void pad_prob_brick_zfast(const float* __restrict__ prob, Brick3 gb, 
 // passes min_low_resolution_score (:384-401). Each pair keeps one 64-bit key
 // sum << 42 | ~leaf_id, updated with atomicMax.
 
-template <int kPts>
+template <int kPts, int kStack>
 struct F3SharedT {
   // The discretized cloud: full-resolution cells (int16 x, y, z), or — once
   // roots are scored from the cell list — packed words relative to an origin
@@ -962,9 +962,9 @@ struct F3SharedT {
   int rel_min[3], rel_max[3];
   int fmin[3], fmax[3];    // full-resolution cloud bounds
   int packed;
-  int16_t sx[kStack3d], sy[kStack3d], sz[kStack3d];
-  int8_t sd[kStack3d];
-  int ssum[kStack3d];
+  int16_t sx[kStack], sy[kStack], sz[kStack];
+  int8_t sd[kStack];
+  int ssum[kStack];
   float lr[kSearch3dThreads];
   alignas(16) uint8_t top[kTopLds3d];
   int bn_x[kBatch3d], bn_y[kBatch3d], bn_z[kBatch3d], bn_d[kBatch3d];
@@ -1061,8 +1061,10 @@ __device__ float LowResScore(Shared& sh, const Submap3Desc& sm, const float* __r
 #endif
 
 // kPts: cloud capacity in LDS; kWaves: waves per SIMD the kernel is built
-// for (= workgroups per CU with 256 threads).
-template <int kPts, int kWaves>
+// for (= workgroups per CU with 256 threads); kStack: DFS stack entries in
+// LDS (the rest of kDfsCap3d spills to global memory); kInflight: octet
+// loads a lane keeps in flight (16, 12, 8 or 4).
+template <int kPts, int kWaves, int kStack, int kInflight>
 __global__ void __launch_bounds__(kSearch3dThreads) __attribute__((amdgpu_waves_per_eu(kWaves, kWaves)))
 fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restrict__ pairs,
               const Yaw3Desc* __restrict__ yaws, int item_begin, int num_items,
@@ -1072,13 +1074,14 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
               unsigned long long* __restrict__ stats, int4* __restrict__ spill_base,
               unsigned long long* __restrict__ best_hi, uint4* __restrict__ ties,
               int32_t* __restrict__ tie_count) {
-  __shared__ F3SharedT<kPts> sh;
+  static_assert(kInflight == 16 || kInflight == 12 || kInflight == 8 || kInflight == 4, "");
+  __shared__ F3SharedT<kPts, kStack> sh;
   const int tid = threadIdx.x;
   unsigned long long lookups = 0, root_lookups = 0;
   F3_PROF_DECL;
-  // DFS stack entries past kStack3d live in this workgroup's spill region
+  // DFS stack entries past kStack live in this workgroup's spill region
   // (global memory, written and read only by this workgroup's waves).
-  int4* spill = spill_base + static_cast<size_t>(blockIdx.x) * kSpill3d;
+  int4* spill = spill_base + static_cast<size_t>(blockIdx.x) * (kDfsCap3d - kStack);
   if (tid == 0) {
     sh.cached_submap = -1;
     sh.high_water = 0;
@@ -1205,7 +1208,7 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
     // the empty stack sums), compacted to a list when box and list fit.
     const int gbx = sh.rmax[0] - sh.rmin[0] + 1, gby = sh.rmax[1] - sh.rmin[1] + 1,
               gbz = sh.rmax[2] - sh.rmin[2] + 1;
-    const bool use_cells = n > 0 && static_cast<int64_t>(gbx) * gby * gbz <= kStack3d &&
+    const bool use_cells = n > 0 && static_cast<int64_t>(gbx) * gby * gbz <= kStack &&
                            sh.rmin[0] >= -1024 && sh.rmax[0] < 1024 && sh.rmin[1] >= -1024 &&
                            sh.rmax[1] < 1024 && sh.rmin[2] >= -512 && sh.rmax[2] < 512;
     if (use_cells) {
@@ -1423,8 +1426,8 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
           bool keep = false;
           int4 e = make_int4(0, 0, 0, 0);
           if (at >= 0) {
-            e = at < kStack3d ? make_int4(sh.sx[at], sh.sy[at], (sh.sz[at] & 0xffff) | (sh.sd[at] << 16), sh.ssum[at])
-                              : spill[at - kStack3d];
+            e = at < kStack ? make_int4(sh.sx[at], sh.sy[at], (sh.sz[at] & 0xffff) | (sh.sd[at] << 16), sh.ssum[at])
+                            : spill[at - kStack];
             s = e.w;
             keep = s >= best_sum && s >= pd.min_sum && s > tie_sum;
           }
@@ -1514,8 +1517,8 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
           a6 = __builtin_amdgcn_udot4(hi, 0x00010000u, a6, false);
           a7 = __builtin_amdgcn_udot4(hi, 0x01000000u, a7, false);
         };
-        // A lane's points in flight at once, 16 per round. A load past the
-        // cloud still costs texture-path cycles (it reads the out-of-range
+        // A lane's points in flight at once, kInflight per round. A load past
+        // the cloud still costs texture-path cycles (it reads the out-of-range
         // offset and adds 0), so the last round is cut to the 4, 8, 12 or 16
         // loads that cover the cloud's nu = ceil(n / 16) points per lane
         // (wave-uniform: every node of the item has the same cloud): a
@@ -1532,14 +1535,14 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
             for (int u = 0; u < K; ++u) accumulate(v[u]);
             u0 += K;
           };
-          while (nu - u0 >= 16) issue(std::integral_constant<int, 16>{});
-          const int left = nu - u0;
-          if (left > 12)
-            issue(std::integral_constant<int, 16>{});
-          else if (left > 8)
-            issue(std::integral_constant<int, 12>{});
-          else if (left > 4)
-            issue(std::integral_constant<int, 8>{});
+          while (nu - u0 >= kInflight) issue(std::integral_constant<int, kInflight>{});
+          const int left = nu - u0;  // < kInflight
+          if (kInflight > 12 && left > 12)
+            issue(std::integral_constant<int, (kInflight > 12 ? 16 : 4)>{});
+          else if (kInflight > 8 && left > 8)
+            issue(std::integral_constant<int, (kInflight > 8 ? 12 : 4)>{});
+          else if (kInflight > 4 && left > 4)
+            issue(std::integral_constant<int, (kInflight > 4 ? 8 : 4)>{});
           else if (left > 0)
             issue(std::integral_constant<int, 4>{});
         };
@@ -1641,19 +1644,19 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
           if (k == 0 && m > 0) {
             base = atomicAdd(&sh.sp, m);
             atomicMax(&sh.high_water, base + m);
-            if (base + m > kStack3d + kSpill3d) sh.error = 1;  // flagged after the batch
+            if (base + m > kDfsCap3d) sh.error = 1;  // flagged after the batch
           }
           base = __shfl(base, (tid & 63) & ~(kLanes - 1), 64);
           const int at = base + rank;
-          if (pres && my >= pd.min_sum && my >= best_sum && my > tie_sum && at < kStack3d + kSpill3d) {
-            if (at < kStack3d) {
+          if (pres && my >= pd.min_sum && my >= best_sum && my > tie_sum && at < kDfsCap3d) {
+            if (at < kStack) {
               sh.sx[at] = static_cast<int16_t>(cxk);
               sh.sy[at] = static_cast<int16_t>(cyk);
               sh.sz[at] = static_cast<int16_t>(czk);
               sh.sd[at] = static_cast<int8_t>(cd);
               sh.ssum[at] = my;
             } else {
-              spill[at - kStack3d] = make_int4(cxk, cyk, (czk & 0xffff) | (cd << 16), my);
+              spill[at - kStack] = make_int4(cxk, cyk, (czk & 0xffff) | (cd << 16), my);
             }
           }
         } else if (pres && my >= pd.min_sum) {
@@ -2040,7 +2043,7 @@ __global__ void __launch_bounds__(kSearch3dThreads)
 fast3d_finalize(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restrict__ pairs,
                 const Yaw3Desc* __restrict__ yaws, const float* __restrict__ low_points,
                 const unsigned long long* __restrict__ best, float* __restrict__ low_score) {
-  __shared__ F3SharedT<kSmall3dPoints> sh;
+  __shared__ F3SharedT<kSmall3dPoints, kStack3d> sh;
   const int p = blockIdx.x;
   const unsigned long long key = best[p];
   const Pair3Desc pd = pairs[p];
@@ -2539,22 +2542,28 @@ hipError_t LaunchRt3dScore3(int num_rot, hipStream_t st, const float* pad, const
   return hipGetLastError();
 }
 
-hipError_t LaunchFast3dSearch(bool large, int grid, hipStream_t st, const Submap3Desc* submaps,
+hipError_t LaunchFast3dSearch(int tier, int grid, hipStream_t st, const Submap3Desc* submaps,
                               const Pair3Desc* pairs, const Yaw3Desc* yaws, int item_begin,
                               int num_items, const float* points, const float* low_points,
                               unsigned* counter, unsigned long long* best, int32_t* status,
                               unsigned long long* stats, int4* spill, unsigned long long* best_hi,
                               uint4* ties, int32_t* tie_count) {
-  if (large)
-    hipLaunchKernelGGL((fast3d_search<kMax3dPoints, kSearch3dBlocksPerCuLarge>), dim3(grid),
-                       dim3(kSearch3dThreads), 0, st, submaps, pairs, yaws, item_begin, num_items,
-                       points, low_points, counter, best, status, stats, spill, best_hi, ties,
-                       tie_count);
+  if (tier == 0)
+    hipLaunchKernelGGL((fast3d_search<kTiny3dPoints, kSearch3dBlocksPerCuTiny, kTinyStack3d,
+                                      kTinyInflight3d>),
+                       dim3(grid), dim3(kSearch3dThreads), 0, st, submaps, pairs, yaws, item_begin,
+                       num_items, points, low_points, counter, best, status, stats, spill, best_hi,
+                       ties, tie_count);
+  else if (tier == 1)
+    hipLaunchKernelGGL((fast3d_search<kSmall3dPoints, kSearch3dBlocksPerCu, kStack3d, 16>),
+                       dim3(grid), dim3(kSearch3dThreads), 0, st, submaps, pairs, yaws, item_begin,
+                       num_items, points, low_points, counter, best, status, stats, spill, best_hi,
+                       ties, tie_count);
   else
-    hipLaunchKernelGGL((fast3d_search<kSmall3dPoints, kSearch3dBlocksPerCu>), dim3(grid),
-                       dim3(kSearch3dThreads), 0, st, submaps, pairs, yaws, item_begin, num_items,
-                       points, low_points, counter, best, status, stats, spill, best_hi, ties,
-                       tie_count);
+    hipLaunchKernelGGL((fast3d_search<kMax3dPoints, kSearch3dBlocksPerCuLarge, kStack3d, 16>),
+                       dim3(grid), dim3(kSearch3dThreads), 0, st, submaps, pairs, yaws, item_begin,
+                       num_items, points, low_points, counter, best, status, stats, spill, best_hi,
+                       ties, tie_count);
   return hipGetLastError();
 }
 

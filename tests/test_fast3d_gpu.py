@@ -516,6 +516,64 @@ def test_large_clouds_match_oracle(csm, oracle, world3d):
     assert res[3].status == csm.CSM_ERANGE
 
 
+def test_search_tiers_match_oracle(csm, oracle, world3d):
+    """One batch over the three search builds (Search3dTier: <= 512 points,
+    <= 2048, <= 8192; each its own launch over its item range) against the
+    oracle and against single calls, clouds listed largest first."""
+    w = world3d
+    o = csm.FastCorrelativeScanMatcherOptions3D()
+    s = 0
+    oh, ol = oracle.hybrid_grid(w.high_resolution), oracle.hybrid_grid(w.low_resolution)
+    oh.set_values(*w.high_cells[s])
+    ol.set_values(*w.low_cells[s])
+    om = oracle.fast3d(oh, ol, w.submap_hist[s], opt_tuple(o))
+    gm = csm.FastCorrelativeScanMatcher3D(csm.HybridGrid(w.high_resolution, *w.high_cells[s]),
+                                          csm.HybridGrid(w.low_resolution, *w.low_cells[s]),
+                                          w.submap_hist[s], o)
+    c = int(w.submap_nodes[s])
+    small = w.node(c)
+    pts = small.high_resolution_point_cloud
+    assert len(pts) <= 512
+    rng = np.random.default_rng(11)
+
+    def grown(target):
+        reps = target // len(pts) + 1
+        cloud = np.concatenate([pts + rng.uniform(-0.03, 0.03, pts.shape).astype(np.float32)
+                                for _ in range(reps)]).astype(np.float32)
+        return csm.NodeData3D(cloud, small.low_resolution_point_cloud,
+                              small.rotational_scan_matcher_histogram, small.gravity_alignment)
+
+    mid, big = grown(900), grown(2300)
+    assert 512 < len(mid.high_resolution_point_cloud) <= 2048
+    assert 2048 < len(big.high_resolution_point_cloud) <= 8192
+    nodes = [big, mid, small]
+    rot = w.node_rotation(c)
+    truth = w.node_in_submap(c, s)
+    init = ((truth[0][0] + 0.3, truth[0][1] - 0.2, 0.1), truth[1])
+    ident = ((0, 0, 0), (1, 0, 0, 0))
+    pairs = [(0, n, full, 0.55, ((0, 0, 0), rot) if full else init, ident)
+             for n in range(3) for full in (True, False)]
+    res = csm.match_batch_3d([gm], nodes, pairs)
+    matched = 0
+    for (sub, n, full, ms, npose, spose), r in zip(pairs, res):
+        node = nodes[n]
+        if full:
+            ref = om.match_full_submap(npose[1], spose[1], node, ms)
+            single = gm.MatchFullSubmap(npose[1], spose[1], node, ms)
+        else:
+            ref = om.match(npose, spose, node, ms)
+            single = gm.Match(npose, spose, node, ms)
+        assert assert_same_result(single, ref, om, full, npose[1] if full else npose,
+                                  spose[1] if full else spose, node,
+                                  o.min_low_resolution_score) in ("exact", "tie", "nomatch")
+        matched += single is not None
+        assert (single is not None) == (r.status == csm.CSM_OK), (n, full)
+        if single is not None:
+            assert np.float32(single.score) == np.float32(r.score)
+            assert single.pose_estimate == r.pose.as_tuple()
+    assert matched >= 3
+
+
 def _qmul(a, b):
     return (a[0] * b[0] - a[1] * b[1] - a[2] * b[2] - a[3] * b[3],
             a[0] * b[1] + a[1] * b[0] + a[2] * b[3] - a[3] * b[2],
