@@ -10,7 +10,7 @@ namespace csm {
 
 constexpr int kMaxLevels3d = 12;
 constexpr int kExtraLevels3d = 2;       // coarser levels above the reference's stack (roots only)
-constexpr int kRootTarget3d = 512;       // a pair's roots start at the lowest level with <= this many
+constexpr int kRootTarget3d = 64;        // a pair's roots start at the lowest level with <= this many
 constexpr int kTiny3dPoints = 512;       // cloud capacity (LDS) of the tiny-cloud build (24 KiB, 5 per CU)
 constexpr int kSmall3dPoints = 2048;      // cloud capacity (LDS) of the 4-workgroups-per-CU build
 constexpr int kMax3dPoints = 8192;        // of the large-cloud build (2 per CU); more: CSM_ERANGE
