@@ -10,6 +10,15 @@ namespace csm {
 
 constexpr int kRt3dThreads = 384;  // translations per RTCSM3D launch
 
+// Pyramid row builds (kernels3d.hip BrickRows): bytes per staged source row
+// of W positions (the dwords holding them, which may start up to 3 bytes
+// early), and the dynamic LDS of a workgroup (4 source rows, 16 for a
+// half-resolution level).
+constexpr int BrickRowsPitch(int W) { return ((W + 3) & ~3) + 4; }
+constexpr int BrickRowsLds(int nx, int h, bool half) {
+  return (half ? 16 : 4) * BrickRowsPitch(half ? 2 * nx + h : nx + h);
+}
+
 hipError_t LaunchBrickFromValues(const uint16_t* values, int64_t n, const float* ptab,
                                  const uint8_t* qtab, float* prob, uint8_t* level0,
                                  hipStream_t st);

@@ -944,9 +944,7 @@ int BuildFast3d(csm_context* ctx, csm_fast3d* const* ms, const Fast3dPlan* plans
   int depth = 0;
   for (int i = 0; i < count; ++i) depth = std::max(depth, plans[i].depth);
   std::vector<std::vector<RowJob3>> level_jobs(depth), oct_jobs(depth);
-  auto row_lds = [](const Brick3& ob, int h, bool half) {
-    return (half ? 16 : 4) * ((half ? 2 * ob.nx + h : ob.nx + h) + 3 & ~3);
-  };
+  auto row_lds = [](const Brick3& ob, int h, bool half) { return BrickRowsLds(ob.nx, h, half); };
   for (int i = 0; i < count; ++i) {
     const Fast3dPlan& pl = plans[i];
     if (pl.empty) continue;

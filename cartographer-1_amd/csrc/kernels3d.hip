@@ -202,7 +202,8 @@ __device__ __forceinline__ void BrickRows(const uint8_t* __restrict__ src, Brick
                                           uint8_t* rows) {
   static_assert(!(kOctet && kHalf), "octets are built at the level's own resolution");
   constexpr int kRows = kHalf ? 16 : 4;
-  const int W = kHalf ? 2 * ob.nx + h : ob.nx + h, pitch = (W + 3) & ~3;
+  const int W = kHalf ? 2 * ob.nx + h : ob.nx + h, pitch = BrickRowsPitch(W);
+  uint32_t* roww = reinterpret_cast<uint32_t*>(rows);
   const int src_bytes = sb.nx * sb.ny * sb.nz;
   // Up to 3 bytes past the brick are read (levels are 256-byte aligned in
   // their buffer) and masked below.
@@ -215,6 +216,11 @@ __device__ __forceinline__ void BrickRows(const uint8_t* __restrict__ src, Brick
       const int ly = row % ob.ny, lz = row / ob.ny;
       const int y = ly + ob.oy, z = lz + ob.oz;
       __syncthreads();  // the previous row's reads are done
+      // Source rows staged as the dwords that hold them (a dword store per
+      // loaded dword; bytes outside the source row zeroed): position pos of
+      // row r is byte roff[r] + pos.
+      int roff[kRows];
+#pragma unroll
       for (int r = 0; r < kRows; ++r) {
         int yy, zz;
         if constexpr (kHalf) {
@@ -228,20 +234,20 @@ __device__ __forceinline__ void BrickRows(const uint8_t* __restrict__ src, Brick
         zz -= sb.oz;
         const bool row_ok = static_cast<unsigned>(yy) < static_cast<unsigned>(sb.ny) &&
                             static_cast<unsigned>(zz) < static_cast<unsigned>(sb.nz);
-        const int b0 = (row_ok ? (zz * sb.ny + yy) * sb.nx : 0) + xs;  // byte of position 0
+        const int rs0 = row_ok ? (zz * sb.ny + yy) * sb.nx : 0;  // byte of source x = 0
+        const int b0 = rs0 + xs;                                  // byte of position 0
         const int a0 = b0 & ~3;
+        roff[r] = r * pitch + (b0 - a0);
         const int nwords = (W + (b0 - a0) + 3) >> 2;
         for (int i = threadIdx.x; i < nwords; i += kRowThreads) {
           const int a = a0 + 4 * i;
-          const uint32_t w = row_ok ? __builtin_amdgcn_raw_buffer_load_b32(rs, a, 0, 0) : 0u;
+          uint32_t w = row_ok ? __builtin_amdgcn_raw_buffer_load_b32(rs, a, 0, 0) : 0u;
+          if (a < rs0 || a + 4 > rs0 + sb.nx) {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int pos = a + j - b0;
-            if (pos >= 0 && pos < W) {
-              const bool in = row_ok && static_cast<unsigned>(xs + pos) < static_cast<unsigned>(sb.nx);
-              rows[r * pitch + pos] = in ? static_cast<uint8_t>(w >> (8 * j)) : 0;
-            }
+            for (int j = 0; j < 4; ++j)
+              if (static_cast<unsigned>(a + j - rs0) >= static_cast<unsigned>(sb.nx)) w &= ~(0xffu << (8 * j));
           }
+          roww[r * (pitch >> 2) + i] = w;
         }
       }
       __syncthreads();
@@ -251,14 +257,14 @@ __device__ __forceinline__ void BrickRows(const uint8_t* __restrict__ src, Brick
           uint64_t v = 0;
 #pragma unroll
           for (int k = 0; k < 8; ++k)
-            v |= static_cast<uint64_t>(rows[(k >> 1) * pitch + lx + h * (k & 1)]) << (8 * k);
+            v |= static_cast<uint64_t>(rows[roff[k >> 1] + lx + h * (k & 1)]) << (8 * k);
           static_cast<uint64_t*>(out)[base + lx] = v;
         } else if constexpr (kHalf) {
           unsigned v = 0;
           const int p = 2 * lx;
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
-            const uint8_t* row = rows + r * pitch + p;
+            const uint8_t* row = rows + roff[r] + p;
             v = max(v, max(max(static_cast<unsigned>(row[0]), static_cast<unsigned>(row[1])),
                            max(static_cast<unsigned>(row[h]), static_cast<unsigned>(row[h + 1]))));
           }
@@ -267,7 +273,7 @@ __device__ __forceinline__ void BrickRows(const uint8_t* __restrict__ src, Brick
           unsigned v = 0;
 #pragma unroll
           for (int k = 0; k < 8; ++k)
-            v = max(v, static_cast<unsigned>(rows[(k >> 1) * pitch + lx + h * (k & 1)]));
+            v = max(v, static_cast<unsigned>(rows[roff[k >> 1] + lx + h * (k & 1)]));
           static_cast<uint8_t*>(out)[base + lx] = static_cast<uint8_t>(v);
         }
       }
@@ -298,9 +304,19 @@ brick_rows_batch(const RowJob3* __restrict__ jobs) {
 __global__ void __launch_bounds__(256)
 values_to_level0_batch(const ValueJob3* __restrict__ jobs, const uint8_t* __restrict__ qtab) {
   const ValueJob3 jb = jobs[blockIdx.y];
-  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < jb.n;
-       i += static_cast<int64_t>(gridDim.x) * 256)
-    jb.level0[i] = qtab[jb.values[i] & 0x7fff];
+  // 4 cells per lane and step: an 8-byte load, a dword store (both bricks
+  // 256-byte aligned); the last < 4 cells one each.
+  const int64_t n4 = jb.n / 4;
+  const uint2* v4 = reinterpret_cast<const uint2*>(jb.values);
+  uint32_t* o4 = reinterpret_cast<uint32_t*>(jb.level0);
+  const int64_t t = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  for (int64_t i = t; i < n4; i += static_cast<int64_t>(gridDim.x) * 256) {
+    const uint2 v = v4[i];
+    o4[i] = static_cast<uint32_t>(qtab[v.x & 0x7fff]) | (static_cast<uint32_t>(qtab[(v.x >> 16) & 0x7fff]) << 8) |
+            (static_cast<uint32_t>(qtab[v.y & 0x7fff]) << 16) |
+            (static_cast<uint32_t>(qtab[(v.y >> 16) & 0x7fff]) << 24);
+  }
+  if (t < jb.n - 4 * n4) jb.level0[4 * n4 + t] = qtab[jb.values[4 * n4 + t] & 0x7fff];
 }
 
 // ------------------------------------------------------------- RTCSM3D ----
@@ -2378,8 +2394,7 @@ hipError_t LaunchBrickFromValues(const uint16_t* values, int64_t n, const float*
 hipError_t LaunchLevelGather(const uint8_t* prev, const Brick3& pb, uint8_t* out, const Brick3& ob,
                              int shift, int half, hipStream_t st) {
   if (ob.nx <= 0 || ob.ny <= 0 || ob.nz <= 0) return hipSuccess;
-  const size_t row_lds = half ? 16 * static_cast<size_t>((2 * ob.nx + shift + 3) & ~3)
-                              : 4 * static_cast<size_t>((ob.nx + shift + 3) & ~3);
+  const size_t row_lds = BrickRowsLds(ob.nx, shift, half != 0);
   if (row_lds <= 65536) {
     const dim3 grid(static_cast<unsigned>(std::min<int64_t>(static_cast<int64_t>(ob.ny) * ob.nz, 1 << 20)));
     if (half)
@@ -2400,7 +2415,7 @@ hipError_t LaunchLevelGather(const uint8_t* prev, const Brick3& pb, uint8_t* out
 hipError_t LaunchOctetBuild(const uint8_t* level, const Brick3& lb, int h, uint64_t* out,
                             const Brick3& ob, hipStream_t st) {
   if (ob.nx <= 0 || ob.ny <= 0 || ob.nz <= 0) return hipSuccess;
-  const size_t row_lds = 4 * static_cast<size_t>((ob.nx + h + 3) & ~3);
+  const size_t row_lds = BrickRowsLds(ob.nx, h, false);
   if (row_lds <= 65536) {
     hipLaunchKernelGGL((brick_rows<true, false>),
                        dim3(static_cast<unsigned>(std::min<int64_t>(static_cast<int64_t>(ob.ny) * ob.nz, 1 << 20))),
@@ -2432,7 +2447,7 @@ hipError_t LaunchValuesToLevel0Batch(const ValueJob3* jobs, int num_jobs, int64_
                                      const uint8_t* qtab, hipStream_t st) {
   if (num_jobs <= 0 || max_n <= 0) return hipSuccess;
   if (num_jobs > 65535) return hipErrorInvalidValue;
-  const dim3 grid(static_cast<unsigned>(std::min<int64_t>((max_n + 255) / 256, 1 << 14)),
+  const dim3 grid(static_cast<unsigned>(std::min<int64_t>((max_n / 4 + 256) / 256, 1 << 14)),
                   static_cast<unsigned>(num_jobs));
   hipLaunchKernelGGL(values_to_level0_batch, grid, dim3(256), 0, st, jobs, qtab);
   return hipGetLastError();
