@@ -18,7 +18,8 @@ constexpr int kTopLds3d = 6 * 1024;       // top pyramid level cached in LDS whe
 constexpr int kRootChunk3d = 128;         // roots fed to the DFS stack at a time
 constexpr int kRootScore3d = 256;         // roots scored at a time (one per lane)
 constexpr int kTopCells3d = 512;          // distinct top-level cells of a cloud (LDS list)
-constexpr int kBatch3d = 16;              // DFS nodes scored per step (16 lanes each)
+constexpr int kBatch3d = 16;              // DFS nodes scored per step (16 lanes each; small, large builds)
+constexpr int kTinyBatch3d = 32;          // of the tiny-cloud build (8 lanes each)
 constexpr int kMax3dTop = 1 << 20;        // top-level candidates per yaw
 constexpr int kTieCap3d = 4096;           // tied leaves recorded per pair (collect search)
 constexpr int kWalkStack3d = 128;         // ordered-walk stack: 1 + 7 x depth entries at most

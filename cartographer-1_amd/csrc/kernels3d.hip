@@ -963,7 +963,7 @@ __global__ void pad_prob_brick_zfast(const float* __restrict__ prob, Brick3 gb, 
 // passes min_low_resolution_score (:384-401). Each pair keeps one 64-bit key
 // sum << 42 | ~leaf_id, updated with atomicMax.
 
-template <int kPts, int kStack>
+template <int kPts, int kStack, int kBatch>
 struct F3SharedT {
   // The discretized cloud: full-resolution cells (int16 x, y, z), or — once
   // roots are scored from the cell list — packed words relative to an origin
@@ -983,9 +983,9 @@ struct F3SharedT {
   int ssum[kStack];
   float lr[kSearch3dThreads];
   alignas(16) uint8_t top[kTopLds3d];
-  int bn_x[kBatch3d], bn_y[kBatch3d], bn_z[kBatch3d], bn_d[kBatch3d];
-  unsigned long long leaf_keys[8 * kBatch3d];
-  int leaf_x[8 * kBatch3d], leaf_y[8 * kBatch3d], leaf_z[8 * kBatch3d];
+  int bn_x[kBatch], bn_y[kBatch], bn_z[kBatch], bn_d[kBatch];
+  unsigned long long leaf_keys[8 * kBatch];
+  int leaf_x[8 * kBatch], leaf_y[8 * kBatch], leaf_z[8 * kBatch];
   int rmin[3], rmax[3];  // bounds of the cloud's cells at the top level
   int16_t rbx[kRootScore3d], rby[kRootScore3d], rbz[kRootScore3d];
   int rbs[kRootScore3d];
@@ -1079,8 +1079,9 @@ __device__ float LowResScore(Shared& sh, const Submap3Desc& sm, const float* __r
 // kPts: cloud capacity in LDS; kWaves: waves per SIMD the kernel is built
 // for (= workgroups per CU with 256 threads); kStack: DFS stack entries in
 // LDS (the rest of kDfsCap3d spills to global memory); kInflight: octet
-// loads a lane keeps in flight (16, 12, 8 or 4).
-template <int kPts, int kWaves, int kStack, int kInflight>
+// loads a lane keeps in flight (16, 12, 8 or 4); kBatch: DFS nodes scored
+// per step (16 or 32: 16 or 8 lanes each).
+template <int kPts, int kWaves, int kStack, int kInflight, int kBatch>
 __global__ void __launch_bounds__(kSearch3dThreads) __attribute__((amdgpu_waves_per_eu(kWaves, kWaves)))
 fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restrict__ pairs,
               const Yaw3Desc* __restrict__ yaws, int item_begin, int num_items,
@@ -1091,7 +1092,7 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
               unsigned long long* __restrict__ best_hi, uint4* __restrict__ ties,
               int32_t* __restrict__ tie_count) {
   static_assert(kInflight == 16 || kInflight == 12 || kInflight == 8 || kInflight == 4, "");
-  __shared__ F3SharedT<kPts, kStack> sh;
+  __shared__ F3SharedT<kPts, kStack, kBatch> sh;
   const int tid = threadIdx.x;
   unsigned long long lookups = 0, root_lookups = 0;
   F3_PROF_DECL;
@@ -1416,11 +1417,11 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
       }
       if (tid == 0) sh.sp = rb_end - k0;
       __syncthreads();
-    // Best-first DFS in batches of up to kBatch3d nodes, kLanes lanes each:
+    // Best-first DFS in batches of up to kBatch nodes, kLanes lanes each:
     // the lanes of a node split the points and score its (up to) 8 children,
     // reduced with shuffles only.
     for (;;) {
-      // Pop up to kBatch3d nodes, skipping pruned ones, 64 entries per step
+      // Pop up to kBatch nodes, skipping pruned ones, 64 entries per step
       // across wave 0 (the same nodes, in the same order, as popping one by
       // one from the top).
       if (tid < 64) {
@@ -1436,7 +1437,7 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
         const bool abandon =
             pd.collect && *reinterpret_cast<volatile int32_t*>(tie_count + pd.collect - 1) > kTieCap3d;
         int sp = abandon ? 0 : sh.sp, m = 0;
-        while (sp > 0 && m < kBatch3d) {
+        while (sp > 0 && m < kBatch) {
           const int at = sp - 1 - tid;
           int s = 0;
           bool keep = false;
@@ -1449,15 +1450,15 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
           }
           const unsigned long long mask = __ballot(keep);
           const int rank = m + __popcll(mask & ((1ull << tid) - 1ull));
-          if (keep && rank < kBatch3d) {
+          if (keep && rank < kBatch) {
             sh.bn_x[rank] = e.x;
             sh.bn_y[rank] = e.y;
             sh.bn_z[rank] = static_cast<int16_t>(e.z & 0xffff);
             sh.bn_d[rank] = e.z >> 16;
           }
-          const unsigned long long last = __ballot(keep && rank == kBatch3d - 1);
+          const unsigned long long last = __ballot(keep && rank == kBatch - 1);
           const int consumed = last ? __ffsll(static_cast<long long>(last)) : min(64, sp);
-          m = min(kBatch3d, m + __popcll(mask));
+          m = min(kBatch, m + __popcll(mask));
           sp -= consumed;
         }
         if (tid == 0) {
@@ -1471,7 +1472,7 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
       __syncthreads();
       const int nb = sh.nbatch;
       if (nb == 0) break;
-      constexpr int kLanes = kSearch3dThreads / kBatch3d;  // lanes per node
+      constexpr int kLanes = kSearch3dThreads / kBatch;  // lanes per node
       const int half = tid / kLanes, hl = tid % kLanes;
       int nc = 0, cd = 0, ox = 0, oy = 0, oz = 0, hw = 0;
       int acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -1623,16 +1624,17 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
         acc[6] = a6;
         acc[7] = a7;
       }
-      // Row (16-lane) sums with DPP: xor 1, xor 2 (quad_perm), then the
-      // half-row and row mirrors; every lane of the row ends with the sum.
-      static_assert(kLanes == 16, "DPP row reduction assumes 16 lanes per node");
+      // Node (8- or 16-lane) sums with DPP: xor 1, xor 2 (quad_perm), then the
+      // half-row mirror (8 lanes) and the row mirror (16); every lane of the
+      // node ends with the sum.
+      static_assert(kLanes == 16 || kLanes == 8, "DPP reduction over 8 or 16 lanes per node");
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         int v = acc[k];
         v += __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
         v += __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
         v += __builtin_amdgcn_update_dpp(0, v, 0x141, 0xF, 0xF, false);  // row_half_mirror
-        v += __builtin_amdgcn_update_dpp(0, v, 0x140, 0xF, 0xF, false);  // row_mirror
+        if (kLanes == 16) v += __builtin_amdgcn_update_dpp(0, v, 0x140, 0xF, 0xF, false);  // row_mirror
         acc[k] = v;
       }
       // Lane k < 8 of a node handles child k: its sum, then its rank among
@@ -2059,7 +2061,7 @@ __global__ void __launch_bounds__(kSearch3dThreads)
 fast3d_finalize(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restrict__ pairs,
                 const Yaw3Desc* __restrict__ yaws, const float* __restrict__ low_points,
                 const unsigned long long* __restrict__ best, float* __restrict__ low_score) {
-  __shared__ F3SharedT<kSmall3dPoints, kStack3d> sh;
+  __shared__ F3SharedT<kSmall3dPoints, kStack3d, kBatch3d> sh;
   const int p = blockIdx.x;
   const unsigned long long key = best[p];
   const Pair3Desc pd = pairs[p];
@@ -2565,17 +2567,17 @@ hipError_t LaunchFast3dSearch(int tier, int grid, hipStream_t st, const Submap3D
                               uint4* ties, int32_t* tie_count) {
   if (tier == 0)
     hipLaunchKernelGGL((fast3d_search<kTiny3dPoints, kSearch3dBlocksPerCuTiny, kTinyStack3d,
-                                      kTinyInflight3d>),
+                                      kTinyInflight3d, kTinyBatch3d>),
                        dim3(grid), dim3(kSearch3dThreads), 0, st, submaps, pairs, yaws, item_begin,
                        num_items, points, low_points, counter, best, status, stats, spill, best_hi,
                        ties, tie_count);
   else if (tier == 1)
-    hipLaunchKernelGGL((fast3d_search<kSmall3dPoints, kSearch3dBlocksPerCu, kStack3d, 16>),
+    hipLaunchKernelGGL((fast3d_search<kSmall3dPoints, kSearch3dBlocksPerCu, kStack3d, 16, kBatch3d>),
                        dim3(grid), dim3(kSearch3dThreads), 0, st, submaps, pairs, yaws, item_begin,
                        num_items, points, low_points, counter, best, status, stats, spill, best_hi,
                        ties, tie_count);
   else
-    hipLaunchKernelGGL((fast3d_search<kMax3dPoints, kSearch3dBlocksPerCuLarge, kStack3d, 16>),
+    hipLaunchKernelGGL((fast3d_search<kMax3dPoints, kSearch3dBlocksPerCuLarge, kStack3d, 16, kBatch3d>),
                        dim3(grid), dim3(kSearch3dThreads), 0, st, submaps, pairs, yaws, item_begin,
                        num_items, points, low_points, counter, best, status, stats, spill, best_hi,
                        ties, tie_count);

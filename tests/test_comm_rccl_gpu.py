@@ -94,3 +94,38 @@ def test_rccl_gather_and_allreduce_multi_rank(world):
     for r in range(world):
         assert outs[r]["sum"] == np.sum(vs, axis=0).tolist()
         assert outs[r]["max"] == np.max(vs, axis=0).tolist()
+
+
+def _real_rank(out_q):
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from conftest import load_package
+    csm = load_package()
+    try:
+        ctx = csm.Context(0)
+        comm = csm.Comm.rccl(ctx, 0, 1, csm.Comm.unique_id())
+        res = {"size": comm.size, "rank": comm.rank,
+               "gather": [len(b) for b in comm.gather(b"\x05" * 1234)],
+               "sum": comm.allreduce(np.arange(6, dtype=np.int64), csm.REDUCE_SUM).tolist()}
+        comm.barrier()
+        comm.close()
+        out_q.put(res)
+    except Exception as e:  # reported to the parent, which fails the test
+        out_q.put({"error": repr(e)})
+
+
+def test_real_rccl_single_rank():
+    """The installed librccl (no stand-in) through csm_comm_create_rccl:
+    ncclGetUniqueId, ncclCommInitRank with the 128-byte id by value, and
+    ncclCommDestroy, in a world of one (RCCL refuses two ranks on one GPU,
+    tools/probe_rccl_real.py; N > 1 is the driver's scaling run)."""
+    assert "CSM_RCCL_LIB" not in os.environ
+    ctx = mp.get_context("spawn")
+    out_q = ctx.Queue()
+    p = ctx.Process(target=_real_rank, args=(out_q,))
+    p.start()
+    o = out_q.get(timeout=100)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    assert "error" not in o, o
+    assert o == {"size": 1, "rank": 0, "gather": [1234], "sum": list(range(6))}
