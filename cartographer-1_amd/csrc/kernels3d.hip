@@ -963,6 +963,7 @@ __global__ void pad_prob_brick_zfast(const float* __restrict__ prob, Brick3 gb, 
 // passes min_low_resolution_score (:384-401). Each pair keeps one 64-bit key
 // sum << 42 | ~leaf_id, updated with atomicMax.
 
+static_assert(kMax3dWindow < 32768, "leaf offsets are kept as int16 in LDS");
 template <int kPts, int kStack, int kBatch>
 struct F3SharedT {
   // The discretized cloud: full-resolution cells (int16 x, y, z), or — once
@@ -985,7 +986,7 @@ struct F3SharedT {
   alignas(16) uint8_t top[kTopLds3d];
   int bn_x[kBatch], bn_y[kBatch], bn_z[kBatch], bn_d[kBatch];
   unsigned long long leaf_keys[8 * kBatch];
-  int leaf_x[8 * kBatch], leaf_y[8 * kBatch], leaf_z[8 * kBatch];
+  int16_t leaf_x[8 * kBatch], leaf_y[8 * kBatch], leaf_z[8 * kBatch];  // |offset| <= kMax3dWindow
   int rmin[3], rmax[3];  // bounds of the cloud's cells at the top level
   int16_t rbx[kRootScore3d], rby[kRootScore3d], rbz[kRootScore3d];
   int rbs[kRootScore3d];
@@ -1627,6 +1628,7 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
       // Node (8- or 16-lane) sums with DPP: xor 1, xor 2 (quad_perm), then the
       // half-row mirror (8 lanes) and the row mirror (16); every lane of the
       // node ends with the sum.
+      // Lane k < 8 of a node ranks and pushes child k below: 8 lanes at least.
       static_assert(kLanes == 16 || kLanes == 8, "DPP reduction over 8 or 16 lanes per node");
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
