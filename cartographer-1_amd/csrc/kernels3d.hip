@@ -1115,68 +1115,18 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
     const Submap3Desc& sm = submaps[pd.submap];
     const int n = pd.num_points;
     const float res = sm.resolution, inv = 1.f / sm.resolution;
-    if (tid == 0) sh.error = 0;
-    __syncthreads();
-    // DiscretizeScan (:201-244): cell of pose * p at full resolution.
-    for (int i = tid; i < n; i += kSearch3dThreads) {
-      const float* p = points + 3 * (pd.point_offset + i);
-      float ox, oy, oz;
-      Rotate3(yw.qw, yw.qx, yw.qy, yw.qz, p[0], p[1], p[2], &ox, &oy, &oz);
-      const int ix = RoundDiv(__fadd_rn(ox, yw.tx), res, inv);
-      const int iy = RoundDiv(__fadd_rn(oy, yw.ty), res, inv);
-      const int iz = RoundDiv(__fadd_rn(oz, yw.tz), res, inv);
-      if (abs(ix) > kCellLimit3d || abs(iy) > kCellLimit3d || abs(iz) > kCellLimit3d) sh.error = 1;
-      sh.cloud.c.x[i] = static_cast<int16_t>(ix);
-      sh.cloud.c.y[i] = static_cast<int16_t>(iy);
-      sh.cloud.c.z[i] = static_cast<int16_t>(iz);
-    }
-    __syncthreads();
-    if (sh.error) {
-      if (tid == 0) atomicExch(reinterpret_cast<int*>(status + yw.pair), -4);
-      __syncthreads();
-      continue;
-    }
-    F3_MARK(0);
     const int top = pd.root_level;
-    const int step = 1 << top;
-    const int T = pd.top_nx * pd.top_ny * pd.top_nz;
+    const int te = max(0, top - sm.full_resolution_depth + 1);
+    const bool treduced = top >= sm.full_resolution_depth;
+    const int lwx = (-pd.wxy) >> te, lwy = (-pd.wxy) >> te, lwz = (-pd.wz) >> te;
     if (tid == 0) {
+      sh.error = 0;
       sh.sp = 0;
       sh.best = best[yw.pair];
       sh.best_seen = 0;
       sh.tie_sum = -1;
       sh.abandon = 0;
     }
-    __syncthreads();
-    // Lowest-resolution candidates (GenerateLowestResolutionCandidates
-    // :297-330), in chunks of kRootChunk3d: each chunk is scored (one root
-    // per lane, the top level from LDS when it fits), ordered best last and
-    // searched to exhaustion before the next one.
-    const Brick3 tb = sm.level[top];
-    const int64_t tbytes = static_cast<int64_t>(tb.nx) * tb.ny * tb.nz;
-    const int tvec = static_cast<int>((tbytes + 15) / 16);  // level offsets are 256-aligned
-    const bool lds_top = tvec * 16 <= kTopLds3d;
-    if (lds_top && sh.cached_submap != pd.submap * 16 + top) {
-      const uint4* src = reinterpret_cast<const uint4*>(sm.levels + tb.offset);
-      uint4* dst = reinterpret_cast<uint4*>(sh.top);
-      static_assert(kTopLds3d <= 2 * 16 * kSearch3dThreads, "two 16-byte pieces per thread");
-      const int k0 = tid, k1 = tid + kSearch3dThreads;
-      uint4 v0 = make_uint4(0, 0, 0, 0), v1 = make_uint4(0, 0, 0, 0);
-      if (k0 < tvec) v0 = src[k0];
-      if (k1 < tvec) v1 = src[k1];
-      if (k0 < tvec) dst[k0] = v0;
-      if (k1 < tvec) dst[k1] = v1;
-      __syncthreads();
-      if (tid == 0) sh.cached_submap = pd.submap * 16 + top;
-    }
-    __syncthreads();
-    F3_MARK(7);
-    const int te = max(0, top - sm.full_resolution_depth + 1);
-    const bool treduced = top >= sm.full_resolution_depth;
-    const int lwx = (-pd.wxy) >> te, lwy = (-pd.wxy) >> te, lwz = (-pd.wz) >> te;
-    const uint8_t* tglobal = sm.levels + tb.offset;
-    // A root whose shifted cloud box misses the top-level brick sums to 0: it
-    // cannot exceed min_score when min_sum > 0 and is not scored.
     if (tid < 3) {
       sh.rmin[tid] = 1 << 30;
       sh.rmax[tid] = -(1 << 30);
@@ -1184,11 +1134,24 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
       sh.fmax[tid] = -(1 << 30);
     }
     __syncthreads();
+    // DiscretizeScan (:201-244): cell of pose * p at full resolution, with
+    // the cloud's box at full resolution and at the root level (in the
+    // reduced coordinates the roots are scored in).
     {
       int mn[3] = {1 << 30, 1 << 30, 1 << 30}, mx[3] = {-(1 << 30), -(1 << 30), -(1 << 30)};
       int fmn[3] = {1 << 30, 1 << 30, 1 << 30}, fmx[3] = {-(1 << 30), -(1 << 30), -(1 << 30)};
       for (int i = tid; i < n; i += kSearch3dThreads) {
-        int c[3] = {sh.cloud.c.x[i], sh.cloud.c.y[i], sh.cloud.c.z[i]};
+        const float* p = points + 3 * (pd.point_offset + i);
+        float ox, oy, oz;
+        Rotate3(yw.qw, yw.qx, yw.qy, yw.qz, p[0], p[1], p[2], &ox, &oy, &oz);
+        const int ix = RoundDiv(__fadd_rn(ox, yw.tx), res, inv);
+        const int iy = RoundDiv(__fadd_rn(oy, yw.ty), res, inv);
+        const int iz = RoundDiv(__fadd_rn(oz, yw.tz), res, inv);
+        if (abs(ix) > kCellLimit3d || abs(iy) > kCellLimit3d || abs(iz) > kCellLimit3d) sh.error = 1;
+        sh.cloud.c.x[i] = static_cast<int16_t>(ix);
+        sh.cloud.c.y[i] = static_cast<int16_t>(iy);
+        sh.cloud.c.z[i] = static_cast<int16_t>(iz);
+        int c[3] = {ix, iy, iz};
         for (int a = 0; a < 3; ++a) {
           fmn[a] = min(fmn[a], c[a]);
           fmx[a] = max(fmx[a], c[a]);
@@ -1221,6 +1184,38 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
       }
     }
     __syncthreads();
+    if (sh.error) {
+      if (tid == 0) atomicExch(reinterpret_cast<int*>(status + yw.pair), -4);
+      __syncthreads();
+      continue;
+    }
+    F3_MARK(0);
+    const int step = 1 << top;
+    const int T = pd.top_nx * pd.top_ny * pd.top_nz;
+    // Lowest-resolution candidates (GenerateLowestResolutionCandidates
+    // :297-330), in chunks of kRootChunk3d: each chunk is scored (one root
+    // per lane, the top level from LDS when it fits), ordered best last and
+    // searched to exhaustion before the next one.
+    const Brick3 tb = sm.level[top];
+    const int64_t tbytes = static_cast<int64_t>(tb.nx) * tb.ny * tb.nz;
+    const int tvec = static_cast<int>((tbytes + 15) / 16);  // level offsets are 256-aligned
+    const bool lds_top = tvec * 16 <= kTopLds3d;
+    if (lds_top && sh.cached_submap != pd.submap * 16 + top) {
+      const uint4* src = reinterpret_cast<const uint4*>(sm.levels + tb.offset);
+      uint4* dst = reinterpret_cast<uint4*>(sh.top);
+      static_assert(kTopLds3d <= 2 * 16 * kSearch3dThreads, "two 16-byte pieces per thread");
+      const int k0 = tid, k1 = tid + kSearch3dThreads;
+      uint4 v0 = make_uint4(0, 0, 0, 0), v1 = make_uint4(0, 0, 0, 0);
+      if (k0 < tvec) v0 = src[k0];
+      if (k1 < tvec) v1 = src[k1];
+      if (k0 < tvec) dst[k0] = v0;
+      if (k1 < tvec) dst[k1] = v1;
+      __syncthreads();
+      if (tid == 0) sh.cached_submap = pd.submap * 16 + top;
+    }
+    __syncthreads();
+    F3_MARK(7);
+    const uint8_t* tglobal = sm.levels + tb.offset;
     F3_MARK(8);
     // Histogram of the cloud's top-level cells over its box (count grid in
     // the empty stack sums), compacted to a list when box and list fit.
@@ -1297,6 +1292,8 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
     }
     __syncthreads();
     F3_MARK(9);
+    // A root whose shifted cloud box misses the top-level brick sums to 0: it
+    // cannot exceed min_score when min_sum > 0 and is not scored.
     const bool skip_empty = pd.min_sum > 0;
     for (int r0 = 0; r0 < T; r0 += kRootScore3d) {
     if (sh.abandon) break;  // uniform: written before the last batch's barrier
