@@ -80,9 +80,11 @@ def parse():
     p.add_argument("--c5-groups", type=int, default=12,
                    help="C5: submap groups per step; group g + 1 builds while group g is searched "
                         "(1: build all, then search all)")
-    p.add_argument("--c5-search-streams", type=int, default=2,
+    p.add_argument("--c5-search-streams", type=int, default=1,
                    help="C5: contexts (streams) the groups' searches alternate over, one host "
-                        "thread each, so one group's host phases overlap another's kernel")
+                        "thread each, so one group's host phases overlap another's kernel "
+                        "(1 since round 6: 231-235 ms per step against 236-239 with 2, whose "
+                        "overlapping searches contend; profiles/r6an/)")
     p.add_argument("--c5-dropin-calls", type=int, default=4000,
                    help="C5: single MatchFullSubmap calls from 16 threads (Option A), 0: skip")
     p.add_argument("--c5-first-group", type=int, default=6,
