@@ -218,8 +218,12 @@ __device__ __forceinline__ void BrickRows(const uint8_t* __restrict__ src, Brick
       __syncthreads();  // the previous row's reads are done
       // Source rows staged as the dwords that hold them (a dword store per
       // loaded dword; bytes outside the source row zeroed): position pos of
-      // row r is byte roff[r] + pos.
-      int roff[kRows];
+      // row r is byte roff[r] + pos. Every row's loads of a 128-dword span are
+      // issued before any is stored, so a row costs one memory round trip
+      // per span, not one per source row.
+      int roff[kRows], a0s[kRows], rs0s[kRows], nws[kRows];
+      bool oks[kRows];
+      int span = 0;
 #pragma unroll
       for (int r = 0; r < kRows; ++r) {
         int yy, zz;
@@ -232,23 +236,39 @@ __device__ __forceinline__ void BrickRows(const uint8_t* __restrict__ src, Brick
         }
         yy -= sb.oy;
         zz -= sb.oz;
-        const bool row_ok = static_cast<unsigned>(yy) < static_cast<unsigned>(sb.ny) &&
-                            static_cast<unsigned>(zz) < static_cast<unsigned>(sb.nz);
-        const int rs0 = row_ok ? (zz * sb.ny + yy) * sb.nx : 0;  // byte of source x = 0
-        const int b0 = rs0 + xs;                                  // byte of position 0
-        const int a0 = b0 & ~3;
-        roff[r] = r * pitch + (b0 - a0);
-        const int nwords = (W + (b0 - a0) + 3) >> 2;
-        for (int i = threadIdx.x; i < nwords; i += kRowThreads) {
-          const int a = a0 + 4 * i;
-          uint32_t w = row_ok ? __builtin_amdgcn_raw_buffer_load_b32(rs, a, 0, 0) : 0u;
-          if (a < rs0 || a + 4 > rs0 + sb.nx) {
+        oks[r] = static_cast<unsigned>(yy) < static_cast<unsigned>(sb.ny) &&
+                 static_cast<unsigned>(zz) < static_cast<unsigned>(sb.nz);
+        rs0s[r] = oks[r] ? (zz * sb.ny + yy) * sb.nx : 0;  // byte of source x = 0
+        const int b0 = rs0s[r] + xs;                        // byte of position 0
+        a0s[r] = b0 & ~3;
+        roff[r] = r * pitch + (b0 - a0s[r]);
+        nws[r] = (W + (b0 - a0s[r]) + 3) >> 2;
+        span = max(span, nws[r]);
+      }
+      for (int i0 = 0; i0 < span; i0 += 2 * kRowThreads) {
+        uint32_t w[kRows][2];
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
-              if (static_cast<unsigned>(a + j - rs0) >= static_cast<unsigned>(sb.nx)) w &= ~(0xffu << (8 * j));
+        for (int r = 0; r < kRows; ++r)
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            const int i = i0 + q * kRowThreads + static_cast<int>(threadIdx.x);
+            w[r][q] = oks[r] && i < nws[r] ? __builtin_amdgcn_raw_buffer_load_b32(rs, a0s[r] + 4 * i, 0, 0) : 0u;
           }
-          roww[r * (pitch >> 2) + i] = w;
-        }
+#pragma unroll
+        for (int r = 0; r < kRows; ++r)
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            const int i = i0 + q * kRowThreads + static_cast<int>(threadIdx.x);
+            if (i >= nws[r]) continue;
+            const int a = a0s[r] + 4 * i;
+            uint32_t v = w[r][q];
+            if (a < rs0s[r] || a + 4 > rs0s[r] + sb.nx) {
+#pragma unroll
+              for (int j = 0; j < 4; ++j)
+                if (static_cast<unsigned>(a + j - rs0s[r]) >= static_cast<unsigned>(sb.nx)) v &= ~(0xffu << (8 * j));
+            }
+            roww[r * (pitch >> 2) + i] = v;
+          }
       }
       __syncthreads();
       const int base = (lz * ob.ny + ly) * ob.nx;
