@@ -1323,17 +1323,8 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
     {
       const int best_sum = static_cast<int>(sh.best >> pd.key_shift);
       const int lane = tid & 63;
-      // At most 64 roots (the usual case with kRootTarget3d = 64): every wave
-      // scores the same roots over a quarter of the cell list and the partial
-      // sums meet in LDS (else one wave scores them while three wait).
-      const bool split = cells_ok && lds_top && r1 - r0 <= 64;
-      int* part = reinterpret_cast<int*>(sh.lr);  // free until the leaves
-      if (split) {
-        if (tid < 64) part[tid] = 0;
-        __syncthreads();
-      }
-      for (int j0 = r0; j0 < r1; j0 += split ? 64 : kSearch3dThreads) {
-        const int j = j0 + (split ? lane : tid);
+      for (int j0 = r0; j0 < r1; j0 += kSearch3dThreads) {
+        const int j = j0 + tid;
         const int ixx = j % pd.top_nx, iyy = (j / pd.top_nx) % pd.top_ny,
                   izz = j / (pd.top_nx * pd.top_ny);
         const int ox = -pd.wxy + ixx * step, oy = -pd.wxy + iyy * step, oz = -pd.wz + izz * step;
@@ -1349,10 +1340,10 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
           // Each group of 64 cells sits in the wave's registers (one per
           // lane) and is broadcast with readlane: only the level value is
           // read per (root, cell).
-          if (valid && (!split || tid < 64)) root_lookups += ntc;
+          if (valid) root_lookups += ntc;
           const int qx = (valid ? sx : -(1 << 20)) - tb.ox - 1024, qy = sy - tb.oy - 1024,
                     qz = sz - tb.oz - 512;
-          for (int cb = split ? (tid >> 6) * 64 : 0; cb < ntc; cb += split ? 256 : 64) {
+          for (int cb = 0; cb < ntc; cb += 64) {
             const int myc = cb + lane < ntc ? sh.tcell[cb + lane] : 0;
             const int mycnt = cb + lane < ntc ? sh.tcount[cb + lane] : 0;
             const int cn = min(64, ntc - cb);
@@ -1394,12 +1385,7 @@ fast3d_search(const Submap3Desc* __restrict__ submaps, const Pair3Desc* __restri
             if (InBrick(tb, x + sx, y + sy, z + sz, &idx)) sum += lds_top ? sh.top[idx] : tglobal[idx];
           }
         }
-        if (split) {  // one iteration, every thread
-          if (valid) atomicAdd(&part[lane], sum);
-          __syncthreads();
-          sum = part[lane];
-        }
-        if (valid && (!split || tid < 64) && sum >= pd.min_sum && sum >= best_sum) {
+        if (valid && sum >= pd.min_sum && sum >= best_sum) {
           const int at = atomicAdd(&sh.nroot, 1);
           sh.rbx[at] = static_cast<int16_t>(ox);
           sh.rby[at] = static_cast<int16_t>(oy);
