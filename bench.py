@@ -38,8 +38,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 # (a traffic file recorded on another kernel version is not reported).
 KERNEL_TAG = "v5-align8"
 # fast3d_search version whose PMC passes TRAFFIC3D_FILE holds.
-KERNEL3D_TAG = "f3-tiny5-r64-b32-split-box"
-TRAFFIC3D_FILE = os.path.join("profiles", "r6am", "traffic_c5.json")
+KERNEL3D_TAG = "f3-tiny5-r64-b32-box"
+TRAFFIC3D_FILE = os.path.join("profiles", "r6ba", "traffic_c5.json")
 
 
 def load_pkg():
